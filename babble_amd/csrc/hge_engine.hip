@@ -1,0 +1,1271 @@
+// hge_engine.hip — host side of the MI355X hashgraph engine (C ABI in include/hge.h).
+//
+// Orchestrates the kernels of hge_kernels.hip over one HIP stream.  The host
+// keeps only control state: the FromParentsLatest admission check (O(1) per
+// event over per-creator chain tails, hashgraph.go:366-396), the consensus log
+// and a handful of scalars (Rounds(), LastConsensusRound, ...).  Every table
+// the ordering path reads lives in HBM.
+//
+// A "batch" is the unit of device work: it absorbs the events inserted since
+// the previous batch and replays a list of RunConsensus calls (each at an
+// event count n_c).  The online API runs one call per batch; hge_replay runs a
+// whole schedule in one batch.  Both produce identical results (tests).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/hge.h"
+#include "hge_kernels.hip"
+
+using namespace hge;
+
+#define HIPCHK(x)                                                                    \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) {                                                          \
+      throw EngineError(HGE_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    }                                                                                \
+  } while (0)
+
+namespace {
+
+struct EngineError {
+  int code;
+  std::string msg;
+  EngineError(int c, std::string m) : code(c), msg(std::move(m)) {}
+};
+
+template <typename T>
+struct DBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  void free_() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  // grow without preserving contents
+  void need(size_t m) {
+    if (m <= n) return;
+    free_();
+    size_t cap = std::max<size_t>(m, 64);
+    HIPCHK(hipMalloc(&p, cap * sizeof(T)));
+    n = cap;
+  }
+  // grow preserving contents [0, keep)
+  void grow_keep(size_t m, size_t keep, hipStream_t st, int fill_byte = -1) {
+    if (m <= n) return;
+    size_t cap = std::max<size_t>(m, n + n / 2);
+    T* q = nullptr;
+    HIPCHK(hipMalloc(&q, cap * sizeof(T)));
+    if (fill_byte >= 0) HIPCHK(hipMemsetAsync(q, fill_byte, cap * sizeof(T), st));
+    if (p && keep) HIPCHK(hipMemcpyAsync(q, p, keep * sizeof(T), hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+    free_();
+    p = q;
+    n = cap;
+  }
+};
+
+inline int div_up(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+}  // namespace
+
+struct hge_engine {
+  int N = 0, NW = 1, SM = 1, BW = 1;
+  int device = 0;
+  hipStream_t st = nullptr;
+  std::string err;
+
+  // ---- host control state ----
+  std::vector<int32_t> h_creator, h_index, h_sp, h_op, h_ntx;
+  std::vector<int64_t> h_ts;
+  std::vector<uint64_t> h_S;
+  std::vector<uint8_t> h_coin;
+  std::vector<int32_t> chain_len, chain_last;
+  int64_t n_events = 0;     // accepted (host)
+  int64_t n_dev = 0;        // uploaded
+  int64_t n_coords = 0;     // coordinates + rounds computed
+  int64_t n_divided = 0;    // visible to DecideFame / FindOrder (DivideRounds)
+  std::vector<int32_t> coords_len;  // chain lengths at n_coords
+
+  int R = 0;                // Store.Rounds()
+  int lcr = -1;             // LastConsensusRound (-1 nil)
+  int lcre = 0;             // LastCommitedRoundEvents
+  int64_t ctx = 0;          // ConsensusTransactions
+  std::vector<int32_t> consensus;  // the consensus log (unbounded)
+  int64_t n_und = 0;
+
+  // replay staging
+  std::vector<int64_t> replay_calls;  // n_c per call (accepted counts)
+  std::vector<int32_t> replay_order;
+  std::vector<int64_t> replay_counts;
+
+  // ---- device tables ----
+  int64_t Ecap = 0;
+  int ccap = 0, Rcap = 0;
+  DBuf<int32_t> d_creator, d_index, d_sp, d_op, d_ntx, d_round, d_rr, d_und;
+  DBuf<int64_t> d_ts, d_cts;
+  DBuf<uint64_t> d_S;
+  DBuf<uint8_t> d_coin, d_wit;
+  DBuf<int32_t> d_chain, d_LA, d_FD;
+  DBuf<int32_t> d_C, d_W, d_rcnt, d_minw;
+  DBuf<uint64_t> d_ssb, d_seeb;
+  DBuf<uint8_t> d_fame;
+  // scratch
+  DBuf<int32_t> s_D, s_enc, s_basis, s_bcount, s_boff, s_BR, s_small, s_len, s_newwit;
+  DBuf<uint64_t> s_dep;
+  DBuf<int64_t> s_nc;
+  DBuf<int32_t> s_Rc, s_Lc, s_LCR, s_pr, s_clast, s_flags;
+  DBuf<uint8_t> s_dec, s_decbit;
+  DBuf<int32_t> s_segcnt, s_segoff, s_segcall, s_seground, s_theta, s_prindex;
+  DBuf<uint8_t> s_segdec;
+  DBuf<uint64_t> s_segfws;
+  DBuf<int32_t> s_recv, s_rr, s_frecv, s_fund, s_rank, s_upos, s_und2, s_ids, s_ccount;
+  DBuf<int64_t> s_cts;
+  DBuf<unsigned char> s_keys, s_keys2;
+  DBuf<unsigned long long> s_ntx;
+
+  hipEvent_t ev[8] = {};
+  bool br_in_lds = true;
+  int R_div = 0;            // Rounds() as seen by the consensus calls (DivideRounds)
+  float stage_ms[7] = {};
+
+  Tables tables() const {
+    Tables t;
+    t.N = N;
+    t.NW = NW;
+    t.SM = SM;
+    t.ccap = ccap;
+    t.Rcap = Rcap;
+    t.creator = d_creator.p;
+    t.index = d_index.p;
+    t.sp = d_sp.p;
+    t.op = d_op.p;
+    t.ts = d_ts.p;
+    t.S = d_S.p;
+    t.coin = d_coin.p;
+    t.ntx = d_ntx.p;
+    t.chain = d_chain.p;
+    t.LA = d_LA.p;
+    t.FD = d_FD.p;
+    t.round = d_round.p;
+    t.wit = d_wit.p;
+    t.C = d_C.p;
+    t.W = d_W.p;
+    t.ssb = d_ssb.p;
+    t.seeb = d_seeb.p;
+    t.fame = d_fame.p;
+    t.rcnt = d_rcnt.p;
+    return t;
+  }
+
+  // ------------------------------------------------------------------------
+  void init(int n, int64_t cap, int dev) {
+    N = n;
+    NW = (N + 63) / 64;
+    SM = 2 * N / 3 + 1;  // hashgraph.go:78-80
+    // external-basis capacity per chunk: >= every chain head + a margin of
+    // historical parents; chunks that overflow are re-run smaller.
+    int bmax = 2 * N + 64;
+    BW = 1;
+    while (BW * 64 < bmax) BW *= 2;
+    device = dev;
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+    chain_len.assign(N, 0);
+    chain_last.assign(N, -1);
+    coords_len.assign(N, 0);
+    set_lds_limits();
+    ensure_events(std::max<int64_t>(cap, 1024));
+    ensure_ccap(std::max<int64_t>(64, 2 * std::max<int64_t>(cap, 1024) / N + 64));
+    ensure_rcap(std::max<int64_t>(64, std::max<int64_t>(cap, 1024) / SM + 8));
+  }
+
+  void set_lds_limits() {
+    // best effort: gfx950 has 160 KiB of LDS per CU; kernels with static LDS
+    // get a smaller dynamic ceiling
+    const int lim = 152 * 1024;
+#define LDSATTR(f)                                                                            \
+  do {                                                                                        \
+    if (hipFuncSetAttribute((const void*)(f), hipFuncAttributeMaxDynamicSharedMemorySize, lim) != \
+        hipSuccess)                                                                           \
+      (void)hipGetLastError();                                                                \
+  } while (0)
+    LDSATTR(k_coord_local<1>);
+    LDSATTR(k_coord_local<2>);
+    LDSATTR(k_coord_local<4>);
+    LDSATTR(k_coord_local<8>);
+    LDSATTR(k_coord_local<16>);
+    LDSATTR(k_coord_final<1>);
+    LDSATTR(k_coord_final<2>);
+    LDSATTR(k_coord_final<4>);
+    LDSATTR(k_coord_final<8>);
+    LDSATTR(k_coord_final<16>);
+    LDSATTR(k_rounds_frontier);
+#undef LDSATTR
+  }
+
+  void destroy() {
+    if (st) (void)hipStreamSynchronize(st);
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+    DBuf<int32_t>* i32s[] = {&d_creator, &d_index, &d_sp, &d_op, &d_ntx, &d_round, &d_rr, &d_und,
+                             &d_chain, &d_LA, &d_FD, &d_C, &d_W, &d_rcnt, &d_minw, &s_D, &s_enc,
+                             &s_basis, &s_bcount, &s_boff, &s_BR, &s_small, &s_len, &s_newwit,
+                             &s_Rc, &s_Lc, &s_LCR, &s_pr, &s_clast, &s_flags, &s_segcnt,
+                             &s_segoff, &s_segcall, &s_seground, &s_theta, &s_prindex, &s_recv,
+                             &s_rr, &s_frecv, &s_fund, &s_rank, &s_upos, &s_und2, &s_ids,
+                             &s_ccount};
+    for (auto* b : i32s) b->free_();
+    d_ts.free_();
+    d_cts.free_();
+    s_nc.free_();
+    s_cts.free_();
+    d_S.free_();
+    d_ssb.free_();
+    d_seeb.free_();
+    s_dep.free_();
+    s_segfws.free_();
+    d_coin.free_();
+    d_wit.free_();
+    d_fame.free_();
+    s_dec.free_();
+    s_decbit.free_();
+    s_segdec.free_();
+    s_keys.free_();
+    s_keys2.free_();
+    s_ntx.free_();
+    if (st) (void)hipStreamDestroy(st);
+    st = nullptr;
+  }
+
+  void ensure_events(int64_t m) {
+    if (m <= Ecap) return;
+    int64_t cap = std::max<int64_t>(m, Ecap + Ecap / 2);
+    d_creator.grow_keep(cap, n_dev, st);
+    d_index.grow_keep(cap, n_dev, st);
+    d_sp.grow_keep(cap, n_dev, st);
+    d_op.grow_keep(cap, n_dev, st);
+    d_ntx.grow_keep(cap, n_dev, st);
+    d_ts.grow_keep(cap, n_dev, st);
+    d_S.grow_keep(4 * cap, 4 * n_dev, st);
+    d_coin.grow_keep(cap, n_dev, st);
+    d_round.grow_keep(cap, n_coords, st);
+    d_wit.grow_keep(cap, n_coords, st);
+    d_rr.grow_keep(cap, n_coords, st, 0xFF);
+    d_cts.grow_keep(cap, n_coords, st, 0);
+    d_und.grow_keep(cap, n_und, st);
+    Ecap = cap;
+  }
+
+  void ensure_ccap(int64_t m) {
+    if (m <= ccap) return;
+    int64_t nc = std::max<int64_t>(m, (int64_t)ccap + ccap / 2);
+    int32_t *chain = nullptr, *la = nullptr, *fd = nullptr;
+    HIPCHK(hipMalloc(&chain, sizeof(int32_t) * N * nc));
+    HIPCHK(hipMalloc(&la, sizeof(int32_t) * (size_t)N * nc * N));
+    HIPCHK(hipMalloc(&fd, sizeof(int32_t) * (size_t)N * nc * N));
+    HIPCHK(hipMemsetAsync(chain, 0xFF, sizeof(int32_t) * N * nc, st));
+    if (ccap > 0) {
+      HIPCHK(hipMemcpy2DAsync(chain, sizeof(int32_t) * nc, d_chain.p, sizeof(int32_t) * ccap,
+                              sizeof(int32_t) * ccap, N, hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipMemcpy2DAsync(la, sizeof(int32_t) * nc * N, d_LA.p, sizeof(int32_t) * ccap * N,
+                              sizeof(int32_t) * ccap * N, N, hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipMemcpy2DAsync(fd, sizeof(int32_t) * nc * N, d_FD.p, sizeof(int32_t) * ccap * N,
+                              sizeof(int32_t) * ccap * N, N, hipMemcpyDeviceToDevice, st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    d_chain.free_();
+    d_LA.free_();
+    d_FD.free_();
+    d_chain.p = chain;
+    d_chain.n = (size_t)N * nc;
+    d_LA.p = la;
+    d_LA.n = (size_t)N * nc * N;
+    d_FD.p = fd;
+    d_FD.n = (size_t)N * nc * N;
+    ccap = (int)nc;
+  }
+
+  void ensure_rcap(int64_t m) {
+    if (m <= Rcap) return;
+    int64_t nr = std::max<int64_t>(m, (int64_t)Rcap + Rcap / 2);
+    const size_t oldn = (size_t)Rcap * N;
+    d_C.grow_keep(nr * N, oldn, st, 0x7F);  // 0x7F7F7F7F is not INF32: fixed below
+    d_W.grow_keep(nr * N, oldn, st, 0xFF);
+    d_ssb.grow_keep(nr * N * NW, oldn * NW, st, 0);
+    d_seeb.grow_keep(nr * N * NW, oldn * NW, st, 0);
+    d_fame.grow_keep(nr * N, oldn, st, 0);
+    d_rcnt.grow_keep(nr, Rcap, st, 0);
+    d_minw.need(nr);
+    // C must be INF32 beyond the old rows
+    std::vector<int32_t> inf((size_t)(nr - Rcap) * N, INF32);
+    HIPCHK(hipMemcpyAsync(d_C.p + oldn, inf.data(), inf.size() * sizeof(int32_t),
+                          hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+    Rcap = (int)nr;
+  }
+
+  void reset_state() {
+    HIPCHK(hipStreamSynchronize(st));
+    h_creator.clear();
+    h_index.clear();
+    h_sp.clear();
+    h_op.clear();
+    h_ntx.clear();
+    h_ts.clear();
+    h_S.clear();
+    h_coin.clear();
+    chain_len.assign(N, 0);
+    chain_last.assign(N, -1);
+    coords_len.assign(N, 0);
+    n_events = n_dev = n_coords = n_divided = 0;
+    R = 0;
+    lcr = -1;
+    lcre = 0;
+    ctx = 0;
+    consensus.clear();
+    n_und = 0;
+    std::vector<int32_t> inf((size_t)Rcap * N, INF32);
+    HIPCHK(hipMemcpyAsync(d_C.p, inf.data(), inf.size() * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(d_W.p, 0xFF, (size_t)Rcap * N * 4, st));
+    HIPCHK(hipMemsetAsync(d_ssb.p, 0, (size_t)Rcap * N * NW * 8, st));
+    HIPCHK(hipMemsetAsync(d_seeb.p, 0, (size_t)Rcap * N * NW * 8, st));
+    HIPCHK(hipMemsetAsync(d_fame.p, 0, (size_t)Rcap * N, st));
+    HIPCHK(hipMemsetAsync(d_rcnt.p, 0, (size_t)Rcap * 4, st));
+    HIPCHK(hipMemsetAsync(d_chain.p, 0xFF, (size_t)N * ccap * 4, st));
+    HIPCHK(hipMemsetAsync(d_rr.p, 0xFF, (size_t)Ecap * 4, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+
+  // ---------------- admission (hashgraph.go:366-396) ----------------
+  int admit(const hge_event& e, int32_t sp, int32_t op) {
+    const int c = e.creator;
+    if (c < 0 || c >= N) {
+      err = "Could not find fake creator id";
+      return HGE_ERR_CREATOR;
+    }
+    const int known = chain_len[c];
+    if (sp == HGE_NONE && op == HGE_NONE && known == 0) {
+      if (e.index != 0) {
+        err = "Event index does not match the creator's chain position";
+        return HGE_ERR_INDEX;
+      }
+      return HGE_OK;
+    }
+    if (sp < 0 || sp >= n_events) {
+      err = "Self-parent not known";
+      return HGE_ERR_SELF_PARENT_UNKNOWN;
+    }
+    if (h_creator[sp] != c) {
+      err = "Self-parent has different creator";
+      return HGE_ERR_SELF_PARENT_CREATOR;
+    }
+    if (op < 0 || op >= n_events) {
+      err = "Other-parent not known";
+      return HGE_ERR_OTHER_PARENT_UNKNOWN;
+    }
+    if (sp != chain_last[c]) {
+      err = "Self-parent not last known event by creator";
+      return HGE_ERR_SELF_PARENT_NOT_LAST;
+    }
+    if (e.index != known) {
+      err = "Event index does not match the creator's chain position";
+      return HGE_ERR_INDEX;
+    }
+    return HGE_OK;
+  }
+
+  void append(const hge_event& e, int32_t sp, int32_t op) {
+    const int64_t id = n_events++;
+    h_creator.push_back(e.creator);
+    h_index.push_back(e.index);
+    h_sp.push_back(sp);
+    h_op.push_back(op);
+    h_ntx.push_back(e.n_tx);
+    h_ts.push_back(e.timestamp_ns);
+    for (int k = 0; k < 4; k++) {
+      uint64_t v = 0;
+      for (int b = 0; b < 8; b++) v = (v << 8) | e.s[8 * k + b];
+      h_S.push_back(v);
+    }
+    h_coin.push_back(e.hash[16] != 0 ? 1 : 0);
+    chain_len[e.creator]++;
+    chain_last[e.creator] = (int32_t)id;
+  }
+
+  void upload() {
+    if (n_dev == n_events) return;
+    ensure_events(n_events);
+    int maxlen = 0;
+    for (int c = 0; c < N; c++) maxlen = std::max(maxlen, chain_len[c]);
+    ensure_ccap(maxlen + 1);
+    const int64_t a = n_dev, m = n_events - n_dev;
+    HIPCHK(hipMemcpyAsync(d_creator.p + a, h_creator.data() + a, 4 * m, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_index.p + a, h_index.data() + a, 4 * m, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_sp.p + a, h_sp.data() + a, 4 * m, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_op.p + a, h_op.data() + a, 4 * m, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_ntx.p + a, h_ntx.data() + a, 4 * m, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_ts.p + a, h_ts.data() + a, 8 * m, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_S.p + 4 * a, h_S.data() + 4 * a, 32 * m, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_coin.p + a, h_coin.data() + a, m, hipMemcpyHostToDevice, st));
+    n_dev = n_events;
+  }
+
+  template <typename F>
+  void readback(F* host, const F* dev, size_t n) {
+    HIPCHK(hipMemcpyAsync(host, dev, n * sizeof(F), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+
+  // ---------------- coordinates + rounds for [n_coords, n_events) ----------------
+  void coords() {
+    upload();
+    const int64_t n0 = n_coords, n1 = n_events;
+    if (n1 == n0) return;
+    Tables t = tables();
+    const int m = (int)(n1 - n0);
+    hipLaunchKernelGGL(k_chain_fill, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0, (int)n1);
+    // chunk length: LDS of phase A = L*(BW*8 + N*4 + 32) + BMAX*4 + ~1KB
+    const int BMAX = BW * 64;
+    int L = 1024;
+    while (L > 64 && (size_t)L * (BW * 8 + N * 4 + 32) + BMAX * 4 + 2048 > 150 * 1024) L /= 2;
+    for (;;) {
+      const int nch = div_up(m, L);
+      s_D.need((size_t)m * N);
+      s_dep.need((size_t)m * BW);
+      s_enc.need((size_t)2 * m);
+      s_basis.need((size_t)nch * BMAX);
+      s_bcount.need(nch);
+      s_boff.need(nch);
+      s_small.need(8);
+      HIPCHK(hipMemsetAsync(s_small.p, 0, 8 * 4, st));
+      const size_t ldsA = (size_t)L * BW * 8 + (size_t)L * N * 4 + (size_t)L * 4 * 4 +
+                          (size_t)2 * L * 4 * 2 + (size_t)BMAX * 4 + (256 + 1) * 4;
+      launch_bw(0, nch, ldsA, t, (int)n0, (int)n1, L, nch);
+      int32_t flag[2];
+      readback(flag, s_small.p, 2);
+      if (flag[0] && L > 16) {
+        L /= 2;
+        continue;
+      }
+      if (flag[0]) throw EngineError(HGE_ERR_INTERNAL, "external basis overflow");
+      hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, st, s_bcount.p, s_boff.p, nch,
+                         s_small.p + 2);
+      int32_t total = 0;
+      readback(&total, s_small.p + 2, 1);
+      s_BR.need((size_t)std::max(total, 1) * N);
+      launch_bw(1, nch, 0, t, (int)n0, (int)n1, L, nch);
+      br_in_lds = (size_t)BMAX * N * 4 + (size_t)L * N * 4 <= 150 * 1024;
+      const size_t ldsC = (size_t)L * N * 4 + (br_in_lds ? (size_t)BMAX * N * 4 : 0);
+      launch_bw(2, nch, ldsC, t, (int)n0, (int)n1, L, nch);
+      break;
+    }
+    // rounds frontier
+    std::vector<int32_t> lens(2 * N);
+    for (int c = 0; c < N; c++) {
+      lens[c] = coords_len[c];
+      lens[N + c] = chain_len[c];
+    }
+    s_len.need(2 * N);
+    HIPCHK(hipMemcpyAsync(s_len.p, lens.data(), 8 * N, hipMemcpyHostToDevice, st));
+    for (;;) {
+      int32_t rs[2] = {R, 0};
+      HIPCHK(hipMemcpyAsync(s_small.p, rs, 8, hipMemcpyHostToDevice, st));
+      int WIN = std::max(4, std::min(64, 16384 / (N * N)));
+      const size_t lds = (size_t)(N * N + 8 * N + N * WIN) * 4;
+      t = tables();
+      hipLaunchKernelGGL(k_rounds_frontier, dim3(1), dim3(1024), lds, st, t, s_len.p,
+                         s_len.p + N, s_small.p, WIN);
+      readback(rs, s_small.p, 2);
+      if (rs[1]) {
+        ensure_rcap((int64_t)Rcap * 2);
+        continue;
+      }
+      R = rs[0];
+      break;
+    }
+    t = tables();
+    s_newwit.need(m);
+    HIPCHK(hipMemsetAsync(s_small.p + 4, 0, 4, st));
+    hipLaunchKernelGGL(k_round_assign, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0,
+                       (int)n1, R, s_newwit.p, s_small.p + 4);
+    int32_t nnew = 0;
+    readback(&nnew, s_small.p + 4, 1);
+    if (nnew) {
+      const int items = nnew * N;
+      hipLaunchKernelGGL(k_witness_bits, dim3(div_up(items, 256)), dim3(256), 0, st, t,
+                         s_newwit.p, nnew);
+    }
+    hipLaunchKernelGGL(k_round_minw, dim3(div_up(R, 256)), dim3(256), 0, st, t, 0, R, d_minw.p);
+    n_coords = n1;
+    coords_len = chain_len;
+  }
+
+  void launch_bw(int which, int nch, size_t lds, const Tables& t, int n0, int n1, int L, int nch2) {
+    switch (BW) {
+#define CASE(B)                                                                                  \
+  case B:                                                                                        \
+    if (which == 0) {                                                                            \
+      hipLaunchKernelGGL(k_coord_local<B>, dim3(nch), dim3(256), lds, st, t, n0, n1, L, s_D.p,  \
+                         s_dep.p, s_enc.p, s_basis.p, s_bcount.p, s_small.p);                    \
+    } else if (which == 1) {                                                                     \
+      hipLaunchKernelGGL(k_coord_basis<B>, dim3(1), dim3(1024), 0, st, t, n0, L, nch2, s_D.p,    \
+                         s_dep.p, s_basis.p, s_bcount.p, s_boff.p, s_BR.p);                      \
+    } else {                                                                                     \
+      hipLaunchKernelGGL(k_coord_final<B>, dim3(nch), dim3(256), lds, st, t, n0, n1, L, s_D.p,  \
+                         s_dep.p, s_enc.p, s_bcount.p, s_boff.p, s_BR.p, br_in_lds ? 1 : 0);     \
+    }                                                                                            \
+    break;
+      CASE(1)
+      CASE(2)
+      CASE(4)
+      CASE(8)
+      CASE(16)
+#undef CASE
+      default:
+        throw EngineError(HGE_ERR_INTERNAL, "unsupported basis width");
+    }
+  }
+
+  // ---------------- one batch of consensus calls ----------------
+  // calls: event counts n_c (<= n_divided), ascending.
+  void consensus_batch(const std::vector<int64_t>& calls, bool do_fame, bool do_order,
+                       bool commit, std::vector<int32_t>* order_out,
+                       std::vector<int64_t>* counts_out) {
+    const int ncalls = (int)calls.size();
+    if (ncalls == 0) return;
+    Tables t = tables();
+    s_nc.need(ncalls);
+    HIPCHK(hipMemcpyAsync(s_nc.p, calls.data(), 8 * ncalls, hipMemcpyHostToDevice, st));
+    s_Rc.need(ncalls);
+    hipLaunchKernelGGL(k_calls_rounds, dim3(div_up(ncalls, 256)), dim3(256), 0, st, s_nc.p,
+                       ncalls, d_minw.p, R, s_Rc.p);
+    std::vector<int32_t> Rc(ncalls);
+    readback(Rc.data(), s_Rc.p, ncalls);
+
+    // ---- DecideFame windows (host enumeration of (round, call) pairs) ----
+    std::vector<int32_t> pr_round, pr_off, pr_cf, pr_len;
+    int npairs = 0, nrounds = 0;
+    int lcr_new = lcr, c_set = -1;
+    std::vector<int32_t> clast;
+    if (do_fame) {
+      const int i_lo = lcr + 1;
+      const int i_hi = Rc[ncalls - 1] - 2;  // processed rounds: i <= R_c - 2
+      int SPEC = 6;
+      for (;;) {
+        pr_round.clear();
+        pr_off.clear();
+        pr_cf.clear();
+        pr_len.clear();
+        npairs = 0;
+        int cfp = 0;
+        for (int i = i_lo; i <= i_hi; i++) {
+          while (cfp < ncalls && Rc[cfp] < i + 2) cfp++;
+          if (cfp >= ncalls) break;
+          int ce = cfp;
+          // last call with R_c <= i + 2 + SPEC
+          int a = cfp, b = ncalls - 1;
+          while (a < b) {
+            int mid = (a + b + 1) / 2;
+            if (Rc[mid] <= i + 2 + SPEC) a = mid;
+            else b = mid - 1;
+          }
+          ce = a;
+          pr_round.push_back(i);
+          pr_off.push_back(npairs);
+          pr_cf.push_back(cfp);
+          pr_len.push_back(ce - cfp + 1);
+          npairs += ce - cfp + 1;
+        }
+        nrounds = (int)pr_round.size();
+        if (nrounds == 0) break;
+        s_pr.need(4 * nrounds);
+        HIPCHK(hipMemcpyAsync(s_pr.p, pr_round.data(), 4 * nrounds, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(s_pr.p + nrounds, pr_off.data(), 4 * nrounds, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(s_pr.p + 2 * nrounds, pr_cf.data(), 4 * nrounds, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(s_pr.p + 3 * nrounds, pr_len.data(), 4 * nrounds, hipMemcpyHostToDevice, st));
+        s_dec.need((size_t)npairs * N);
+        s_decbit.need(npairs);
+        s_Lc.need(ncalls);
+        s_LCR.need(ncalls);
+        s_clast.need(nrounds);
+        s_flags.need(4);
+        HIPCHK(hipMemsetAsync(s_Lc.p, 0xFF, 4 * ncalls, st));
+        HIPCHK(hipMemsetAsync(s_flags.p, 0, 16, st));
+        const int items = npairs * N;
+        fame_dispatch(0, t, nrounds, npairs, items, ncalls);
+        hipLaunchKernelGGL(k_lcr_scan, dim3(1), dim3(1024), 0, st, s_Lc.p, ncalls, lcr, s_LCR.p,
+                           s_pr.p, s_pr.p + 2 * nrounds, s_pr.p + 3 * nrounds, nrounds,
+                           s_clast.p, s_flags.p);
+        int32_t fl = 0;
+        readback(&fl, s_flags.p, 1);
+        if (fl) {
+          SPEC *= 2;
+          continue;
+        }
+        clast.resize(nrounds);
+        readback(clast.data(), s_clast.p, nrounds);
+        std::vector<int32_t> LCRv(ncalls);
+        readback(LCRv.data(), s_LCR.p, ncalls);
+        lcr_new = LCRv[ncalls - 1];
+        if (lcr_new > lcr) {
+          c_set = 0;
+          while (LCRv[c_set] != lcr_new) c_set++;
+        }
+        break;
+      }
+    }
+
+    // ---- DecideRoundReceived / FindOrder ----
+    if (do_order && n_und > 0) {
+      const int ncand = (int)n_und;
+      int32_t* cand = d_und.p;
+      // lowest candidate round
+      std::vector<int32_t> hr;
+      int rr_lo;
+      {
+        // min round of candidates: read rounds of candidate ids (host gather via device copy)
+        s_small.need(8);
+        std::vector<int32_t> ids(ncand);
+        readback(ids.data(), cand, ncand);
+        std::vector<int32_t> rounds(ncand);
+        // rounds are monotone-ish; gather on host for simplicity (ids are few relative to E)
+        gather_rounds(ids, rounds);
+        int mn = INF32;
+        for (int v : rounds) mn = std::min(mn, v);
+        rr_lo = mn + 1;
+      }
+      const int R_last = Rc[ncalls - 1];
+      const int nr = std::max(0, R_last - rr_lo);
+      if (nr > 0) {
+        // map rounds -> fame window index
+        std::vector<int32_t> pidx(nr, -1);
+        for (int k = 0; k < nrounds; k++) {
+          int i = pr_round[k];
+          if (i >= rr_lo && i < R_last) pidx[i - rr_lo] = k;
+        }
+        s_prindex.need(nr);
+        HIPCHK(hipMemcpyAsync(s_prindex.p, pidx.data(), 4 * nr, hipMemcpyHostToDevice, st));
+        SegInfo si;
+        si.pr_index = s_prindex.p;
+        if (nrounds > 0) {
+          si.pr_off = s_pr.p + nrounds;
+          si.pr_cf = s_pr.p + 2 * nrounds;
+          si.pr_len = s_pr.p + 3 * nrounds;
+          si.clast = s_clast.p;
+          si.dec = s_dec.p;
+        } else {
+          si.pr_off = si.pr_cf = si.pr_len = si.clast = nullptr;
+          si.dec = nullptr;
+        }
+        s_segcnt.need(nr);
+        s_segoff.need(nr + 1);
+        seg_dispatch(0, t, rr_lo, nr, ncalls, si, 0);
+        hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, st, s_segcnt.p, s_segoff.p, nr,
+                           s_small.p + 6);
+        int32_t nseg = 0;
+        readback(&nseg, s_small.p + 6, 1);
+        s_segcall.need(std::max(nseg, 1));
+        s_seground.need(std::max(nseg, 1));
+        s_segdec.need(std::max(nseg, 1));
+        s_segfws.need((size_t)std::max(nseg, 1) * NW);
+        s_theta.need((size_t)std::max(nseg, 1) * N);
+        seg_dispatch(1, t, rr_lo, nr, ncalls, si, nseg);
+        // round-received per candidate
+        s_recv.need(ncand);
+        s_rr.need(ncand);
+        s_cts.need(ncand);
+        recv_dispatch(t, cand, ncand, ncalls, rr_lo, R_last);
+      } else {
+        s_recv.need(ncand);
+        HIPCHK(hipMemsetAsync(s_recv.p, 0xFF, 4 * ncand, st));
+      }
+      // compaction + sort
+      s_frecv.need(ncand);
+      s_fund.need(ncand);
+      s_rank.need(ncand);
+      s_upos.need(ncand);
+      hipLaunchKernelGGL(k_recv_flags, dim3(div_up(ncand, 256)), dim3(256), 0, st, s_recv.p, ncand,
+                         s_frecv.p, s_fund.p, commit ? 1 : 0);
+      scan_large(s_frecv.p, s_rank.p, ncand, s_small.p + 2);
+      int32_t nrecv = 0;
+      readback(&nrecv, s_small.p + 2, 1);
+      s_ntx.need(1);
+      HIPCHK(hipMemsetAsync(s_ntx.p, 0, 8, st));
+      if (nrecv > 0) {
+        hipLaunchKernelGGL(k_set_rr, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand,
+                           s_recv.p, s_rr.p, s_cts.p, d_rr.p, d_cts.p, s_ntx.p, commit ? 1 : 0);
+      }
+      if (commit && nrecv > 0) {
+        s_keys.need((size_t)nrecv * sizeof(OKey));
+        s_keys2.need((size_t)nrecv * sizeof(OKey));
+        OKey* k1 = (OKey*)s_keys.p;
+        OKey* k2 = (OKey*)s_keys2.p;
+        hipLaunchKernelGGL(k_make_keys, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand,
+                           s_recv.p, s_rr.p, s_cts.p, s_rank.p, k1);
+        hipLaunchKernelGGL(k_sort_tiles, dim3(div_up(nrecv, 1024)), dim3(512), 0, st, k1, nrecv);
+        for (int run = 1024; run < nrecv; run *= 2) {
+          hipLaunchKernelGGL(k_merge_pass, dim3(div_up(nrecv, 256)), dim3(256), 0, st, k1, k2,
+                             nrecv, run);
+          std::swap(k1, k2);
+        }
+        s_ids.need(nrecv);
+        s_ccount.need(ncalls);
+        HIPCHK(hipMemsetAsync(s_ccount.p, 0, 4 * ncalls, st));
+        hipLaunchKernelGGL(k_emit_order, dim3(div_up(nrecv, 256)), dim3(256), 0, st, k1, nrecv,
+                           s_ids.p, s_ccount.p, 0);
+        std::vector<int32_t> ids(nrecv);
+        std::vector<int32_t> cc(ncalls);
+        HIPCHK(hipMemcpyAsync(ids.data(), s_ids.p, 4 * nrecv, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(cc.data(), s_ccount.p, 4 * ncalls, hipMemcpyDeviceToHost, st));
+        unsigned long long ntx = 0;
+        HIPCHK(hipMemcpyAsync(&ntx, s_ntx.p, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        consensus.insert(consensus.end(), ids.begin(), ids.end());
+        ctx += (int64_t)ntx;
+        if (order_out) order_out->insert(order_out->end(), ids.begin(), ids.end());
+        if (counts_out)
+          for (int c = 0; c < ncalls; c++) counts_out->push_back(cc[c]);
+        // new undetermined list
+        scan_large(s_fund.p, s_upos.p, ncand, s_small.p + 3);
+        int32_t nund = 0;
+        readback(&nund, s_small.p + 3, 1);
+        s_und2.need(std::max(nund, 1));
+        hipLaunchKernelGGL(k_scatter_und, dim3(div_up(ncand, 256)), dim3(256), 0, st, cand, ncand,
+                           s_fund.p, s_upos.p, s_und2.p);
+        HIPCHK(hipMemcpyAsync(d_und.p, s_und2.p, 4 * (size_t)nund, hipMemcpyDeviceToDevice, st));
+        n_und = nund;
+      } else if (counts_out) {
+        for (int c = 0; c < ncalls; c++) counts_out->push_back(0);
+      }
+    } else if (do_order && counts_out) {
+      for (int c = 0; c < ncalls; c++) counts_out->push_back(0);
+    }
+
+    // ---- persist fame / LCR ----
+    if (do_fame && nrounds > 0) {
+      fame_dispatch(1, t, nrounds, npairs, 0, ncalls);
+      if (lcr_new > lcr) {
+        // RoundEvents(lcr_new - 1) at call c_set
+        int r = lcr_new - 1;
+        int32_t cnt = 0;
+        if (r >= 0) {
+          readback(&cnt, d_rcnt.p + r, 1);
+          const int64_t nfrom = calls[c_set];
+          if (nfrom < n_coords) {
+            HIPCHK(hipMemsetAsync(s_small.p + 5, 0, 4, st));
+            hipLaunchKernelGGL(k_count_late, dim3(div_up(n_coords - nfrom, 256)), dim3(256), 0, st,
+                               t, (int)nfrom, (int)n_coords, r, s_small.p + 5);
+            int32_t late = 0;
+            readback(&late, s_small.p + 5, 1);
+            cnt -= late;
+          }
+        }
+        lcr = lcr_new;
+        lcre = cnt;
+      }
+    }
+    HIPCHK(hipStreamSynchronize(st));
+  }
+
+  void gather_rounds(const std::vector<int32_t>& ids, std::vector<int32_t>& out) {
+    // contiguous-range copy of d_round covering all ids
+    int lo = INF32, hi = -1;
+    for (int v : ids) {
+      lo = std::min(lo, v);
+      hi = std::max(hi, v);
+    }
+    std::vector<int32_t> r(hi - lo + 1);
+    readback(r.data(), d_round.p + lo, r.size());
+    for (size_t k = 0; k < ids.size(); k++) out[k] = r[ids[k] - lo];
+  }
+
+  void scan_large(const int32_t* in, int32_t* out, int n, int32_t* total) {
+    // one block of 1024 threads; adequate for the candidate counts involved
+    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, st, in, out, n, total);
+  }
+
+  void fame_dispatch(int which, const Tables& t, int nrounds, int npairs, int items, int ncalls) {
+    switch (NW) {
+#define FCASE(B)                                                                                 \
+  case B:                                                                                        \
+    if (which == 0) {                                                                            \
+      hipLaunchKernelGGL(k_fame_decide<B>, dim3(div_up(items, 256)), dim3(256), 0, st, t,        \
+                         s_pr.p, s_pr.p + nrounds, s_pr.p + 2 * nrounds, nrounds, npairs,        \
+                         s_nc.p, s_Rc.p, s_dec.p);                                               \
+      hipLaunchKernelGGL(k_fame_timeline<B>, dim3(div_up(nrounds, 64)), dim3(64), 0, st, t,      \
+                         s_pr.p, s_pr.p + nrounds, s_pr.p + 2 * nrounds, s_pr.p + 3 * nrounds,   \
+                         nrounds, s_nc.p, s_dec.p, s_decbit.p, s_Lc.p);                          \
+    } else {                                                                                     \
+      hipLaunchKernelGGL(k_fame_persist<B>, dim3(div_up(nrounds, 64)), dim3(64), 0, st, t,       \
+                         s_pr.p, s_pr.p + nrounds, s_pr.p + 2 * nrounds, s_pr.p + 3 * nrounds,   \
+                         nrounds, s_clast.p, s_dec.p);                                           \
+    }                                                                                            \
+    break;
+      FCASE(1)
+      FCASE(2)
+      FCASE(3)
+      FCASE(4)
+#undef FCASE
+      default:
+        throw EngineError(HGE_ERR_INTERNAL, "unsupported N");
+    }
+    (void)ncalls;
+  }
+
+  void seg_dispatch(int mode, const Tables& t, int rr_lo, int nr, int ncalls, const SegInfo& si,
+                    int nseg) {
+    switch (NW) {
+#define SCASE(B)                                                                                 \
+  case B:                                                                                        \
+    hipLaunchKernelGGL(k_segments<B>, dim3(div_up(nr, 64)), dim3(64), 0, st, t, rr_lo, nr,       \
+                       s_nc.p, ncalls, si, s_segcnt.p, s_segoff.p, s_segcall.p, s_seground.p,    \
+                       s_segdec.p, s_segfws.p, mode);                                            \
+    if (mode == 1 && nseg > 0)                                                                   \
+      hipLaunchKernelGGL(k_seg_theta<B>, dim3(div_up(nseg * N, 256)), dim3(256), 0, st, t,       \
+                         rr_lo, s_seground.p, nseg, s_segfws.p, s_theta.p);                      \
+    break;
+      SCASE(1)
+      SCASE(2)
+      SCASE(3)
+      SCASE(4)
+#undef SCASE
+      default:
+        throw EngineError(HGE_ERR_INTERNAL, "unsupported N");
+    }
+  }
+
+  void recv_dispatch(const Tables& t, const int32_t* cand, int ncand, int ncalls, int rr_lo,
+                     int R_last) {
+    switch (NW) {
+#define RCASE(B)                                                                                 \
+  case B:                                                                                        \
+    hipLaunchKernelGGL(k_round_received<B>, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, \
+                       ncand, s_nc.p, ncalls, 0, rr_lo, R_last, s_segoff.p, s_segcnt.p,          \
+                       s_segcall.p, s_segdec.p, s_segfws.p, s_theta.p, s_recv.p, s_rr.p,         \
+                       s_cts.p);                                                                 \
+    break;
+      RCASE(1)
+      RCASE(2)
+      RCASE(3)
+      RCASE(4)
+#undef RCASE
+      default:
+        throw EngineError(HGE_ERR_INTERNAL, "unsupported N");
+    }
+  }
+
+  // DivideRounds: everything inserted becomes visible to the consensus calls
+  void divide() {
+    coords();
+    if (n_divided < n_coords) {
+      // append the newly divided events to the undetermined list (insertion order)
+      const int64_t a = n_divided, m = n_coords - n_divided;
+      ensure_events(n_coords);
+      std::vector<int32_t> ids(m);
+      for (int64_t k = 0; k < m; k++) ids[k] = (int32_t)(a + k);
+      HIPCHK(hipMemcpyAsync(d_und.p + n_und, ids.data(), 4 * m, hipMemcpyHostToDevice, st));
+      HIPCHK(hipStreamSynchronize(st));
+      n_und += m;
+      n_divided = n_coords;
+    }
+    update_rdiv();
+  }
+
+  void update_rdiv() {
+    if (R == 0) {
+      R_div = 0;
+      return;
+    }
+    std::vector<int32_t> mw(R);
+    readback(mw.data(), d_minw.p, R);
+    R_div = (int)(std::lower_bound(mw.begin(), mw.end(), (int32_t)std::min<int64_t>(n_divided, INF32)) - mw.begin());
+  }
+};
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+#define GUARD_BEGIN try {
+#define GUARD_END(h)                 \
+  }                                  \
+  catch (EngineError & e) {          \
+    (h)->err = e.msg;                \
+    return e.code;                   \
+  }                                  \
+  catch (std::exception & e) {       \
+    (h)->err = e.what();             \
+    return HGE_ERR_INTERNAL;         \
+  }
+
+extern "C" {
+
+int hge_create(int32_t n_participants, int64_t capacity_events, int32_t device, uint32_t flags,
+               hge_engine** out) {
+  (void)flags;
+  if (!out || n_participants < 1 || n_participants > 256) return HGE_ERR_ARG;
+  hge_engine* h = new hge_engine();
+  try {
+    h->init(n_participants, capacity_events, device);
+  } catch (EngineError& e) {
+    fprintf(stderr, "hge_create: %s\n", e.msg.c_str());
+    h->destroy();
+    delete h;
+    *out = nullptr;
+    return e.code;
+  }
+  *out = h;
+  return HGE_OK;
+}
+
+void hge_destroy(hge_engine* h) {
+  if (!h) return;
+  h->destroy();
+  delete h;
+}
+
+const char* hge_last_error(hge_engine* h) { return h ? h->err.c_str() : "null handle"; }
+
+int hge_reset(hge_engine* h) {
+  GUARD_BEGIN
+  h->reset_state();
+  return HGE_OK;
+  GUARD_END(h)
+}
+
+int hge_insert_events(hge_engine* h, const hge_event* ev, int64_t n, int32_t* status_out,
+                      int64_t* n_accepted) {
+  GUARD_BEGIN
+  int64_t acc = 0;
+  int rc = HGE_OK;
+  for (int64_t i = 0; i < n; i++) {
+    const int32_t sp = ev[i].self_parent, op = ev[i].other_parent;
+    int r = h->admit(ev[i], sp, op);
+    if (r != HGE_OK) {
+      if (status_out) status_out[i] = r;
+      rc = r;
+      break;
+    }
+    if (status_out) status_out[i] = (int32_t)h->n_events;
+    h->append(ev[i], sp, op);
+    acc++;
+  }
+  if (n_accepted) *n_accepted = acc;
+  return rc;
+  GUARD_END(h)
+}
+
+int hge_divide_rounds(hge_engine* h) {
+  GUARD_BEGIN
+  h->divide();
+  return HGE_OK;
+  GUARD_END(h)
+}
+
+int hge_decide_fame(hge_engine* h) {
+  GUARD_BEGIN
+    h->consensus_batch({h->n_divided}, true, false, false, nullptr, nullptr);
+  return HGE_OK;
+  GUARD_END(h)
+}
+
+int hge_decide_round_received(hge_engine* h) {
+  GUARD_BEGIN
+    h->consensus_batch({h->n_divided}, false, true, false, nullptr, nullptr);
+  return HGE_OK;
+  GUARD_END(h)
+}
+
+int hge_find_order(hge_engine* h, int32_t* ids_out, int64_t cap, int64_t* n_out) {
+  GUARD_BEGIN
+    std::vector<int32_t> order;
+  h->consensus_batch({h->n_divided}, false, true, true, &order, nullptr);
+  for (int64_t i = 0; i < (int64_t)order.size() && i < cap && ids_out; i++) ids_out[i] = order[i];
+  if (n_out) *n_out = (int64_t)order.size();
+  return HGE_OK;
+  GUARD_END(h)
+}
+
+int hge_run_consensus(hge_engine* h, int32_t* ids_out, int64_t cap, int64_t* n_out) {
+  GUARD_BEGIN
+  h->divide();
+  std::vector<int32_t> order;
+  h->consensus_batch({h->n_divided}, true, true, true, &order, nullptr);
+  for (int64_t i = 0; i < (int64_t)order.size() && i < cap && ids_out; i++) ids_out[i] = order[i];
+  if (n_out) *n_out = (int64_t)order.size();
+  return HGE_OK;
+  GUARD_END(h)
+}
+
+int hge_replay_prepare(hge_engine* h, const hge_event* ev, int64_t n_sub,
+                       const int64_t* call_points, int64_t n_calls, int32_t* status_out) {
+  GUARD_BEGIN
+  h->reset_state();
+  std::vector<int32_t> idmap(n_sub, -1);
+  h->replay_calls.clear();
+  int64_t nc = 0;
+  for (int64_t i = 0; i < n_sub; i++) {
+    const int32_t s = ev[i].self_parent, o = ev[i].other_parent;
+    int32_t sp = s < 0 ? HGE_NONE : (s < i && idmap[s] >= 0 ? idmap[s] : HGE_UNKNOWN);
+    int32_t op = o < 0 ? HGE_NONE : (o < i && idmap[o] >= 0 ? idmap[o] : HGE_UNKNOWN);
+    int r = h->admit(ev[i], sp, op);
+    if (r == HGE_OK) {
+      idmap[i] = (int32_t)h->n_events;
+      h->append(ev[i], sp, op);
+    }
+    if (status_out) status_out[i] = r == HGE_OK ? idmap[i] : r;
+    while (nc < n_calls && call_points[nc] == i + 1) {
+      h->replay_calls.push_back(h->n_events);
+      nc++;
+    }
+  }
+  h->upload();
+  HIPCHK(hipStreamSynchronize(h->st));
+  return HGE_OK;
+  GUARD_END(h)
+}
+
+int hge_replay_run(hge_engine* h, int64_t* n_ordered) {
+  GUARD_BEGIN
+  // fresh consensus state over the staged events (they stay resident in HBM)
+  const int64_t keep = h->n_events;
+  h->n_coords = h->n_divided = 0;
+  h->coords_len.assign(h->N, 0);
+  h->R = 0;
+  h->lcr = -1;
+  h->lcre = 0;
+  h->ctx = 0;
+  h->consensus.clear();
+  h->n_und = 0;
+  {
+    std::vector<int32_t> inf((size_t)h->Rcap * h->N, INF32);
+    HIPCHK(hipMemcpyAsync(h->d_C.p, inf.data(), inf.size() * 4, hipMemcpyHostToDevice, h->st));
+    HIPCHK(hipMemsetAsync(h->d_W.p, 0xFF, (size_t)h->Rcap * h->N * 4, h->st));
+    HIPCHK(hipMemsetAsync(h->d_ssb.p, 0, (size_t)h->Rcap * h->N * h->NW * 8, h->st));
+    HIPCHK(hipMemsetAsync(h->d_seeb.p, 0, (size_t)h->Rcap * h->N * h->NW * 8, h->st));
+    HIPCHK(hipMemsetAsync(h->d_fame.p, 0, (size_t)h->Rcap * h->N, h->st));
+    HIPCHK(hipMemsetAsync(h->d_rcnt.p, 0, (size_t)h->Rcap * 4, h->st));
+    HIPCHK(hipMemsetAsync(h->d_rr.p, 0xFF, (size_t)h->Ecap * 4, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+  }
+  HIPCHK(hipEventRecord(h->ev[0], h->st));
+  h->coords();
+  HIPCHK(hipEventRecord(h->ev[1], h->st));
+  h->n_divided = keep;
+  h->update_rdiv();
+  {
+    std::vector<int32_t> ids(keep);
+    for (int64_t k = 0; k < keep; k++) ids[k] = (int32_t)k;
+    HIPCHK(hipMemcpyAsync(h->d_und.p, ids.data(), 4 * keep, hipMemcpyHostToDevice, h->st));
+    h->n_und = keep;
+  }
+  h->replay_order.clear();
+  h->replay_counts.clear();
+  h->consensus_batch(h->replay_calls, true, true, true, &h->replay_order, &h->replay_counts);
+  HIPCHK(hipEventRecord(h->ev[2], h->st));
+  HIPCHK(hipEventSynchronize(h->ev[2]));
+  float a = 0, b = 0;
+  HIPCHK(hipEventElapsedTime(&a, h->ev[0], h->ev[1]));
+  HIPCHK(hipEventElapsedTime(&b, h->ev[1], h->ev[2]));
+  h->stage_ms[0] = a;
+  h->stage_ms[3] = b;
+  h->stage_ms[6] = a + b;
+  if (n_ordered) *n_ordered = (int64_t)h->replay_order.size();
+  return HGE_OK;
+  GUARD_END(h)
+}
+
+int hge_replay_fetch(hge_engine* h, int32_t* order_out, int64_t cap, int64_t* call_counts_out) {
+  GUARD_BEGIN
+  for (int64_t i = 0; i < (int64_t)h->replay_order.size() && i < cap && order_out; i++)
+    order_out[i] = h->replay_order[i];
+  if (call_counts_out)
+    for (size_t c = 0; c < h->replay_counts.size(); c++) call_counts_out[c] = h->replay_counts[c];
+  return HGE_OK;
+  GUARD_END(h)
+}
+
+int hge_replay(hge_engine* h, const hge_event* ev, int64_t n_sub, const int64_t* call_points,
+               int64_t n_calls, int32_t* status_out, int32_t* order_out, int64_t cap,
+               int64_t* n_ordered, int64_t* call_counts_out) {
+  int rc = hge_replay_prepare(h, ev, n_sub, call_points, n_calls, status_out);
+  if (rc) return rc;
+  rc = hge_replay_run(h, n_ordered);
+  if (rc) return rc;
+  return hge_replay_fetch(h, order_out, cap, call_counts_out);
+}
+
+int64_t hge_event_count(hge_engine* h) { return h->n_events; }
+int32_t hge_participants(hge_engine* h) { return h->N; }
+int32_t hge_rounds(hge_engine* h) { return h->R_div; }
+int32_t hge_last_consensus_round(hge_engine* h) { return h->lcr; }
+int32_t hge_last_committed_round_events(hge_engine* h) { return h->lcre; }
+int64_t hge_consensus_transactions(hge_engine* h) { return h->ctx; }
+int64_t hge_consensus_count(hge_engine* h) { return (int64_t)h->consensus.size(); }
+int64_t hge_consensus_events(hge_engine* h, int32_t* ids_out, int64_t cap) {
+  for (int64_t i = 0; i < (int64_t)h->consensus.size() && i < cap && ids_out; i++)
+    ids_out[i] = h->consensus[i];
+  return (int64_t)h->consensus.size();
+}
+int64_t hge_undetermined(hge_engine* h, int32_t* ids_out, int64_t cap) {
+  try {
+    if (ids_out && h->n_und > 0) {
+      int64_t m = std::min<int64_t>(cap, h->n_und);
+      h->readback(ids_out, h->d_und.p, m);
+    }
+  } catch (EngineError& e) {
+    h->err = e.msg;
+    return e.code;
+  }
+  return h->n_und;
+}
+int hge_known(hge_engine* h, int32_t* counts_out) {
+  for (int c = 0; c < h->N; c++) counts_out[c] = h->chain_len[c];
+  return HGE_OK;
+}
+
+static int32_t read1(hge_engine* h, const int32_t* p) {
+  int32_t v = -1;
+  h->readback(&v, p, 1);
+  return v;
+}
+
+int32_t hge_round_of(hge_engine* h, int32_t id) {
+  try {
+    if (id < 0 || id >= h->n_events) return -1;
+    h->coords();
+    return read1(h, h->d_round.p + id);
+  } catch (EngineError& e) {
+    h->err = e.msg;
+    return e.code;
+  }
+}
+int32_t hge_is_witness(hge_engine* h, int32_t id) {
+  try {
+    if (id < 0 || id >= h->n_events) return 0;
+    h->coords();
+    uint8_t v = 0;
+    h->readback(&v, h->d_wit.p + id, 1);
+    return v;
+  } catch (EngineError& e) {
+    h->err = e.msg;
+    return e.code;
+  }
+}
+int32_t hge_round_witness(hge_engine* h, int32_t round, int32_t creator) {
+  try {
+    if (round < 0 || round >= h->R || creator < 0 || creator >= h->N) return -1;
+    int32_t w = read1(h, h->d_W.p + (size_t)round * h->N + creator);
+    if (w >= h->n_divided) return -1;
+    return w;
+  } catch (EngineError& e) {
+    h->err = e.msg;
+    return e.code;
+  }
+}
+int32_t hge_fame(hge_engine* h, int32_t round, int32_t creator) {
+  try {
+    if (hge_round_witness(h, round, creator) < 0) return -1;
+    uint8_t v = 0;
+    h->readback(&v, h->d_fame.p + (size_t)round * h->N + creator, 1);
+    return v;
+  } catch (EngineError& e) {
+    h->err = e.msg;
+    return e.code;
+  }
+}
+int32_t hge_round_events(hge_engine* h, int32_t round) {
+  try {
+    if (round < 0 || round >= h->R) return 0;
+    return read1(h, h->d_rcnt.p + round);
+  } catch (EngineError& e) {
+    h->err = e.msg;
+    return e.code;
+  }
+}
+int32_t hge_round_received(hge_engine* h, int32_t id) {
+  try {
+    if (id < 0 || id >= h->n_events) return -1;
+    return read1(h, h->d_rr.p + id);
+  } catch (EngineError& e) {
+    h->err = e.msg;
+    return e.code;
+  }
+}
+int64_t hge_consensus_timestamp(hge_engine* h, int32_t id) {
+  try {
+    if (id < 0 || id >= h->n_events) return 0;
+    int64_t v = 0;
+    h->readback(&v, h->d_cts.p + id, 1);
+    return v;
+  } catch (EngineError& e) {
+    h->err = e.msg;
+    return e.code;
+  }
+}
+
+int hge_coordinates(hge_engine* h, int32_t id, int32_t* la_out, int32_t* fd_out) {
+  GUARD_BEGIN
+  if (id < 0 || id >= h->n_events) return HGE_ERR_ARG;
+  h->coords();
+  const size_t off = ((size_t)h->h_creator[id] * h->ccap + h->h_index[id]) * h->N;
+  if (la_out) h->readback(la_out, h->d_LA.p + off, h->N);
+  if (fd_out) h->readback(fd_out, h->d_FD.p + off, h->N);
+  return HGE_OK;
+  GUARD_END(h)
+}
+
+// predicates on the materialised coordinates (hashgraph.go:83-208)
+int32_t hge_ancestor(hge_engine* h, int32_t x, int32_t y) {
+  if (x < 0 || x >= h->n_events || y < 0 || y >= h->n_events) return 0;
+  if (x == y) return 1;
+  std::vector<int32_t> la(h->N);
+  if (hge_coordinates(h, x, la.data(), nullptr)) return 0;
+  return la[h->h_creator[y]] >= h->h_index[y] ? 1 : 0;
+}
+int32_t hge_self_ancestor(hge_engine* h, int32_t x, int32_t y) {
+  if (x < 0 || x >= h->n_events || y < 0 || y >= h->n_events) return 0;
+  if (x == y) return 1;
+  return (h->h_creator[x] == h->h_creator[y] && h->h_index[x] >= h->h_index[y]) ? 1 : 0;
+}
+int32_t hge_see(hge_engine* h, int32_t x, int32_t y) { return hge_ancestor(h, x, y); }
+int32_t hge_strongly_see(hge_engine* h, int32_t x, int32_t y) {
+  if (x < 0 || x >= h->n_events || y < 0 || y >= h->n_events) return 0;
+  std::vector<int32_t> la(h->N), fd(h->N);
+  if (hge_coordinates(h, x, la.data(), nullptr)) return 0;
+  if (hge_coordinates(h, y, nullptr, fd.data())) return 0;
+  int c = 0;
+  for (int i = 0; i < h->N; i++) c += la[i] >= fd[i];
+  return c >= h->SM ? 1 : 0;
+}
+int32_t hge_oldest_self_ancestor_to_see(hge_engine* h, int32_t x, int32_t y) {
+  if (x < 0 || x >= h->n_events || y < 0 || y >= h->n_events) return -1;
+  std::vector<int32_t> fd(h->N);
+  if (hge_coordinates(h, y, nullptr, fd.data())) return -1;
+  const int cx = h->h_creator[x];
+  const int32_t a = fd[cx];
+  if (a <= h->h_index[x]) {
+    try {
+      return read1(h, h->d_chain.p + (size_t)cx * h->ccap + a);
+    } catch (EngineError& e) {
+      h->err = e.msg;
+      return -1;
+    }
+  }
+  return -1;
+}
+
+int hge_stage_times(hge_engine* h, float* ms_out, int cap) {
+  int n = std::min(cap, 7);
+  for (int i = 0; i < n; i++) ms_out[i] = h->stage_ms[i];
+  return n;
+}
+
+}  // extern "C"

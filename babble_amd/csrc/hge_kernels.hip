@@ -1,0 +1,1197 @@
+// hge_kernels.hip — CDNA4 (gfx950) kernels of the hashgraph ordering engine.
+//
+// The reference (mpitid/babble hashgraph.go) evaluates everything lazily per
+// event pair behind LRU caches.  Here every schedule-independent quantity is
+// computed in bulk over dense, chain-major HBM tables, and the schedule-
+// dependent part (DecideFame / DecideRoundReceived, which depend on WHEN
+// RunConsensus is called) is replayed exactly, but in parallel over
+// (round, call) pairs.  DESIGN.md derives each reformulation; the parity tests
+// check them against the Go-faithful oracle.
+//
+// Tables (N participants; a "row" is N int32 over participants):
+//   LA[c][p][:]  lastAncestors index row of the event at chain c position p
+//   FD[c][p][:]  firstDescendants index row (INF32 = unset)
+//   chain[c][p]  event id at (c, p); ids are dense in insertion order
+//   C[r][c]      first position on chain c whose round is >= r (INF32 = none yet)
+//   W[r][c]      witness of round r created by c (-1 none)
+//   ssb/seeb[r][c][NW]  strongly-see / see bitsets of witness W[r][c] over the
+//                slots of round r-1
+//   fame[r][c]   0 undefined, 1 true, 2 false (persisted across calls)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define INF32 0x7FFFFFFF
+
+namespace hge {
+
+struct Tables {
+  int N, NW, SM, ccap, Rcap;
+  const int32_t* creator;
+  const int32_t* index;
+  const int32_t* sp;
+  const int32_t* op;
+  const int64_t* ts;
+  const uint64_t* S;
+  const uint8_t* coin;
+  const int32_t* ntx;
+  int32_t* chain;
+  int32_t* LA;
+  int32_t* FD;
+  int32_t* round;
+  uint8_t* wit;
+  int32_t* C;
+  int32_t* W;
+  uint64_t* ssb;
+  uint64_t* seeb;
+  uint8_t* fame;
+  int32_t* rcnt;  // events per round
+};
+
+__device__ __forceinline__ size_t rowoff(const Tables& t, int c, int p) {
+  return ((size_t)c * t.ccap + p) * (size_t)t.N;
+}
+
+template <typename T>
+__device__ __forceinline__ T ntload(const T* p) {
+  return __builtin_nontemporal_load(p);
+}
+
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// ---------------------------------------------------------------------------
+// block-wide exclusive scan over `n` ints in LDS (n <= 8 * blockDim.x)
+// ---------------------------------------------------------------------------
+__device__ int block_exclusive_scan(int* a, int n, int* tmp /* blockDim.x + 1 */) {
+  const int T = blockDim.x, tid = threadIdx.x;
+  const int per = (n + T - 1) / T;
+  const int lo = min(n, tid * per), hi = min(n, lo + per);
+  int s = 0;
+  for (int i = lo; i < hi; i++) s += a[i];
+  tmp[tid] = s;
+  __syncthreads();
+  if (tid == 0) {
+    int run = 0;
+    for (int i = 0; i < T; i++) {
+      int v = tmp[i];
+      tmp[i] = run;
+      run += v;
+    }
+    tmp[T] = run;
+  }
+  __syncthreads();
+  int run = tmp[tid];
+  for (int i = lo; i < hi; i++) {
+    int v = a[i];
+    a[i] = run;
+    run += v;
+  }
+  __syncthreads();
+  return tmp[T];
+}
+
+// ---------------------------------------------------------------------------
+// Coordinates, phase A: one workgroup per chunk of L consecutive new events.
+// Computes, by one sequential pass in LDS, for every event of the chunk
+//   D[x]   = max own-index contributions of in-chunk ancestors (row of N)
+//   dep[x] = bitset over the chunk's external basis (distinct parents that
+//            precede the chunk) reachable from x inside the chunk,
+// so that lastAncestors(x) = max(D[x], max_{b in dep[x]} LA[basis b])
+// (InitEventCoordinates, hashgraph.go:399-463, unrolled over the chunk).
+// Also initialises the new events' FD rows to INF32 (hashgraph.go:402-407).
+// ---------------------------------------------------------------------------
+template <int BW>
+__global__ void __launch_bounds__(256) k_coord_local(Tables t, int n0, int n1, int L,
+                                                      int32_t* Dbuf, uint64_t* depbuf,
+                                                      int32_t* enc, int32_t* basis,
+                                                      int32_t* bcount, int* overflow) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BMAX = BW * 64;
+  const int N = t.N;
+  const int k = blockIdx.x;
+  const int s = n0 + k * L;
+  const int e = min(n1, s + L);
+  const int cnt = e - s;
+  const int tid = threadIdx.x;
+  const int T = blockDim.x;
+
+  uint64_t* sdep = (uint64_t*)smem;                 // L * BW
+  int32_t* sD = (int32_t*)(sdep + (size_t)L * BW);  // L * N
+  int32_t* ssp = sD + (size_t)L * N;                // L
+  int32_t* sop = ssp + L;                           // L
+  int32_t* scr = sop + L;                           // L
+  int32_t* sidx = scr + L;                          // L
+  int32_t* sext = sidx + L;                         // 2L (sorted externals)
+  int32_t* sflag = sext + 2 * L;                    // 2L
+  int32_t* sbas = sflag + 2 * L;                    // BMAX
+  int32_t* stmp = sbas + BMAX;                      // T + 1
+
+  const int M = 2 * L;
+  for (int i = tid; i < L; i += T) {
+    int x = s + i;
+    int p0 = -1, p1 = -1, cr = 0, ix = 0;
+    if (i < cnt) {
+      p0 = t.sp[x];
+      p1 = t.op[x];
+      cr = t.creator[x];
+      ix = t.index[x];
+      int32_t* fdr = t.FD + rowoff(t, cr, ix);
+      for (int c = 0; c < N; c++) fdr[c] = INF32;
+    }
+    ssp[i] = p0;
+    sop[i] = p1;
+    scr[i] = cr;
+    sidx[i] = ix;
+    sext[2 * i] = (p0 >= 0 && p0 < s) ? p0 : INF32;
+    sext[2 * i + 1] = (p1 >= 0 && p1 < s) ? p1 : INF32;
+  }
+  __syncthreads();
+  // bitonic sort of the 2L external candidates (M is a power of two)
+  for (int size = 2; size <= M; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < M / 2; i += T) {
+        int lo = 2 * stride * (i / stride) + (i % stride);
+        int hi = lo + stride;
+        bool up = ((lo & size) == 0);
+        int a = sext[lo], b = sext[hi];
+        if ((a > b) == up) {
+          sext[lo] = b;
+          sext[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < M; i += T) {
+    int v = sext[i];
+    sflag[i] = (v != INF32 && (i == 0 || sext[i - 1] != v)) ? 1 : 0;
+  }
+  __syncthreads();
+  // keep the flags (scan overwrites): rank = exclusive prefix
+  const int nb = block_exclusive_scan(sflag, M, stmp);
+  if (nb > BMAX) {
+    if (tid == 0) atomicOr(overflow, 1);
+    return;
+  }
+  for (int i = tid; i < M; i += T) {
+    int v = sext[i];
+    int r = sflag[i];
+    int nxt = (i + 1 < M) ? sflag[i + 1] : nb;
+    if (v != INF32 && nxt != r) sbas[r] = v;  // first occurrence
+  }
+  __syncthreads();
+  for (int i = tid; i < nb; i += T) basis[(size_t)k * BMAX + i] = sbas[i];
+  if (tid == 0) bcount[k] = nb;
+  // encode parents: >= 0 local offset, -1 none, -(2 + b) basis slot b
+  for (int i = tid; i < cnt; i += T) {
+    int pr[2] = {ssp[i], sop[i]};
+    for (int q = 0; q < 2; q++) {
+      int p = pr[q];
+      int code;
+      if (p < 0) code = -1;
+      else if (p >= s) code = p - s;
+      else {
+        int lo = 0, hi = nb - 1;
+        while (lo < hi) {
+          int mid = (lo + hi) >> 1;
+          if (sbas[mid] < p) lo = mid + 1;
+          else hi = mid;
+        }
+        code = -(2 + lo);
+      }
+      pr[q] = code;
+    }
+    ssp[i] = pr[0];
+    sop[i] = pr[1];
+    enc[2 * (size_t)(s - n0 + i)] = pr[0];
+    enc[2 * (size_t)(s - n0 + i) + 1] = pr[1];
+  }
+  __syncthreads();
+  // sequential in-chunk propagation: one wave, lanes over columns / dep words
+  if (tid < 64) {
+    const int lane = tid;
+    for (int i = 0; i < cnt; i++) {
+      const int psp = ssp[i], pop = sop[i], cx = scr[i], ix = sidx[i];
+      for (int c = lane; c < N; c += 64) {
+        int v = -1;
+        if (psp >= 0) v = sD[psp * N + c];
+        if (pop >= 0) v = max(v, sD[pop * N + c]);
+        if (c == cx) v = ix;
+        sD[i * N + c] = v;
+      }
+      for (int w = lane; w < BW; w += 64) {
+        uint64_t d = 0;
+        if (psp >= 0) d |= sdep[psp * BW + w];
+        else if (psp <= -2 && ((-psp - 2) >> 6) == w) d |= 1ull << ((-psp - 2) & 63);
+        if (pop >= 0) d |= sdep[pop * BW + w];
+        else if (pop <= -2 && ((-pop - 2) >> 6) == w) d |= 1ull << ((-pop - 2) & 63);
+        sdep[i * BW + w] = d;
+      }
+    }
+  }
+  __syncthreads();
+  const size_t base = (size_t)(s - n0);
+  for (int i = tid; i < cnt * N; i += T) Dbuf[base * N + i] = sD[i];
+  for (int i = tid; i < cnt * BW; i += T) depbuf[base * BW + i] = sdep[i];
+}
+
+// exclusive scan of a small int array by one block (n <= ~64k)
+__global__ void __launch_bounds__(1024) k_scan_small(const int32_t* in, int32_t* out, int n,
+                                                     int32_t* total) {
+  __shared__ int tmp[1025];
+  const int T = blockDim.x, tid = threadIdx.x;
+  const int per = (n + T - 1) / T;
+  const int lo = min(n, tid * per), hi = min(n, lo + per);
+  int s = 0;
+  for (int i = lo; i < hi; i++) s += in[i];
+  tmp[tid] = s;
+  __syncthreads();
+  if (tid == 0) {
+    int run = 0;
+    for (int i = 0; i < T; i++) {
+      int v = tmp[i];
+      tmp[i] = run;
+      run += v;
+    }
+    tmp[T] = run;
+  }
+  __syncthreads();
+  int run = tmp[tid];
+  for (int i = lo; i < hi; i++) {
+    int v = in[i];
+    out[i] = run;
+    run += v;
+  }
+  if (tid == 0 && total) *total = tmp[T];
+}
+
+// ---------------------------------------------------------------------------
+// Coordinates, phase B: one persistent workgroup walks the chunks in order and
+// materialises the lastAncestors rows of every basis element (the only rows a
+// later chunk needs from an earlier one).  Basis element e of chunk k lies
+// before chunk k: either before this batch (final LA row in HBM) or in an
+// earlier chunk j of this batch: row = max(D_j[e], max_{b in dep_j[e]} BR_j[b]).
+// ---------------------------------------------------------------------------
+template <int BW>
+__global__ void __launch_bounds__(1024) k_coord_basis(Tables t, int n0, int L, int nchunks,
+                                                       const int32_t* Dbuf,
+                                                       const uint64_t* depbuf,
+                                                       const int32_t* basis,
+                                                       const int32_t* bcount,
+                                                       const int32_t* boff, int32_t* BR) {
+  constexpr int BMAX = BW * 64;
+  const int N = t.N;
+  for (int k = 0; k < nchunks; k++) {
+    const int nb = bcount[k];
+    const int off = boff[k];
+    for (int item = threadIdx.x; item < nb * N; item += blockDim.x) {
+      const int b = item / N, c = item - (item / N) * N;
+      const int e = basis[(size_t)k * BMAX + b];
+      int v;
+      if (e < n0) {
+        v = t.LA[rowoff(t, t.creator[e], t.index[e]) + c];
+      } else {
+        const int le = e - n0;
+        const int j = le / L;
+        const int bj = boff[j];
+        v = Dbuf[(size_t)le * N + c];
+#pragma unroll
+        for (int w = 0; w < BW; w++) {
+          uint64_t m = depbuf[(size_t)le * BW + w];
+          while (m) {
+            const int tb = w * 64 + __builtin_ctzll(m);
+            m &= m - 1;
+            v = max(v, ntload(&BR[(size_t)(bj + tb) * N + c]));
+          }
+        }
+      }
+      BR[(size_t)(off + b) * N + c] = v;
+    }
+    drain_stores();
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Coordinates, phase C: per chunk, final LA rows (to HBM, chain-major) and the
+// firstDescendants scatter (UpdateAncestorFirstDescendant, hashgraph.go:466-494):
+// event x on chain cx is the first cx-descendant of exactly the chain-j events
+// at positions (LA[sp(x)][j], LA[x][j]], so FD[j][q][cx] = index(x) there.
+// ---------------------------------------------------------------------------
+template <int BW>
+__global__ void __launch_bounds__(256) k_coord_final(Tables t, int n0, int n1, int L,
+                                                      const int32_t* Dbuf,
+                                                      const uint64_t* depbuf,
+                                                      const int32_t* enc,
+                                                      const int32_t* bcount,
+                                                      const int32_t* boff,
+                                                      const int32_t* BR, int br_in_lds) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BMAX = BW * 64;
+  const int N = t.N;
+  const int k = blockIdx.x;
+  const int s = n0 + k * L;
+  const int e = min(n1, s + L);
+  const int cnt = e - s;
+  const int tid = threadIdx.x, T = blockDim.x;
+  const int nb = bcount[k];
+  const size_t bo = (size_t)boff[k] * N;
+  int32_t* sLA = (int32_t*)smem;  // L * N
+  const int32_t* sBR;             // BMAX * N basis rows (LDS when they fit)
+  if (br_in_lds) {
+    int32_t* b = sLA + (size_t)L * N;
+    for (int i = tid; i < nb * N; i += T) b[i] = BR[bo + i];
+    sBR = b;
+  } else {
+    sBR = BR + bo;
+  }
+  __syncthreads();
+  const size_t base = (size_t)(s - n0);
+  for (int item = tid; item < cnt * N; item += T) {
+    const int i = item / N, c = item - (item / N) * N;
+    int v = Dbuf[base * N + item];
+#pragma unroll
+    for (int w = 0; w < BW; w++) {
+      uint64_t m = depbuf[(base + i) * BW + w];
+      while (m) {
+        const int tb = w * 64 + __builtin_ctzll(m);
+        m &= m - 1;
+        v = max(v, sBR[tb * N + c]);
+      }
+    }
+    sLA[item] = v;
+    const int x = s + i;
+    t.LA[rowoff(t, t.creator[x], t.index[x]) + c] = v;
+  }
+  __syncthreads();
+  for (int item = tid; item < cnt * N; item += T) {
+    const int i = item / N, j = item - (item / N) * N;
+    const int x = s + i;
+    const int cx = t.creator[x], ix = t.index[x];
+    const int psp = enc[2 * (base + i)];
+    int lo = -1;
+    if (psp >= 0) lo = sLA[psp * N + j];
+    else if (psp <= -2) lo = sBR[(-psp - 2) * N + j];
+    const int hi = sLA[i * N + j];
+    for (int q = lo + 1; q <= hi; q++) t.FD[rowoff(t, j, q) + cx] = ix;
+  }
+}
+
+// chain table: chain[c][index] = id for the new events
+__global__ void k_chain_fill(Tables t, int n0, int n1) {
+  const int x = n0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (x < n1) t.chain[(size_t)t.creator[x] * t.ccap + t.index[x]] = x;
+}
+
+// ---------------------------------------------------------------------------
+// Rounds (DivideRounds/Round/RoundInc, hashgraph.go:211-305, 573-588) as a
+// frontier over rounds.  C[r][c] = first position on chain c with round >= r.
+// Proved in DESIGN.md: round(x) >= r+1  <=>  x strongly sees >= SM of
+// C_r \ {x}; the predicate is monotone along a chain, so C[r+1][c] is the first
+// position at or after max(C[r][c], old chain length) that satisfies it.
+// One persistent workgroup walks the rounds; each round probes a window of
+// candidate positions per chain against the members' FD rows staged in LDS.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) k_rounds_frontier(Tables t, const int32_t* olen,
+                                                          const int32_t* len, int32_t* rstate,
+                                                          int WIN) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int N = t.N, SM = t.SM;
+  const int tid = threadIdx.x, T = blockDim.x;
+  int32_t* sFD = (int32_t*)smem;     // N*N member FD rows
+  int32_t* sP = sFD + N * N;         // N  C_r positions (carried in LDS across rounds)
+  int32_t* sMid = sP + N;            // N  member ids
+  int32_t* sLo = sMid + N;           // N  search start
+  int32_t* sLen = sLo + N;           // N
+  int32_t* sOlen = sLen + N;         // N
+  int32_t* sNeed = sOlen + N;        // N
+  int32_t* sFirst = sNeed + N;       // N
+  int32_t* sNext = sFirst + N;       // N  C_{r+1}
+  int32_t* sCnt = sNext + N;         // N * WIN
+  __shared__ int s_rlo, s_any, s_more;
+
+  if (tid == 0) s_rlo = INF32;
+  __syncthreads();
+  for (int c = tid; c < N; c += T) {
+    const int ol = olen[c], ln = len[c];
+    sOlen[c] = ol;
+    sLen[c] = ln;
+    if (ln > ol) {
+      int r0 = 0;
+      if (ol == 0) t.C[c] = 0;  // initial event: first position with round >= 0
+      else r0 = t.round[t.chain[(size_t)c * t.ccap + ol - 1]];
+      atomicMin(&s_rlo, r0);
+    }
+  }
+  __syncthreads();
+  const int rlo = s_rlo;
+  if (rlo == INF32) return;  // no new events
+  // rows written by this kernel are only ever re-read from LDS (a CU's L1 may
+  // hold a stale copy of a line this workgroup stored)
+  for (int c = tid; c < N; c += T) {
+    int p = t.C[(size_t)rlo * N + c];
+    if (rlo == 0 && sOlen[c] == 0 && sLen[c] > 0) p = 0;
+    sP[c] = p;
+  }
+  __syncthreads();
+  int r = rlo;
+  for (;; r++) {
+    if (r + 1 >= t.Rcap) {
+      if (tid == 0) rstate[1] = 1;  // overflow: host grows Rcap and reruns
+      return;
+    }
+    for (int c = tid; c < N; c += T) {
+      const int p = sP[c];
+      sMid[c] = (p != INF32) ? t.chain[(size_t)c * t.ccap + p] : -1;
+      const int cur = t.C[(size_t)(r + 1) * N + c];  // not yet written by this kernel
+      sNext[c] = cur;
+      const int lo = max(p, sOlen[c]);
+      sLo[c] = lo;
+      sNeed[c] = (cur == INF32 && p != INF32 && lo < sLen[c]) ? 1 : 0;
+    }
+    __syncthreads();
+    for (int item = tid; item < N * N; item += T) {
+      const int d = item / N, i = item - (item / N) * N;
+      const int p = sP[d];
+      sFD[item] = (p != INF32) ? t.FD[rowoff(t, d, p) + i] : INF32;
+    }
+    __syncthreads();
+    for (;;) {
+      for (int i = tid; i < N * WIN; i += T) sCnt[i] = 0;
+      for (int c = tid; c < N; c += T) sFirst[c] = INF32;
+      if (tid == 0) s_more = 0;
+      __syncthreads();
+      const int items = N * WIN * N;
+      for (int item = tid; item < items; item += T) {
+        const int c = item / (WIN * N);
+        const int rem = item - c * (WIN * N);
+        const int k = rem / N, d = rem - (rem / N) * N;
+        if (!sNeed[c] || sMid[d] < 0) continue;
+        const int p = sLo[c] + k;
+        if (p >= sLen[c]) continue;
+        if (d == c && p == sP[c]) continue;  // x itself is excluded (not yet in its round)
+        const int32_t* la = t.LA + rowoff(t, c, p);
+        const int32_t* fd = sFD + d * N;
+        int cntss = 0;
+        for (int i = 0; i < N; i++) cntss += (la[i] >= fd[i]) ? 1 : 0;
+        if (cntss >= SM) atomicAdd(&sCnt[c * WIN + k], 1);
+      }
+      __syncthreads();
+      for (int item = tid; item < N * WIN; item += T) {
+        const int c = item / WIN, k = item - (item / WIN) * WIN;
+        if (sNeed[c] && sCnt[item] >= SM) atomicMin(&sFirst[c], k);
+      }
+      __syncthreads();
+      for (int c = tid; c < N; c += T) {
+        if (!sNeed[c]) continue;
+        if (sFirst[c] != INF32) {
+          const int pos = sLo[c] + sFirst[c];
+          sNext[c] = pos;
+          t.C[(size_t)(r + 1) * N + c] = pos;
+          sNeed[c] = 0;
+        } else if (sLo[c] + WIN >= sLen[c]) {
+          sNeed[c] = 0;
+        } else {
+          sLo[c] += WIN;
+          s_more = 1;
+        }
+      }
+      __syncthreads();
+      if (!s_more) break;
+    }
+    if (tid == 0) s_any = 0;
+    __syncthreads();
+    for (int c = tid; c < N; c += T) {
+      if (sNext[c] != INF32) s_any = 1;
+      sP[c] = sNext[c];
+    }
+    __syncthreads();
+    if (!s_any) break;
+  }
+  if (tid == 0) rstate[0] = max(rstate[0], r + 1);  // Rounds()
+}
+
+// round(x) = max r with C[r][cx] <= px; witness iff C[round][cx] == px
+__global__ void k_round_assign(Tables t, int n0, int n1, int R, int32_t* newwit,
+                               int32_t* nnewwit) {
+  const int x = n0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= n1) return;
+  const int N = t.N;
+  const int cx = t.creator[x], px = t.index[x];
+  int lo = 0, hi = R - 1;  // C[0][cx] == 0 <= px
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (t.C[(size_t)mid * N + cx] <= px) lo = mid;
+    else hi = mid - 1;
+  }
+  t.round[x] = lo;
+  const bool w = (t.C[(size_t)lo * N + cx] == px);
+  t.wit[x] = w ? 1 : 0;
+  atomicAdd(&t.rcnt[lo], 1);
+  if (w) {
+    t.W[(size_t)lo * N + cx] = x;
+    const int slot = atomicAdd(nnewwit, 1);
+    newwit[slot] = x;
+  }
+}
+
+// first witness id per round (monotone increasing in r); rounds [r0, R)
+__global__ void k_round_minw(Tables t, int r0, int R, int32_t* minw) {
+  const int r = r0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  int m = INF32;
+  for (int c = 0; c < t.N; c++) {
+    const int w = t.W[(size_t)r * t.N + c];
+    if (w >= 0) m = min(m, w);
+  }
+  minw[r] = m;
+}
+
+// R_c = Rounds() after the DivideRounds of call c = #{r : minw[r] < n_c}
+__global__ void k_calls_rounds(const int64_t* nc, int ncalls, const int32_t* minw, int R,
+                               int32_t* Rc) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncalls) return;
+  const int64_t n = nc[c];
+  int lo = 0, hi = R;  // count of minw < n
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((int64_t)minw[mid] < n) lo = mid + 1;
+    else hi = mid;
+  }
+  Rc[c] = lo;
+}
+
+// strongly-see / see bitsets of each new witness y (round j >= 1) over the
+// slots of round j-1: StronglySee (hashgraph.go:189-208), See (:149-154)
+__global__ void k_witness_bits(Tables t, const int32_t* newwit, int nnew) {
+  const int item = blockIdx.x * blockDim.x + threadIdx.x;
+  const int N = t.N, NW = t.NW;
+  if (item >= nnew * N) return;
+  const int y = newwit[item / N];
+  const int d = item - (item / N) * N;
+  const int j = t.round[y];
+  if (j == 0) return;
+  const int w = t.W[(size_t)(j - 1) * N + d];
+  if (w < 0) return;
+  const int cy = t.creator[y];
+  const int32_t* la = t.LA + rowoff(t, cy, t.index[y]);
+  const int32_t* fd = t.FD + rowoff(t, d, t.index[w]);
+  const bool see = la[d] >= t.index[w];
+  int c = 0;
+  for (int i = 0; i < N; i++) c += (la[i] >= fd[i]) ? 1 : 0;
+  const size_t off = ((size_t)j * N + cy) * NW + (d >> 6);
+  const uint64_t bit = 1ull << (d & 63);
+  if (see) atomicOr((unsigned long long*)&t.seeb[off], (unsigned long long)bit);
+  if (c >= t.SM) atomicOr((unsigned long long*)&t.ssb[off], (unsigned long long)bit);
+}
+
+// ---------------------------------------------------------------------------
+// DecideFame (hashgraph.go:598-664) for one (round i, call c) pair and one
+// witness slot x of round i: the votes of this call are rebuilt from scratch
+// (hashgraph.go:599), y iterates in canonical (ascending creator) order, a
+// decision breaks the y loop leaving later y without a vote (read as "no" at
+// j+1), and the LAST decision over j is what SetFame leaves.  Output per
+// (pair, slot): 0 no decision in this call, 1 famous, 2 not famous.
+// ---------------------------------------------------------------------------
+template <int NWT>
+__global__ void k_fame_decide(Tables t, const int32_t* pr_round, const int32_t* pr_off,
+                              const int32_t* pr_cf, int nrounds, int npairs,
+                              const int64_t* nc, const int32_t* Rc, uint8_t* dec) {
+  const int item = blockIdx.x * blockDim.x + threadIdx.x;
+  const int N = t.N, SM = t.SM;
+  if (item >= npairs * N) return;
+  const int p = item / N, xd = item - (item / N) * N;
+  int lo = 0, hi = nrounds - 1;  // last round with pr_off <= p
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (pr_off[mid] <= p) lo = mid;
+    else hi = mid - 1;
+  }
+  const int i = pr_round[lo];
+  const int c = pr_cf[lo] + (p - pr_off[lo]);
+  const int64_t n = nc[c];
+  const int R = Rc[c];
+  uint8_t out = 0;
+  const int x = t.W[(size_t)i * N + xd];
+  if (x >= 0 && x < n) {
+    uint64_t votes[NWT], cur[NWT];
+#pragma unroll
+    for (int w = 0; w < NWT; w++) votes[w] = 0;
+    // diff == 1: vote = See(y, x)
+    for (int d = 0; d < N; d++) {
+      const int y = t.W[(size_t)(i + 1) * N + d];
+      if (y < 0 || y >= n) continue;
+      const uint64_t sb = t.seeb[((size_t)(i + 1) * N + d) * NWT + (xd >> 6)];
+      if ((sb >> (xd & 63)) & 1ull) votes[d >> 6] |= 1ull << (d & 63);
+    }
+    for (int j = i + 2; j < R; j++) {
+      const int diff = j - i;
+      const bool coinr = (diff % N) == 0;
+#pragma unroll
+      for (int w = 0; w < NWT; w++) cur[w] = 0;
+      for (int d = 0; d < N; d++) {
+        const int y = t.W[(size_t)j * N + d];
+        if (y < 0 || y >= n) continue;
+        const uint64_t* ss = t.ssb + ((size_t)j * N + d) * NWT;
+        int yays = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < NWT; w++) {
+          const uint64_t m = ss[w];
+          yays += __popcll(m & votes[w]);
+          tot += __popcll(m);
+        }
+        const int nays = tot - yays;
+        const bool v = yays >= nays;
+        const int tt = v ? yays : nays;
+        if (!coinr) {
+          if (tt >= SM) {
+            out = v ? 1 : 2;
+            break;
+          }
+          if (v) cur[d >> 6] |= 1ull << (d & 63);
+        } else {
+          const bool vv = (tt >= SM) ? v : (t.coin[y] != 0);
+          if (vv) cur[d >> 6] |= 1ull << (d & 63);
+        }
+      }
+#pragma unroll
+      for (int w = 0; w < NWT; w++) votes[w] = cur[w];
+    }
+  }
+  dec[(size_t)p * N + xd] = out;
+}
+
+// Per processed round: fame state along its window of calls (persisted state
+// + decisions of each call), WitnessesDecided per call (roundInfo.go:78-85) and
+// the candidate LastConsensusRound per call (hashgraph.go:654-657).
+template <int NWT>
+__global__ void k_fame_timeline(Tables t, const int32_t* pr_round, const int32_t* pr_off,
+                                const int32_t* pr_cf, const int32_t* pr_len, int nrounds,
+                                const int64_t* nc, const uint8_t* dec, uint8_t* decbit,
+                                int32_t* Lc) {
+  const int ri = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ri >= nrounds) return;
+  const int N = t.N;
+  const int i = pr_round[ri];
+  uint64_t known[NWT], val[NWT];
+#pragma unroll
+  for (int w = 0; w < NWT; w++) known[w] = val[w] = 0;
+  for (int d = 0; d < N; d++) {
+    const uint8_t f = t.fame[(size_t)i * N + d];
+    if (f) known[d >> 6] |= 1ull << (d & 63);
+    if (f == 1) val[d >> 6] |= 1ull << (d & 63);
+  }
+  for (int q = 0; q < pr_len[ri]; q++) {
+    const int p = pr_off[ri] + q;
+    const int c = pr_cf[ri] + q;
+    const int64_t n = nc[c];
+    bool decided = true;
+    for (int d = 0; d < N; d++) {
+      const uint8_t o = dec[(size_t)p * N + d];
+      const uint64_t b = 1ull << (d & 63);
+      if (o) {
+        known[d >> 6] |= b;
+        if (o == 1) val[d >> 6] |= b;
+        else val[d >> 6] &= ~b;
+      }
+      const int x = t.W[(size_t)i * N + d];
+      if (x >= 0 && x < n && !((known[d >> 6] >> (d & 63)) & 1ull)) decided = false;
+    }
+    decbit[p] = decided ? 1 : 0;
+    if (decided) atomicMax(&Lc[c], i);
+  }
+}
+
+// LCR_c = max(LCR_start, prefix max of Lc); c_last(i) = first call with LCR >= i;
+// coverage check of each round's speculative window.
+__global__ void __launch_bounds__(1024) k_lcr_scan(const int32_t* Lc, int ncalls, int lcr_start,
+                                                   int32_t* LCR, const int32_t* pr_round,
+                                                   const int32_t* pr_cf, const int32_t* pr_len,
+                                                   int nrounds, int32_t* clast, int32_t* flags) {
+  __shared__ int tmp[1025];
+  const int T = blockDim.x, tid = threadIdx.x;
+  const int per = (ncalls + T - 1) / T;
+  const int lo = min(ncalls, tid * per), hi = min(ncalls, lo + per);
+  int m = -1;
+  for (int i = lo; i < hi; i++) m = max(m, Lc[i]);
+  tmp[tid] = m;
+  __syncthreads();
+  if (tid == 0) {
+    int run = lcr_start;
+    for (int i = 0; i < T; i++) {
+      const int v = tmp[i];
+      tmp[i] = run;
+      run = max(run, v);
+    }
+  }
+  __syncthreads();
+  int run = tmp[tid];
+  for (int i = lo; i < hi; i++) {
+    run = max(run, Lc[i]);
+    LCR[i] = run;
+  }
+  __syncthreads();
+  for (int ri = tid; ri < nrounds; ri += T) {
+    const int i = pr_round[ri];
+    int a = 0, b = ncalls;  // first c with LCR[c] >= i
+    while (a < b) {
+      const int mid = (a + b) >> 1;
+      if (LCR[mid] >= i) b = mid;
+      else a = mid + 1;
+    }
+    clast[ri] = a;
+    const int ce = pr_cf[ri] + pr_len[ri] - 1;
+    if (pr_len[ri] > 0) {
+      if (a < ncalls) {
+        if (a > ce) atomicOr(&flags[0], 1);
+      } else if (ce < ncalls - 1) {
+        atomicOr(&flags[0], 1);
+      }
+    }
+  }
+}
+
+// persisted fame after the batch: decisions up to c_last(i)
+template <int NWT>
+__global__ void k_fame_persist(Tables t, const int32_t* pr_round, const int32_t* pr_off,
+                               const int32_t* pr_cf, const int32_t* pr_len, int nrounds,
+                               const int32_t* clast, const uint8_t* dec) {
+  const int ri = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ri >= nrounds) return;
+  const int N = t.N;
+  const int i = pr_round[ri];
+  const int qend = min(pr_len[ri], clast[ri] - pr_cf[ri] + 1);
+  for (int d = 0; d < N; d++) {
+    uint8_t f = t.fame[(size_t)i * N + d];
+    for (int q = 0; q < qend; q++) {
+      const uint8_t o = dec[(size_t)(pr_off[ri] + q) * N + d];
+      if (o) f = o;
+    }
+    t.fame[(size_t)i * N + d] = f;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Round-state segments for DecideRoundReceived (hashgraph.go:676-721): for each
+// round i, the calls at which (WitnessesDecided, famous set) changes.  State
+// changes only when a witness of round i becomes visible (its call of arrival)
+// or, while the round is processed by DecideFame, when a decision lands.
+// Mode 0 counts segments, mode 1 writes them.
+// ---------------------------------------------------------------------------
+struct SegInfo {
+  const int32_t* pr_index;  // [rounds rr_lo..] -> index into pr_* arrays or -1
+  const int32_t* pr_off;
+  const int32_t* pr_cf;
+  const int32_t* pr_len;
+  const int32_t* clast;
+  const uint8_t* dec;
+};
+
+template <int NWT>
+__global__ void k_segments(Tables t, int rr_lo, int nr, const int64_t* nc, int ncalls,
+                           SegInfo si, int32_t* segcnt, const int32_t* segoff, int32_t* seg_call,
+                           int32_t* seg_round, uint8_t* seg_dec, uint64_t* seg_fws, int mode) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nr) return;
+  const int N = t.N;
+  const int i = rr_lo + q;
+  uint64_t known[NWT], val[NWT], pres[NWT], prevf[NWT];
+#pragma unroll
+  for (int w = 0; w < NWT; w++) known[w] = val[w] = pres[w] = prevf[w] = 0;
+  for (int d = 0; d < N; d++) {
+    const uint8_t f = t.fame[(size_t)i * N + d];  // persisted BEFORE this batch's update
+    if (f) known[d >> 6] |= 1ull << (d & 63);
+    if (f == 1) val[d >> 6] |= 1ull << (d & 63);
+  }
+  const int pi = si.pr_index[q];
+  const int cf = pi >= 0 ? si.pr_cf[pi] : INF32;
+  const int wl = pi >= 0 ? min(si.pr_len[pi], si.clast[pi] - cf + 1) : 0;  // processed calls
+  int prevdec = -1;
+  int nseg = 0;
+  const int base = mode ? segoff[q] : 0;
+  int c = 0;
+  while (c < ncalls) {
+    // state at call c
+    const int64_t n = nc[c];
+#pragma unroll
+    for (int w = 0; w < NWT; w++) pres[w] = 0;
+    int nxt_arrival = INF32;
+    for (int d = 0; d < N; d++) {
+      const int x = t.W[(size_t)i * N + d];
+      if (x < 0) continue;
+      if (x < n) pres[d >> 6] |= 1ull << (d & 63);
+      else {
+        // first call at which x is visible
+        int a = c + 1, b = ncalls;
+        while (a < b) {
+          const int mid = (a + b) >> 1;
+          if (nc[mid] > x) b = mid;
+          else a = mid + 1;
+        }
+        nxt_arrival = min(nxt_arrival, a);
+      }
+    }
+    if (c >= cf && c - cf < wl) {
+      const int p = si.pr_off[pi] + (c - cf);
+      for (int d = 0; d < N; d++) {
+        const uint8_t o = si.dec[(size_t)p * N + d];
+        const uint64_t b = 1ull << (d & 63);
+        if (o) {
+          known[d >> 6] |= b;
+          if (o == 1) val[d >> 6] |= b;
+          else val[d >> 6] &= ~b;
+        }
+      }
+    }
+    bool exists = false, decided = true, same = true;
+#pragma unroll
+    for (int w = 0; w < NWT; w++) {
+      if (pres[w]) exists = true;
+      if (pres[w] & ~known[w]) decided = false;
+    }
+    uint64_t fws[NWT];
+#pragma unroll
+    for (int w = 0; w < NWT; w++) {
+      fws[w] = pres[w] & known[w] & val[w];
+      if (fws[w] != prevf[w]) same = false;
+    }
+    if (exists && (prevdec != (int)decided || !same)) {
+      if (mode) {
+        const int sidx = base + nseg;
+        seg_call[sidx] = c;
+        seg_round[sidx] = i;
+        seg_dec[sidx] = decided ? 1 : 0;
+#pragma unroll
+        for (int w = 0; w < NWT; w++) seg_fws[(size_t)sidx * NWT + w] = fws[w];
+      }
+      nseg++;
+      prevdec = decided;
+#pragma unroll
+      for (int w = 0; w < NWT; w++) prevf[w] = fws[w];
+    }
+    // next change point
+    int nxt = nxt_arrival;
+    if (c + 1 >= cf && c + 1 - cf < wl) nxt = min(nxt, c + 1);
+    else if (c + 1 < cf && cf < wl + cf) nxt = min(nxt, cf);
+    if (nxt <= c) nxt = c + 1;
+    c = nxt;
+  }
+  if (!mode) segcnt[q] = nseg;
+}
+
+// theta[seg][cx] = the (|fws|/2 + 1)-th largest LA[w][cx] over famous witnesses
+// w: event x (creator cx, index ix) is seen by a strict majority of them iff
+// ix <= theta (hashgraph.go:689-697).  INT32_MIN when nobody is famous.
+template <int NWT>
+__global__ void k_seg_theta(Tables t, int rr_lo, const int32_t* seg_round, int nseg,
+                            const uint64_t* seg_fws, int32_t* theta) {
+  const int item = blockIdx.x * blockDim.x + threadIdx.x;
+  const int N = t.N;
+  if (item >= nseg * N) return;
+  const int sg = item / N, cx = item - (item / N) * N;
+  const int i = seg_round[sg];
+  int vals[64];
+  int m = 0;
+  int k = 0;
+  // count famous
+  int nf = 0;
+#pragma unroll
+  for (int w = 0; w < NWT; w++) nf += __popcll(seg_fws[(size_t)sg * NWT + w]);
+  k = nf / 2 + 1;
+  if (nf == 0) {
+    theta[item] = (int)0x80000000;
+    return;
+  }
+  // k-th largest by repeated selection over a bounded buffer (N <= 64 fast path)
+  if (nf <= 64) {
+    for (int d = 0; d < N; d++) {
+      if (!((seg_fws[(size_t)sg * NWT + (d >> 6)] >> (d & 63)) & 1ull)) continue;
+      const int w = t.W[(size_t)i * N + d];
+      vals[m++] = t.LA[rowoff(t, d, t.index[w]) + cx];
+    }
+    // partial selection sort (descending) for k elements
+    for (int a = 0; a < k; a++) {
+      int best = a;
+      for (int b = a + 1; b < m; b++)
+        if (vals[b] > vals[best]) best = b;
+      const int tmp = vals[a];
+      vals[a] = vals[best];
+      vals[best] = tmp;
+    }
+    theta[item] = vals[k - 1];
+  } else {
+    // general: threshold search by counting (values are chain positions >= -1)
+    int lo = -1, hi = INF32 - 1;  // largest v with count(>= v) >= k
+    while (lo < hi) {
+      const int mid = lo + (int)(((int64_t)hi - lo + 1) / 2);
+      int ccount = 0;
+      for (int d = 0; d < N; d++) {
+        if (!((seg_fws[(size_t)sg * NWT + (d >> 6)] >> (d & 63)) & 1ull)) continue;
+        const int w = t.W[(size_t)i * N + d];
+        ccount += (t.LA[rowoff(t, d, t.index[w]) + cx] >= mid) ? 1 : 0;
+      }
+      if (ccount >= k) lo = mid;
+      else hi = mid - 1;
+    }
+    theta[item] = lo;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// DecideRoundReceived + MedianTimestamp (hashgraph.go:676-721, 762-770) for
+// every candidate event (undetermined at batch start, or new): the first call
+// c >= arrival(x) and, within it, the lowest round i > round(x) that is decided
+// at c and whose famous witnesses see x by strict majority.
+// ---------------------------------------------------------------------------
+template <int NWT>
+__global__ void k_round_received(Tables t, const int32_t* cand, int ncand, const int64_t* nc,
+                                 int ncalls, int call_lo, int rr_lo, int R_last,
+                                 const int32_t* segoff, const int32_t* segcnt,
+                                 const int32_t* seg_call, const uint8_t* seg_dec,
+                                 const uint64_t* seg_fws, const int32_t* theta,
+                                 int32_t* recv_call, int32_t* rr_out, int64_t* cts_out) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= ncand) return;
+  const int N = t.N;
+  const int x = cand[q];
+  const int cx = t.creator[x], ix = t.index[x];
+  const int rx = t.round[x];
+  // first call at which x is visible
+  int a = call_lo, b = ncalls;
+  while (a < b) {
+    const int mid = (a + b) >> 1;
+    if (nc[mid] > x) b = mid;
+    else a = mid + 1;
+  }
+  const int c0 = a;
+  int best = INF32, rr = -1, bseg = -1;
+  for (int i = rx + 1; i < R_last; i++) {
+    const int qi = i - rr_lo;
+    const int so = segoff[qi], sc = segcnt[qi];
+    if (sc == 0) continue;
+    if (seg_call[so] >= best) break;
+    for (int k = 0; k < sc; k++) {
+      const int sstart = seg_call[so + k];
+      const int send = (k + 1 < sc) ? seg_call[so + k + 1] : ncalls;
+      if (send <= c0) continue;
+      if (sstart >= best) break;
+      if (seg_dec[so + k] && ix <= theta[(size_t)(so + k) * N + cx]) {
+        const int f = max(sstart, c0);
+        if (f < best) {
+          best = f;
+          rr = i;
+          bseg = so + k;
+        }
+        break;
+      }
+    }
+  }
+  if (rr < 0 || best >= ncalls) {
+    recv_call[q] = -1;
+    return;
+  }
+  // median of the oldest-self-ancestor-to-see timestamps (OSA(w,x) = FD[x][cw])
+  int64_t tv[64];
+  int m = 0;
+  const int32_t* fdx = t.FD + rowoff(t, cx, ix);
+  int64_t med = 0;
+  int nsee = 0;
+  for (int d = 0; d < N; d++) {
+    if (!((seg_fws[(size_t)bseg * NWT + (d >> 6)] >> (d & 63)) & 1ull)) continue;
+    const int w = t.W[(size_t)rr * N + d];
+    if (t.LA[rowoff(t, d, t.index[w]) + cx] < ix) continue;
+    nsee++;
+  }
+  if (nsee <= 64) {
+    for (int d = 0; d < N; d++) {
+      if (!((seg_fws[(size_t)bseg * NWT + (d >> 6)] >> (d & 63)) & 1ull)) continue;
+      const int w = t.W[(size_t)rr * N + d];
+      if (t.LA[rowoff(t, d, t.index[w]) + cx] < ix) continue;
+      const int osa = t.chain[(size_t)d * t.ccap + fdx[d]];
+      int64_t v = t.ts[osa];
+      int j = m++;
+      while (j > 0 && tv[j - 1] > v) {
+        tv[j] = tv[j - 1];
+        j--;
+      }
+      tv[j] = v;
+    }
+    med = tv[m / 2];
+  } else {
+    // k-th smallest by counting selection
+    const int kk = nsee / 2;  // 0-based
+    int64_t lo = INT64_MIN, hi = INT64_MAX;
+    // candidate values are the timestamps themselves: pick the smallest v with count(<= v) > kk
+    for (int d = 0; d < N; d++) {
+      if (!((seg_fws[(size_t)bseg * NWT + (d >> 6)] >> (d & 63)) & 1ull)) continue;
+      const int w = t.W[(size_t)rr * N + d];
+      if (t.LA[rowoff(t, d, t.index[w]) + cx] < ix) continue;
+      const int64_t v = t.ts[t.chain[(size_t)d * t.ccap + fdx[d]]];
+      int le = 0;
+      for (int e2 = 0; e2 < N; e2++) {
+        if (!((seg_fws[(size_t)bseg * NWT + (e2 >> 6)] >> (e2 & 63)) & 1ull)) continue;
+        const int w2 = t.W[(size_t)rr * N + e2];
+        if (t.LA[rowoff(t, e2, t.index[w2]) + cx] < ix) continue;
+        le += (t.ts[t.chain[(size_t)e2 * t.ccap + fdx[e2]]] <= v) ? 1 : 0;
+      }
+      if (le > kk && v < hi) hi = v;
+    }
+    (void)lo;
+    med = hi;
+  }
+  recv_call[q] = best;
+  rr_out[q] = rr;
+  cts_out[q] = med;
+}
+
+// ---------------------------------------------------------------------------
+// FindOrder sort (hashgraph.go:744-745, consensus_sorter.go:36-59): key
+// (call, roundReceived, consensusTimestamp, S) with S compared as an unsigned
+// 256-bit integer (the whitening PRN is identically 0), id as a final tie-break.
+// ---------------------------------------------------------------------------
+struct OKey {
+  uint64_t a;  // call << 32 | rr
+  uint64_t b;  // cts ^ sign
+  uint64_t s0, s1, s2, s3;
+  uint32_t id;
+  uint32_t pad;
+};
+
+__device__ __forceinline__ bool okless(const OKey& x, const OKey& y) {
+  if (x.a != y.a) return x.a < y.a;
+  if (x.b != y.b) return x.b < y.b;
+  if (x.s0 != y.s0) return x.s0 < y.s0;
+  if (x.s1 != y.s1) return x.s1 < y.s1;
+  if (x.s2 != y.s2) return x.s2 < y.s2;
+  if (x.s3 != y.s3) return x.s3 < y.s3;
+  return x.id < y.id;
+}
+
+__global__ void k_make_keys(Tables t, const int32_t* cand, int ncand, const int32_t* recv_call,
+                            const int32_t* rr, const int64_t* cts, const int32_t* rank,
+                            OKey* keys) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= ncand || recv_call[q] < 0) return;
+  const int x = cand[q];
+  OKey k;
+  k.a = ((uint64_t)(uint32_t)recv_call[q] << 32) | (uint32_t)rr[q];
+  k.b = (uint64_t)cts[q] ^ 0x8000000000000000ull;
+  k.s0 = t.S[4 * (size_t)x];
+  k.s1 = t.S[4 * (size_t)x + 1];
+  k.s2 = t.S[4 * (size_t)x + 2];
+  k.s3 = t.S[4 * (size_t)x + 3];
+  k.id = (uint32_t)x;
+  k.pad = 0;
+  keys[rank[q]] = k;
+}
+
+// bitonic sort of 1024-key tiles in LDS (tail padded with +inf keys)
+__global__ void __launch_bounds__(512) k_sort_tiles(OKey* keys, int n) {
+  __shared__ OKey sk[1024];
+  const int base = blockIdx.x * 1024;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 1024; i += 512) {
+    if (base + i < n) sk[i] = keys[base + i];
+    else {
+      OKey inf;
+      inf.a = inf.b = inf.s0 = inf.s1 = inf.s2 = inf.s3 = ~0ull;
+      inf.id = 0xFFFFFFFFu;
+      inf.pad = 0;
+      sk[i] = inf;
+    }
+  }
+  __syncthreads();
+  for (int size = 2; size <= 1024; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const int i = tid;
+      const int lo = 2 * stride * (i / stride) + (i % stride);
+      const int hi = lo + stride;
+      const bool up = ((lo & size) == 0);
+      OKey a = sk[lo], b = sk[hi];
+      if (okless(b, a) == up) {
+        sk[lo] = b;
+        sk[hi] = a;
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < 1024; i += 512)
+    if (base + i < n) keys[base + i] = sk[i];
+}
+
+// one merge pass of sorted runs of length `run`: rank-based (keys are unique)
+__global__ void k_merge_pass(const OKey* in, OKey* out, int n, int run) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int pair = i / (2 * run);
+  const int a0 = pair * 2 * run;
+  const int b0 = min(n, a0 + run);
+  const int b1 = min(n, a0 + 2 * run);
+  const OKey k = in[i];
+  int pos;
+  if (i < b0) {
+    // count of right-run keys less than k
+    int lo = b0, hi = b1;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (okless(in[mid], k)) lo = mid + 1;
+      else hi = mid;
+    }
+    pos = a0 + (i - a0) + (lo - b0);
+  } else {
+    int lo = a0, hi = b0;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (okless(in[mid], k)) lo = mid + 1;
+      else hi = mid;
+    }
+    pos = a0 + (i - b0) + (lo - a0);
+  }
+  out[pos] = k;
+}
+
+__global__ void k_emit_order(const OKey* keys, int n, int32_t* ids, int32_t* call_counts,
+                             int32_t call_lo) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  ids[i] = (int32_t)keys[i].id;
+  atomicAdd(&call_counts[(int)(keys[i].a >> 32) - call_lo], 1);
+}
+
+// flags for compaction: received (and committing) vs still undetermined
+__global__ void k_recv_flags(const int32_t* recv_call, int ncand, int32_t* f_recv,
+                             int32_t* f_und, int commit) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= ncand) return;
+  const int r = recv_call[q] >= 0;
+  f_recv[q] = r;
+  f_und[q] = commit ? !r : 1;
+}
+
+__global__ void k_scatter_und(const int32_t* cand, int ncand, const int32_t* f_und,
+                              const int32_t* pos, int32_t* und) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= ncand || !f_und[q]) return;
+  und[pos[q]] = cand[q];
+}
+
+__global__ void k_set_rr(Tables t, const int32_t* cand, int ncand, const int32_t* recv_call,
+                         const int32_t* rr, const int64_t* cts, int32_t* ev_rr, int64_t* ev_cts,
+                         unsigned long long* ntx_sum, int commit) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= ncand || recv_call[q] < 0) return;
+  const int x = cand[q];
+  ev_rr[x] = rr[q];
+  ev_cts[x] = cts[q];
+  if (commit) atomicAdd(ntx_sum, (unsigned long long)t.ntx[x]);
+}
+
+// LastCommitedRoundEvents = RoundEvents(LCR-1) at the call that set LCR
+// (hashgraph.go:666-673): events of round r minus those inserted after that call.
+__global__ void k_count_late(Tables t, int n_from, int n1, int r, int32_t* out) {
+  const int x = n_from + blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= n1) return;
+  if (t.round[x] == r) atomicAdd(out, 1);
+}
+
+}  // namespace hge

@@ -1,0 +1,333 @@
+"""ctypes front-end of the MI355X engine's C ABI (include/hge.h).
+
+`Engine` mirrors the methods of babble's Go `hashgraph.Hashgraph` that the
+caller (node/core.go) uses — InsertEvent, DivideRounds, DecideFame,
+DecideRoundReceived, FindOrder, ConsensusEvents, Known — plus the predicates
+the reference's tests call.  Events are addressed by the dense ids the engine
+assigns in insertion order.  The library is the product path: if it is
+missing or cannot load, this module raises — there is no CPU fallback.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("HGE_LIB", os.path.join(_ROOT, "build", "libhge.so"))
+
+HGE_NONE = -1
+HGE_UNKNOWN = -2
+
+ERRORS = {
+    -1: "Could not find fake creator id",
+    -2: "Self-parent not known",
+    -3: "Self-parent has different creator",
+    -4: "Other-parent not known",
+    -5: "Self-parent not last known event by creator",
+    -6: "Event index does not match the creator's chain position",
+}
+
+
+class HgeEvent(ctypes.Structure):
+    _fields_ = [
+        ("creator", ctypes.c_int32),
+        ("index", ctypes.c_int32),
+        ("self_parent", ctypes.c_int32),
+        ("other_parent", ctypes.c_int32),
+        ("timestamp_ns", ctypes.c_int64),
+        ("s", ctypes.c_uint8 * 32),
+        ("hash", ctypes.c_uint8 * 32),
+        ("n_tx", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+EVENT_DTYPE = np.dtype([
+    ("creator", "<i4"), ("index", "<i4"), ("self_parent", "<i4"), ("other_parent", "<i4"),
+    ("timestamp_ns", "<i8"), ("s", "u1", (32,)), ("hash", "u1", (32,)), ("n_tx", "<i4"),
+    ("reserved", "<i4"),
+])
+assert EVENT_DTYPE.itemsize == ctypes.sizeof(HgeEvent)
+
+EXPORTS = [
+    "hge_create", "hge_destroy", "hge_last_error", "hge_reset", "hge_insert_events",
+    "hge_divide_rounds", "hge_decide_fame", "hge_decide_round_received", "hge_find_order",
+    "hge_run_consensus", "hge_replay", "hge_replay_prepare", "hge_replay_run",
+    "hge_replay_fetch", "hge_event_count", "hge_participants", "hge_rounds",
+    "hge_last_consensus_round", "hge_last_committed_round_events",
+    "hge_consensus_transactions", "hge_consensus_count", "hge_consensus_events",
+    "hge_undetermined", "hge_known", "hge_round_of", "hge_is_witness", "hge_round_witness",
+    "hge_fame", "hge_round_events", "hge_round_received", "hge_consensus_timestamp",
+    "hge_ancestor", "hge_self_ancestor", "hge_see", "hge_strongly_see",
+    "hge_oldest_self_ancestor_to_see", "hge_coordinates", "hge_stage_times",
+]
+
+_lib = None
+
+
+class HgeError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{msg} (hge status {code})")
+        self.code = code
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"HIP engine library not built: {LIB_PATH} (run __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    P = ctypes.POINTER
+    L.hge_create.argtypes = [i32, i64, i32, ctypes.c_uint32, P(vp)]
+    L.hge_destroy.argtypes = [vp]
+    L.hge_destroy.restype = None
+    L.hge_last_error.argtypes = [vp]
+    L.hge_last_error.restype = ctypes.c_char_p
+    L.hge_reset.argtypes = [vp]
+    L.hge_insert_events.argtypes = [vp, ctypes.c_void_p, i64, P(i32), P(i64)]
+    for f in ("hge_divide_rounds", "hge_decide_fame", "hge_decide_round_received"):
+        getattr(L, f).argtypes = [vp]
+    for f in ("hge_find_order", "hge_run_consensus"):
+        getattr(L, f).argtypes = [vp, P(i32), i64, P(i64)]
+    L.hge_replay.argtypes = [vp, ctypes.c_void_p, i64, P(i64), i64, P(i32), P(i32), i64, P(i64),
+                             P(i64)]
+    L.hge_replay_prepare.argtypes = [vp, ctypes.c_void_p, i64, P(i64), i64, P(i32)]
+    L.hge_replay_run.argtypes = [vp, P(i64)]
+    L.hge_replay_fetch.argtypes = [vp, P(i32), i64, P(i64)]
+    for f in ("hge_event_count", "hge_consensus_transactions", "hge_consensus_count"):
+        getattr(L, f).argtypes = [vp]
+        getattr(L, f).restype = i64
+    for f in ("hge_participants", "hge_rounds", "hge_last_consensus_round",
+              "hge_last_committed_round_events"):
+        getattr(L, f).argtypes = [vp]
+        getattr(L, f).restype = i32
+    for f in ("hge_consensus_events", "hge_undetermined"):
+        getattr(L, f).argtypes = [vp, P(i32), i64]
+        getattr(L, f).restype = i64
+    L.hge_known.argtypes = [vp, P(i32)]
+    for f in ("hge_round_of", "hge_is_witness", "hge_round_events", "hge_round_received"):
+        getattr(L, f).argtypes = [vp, i32]
+        getattr(L, f).restype = i32
+    L.hge_consensus_timestamp.argtypes = [vp, i32]
+    L.hge_consensus_timestamp.restype = i64
+    for f in ("hge_round_witness", "hge_fame", "hge_ancestor", "hge_self_ancestor", "hge_see",
+              "hge_strongly_see", "hge_oldest_self_ancestor_to_see"):
+        getattr(L, f).argtypes = [vp, i32, i32]
+        getattr(L, f).restype = i32
+    L.hge_coordinates.argtypes = [vp, i32, P(i32), P(i32)]
+    L.hge_stage_times.argtypes = [vp, P(ctypes.c_float), ctypes.c_int]
+    _lib = L
+    return L
+
+
+def _p32(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+
+
+def _p64(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+
+
+def events_array(dag):
+    """Pack a submission-stream dict (babble_amd.gossip layout) into hge_event records.
+    Parents stay submission indices (hge_replay's convention)."""
+    E = len(dag["creator"])
+    ev = np.zeros(E, EVENT_DTYPE)
+    ev["creator"] = dag["creator"]
+    ev["index"] = dag["index"]
+    ev["self_parent"] = dag["sp"]
+    ev["other_parent"] = dag["op"]
+    ev["timestamp_ns"] = dag["ts"]
+    ev["s"] = dag["S"]
+    ev["hash"] = dag["hash"]
+    ev["n_tx"] = dag.get("ntx", np.zeros(E, np.int32))
+    return ev
+
+
+class Engine:
+    """One hashgraph (Hashgraph + Store) resident on one GPU."""
+
+    def __init__(self, n_participants, capacity_events=1 << 16, device=0):
+        self.L = lib()
+        h = ctypes.c_void_p()
+        rc = self.L.hge_create(n_participants, capacity_events, device, 0, ctypes.byref(h))
+        if rc != 0:
+            raise HgeError(rc, "hge_create failed")
+        self.h = h
+        self.n = n_participants
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.hge_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != 0:
+            raise HgeError(rc, self.L.hge_last_error(self.h).decode())
+        return rc
+
+    # --- ingest ----------------------------------------------------------
+    def insert_events(self, ev):
+        """InsertEvent for each record (stops at the first rejection, like Core.Sync).
+        Returns the assigned ids; raises HgeError on the first rejected event."""
+        ev = np.ascontiguousarray(ev, EVENT_DTYPE)
+        status = np.zeros(len(ev), np.int32)
+        acc = ctypes.c_int64()
+        rc = self.L.hge_insert_events(self.h, ev.ctypes.data, len(ev), _p32(status), ctypes.byref(acc))
+        if rc != 0:
+            raise HgeError(rc, self.L.hge_last_error(self.h).decode())
+        return status[:acc.value]
+
+    def insert(self, creator, index, sp, op, ts, S=b"\0" * 32, hash32=b"\1" * 32, ntx=0):
+        ev = np.zeros(1, EVENT_DTYPE)
+        ev["creator"], ev["index"], ev["self_parent"], ev["other_parent"] = creator, index, sp, op
+        ev["timestamp_ns"] = ts
+        ev["s"][0] = np.frombuffer(S, np.uint8)
+        ev["hash"][0] = np.frombuffer(hash32, np.uint8)
+        ev["n_tx"] = ntx
+        return int(self.insert_events(ev)[0])
+
+    # --- consensus -------------------------------------------------------
+    def divide_rounds(self):
+        self._check(self.L.hge_divide_rounds(self.h))
+
+    def decide_fame(self):
+        self._check(self.L.hge_decide_fame(self.h))
+
+    def decide_round_received(self):
+        self._check(self.L.hge_decide_round_received(self.h))
+
+    def _order_call(self, fn):
+        cap = max(1, int(self.L.hge_event_count(self.h)))
+        out = np.zeros(cap, np.int32)
+        n = ctypes.c_int64()
+        self._check(fn(self.h, _p32(out), cap, ctypes.byref(n)))
+        return out[:n.value]
+
+    def find_order(self):
+        return self._order_call(self.L.hge_find_order)
+
+    def run_consensus(self):
+        return self._order_call(self.L.hge_run_consensus)
+
+    def replay(self, dag_or_events, call_points):
+        ev = dag_or_events if isinstance(dag_or_events, np.ndarray) else events_array(dag_or_events)
+        self.prepare(ev, call_points)
+        self.run()
+        return self.fetch()
+
+    def prepare(self, ev, call_points):
+        ev = np.ascontiguousarray(ev, EVENT_DTYPE)
+        cp = np.ascontiguousarray(call_points, np.int64)
+        self._status = np.zeros(len(ev), np.int32)
+        self._ncalls = len(cp)
+        self._check(self.L.hge_replay_prepare(self.h, ev.ctypes.data, len(ev), _p64(cp), len(cp),
+                                              _p32(self._status)))
+        return self._status
+
+    def run(self):
+        n = ctypes.c_int64()
+        self._check(self.L.hge_replay_run(self.h, ctypes.byref(n)))
+        self._nordered = n.value
+        return n.value
+
+    def fetch(self):
+        order = np.zeros(max(1, self._nordered), np.int32)
+        counts = np.zeros(max(1, self._ncalls), np.int64)
+        self._check(self.L.hge_replay_fetch(self.h, _p32(order), len(order), _p64(counts)))
+        return self._status, order[:self._nordered], counts[:self._ncalls]
+
+    def stage_times(self):
+        out = (ctypes.c_float * 7)()
+        n = self.L.hge_stage_times(self.h, out, 7)
+        return list(out)[:n]
+
+    # --- state -----------------------------------------------------------
+    def event_count(self):
+        return self.L.hge_event_count(self.h)
+
+    def rounds(self):
+        return self.L.hge_rounds(self.h)
+
+    def last_consensus_round(self):
+        r = self.L.hge_last_consensus_round(self.h)
+        return None if r < 0 else r
+
+    def last_committed_round_events(self):
+        return self.L.hge_last_committed_round_events(self.h)
+
+    def consensus_transactions(self):
+        return self.L.hge_consensus_transactions(self.h)
+
+    def consensus_events(self):
+        m = self.L.hge_consensus_count(self.h)
+        out = np.zeros(max(1, m), np.int32)
+        self.L.hge_consensus_events(self.h, _p32(out), m)
+        return out[:m]
+
+    def undetermined(self):
+        m = self.L.hge_undetermined(self.h, None, 0)
+        out = np.zeros(max(1, m), np.int32)
+        self.L.hge_undetermined(self.h, _p32(out), m)
+        return out[:m]
+
+    def known(self):
+        out = np.zeros(self.n, np.int32)
+        self.L.hge_known(self.h, _p32(out))
+        return out
+
+    def round(self, x):
+        return self.L.hge_round_of(self.h, x)
+
+    def witness(self, x):
+        return bool(self.L.hge_is_witness(self.h, x))
+
+    def round_witness(self, r, creator):
+        w = self.L.hge_round_witness(self.h, r, creator)
+        return None if w < 0 else w
+
+    def round_witnesses(self, r):
+        return sorted(w for w in (self.round_witness(r, c) for c in range(self.n)) if w is not None)
+
+    def fame(self, r, creator):
+        return self.L.hge_fame(self.h, r, creator)
+
+    def round_events(self, r):
+        return self.L.hge_round_events(self.h, r)
+
+    def round_received(self, x):
+        r = self.L.hge_round_received(self.h, x)
+        return None if r < 0 else r
+
+    def consensus_timestamp(self, x):
+        return self.L.hge_consensus_timestamp(self.h, x)
+
+    def ancestor(self, x, y):
+        return bool(self.L.hge_ancestor(self.h, x, y))
+
+    def self_ancestor(self, x, y):
+        return bool(self.L.hge_self_ancestor(self.h, x, y))
+
+    def see(self, x, y):
+        return bool(self.L.hge_see(self.h, x, y))
+
+    def strongly_see(self, x, y):
+        return bool(self.L.hge_strongly_see(self.h, x, y))
+
+    def oldest_self_ancestor_to_see(self, x, y):
+        r = self.L.hge_oldest_self_ancestor_to_see(self.h, x, y)
+        return None if r < 0 else r
+
+    def coordinates(self, x):
+        la = np.zeros(self.n, np.int32)
+        fd = np.zeros(self.n, np.int32)
+        self._check(self.L.hge_coordinates(self.h, x, _p32(la), _p32(fd)))
+        return la, fd

@@ -1,0 +1,151 @@
+"""Seeded synthetic event streams.
+
+Random gossip, mirroring babble's RandomPeerSelector
+(/root/reference/node/peer_selector.go:53-61: a node never picks itself):
+  * the first N submissions are the initial events (index 0, no parents);
+  * every later submission picks creator a ~ U[0,N) and peer b ~ U[0,N)\\{a}
+    and emits (creator a, index seq[a]++, self-parent head[a], other-parent head[b]).
+
+Fields: ts = base + 1000 * submission (strictly increasing ns), S = 256-bit
+uniform (SplitMix64 stream keyed by (seed, submission)), hash = 32 bytes from
+the same family (only hash[16], the coin bit of hashgraph.go:781-790, and
+identity matter to the ordering path).
+
+Byzantine forkers (config 5): a subset of creators, with probability p per
+event, also submit a second event with the same (creator, index, parents) and
+a different hash/S right after the honest one.  The first-inserted branch wins;
+the fork is rejected by FromParentsLatest (hashgraph.go:366-396) and nothing
+references it.
+"""
+import numpy as np
+
+TS_BASE = 1_500_000_000_000_000_000  # 2017-07-14 in ns; any fixed epoch works
+
+
+def _splitmix64(x):
+    x = (x + np.uint64(0x9E3779B97F4A7C15)) & np.uint64(0xFFFFFFFFFFFFFFFF)
+    z = x
+    z = ((z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & np.uint64(0xFFFFFFFFFFFFFFFF)
+    z = ((z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & np.uint64(0xFFFFFFFFFFFFFFFF)
+    return z ^ (z >> np.uint64(31))
+
+
+def _bytes32(seed, salt, n):
+    """n x 32 pseudo-random bytes keyed by (seed, salt, row)."""
+    rows = np.arange(n, dtype=np.uint64)
+    out = np.empty((n, 4), np.uint64)
+    base = np.uint64((seed * 0x100000001B3 + salt * 0x9E3779B1) & 0xFFFFFFFFFFFFFFFF)
+    with np.errstate(over="ignore"):
+        for k in range(4):
+            out[:, k] = _splitmix64(rows * np.uint64(4) + np.uint64(k) + base * np.uint64(7919))
+    return out.astype(">u8").view(np.uint8).reshape(n, 32)
+
+
+def random_gossip(n, events, seed=1, forkers=0, fork_p=0.0):
+    """Return a dict describing a submission stream of `events` honest events.
+
+    Keys: n, creator, index, sp, op (submission indices, -1 = none), ts, S
+    (uint8[E,32] big-endian), hash (uint8[E,32]), ntx, honest (bool mask).
+    """
+    assert n >= 1 and events >= n
+    rng = np.random.default_rng(seed)
+    m = events - n
+    a = rng.integers(0, n, m)
+    if n > 1:
+        b = rng.integers(0, n - 1, m)
+        b = b + (b >= a)  # U[0,N) \ {a}
+    else:
+        b = np.zeros(m, np.int64)
+    creator = np.concatenate([np.arange(n), a]).astype(np.int32)
+    E = events
+    # sp = previous submission of the same creator
+    order = np.argsort(creator, kind="stable")
+    cs = creator[order]
+    prev = np.full(E, -1, np.int64)
+    same = cs[1:] == cs[:-1]
+    prev[order[1:][same]] = order[:-1][same]
+    index = np.zeros(E, np.int64)
+    # index = rank within creator
+    starts = np.searchsorted(cs, np.arange(n))
+    rank = np.arange(E) - starts[cs]
+    index[order] = rank
+    # op = latest submission of creator b strictly before this one
+    op = np.full(E, -1, np.int64)
+    if m:
+        subs = np.arange(n, E)
+        ends = np.searchsorted(cs, np.arange(n), side="right")
+        # position of the last event of creator b before `sub`: events of b sorted by submission
+        bb = b.astype(np.int64)
+        lo = starts[bb]
+        # per creator, submissions in order -> searchsorted within the creator's slice
+        pos = np.empty(m, np.int64)
+        for c in range(n):
+            sel = np.nonzero(bb == c)[0]
+            if sel.size == 0:
+                continue
+            slice_ = order[starts[c]:ends[c]]
+            k = np.searchsorted(slice_, subs[sel], side="left") - 1
+            pos[sel] = slice_[k]
+        del lo
+        op[n:] = pos
+    dag = {
+        "n": n,
+        "creator": creator,
+        "index": index.astype(np.int32),
+        "sp": prev.astype(np.int32),
+        "op": op.astype(np.int32),
+        "ts": (TS_BASE + 1000 * np.arange(E, dtype=np.int64)),
+        "S": _bytes32(seed, 1, E),
+        "hash": _bytes32(seed, 2, E),
+        "ntx": np.ones(E, np.int32),
+        "honest": np.ones(E, bool),
+    }
+    if forkers and fork_p > 0:
+        dag = _inject_forks(dag, rng, forkers, fork_p, seed)
+    return dag
+
+
+def _inject_forks(dag, rng, forkers, p, seed):
+    E = len(dag["creator"])
+    n = dag["n"]
+    fset = np.zeros(n, bool)
+    fset[rng.choice(n, size=min(forkers, n), replace=False)] = True
+    fork = fset[dag["creator"]] & (rng.random(E) < p) & (dag["sp"] >= 0)
+    nf = int(fork.sum())
+    if nf == 0:
+        return dag
+    # new submission order: each forked event is followed by its fork twin
+    reps = 1 + fork.astype(np.int64)
+    new_pos = np.cumsum(reps) - reps  # position of the honest copy
+    tot = E + nf
+    src = np.repeat(np.arange(E), reps)
+    is_twin = np.zeros(tot, bool)
+    is_twin[new_pos[fork] + 1] = True
+
+    def remap(p_):
+        return np.where(p_ >= 0, new_pos[np.maximum(p_, 0)], -1).astype(np.int32)
+
+    out = {"n": n}
+    for k in ("creator", "index", "ntx"):
+        out[k] = dag[k][src]
+    out["sp"] = remap(dag["sp"])[src]
+    out["op"] = remap(dag["op"])[src]
+    out["ts"] = dag["ts"][src].copy()
+    out["S"] = dag["S"][src].copy()
+    out["hash"] = dag["hash"][src].copy()
+    twin_S = _bytes32(seed, 3, nf)
+    twin_H = _bytes32(seed, 4, nf)
+    out["S"][is_twin] = twin_S
+    out["hash"][is_twin] = twin_H
+    out["ts"][is_twin] += 1
+    out["honest"] = ~is_twin
+    return out
+
+
+def schedule(n_submissions, k):
+    """RunConsensus after every k submissions and after the last one."""
+    k = max(1, int(k))
+    pts = list(range(k, n_submissions + 1, k))
+    if not pts or pts[-1] != n_submissions:
+        pts.append(n_submissions)
+    return np.array(pts, np.int64)

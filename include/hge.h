@@ -1,0 +1,141 @@
+/*
+ * hge.h — C ABI of the MI355X hashgraph consensus-ordering engine.
+ *
+ * Drop-in boundary for babble's `hashgraph` package (mpitid/babble,
+ * /root/reference/hashgraph).  A thin cgo shim (go/hashgraph/engine.go,
+ * INTEGRATION.md) keeps the Go `Hashgraph` / `Store` method set and forwards
+ * here; node/, net/ and proxy/ are untouched.  Plain pointers and sizes only.
+ *
+ * Events are identified by dense engine ids assigned in insertion order (the
+ * shim keeps the hash <-> id map).  Hashing and ECDSA verification stay with
+ * the caller (event.go:140-186).
+ *
+ * Threading: one handle is used by one thread at a time (the reference
+ * serialises Core under Node.coreLock, node/node.go:167-169).
+ * Errors: functions return HGE_OK or a negative hge_status; hge_last_error()
+ * gives the reference's error text.
+ */
+#ifndef HGE_H
+#define HGE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct hge_engine hge_engine;
+
+/* Status codes.  -1..-5 mirror the reference's InsertEvent errors. */
+enum hge_status {
+  HGE_OK = 0,
+  HGE_ERR_CREATOR = -1,              /* "Could not find fake creator id"        hashgraph.go:453-456 */
+  HGE_ERR_SELF_PARENT_UNKNOWN = -2,  /* "Self-parent not known"                 hashgraph.go:373-376 */
+  HGE_ERR_SELF_PARENT_CREATOR = -3,  /* "Self-parent has different creator"     hashgraph.go:377-379 */
+  HGE_ERR_OTHER_PARENT_UNKNOWN = -4, /* "Other-parent not known"                hashgraph.go:381-384 */
+  HGE_ERR_SELF_PARENT_NOT_LAST = -5, /* "Self-parent not last known event..."   hashgraph.go:390-393 */
+  HGE_ERR_INDEX = -6,      /* Body.Index != position in the creator's chain (stricter than the reference) */
+  HGE_ERR_CAPACITY = -7,   /* device allocation failed */
+  HGE_ERR_ARG = -8,        /* bad argument */
+  HGE_ERR_DEVICE = -9,     /* HIP runtime error */
+  HGE_ERR_INTERNAL = -10
+};
+
+/* Parent reference values. */
+#define HGE_NONE (-1)    /* empty parent ""                                   */
+#define HGE_UNKNOWN (-2) /* hash the caller could not resolve: "not known"    */
+
+/* One event as handed over by the caller (Event, event.go:73-88). */
+typedef struct hge_event {
+  int32_t creator;       /* participant id (Participants[pubkey])                  */
+  int32_t index;         /* Body.Index                                             */
+  int32_t self_parent;   /* engine id, HGE_NONE or HGE_UNKNOWN  (Body.Parents[0])  */
+  int32_t other_parent;  /* engine id, HGE_NONE or HGE_UNKNOWN  (Body.Parents[1])  */
+  int64_t timestamp_ns;  /* Body.Timestamp                                         */
+  uint8_t s[32];         /* signature S, unsigned big-endian (consensus tie-break) */
+  uint8_t hash[32];      /* SHA-256 of the event; hash[16] is the coin bit         */
+  int32_t n_tx;          /* len(Body.Transactions)                                 */
+  int32_t reserved;
+} hge_event;
+
+/* ---- lifecycle ------------------------------------------------------------ */
+/* NewHashgraph (hashgraph.go:51-76) + NewInmemStore (inmem_store.go:27-36) with
+ * unbounded capacity.  capacity_events is a sizing hint (tables grow). */
+int hge_create(int32_t n_participants, int64_t capacity_events, int32_t device,
+               uint32_t flags, hge_engine** out);
+void hge_destroy(hge_engine* h);
+const char* hge_last_error(hge_engine* h);
+int hge_reset(hge_engine* h); /* forget all events, keep allocations */
+
+/* ---- ingest ---------------------------------------------------------------- */
+/* InsertEvent (hashgraph.go:328-363) for n events in order.  Processing stops at
+ * the first rejected event, like Core.Sync (node/core.go:137-145).  Accepted
+ * events receive ids hge_event_count() .. +n_accepted-1; status_out[i] is the
+ * id or a negative hge_status for the first rejection (may be NULL). */
+int hge_insert_events(hge_engine* h, const hge_event* ev, int64_t n, int32_t* status_out,
+                      int64_t* n_accepted);
+
+/* ---- consensus (node/core.go:179-202) --------------------------------------- */
+int hge_divide_rounds(hge_engine* h);          /* hashgraph.go:573-588 */
+int hge_decide_fame(hge_engine* h);            /* hashgraph.go:598-664 */
+int hge_decide_round_received(hge_engine* h);  /* hashgraph.go:676-721 (no commit) */
+/* FindOrder (hashgraph.go:723-760): commits this call's batch in consensus order.
+ * ids_out may be NULL; *n_out = batch size (ids beyond cap are dropped). */
+int hge_find_order(hge_engine* h, int32_t* ids_out, int64_t cap, int64_t* n_out);
+/* DivideRounds + DecideFame + FindOrder */
+int hge_run_consensus(hge_engine* h, int32_t* ids_out, int64_t cap, int64_t* n_out);
+
+/* ---- bulk replay (bench / Monte Carlo) --------------------------------------- */
+/* Replays a whole submission stream on a fresh state: parents are submission
+ * indices (-1 none); rejected submissions are skipped and status_out records
+ * them; RunConsensus runs after each submission count in call_points (1-based,
+ * ascending).  Results are identical to calling hge_insert_events and
+ * hge_run_consensus at every call point.  order_out receives the full consensus
+ * order, call_counts_out[c] the batch size of call c (both may be NULL). */
+int hge_replay(hge_engine* h, const hge_event* ev, int64_t n_sub, const int64_t* call_points,
+               int64_t n_calls, int32_t* status_out, int32_t* order_out, int64_t cap,
+               int64_t* n_ordered, int64_t* call_counts_out);
+/* Split form for timing: prepare (validate + stage in HBM) then run on the device. */
+int hge_replay_prepare(hge_engine* h, const hge_event* ev, int64_t n_sub,
+                       const int64_t* call_points, int64_t n_calls, int32_t* status_out);
+int hge_replay_run(hge_engine* h, int64_t* n_ordered);
+int hge_replay_fetch(hge_engine* h, int32_t* order_out, int64_t cap, int64_t* call_counts_out);
+
+/* ---- state queries --------------------------------------------------------- */
+int64_t hge_event_count(hge_engine* h);
+int32_t hge_participants(hge_engine* h);
+int32_t hge_rounds(hge_engine* h);                    /* Store.Rounds()            */
+int32_t hge_last_consensus_round(hge_engine* h);      /* -1 = nil                  */
+int32_t hge_last_committed_round_events(hge_engine* h);
+int64_t hge_consensus_transactions(hge_engine* h);
+int64_t hge_consensus_count(hge_engine* h);           /* Store.ConsensusEventsCount */
+int64_t hge_consensus_events(hge_engine* h, int32_t* ids_out, int64_t cap);
+int64_t hge_undetermined(hge_engine* h, int32_t* ids_out, int64_t cap);
+int hge_known(hge_engine* h, int32_t* counts_out);    /* Known(), n_participants ints */
+int32_t hge_round_of(hge_engine* h, int32_t id);      /* Round(x) (after DivideRounds) */
+int32_t hge_is_witness(hge_engine* h, int32_t id);    /* Witness(x)                    */
+int32_t hge_round_witness(hge_engine* h, int32_t round, int32_t creator); /* id or -1 */
+int32_t hge_fame(hge_engine* h, int32_t round, int32_t creator); /* 0 undef, 1 true, 2 false, -1 none */
+int32_t hge_round_events(hge_engine* h, int32_t round);          /* Store.RoundEvents(r) */
+int32_t hge_round_received(hge_engine* h, int32_t id);           /* -1 = nil */
+int64_t hge_consensus_timestamp(hge_engine* h, int32_t id);
+
+/* ---- test predicates (hashgraph.go:82-208) --------------------------------- */
+int32_t hge_ancestor(hge_engine* h, int32_t x, int32_t y);
+int32_t hge_self_ancestor(hge_engine* h, int32_t x, int32_t y);
+int32_t hge_see(hge_engine* h, int32_t x, int32_t y);
+int32_t hge_strongly_see(hge_engine* h, int32_t x, int32_t y);
+int32_t hge_oldest_self_ancestor_to_see(hge_engine* h, int32_t x, int32_t y); /* id or -1 */
+/* lastAncestors / firstDescendants indices of x (FD unset = INT32_MAX), N ints each. */
+int hge_coordinates(hge_engine* h, int32_t id, int32_t* la_out, int32_t* fd_out);
+
+/* ---- profiling ------------------------------------------------------------- */
+/* Device milliseconds of the last replay/batch by stage (HIP events on the
+ * engine's stream): 0 coords, 1 rounds, 2 witness bits, 3 fame, 4 received,
+ * 5 order, 6 total.  Returns the number of stages written. */
+int hge_stage_times(hge_engine* h, float* ms_out, int cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HGE_H */
