@@ -31,6 +31,13 @@ using namespace hge;
     }                                                                                \
   } while (0)
 
+#define KLAUNCH(kern, ...)             \
+  do {                                 \
+    prof_begin(#kern);                 \
+    hipLaunchKernelGGL(kern, __VA_ARGS__); \
+    prof_end();                        \
+  } while (0)
+
 namespace {
 
 struct EngineError {
@@ -131,6 +138,13 @@ struct hge_engine {
   DBuf<unsigned long long> s_ntx;
 
   hipEvent_t ev[8] = {};
+  // per-kernel HIP-event timing on the engine stream (hge_set_profiling)
+  bool prof_on = false;
+  std::vector<hipEvent_t> prof_pool;
+  std::vector<std::pair<std::string, int>> prof_rec;
+  std::vector<std::string> prof_names;
+  std::vector<double> prof_ms;
+  std::vector<int64_t> prof_cnt;
   bool br_in_lds = true;
   int R_div = 0;            // Rounds() as seen by the consensus calls (DivideRounds)
   float stage_ms[7] = {};
@@ -187,6 +201,40 @@ struct hge_engine {
     ensure_rcap(std::max<int64_t>(64, std::max<int64_t>(cap, 1024) / SM + 8));
   }
 
+  void prof_begin(const char* name) {
+    if (!prof_on) return;
+    const int slot = (int)prof_rec.size() * 2;
+    while ((int)prof_pool.size() < slot + 2) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreate(&e));
+      prof_pool.push_back(e);
+    }
+    HIPCHK(hipEventRecord(prof_pool[slot], st));
+    prof_rec.push_back({name, slot});
+  }
+  void prof_end() {
+    if (!prof_on) return;
+    HIPCHK(hipEventRecord(prof_pool[prof_rec.back().second + 1], st));
+  }
+  void prof_collect() {
+    if (prof_rec.empty()) return;
+    HIPCHK(hipStreamSynchronize(st));
+    for (auto& r : prof_rec) {
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, prof_pool[r.second], prof_pool[r.second + 1]));
+      size_t k = 0;
+      while (k < prof_names.size() && prof_names[k] != r.first) k++;
+      if (k == prof_names.size()) {
+        prof_names.push_back(r.first);
+        prof_ms.push_back(0);
+        prof_cnt.push_back(0);
+      }
+      prof_ms[k] += ms;
+      prof_cnt[k] += 1;
+    }
+    prof_rec.clear();
+  }
+
   void set_lds_limits() {
     // best effort: gfx950 has 160 KiB of LDS per CU; kernels with static LDS
     // get a smaller dynamic ceiling
@@ -215,6 +263,8 @@ struct hge_engine {
     if (st) (void)hipStreamSynchronize(st);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
+    for (auto& e : prof_pool) (void)hipEventDestroy(e);
+    prof_pool.clear();
     DBuf<int32_t>* i32s[] = {&d_creator, &d_index, &d_sp, &d_op, &d_ntx, &d_round, &d_rr, &d_und,
                              &d_chain, &d_LA, &d_FD, &d_C, &d_W, &d_rcnt, &d_minw, &s_D, &s_enc,
                              &s_basis, &s_bcount, &s_boff, &s_BR, &s_small, &s_len, &s_newwit,
@@ -431,7 +481,7 @@ struct hge_engine {
     if (n1 == n0) return;
     Tables t = tables();
     const int m = (int)(n1 - n0);
-    hipLaunchKernelGGL(k_chain_fill, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0, (int)n1);
+    KLAUNCH(k_chain_fill, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0, (int)n1);
     // chunk length: LDS of phase A = L*(BW*8 + N*4 + 32) + BMAX*4 + ~1KB
     const int BMAX = BW * 64;
     int L = 1024;
@@ -456,7 +506,7 @@ struct hge_engine {
         continue;
       }
       if (flag[0]) throw EngineError(HGE_ERR_INTERNAL, "external basis overflow");
-      hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, st, s_bcount.p, s_boff.p, nch,
+      KLAUNCH(k_scan_small, dim3(1), dim3(1024), 0, st, s_bcount.p, s_boff.p, nch,
                          s_small.p + 2);
       int32_t total = 0;
       readback(&total, s_small.p + 2, 1);
@@ -481,7 +531,7 @@ struct hge_engine {
       int WIN = std::max(4, std::min(64, 16384 / (N * N)));
       const size_t lds = (size_t)(N * N + 8 * N + N * WIN) * 4;
       t = tables();
-      hipLaunchKernelGGL(k_rounds_frontier, dim3(1), dim3(1024), lds, st, t, s_len.p,
+      KLAUNCH(k_rounds_frontier, dim3(1), dim3(1024), lds, st, t, s_len.p,
                          s_len.p + N, s_small.p, WIN);
       readback(rs, s_small.p, 2);
       if (rs[1]) {
@@ -494,18 +544,19 @@ struct hge_engine {
     t = tables();
     s_newwit.need(m);
     HIPCHK(hipMemsetAsync(s_small.p + 4, 0, 4, st));
-    hipLaunchKernelGGL(k_round_assign, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0,
+    KLAUNCH(k_round_assign, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0,
                        (int)n1, R, s_newwit.p, s_small.p + 4);
     int32_t nnew = 0;
     readback(&nnew, s_small.p + 4, 1);
     if (nnew) {
       const int items = nnew * N;
-      hipLaunchKernelGGL(k_witness_bits, dim3(div_up(items, 256)), dim3(256), 0, st, t,
+      KLAUNCH(k_witness_bits, dim3(div_up(items, 256)), dim3(256), 0, st, t,
                          s_newwit.p, nnew);
     }
-    hipLaunchKernelGGL(k_round_minw, dim3(div_up(R, 256)), dim3(256), 0, st, t, 0, R, d_minw.p);
+    KLAUNCH(k_round_minw, dim3(div_up(R, 256)), dim3(256), 0, st, t, 0, R, d_minw.p);
     n_coords = n1;
     coords_len = chain_len;
+    prof_collect();
   }
 
   void launch_bw(int which, int nch, size_t lds, const Tables& t, int n0, int n1, int L, int nch2) {
@@ -513,13 +564,13 @@ struct hge_engine {
 #define CASE(B)                                                                                  \
   case B:                                                                                        \
     if (which == 0) {                                                                            \
-      hipLaunchKernelGGL(k_coord_local<B>, dim3(nch), dim3(256), lds, st, t, n0, n1, L, s_D.p,  \
+      KLAUNCH(k_coord_local<B>, dim3(nch), dim3(256), lds, st, t, n0, n1, L, s_D.p,  \
                          s_dep.p, s_enc.p, s_basis.p, s_bcount.p, s_small.p);                    \
     } else if (which == 1) {                                                                     \
-      hipLaunchKernelGGL(k_coord_basis<B>, dim3(1), dim3(1024), 0, st, t, n0, L, nch2, s_D.p,    \
+      KLAUNCH(k_coord_basis<B>, dim3(1), dim3(1024), 0, st, t, n0, L, nch2, s_D.p,    \
                          s_dep.p, s_basis.p, s_bcount.p, s_boff.p, s_BR.p);                      \
     } else {                                                                                     \
-      hipLaunchKernelGGL(k_coord_final<B>, dim3(nch), dim3(256), lds, st, t, n0, n1, L, s_D.p,  \
+      KLAUNCH(k_coord_final<B>, dim3(nch), dim3(256), lds, st, t, n0, n1, L, s_D.p,  \
                          s_dep.p, s_enc.p, s_bcount.p, s_boff.p, s_BR.p, br_in_lds ? 1 : 0);     \
     }                                                                                            \
     break;
@@ -545,7 +596,7 @@ struct hge_engine {
     s_nc.need(ncalls);
     HIPCHK(hipMemcpyAsync(s_nc.p, calls.data(), 8 * ncalls, hipMemcpyHostToDevice, st));
     s_Rc.need(ncalls);
-    hipLaunchKernelGGL(k_calls_rounds, dim3(div_up(ncalls, 256)), dim3(256), 0, st, s_nc.p,
+    KLAUNCH(k_calls_rounds, dim3(div_up(ncalls, 256)), dim3(256), 0, st, s_nc.p,
                        ncalls, d_minw.p, R, s_Rc.p);
     std::vector<int32_t> Rc(ncalls);
     readback(Rc.data(), s_Rc.p, ncalls);
@@ -601,7 +652,7 @@ struct hge_engine {
         HIPCHK(hipMemsetAsync(s_flags.p, 0, 16, st));
         const int items = npairs * N;
         fame_dispatch(0, t, nrounds, npairs, items, ncalls);
-        hipLaunchKernelGGL(k_lcr_scan, dim3(1), dim3(1024), 0, st, s_Lc.p, ncalls, lcr, s_LCR.p,
+        KLAUNCH(k_lcr_scan, dim3(1), dim3(1024), 0, st, s_Lc.p, ncalls, lcr, s_LCR.p,
                            s_pr.p, s_pr.p + 2 * nrounds, s_pr.p + 3 * nrounds, nrounds,
                            s_clast.p, s_flags.p);
         int32_t fl = 0;
@@ -668,7 +719,7 @@ struct hge_engine {
         s_segcnt.need(nr);
         s_segoff.need(nr + 1);
         seg_dispatch(0, t, rr_lo, nr, ncalls, si, 0);
-        hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, st, s_segcnt.p, s_segoff.p, nr,
+        KLAUNCH(k_scan_small, dim3(1), dim3(1024), 0, st, s_segcnt.p, s_segoff.p, nr,
                            s_small.p + 6);
         int32_t nseg = 0;
         readback(&nseg, s_small.p + 6, 1);
@@ -692,7 +743,7 @@ struct hge_engine {
       s_fund.need(ncand);
       s_rank.need(ncand);
       s_upos.need(ncand);
-      hipLaunchKernelGGL(k_recv_flags, dim3(div_up(ncand, 256)), dim3(256), 0, st, s_recv.p, ncand,
+      KLAUNCH(k_recv_flags, dim3(div_up(ncand, 256)), dim3(256), 0, st, s_recv.p, ncand,
                          s_frecv.p, s_fund.p, commit ? 1 : 0);
       scan_large(s_frecv.p, s_rank.p, ncand, s_small.p + 2);
       int32_t nrecv = 0;
@@ -700,7 +751,7 @@ struct hge_engine {
       s_ntx.need(1);
       HIPCHK(hipMemsetAsync(s_ntx.p, 0, 8, st));
       if (nrecv > 0) {
-        hipLaunchKernelGGL(k_set_rr, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand,
+        KLAUNCH(k_set_rr, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand,
                            s_recv.p, s_rr.p, s_cts.p, d_rr.p, d_cts.p, s_ntx.p, commit ? 1 : 0);
       }
       if (commit && nrecv > 0) {
@@ -708,18 +759,18 @@ struct hge_engine {
         s_keys2.need((size_t)nrecv * sizeof(OKey));
         OKey* k1 = (OKey*)s_keys.p;
         OKey* k2 = (OKey*)s_keys2.p;
-        hipLaunchKernelGGL(k_make_keys, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand,
+        KLAUNCH(k_make_keys, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand,
                            s_recv.p, s_rr.p, s_cts.p, s_rank.p, k1);
-        hipLaunchKernelGGL(k_sort_tiles, dim3(div_up(nrecv, 1024)), dim3(512), 0, st, k1, nrecv);
+        KLAUNCH(k_sort_tiles, dim3(div_up(nrecv, 1024)), dim3(512), 0, st, k1, nrecv);
         for (int run = 1024; run < nrecv; run *= 2) {
-          hipLaunchKernelGGL(k_merge_pass, dim3(div_up(nrecv, 256)), dim3(256), 0, st, k1, k2,
+          KLAUNCH(k_merge_pass, dim3(div_up(nrecv, 256)), dim3(256), 0, st, k1, k2,
                              nrecv, run);
           std::swap(k1, k2);
         }
         s_ids.need(nrecv);
         s_ccount.need(ncalls);
         HIPCHK(hipMemsetAsync(s_ccount.p, 0, 4 * ncalls, st));
-        hipLaunchKernelGGL(k_emit_order, dim3(div_up(nrecv, 256)), dim3(256), 0, st, k1, nrecv,
+        KLAUNCH(k_emit_order, dim3(div_up(nrecv, 256)), dim3(256), 0, st, k1, nrecv,
                            s_ids.p, s_ccount.p, 0);
         std::vector<int32_t> ids(nrecv);
         std::vector<int32_t> cc(ncalls);
@@ -738,7 +789,7 @@ struct hge_engine {
         int32_t nund = 0;
         readback(&nund, s_small.p + 3, 1);
         s_und2.need(std::max(nund, 1));
-        hipLaunchKernelGGL(k_scatter_und, dim3(div_up(ncand, 256)), dim3(256), 0, st, cand, ncand,
+        KLAUNCH(k_scatter_und, dim3(div_up(ncand, 256)), dim3(256), 0, st, cand, ncand,
                            s_fund.p, s_upos.p, s_und2.p);
         HIPCHK(hipMemcpyAsync(d_und.p, s_und2.p, 4 * (size_t)nund, hipMemcpyDeviceToDevice, st));
         n_und = nund;
@@ -761,7 +812,7 @@ struct hge_engine {
           const int64_t nfrom = calls[c_set];
           if (nfrom < n_coords) {
             HIPCHK(hipMemsetAsync(s_small.p + 5, 0, 4, st));
-            hipLaunchKernelGGL(k_count_late, dim3(div_up(n_coords - nfrom, 256)), dim3(256), 0, st,
+            KLAUNCH(k_count_late, dim3(div_up(n_coords - nfrom, 256)), dim3(256), 0, st,
                                t, (int)nfrom, (int)n_coords, r, s_small.p + 5);
             int32_t late = 0;
             readback(&late, s_small.p + 5, 1);
@@ -773,6 +824,7 @@ struct hge_engine {
       }
     }
     HIPCHK(hipStreamSynchronize(st));
+    prof_collect();
   }
 
   void gather_rounds(const std::vector<int32_t>& ids, std::vector<int32_t>& out) {
@@ -789,7 +841,7 @@ struct hge_engine {
 
   void scan_large(const int32_t* in, int32_t* out, int n, int32_t* total) {
     // one block of 1024 threads; adequate for the candidate counts involved
-    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, st, in, out, n, total);
+    KLAUNCH(k_scan_small, dim3(1), dim3(1024), 0, st, in, out, n, total);
   }
 
   void fame_dispatch(int which, const Tables& t, int nrounds, int npairs, int items, int ncalls) {
@@ -797,14 +849,14 @@ struct hge_engine {
 #define FCASE(B)                                                                                 \
   case B:                                                                                        \
     if (which == 0) {                                                                            \
-      hipLaunchKernelGGL(k_fame_decide<B>, dim3(div_up(items, 256)), dim3(256), 0, st, t,        \
+      KLAUNCH(k_fame_decide<B>, dim3(div_up(items, 256)), dim3(256), 0, st, t,        \
                          s_pr.p, s_pr.p + nrounds, s_pr.p + 2 * nrounds, nrounds, npairs,        \
                          s_nc.p, s_Rc.p, s_dec.p);                                               \
-      hipLaunchKernelGGL(k_fame_timeline<B>, dim3(div_up(nrounds, 64)), dim3(64), 0, st, t,      \
+      KLAUNCH(k_fame_timeline<B>, dim3(div_up(nrounds, 64)), dim3(64), 0, st, t,      \
                          s_pr.p, s_pr.p + nrounds, s_pr.p + 2 * nrounds, s_pr.p + 3 * nrounds,   \
                          nrounds, s_nc.p, s_dec.p, s_decbit.p, s_Lc.p);                          \
     } else {                                                                                     \
-      hipLaunchKernelGGL(k_fame_persist<B>, dim3(div_up(nrounds, 64)), dim3(64), 0, st, t,       \
+      KLAUNCH(k_fame_persist<B>, dim3(div_up(nrounds, 64)), dim3(64), 0, st, t,       \
                          s_pr.p, s_pr.p + nrounds, s_pr.p + 2 * nrounds, s_pr.p + 3 * nrounds,   \
                          nrounds, s_clast.p, s_dec.p);                                           \
     }                                                                                            \
@@ -825,11 +877,11 @@ struct hge_engine {
     switch (NW) {
 #define SCASE(B)                                                                                 \
   case B:                                                                                        \
-    hipLaunchKernelGGL(k_segments<B>, dim3(div_up(nr, 64)), dim3(64), 0, st, t, rr_lo, nr,       \
+    KLAUNCH(k_segments<B>, dim3(div_up(nr, 64)), dim3(64), 0, st, t, rr_lo, nr,       \
                        s_nc.p, ncalls, si, s_segcnt.p, s_segoff.p, s_segcall.p, s_seground.p,    \
                        s_segdec.p, s_segfws.p, mode);                                            \
     if (mode == 1 && nseg > 0)                                                                   \
-      hipLaunchKernelGGL(k_seg_theta<B>, dim3(div_up(nseg * N, 256)), dim3(256), 0, st, t,       \
+      KLAUNCH(k_seg_theta<B>, dim3(div_up(nseg * N, 256)), dim3(256), 0, st, t,       \
                          rr_lo, s_seground.p, nseg, s_segfws.p, s_theta.p);                      \
     break;
       SCASE(1)
@@ -847,7 +899,7 @@ struct hge_engine {
     switch (NW) {
 #define RCASE(B)                                                                                 \
   case B:                                                                                        \
-    hipLaunchKernelGGL(k_round_received<B>, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, \
+    KLAUNCH(k_round_received<B>, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, \
                        ncand, s_nc.p, ncalls, 0, rr_lo, R_last, s_segoff.p, s_segcnt.p,          \
                        s_segcall.p, s_segdec.p, s_segfws.p, s_theta.p, s_recv.p, s_rr.p,         \
                        s_cts.p);                                                                 \
@@ -1260,6 +1312,30 @@ int32_t hge_oldest_self_ancestor_to_see(hge_engine* h, int32_t x, int32_t y) {
     }
   }
   return -1;
+}
+
+int hge_set_profiling(hge_engine* h, int on) {
+  h->prof_on = on != 0;
+  return HGE_OK;
+}
+
+int hge_reset_kernel_stats(hge_engine* h) {
+  h->prof_names.clear();
+  h->prof_ms.clear();
+  h->prof_cnt.clear();
+  return HGE_OK;
+}
+
+int hge_kernel_stats(hge_engine* h, int k, char* name, int namecap, double* total_ms,
+                     int64_t* launches) {
+  const int n = (int)h->prof_names.size();
+  if (k < 0 || k >= n) return n;
+  if (name && namecap > 0) {
+    snprintf(name, namecap, "%s", h->prof_names[k].c_str());
+  }
+  if (total_ms) *total_ms = h->prof_ms[k];
+  if (launches) *launches = h->prof_cnt[k];
+  return n;
 }
 
 int hge_stage_times(hge_engine* h, float* ms_out, int cap) {

@@ -60,6 +60,7 @@ EXPORTS = [
     "hge_fame", "hge_round_events", "hge_round_received", "hge_consensus_timestamp",
     "hge_ancestor", "hge_self_ancestor", "hge_see", "hge_strongly_see",
     "hge_oldest_self_ancestor_to_see", "hge_coordinates", "hge_stage_times",
+    "hge_set_profiling", "hge_reset_kernel_stats", "hge_kernel_stats",
 ]
 
 _lib = None
@@ -118,6 +119,10 @@ def lib():
         getattr(L, f).restype = i32
     L.hge_coordinates.argtypes = [vp, i32, P(i32), P(i32)]
     L.hge_stage_times.argtypes = [vp, P(ctypes.c_float), ctypes.c_int]
+    L.hge_set_profiling.argtypes = [vp, ctypes.c_int]
+    L.hge_reset_kernel_stats.argtypes = [vp]
+    L.hge_kernel_stats.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                   P(ctypes.c_double), P(i64)]
     _lib = L
     return L
 
@@ -244,6 +249,22 @@ class Engine:
         counts = np.zeros(max(1, self._ncalls), np.int64)
         self._check(self.L.hge_replay_fetch(self.h, _p32(order), len(order), _p64(counts)))
         return self._status, order[:self._nordered], counts[:self._ncalls]
+
+    def set_profiling(self, on=True):
+        self.L.hge_set_profiling(self.h, 1 if on else 0)
+        self.L.hge_reset_kernel_stats(self.h)
+
+    def kernel_stats(self):
+        """{kernel name: (total device ms, launches)} from HIP events on the engine stream."""
+        out = {}
+        n = self.L.hge_kernel_stats(self.h, -1, None, 0, None, None)
+        buf = ctypes.create_string_buffer(128)
+        for k in range(n):
+            ms = ctypes.c_double()
+            cnt = ctypes.c_int64()
+            self.L.hge_kernel_stats(self.h, k, buf, 128, ctypes.byref(ms), ctypes.byref(cnt))
+            out[buf.value.decode()] = (ms.value, cnt.value)
+        return out
 
     def stage_times(self):
         out = (ctypes.c_float * 7)()

@@ -134,6 +134,13 @@ int hge_coordinates(hge_engine* h, int32_t id, int32_t* la_out, int32_t* fd_out)
  * engine's stream): 0 coords, 1 rounds, 2 witness bits, 3 fame, 4 received,
  * 5 order, 6 total.  Returns the number of stages written. */
 int hge_stage_times(hge_engine* h, float* ms_out, int cap);
+/* Per-kernel timing: HIP events around every launch on the engine stream. */
+int hge_set_profiling(hge_engine* h, int on);
+int hge_reset_kernel_stats(hge_engine* h);
+/* Kernel k's name, accumulated device ms and launch count; returns the number
+ * of distinct kernels recorded. */
+int hge_kernel_stats(hge_engine* h, int k, char* name, int namecap, double* total_ms,
+                     int64_t* launches);
 
 #ifdef __cplusplus
 }
