@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -99,6 +100,7 @@ struct hge_engine {
   int64_t n_coords = 0;     // coordinates + rounds computed
   int64_t n_divided = 0;    // visible to DecideFame / FindOrder (DivideRounds)
   std::vector<int32_t> coords_len;  // chain lengths at n_coords
+  std::vector<int32_t> h_lens;      // staging for the chain-length upload
 
   int R = 0;                // Store.Rounds()
   int lcr = -1;             // LastConsensusRound (-1 nil)
@@ -119,7 +121,7 @@ struct hge_engine {
   DBuf<int64_t> d_ts, d_cts;
   DBuf<uint64_t> d_S;
   DBuf<uint8_t> d_coin, d_wit;
-  DBuf<int32_t> d_chain, d_LA, d_FD;
+  DBuf<int32_t> d_chain, d_LA, d_FD, d_FSS;
   DBuf<int32_t> d_C, d_W, d_rcnt, d_minw;
   DBuf<uint64_t> d_ssb, d_seeb;
   DBuf<uint8_t> d_fame;
@@ -136,6 +138,7 @@ struct hge_engine {
   DBuf<int64_t> s_cts;
   DBuf<unsigned char> s_keys, s_keys2;
   DBuf<unsigned long long> s_ntx;
+  DBuf<int32_t> s_part, s_arr, s_fst, s_fsslo;
 
   hipEvent_t ev[8] = {};
   // per-kernel HIP-event timing on the engine stream (hge_set_profiling)
@@ -235,6 +238,26 @@ struct hge_engine {
     prof_rec.clear();
   }
 
+  // diagnostic stamps (HGE_STAMPS=1): per-section cycle counters of some kernels
+  DBuf<uint64_t> s_dbg;
+  bool dbg_on = getenv("HGE_STAMPS") != nullptr;
+  uint64_t* dbg_p() {
+    if (!dbg_on) return nullptr;
+    if (!s_dbg.p) {
+      s_dbg.need(16);
+      HIPCHK(hipMemset(s_dbg.p, 0, 16 * 8));
+    }
+    return s_dbg.p;
+  }
+  void dbg_dump() {
+    if (!dbg_on || !s_dbg.p) return;
+    uint64_t v[16];
+    readback(v, s_dbg.p, 16);
+    fprintf(stderr, "[hge stamps]");
+    for (int i = 0; i < 16; i++) fprintf(stderr, " %llu", (unsigned long long)v[i]);
+    fprintf(stderr, "\n");
+  }
+
   void set_lds_limits() {
     // best effort: gfx950 has 160 KiB of LDS per CU; kernels with static LDS
     // get a smaller dynamic ceiling
@@ -250,12 +273,21 @@ struct hge_engine {
     LDSATTR(k_coord_local<4>);
     LDSATTR(k_coord_local<8>);
     LDSATTR(k_coord_local<16>);
+    LDSATTR(k_coord_basis<1>);
+    LDSATTR(k_coord_basis<2>);
+    LDSATTR(k_coord_basis<4>);
+    LDSATTR(k_coord_basis<8>);
+    LDSATTR(k_coord_basis<16>);
     LDSATTR(k_coord_final<1>);
     LDSATTR(k_coord_final<2>);
     LDSATTR(k_coord_final<4>);
     LDSATTR(k_coord_final<8>);
     LDSATTR(k_coord_final<16>);
-    LDSATTR(k_rounds_frontier);
+    LDSATTR(k_rounds_ring<16>);
+    LDSATTR(k_rounds_frontier<16>);
+    LDSATTR(k_rounds_frontier<32>);
+    LDSATTR(k_rounds_frontier<64>);
+    LDSATTR(k_rounds_frontier<0>);
 #undef LDSATTR
   }
 
@@ -270,7 +302,7 @@ struct hge_engine {
                              &s_basis, &s_bcount, &s_boff, &s_BR, &s_small, &s_len, &s_newwit,
                              &s_Rc, &s_Lc, &s_LCR, &s_pr, &s_clast, &s_flags, &s_segcnt,
                              &s_segoff, &s_segcall, &s_seground, &s_theta, &s_prindex, &s_recv,
-                             &s_rr, &s_frecv, &s_fund, &s_rank, &s_upos, &s_und2, &s_ids,
+                             &s_rr, &s_frecv, &s_fund, &s_rank, &s_upos, &s_und2, &s_ids, &s_part, &s_arr, &s_fst, &s_fsslo, &d_FSS,
                              &s_ccount};
     for (auto* b : i32s) b->free_();
     d_ts.free_();
@@ -317,7 +349,8 @@ struct hge_engine {
   void ensure_ccap(int64_t m) {
     if (m <= ccap) return;
     int64_t nc = std::max<int64_t>(m, (int64_t)ccap + ccap / 2);
-    int32_t *chain = nullptr, *la = nullptr, *fd = nullptr;
+    int32_t *chain = nullptr, *la = nullptr, *fd = nullptr, *fss = nullptr;
+    HIPCHK(hipMalloc(&fss, sizeof(int32_t) * (size_t)N * nc * N));
     HIPCHK(hipMalloc(&chain, sizeof(int32_t) * N * nc));
     HIPCHK(hipMalloc(&la, sizeof(int32_t) * (size_t)N * nc * N));
     HIPCHK(hipMalloc(&fd, sizeof(int32_t) * (size_t)N * nc * N));
@@ -329,11 +362,16 @@ struct hge_engine {
                               sizeof(int32_t) * ccap * N, N, hipMemcpyDeviceToDevice, st));
       HIPCHK(hipMemcpy2DAsync(fd, sizeof(int32_t) * nc * N, d_FD.p, sizeof(int32_t) * ccap * N,
                               sizeof(int32_t) * ccap * N, N, hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipMemcpy2DAsync(fss, sizeof(int32_t) * nc * N, d_FSS.p, sizeof(int32_t) * ccap * N,
+                              sizeof(int32_t) * ccap * N, N, hipMemcpyDeviceToDevice, st));
     }
     HIPCHK(hipStreamSynchronize(st));
     d_chain.free_();
     d_LA.free_();
     d_FD.free_();
+    d_FSS.free_();
+    d_FSS.p = fss;
+    d_FSS.n = (size_t)N * nc * N;
     d_chain.p = chain;
     d_chain.n = (size_t)N * nc;
     d_LA.p = la;
@@ -481,23 +519,33 @@ struct hge_engine {
     if (n1 == n0) return;
     Tables t = tables();
     const int m = (int)(n1 - n0);
+    std::vector<int32_t>& lens = h_lens;
+    lens.resize(2 * N);
+    for (int c = 0; c < N; c++) {
+      lens[c] = coords_len[c];
+      lens[N + c] = chain_len[c];
+    }
+    s_len.need(2 * N);
+    HIPCHK(hipMemcpyAsync(s_len.p, lens.data(), 8 * N, hipMemcpyHostToDevice, st));
     KLAUNCH(k_chain_fill, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0, (int)n1);
     // chunk length: LDS of phase A = L*(BW*8 + N*4 + 32) + BMAX*4 + ~1KB
     const int BMAX = BW * 64;
     int L = 1024;
-    while (L > 64 && (size_t)L * (BW * 8 + N * 4 + 32) + BMAX * 4 + 2048 > 150 * 1024) L /= 2;
+    if (getenv("HGE_CHUNK")) L = atoi(getenv("HGE_CHUNK"));
+    while (L > 64 && (size_t)(L + 1) * (BW * 8 + N * 4 + 32) + BMAX * 4 + 2048 + N * 4 > 150 * 1024) L /= 2;
     for (;;) {
       const int nch = div_up(m, L);
       s_D.need((size_t)m * N);
       s_dep.need((size_t)m * BW);
       s_enc.need((size_t)2 * m);
-      s_basis.need((size_t)nch * BMAX);
+      const int RECW = 2 * BMAX + N + N * N + 2 * N * BW + 1;
+      s_basis.need((size_t)nch * RECW);
       s_bcount.need(nch);
       s_boff.need(nch);
       s_small.need(8);
       HIPCHK(hipMemsetAsync(s_small.p, 0, 8 * 4, st));
-      const size_t ldsA = (size_t)L * BW * 8 + (size_t)L * N * 4 + (size_t)L * 4 * 4 +
-                          (size_t)2 * L * 4 * 2 + (size_t)BMAX * 4 + (256 + 1) * 4;
+      const size_t ldsA = (size_t)(L + 1) * (N + 2 * BW) * 4 + (size_t)L * 4 * 4 +
+                          (size_t)2 * L * 4 * 2 + (size_t)BMAX * 4 + (256 + 1) * 4 + N * 4;
       launch_bw(0, nch, ldsA, t, (int)n0, (int)n1, L, nch);
       int32_t flag[2];
       readback(flag, s_small.p, 2);
@@ -511,28 +559,60 @@ struct hge_engine {
       int32_t total = 0;
       readback(&total, s_small.p + 2, 1);
       s_BR.need((size_t)std::max(total, 1) * N);
-      launch_bw(1, nch, 0, t, (int)n0, (int)n1, L, nch);
+      const size_t ldsB = ((size_t)N * N + (size_t)BMAX * N + 2 * (size_t)RECW) * 4;
+      launch_bw(1, nch, ldsB, t, (int)n0, (int)n1, L, nch);
       br_in_lds = (size_t)BMAX * N * 4 + (size_t)L * N * 4 <= 150 * 1024;
       const size_t ldsC = (size_t)L * N * 4 + (br_in_lds ? (size_t)BMAX * N * 4 : 0);
       launch_bw(2, nch, ldsC, t, (int)n0, (int)n1, L, nch);
       break;
     }
     // rounds frontier
-    std::vector<int32_t> lens(2 * N);
-    for (int c = 0; c < N; c++) {
-      lens[c] = coords_len[c];
-      lens[N + c] = chain_len[c];
-    }
-    s_len.need(2 * N);
-    HIPCHK(hipMemcpyAsync(s_len.p, lens.data(), 8 * N, hipMemcpyHostToDevice, st));
     for (;;) {
       int32_t rs[2] = {R, 0};
       HIPCHK(hipMemcpyAsync(s_small.p, rs, 8, hipMemcpyHostToDevice, st));
-      int WIN = std::max(4, std::min(64, 16384 / (N * N)));
-      const size_t lds = (size_t)(N * N + 8 * N + N * WIN) * 4;
       t = tables();
-      KLAUNCH(k_rounds_frontier, dim3(1), dim3(1024), lds, st, t, s_len.p,
-                         s_len.p + N, s_small.p, WIN);
+      const int NP = (N + 15) & ~15;
+      if (NP <= 64 && !getenv("HGE_PROBE_FRONTIER")) {
+        // first-strong-seer rows for every event that can still be a frontier member
+        s_fst.need(N + 1);
+        KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, s_len.p, s_len.p + N, s_fst.p);
+        std::vector<int32_t> fst(N + 1);
+        readback(fst.data(), s_fst.p, N + 1);
+        const int rlo = fst[0];
+        if (rlo != INF32) {
+          std::vector<int32_t> lo_off(2 * N + 1);
+          int tot = 0;
+          for (int c = 0; c < N; c++) {
+            lo_off[c] = fst[1 + c];
+            lo_off[N + c] = tot;
+            tot += std::max(0, chain_len[c] - fst[1 + c]);
+          }
+          lo_off[2 * N] = tot;
+          s_fsslo.need(2 * N + 1);
+          HIPCHK(hipMemcpyAsync(s_fsslo.p, lo_off.data(), 4 * (2 * N + 1), hipMemcpyHostToDevice, st));
+          if (tot > 0) {
+#define FSSL(NPC)                                                                                 \
+  KLAUNCH(k_fss<NPC>, dim3(div_up((int64_t)tot * NPC, 256)), dim3(256), 0, st, t, s_fsslo.p,      \
+          s_fsslo.p + N, tot, d_FSS.p);                                                           \
+  KLAUNCH(k_rounds_fss<NPC>, dim3(1), dim3(64), 0, st, t, d_FSS.p, s_len.p, s_len.p + N, s_small.p, rlo);
+            if (NP == 16) { FSSL(16) } else if (NP == 32) { FSSL(32) } else { FSSL(64) }
+#undef FSSL
+          }
+        }
+      } else {
+        // probe window per chain: a few rounds' worth of a chain's events, bounded by LDS
+        int WIN = 16;
+        while (WIN > 2 && (size_t)N * WIN * NP * 4 > 96 * 1024) WIN /= 2;
+        const size_t lds = (size_t)(N * NP + N * WIN * NP + 8 * N + 2 * N * WIN) * 4 + 64;
+        if (NP == 16)
+          KLAUNCH(k_rounds_frontier<16>, dim3(1), dim3(1024), lds, st, t, s_len.p, s_len.p + N, s_small.p, WIN, dbg_p());
+        else if (NP == 32)
+          KLAUNCH(k_rounds_frontier<32>, dim3(1), dim3(1024), lds, st, t, s_len.p, s_len.p + N, s_small.p, WIN, dbg_p());
+        else if (NP == 64)
+          KLAUNCH(k_rounds_frontier<64>, dim3(1), dim3(1024), lds, st, t, s_len.p, s_len.p + N, s_small.p, WIN, dbg_p());
+        else
+          KLAUNCH(k_rounds_frontier<0>, dim3(1), dim3(1024), lds, st, t, s_len.p, s_len.p + N, s_small.p, WIN, dbg_p());
+      }
       readback(rs, s_small.p, 2);
       if (rs[1]) {
         ensure_rcap((int64_t)Rcap * 2);
@@ -567,8 +647,8 @@ struct hge_engine {
       KLAUNCH(k_coord_local<B>, dim3(nch), dim3(256), lds, st, t, n0, n1, L, s_D.p,  \
                          s_dep.p, s_enc.p, s_basis.p, s_bcount.p, s_small.p);                    \
     } else if (which == 1) {                                                                     \
-      KLAUNCH(k_coord_basis<B>, dim3(1), dim3(1024), 0, st, t, n0, L, nch2, s_D.p,    \
-                         s_dep.p, s_basis.p, s_bcount.p, s_boff.p, s_BR.p);                      \
+      KLAUNCH(k_coord_basis<B>, dim3(1), dim3(1024), lds, st, t, n0, L, nch2, s_D.p,  \
+                         s_dep.p, s_basis.p, s_boff.p, s_len.p, s_BR.p);                         \
     } else {                                                                                     \
       KLAUNCH(k_coord_final<B>, dim3(nch), dim3(256), lds, st, t, n0, n1, L, s_D.p,  \
                          s_dep.p, s_enc.p, s_bcount.p, s_boff.p, s_BR.p, br_in_lds ? 1 : 0);     \
@@ -718,6 +798,9 @@ struct hge_engine {
         }
         s_segcnt.need(nr);
         s_segoff.need(nr + 1);
+        s_arr.need((size_t)nr * N);
+        KLAUNCH(k_arrivals, dim3(div_up(nr * N, 256)), dim3(256), 0, st, t, rr_lo, nr, s_nc.p,
+                ncalls, s_arr.p);
         seg_dispatch(0, t, rr_lo, nr, ncalls, si, 0);
         KLAUNCH(k_scan_small, dim3(1), dim3(1024), 0, st, s_segcnt.p, s_segoff.p, nr,
                            s_small.p + 6);
@@ -840,8 +923,11 @@ struct hge_engine {
   }
 
   void scan_large(const int32_t* in, int32_t* out, int n, int32_t* total) {
-    // one block of 1024 threads; adequate for the candidate counts involved
-    KLAUNCH(k_scan_small, dim3(1), dim3(1024), 0, st, in, out, n, total);
+    const int nb = div_up(n, 1024);
+    s_part.need(2 * (size_t)nb + 2);
+    KLAUNCH(k_scan_blocks, dim3(nb), dim3(256), 0, st, in, out, n, s_part.p);
+    KLAUNCH(k_scan_small, dim3(1), dim3(1024), 0, st, s_part.p, s_part.p + nb, nb, total);
+    KLAUNCH(k_scan_add, dim3(div_up(n, 256)), dim3(256), 0, st, out, n, s_part.p + nb);
   }
 
   void fame_dispatch(int which, const Tables& t, int nrounds, int npairs, int items, int ncalls) {
@@ -878,7 +964,7 @@ struct hge_engine {
 #define SCASE(B)                                                                                 \
   case B:                                                                                        \
     KLAUNCH(k_segments<B>, dim3(div_up(nr, 64)), dim3(64), 0, st, t, rr_lo, nr,       \
-                       s_nc.p, ncalls, si, s_segcnt.p, s_segoff.p, s_segcall.p, s_seground.p,    \
+                       s_nc.p, ncalls, si, s_arr.p, s_segcnt.p, s_segoff.p, s_segcall.p, s_seground.p,    \
                        s_segdec.p, s_segfws.p, mode);                                            \
     if (mode == 1 && nseg > 0)                                                                   \
       KLAUNCH(k_seg_theta<B>, dim3(div_up(nseg * N, 256)), dim3(256), 0, st, t,       \
@@ -1130,6 +1216,7 @@ int hge_replay_run(hge_engine* h, int64_t* n_ordered) {
   h->stage_ms[3] = b;
   h->stage_ms[6] = a + b;
   if (n_ordered) *n_ordered = (int64_t)h->replay_order.size();
+  h->dbg_dump();
   return HGE_OK;
   GUARD_END(h)
 }

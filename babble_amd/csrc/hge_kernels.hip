@@ -69,24 +69,21 @@ __device__ int block_exclusive_scan(int* a, int n, int* tmp /* blockDim.x + 1 */
   for (int i = lo; i < hi; i++) s += a[i];
   tmp[tid] = s;
   __syncthreads();
-  if (tid == 0) {
-    int run = 0;
-    for (int i = 0; i < T; i++) {
-      int v = tmp[i];
-      tmp[i] = run;
-      run += v;
-    }
-    tmp[T] = run;
+  for (int off = 1; off < T; off <<= 1) {
+    const int add = (tid >= off) ? tmp[tid - off] : 0;
+    __syncthreads();
+    tmp[tid] += add;
+    __syncthreads();
   }
-  __syncthreads();
-  int run = tmp[tid];
+  const int total = tmp[T - 1];
+  int run = tmp[tid] - s;
   for (int i = lo; i < hi; i++) {
     int v = a[i];
     a[i] = run;
     run += v;
   }
   __syncthreads();
-  return tmp[T];
+  return total;
 }
 
 // ---------------------------------------------------------------------------
@@ -114,9 +111,8 @@ __global__ void __launch_bounds__(256) k_coord_local(Tables t, int n0, int n1, i
   const int tid = threadIdx.x;
   const int T = blockDim.x;
 
-  uint64_t* sdep = (uint64_t*)smem;                 // L * BW
-  int32_t* sD = (int32_t*)(sdep + (size_t)L * BW);  // L * N
-  int32_t* ssp = sD + (size_t)L * N;                // L
+  int32_t* sRow = (int32_t*)smem;                   // (L + 1) * (N + 2*BW)
+  int32_t* ssp = sRow + (size_t)(L + 1) * (N + 2 * BW);  // L
   int32_t* sop = ssp + L;                           // L
   int32_t* scr = sop + L;                           // L
   int32_t* sidx = scr + L;                          // L
@@ -124,6 +120,7 @@ __global__ void __launch_bounds__(256) k_coord_local(Tables t, int n0, int n1, i
   int32_t* sflag = sext + 2 * L;                    // 2L
   int32_t* sbas = sflag + 2 * L;                    // BMAX
   int32_t* stmp = sbas + BMAX;                      // T + 1
+  int32_t* sExit = stmp + T + 1;                    // N
 
   const int M = 2 * L;
   for (int i = tid; i < L; i += T) {
@@ -179,8 +176,15 @@ __global__ void __launch_bounds__(256) k_coord_local(Tables t, int n0, int n1, i
     if (v != INF32 && nxt != r) sbas[r] = v;  // first occurrence
   }
   __syncthreads();
-  for (int i = tid; i < nb; i += T) basis[(size_t)k * BMAX + i] = sbas[i];
-  if (tid == 0) bcount[k] = nb;
+  // record layout (RECW ints): [basis ids BMAX | head kinds BMAX | exits N |
+  //  exit D rows N*N | exit dep words N*2BW | nb]
+  const int RECW = 2 * BMAX + N + N * N + 2 * N * BW + 1;
+  int32_t* rec = basis + (size_t)k * RECW;
+  for (int i = tid; i < nb; i += T) rec[i] = sbas[i];
+  if (tid == 0) {
+    bcount[k] = nb;
+    rec[RECW - 1] = nb;
+  }
   // encode parents: >= 0 local offset, -1 none, -(2 + b) basis slot b
   for (int i = tid; i < cnt; i += T) {
     int pr[2] = {ssp[i], sop[i]};
@@ -206,38 +210,91 @@ __global__ void __launch_bounds__(256) k_coord_local(Tables t, int n0, int n1, i
     enc[2 * (size_t)(s - n0 + i) + 1] = pr[1];
   }
   __syncthreads();
-  // sequential in-chunk propagation: one wave, lanes over columns / dep words
+  // sequential in-chunk propagation: one wave.  Row i of sRow = [D (N int32) |
+  // dep (2*BW uint32)]; row L is the all-"none" row used for absent parents,
+  // so every step is one pair of independent LDS loads and one store.  Parent
+  // codes of 64 steps sit in registers (one step per lane) and are broadcast
+  // with v_readlane.
   if (tid < 64) {
     const int lane = tid;
-    for (int i = 0; i < cnt; i++) {
-      const int psp = ssp[i], pop = sop[i], cx = scr[i], ix = sidx[i];
-      for (int c = lane; c < N; c += 64) {
-        int v = -1;
-        if (psp >= 0) v = sD[psp * N + c];
-        if (pop >= 0) v = max(v, sD[pop * N + c]);
-        if (c == cx) v = ix;
-        sD[i * N + c] = v;
+    const int RW = N + 2 * BW;
+    for (int col = lane; col < RW; col += 64) sRow[L * RW + col] = (col < N) ? -1 : 0;
+    for (int b0 = 0; b0 < cnt; b0 += 64) {
+      int msp = -1, mop = -1, mcx = 0, mix = 0;
+      if (b0 + lane < cnt) {
+        msp = ssp[b0 + lane];
+        mop = sop[b0 + lane];
+        mcx = scr[b0 + lane];
+        mix = sidx[b0 + lane];
       }
-      for (int w = lane; w < BW; w += 64) {
-        uint64_t d = 0;
-        if (psp >= 0) d |= sdep[psp * BW + w];
-        else if (psp <= -2 && ((-psp - 2) >> 6) == w) d |= 1ull << ((-psp - 2) & 63);
-        if (pop >= 0) d |= sdep[pop * BW + w];
-        else if (pop <= -2 && ((-pop - 2) >> 6) == w) d |= 1ull << ((-pop - 2) & 63);
-        sdep[i * BW + w] = d;
+      const int nb = min(64, cnt - b0);
+      for (int j = 0; j < nb; j++) {
+        const int psp = __builtin_amdgcn_readlane(msp, j);
+        const int pop = __builtin_amdgcn_readlane(mop, j);
+        const int cx = __builtin_amdgcn_readlane(mcx, j);
+        const int ix = __builtin_amdgcn_readlane(mix, j);
+        const int ra = (psp >= 0 ? psp : L) * RW;
+        const int rb = (pop >= 0 ? pop : L) * RW;
+        const int bsp = psp <= -2 ? -psp - 2 : -1;  // external basis slots
+        const int bop = pop <= -2 ? -pop - 2 : -1;
+        int* dst = sRow + (b0 + j) * RW;
+        for (int col = lane; col < RW; col += 64) {
+          const int va = sRow[ra + col], vb = sRow[rb + col];
+          int v;
+          if (col < N) {
+            v = (col == cx) ? ix : max(va, vb);
+          } else {
+            const int w = col - N;  // 32-bit dep word
+            v = va | vb;
+            if (bsp >= 0 && (bsp >> 5) == w) v |= 1 << (bsp & 31);
+            if (bop >= 0 && (bop >> 5) == w) v |= 1 << (bop & 31);
+          }
+          dst[col] = v;
+        }
       }
     }
   }
   __syncthreads();
   const size_t base = (size_t)(s - n0);
-  for (int i = tid; i < cnt * N; i += T) Dbuf[base * N + i] = sD[i];
-  for (int i = tid; i < cnt * BW; i += T) depbuf[base * BW + i] = sdep[i];
+  const int RW = N + 2 * BW;
+  for (int item = tid; item < cnt * N; item += T) {
+    const int i = item / N, c = item - (item / N) * N;
+    Dbuf[base * N + item] = sRow[i * RW + c];
+  }
+  uint32_t* dep32 = (uint32_t*)depbuf;
+  for (int item = tid; item < cnt * 2 * BW; item += T) {
+    const int i = item / (2 * BW), w = item - (item / (2 * BW)) * (2 * BW);
+    dep32[base * 2 * BW + item] = (uint32_t)sRow[i * RW + N + w];
+  }
+  // per-chain exits (last event of each chain in the chunk) and head flags of
+  // the basis: consumed by phase B's head-table fast path
+  for (int c = tid; c < N; c += T) sExit[c] = -1;
+  __syncthreads();
+  for (int i = tid; i < cnt; i += T) atomicMax(&sExit[scr[i]], i);
+  __syncthreads();
+  for (int c = tid; c < N; c += T) rec[2 * BMAX + c] = sExit[c] >= 0 ? s + sExit[c] : -1;
+  for (int item = tid; item < N * N; item += T) {
+    const int c = item / N, i = item - (item / N) * N;
+    rec[2 * BMAX + N + item] = sExit[c] >= 0 ? sRow[sExit[c] * RW + i] : -1;
+  }
+  for (int item = tid; item < N * 2 * BW; item += T) {
+    const int c = item / (2 * BW), w = item - (item / (2 * BW)) * (2 * BW);
+    rec[2 * BMAX + N + N * N + item] = sExit[c] >= 0 ? sRow[sExit[c] * RW + N + w] : 0;
+  }
+  for (int b = tid; b < nb; b += T) {
+    const int e = sbas[b];
+    const int ce = t.creator[e], pe = t.index[e];
+    const int nxt = (pe + 1 < t.ccap) ? t.chain[(size_t)ce * t.ccap + pe + 1] : -1;
+    // kind 1 + creator: e is its chain's head at chunk start (row in phase B's
+    // head table); 0: older event (row recomputed from HBM)
+    rec[BMAX + b] = (nxt < 0 || nxt >= s) ? 1 + ce : 0;
+  }
 }
 
 // exclusive scan of a small int array by one block (n <= ~64k)
 __global__ void __launch_bounds__(1024) k_scan_small(const int32_t* in, int32_t* out, int n,
                                                      int32_t* total) {
-  __shared__ int tmp[1025];
+  __shared__ int tmp[1024];
   const int T = blockDim.x, tid = threadIdx.x;
   const int per = (n + T - 1) / T;
   const int lo = min(n, tid * per), hi = min(n, lo + per);
@@ -245,67 +302,157 @@ __global__ void __launch_bounds__(1024) k_scan_small(const int32_t* in, int32_t*
   for (int i = lo; i < hi; i++) s += in[i];
   tmp[tid] = s;
   __syncthreads();
-  if (tid == 0) {
-    int run = 0;
-    for (int i = 0; i < T; i++) {
-      int v = tmp[i];
-      tmp[i] = run;
-      run += v;
-    }
-    tmp[T] = run;
+  for (int off = 1; off < T; off <<= 1) {
+    const int add = (tid >= off) ? tmp[tid - off] : 0;
+    __syncthreads();
+    tmp[tid] += add;
+    __syncthreads();
   }
-  __syncthreads();
-  int run = tmp[tid];
+  int run = tmp[tid] - s;
   for (int i = lo; i < hi; i++) {
     int v = in[i];
     out[i] = run;
     run += v;
   }
-  if (tid == 0 && total) *total = tmp[T];
+  if (tid == T - 1 && total) *total = tmp[T - 1];
+}
+
+// multi-block exclusive scan: 1024 elements per 256-thread block
+__global__ void __launch_bounds__(256) k_scan_blocks(const int32_t* in, int32_t* out, int n,
+                                                     int32_t* partial) {
+  __shared__ int ws[256];
+  const int tid = threadIdx.x;
+  const int base = blockIdx.x * 1024 + tid * 4;
+  int v[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) v[j] = (base + j < n) ? in[base + j] : 0;
+  const int s = v[0] + v[1] + v[2] + v[3];
+  ws[tid] = s;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    const int add = (tid >= off) ? ws[tid - off] : 0;
+    __syncthreads();
+    ws[tid] += add;
+    __syncthreads();
+  }
+  int run = ws[tid] - s;  // exclusive
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    if (base + j < n) out[base + j] = run;
+    run += v[j];
+  }
+  if (tid == 255) partial[blockIdx.x] = ws[255];
+}
+
+__global__ void k_scan_add(int32_t* out, int n, const int32_t* partial_scanned) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] += partial_scanned[i / 1024];
 }
 
 // ---------------------------------------------------------------------------
 // Coordinates, phase B: one persistent workgroup walks the chunks in order and
 // materialises the lastAncestors rows of every basis element (the only rows a
-// later chunk needs from an earlier one).  Basis element e of chunk k lies
-// before chunk k: either before this batch (final LA row in HBM) or in an
-// earlier chunk j of this batch: row = max(D_j[e], max_{b in dep_j[e]} BR_j[b]).
+// later chunk needs from an earlier one).  It keeps the LA rows of all chain
+// heads in LDS: a basis element that is its chain's head at chunk start (the
+// common case: self-parents always are, gossip other-parents usually are) is an
+// LDS read; after chunk k the heads advance to the chunk's exits,
+//   LA(exit) = max(D_k[exit], max_{b in dep_k[exit]} BR_k[b]).
+// Older basis elements are recomputed from HBM.  The next chunk's packed
+// record is prefetched into registers while the current one is processed.
 // ---------------------------------------------------------------------------
 template <int BW>
 __global__ void __launch_bounds__(1024) k_coord_basis(Tables t, int n0, int L, int nchunks,
                                                        const int32_t* Dbuf,
                                                        const uint64_t* depbuf,
-                                                       const int32_t* basis,
-                                                       const int32_t* bcount,
-                                                       const int32_t* boff, int32_t* BR) {
+                                                       const int32_t* rec,
+                                                       const int32_t* boff, const int32_t* olen,
+                                                       int32_t* BR) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int BMAX = BW * 64;
+  constexpr int PF = 8;
   const int N = t.N;
+  const int tid = threadIdx.x, T = blockDim.x;
+  const int RECW = 2 * BMAX + N + N * N + 2 * N * BW + 1;
+  int32_t* sH = (int32_t*)smem;     // N*N head rows
+  int32_t* sBR = sH + N * N;        // BMAX*N basis rows of the current chunk
+  int32_t* sIn0 = sBR + BMAX * N;   // RECW
+  int32_t* sIn1 = sIn0 + RECW;      // RECW
+  for (int item = tid; item < N * N; item += T) {
+    const int c = item / N, i = item - (item / N) * N;
+    const int ol = olen[c];
+    sH[item] = ol > 0 ? t.LA[rowoff(t, c, ol - 1) + i] : -1;
+  }
+  for (int j = tid; j < RECW; j += T) sIn0[j] = rec[j];
+  __syncthreads();
+  int off = 0;
   for (int k = 0; k < nchunks; k++) {
-    const int nb = bcount[k];
-    const int off = boff[k];
-    for (int item = threadIdx.x; item < nb * N; item += blockDim.x) {
-      const int b = item / N, c = item - (item / N) * N;
-      const int e = basis[(size_t)k * BMAX + b];
-      int v;
-      if (e < n0) {
-        v = t.LA[rowoff(t, t.creator[e], t.index[e]) + c];
-      } else {
-        const int le = e - n0;
-        const int j = le / L;
-        const int bj = boff[j];
-        v = Dbuf[(size_t)le * N + c];
+    int32_t* cur = (k & 1) ? sIn1 : sIn0;
+    int32_t* nxt = (k & 1) ? sIn0 : sIn1;
+    int pf[PF];
+    const bool more = k + 1 < nchunks;
 #pragma unroll
-        for (int w = 0; w < BW; w++) {
-          uint64_t m = depbuf[(size_t)le * BW + w];
-          while (m) {
-            const int tb = w * 64 + __builtin_ctzll(m);
-            m &= m - 1;
-            v = max(v, ntload(&BR[(size_t)(bj + tb) * N + c]));
+    for (int m = 0; m < PF; m++) {
+      const int j = tid + m * T;
+      pf[m] = (more && j < RECW) ? rec[(size_t)(k + 1) * RECW + j] : 0;
+    }
+    const int nb = cur[RECW - 1];
+    const int32_t* ids = cur;
+    const int32_t* kinds = cur + BMAX;
+    const int32_t* ex = cur + 2 * BMAX;
+    const int32_t* exD = ex + N;
+    const uint32_t* exdep = (const uint32_t*)(exD + N * N);
+    for (int item = tid; item < nb * N; item += T) {
+      const int b = item / N, c = item - (item / N) * N;
+      const int kind = kinds[b];
+      int v;
+      if (kind > 0) {
+        v = sH[(kind - 1) * N + c];
+      } else {
+        const int e = ids[b];
+        if (e < n0) {
+          v = t.LA[rowoff(t, t.creator[e], t.index[e]) + c];
+        } else {
+          const int le = e - n0;
+          const int j = le / L;
+          const int bj = boff[j];
+          v = Dbuf[(size_t)le * N + c];
+#pragma unroll
+          for (int w = 0; w < BW; w++) {
+            uint64_t msk = depbuf[(size_t)le * BW + w];
+            while (msk) {
+              const int tb = w * 64 + __builtin_ctzll(msk);
+              msk &= msk - 1;
+              v = max(v, ntload(&BR[(size_t)(bj + tb) * N + c]));
+            }
           }
         }
       }
+      sBR[item] = v;
       BR[(size_t)(off + b) * N + c] = v;
     }
+    __syncthreads();
+    for (int item = tid; item < N * N; item += T) {
+      const int c = item / N, i = item - (item / N) * N;
+      if (ex[c] < 0) continue;
+      int v = exD[item];
+      for (int w = 0; w < 2 * BW; w++) {
+        uint32_t msk = exdep[c * 2 * BW + w];
+        while (msk) {
+          const int tb = w * 32 + __builtin_ctz(msk);
+          msk &= msk - 1;
+          v = max(v, sBR[tb * N + i]);
+        }
+      }
+      sH[item] = v;
+    }
+#pragma unroll
+    for (int m = 0; m < PF; m++) {
+      const int j = tid + m * T;
+      if (more && j < RECW) nxt[j] = pf[m];
+    }
+    if (more)
+      for (int j = tid + PF * T; j < RECW; j += T) nxt[j] = rec[(size_t)(k + 1) * RECW + j];
+    off += nb;
     drain_stores();
     __syncthreads();
   }
@@ -391,22 +538,65 @@ __global__ void k_chain_fill(Tables t, int n0, int n1) {
 // One persistent workgroup walks the rounds; each round probes a window of
 // candidate positions per chain against the members' FD rows staged in LDS.
 // ---------------------------------------------------------------------------
+// strongly-see test of one LA row against one FD row, both padded to NP
+// columns (LA pad -1, FD pad INF32) and 16-byte aligned in LDS
+template <int NPC>
+__device__ __forceinline__ int ss_count(const int4* la4, const int4* fd4, int NP) {
+  int cnt = 0;
+  const int nq = (NPC > 0) ? NPC / 4 : NP / 4;
+#pragma unroll
+  for (int q = 0; q < (NPC > 0 ? NPC / 4 : 1); q++) {
+    if (NPC == 0) break;
+    const int4 a = la4[q], b = fd4[q];
+    cnt += (a.x >= b.x) + (a.y >= b.y) + (a.z >= b.z) + (a.w >= b.w);
+  }
+  if (NPC == 0) {
+    for (int q = 0; q < nq; q += 4) {
+      const int4 a0 = la4[q], a1 = la4[q + 1], a2 = la4[q + 2], a3 = la4[q + 3];
+      const int4 b0 = fd4[q], b1 = fd4[q + 1], b2 = fd4[q + 2], b3 = fd4[q + 3];
+      cnt += (a0.x >= b0.x) + (a0.y >= b0.y) + (a0.z >= b0.z) + (a0.w >= b0.w);
+      cnt += (a1.x >= b1.x) + (a1.y >= b1.y) + (a1.z >= b1.z) + (a1.w >= b1.w);
+      cnt += (a2.x >= b2.x) + (a2.y >= b2.y) + (a2.z >= b2.z) + (a2.w >= b2.w);
+      cnt += (a3.x >= b3.x) + (a3.y >= b3.y) + (a3.z >= b3.z) + (a3.w >= b3.w);
+    }
+  }
+  return cnt;
+}
+
+__device__ __forceinline__ uint64_t stamp() {
+  uint64_t v;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");
+  return v;
+}
+
+template <int NPC>
 __global__ void __launch_bounds__(1024) k_rounds_frontier(Tables t, const int32_t* olen,
                                                           const int32_t* len, int32_t* rstate,
-                                                          int WIN) {
+                                                          int WIN, uint64_t* dbg) {
+  uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t st_t = 0;
+#define STAMP(k)                                   \
+  if (dbg && threadIdx.x == 0) {                   \
+    const uint64_t now_ = stamp();                 \
+    if ((k) > 0) st_acc[(k) - 1] += now_ - st_t;   \
+    st_t = now_;                                   \
+  }
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int N = t.N, SM = t.SM;
+  const int NP = (N + 15) & ~15;
   const int tid = threadIdx.x, T = blockDim.x;
-  int32_t* sFD = (int32_t*)smem;     // N*N member FD rows
-  int32_t* sP = sFD + N * N;         // N  C_r positions (carried in LDS across rounds)
-  int32_t* sMid = sP + N;            // N  member ids
-  int32_t* sLo = sMid + N;           // N  search start
-  int32_t* sLen = sLo + N;           // N
-  int32_t* sOlen = sLen + N;         // N
-  int32_t* sNeed = sOlen + N;        // N
-  int32_t* sFirst = sNeed + N;       // N
-  int32_t* sNext = sFirst + N;       // N  C_{r+1}
-  int32_t* sCnt = sNext + N;         // N * WIN
+  int32_t* sFD = (int32_t*)smem;       // N*NP   member FD rows (C_r)
+  int32_t* sLAw = sFD + N * NP;        // N*WIN*NP window LA rows
+  int32_t* sP = sLAw + N * WIN * NP;   // N     C_r positions (carried in LDS across rounds)
+  int32_t* sMid = sP + N;              // N     member ids
+  int32_t* sLo = sMid + N;             // N     window start
+  int32_t* sLen = sLo + N;             // N
+  int32_t* sOlen = sLen + N;           // N
+  int32_t* sNeed = sOlen + N;          // N
+  int32_t* sCur = sNeed + N;           // N     C_{r+1} as stored before this kernel
+  int32_t* sNext = sCur + N;           // N     C_{r+1}
+  int32_t* sFlag = sNext + N;          // N*WIN probe satisfied
+  int32_t* sIdw = sFlag + N * WIN;     // N*WIN event ids of the window
   __shared__ int s_rlo, s_any, s_more;
 
   if (tid == 0) s_rlo = INF32;
@@ -425,12 +615,14 @@ __global__ void __launch_bounds__(1024) k_rounds_frontier(Tables t, const int32_
   __syncthreads();
   const int rlo = s_rlo;
   if (rlo == INF32) return;  // no new events
-  // rows written by this kernel are only ever re-read from LDS (a CU's L1 may
-  // hold a stale copy of a line this workgroup stored)
+  // Rows this kernel writes are only re-read from LDS (a CU's L1 may keep a
+  // stale copy of a line the workgroup stored).
   for (int c = tid; c < N; c += T) {
     int p = t.C[(size_t)rlo * N + c];
     if (rlo == 0 && sOlen[c] == 0 && sLen[c] > 0) p = 0;
     sP[c] = p;
+    sMid[c] = (p != INF32) ? t.chain[(size_t)c * t.ccap + p] : -1;
+    sLo[c] = max(p, sOlen[c]);
   }
   __syncthreads();
   int r = rlo;
@@ -439,55 +631,88 @@ __global__ void __launch_bounds__(1024) k_rounds_frontier(Tables t, const int32_
       if (tid == 0) rstate[1] = 1;  // overflow: host grows Rcap and reruns
       return;
     }
-    for (int c = tid; c < N; c += T) {
-      const int p = sP[c];
-      sMid[c] = (p != INF32) ? t.chain[(size_t)c * t.ccap + p] : -1;
-      const int cur = t.C[(size_t)(r + 1) * N + c];  // not yet written by this kernel
-      sNext[c] = cur;
-      const int lo = max(p, sOlen[c]);
-      sLo[c] = lo;
-      sNeed[c] = (cur == INF32 && p != INF32 && lo < sLen[c]) ? 1 : 0;
-    }
-    __syncthreads();
-    for (int item = tid; item < N * N; item += T) {
-      const int d = item / N, i = item - (item / N) * N;
+    STAMP(0);
+    // ---- one burst of independent loads: member FD rows, C_{r+1} as stored,
+    //      and the first probe window (LA rows + ids) of every chain
+    for (int item = tid; item < N * NP; item += T) {
+      const int d = item / NP, i = item - (item / NP) * NP;
       const int p = sP[d];
-      sFD[item] = (p != INF32) ? t.FD[rowoff(t, d, p) + i] : INF32;
+      sFD[item] = (p != INF32 && i < N) ? t.FD[rowoff(t, d, p) + i] : INF32;
     }
-    __syncthreads();
+    for (int c = tid; c < N; c += T) sCur[c] = t.C[(size_t)(r + 1) * N + c];
+    bool first = true;
     for (;;) {
-      for (int i = tid; i < N * WIN; i += T) sCnt[i] = 0;
-      for (int c = tid; c < N; c += T) sFirst[c] = INF32;
       if (tid == 0) s_more = 0;
-      __syncthreads();
-      const int items = N * WIN * N;
-      for (int item = tid; item < items; item += T) {
-        const int c = item / (WIN * N);
-        const int rem = item - c * (WIN * N);
-        const int k = rem / N, d = rem - (rem / N) * N;
-        if (!sNeed[c] || sMid[d] < 0) continue;
+      // loads first (8 per thread in flight), LDS stores after: one HBM latency
+      for (int b0 = tid; b0 < N * WIN * NP; b0 += 8 * T) {
+        int v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const int item = b0 + u * T;
+          v[u] = -1;
+          if (item < N * WIN * NP) {
+            const int c = item / (WIN * NP);
+            const int rem = item - c * (WIN * NP);
+            const int k = rem / NP, i = rem - (rem / NP) * NP;
+            const int p = sLo[c] + k;
+            const bool ok = sP[c] != INF32 && p < sLen[c] && (first || sNeed[c]);
+            if (ok && i < N) v[u] = t.LA[rowoff(t, c, p) + i];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const int item = b0 + u * T;
+          if (item < N * WIN * NP) sLAw[item] = v[u];
+        }
+      }
+      for (int pr = tid; pr < N * WIN; pr += T) {
+        const int c = pr / WIN, k = pr - (pr / WIN) * WIN;
         const int p = sLo[c] + k;
-        if (p >= sLen[c]) continue;
-        if (d == c && p == sP[c]) continue;  // x itself is excluded (not yet in its round)
-        const int32_t* la = t.LA + rowoff(t, c, p);
-        const int32_t* fd = sFD + d * N;
-        int cntss = 0;
-        for (int i = 0; i < N; i++) cntss += (la[i] >= fd[i]) ? 1 : 0;
-        if (cntss >= SM) atomicAdd(&sCnt[c * WIN + k], 1);
+        const bool ok = sP[c] != INF32 && p < sLen[c] && (first || sNeed[c]);
+        sIdw[pr] = ok ? t.chain[(size_t)c * t.ccap + p] : -1;
       }
       __syncthreads();
-      for (int item = tid; item < N * WIN; item += T) {
-        const int c = item / WIN, k = item - (item / WIN) * WIN;
-        if (sNeed[c] && sCnt[item] >= SM) atomicMin(&sFirst[c], k);
+      STAMP(1);
+      if (first) {
+        for (int c = tid; c < N; c += T) {
+          const int p = sP[c];
+          sNext[c] = sCur[c];
+          sNeed[c] = (sCur[c] == INF32 && p != INF32 && sLo[c] < sLen[c]) ? 1 : 0;
+        }
+        __syncthreads();
+        first = false;
+      }
+      // one thread per probe (c, k): x strongly sees >= SM members of C_r \ {x}?
+      for (int pr = tid; pr < N * WIN; pr += T) {
+        const int c = pr / WIN, k = pr - (pr / WIN) * WIN;
+        int flag = 0;
+        const int p = sLo[c] + k;
+        if (sNeed[c] && p < sLen[c]) {
+          const int4* la4 = (const int4*)(sLAw + (size_t)pr * NP);
+          int ss = 0;
+#pragma unroll 4
+          for (int d = 0; d < N; d++) {
+            const bool skip = sMid[d] < 0 || (d == c && p == sP[c]);
+            const int cnt = ss_count<NPC>(la4, (const int4*)(sFD + d * NP), NP);
+            ss += (!skip && cnt >= SM) ? 1 : 0;
+          }
+          flag = ss >= SM;
+        }
+        sFlag[pr] = flag;
       }
       __syncthreads();
+      STAMP(2);
       for (int c = tid; c < N; c += T) {
         if (!sNeed[c]) continue;
-        if (sFirst[c] != INF32) {
-          const int pos = sLo[c] + sFirst[c];
+        int k = 0;
+        while (k < WIN && !sFlag[c * WIN + k]) k++;
+        if (k < WIN) {
+          const int pos = sLo[c] + k;
           sNext[c] = pos;
           t.C[(size_t)(r + 1) * N + c] = pos;
           sNeed[c] = 0;
+          sMid[c] = sIdw[c * WIN + k];  // next round's member
+          sCur[c] = -2;                  // marks "member id known"
         } else if (sLo[c] + WIN >= sLen[c]) {
           sNeed[c] = 0;
         } else {
@@ -496,18 +721,450 @@ __global__ void __launch_bounds__(1024) k_rounds_frontier(Tables t, const int32_
         }
       }
       __syncthreads();
+      STAMP(3);
       if (!s_more) break;
     }
+    // ---- advance: C_{r+1} becomes the member set
     if (tid == 0) s_any = 0;
     __syncthreads();
     for (int c = tid; c < N; c += T) {
-      if (sNext[c] != INF32) s_any = 1;
-      sP[c] = sNext[c];
+      const int p = sNext[c];
+      if (p != INF32) s_any = 1;
+      if (sCur[c] != -2) sMid[c] = (p != INF32) ? t.chain[(size_t)c * t.ccap + p] : -1;
+      sP[c] = p;
+      sLo[c] = max(p, sOlen[c]);
     }
     __syncthreads();
+    STAMP(4);
     if (!s_any) break;
   }
   if (tid == 0) rstate[0] = max(rstate[0], r + 1);  // Rounds()
+  if (dbg && tid == 0) {
+    for (int q = 0; q < 4; q++) dbg[q] += st_acc[q];
+    dbg[5] += (uint64_t)(r - rlo + 1);
+  }
+#undef STAMP
+}
+
+// ---------------------------------------------------------------------------
+// Rounds frontier, ring variant for N <= 16 (the headline configuration).
+// Same recursion as k_rounds_frontier, but the LA/FD rows a round needs are
+// already in LDS: every chain keeps a ring of RING = 2*WIN consecutive chain
+// positions [base, base + RING) starting at its previous probe window.  A
+// round probes [lo, lo + WIN) with lo <= base + WIN, so the ring always covers
+// it; the rows that slide in ([base + RING, lo' + RING)) are loaded into
+// registers at the start of the NEXT round and written to the ring at its end,
+// so their HBM latency hides behind that round's probe work.  Probes run one
+// (probe, member) pair per lane and are reduced with a wave ballot.
+// ---------------------------------------------------------------------------
+template <int WIN>
+__global__ void __launch_bounds__(1024) k_rounds_ring(Tables t, const int32_t* olen,
+                                                      const int32_t* len, int32_t* rstate,
+                                                      uint64_t* dbg) {
+  constexpr int NP = 16, RING = 2 * WIN, RW = 2 * NP + 1, PF = 8;
+  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t st_t = 0;
+#define STAMP(k)                                   \
+  if (dbg && threadIdx.x == 0) {                   \
+    const uint64_t now_ = stamp();                 \
+    if ((k) > 0) st_acc[(k) - 1] += now_ - st_t;   \
+    st_t = now_;                                   \
+  }
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int N = t.N, SM = t.SM;
+  const int tid = threadIdx.x, T = blockDim.x, lane = tid & 63, wv = tid >> 6;
+  int32_t* sRLA = (int32_t*)smem;               // N*RING*NP
+  int32_t* sRFD = sRLA + N * RING * NP;         // N*RING*NP
+  int32_t* sFD = sRFD + N * RING * NP;          // N*NP member FD rows
+  int32_t* sRid = sFD + N * NP;                 // N*RING
+  int32_t* sFlag = sRid + N * RING;             // N*WIN
+  int32_t* sP = sFlag + N * WIN;                // N
+  int32_t* sMid = sP + N;
+  int32_t* sLo = sMid + N;
+  int32_t* sLen = sLo + N;
+  int32_t* sOlen = sLen + N;
+  int32_t* sNeed = sOlen + N;
+  int32_t* sCur = sNeed + N;
+  int32_t* sNext = sCur + N;
+  int32_t* sBase = sNext + N;
+  int32_t* sPa = sBase + N;                     // pending refill [sPa, sPb)
+  int32_t* sPb = sPa + N;
+  int32_t* sPo = sPb + N;                       // N+1 item offsets of the pending refill
+  int32_t* sSync = sPo + N + 1;                 // N  chains needing a synchronous ring load
+  int32_t* sCov = sSync + N;                    // N  start of the ring's coverage
+  __shared__ int s_rlo, s_any, s_more, s_sync;
+
+  // one ring row (LA, FD, id) of chain c, position p into slot p % RING
+  auto ring_field = [&](int c, int p, int f) -> int {
+    if (p >= sLen[c]) return f < NP ? -1 : (f < 2 * NP ? INF32 : -1);
+    if (f < NP) return f < N ? t.LA[rowoff(t, c, p) + f] : -1;
+    if (f < 2 * NP) return (f - NP) < N ? t.FD[rowoff(t, c, p) + (f - NP)] : INF32;
+    return t.chain[(size_t)c * t.ccap + p];
+  };
+  auto ring_store = [&](int c, int p, int f, int v) {
+    const int slot = p % RING;
+    if (f < NP) sRLA[(c * RING + slot) * NP + f] = v;
+    else if (f < 2 * NP) sRFD[(c * RING + slot) * NP + (f - NP)] = v;
+    else sRid[c * RING + slot] = v;
+  };
+  // synchronous ring (re)load of every chain flagged in sSync: [sLo, sLo + RING)
+  auto sync_load = [&]() {
+    for (int item = tid; item < N * RING * RW; item += T) {
+      const int c = item / (RING * RW);
+      if (!sSync[c]) continue;
+      const int rem = item - c * (RING * RW);
+      const int k = rem / RW, f = rem - (rem / RW) * RW;
+      const int p = sLo[c] + k;
+      ring_store(c, p, f, ring_field(c, p, f));
+    }
+  };
+
+  if (tid == 0) s_rlo = INF32;
+  __syncthreads();
+  for (int c = tid; c < N; c += T) {
+    const int ol = olen[c], ln = len[c];
+    sOlen[c] = ol;
+    sLen[c] = ln;
+    if (ln > ol) {
+      int r0 = 0;
+      if (ol == 0) t.C[c] = 0;
+      else r0 = t.round[t.chain[(size_t)c * t.ccap + ol - 1]];
+      atomicMin(&s_rlo, r0);
+    }
+  }
+  __syncthreads();
+  const int rlo = s_rlo;
+  if (rlo == INF32) return;
+  for (int c = tid; c < N; c += T) {
+    int p = t.C[(size_t)rlo * N + c];
+    if (rlo == 0 && sOlen[c] == 0 && sLen[c] > 0) p = 0;
+    sP[c] = p;
+    sLo[c] = p != INF32 ? max(p, sOlen[c]) : 0;
+    sBase[c] = sLo[c];
+    sSync[c] = p != INF32 ? 1 : 0;
+    sPa[c] = sPb[c] = 0;
+  }
+  for (int c = tid; c <= N; c += T) sPo[c] = 0;
+  __syncthreads();
+  sync_load();
+  for (int item = tid; item < N * NP; item += T) {
+    const int d = item / NP, i = item - (item / NP) * NP;
+    const int p = sP[d];
+    sFD[item] = (p != INF32 && i < N) ? t.FD[rowoff(t, d, p) + i] : INF32;
+  }
+  for (int c = tid; c < N; c += T) sMid[c] = sP[c] != INF32 ? t.chain[(size_t)c * t.ccap + sP[c]] : -1;
+  __syncthreads();
+
+  int r = rlo;
+  for (;; r++) {
+    if (r + 1 >= t.Rcap) {
+      if (tid == 0) rstate[1] = 1;
+      return;
+    }
+    STAMP(0);
+    // ---- issue the pending ring refill (landed and stored at the end of the round)
+    const int ptot = sPo[N];
+    int pv[PF];
+#pragma unroll
+    for (int m = 0; m < PF; m++) {
+      const int item = tid + m * T;
+      pv[m] = 0;
+      if (item < ptot) {
+        int c = 0;
+        while (sPo[c + 1] <= item) c++;
+        const int rem = item - sPo[c];
+        const int p = sPa[c] + rem / RW, f = rem - (rem / RW) * RW;
+        pv[m] = ring_field(c, p, f);
+      }
+    }
+    for (int c = tid; c < N; c += T) {
+      const int cur = t.C[(size_t)(r + 1) * N + c];
+      sCur[c] = cur;
+      sNext[c] = cur;
+      sNeed[c] = (cur == INF32 && sP[c] != INF32 && sLo[c] < sLen[c]) ? 1 : 0;
+    }
+    __syncthreads();
+    STAMP(1);
+    for (;;) {
+      // ---- probes: lane = member d, NP lanes per probe (c, k)
+      for (int pair = tid; pair < N * WIN * NP; pair += T) {
+        const int pr = pair / NP, d = pair - (pair / NP) * NP;
+        const int c = pr / WIN, k = pr - (pr / WIN) * WIN;
+        const int p = sLo[c] + k;
+        bool ss = false;
+        if (d < N && sNeed[c] && p < sLen[c] && sMid[d] >= 0 && !(d == c && p == sP[c])) {
+          const int4* la4 = (const int4*)(sRLA + (c * RING + p % RING) * NP);
+          const int4* fd4 = (const int4*)(sFD + d * NP);
+          int cnt = 0;
+#pragma unroll
+          for (int q = 0; q < NP / 4; q++) {
+            const int4 a = la4[q], b = fd4[q];
+            cnt += (a.x >= b.x) + (a.y >= b.y) + (a.z >= b.z) + (a.w >= b.w);
+          }
+          ss = cnt >= SM;
+        }
+        const uint64_t bal = __ballot(ss);
+        if (d == 0) sFlag[pr] = __popcll((bal >> (lane & ~(NP - 1))) & ((1ull << NP) - 1)) >= SM;
+      }
+      __syncthreads();
+      STAMP(2);
+      if (tid == 0) {
+        s_more = 0;
+        s_sync = 0;
+      }
+      __syncthreads();
+      // ---- first satisfied probe per chain (wave per chain, lane per window slot)
+      for (int c = wv; c < N; c += T / 64) {
+        const bool f = lane < WIN && sNeed[c] && sFlag[c * WIN + lane];
+        const uint64_t bal = __ballot(f);
+        if (lane == 0 && sNeed[c]) {
+          if (bal) {
+            const int k = __builtin_ctzll(bal);
+            const int pos = sLo[c] + k;
+            sNext[c] = pos;
+            t.C[(size_t)(r + 1) * N + c] = pos;
+            sNeed[c] = 0;
+          } else if (sLo[c] + WIN >= sLen[c]) {
+            sNeed[c] = 0;
+          } else {
+            // window exhausted without a hit: slide and reload synchronously (rare)
+            sLo[c] += WIN;
+            sBase[c] = sLo[c];
+            sSync[c] = 1;
+            sPa[c] = sPb[c] = 0;
+            s_more = 1;
+          }
+        }
+      }
+      __syncthreads();
+      if (!s_more) break;
+      sync_load();
+      __syncthreads();
+      for (int c = tid; c < N; c += T) sSync[c] = 0;
+      __syncthreads();
+    }
+    STAMP(3);
+    // ---- the pending refill has landed: store it (its slots are no longer probed)
+#pragma unroll
+    for (int m = 0; m < PF; m++) {
+      const int item = tid + m * T;
+      if (item < ptot) {
+        int c = 0;
+        while (sPo[c + 1] <= item) c++;
+        const int rem = item - sPo[c];
+        const int p = sPa[c] + rem / RW, f = rem - (rem / RW) * RW;
+        if (sPa[c] < sPb[c]) ring_store(c, p, f, pv[m]);
+      }
+    }
+    for (int item = tid + PF * T; item < ptot; item += T) {
+      int c = 0;
+      while (sPo[c + 1] <= item) c++;
+      const int rem = item - sPo[c];
+      const int p = sPa[c] + rem / RW, f = rem - (rem / RW) * RW;
+      if (sPa[c] < sPb[c]) ring_store(c, p, f, ring_field(c, p, f));
+    }
+    __syncthreads();
+    STAMP(4);
+    // the ring now covers [sBase, sBase + RING)
+    for (int c = tid; c < N; c += T) sCov[c] = sBase[c];
+    __syncthreads();
+    // ---- member rows of round r+1 (C_{r+1}) from the ring, or HBM outside it
+    for (int item = tid; item < N * NP; item += T) {
+      const int d = item / NP, i = item - (item / NP) * NP;
+      const int p = sNext[d];
+      int v = INF32;
+      if (p != INF32 && i < N) {
+        if (p >= sCov[d] && p < sCov[d] + RING && p < sLen[d])
+          v = sRFD[(d * RING + p % RING) * NP + i];
+        else
+          v = t.FD[rowoff(t, d, p) + i];
+      }
+      sFD[item] = v;
+    }
+    if (tid == 0) s_any = 0;
+    __syncthreads();
+    // ---- advance and plan the next refill
+    for (int c = tid; c < N; c += T) {
+      const int p = sNext[c];
+      if (p != INF32) s_any = 1;
+      int id = -1;
+      if (p != INF32) {
+        if (p >= sCov[c] && p < sCov[c] + RING && p < sLen[c]) id = sRid[c * RING + p % RING];
+        else id = t.chain[(size_t)c * t.ccap + p];
+      }
+      sMid[c] = id;
+      sP[c] = p;
+      const int lo = p != INF32 ? max(p, sOlen[c]) : sLo[c];
+      const int cov = sCov[c];
+      sSync[c] = 0;
+      sPa[c] = sPb[c] = 0;
+      if (p != INF32) {
+        if (lo >= cov && lo + WIN <= cov + RING) {
+          sPa[c] = cov + RING;
+          sPb[c] = max(cov + RING, min(lo + RING, sLen[c]));
+        } else {
+          sSync[c] = 1;
+        }
+        sBase[c] = lo;
+      }
+      sLo[c] = lo;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int o = 0;
+      for (int c = 0; c < N; c++) {
+        sPo[c] = o;
+        o += (sPb[c] - sPa[c]) * RW;
+      }
+      sPo[N] = o;
+      int sy = 0;
+      for (int c = 0; c < N; c++) sy |= sSync[c];
+      s_sync = sy;
+    }
+    __syncthreads();
+    if (s_sync) {
+      sync_load();
+      __syncthreads();
+    }
+    STAMP(5);
+    if (!s_any) break;
+  }
+  if (tid == 0) rstate[0] = max(rstate[0], r + 1);
+  if (dbg && tid == 0) {
+    for (int q = 0; q < 5; q++) dbg[q] += st_acc[q];
+    dbg[5] += (uint64_t)(r - rlo + 1);
+  }
+#undef STAMP
+}
+
+// ---------------------------------------------------------------------------
+// Rounds via first-strong-seer rows (the fast path).
+// fss_c(w) = first position on chain c whose event strongly sees w
+//          = SM-th smallest over i of FD[i][FD[w][i]][c]
+// (x on chain c sees w's first descendant on chain i iff pos(x) >= that FD
+// entry, and strongly seeing w is seeing >= SM of them).  Then, with C_r the
+// round-r frontier (first position per chain with round >= r),
+//   C_{r+1}[c] = SM-th smallest over d of fss_c(C_r[d]),
+// the own-chain term clamped to C_r[c] + 1 (x never strongly sees itself;
+// this only matters for N = 1).  DESIGN.md §Rounds proves both steps.
+// ---------------------------------------------------------------------------
+// k-th smallest (1-based, k <= NPC) of NPC register values: a fully unrolled
+// bitonic network (constant indices keep everything in VGPRs), then a select
+template <int NPC>
+__device__ __forceinline__ int select_kth(int (&v)[NPC], int k) {
+#pragma unroll
+  for (int size = 2; size <= NPC; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+#pragma unroll
+      for (int i = 0; i < NPC; i++) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool up = (i & size) == 0;
+          const int a = v[i], b = v[j];
+          v[i] = up ? min(a, b) : max(a, b);
+          v[j] = up ? max(a, b) : min(a, b);
+        }
+      }
+    }
+  }
+  int r = v[0];
+#pragma unroll
+  for (int i = 1; i < NPC; i++) r = (i == k - 1) ? v[i] : r;
+  return r;
+}
+
+// one lane per (event w, target chain c); events of chain cw from position lo[cw]
+template <int NPC>
+__global__ void k_fss(Tables t, const int32_t* lo, const int32_t* off, int total,
+                      int32_t* FSS) {
+  const int N = t.N;
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  const int ev = g / NPC, c = g - (g / NPC) * NPC;
+  if (ev >= total) return;
+  int cw = 0;
+  while (off[cw + 1] <= ev) cw++;
+  const int pw = lo[cw] + (ev - off[cw]);
+  const int32_t* fdw = t.FD + rowoff(t, cw, pw);
+  int v[NPC];
+#pragma unroll
+  for (int i = 0; i < NPC; i++) {
+    v[i] = INF32;
+    if (i < N) {
+      const int z = fdw[i];
+      if (z != INF32 && c < N) v[i] = t.FD[rowoff(t, i, z) + c];
+    }
+  }
+  if (c < N) FSS[rowoff(t, cw, pw) + c] = select_kth<NPC>(v, t.SM);
+}
+
+// the sequential frontier walk: one wave, lane = chain
+template <int NPC>
+__global__ void __launch_bounds__(64) k_rounds_fss(Tables t, const int32_t* FSS,
+                                                   const int32_t* olen, const int32_t* len,
+                                                   int32_t* rstate, int rlo) {
+  const int N = t.N, SM = t.SM;
+  const int c = threadIdx.x;
+  const bool act = c < N;
+  const int ln = act ? len[c] : 0;
+  const int ol = act ? olen[c] : 0;
+  int P = act ? t.C[(size_t)rlo * N + c] : INF32;
+  if (act && rlo == 0 && ol == 0 && ln > 0) {
+    P = 0;
+    t.C[c] = 0;
+  }
+  int r = rlo;
+  for (;; r++) {
+    if (r + 1 >= t.Rcap) {
+      if (c == 0) rstate[1] = 1;
+      return;
+    }
+    int v[NPC];
+#pragma unroll
+    for (int d = 0; d < NPC; d++) {
+      const int Pd = __builtin_amdgcn_readlane(P, d);
+      v[d] = INF32;
+      if (d < N && act && Pd != INF32) v[d] = FSS[rowoff(t, d, Pd) + c];
+    }
+    const int cur = act ? t.C[(size_t)(r + 1) * N + c] : INF32;
+    int nxt = INF32;
+    if (act && P != INF32) {
+#pragma unroll
+      for (int d = 0; d < NPC; d++)
+        if (d == c) v[d] = max(v[d], P + 1);
+      const int sel = select_kth<NPC>(v, SM);
+      nxt = cur != INF32 ? cur : (sel < ln ? sel : INF32);
+      if (cur == INF32 && nxt != INF32) t.C[(size_t)(r + 1) * N + c] = nxt;
+    }
+    const uint64_t any = __ballot(act && nxt != INF32);
+    P = nxt;
+    if (!any) break;
+  }
+  if (c == 0) rstate[0] = max(rstate[0], r + 1);
+}
+
+// frontier start: r_lo and the first position per chain that can be a member
+__global__ void k_frontier_start(Tables t, const int32_t* olen, const int32_t* len,
+                                 int32_t* out /* [0] rlo, [1..N] start positions */) {
+  __shared__ int s_rlo;
+  const int N = t.N;
+  if (threadIdx.x == 0) s_rlo = INF32;
+  __syncthreads();
+  for (int c = threadIdx.x; c < N; c += blockDim.x) {
+    const int ol = olen[c], ln = len[c];
+    if (ln > ol) atomicMin(&s_rlo, ol == 0 ? 0 : t.round[t.chain[(size_t)c * t.ccap + ol - 1]]);
+  }
+  __syncthreads();
+  const int rlo = s_rlo;
+  if (threadIdx.x == 0) out[0] = rlo;
+  for (int c = threadIdx.x; c < N; c += blockDim.x) {
+    int p = INF32;
+    if (rlo != INF32) {
+      p = t.C[(size_t)rlo * N + c];
+      if (rlo == 0 && olen[c] == 0 && len[c] > 0) p = 0;
+    }
+    out[1 + c] = p == INF32 ? len[c] : p;
+  }
 }
 
 // round(x) = max r with C[r][cx] <= px; witness iff C[round][cx] == px
@@ -787,14 +1444,37 @@ struct SegInfo {
   const uint8_t* dec;
 };
 
+// first call of the batch at which witness W[r][d] is visible (INF32: none / later)
+__global__ void k_arrivals(Tables t, int rr_lo, int nr, const int64_t* nc, int ncalls,
+                           int32_t* arr) {
+  const int item = blockIdx.x * blockDim.x + threadIdx.x;
+  const int N = t.N;
+  if (item >= nr * N) return;
+  const int q = item / N, d = item - (item / N) * N;
+  const int x = t.W[(size_t)(rr_lo + q) * N + d];
+  int a = INF32;
+  if (x >= 0) {
+    int lo = 0, hi = ncalls;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (nc[mid] > x) hi = mid;
+      else lo = mid + 1;
+    }
+    a = lo < ncalls ? lo : INF32;
+  }
+  arr[item] = a;
+}
+
 template <int NWT>
 __global__ void k_segments(Tables t, int rr_lo, int nr, const int64_t* nc, int ncalls,
-                           SegInfo si, int32_t* segcnt, const int32_t* segoff, int32_t* seg_call,
-                           int32_t* seg_round, uint8_t* seg_dec, uint64_t* seg_fws, int mode) {
+                           SegInfo si, const int32_t* arr, int32_t* segcnt, const int32_t* segoff,
+                           int32_t* seg_call, int32_t* seg_round, uint8_t* seg_dec,
+                           uint64_t* seg_fws, int mode) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= nr) return;
   const int N = t.N;
   const int i = rr_lo + q;
+  const int32_t* ar = arr + (size_t)q * N;
   uint64_t known[NWT], val[NWT], pres[NWT], prevf[NWT];
 #pragma unroll
   for (int w = 0; w < NWT; w++) known[w] = val[w] = pres[w] = prevf[w] = 0;
@@ -811,30 +1491,18 @@ __global__ void k_segments(Tables t, int rr_lo, int nr, const int64_t* nc, int n
   const int base = mode ? segoff[q] : 0;
   int c = 0;
   while (c < ncalls) {
-    // state at call c
-    const int64_t n = nc[c];
 #pragma unroll
     for (int w = 0; w < NWT; w++) pres[w] = 0;
-    int nxt_arrival = INF32;
+    int nxt = INF32;
     for (int d = 0; d < N; d++) {
-      const int x = t.W[(size_t)i * N + d];
-      if (x < 0) continue;
-      if (x < n) pres[d >> 6] |= 1ull << (d & 63);
-      else {
-        // first call at which x is visible
-        int a = c + 1, b = ncalls;
-        while (a < b) {
-          const int mid = (a + b) >> 1;
-          if (nc[mid] > x) b = mid;
-          else a = mid + 1;
-        }
-        nxt_arrival = min(nxt_arrival, a);
-      }
+      const int a = ar[d];
+      if (a <= c) pres[d >> 6] |= 1ull << (d & 63);
+      else nxt = min(nxt, a);
     }
     if (c >= cf && c - cf < wl) {
-      const int p = si.pr_off[pi] + (c - cf);
+      const uint8_t* dp = si.dec + (size_t)(si.pr_off[pi] + (c - cf)) * N;
       for (int d = 0; d < N; d++) {
-        const uint8_t o = si.dec[(size_t)p * N + d];
+        const uint8_t o = dp[d];
         const uint64_t b = 1ull << (d & 63);
         if (o) {
           known[d >> 6] |= b;
@@ -844,14 +1512,11 @@ __global__ void k_segments(Tables t, int rr_lo, int nr, const int64_t* nc, int n
       }
     }
     bool exists = false, decided = true, same = true;
+    uint64_t fws[NWT];
 #pragma unroll
     for (int w = 0; w < NWT; w++) {
       if (pres[w]) exists = true;
       if (pres[w] & ~known[w]) decided = false;
-    }
-    uint64_t fws[NWT];
-#pragma unroll
-    for (int w = 0; w < NWT; w++) {
       fws[w] = pres[w] & known[w] & val[w];
       if (fws[w] != prevf[w]) same = false;
     }
@@ -869,10 +1534,9 @@ __global__ void k_segments(Tables t, int rr_lo, int nr, const int64_t* nc, int n
 #pragma unroll
       for (int w = 0; w < NWT; w++) prevf[w] = fws[w];
     }
-    // next change point
-    int nxt = nxt_arrival;
+    // next change point: an arrival, or the next call DecideFame processes round i
     if (c + 1 >= cf && c + 1 - cf < wl) nxt = min(nxt, c + 1);
-    else if (c + 1 < cf && cf < wl + cf) nxt = min(nxt, cf);
+    else if (c + 1 < cf && wl > 0) nxt = min(nxt, cf);
     if (nxt <= c) nxt = c + 1;
     c = nxt;
   }

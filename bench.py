@@ -89,7 +89,6 @@ def main():
 
     for _ in range(args.warmup):
         eng.run()
-    ordered = eng._nordered
 
     def sync_all():
         if dist is not None:
@@ -103,6 +102,7 @@ def main():
     for _ in range(args.steps):
         eng.run()  # returns after the device finished (stream synchronised)
     t1 = time.perf_counter()
+    ordered = eng._nordered
     sync_all()
     step_s = (t1 - t0) / args.steps
     kstats = eng.kernel_stats()
