@@ -32,6 +32,12 @@ using namespace hge;
     }                                                                                \
   } while (0)
 
+#define KLAUNCH_H(h, kern, ...)        \
+  do {                                 \
+    (h)->prof_begin(#kern);            \
+    hipLaunchKernelGGL(kern, __VA_ARGS__); \
+    (h)->prof_end();                   \
+  } while (0)
 #define KLAUNCH(kern, ...)             \
   do {                                 \
     prof_begin(#kern);                 \
@@ -80,6 +86,7 @@ struct DBuf {
 };
 
 inline int div_up(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+static const int32_t kInf = INF32;
 
 }  // namespace
 
@@ -393,9 +400,7 @@ struct hge_engine {
     d_rcnt.grow_keep(nr, Rcap, st, 0);
     d_minw.need(nr);
     // C must be INF32 beyond the old rows
-    std::vector<int32_t> inf((size_t)(nr - Rcap) * N, INF32);
-    HIPCHK(hipMemcpyAsync(d_C.p + oldn, inf.data(), inf.size() * sizeof(int32_t),
-                          hipMemcpyHostToDevice, st));
+    fill_i32(d_C.p + oldn, (int64_t)(nr - Rcap) * N, INF32);
     HIPCHK(hipStreamSynchronize(st));
     Rcap = (int)nr;
   }
@@ -420,8 +425,7 @@ struct hge_engine {
     ctx = 0;
     consensus.clear();
     n_und = 0;
-    std::vector<int32_t> inf((size_t)Rcap * N, INF32);
-    HIPCHK(hipMemcpyAsync(d_C.p, inf.data(), inf.size() * 4, hipMemcpyHostToDevice, st));
+    fill_i32(d_C.p, (int64_t)Rcap * N, INF32);
     HIPCHK(hipMemsetAsync(d_W.p, 0xFF, (size_t)Rcap * N * 4, st));
     HIPCHK(hipMemsetAsync(d_ssb.p, 0, (size_t)Rcap * N * NW * 8, st));
     HIPCHK(hipMemsetAsync(d_seeb.p, 0, (size_t)Rcap * N * NW * 8, st));
@@ -506,6 +510,10 @@ struct hge_engine {
     n_dev = n_events;
   }
 
+  void fill_i32(int32_t* p, int64_t n, int32_t v) {
+    if (n > 0) KLAUNCH(k_fill_i32, dim3(div_up(n, 256)), dim3(256), 0, st, p, n, v);
+  }
+
   template <typename F>
   void readback(F* host, const F* dev, size_t n) {
     HIPCHK(hipMemcpyAsync(host, dev, n * sizeof(F), hipMemcpyDeviceToHost, st));
@@ -547,17 +555,15 @@ struct hge_engine {
       const size_t ldsA = (size_t)(L + 1) * (N + 2 * BW) * 4 + (size_t)L * 4 * 4 +
                           (size_t)2 * L * 4 * 2 + (size_t)BMAX * 4 + (256 + 1) * 4 + N * 4;
       launch_bw(0, nch, ldsA, t, (int)n0, (int)n1, L, nch);
-      int32_t flag[2];
-      readback(flag, s_small.p, 2);
-      if (flag[0] && L > 16) {
+      KLAUNCH(k_scan_small, dim3(1), dim3(1024), 0, st, s_bcount.p, s_boff.p, nch, s_small.p + 2);
+      int32_t fl3[3];
+      readback(fl3, s_small.p, 3);
+      if (fl3[0] && L > 16) {
         L /= 2;
         continue;
       }
-      if (flag[0]) throw EngineError(HGE_ERR_INTERNAL, "external basis overflow");
-      KLAUNCH(k_scan_small, dim3(1), dim3(1024), 0, st, s_bcount.p, s_boff.p, nch,
-                         s_small.p + 2);
-      int32_t total = 0;
-      readback(&total, s_small.p + 2, 1);
+      if (fl3[0]) throw EngineError(HGE_ERR_INTERNAL, "external basis overflow");
+      const int32_t total = fl3[2];
       s_BR.need((size_t)std::max(total, 1) * N);
       const size_t ldsB = ((size_t)N * N + (size_t)BMAX * N + 2 * (size_t)RECW) * 4;
       launch_bw(1, nch, ldsB, t, (int)n0, (int)n1, L, nch);
@@ -579,6 +585,7 @@ struct hge_engine {
         std::vector<int32_t> fst(N + 1);
         readback(fst.data(), s_fst.p, N + 1);
         const int rlo = fst[0];
+        const int Rprev = R;  // C rows >= Rprev are empty before this batch
         if (rlo != INF32) {
           std::vector<int32_t> lo_off(2 * N + 1);
           int tot = 0;
@@ -594,7 +601,15 @@ struct hge_engine {
 #define FSSL(NPC)                                                                                 \
   KLAUNCH(k_fss<NPC>, dim3(div_up((int64_t)tot * NPC, 256)), dim3(256), 0, st, t, s_fsslo.p,      \
           s_fsslo.p + N, tot, d_FSS.p);                                                           \
-  KLAUNCH(k_rounds_fss<NPC>, dim3(1), dim3(64), 0, st, t, d_FSS.p, s_len.p, s_len.p + N, s_small.p, rlo);
+  if (NPC == 16 && !getenv("HGE_NO_BLK"))                                                        \
+    KLAUNCH((k_rounds_fss_blk<16, 128>), dim3(1), dim3(1024), 0, st, t, d_FSS.p, s_len.p,        \
+            s_len.p + N, s_small.p, rlo, Rprev);                                                  \
+  else if (NPC == 32 && !getenv("HGE_NO_BLK"))                                                   \
+    KLAUNCH((k_rounds_fss_blk<32, 32>), dim3(1), dim3(1024), 0, st, t, d_FSS.p, s_len.p,         \
+            s_len.p + N, s_small.p, rlo, Rprev);                                                  \
+  else                                                                                            \
+    KLAUNCH(k_rounds_fss<NPC>, dim3(1), dim3(64), 0, st, t, d_FSS.p, s_len.p, s_len.p + N,       \
+            s_small.p, rlo);
             if (NP == 16) { FSSL(16) } else if (NP == 32) { FSSL(32) } else { FSSL(64) }
 #undef FSSL
           }
@@ -626,13 +641,8 @@ struct hge_engine {
     HIPCHK(hipMemsetAsync(s_small.p + 4, 0, 4, st));
     KLAUNCH(k_round_assign, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0,
                        (int)n1, R, s_newwit.p, s_small.p + 4);
-    int32_t nnew = 0;
-    readback(&nnew, s_small.p + 4, 1);
-    if (nnew) {
-      const int items = nnew * N;
-      KLAUNCH(k_witness_bits, dim3(div_up(items, 256)), dim3(256), 0, st, t,
-                         s_newwit.p, nnew);
-    }
+    KLAUNCH(k_witness_bits, dim3(div_up((int64_t)m * N, 256)), dim3(256), 0, st, t, s_newwit.p,
+            s_small.p + 4);
     KLAUNCH(k_round_minw, dim3(div_up(R, 256)), dim3(256), 0, st, t, 0, R, d_minw.p);
     n_coords = n1;
     coords_len = chain_len;
@@ -735,21 +745,14 @@ struct hge_engine {
         KLAUNCH(k_lcr_scan, dim3(1), dim3(1024), 0, st, s_Lc.p, ncalls, lcr, s_LCR.p,
                            s_pr.p, s_pr.p + 2 * nrounds, s_pr.p + 3 * nrounds, nrounds,
                            s_clast.p, s_flags.p);
-        int32_t fl = 0;
-        readback(&fl, s_flags.p, 1);
-        if (fl) {
+        int32_t fl[3];
+        readback(fl, s_flags.p, 3);
+        if (fl[0]) {
           SPEC *= 2;
           continue;
         }
-        clast.resize(nrounds);
-        readback(clast.data(), s_clast.p, nrounds);
-        std::vector<int32_t> LCRv(ncalls);
-        readback(LCRv.data(), s_LCR.p, ncalls);
-        lcr_new = LCRv[ncalls - 1];
-        if (lcr_new > lcr) {
-          c_set = 0;
-          while (LCRv[c_set] != lcr_new) c_set++;
-        }
+        lcr_new = fl[1];
+        if (lcr_new > lcr) c_set = fl[2];
         break;
       }
     }
@@ -759,20 +762,12 @@ struct hge_engine {
       const int ncand = (int)n_und;
       int32_t* cand = d_und.p;
       // lowest candidate round
-      std::vector<int32_t> hr;
-      int rr_lo;
-      {
-        // min round of candidates: read rounds of candidate ids (host gather via device copy)
-        s_small.need(8);
-        std::vector<int32_t> ids(ncand);
-        readback(ids.data(), cand, ncand);
-        std::vector<int32_t> rounds(ncand);
-        // rounds are monotone-ish; gather on host for simplicity (ids are few relative to E)
-        gather_rounds(ids, rounds);
-        int mn = INF32;
-        for (int v : rounds) mn = std::min(mn, v);
-        rr_lo = mn + 1;
-      }
+      HIPCHK(hipMemcpyAsync(s_small.p + 7, &kInf, 4, hipMemcpyHostToDevice, st));
+      KLAUNCH(k_min_round, dim3(div_up(ncand, 256)), dim3(256), 0, st, d_round.p, cand, ncand,
+              s_small.p + 7);
+      int32_t mnr = INF32;
+      readback(&mnr, s_small.p + 7, 1);
+      const int rr_lo = mnr + 1;
       const int R_last = Rc[ncalls - 1];
       const int nr = std::max(0, R_last - rr_lo);
       if (nr > 0) {
@@ -1007,10 +1002,7 @@ struct hge_engine {
       // append the newly divided events to the undetermined list (insertion order)
       const int64_t a = n_divided, m = n_coords - n_divided;
       ensure_events(n_coords);
-      std::vector<int32_t> ids(m);
-      for (int64_t k = 0; k < m; k++) ids[k] = (int32_t)(a + k);
-      HIPCHK(hipMemcpyAsync(d_und.p + n_und, ids.data(), 4 * m, hipMemcpyHostToDevice, st));
-      HIPCHK(hipStreamSynchronize(st));
+      KLAUNCH(k_iota, dim3(div_up(m, 256)), dim3(256), 0, st, d_und.p + n_und, m, (int32_t)a);
       n_und += m;
       n_divided = n_coords;
     }
@@ -1183,8 +1175,7 @@ int hge_replay_run(hge_engine* h, int64_t* n_ordered) {
   h->consensus.clear();
   h->n_und = 0;
   {
-    std::vector<int32_t> inf((size_t)h->Rcap * h->N, INF32);
-    HIPCHK(hipMemcpyAsync(h->d_C.p, inf.data(), inf.size() * 4, hipMemcpyHostToDevice, h->st));
+    h->fill_i32(h->d_C.p, (int64_t)h->Rcap * h->N, INF32);
     HIPCHK(hipMemsetAsync(h->d_W.p, 0xFF, (size_t)h->Rcap * h->N * 4, h->st));
     HIPCHK(hipMemsetAsync(h->d_ssb.p, 0, (size_t)h->Rcap * h->N * h->NW * 8, h->st));
     HIPCHK(hipMemsetAsync(h->d_seeb.p, 0, (size_t)h->Rcap * h->N * h->NW * 8, h->st));
@@ -1198,12 +1189,8 @@ int hge_replay_run(hge_engine* h, int64_t* n_ordered) {
   HIPCHK(hipEventRecord(h->ev[1], h->st));
   h->n_divided = keep;
   h->update_rdiv();
-  {
-    std::vector<int32_t> ids(keep);
-    for (int64_t k = 0; k < keep; k++) ids[k] = (int32_t)k;
-    HIPCHK(hipMemcpyAsync(h->d_und.p, ids.data(), 4 * keep, hipMemcpyHostToDevice, h->st));
-    h->n_und = keep;
-  }
+  if (keep > 0) KLAUNCH_H(h, k_iota, dim3(div_up(keep, 256)), dim3(256), 0, h->st, h->d_und.p, keep, 0);
+  h->n_und = keep;
   h->replay_order.clear();
   h->replay_counts.clear();
   h->consensus_batch(h->replay_calls, true, true, true, &h->replay_order, &h->replay_counts);

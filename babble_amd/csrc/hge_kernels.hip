@@ -86,6 +86,25 @@ __device__ int block_exclusive_scan(int* a, int n, int* tmp /* blockDim.x + 1 */
   return total;
 }
 
+__global__ void k_fill_i32(int32_t* p, int64_t n, int32_t v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+__global__ void k_iota(int32_t* p, int64_t n, int32_t base) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = base + (int32_t)i;
+}
+
+// lowest round among the candidate events (DecideRoundReceived starts above it)
+__global__ void k_min_round(const int32_t* round, const int32_t* cand, int n, int32_t* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  int v = INF32;
+  if (i < n) v = round[cand[i]];
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+  if ((threadIdx.x & 63) == 0 && v != INF32) atomicMin(out, v);
+}
+
 // ---------------------------------------------------------------------------
 // Coordinates, phase A: one workgroup per chunk of L consecutive new events.
 // Computes, by one sequential pass in LDS, for every event of the chunk
@@ -1143,6 +1162,237 @@ __global__ void __launch_bounds__(64) k_rounds_fss(Tables t, const int32_t* FSS,
   if (c == 0) rstate[0] = max(rstate[0], r + 1);
 }
 
+// The frontier walk with its fss rows prefetched: each chain keeps a ring of
+// RING consecutive fss rows [cov, cov + RING) in LDS.  A round reads one row
+// per chain (its member's); once the next members are known, the ring slides
+// to start at them and the rows sliding in are loaded into registers at the
+// start of the next round and written at its end, a full round before any
+// member can land on them.  One wave, no barriers.  Lane l: in the walk, chain
+// l; in the refill, chain l/4 and int4 column block l%4 (N <= 16).
+template <int RING>
+__global__ void __launch_bounds__(64) k_rounds_fss_ring(Tables t, const int32_t* FSS,
+                                                        const int32_t* olen, const int32_t* len,
+                                                        int32_t* rstate, int rlo, uint64_t* dbg) {
+  constexpr int NPC = 16, Q = 4, PF = 16;
+  __shared__ __attribute__((aligned(16))) int4 ring[NPC * RING * Q];
+  const int N = t.N, SM = t.SM;
+  const int lane = threadIdx.x;
+  const int c = lane;                 // walk role
+  const int fd_ = lane >> 2, fq = lane & 3;  // refill role
+  const bool act = c < N;
+  const bool fact = fd_ < N;
+  const int ln = act ? len[c] : 0;
+  const int fln = fact ? len[fd_] : 0;
+  (void)dbg;
+  auto rowq = [&](int d, int p, int q) -> int4 {
+    const int32_t* row = FSS + rowoff(t, d, p);
+    if (N == 16) return *(const int4*)(row + 4 * q);
+    int4 v;
+    v.x = (4 * q + 0 < N) ? row[4 * q + 0] : INF32;
+    v.y = (4 * q + 1 < N) ? row[4 * q + 1] : INF32;
+    v.z = (4 * q + 2 < N) ? row[4 * q + 2] : INF32;
+    v.w = (4 * q + 3 < N) ? row[4 * q + 3] : INF32;
+    return v;
+  };
+  int P = act ? t.C[(size_t)rlo * N + c] : INF32;
+  if (act && rlo == 0 && (olen[c] == 0) && ln > 0) {
+    P = 0;
+    t.C[c] = 0;
+  }
+  // refill role state: chain fd_'s ring coverage start and pending rows [pa, pb)
+  int fcov = __shfl(P, fd_);
+  int pa = 0, pb = 0;
+  if (fact && fcov != INF32)
+    for (int k = 0; k < RING && fcov + k < fln; k++)
+      ring[(fd_ * RING + ((fcov + k) % RING)) * Q + fq] = rowq(fd_, fcov + k, fq);
+  int curn = act ? t.C[(size_t)(rlo + 1) * N + c] : INF32;  // C[r+1] as stored
+  int r = rlo;
+  for (;; r++) {
+    if (r + 1 >= t.Rcap) {
+      if (lane == 0) rstate[1] = 1;
+      return;
+    }
+    // refill loads planned last round: in flight during this round
+    int4 pv[PF];
+#pragma unroll
+    for (int k = 0; k < PF; k++)
+      pv[k] = (pa + k < pb) ? rowq(fd_, pa + k, fq) : make_int4(0, 0, 0, 0);
+    const int cur = curn;
+    curn = (act && r + 2 < t.Rcap) ? t.C[(size_t)(r + 2) * N + c] : INF32;  // prefetch
+    // member rows from the ring: column c of ring row (d, P_d)
+    int v[NPC];
+    bool miss = false;
+#pragma unroll
+    for (int d = 0; d < NPC; d++) {
+      const int Pd = __builtin_amdgcn_readlane(P, d);
+      const int cd = __builtin_amdgcn_readlane(fcov, 4 * d);
+      const bool inring = d < N && Pd != INF32 && Pd >= cd && Pd < cd + RING;
+      miss |= d < N && Pd != INF32 && !inring;
+      const int* rr = (const int*)&ring[(d * RING + ((inring ? Pd : 0) % RING)) * Q];
+      v[d] = (inring && act) ? rr[c] : INF32;
+    }
+    if (__ballot(miss)) {  // a member outside its ring (incremental batches): read HBM
+#pragma unroll
+      for (int d = 0; d < NPC; d++) {
+        const int Pd = __builtin_amdgcn_readlane(P, d);
+        const int cd = __builtin_amdgcn_readlane(fcov, 4 * d);
+        if (d < N && act && Pd != INF32 && !(Pd >= cd && Pd < cd + RING))
+          v[d] = FSS[rowoff(t, d, Pd) + c];
+      }
+    }
+    int nxt = INF32;
+    if (act && P != INF32) {
+#pragma unroll
+      for (int d = 0; d < NPC; d++)
+        if (d == c) v[d] = max(v[d], P + 1);
+      const int sel = select_kth<NPC>(v, SM);
+      nxt = cur != INF32 ? cur : (sel < ln ? sel : INF32);
+      if (cur == INF32 && nxt != INF32) t.C[(size_t)(r + 1) * N + c] = nxt;
+    }
+    const uint64_t any = __ballot(act && nxt != INF32);
+    // store the refill (slots of rows below the current members: never read again)
+#pragma unroll
+    for (int k = 0; k < PF; k++)
+      if (pa + k < pb) ring[(fd_ * RING + ((pa + k) % RING)) * Q + fq] = pv[k];
+    for (int p = pa + PF; p < pb; p++) ring[(fd_ * RING + (p % RING)) * Q + fq] = rowq(fd_, p, fq);
+    // slide chain fd_'s ring to its next member and plan the rows sliding in
+    const int fnxt = __shfl(nxt, fd_);
+    pa = pb = 0;
+    if (fact && fnxt != INF32) {
+      if (fnxt >= fcov && fnxt < fcov + RING) {
+        pa = fcov + RING;
+        pb = max(pa, min(fnxt + RING, fln));
+      } else {  // jumped past the ring: rebuild it from HBM (rare)
+        for (int k = 0; k < RING && fnxt + k < fln; k++)
+          ring[(fd_ * RING + ((fnxt + k) % RING)) * Q + fq] = rowq(fd_, fnxt + k, fq);
+      }
+      fcov = fnxt;
+    }
+    P = nxt;
+    if (!any) break;
+  }
+  if (lane == 0) rstate[0] = max(rstate[0], r + 1);
+}
+
+// The frontier walk over block-staged fss rows: all waves load rows
+// [P_c, P_c + B) of every chain into LDS in one burst; wave 0 then walks the
+// rounds from LDS alone (wave-synchronous, no barriers) until some member
+// leaves its block; repeat.  C rows are read from HBM only below Rprev (the
+// rounds that existed before this batch; later rows are known to be empty).
+template <int NPC, int B>
+__global__ void __launch_bounds__(1024) k_rounds_fss_blk(Tables t, const int32_t* FSS,
+                                                         const int32_t* olen,
+                                                         const int32_t* len, int32_t* rstate,
+                                                         int rlo, int Rprev) {
+  constexpr int Q = NPC / 4;
+  __shared__ __attribute__((aligned(16))) int4 blk[NPC * B * Q];
+  __shared__ int sP[NPC], sBase[NPC], sLen[NPC], s_done, s_r;
+  const int N = t.N, SM = t.SM;
+  const int tid = threadIdx.x, T = blockDim.x;
+  if (tid < NPC) {
+    const int c = tid;
+    int P = INF32, ln = 0;
+    if (c < N) {
+      ln = len[c];
+      P = t.C[(size_t)rlo * N + c];
+      if (rlo == 0 && olen[c] == 0 && ln > 0) {
+        P = 0;
+        t.C[c] = 0;
+      }
+    }
+    sP[c] = P;
+    sLen[c] = ln;
+  }
+  if (tid == 0) {
+    s_done = 0;
+    s_r = rlo;
+  }
+  __syncthreads();
+  for (;;) {
+    // ---- stage rows [P_c, P_c + B) of every chain
+    for (int c = tid; c < NPC; c += T) sBase[c] = sP[c];
+    constexpr int ITEMS = NPC * B * Q;
+    constexpr int PER = (ITEMS + 1023) / 1024;
+    int4 vals[PER];
+#pragma unroll
+    for (int m = 0; m < PER; m++) {
+      const int item = tid + m * T;
+      vals[m] = make_int4(INF32, INF32, INF32, INF32);
+      if (item < ITEMS) {
+        const int d = item / (B * Q), rem = item - d * (B * Q), k = rem / Q, q = rem - (rem / Q) * Q;
+        const int p = sP[d] + k;
+        if (d < N && sP[d] != INF32 && p < sLen[d]) {
+          const int32_t* row = FSS + rowoff(t, d, p) + 4 * q;
+          if (N == NPC) vals[m] = *(const int4*)row;
+          else {
+            vals[m].x = (4 * q + 0 < N) ? row[0] : INF32;
+            vals[m].y = (4 * q + 1 < N) ? row[1] : INF32;
+            vals[m].z = (4 * q + 2 < N) ? row[2] : INF32;
+            vals[m].w = (4 * q + 3 < N) ? row[3] : INF32;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < PER; m++) {
+      const int item = tid + m * T;
+      if (item < ITEMS) blk[item] = vals[m];
+    }
+    __syncthreads();
+    // ---- wave 0 walks rounds from LDS
+    if (tid < 64) {
+      const int c = tid;
+      const bool act = c < N;
+      int P = act ? sP[c] : INF32;
+      const int base = act ? sBase[c] : 0;
+      const int ln = act ? sLen[c] : 0;
+      int r = s_r;
+      bool done = false;
+      for (;; r++) {
+        const bool out = act && P != INF32 && P - base >= B;
+        if (__ballot(out)) break;  // restage
+        if (r + 1 >= t.Rcap) {
+          if (c == 0) rstate[1] = 1;
+          done = true;
+          break;
+        }
+        int v[NPC];
+#pragma unroll
+        for (int d = 0; d < NPC; d++) {
+          const int Pd = __builtin_amdgcn_readlane(P, d);
+          const int bd = __builtin_amdgcn_readlane(base, d);
+          const int* row = (const int*)&blk[(d * B + (Pd != INF32 ? Pd - bd : 0)) * Q];
+          v[d] = (act && d < N && Pd != INF32) ? row[c] : INF32;
+        }
+        const int cur = (act && r + 1 < Rprev) ? t.C[(size_t)(r + 1) * N + c] : INF32;
+        int nxt = INF32;
+        if (act && P != INF32) {
+#pragma unroll
+          for (int d = 0; d < NPC; d++)
+            if (d == c) v[d] = max(v[d], P + 1);
+          const int sel = select_kth<NPC>(v, SM);
+          nxt = cur != INF32 ? cur : (sel < ln ? sel : INF32);
+          if (cur == INF32 && nxt != INF32) t.C[(size_t)(r + 1) * N + c] = nxt;
+        }
+        const uint64_t any = __ballot(act && nxt != INF32);
+        P = nxt;
+        if (!any) {
+          done = true;
+          break;
+        }
+      }
+      if (c < NPC) sP[c] = P;
+      if (c == 0) {
+        s_r = r;
+        s_done = done;
+        if (done && !rstate[1]) rstate[0] = max(rstate[0], r + 1);
+      }
+    }
+    __syncthreads();
+    if (s_done) break;
+  }
+}
+
 // frontier start: r_lo and the first position per chain that can be a member
 __global__ void k_frontier_start(Tables t, const int32_t* olen, const int32_t* len,
                                  int32_t* out /* [0] rlo, [1..N] start positions */) {
@@ -1220,9 +1470,10 @@ __global__ void k_calls_rounds(const int64_t* nc, int ncalls, const int32_t* min
 
 // strongly-see / see bitsets of each new witness y (round j >= 1) over the
 // slots of round j-1: StronglySee (hashgraph.go:189-208), See (:149-154)
-__global__ void k_witness_bits(Tables t, const int32_t* newwit, int nnew) {
+__global__ void k_witness_bits(Tables t, const int32_t* newwit, const int32_t* pnnew) {
   const int item = blockIdx.x * blockDim.x + threadIdx.x;
   const int N = t.N, NW = t.NW;
+  const int nnew = *pnnew;
   if (item >= nnew * N) return;
   const int y = newwit[item / N];
   const int d = item - (item / N) * N;
@@ -1388,6 +1639,17 @@ __global__ void __launch_bounds__(1024) k_lcr_scan(const int32_t* Lc, int ncalls
     LCR[i] = run;
   }
   __syncthreads();
+  if (tid == 0) {
+    const int fin = LCR[ncalls - 1];
+    flags[1] = fin;
+    int a = 0, b = ncalls - 1;  // first call where LCR reached its final value
+    while (a < b) {
+      const int mid = (a + b) >> 1;
+      if (LCR[mid] >= fin) b = mid;
+      else a = mid + 1;
+    }
+    flags[2] = a;
+  }
   for (int ri = tid; ri < nrounds; ri += T) {
     const int i = pr_round[ri];
     int a = 0, b = ncalls;  // first c with LCR[c] >= i
