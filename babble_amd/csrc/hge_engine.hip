@@ -32,17 +32,16 @@ using namespace hge;
     }                                                                                \
   } while (0)
 
-#define KLAUNCH_H(h, kern, ...)        \
-  do {                                 \
-    (h)->prof_begin(#kern);            \
-    hipLaunchKernelGGL(kern, __VA_ARGS__); \
-    (h)->prof_end();                   \
-  } while (0)
-#define KLAUNCH(kern, ...)             \
-  do {                                 \
-    prof_begin(#kern);                 \
-    hipLaunchKernelGGL(kern, __VA_ARGS__); \
-    prof_end();                        \
+// every launch is checked: a launch the runtime refuses (e.g. too much LDS)
+// must fail the call, never leave a table silently unwritten
+#define KLAUNCH(kern, ...)                                                             \
+  do {                                                                                 \
+    prof_begin(#kern);                                                                 \
+    hipLaunchKernelGGL(kern, __VA_ARGS__);                                             \
+    const hipError_t le_ = hipGetLastError();                                          \
+    if (le_ != hipSuccess)                                                             \
+      throw EngineError(HGE_ERR_DEVICE, std::string("launch " #kern ": ") + hipGetErrorString(le_)); \
+    prof_end();                                                                        \
   } while (0)
 
 namespace {
@@ -290,7 +289,6 @@ struct hge_engine {
     LDSATTR(k_coord_final<4>);
     LDSATTR(k_coord_final<8>);
     LDSATTR(k_coord_final<16>);
-    LDSATTR(k_rounds_ring<16>);
     LDSATTR(k_rounds_frontier<16>);
     LDSATTR(k_rounds_frontier<32>);
     LDSATTR(k_rounds_frontier<64>);
@@ -510,6 +508,10 @@ struct hge_engine {
     n_dev = n_events;
   }
 
+  void fill_iota(int32_t* p, int64_t n, int32_t base) {
+    if (n > 0) KLAUNCH(k_iota, dim3(div_up(n, 256)), dim3(256), 0, st, p, n, base);
+  }
+
   void fill_i32(int32_t* p, int64_t n, int32_t v) {
     if (n > 0) KLAUNCH(k_fill_i32, dim3(div_up(n, 256)), dim3(256), 0, st, p, n, v);
   }
@@ -597,15 +599,17 @@ struct hge_engine {
           lo_off[2 * N] = tot;
           s_fsslo.need(2 * N + 1);
           HIPCHK(hipMemcpyAsync(s_fsslo.p, lo_off.data(), 4 * (2 * N + 1), hipMemcpyHostToDevice, st));
+          int maxlen = 0;
+          for (int c = 0; c < N; c++) maxlen = std::max(maxlen, chain_len[c]);
           if (tot > 0) {
 #define FSSL(NPC)                                                                                 \
   KLAUNCH(k_fss<NPC>, dim3(div_up((int64_t)tot * NPC, 256)), dim3(256), 0, st, t, s_fsslo.p,      \
           s_fsslo.p + N, tot, d_FSS.p);                                                           \
-  if (NPC == 16 && !getenv("HGE_NO_BLK"))                                                        \
-    KLAUNCH((k_rounds_fss_blk<16, 128>), dim3(1), dim3(1024), 0, st, t, d_FSS.p, s_len.p,        \
+  if (NPC == 16 && maxlen < 0xFFFF)                                                               \
+    KLAUNCH((k_rounds_walk<16, 4, 256>), dim3(1), dim3(1024), 0, st, t, d_FSS.p, s_len.p,         \
             s_len.p + N, s_small.p, rlo, Rprev);                                                  \
-  else if (NPC == 32 && !getenv("HGE_NO_BLK"))                                                   \
-    KLAUNCH((k_rounds_fss_blk<32, 32>), dim3(1), dim3(1024), 0, st, t, d_FSS.p, s_len.p,         \
+  else if (NPC == 32 && maxlen < 0xFFFF)                                                          \
+    KLAUNCH((k_rounds_walk<32, 2, 64>), dim3(1), dim3(1024), 0, st, t, d_FSS.p, s_len.p,          \
             s_len.p + N, s_small.p, rlo, Rprev);                                                  \
   else                                                                                            \
     KLAUNCH(k_rounds_fss<NPC>, dim3(1), dim3(64), 0, st, t, d_FSS.p, s_len.p, s_len.p + N,       \
@@ -1189,7 +1193,7 @@ int hge_replay_run(hge_engine* h, int64_t* n_ordered) {
   HIPCHK(hipEventRecord(h->ev[1], h->st));
   h->n_divided = keep;
   h->update_rdiv();
-  if (keep > 0) KLAUNCH_H(h, k_iota, dim3(div_up(keep, 256)), dim3(256), 0, h->st, h->d_und.p, keep, 0);
+  if (keep > 0) h->fill_iota(h->d_und.p, keep, 0);
   h->n_und = keep;
   h->replay_order.clear();
   h->replay_counts.clear();

@@ -766,297 +766,6 @@ __global__ void __launch_bounds__(1024) k_rounds_frontier(Tables t, const int32_
 }
 
 // ---------------------------------------------------------------------------
-// Rounds frontier, ring variant for N <= 16 (the headline configuration).
-// Same recursion as k_rounds_frontier, but the LA/FD rows a round needs are
-// already in LDS: every chain keeps a ring of RING = 2*WIN consecutive chain
-// positions [base, base + RING) starting at its previous probe window.  A
-// round probes [lo, lo + WIN) with lo <= base + WIN, so the ring always covers
-// it; the rows that slide in ([base + RING, lo' + RING)) are loaded into
-// registers at the start of the NEXT round and written to the ring at its end,
-// so their HBM latency hides behind that round's probe work.  Probes run one
-// (probe, member) pair per lane and are reduced with a wave ballot.
-// ---------------------------------------------------------------------------
-template <int WIN>
-__global__ void __launch_bounds__(1024) k_rounds_ring(Tables t, const int32_t* olen,
-                                                      const int32_t* len, int32_t* rstate,
-                                                      uint64_t* dbg) {
-  constexpr int NP = 16, RING = 2 * WIN, RW = 2 * NP + 1, PF = 8;
-  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t st_t = 0;
-#define STAMP(k)                                   \
-  if (dbg && threadIdx.x == 0) {                   \
-    const uint64_t now_ = stamp();                 \
-    if ((k) > 0) st_acc[(k) - 1] += now_ - st_t;   \
-    st_t = now_;                                   \
-  }
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int N = t.N, SM = t.SM;
-  const int tid = threadIdx.x, T = blockDim.x, lane = tid & 63, wv = tid >> 6;
-  int32_t* sRLA = (int32_t*)smem;               // N*RING*NP
-  int32_t* sRFD = sRLA + N * RING * NP;         // N*RING*NP
-  int32_t* sFD = sRFD + N * RING * NP;          // N*NP member FD rows
-  int32_t* sRid = sFD + N * NP;                 // N*RING
-  int32_t* sFlag = sRid + N * RING;             // N*WIN
-  int32_t* sP = sFlag + N * WIN;                // N
-  int32_t* sMid = sP + N;
-  int32_t* sLo = sMid + N;
-  int32_t* sLen = sLo + N;
-  int32_t* sOlen = sLen + N;
-  int32_t* sNeed = sOlen + N;
-  int32_t* sCur = sNeed + N;
-  int32_t* sNext = sCur + N;
-  int32_t* sBase = sNext + N;
-  int32_t* sPa = sBase + N;                     // pending refill [sPa, sPb)
-  int32_t* sPb = sPa + N;
-  int32_t* sPo = sPb + N;                       // N+1 item offsets of the pending refill
-  int32_t* sSync = sPo + N + 1;                 // N  chains needing a synchronous ring load
-  int32_t* sCov = sSync + N;                    // N  start of the ring's coverage
-  __shared__ int s_rlo, s_any, s_more, s_sync;
-
-  // one ring row (LA, FD, id) of chain c, position p into slot p % RING
-  auto ring_field = [&](int c, int p, int f) -> int {
-    if (p >= sLen[c]) return f < NP ? -1 : (f < 2 * NP ? INF32 : -1);
-    if (f < NP) return f < N ? t.LA[rowoff(t, c, p) + f] : -1;
-    if (f < 2 * NP) return (f - NP) < N ? t.FD[rowoff(t, c, p) + (f - NP)] : INF32;
-    return t.chain[(size_t)c * t.ccap + p];
-  };
-  auto ring_store = [&](int c, int p, int f, int v) {
-    const int slot = p % RING;
-    if (f < NP) sRLA[(c * RING + slot) * NP + f] = v;
-    else if (f < 2 * NP) sRFD[(c * RING + slot) * NP + (f - NP)] = v;
-    else sRid[c * RING + slot] = v;
-  };
-  // synchronous ring (re)load of every chain flagged in sSync: [sLo, sLo + RING)
-  auto sync_load = [&]() {
-    for (int item = tid; item < N * RING * RW; item += T) {
-      const int c = item / (RING * RW);
-      if (!sSync[c]) continue;
-      const int rem = item - c * (RING * RW);
-      const int k = rem / RW, f = rem - (rem / RW) * RW;
-      const int p = sLo[c] + k;
-      ring_store(c, p, f, ring_field(c, p, f));
-    }
-  };
-
-  if (tid == 0) s_rlo = INF32;
-  __syncthreads();
-  for (int c = tid; c < N; c += T) {
-    const int ol = olen[c], ln = len[c];
-    sOlen[c] = ol;
-    sLen[c] = ln;
-    if (ln > ol) {
-      int r0 = 0;
-      if (ol == 0) t.C[c] = 0;
-      else r0 = t.round[t.chain[(size_t)c * t.ccap + ol - 1]];
-      atomicMin(&s_rlo, r0);
-    }
-  }
-  __syncthreads();
-  const int rlo = s_rlo;
-  if (rlo == INF32) return;
-  for (int c = tid; c < N; c += T) {
-    int p = t.C[(size_t)rlo * N + c];
-    if (rlo == 0 && sOlen[c] == 0 && sLen[c] > 0) p = 0;
-    sP[c] = p;
-    sLo[c] = p != INF32 ? max(p, sOlen[c]) : 0;
-    sBase[c] = sLo[c];
-    sSync[c] = p != INF32 ? 1 : 0;
-    sPa[c] = sPb[c] = 0;
-  }
-  for (int c = tid; c <= N; c += T) sPo[c] = 0;
-  __syncthreads();
-  sync_load();
-  for (int item = tid; item < N * NP; item += T) {
-    const int d = item / NP, i = item - (item / NP) * NP;
-    const int p = sP[d];
-    sFD[item] = (p != INF32 && i < N) ? t.FD[rowoff(t, d, p) + i] : INF32;
-  }
-  for (int c = tid; c < N; c += T) sMid[c] = sP[c] != INF32 ? t.chain[(size_t)c * t.ccap + sP[c]] : -1;
-  __syncthreads();
-
-  int r = rlo;
-  for (;; r++) {
-    if (r + 1 >= t.Rcap) {
-      if (tid == 0) rstate[1] = 1;
-      return;
-    }
-    STAMP(0);
-    // ---- issue the pending ring refill (landed and stored at the end of the round)
-    const int ptot = sPo[N];
-    int pv[PF];
-#pragma unroll
-    for (int m = 0; m < PF; m++) {
-      const int item = tid + m * T;
-      pv[m] = 0;
-      if (item < ptot) {
-        int c = 0;
-        while (sPo[c + 1] <= item) c++;
-        const int rem = item - sPo[c];
-        const int p = sPa[c] + rem / RW, f = rem - (rem / RW) * RW;
-        pv[m] = ring_field(c, p, f);
-      }
-    }
-    for (int c = tid; c < N; c += T) {
-      const int cur = t.C[(size_t)(r + 1) * N + c];
-      sCur[c] = cur;
-      sNext[c] = cur;
-      sNeed[c] = (cur == INF32 && sP[c] != INF32 && sLo[c] < sLen[c]) ? 1 : 0;
-    }
-    __syncthreads();
-    STAMP(1);
-    for (;;) {
-      // ---- probes: lane = member d, NP lanes per probe (c, k)
-      for (int pair = tid; pair < N * WIN * NP; pair += T) {
-        const int pr = pair / NP, d = pair - (pair / NP) * NP;
-        const int c = pr / WIN, k = pr - (pr / WIN) * WIN;
-        const int p = sLo[c] + k;
-        bool ss = false;
-        if (d < N && sNeed[c] && p < sLen[c] && sMid[d] >= 0 && !(d == c && p == sP[c])) {
-          const int4* la4 = (const int4*)(sRLA + (c * RING + p % RING) * NP);
-          const int4* fd4 = (const int4*)(sFD + d * NP);
-          int cnt = 0;
-#pragma unroll
-          for (int q = 0; q < NP / 4; q++) {
-            const int4 a = la4[q], b = fd4[q];
-            cnt += (a.x >= b.x) + (a.y >= b.y) + (a.z >= b.z) + (a.w >= b.w);
-          }
-          ss = cnt >= SM;
-        }
-        const uint64_t bal = __ballot(ss);
-        if (d == 0) sFlag[pr] = __popcll((bal >> (lane & ~(NP - 1))) & ((1ull << NP) - 1)) >= SM;
-      }
-      __syncthreads();
-      STAMP(2);
-      if (tid == 0) {
-        s_more = 0;
-        s_sync = 0;
-      }
-      __syncthreads();
-      // ---- first satisfied probe per chain (wave per chain, lane per window slot)
-      for (int c = wv; c < N; c += T / 64) {
-        const bool f = lane < WIN && sNeed[c] && sFlag[c * WIN + lane];
-        const uint64_t bal = __ballot(f);
-        if (lane == 0 && sNeed[c]) {
-          if (bal) {
-            const int k = __builtin_ctzll(bal);
-            const int pos = sLo[c] + k;
-            sNext[c] = pos;
-            t.C[(size_t)(r + 1) * N + c] = pos;
-            sNeed[c] = 0;
-          } else if (sLo[c] + WIN >= sLen[c]) {
-            sNeed[c] = 0;
-          } else {
-            // window exhausted without a hit: slide and reload synchronously (rare)
-            sLo[c] += WIN;
-            sBase[c] = sLo[c];
-            sSync[c] = 1;
-            sPa[c] = sPb[c] = 0;
-            s_more = 1;
-          }
-        }
-      }
-      __syncthreads();
-      if (!s_more) break;
-      sync_load();
-      __syncthreads();
-      for (int c = tid; c < N; c += T) sSync[c] = 0;
-      __syncthreads();
-    }
-    STAMP(3);
-    // ---- the pending refill has landed: store it (its slots are no longer probed)
-#pragma unroll
-    for (int m = 0; m < PF; m++) {
-      const int item = tid + m * T;
-      if (item < ptot) {
-        int c = 0;
-        while (sPo[c + 1] <= item) c++;
-        const int rem = item - sPo[c];
-        const int p = sPa[c] + rem / RW, f = rem - (rem / RW) * RW;
-        if (sPa[c] < sPb[c]) ring_store(c, p, f, pv[m]);
-      }
-    }
-    for (int item = tid + PF * T; item < ptot; item += T) {
-      int c = 0;
-      while (sPo[c + 1] <= item) c++;
-      const int rem = item - sPo[c];
-      const int p = sPa[c] + rem / RW, f = rem - (rem / RW) * RW;
-      if (sPa[c] < sPb[c]) ring_store(c, p, f, ring_field(c, p, f));
-    }
-    __syncthreads();
-    STAMP(4);
-    // the ring now covers [sBase, sBase + RING)
-    for (int c = tid; c < N; c += T) sCov[c] = sBase[c];
-    __syncthreads();
-    // ---- member rows of round r+1 (C_{r+1}) from the ring, or HBM outside it
-    for (int item = tid; item < N * NP; item += T) {
-      const int d = item / NP, i = item - (item / NP) * NP;
-      const int p = sNext[d];
-      int v = INF32;
-      if (p != INF32 && i < N) {
-        if (p >= sCov[d] && p < sCov[d] + RING && p < sLen[d])
-          v = sRFD[(d * RING + p % RING) * NP + i];
-        else
-          v = t.FD[rowoff(t, d, p) + i];
-      }
-      sFD[item] = v;
-    }
-    if (tid == 0) s_any = 0;
-    __syncthreads();
-    // ---- advance and plan the next refill
-    for (int c = tid; c < N; c += T) {
-      const int p = sNext[c];
-      if (p != INF32) s_any = 1;
-      int id = -1;
-      if (p != INF32) {
-        if (p >= sCov[c] && p < sCov[c] + RING && p < sLen[c]) id = sRid[c * RING + p % RING];
-        else id = t.chain[(size_t)c * t.ccap + p];
-      }
-      sMid[c] = id;
-      sP[c] = p;
-      const int lo = p != INF32 ? max(p, sOlen[c]) : sLo[c];
-      const int cov = sCov[c];
-      sSync[c] = 0;
-      sPa[c] = sPb[c] = 0;
-      if (p != INF32) {
-        if (lo >= cov && lo + WIN <= cov + RING) {
-          sPa[c] = cov + RING;
-          sPb[c] = max(cov + RING, min(lo + RING, sLen[c]));
-        } else {
-          sSync[c] = 1;
-        }
-        sBase[c] = lo;
-      }
-      sLo[c] = lo;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      int o = 0;
-      for (int c = 0; c < N; c++) {
-        sPo[c] = o;
-        o += (sPb[c] - sPa[c]) * RW;
-      }
-      sPo[N] = o;
-      int sy = 0;
-      for (int c = 0; c < N; c++) sy |= sSync[c];
-      s_sync = sy;
-    }
-    __syncthreads();
-    if (s_sync) {
-      sync_load();
-      __syncthreads();
-    }
-    STAMP(5);
-    if (!s_any) break;
-  }
-  if (tid == 0) rstate[0] = max(rstate[0], r + 1);
-  if (dbg && tid == 0) {
-    for (int q = 0; q < 5; q++) dbg[q] += st_acc[q];
-    dbg[5] += (uint64_t)(r - rlo + 1);
-  }
-#undef STAMP
-}
-
-// ---------------------------------------------------------------------------
 // Rounds via first-strong-seer rows (the fast path).
 // fss_c(w) = first position on chain c whose event strongly sees w
 //          = SM-th smallest over i of FD[i][FD[w][i]][c]
@@ -1162,131 +871,37 @@ __global__ void __launch_bounds__(64) k_rounds_fss(Tables t, const int32_t* FSS,
   if (c == 0) rstate[0] = max(rstate[0], r + 1);
 }
 
-// The frontier walk with its fss rows prefetched: each chain keeps a ring of
-// RING consecutive fss rows [cov, cov + RING) in LDS.  A round reads one row
-// per chain (its member's); once the next members are known, the ring slides
-// to start at them and the rows sliding in are loaded into registers at the
-// start of the next round and written at its end, a full round before any
-// member can land on them.  One wave, no barriers.  Lane l: in the walk, chain
-// l; in the refill, chain l/4 and int4 column block l%4 (N <= 16).
-template <int RING>
-__global__ void __launch_bounds__(64) k_rounds_fss_ring(Tables t, const int32_t* FSS,
-                                                        const int32_t* olen, const int32_t* len,
-                                                        int32_t* rstate, int rlo, uint64_t* dbg) {
-  constexpr int NPC = 16, Q = 4, PF = 16;
-  __shared__ __attribute__((aligned(16))) int4 ring[NPC * RING * Q];
-  const int N = t.N, SM = t.SM;
-  const int lane = threadIdx.x;
-  const int c = lane;                 // walk role
-  const int fd_ = lane >> 2, fq = lane & 3;  // refill role
-  const bool act = c < N;
-  const bool fact = fd_ < N;
-  const int ln = act ? len[c] : 0;
-  const int fln = fact ? len[fd_] : 0;
-  (void)dbg;
-  auto rowq = [&](int d, int p, int q) -> int4 {
-    const int32_t* row = FSS + rowoff(t, d, p);
-    if (N == 16) return *(const int4*)(row + 4 * q);
-    int4 v;
-    v.x = (4 * q + 0 < N) ? row[4 * q + 0] : INF32;
-    v.y = (4 * q + 1 < N) ? row[4 * q + 1] : INF32;
-    v.z = (4 * q + 2 < N) ? row[4 * q + 2] : INF32;
-    v.w = (4 * q + 3 < N) ? row[4 * q + 3] : INF32;
-    return v;
-  };
-  int P = act ? t.C[(size_t)rlo * N + c] : INF32;
-  if (act && rlo == 0 && (olen[c] == 0) && ln > 0) {
-    P = 0;
-    t.C[c] = 0;
-  }
-  // refill role state: chain fd_'s ring coverage start and pending rows [pa, pb)
-  int fcov = __shfl(P, fd_);
-  int pa = 0, pb = 0;
-  if (fact && fcov != INF32)
-    for (int k = 0; k < RING && fcov + k < fln; k++)
-      ring[(fd_ * RING + ((fcov + k) % RING)) * Q + fq] = rowq(fd_, fcov + k, fq);
-  int curn = act ? t.C[(size_t)(rlo + 1) * N + c] : INF32;  // C[r+1] as stored
-  int r = rlo;
-  for (;; r++) {
-    if (r + 1 >= t.Rcap) {
-      if (lane == 0) rstate[1] = 1;
-      return;
-    }
-    // refill loads planned last round: in flight during this round
-    int4 pv[PF];
-#pragma unroll
-    for (int k = 0; k < PF; k++)
-      pv[k] = (pa + k < pb) ? rowq(fd_, pa + k, fq) : make_int4(0, 0, 0, 0);
-    const int cur = curn;
-    curn = (act && r + 2 < t.Rcap) ? t.C[(size_t)(r + 2) * N + c] : INF32;  // prefetch
-    // member rows from the ring: column c of ring row (d, P_d)
-    int v[NPC];
-    bool miss = false;
-#pragma unroll
-    for (int d = 0; d < NPC; d++) {
-      const int Pd = __builtin_amdgcn_readlane(P, d);
-      const int cd = __builtin_amdgcn_readlane(fcov, 4 * d);
-      const bool inring = d < N && Pd != INF32 && Pd >= cd && Pd < cd + RING;
-      miss |= d < N && Pd != INF32 && !inring;
-      const int* rr = (const int*)&ring[(d * RING + ((inring ? Pd : 0) % RING)) * Q];
-      v[d] = (inring && act) ? rr[c] : INF32;
-    }
-    if (__ballot(miss)) {  // a member outside its ring (incremental batches): read HBM
-#pragma unroll
-      for (int d = 0; d < NPC; d++) {
-        const int Pd = __builtin_amdgcn_readlane(P, d);
-        const int cd = __builtin_amdgcn_readlane(fcov, 4 * d);
-        if (d < N && act && Pd != INF32 && !(Pd >= cd && Pd < cd + RING))
-          v[d] = FSS[rowoff(t, d, Pd) + c];
-      }
-    }
-    int nxt = INF32;
-    if (act && P != INF32) {
-#pragma unroll
-      for (int d = 0; d < NPC; d++)
-        if (d == c) v[d] = max(v[d], P + 1);
-      const int sel = select_kth<NPC>(v, SM);
-      nxt = cur != INF32 ? cur : (sel < ln ? sel : INF32);
-      if (cur == INF32 && nxt != INF32) t.C[(size_t)(r + 1) * N + c] = nxt;
-    }
-    const uint64_t any = __ballot(act && nxt != INF32);
-    // store the refill (slots of rows below the current members: never read again)
-#pragma unroll
-    for (int k = 0; k < PF; k++)
-      if (pa + k < pb) ring[(fd_ * RING + ((pa + k) % RING)) * Q + fq] = pv[k];
-    for (int p = pa + PF; p < pb; p++) ring[(fd_ * RING + (p % RING)) * Q + fq] = rowq(fd_, p, fq);
-    // slide chain fd_'s ring to its next member and plan the rows sliding in
-    const int fnxt = __shfl(nxt, fd_);
-    pa = pb = 0;
-    if (fact && fnxt != INF32) {
-      if (fnxt >= fcov && fnxt < fcov + RING) {
-        pa = fcov + RING;
-        pb = max(pa, min(fnxt + RING, fln));
-      } else {  // jumped past the ring: rebuild it from HBM (rare)
-        for (int k = 0; k < RING && fnxt + k < fln; k++)
-          ring[(fd_ * RING + ((fnxt + k) % RING)) * Q + fq] = rowq(fd_, fnxt + k, fq);
-      }
-      fcov = fnxt;
-    }
-    P = nxt;
-    if (!any) break;
-  }
-  if (lane == 0) rstate[0] = max(rstate[0], r + 1);
+// The frontier walk (C_{r+1}[c] = SM-th smallest over d of fss_c(C_r[d])).
+// Every step depends on the previous one, so the walk is latency-bound and
+// runs in ONE wave with no barriers: lane (c, q) = chain c, quarter q of the
+// d range (LPC lanes per chain, VPL = NPC/LPC values per lane).  A step is
+// VPL LDS gathers, a bitonic network over the NPC values of each chain whose
+// in-lane stages are register min/max and whose cross-lane stages are DPP
+// quad permutes, and one LDS store of the new frontier.  Global traffic is
+// taken out of the step entirely: all 16 waves stage blocks of fss rows
+// [P_d, P_d + B) of every chain into LDS as uint16 (chain positions < 65535,
+// checked by the host) together with the already-known C rows of the next RB
+// rounds; the walk buffers its C rows in LDS and they are flushed at the next
+// restage.
+// ---------------------------------------------------------------------------
+template <int X>
+__device__ __forceinline__ int dpp_xor(int v) {
+  static_assert(X == 1 || X == 2, "quad permutes only");
+  // quad_perm [1,0,3,2] = 0xB1, [2,3,0,1] = 0x4E
+  return __builtin_amdgcn_mov_dpp(v, X == 1 ? 0xB1 : 0x4E, 0xF, 0xF, false);
 }
 
-// The frontier walk over block-staged fss rows: all waves load rows
-// [P_c, P_c + B) of every chain into LDS in one burst; wave 0 then walks the
-// rounds from LDS alone (wave-synchronous, no barriers) until some member
-// leaves its block; repeat.  C rows are read from HBM only below Rprev (the
-// rounds that existed before this batch; later rows are known to be empty).
-template <int NPC, int B>
-__global__ void __launch_bounds__(1024) k_rounds_fss_blk(Tables t, const int32_t* FSS,
-                                                         const int32_t* olen,
-                                                         const int32_t* len, int32_t* rstate,
-                                                         int rlo, int Rprev) {
-  constexpr int Q = NPC / 4;
-  __shared__ __attribute__((aligned(16))) int4 blk[NPC * B * Q];
-  __shared__ int sP[NPC], sBase[NPC], sLen[NPC], s_done, s_r;
+template <int NPC, int LPC, int B>
+__global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const int32_t* FSS,
+                                                      const int32_t* olen, const int32_t* len,
+                                                      int32_t* rstate, int rlo, int Rprev) {
+  constexpr int VPL = NPC / LPC;
+  constexpr int RB = 64;  // C rows buffered per restage
+  static_assert(NPC * LPC == 64, "one wave walks");
+  __shared__ __attribute__((aligned(16))) uint16_t blk[NPC * B * NPC];  // [d][k][c]
+  __shared__ __attribute__((aligned(16))) int sP[NPC];
+  __shared__ int sBase[NPC], sLen[NPC], sC[RB * NPC];
+  __shared__ int s_r, s_done, s_nr;
   const int N = t.N, SM = t.SM;
   const int tid = threadIdx.x, T = blockDim.x;
   if (tid < NPC) {
@@ -1304,95 +919,167 @@ __global__ void __launch_bounds__(1024) k_rounds_fss_blk(Tables t, const int32_t
     sLen[c] = ln;
   }
   if (tid == 0) {
-    s_done = 0;
     s_r = rlo;
+    s_done = 0;
   }
   __syncthreads();
   for (;;) {
-    // ---- stage rows [P_c, P_c + B) of every chain
-    for (int c = tid; c < NPC; c += T) sBase[c] = sP[c];
-    constexpr int ITEMS = NPC * B * Q;
-    constexpr int PER = (ITEMS + 1023) / 1024;
+    const int r0 = s_r;
+    // ---- restage: fss rows [P_d, P_d + B) of every chain, 4 columns per item;
+    //      all loads of a thread are in flight before the first LDS store
+    constexpr int ITEMS = NPC * B * (NPC / 4);
+    constexpr int PER = (ITEMS + 1023) / 1024;  // launched with 1024 threads
     int4 vals[PER];
 #pragma unroll
     for (int m = 0; m < PER; m++) {
-      const int item = tid + m * T;
-      vals[m] = make_int4(INF32, INF32, INF32, INF32);
-      if (item < ITEMS) {
-        const int d = item / (B * Q), rem = item - d * (B * Q), k = rem / Q, q = rem - (rem / Q) * Q;
-        const int p = sP[d] + k;
-        if (d < N && sP[d] != INF32 && p < sLen[d]) {
-          const int32_t* row = FSS + rowoff(t, d, p) + 4 * q;
-          if (N == NPC) vals[m] = *(const int4*)row;
-          else {
-            vals[m].x = (4 * q + 0 < N) ? row[0] : INF32;
-            vals[m].y = (4 * q + 1 < N) ? row[1] : INF32;
-            vals[m].z = (4 * q + 2 < N) ? row[2] : INF32;
-            vals[m].w = (4 * q + 3 < N) ? row[3] : INF32;
-          }
+      const int item = tid + m * 1024;
+      const int d = item / (B * (NPC / 4));
+      const int rem = item - d * (B * (NPC / 4));
+      const int k = rem / (NPC / 4), q4 = rem - k * (NPC / 4);
+      int4 w = make_int4(INF32, INF32, INF32, INF32);
+      if (item < ITEMS && d < N && sP[d] != INF32 && sP[d] + k < sLen[d]) {
+        const int32_t* row = FSS + rowoff(t, d, sP[d] + k) + 4 * q4;
+        if ((N & 3) == 0) {
+          if (4 * q4 < N) w = *(const int4*)row;
+        } else {
+          if (4 * q4 + 0 < N) w.x = row[0];
+          if (4 * q4 + 1 < N) w.y = row[1];
+          if (4 * q4 + 2 < N) w.z = row[2];
+          if (4 * q4 + 3 < N) w.w = row[3];
         }
       }
+      vals[m] = w;
     }
 #pragma unroll
     for (int m = 0; m < PER; m++) {
-      const int item = tid + m * T;
-      if (item < ITEMS) blk[item] = vals[m];
+      const int item = tid + m * 1024;
+      if (item >= ITEMS) break;
+      const int d = item / (B * (NPC / 4));
+      const int rem = item - d * (B * (NPC / 4));
+      const int k = rem / (NPC / 4), q4 = rem - k * (NPC / 4);
+      const int4 w = vals[m];
+      const uint32_t lo = (uint32_t)(w.x == INF32 ? 0xFFFF : w.x) |
+                          ((uint32_t)(w.y == INF32 ? 0xFFFF : w.y) << 16);
+      const uint32_t hi = (uint32_t)(w.z == INF32 ? 0xFFFF : w.z) |
+                          ((uint32_t)(w.w == INF32 ? 0xFFFF : w.w) << 16);
+      *(uint2*)&blk[(d * B + k) * NPC + 4 * q4] = make_uint2(lo, hi);
     }
+    // the next RB rounds' C rows as stored before this kernel (rows < Rprev)
+    for (int item = tid; item < RB * NPC; item += T) {
+      const int q = item / NPC, c = item - q * NPC;
+      const int rr = r0 + 1 + q;
+      sC[item] = (c < N && rr < Rprev && rr < t.Rcap) ? t.C[(size_t)rr * N + c] : INF32;
+    }
+    if (tid < NPC) sBase[tid] = sP[tid];
     __syncthreads();
-    // ---- wave 0 walks rounds from LDS
+    // ---- wave 0 walks from LDS only
     if (tid < 64) {
-      const int c = tid;
+      const int lane = tid;
+      const int c = lane / LPC, q = lane - (lane / LPC) * LPC;
       const bool act = c < N;
-      int P = act ? sP[c] : INF32;
-      const int base = act ? sBase[c] : 0;
-      const int ln = act ? sLen[c] : 0;
-      int r = s_r;
+      const int ln = sLen[c];
+      const int base_c = sBase[c];
+      int bd[VPL];
+#pragma unroll
+      for (int k = 0; k < VPL; k++) bd[k] = sBase[q * VPL + k];
+      int r = r0;
       bool done = false;
-      for (;; r++) {
-        const bool out = act && P != INF32 && P - base >= B;
-        if (__ballot(out)) break;  // restage
+      for (;;) {
         if (r + 1 >= t.Rcap) {
-          if (c == 0) rstate[1] = 1;
+          if (lane == 0) rstate[1] = 1;
           done = true;
           break;
         }
-        int v[NPC];
+        if (r - r0 >= RB) break;  // C buffer full
+        const int Pc = sP[c];
+        if (__ballot(act && Pc != INF32 && Pc - base_c >= B)) break;  // leave the block
+        // branch-free gathers: all VPL LDS reads issue back to back
+        int Pv[VPL], v[VPL];
 #pragma unroll
-        for (int d = 0; d < NPC; d++) {
-          const int Pd = __builtin_amdgcn_readlane(P, d);
-          const int bd = __builtin_amdgcn_readlane(base, d);
-          const int* row = (const int*)&blk[(d * B + (Pd != INF32 ? Pd - bd : 0)) * Q];
-          v[d] = (act && d < N && Pd != INF32) ? row[c] : INF32;
+        for (int k = 0; k < VPL; k++) Pv[k] = sP[q * VPL + k];
+#pragma unroll
+        for (int k = 0; k < VPL; k++) {
+          const int d = q * VPL + k;
+          const int off = (Pv[k] != INF32) ? Pv[k] - bd[k] : 0;
+          v[k] = blk[(d * B + off) * NPC + c];
         }
-        const int cur = (act && r + 1 < Rprev) ? t.C[(size_t)(r + 1) * N + c] : INF32;
+#pragma unroll
+        for (int k = 0; k < VPL; k++) {
+          const int d = q * VPL + k;
+          int x = (Pv[k] == INF32 || v[k] == 0xFFFF) ? INF32 : v[k];
+          if (d == c && Pc != INF32) x = max(x, Pc + 1);  // x never strongly sees itself
+          v[k] = x;
+        }
+        // bitonic sort of the NPC values of chain c over its LPC lanes
+#pragma unroll
+        for (int size = 2; size <= NPC; size <<= 1) {
+#pragma unroll
+          for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride < VPL) {
+#pragma unroll
+              for (int k = 0; k < VPL; k++) {
+                const int k2 = k ^ stride;
+                if (k2 > k) {
+                  const bool up = (((q * VPL + k) & size) == 0);
+                  const int a = v[k], b = v[k2];
+                  v[k] = up ? min(a, b) : max(a, b);
+                  v[k2] = up ? max(a, b) : min(a, b);
+                }
+              }
+            } else {
+              const int ls = stride / VPL;  // lane distance: 1 or 2
+              const bool lower = ((q & ls) == 0);
+#pragma unroll
+              for (int k = 0; k < VPL; k++) {
+                const int o = (ls == 1) ? dpp_xor<1>(v[k]) : dpp_xor<2>(v[k]);
+                const bool up = (((q * VPL + k) & size) == 0);
+                v[k] = (lower == up) ? min(v[k], o) : max(v[k], o);
+              }
+            }
+          }
+        }
+        const int qo = (SM - 1) / VPL, ko = (SM - 1) - qo * VPL;
+        int sel = v[0];
+#pragma unroll
+        for (int k = 1; k < VPL; k++) sel = (k == ko) ? v[k] : sel;
+        const bool owner = act && q == qo;
         int nxt = INF32;
-        if (act && P != INF32) {
-#pragma unroll
-          for (int d = 0; d < NPC; d++)
-            if (d == c) v[d] = max(v[d], P + 1);
-          const int sel = select_kth<NPC>(v, SM);
+        if (owner && Pc != INF32) {
+          const int cur = sC[(r - r0) * NPC + c];
           nxt = cur != INF32 ? cur : (sel < ln ? sel : INF32);
-          if (cur == INF32 && nxt != INF32) t.C[(size_t)(r + 1) * N + c] = nxt;
         }
-        const uint64_t any = __ballot(act && nxt != INF32);
-        P = nxt;
-        if (!any) {
+        if (owner) {
+          sP[c] = nxt;
+          sC[(r - r0) * NPC + c] = nxt;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (!__ballot(owner && nxt != INF32)) {
           done = true;
           break;
         }
+        r++;
       }
-      if (c < NPC) sP[c] = P;
-      if (c == 0) {
+      if (lane == 0) {
+        s_nr = r - r0 + (done ? 1 : 0);  // C rows r0+1 .. r0+s_nr were produced
         s_r = r;
         s_done = done;
         if (done && !rstate[1]) rstate[0] = max(rstate[0], r + 1);
       }
     }
     __syncthreads();
-    if (s_done) break;
+    // ---- flush the walked C rows (rows < Rprev are rewritten with their own values)
+    const int nr = min(s_nr, RB);
+    for (int item = tid; item < nr * NPC; item += T) {
+      const int qq = item / NPC, c = item - qq * NPC;
+      const int v = sC[item];
+      if (c < N && v != INF32) t.C[(size_t)(r0 + 1 + qq) * N + c] = v;
+    }
+    const bool fin = s_done;
+    __syncthreads();
+    if (fin) break;
   }
 }
-
 // frontier start: r_lo and the first position per chain that can be a member
 __global__ void k_frontier_start(Tables t, const int32_t* olen, const int32_t* len,
                                  int32_t* out /* [0] rlo, [1..N] start positions */) {
