@@ -31,6 +31,11 @@ CASES = [
     ("gossip_n4_e1000_oneshot", 4, 1000, 1000, 1, 0, 0.0),
     ("gossip_n16_e3000_k16", 16, 3000, 16, 2, 0, 0.0),
     ("gossip_n32_e2000_k32_forks", 32, 2000, 32, 3, 10, 0.05),
+    # wide hashgraphs (N > 32: sweep coordinates + cooperative rounds); the
+    # oracle takes 5-40 s on these, so the GPU tests compare against the file
+    ("wide_n64_e8000_k64", 64, 8000, 64, 6, 0, 0.0),
+    ("wide_n128_e15000_k128", 128, 15000, 128, 5, 0, 0.0),
+    ("wide_n256_e25000_k256", 256, 25000, 256, 5, 0, 0.0),
 ]
 
 
@@ -56,8 +61,10 @@ def describe(o, dag, status, order, counts, calls):
                                  np.int64))
 
 
-def main():
+def main(only=None):
     for name, n, events, k, seed, fk, fp in CASES:
+        if only and only not in name:
+            continue
         dag = random_gossip(n, events, seed=seed, forkers=fk, fork_p=fp)
         calls = schedule(len(dag["creator"]), k)
         o, status, order, counts = replay(dag, calls)
@@ -65,6 +72,8 @@ def main():
         stream = {k2: dag[k2] for k2 in ("creator", "index", "sp", "op", "ts", "S", "hash", "ntx")}
         np.savez_compressed(os.path.join(HERE, name + ".npz"), n=np.int32(n), **stream, **out)
         print(name, "ordered", len(order), "rounds", out["scalars"][0])
+    if only:
+        return
     # reference hand DAGs: names, expected results (by name)
     ref = {}
     for nm, dag in (("small", SMALL_DAG), ("round", ROUND_DAG), ("consensus", CONSENSUS_DAG)):
@@ -83,4 +92,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else None)
