@@ -150,6 +150,8 @@ struct hge_engine {
   bool wide = false;
   int n_sweeps = 0;
   DBuf<int32_t> d_LAT, d_FDT, s_chg, s_plo, s_bar;
+  DBuf<uint64_t> d_ssc, s_gran;
+  DBuf<int32_t> s_bseg;
   bool coop_checked = false;
   DBuf<int2> s_segs;
 
@@ -315,7 +317,7 @@ struct hge_engine {
                              &s_basis, &s_bcount, &s_boff, &s_BR, &s_small, &s_len, &s_newwit,
                              &s_Rc, &s_Lc, &s_LCR, &s_pr, &s_clast, &s_flags, &s_segcnt,
                              &s_segoff, &s_segcall, &s_seground, &s_theta, &s_prindex, &s_recv,
-                             &s_rr, &s_frecv, &s_fund, &s_rank, &s_upos, &s_und2, &s_ids, &s_part, &s_arr, &s_fst, &s_fsslo, &d_FSS, &d_LAT, &d_FDT, &s_chg, &s_plo, &s_bar,
+                             &s_rr, &s_frecv, &s_fund, &s_rank, &s_upos, &s_und2, &s_ids, &s_part, &s_arr, &s_fst, &s_fsslo, &d_FSS, &d_LAT, &d_FDT, &s_chg, &s_plo, &s_bar, &s_bseg,
                              &s_ccount};
     for (auto* b : i32s) b->free_();
     d_ts.free_();
@@ -337,6 +339,8 @@ struct hge_engine {
     s_keys2.free_();
     s_ntx.free_();
     s_segs.free_();
+    d_ssc.free_();
+    s_gran.free_();
     if (st) (void)hipStreamDestroy(st);
     st = nullptr;
   }
@@ -406,6 +410,7 @@ struct hge_engine {
     d_W.grow_keep(nr * N, oldn, st, 0xFF);
     d_ssb.grow_keep(nr * N * NW, oldn * NW, st, 0);
     d_seeb.grow_keep(nr * N * NW, oldn * NW, st, 0);
+    if (wide) d_ssc.grow_keep(nr * N * NW, oldn * NW, st, 0);
     d_fame.grow_keep(nr * N, oldn, st, 0);
     d_rcnt.grow_keep(nr, Rcap, st, 0);
     d_minw.need(nr);
@@ -627,7 +632,7 @@ struct hge_engine {
     KLAUNCH(k_round_assign, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0,
                        (int)n1, R, s_newwit.p, s_small.p + 4);
     KLAUNCH(k_witness_bits, dim3(div_up((int64_t)m * N, 256)), dim3(256), 0, st, t, s_newwit.p,
-            s_small.p + 4);
+            s_small.p + 4, (wide && N > 32) ? (const uint64_t*)d_ssc.p : nullptr);
     KLAUNCH(k_round_minw, dim3(div_up(R, 256)), dim3(256), 0, st, t, 0, R, d_minw.p);
     n_coords = n1;
     coords_len = chain_len;
@@ -652,21 +657,30 @@ struct hge_engine {
         throw EngineError(HGE_ERR_DEVICE, "cooperative rounds kernel cannot be co-resident");
       coop_checked = true;
     }
+    int maxlen = 0;
+    for (int c = 0; c < N; c++) maxlen = std::max(maxlen, chain_len[c]);
+    if (maxlen >= 0xFFFF)
+      throw EngineError(HGE_ERR_CAPACITY, "wide rounds: chain longer than 65534 events");
     s_bar.need(2);
+    s_gran.need(2 * (size_t)N);
     HIPCHK(hipMemsetAsync(s_bar.p, 0, 8, st));
+    HIPCHK(hipMemsetAsync(s_gran.p, 0, 16 * (size_t)N, st));
     const int32_t* FDT = d_FDT.p;
     const int32_t* olen = s_len.p;
     const int32_t* len = s_len.p + N;
     int32_t* rstate = s_small.p;
-    unsigned* bar = (unsigned*)s_bar.p;
+    uint64_t* gran = s_gran.p;
     int32_t* err = s_bar.p + 1;
-    void* args[] = {&t, &FDT, &olen, &len, &rstate, &rlo, &Rprev, &bar, &err};
+    uint64_t* ssc = d_ssc.p;
+    uint64_t* dbg = dbg_p();
+    void* args[] = {&t, &FDT, &olen, &len, &rstate, &rlo, &Rprev, &gran, &err, &ssc, &dbg};
     prof_begin("k_rounds_coop");
     HIPCHK(hipLaunchCooperativeKernel((const void*)k_rounds_coop, dim3(N), dim3(256), args, 0, st));
     prof_end();
     int32_t e = 0;
     readback(&e, s_bar.p + 1, 1);
-    if (e) throw EngineError(HGE_ERR_DEVICE, "rounds grid barrier timed out");
+    if (e) throw EngineError(HGE_ERR_DEVICE, "rounds frontier hand-off timed out");
+    dbg_dump();
   }
 
   // chunked coordinate pipeline (N <= 32): DESIGN.md §4.1
@@ -1106,13 +1120,23 @@ struct hge_engine {
 
   void recv_dispatch(const Tables& t, const int32_t* cand, int ncand, int ncalls, int rr_lo,
                      int R_last) {
+    // N > 16: the median is a wave-wide radix select (k_median_wave)
+    const bool wmed = N > 16;
+    int32_t* bseg = nullptr;
+    if (wmed) {
+      s_bseg.need(ncand);
+      bseg = s_bseg.p;
+    }
     switch (NW) {
 #define RCASE(B)                                                                                 \
   case B:                                                                                        \
     KLAUNCH(k_round_received<B>, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, \
                        ncand, s_nc.p, ncalls, 0, rr_lo, R_last, s_segoff.p, s_segcnt.p,          \
                        s_segcall.p, s_segdec.p, s_segfws.p, s_theta.p, s_recv.p, s_rr.p,         \
-                       s_cts.p);                                                                 \
+                       s_cts.p, bseg);                                                           \
+    if (wmed)                                                                                    \
+      KLAUNCH(k_median_wave<B>, dim3(div_up(ncand, 4)), dim3(256), 0, st, t, cand, ncand,        \
+              s_recv.p, s_rr.p, bseg, s_segfws.p, s_cts.p);                                      \
     break;
       RCASE(1)
       RCASE(2)

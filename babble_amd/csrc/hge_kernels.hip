@@ -1157,7 +1157,9 @@ __global__ void k_calls_rounds(const int64_t* nc, int ncalls, const int32_t* min
 
 // strongly-see / see bitsets of each new witness y (round j >= 1) over the
 // slots of round j-1: StronglySee (hashgraph.go:189-208), See (:149-154)
-__global__ void k_witness_bits(Tables t, const int32_t* newwit, const int32_t* pnnew) {
+// ssc (wide path): strongly-see bits already produced by k_rounds_coop
+__global__ void k_witness_bits(Tables t, const int32_t* newwit, const int32_t* pnnew,
+                               const uint64_t* ssc) {
   const int item = blockIdx.x * blockDim.x + threadIdx.x;
   const int N = t.N, NW = t.NW;
   const int nnew = *pnnew;
@@ -1173,7 +1175,11 @@ __global__ void k_witness_bits(Tables t, const int32_t* newwit, const int32_t* p
   const int32_t* fd = t.FD + rowoff(t, d, t.index[w]);
   const bool see = la[d] >= t.index[w];
   int c = 0;
-  for (int i = 0; i < N; i++) c += (la[i] >= fd[i]) ? 1 : 0;
+  if (ssc) {
+    c = ((ssc[((size_t)j * N + cy) * NW + (d >> 6)] >> (d & 63)) & 1ull) ? t.SM : 0;
+  } else {
+    for (int i = 0; i < N; i++) c += (la[i] >= fd[i]) ? 1 : 0;
+  }
   const size_t off = ((size_t)j * N + cy) * NW + (d >> 6);
   const uint64_t bit = 1ull << (d & 63);
   if (see) atomicOr((unsigned long long*)&t.seeb[off], (unsigned long long)bit);
@@ -1562,7 +1568,8 @@ __global__ void k_round_received(Tables t, const int32_t* cand, int ncand, const
                                  const int32_t* segoff, const int32_t* segcnt,
                                  const int32_t* seg_call, const uint8_t* seg_dec,
                                  const uint64_t* seg_fws, const int32_t* theta,
-                                 int32_t* recv_call, int32_t* rr_out, int64_t* cts_out) {
+                                 int32_t* recv_call, int32_t* rr_out, int64_t* cts_out,
+                                 int32_t* bseg_out) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= ncand) return;
   const int N = t.N;
@@ -1601,6 +1608,12 @@ __global__ void k_round_received(Tables t, const int32_t* cand, int ncand, const
   }
   if (rr < 0 || best >= ncalls) {
     recv_call[q] = -1;
+    return;
+  }
+  if (bseg_out) {  // wide: the median is taken by k_median_wave
+    recv_call[q] = best;
+    rr_out[q] = rr;
+    bseg_out[q] = bseg;
     return;
   }
   // median of the oldest-self-ancestor-to-see timestamps (OSA(w,x) = FD[x][cw])
@@ -1655,6 +1668,80 @@ __global__ void k_round_received(Tables t, const int32_t* cand, int ncand, const
   recv_call[q] = best;
   rr_out[q] = rr;
   cts_out[q] = med;
+}
+
+// MedianTimestamp (hashgraph.go:762-770) for wide hashgraphs: one wave per
+// received event.  Lane l holds the timestamps of the famous witnesses
+// d = l, l+64, ... that see x (OSA(w, x) = FD[x][cw]); the upper median
+// (element len/2 of the sorted list) is found by a bitwise radix select over
+// the order-preserving uint64 image of the int64 timestamps, skipping the
+// high bits every candidate shares.
+template <int VPL>
+__global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* cand, int ncand,
+                                                     const int32_t* recv_call, const int32_t* rr_in,
+                                                     const int32_t* bseg, const uint64_t* seg_fws,
+                                                     int64_t* cts_out) {
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (q >= ncand || recv_call[q] < 0) return;  // wave-uniform
+  const int N = t.N, NW = t.NW;
+  const int x = cand[q];
+  const int cx = t.creator[x], ix = t.index[x];
+  const int rr = rr_in[q], sg = bseg[q];
+  const int32_t* fdx = t.FD + rowoff(t, cx, ix);
+  uint64_t v[VPL];
+  bool in[VPL];
+#pragma unroll
+  for (int k = 0; k < VPL; k++) {
+    const int d = lane + 64 * k;
+    in[k] = false;
+    v[k] = ~0ull;
+    if (d < N && ((seg_fws[(size_t)sg * NW + (d >> 6)] >> (d & 63)) & 1ull)) {
+      const int w = t.W[(size_t)rr * N + d];
+      if (t.LA[rowoff(t, d, t.index[w]) + cx] >= ix) {
+        const int osa = t.chain[(size_t)d * t.ccap + fdx[d]];
+        v[k] = (uint64_t)t.ts[osa] ^ 0x8000000000000000ull;
+        in[k] = true;
+      }
+    }
+  }
+  int n = 0;
+  uint64_t mn = ~0ull, mx = 0;
+#pragma unroll
+  for (int k = 0; k < VPL; k++) {
+    n += __popcll(__ballot(in[k]));
+    if (in[k]) {
+      mn = min(mn, v[k]);
+      mx = max(mx, v[k]);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = min(mn, (uint64_t)__shfl_xor((long long)mn, o));
+    mx = max(mx, (uint64_t)__shfl_xor((long long)mx, o));
+  }
+  int kk = n / 2;  // 0-based rank of the upper median
+  uint64_t prefix = mn;
+  const uint64_t diff = mn ^ mx;
+  if (diff) {
+    const int top = 63 - __builtin_clzll(diff);
+    prefix = (mn >> (top + 1)) << (top + 1);  // shared high bits
+    bool live[VPL];
+#pragma unroll
+    for (int k = 0; k < VPL; k++) live[k] = in[k];
+    for (int b = top; b >= 0; b--) {
+      int c0 = 0;
+#pragma unroll
+      for (int k = 0; k < VPL; k++) c0 += __popcll(__ballot(live[k] && !((v[k] >> b) & 1ull)));
+      const bool one = kk >= c0;
+      if (one) {
+        kk -= c0;
+        prefix |= 1ull << b;
+      }
+#pragma unroll
+      for (int k = 0; k < VPL; k++) live[k] = live[k] && (((v[k] >> b) & 1ull) == (one ? 1ull : 0ull));
+    }
+  }
+  if (lane == 0) cts_out[q] = (int64_t)(prefix ^ 0x8000000000000000ull);
 }
 
 // ---------------------------------------------------------------------------
