@@ -21,7 +21,8 @@
 
 #include "../../include/hge.h"
 #include "hge_kernels.hip"
-#include "hge_wide.hip"
+#include "hge_coords.hip"
+#include "hge_rounds_coop.hip"
 
 using namespace hge;
 
@@ -91,7 +92,7 @@ static const int32_t kInf = INF32;
 }  // namespace
 
 struct hge_engine {
-  int N = 0, NW = 1, SM = 1, BW = 1;
+  int N = 0, NW = 1, SM = 1;
   int device = 0;
   hipStream_t st = nullptr;
   std::string err;
@@ -133,8 +134,7 @@ struct hge_engine {
   DBuf<uint64_t> d_ssb, d_seeb;
   DBuf<uint8_t> d_fame;
   // scratch
-  DBuf<int32_t> s_D, s_enc, s_basis, s_bcount, s_boff, s_BR, s_small, s_len, s_newwit;
-  DBuf<uint64_t> s_dep;
+  DBuf<int32_t> s_small, s_len, s_newwit;
   DBuf<int64_t> s_nc;
   DBuf<int32_t> s_Rc, s_Lc, s_LCR, s_pr, s_clast, s_flags;
   DBuf<uint8_t> s_dec, s_decbit;
@@ -146,8 +146,7 @@ struct hge_engine {
   DBuf<unsigned char> s_keys, s_keys2;
   DBuf<unsigned long long> s_ntx;
   DBuf<int32_t> s_part, s_arr, s_fst, s_fsslo;
-  // wide path (N > 32): transposed coordinate tables and sweep scratch
-  bool wide = false;
+  // coordinate sweeps: transposed tables and scratch
   int n_sweeps = 0;
   DBuf<int32_t> d_LAT, d_FDT, s_chg, s_plo, s_bar;
   DBuf<uint64_t> d_ssc, s_gran;
@@ -163,7 +162,6 @@ struct hge_engine {
   std::vector<std::string> prof_names;
   std::vector<double> prof_ms;
   std::vector<int64_t> prof_cnt;
-  bool br_in_lds = true;
   int R_div = 0;            // Rounds() as seen by the consensus calls (DivideRounds)
   float stage_ms[7] = {};
 
@@ -201,12 +199,6 @@ struct hge_engine {
     N = n;
     NW = (N + 63) / 64;
     SM = 2 * N / 3 + 1;  // hashgraph.go:78-80
-    wide = N > 32 || getenv("HGE_WIDE") != nullptr;
-    // external-basis capacity per chunk: >= every chain head + a margin of
-    // historical parents; chunks that overflow are re-run smaller.
-    int bmax = 2 * N + 64;
-    BW = 1;
-    while (BW * 64 < bmax) BW *= 2;
     device = dev;
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -214,7 +206,6 @@ struct hge_engine {
     chain_len.assign(N, 0);
     chain_last.assign(N, -1);
     coords_len.assign(N, 0);
-    set_lds_limits();
     ensure_events(std::max<int64_t>(cap, 1024));
     ensure_ccap(std::max<int64_t>(64, 2 * std::max<int64_t>(cap, 1024) / N + 64));
     ensure_rcap(std::max<int64_t>(64, std::max<int64_t>(cap, 1024) / SM + 8));
@@ -274,38 +265,6 @@ struct hge_engine {
     fprintf(stderr, "\n");
   }
 
-  void set_lds_limits() {
-    // best effort: gfx950 has 160 KiB of LDS per CU; kernels with static LDS
-    // get a smaller dynamic ceiling
-    const int lim = 152 * 1024;
-#define LDSATTR(f)                                                                            \
-  do {                                                                                        \
-    if (hipFuncSetAttribute((const void*)(f), hipFuncAttributeMaxDynamicSharedMemorySize, lim) != \
-        hipSuccess)                                                                           \
-      (void)hipGetLastError();                                                                \
-  } while (0)
-    LDSATTR(k_coord_local<1>);
-    LDSATTR(k_coord_local<2>);
-    LDSATTR(k_coord_local<4>);
-    LDSATTR(k_coord_local<8>);
-    LDSATTR(k_coord_local<16>);
-    LDSATTR(k_coord_basis<1>);
-    LDSATTR(k_coord_basis<2>);
-    LDSATTR(k_coord_basis<4>);
-    LDSATTR(k_coord_basis<8>);
-    LDSATTR(k_coord_basis<16>);
-    LDSATTR(k_coord_final<1>);
-    LDSATTR(k_coord_final<2>);
-    LDSATTR(k_coord_final<4>);
-    LDSATTR(k_coord_final<8>);
-    LDSATTR(k_coord_final<16>);
-    LDSATTR(k_rounds_frontier<16>);
-    LDSATTR(k_rounds_frontier<32>);
-    LDSATTR(k_rounds_frontier<64>);
-    LDSATTR(k_rounds_frontier<0>);
-#undef LDSATTR
-  }
-
   void destroy() {
     if (st) (void)hipStreamSynchronize(st);
     for (auto& e : ev)
@@ -313,8 +272,7 @@ struct hge_engine {
     for (auto& e : prof_pool) (void)hipEventDestroy(e);
     prof_pool.clear();
     DBuf<int32_t>* i32s[] = {&d_creator, &d_index, &d_sp, &d_op, &d_ntx, &d_round, &d_rr, &d_und,
-                             &d_chain, &d_LA, &d_FD, &d_C, &d_W, &d_rcnt, &d_minw, &s_D, &s_enc,
-                             &s_basis, &s_bcount, &s_boff, &s_BR, &s_small, &s_len, &s_newwit,
+                             &d_chain, &d_LA, &d_FD, &d_C, &d_W, &d_rcnt, &d_minw, &s_small, &s_len, &s_newwit,
                              &s_Rc, &s_Lc, &s_LCR, &s_pr, &s_clast, &s_flags, &s_segcnt,
                              &s_segoff, &s_segcall, &s_seground, &s_theta, &s_prindex, &s_recv,
                              &s_rr, &s_frecv, &s_fund, &s_rank, &s_upos, &s_und2, &s_ids, &s_part, &s_arr, &s_fst, &s_fsslo, &d_FSS, &d_LAT, &d_FDT, &s_chg, &s_plo, &s_bar, &s_bseg,
@@ -327,7 +285,6 @@ struct hge_engine {
     d_S.free_();
     d_ssb.free_();
     d_seeb.free_();
-    s_dep.free_();
     s_segfws.free_();
     d_coin.free_();
     d_wit.free_();
@@ -394,11 +351,9 @@ struct hge_engine {
     d_chain.n = (size_t)N * nc;
     grow_chain_table(d_LA, nc, true);
     grow_chain_table(d_FD, nc, true);
-    if (N <= 64) grow_chain_table(d_FSS, nc, true);  // first-strong-seer rows (rounds, N <= 64)
-    if (wide) {
-      grow_chain_table(d_LAT, nc, false, false);  // rebuilt per batch from LA
-      grow_chain_table(d_FDT, nc, true, false);   // persistent: FD in run layout
-    }
+    if (N <= 32) grow_chain_table(d_FSS, nc, true);  // first-strong-seer rows (walk, N <= 32)
+    grow_chain_table(d_LAT, nc, false, false);      // rebuilt per batch from LA
+    grow_chain_table(d_FDT, nc, true, false);       // persistent: FD in run layout
     ccap = (int)nc;
   }
 
@@ -410,7 +365,7 @@ struct hge_engine {
     d_W.grow_keep(nr * N, oldn, st, 0xFF);
     d_ssb.grow_keep(nr * N * NW, oldn * NW, st, 0);
     d_seeb.grow_keep(nr * N * NW, oldn * NW, st, 0);
-    if (wide) d_ssc.grow_keep(nr * N * NW, oldn * NW, st, 0);
+    if (N > 32) d_ssc.grow_keep(nr * N * NW, oldn * NW, st, 0);
     d_fame.grow_keep(nr * N, oldn, st, 0);
     d_rcnt.grow_keep(nr, Rcap, st, 0);
     d_minw.need(nr);
@@ -556,17 +511,16 @@ struct hge_engine {
     HIPCHK(hipMemcpyAsync(s_len.p, lens.data(), 8 * N, hipMemcpyHostToDevice, st));
     KLAUNCH(k_chain_fill, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0, (int)n1);
     s_small.need(8);
-    if (wide) coords_wide(t, m);
-    else coords_chunked(t, (int)n0, (int)n1, m);
+    coords_sweep(t);
     // rounds frontier
     for (;;) {
       int32_t rs[2] = {R, 0};
       HIPCHK(hipMemcpyAsync(s_small.p, rs, 8, hipMemcpyHostToDevice, st));
       t = tables();
       const int NP = (N + 15) & ~15;
-      if (wide && N > 32) {
+      if (N > 32) {
         rounds_coop();
-      } else if (NP <= 64 && !getenv("HGE_PROBE_FRONTIER")) {
+      } else {
         // first-strong-seer rows for every event that can still be a frontier member
         s_fst.need(N + 1);
         KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, s_len.p, s_len.p + N, s_fst.p);
@@ -588,35 +542,25 @@ struct hge_engine {
           int maxlen = 0;
           for (int c = 0; c < N; c++) maxlen = std::max(maxlen, chain_len[c]);
           if (tot > 0) {
-#define FSSL(NPC)                                                                                 \
-  KLAUNCH(k_fss<NPC>, dim3(div_up((int64_t)tot * NPC, 256)), dim3(256), 0, st, t, s_fsslo.p,      \
-          s_fsslo.p + N, tot, d_FSS.p);                                                           \
-  if (NPC == 16 && maxlen < 0xFFFF)                                                               \
-    KLAUNCH((k_rounds_walk<16, 4, 256>), dim3(1), dim3(1024), 0, st, t, d_FSS.p, s_len.p,         \
-            s_len.p + N, s_small.p, rlo, Rprev);                                                  \
-  else if (NPC == 32 && maxlen < 0xFFFF)                                                          \
-    KLAUNCH((k_rounds_walk<32, 2, 64>), dim3(1), dim3(1024), 0, st, t, d_FSS.p, s_len.p,          \
-            s_len.p + N, s_small.p, rlo, Rprev);                                                  \
-  else                                                                                            \
-    KLAUNCH(k_rounds_fss<NPC>, dim3(1), dim3(64), 0, st, t, d_FSS.p, s_len.p, s_len.p + N,       \
+            // the LDS walk keeps chain positions as uint16; longer chains take the
+            // register walk over the global fss rows
+#define FSSL(NPC, LPC, B)                                                                          \
+  KLAUNCH(k_fss<NPC>, dim3(div_up((int64_t)tot * NPC, 256)), dim3(256), 0, st, t, s_fsslo.p,       \
+          s_fsslo.p + N, tot, d_FSS.p);                                                            \
+  if (maxlen < 0xFFFF)                                                                             \
+    KLAUNCH((k_rounds_walk<NPC, LPC, B>), dim3(1), dim3(1024), 0, st, t, d_FSS.p, s_len.p,         \
+            s_len.p + N, s_small.p, rlo, Rprev);                                                   \
+  else                                                                                             \
+    KLAUNCH(k_rounds_fss<NPC>, dim3(1), dim3(64), 0, st, t, d_FSS.p, s_len.p, s_len.p + N,        \
             s_small.p, rlo);
-            if (NP == 16) { FSSL(16) } else if (NP == 32) { FSSL(32) } else { FSSL(64) }
+            if (NP == 16) {
+              FSSL(16, 4, 256)
+            } else {
+              FSSL(32, 2, 64)
+            }
 #undef FSSL
           }
         }
-      } else {
-        // probe window per chain: a few rounds' worth of a chain's events, bounded by LDS
-        int WIN = 16;
-        while (WIN > 2 && (size_t)N * WIN * NP * 4 > 96 * 1024) WIN /= 2;
-        const size_t lds = (size_t)(N * NP + N * WIN * NP + 8 * N + 2 * N * WIN) * 4 + 64;
-        if (NP == 16)
-          KLAUNCH(k_rounds_frontier<16>, dim3(1), dim3(1024), lds, st, t, s_len.p, s_len.p + N, s_small.p, WIN, dbg_p());
-        else if (NP == 32)
-          KLAUNCH(k_rounds_frontier<32>, dim3(1), dim3(1024), lds, st, t, s_len.p, s_len.p + N, s_small.p, WIN, dbg_p());
-        else if (NP == 64)
-          KLAUNCH(k_rounds_frontier<64>, dim3(1), dim3(1024), lds, st, t, s_len.p, s_len.p + N, s_small.p, WIN, dbg_p());
-        else
-          KLAUNCH(k_rounds_frontier<0>, dim3(1), dim3(1024), lds, st, t, s_len.p, s_len.p + N, s_small.p, WIN, dbg_p());
       }
       readback(rs, s_small.p, 2);
       if (rs[1]) {
@@ -632,14 +576,14 @@ struct hge_engine {
     KLAUNCH(k_round_assign, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0,
                        (int)n1, R, s_newwit.p, s_small.p + 4);
     KLAUNCH(k_witness_bits, dim3(div_up((int64_t)m * N, 256)), dim3(256), 0, st, t, s_newwit.p,
-            s_small.p + 4, (wide && N > 32) ? (const uint64_t*)d_ssc.p : nullptr);
+            s_small.p + 4, N > 32 ? (const uint64_t*)d_ssc.p : nullptr);
     KLAUNCH(k_round_minw, dim3(div_up(R, 256)), dim3(256), 0, st, t, 0, R, d_minw.p);
     n_coords = n1;
     coords_len = chain_len;
     prof_collect();
   }
 
-  // rounds of a wide hashgraph: cooperative frontier kernel (hge_wide.hip)
+  // rounds of a wide hashgraph: cooperative frontier kernel (hge_rounds_coop.hip)
   void rounds_coop() {
     Tables t = tables();
     s_fst.need(N + 1);
@@ -683,48 +627,8 @@ struct hge_engine {
     dbg_dump();
   }
 
-  // chunked coordinate pipeline (N <= 32): DESIGN.md §4.1
-  void coords_chunked(Tables t, int n0, int n1, int m) {
-    // chunk length: LDS of phase A = L*(BW*8 + N*4 + 32) + BMAX*4 + ~1KB
-    const int BMAX = BW * 64;
-    int L = 1024;
-    if (getenv("HGE_CHUNK")) L = atoi(getenv("HGE_CHUNK"));
-    while (L > 64 && (size_t)(L + 1) * (BW * 8 + N * 4 + 32) + BMAX * 4 + 2048 + N * 4 > 150 * 1024) L /= 2;
-    for (;;) {
-      const int nch = div_up(m, L);
-      s_D.need((size_t)m * N);
-      s_dep.need((size_t)m * BW);
-      s_enc.need((size_t)2 * m);
-      const int RECW = 2 * BMAX + N + N * N + 2 * N * BW + 1;
-      s_basis.need((size_t)nch * RECW);
-      s_bcount.need(nch);
-      s_boff.need(nch);
-      s_small.need(8);
-      HIPCHK(hipMemsetAsync(s_small.p, 0, 8 * 4, st));
-      const size_t ldsA = (size_t)(L + 1) * (N + 2 * BW) * 4 + (size_t)L * 4 * 4 +
-                          (size_t)2 * L * 4 * 2 + (size_t)BMAX * 4 + (256 + 1) * 4 + N * 4;
-      launch_bw(0, nch, ldsA, t, n0, n1, L, nch);
-      KLAUNCH(k_scan_small, dim3(1), dim3(1024), 0, st, s_bcount.p, s_boff.p, nch, s_small.p + 2);
-      int32_t fl3[3];
-      readback(fl3, s_small.p, 3);
-      if (fl3[0] && L > 16) {
-        L /= 2;
-        continue;
-      }
-      if (fl3[0]) throw EngineError(HGE_ERR_INTERNAL, "external basis overflow");
-      const int32_t total = fl3[2];
-      s_BR.need((size_t)std::max(total, 1) * N);
-      const size_t ldsB = ((size_t)N * N + (size_t)BMAX * N + 2 * (size_t)RECW) * 4;
-      launch_bw(1, nch, ldsB, t, n0, n1, L, nch);
-      br_in_lds = (size_t)BMAX * N * 4 + (size_t)L * N * 4 <= 150 * 1024;
-      const size_t ldsC = (size_t)L * N * 4 + (br_in_lds ? (size_t)BMAX * N * 4 : 0);
-      launch_bw(2, nch, ldsC, t, n0, n1, L, nch);
-      break;
-    }
-  }
-
-  // wide coordinate pipeline (N > 32): chain-prefix sweeps + transposes (hge_wide.hip)
-  void coords_wide(Tables t, int m) {
+  // coordinates: chain-prefix sweeps + transposes (hge_coords.hip)
+  void coords_sweep(Tables t) {
     const int32_t* olen = s_len.p;
     const int32_t* len = s_len.p + N;
     int maxnew = 0, maxlen = 0;
@@ -788,34 +692,7 @@ struct hge_engine {
     for (int c = 0; c < N; c++) span = std::max(span, chain_len[c] - qlo[c]);
     KLAUNCH(k_transpose, dim3(div_up(span, 64), div_up(N, 64), N), dim3(256), 0, st, t, d_FDT.p,
             (int32_t*)nullptr, s_plo.p + N, len, 1);
-    (void)m;
     (void)maxlen;
-  }
-
-  void launch_bw(int which, int nch, size_t lds, const Tables& t, int n0, int n1, int L, int nch2) {
-    switch (BW) {
-#define CASE(B)                                                                                  \
-  case B:                                                                                        \
-    if (which == 0) {                                                                            \
-      KLAUNCH(k_coord_local<B>, dim3(nch), dim3(256), lds, st, t, n0, n1, L, s_D.p,  \
-                         s_dep.p, s_enc.p, s_basis.p, s_bcount.p, s_small.p);                    \
-    } else if (which == 1) {                                                                     \
-      KLAUNCH(k_coord_basis<B>, dim3(1), dim3(1024), lds, st, t, n0, L, nch2, s_D.p,  \
-                         s_dep.p, s_basis.p, s_boff.p, s_len.p, s_BR.p);                         \
-    } else {                                                                                     \
-      KLAUNCH(k_coord_final<B>, dim3(nch), dim3(256), lds, st, t, n0, n1, L, s_D.p,  \
-                         s_dep.p, s_enc.p, s_bcount.p, s_boff.p, s_BR.p, br_in_lds ? 1 : 0);     \
-    }                                                                                            \
-    break;
-      CASE(1)
-      CASE(2)
-      CASE(4)
-      CASE(8)
-      CASE(16)
-#undef CASE
-      default:
-        throw EngineError(HGE_ERR_INTERNAL, "unsupported basis width");
-    }
   }
 
   // ---------------- one batch of consensus calls ----------------

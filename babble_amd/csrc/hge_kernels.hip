@@ -51,41 +51,6 @@ __device__ __forceinline__ size_t rowoff(const Tables& t, int c, int p) {
   return ((size_t)c * t.ccap + p) * (size_t)t.N;
 }
 
-template <typename T>
-__device__ __forceinline__ T ntload(const T* p) {
-  return __builtin_nontemporal_load(p);
-}
-
-__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// ---------------------------------------------------------------------------
-// block-wide exclusive scan over `n` ints in LDS (n <= 8 * blockDim.x)
-// ---------------------------------------------------------------------------
-__device__ int block_exclusive_scan(int* a, int n, int* tmp /* blockDim.x + 1 */) {
-  const int T = blockDim.x, tid = threadIdx.x;
-  const int per = (n + T - 1) / T;
-  const int lo = min(n, tid * per), hi = min(n, lo + per);
-  int s = 0;
-  for (int i = lo; i < hi; i++) s += a[i];
-  tmp[tid] = s;
-  __syncthreads();
-  for (int off = 1; off < T; off <<= 1) {
-    const int add = (tid >= off) ? tmp[tid - off] : 0;
-    __syncthreads();
-    tmp[tid] += add;
-    __syncthreads();
-  }
-  const int total = tmp[T - 1];
-  int run = tmp[tid] - s;
-  for (int i = lo; i < hi; i++) {
-    int v = a[i];
-    a[i] = run;
-    run += v;
-  }
-  __syncthreads();
-  return total;
-}
-
 __global__ void k_fill_i32(int32_t* p, int64_t n, int32_t v) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = v;
@@ -103,211 +68,6 @@ __global__ void k_min_round(const int32_t* round, const int32_t* cand, int n, in
   if (i < n) v = round[cand[i]];
   for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
   if ((threadIdx.x & 63) == 0 && v != INF32) atomicMin(out, v);
-}
-
-// ---------------------------------------------------------------------------
-// Coordinates, phase A: one workgroup per chunk of L consecutive new events.
-// Computes, by one sequential pass in LDS, for every event of the chunk
-//   D[x]   = max own-index contributions of in-chunk ancestors (row of N)
-//   dep[x] = bitset over the chunk's external basis (distinct parents that
-//            precede the chunk) reachable from x inside the chunk,
-// so that lastAncestors(x) = max(D[x], max_{b in dep[x]} LA[basis b])
-// (InitEventCoordinates, hashgraph.go:399-463, unrolled over the chunk).
-// Also initialises the new events' FD rows to INF32 (hashgraph.go:402-407).
-// ---------------------------------------------------------------------------
-template <int BW>
-__global__ void __launch_bounds__(256) k_coord_local(Tables t, int n0, int n1, int L,
-                                                      int32_t* Dbuf, uint64_t* depbuf,
-                                                      int32_t* enc, int32_t* basis,
-                                                      int32_t* bcount, int* overflow) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int BMAX = BW * 64;
-  const int N = t.N;
-  const int k = blockIdx.x;
-  const int s = n0 + k * L;
-  const int e = min(n1, s + L);
-  const int cnt = e - s;
-  const int tid = threadIdx.x;
-  const int T = blockDim.x;
-
-  int32_t* sRow = (int32_t*)smem;                   // (L + 1) * (N + 2*BW)
-  int32_t* ssp = sRow + (size_t)(L + 1) * (N + 2 * BW);  // L
-  int32_t* sop = ssp + L;                           // L
-  int32_t* scr = sop + L;                           // L
-  int32_t* sidx = scr + L;                          // L
-  int32_t* sext = sidx + L;                         // 2L (sorted externals)
-  int32_t* sflag = sext + 2 * L;                    // 2L
-  int32_t* sbas = sflag + 2 * L;                    // BMAX
-  int32_t* stmp = sbas + BMAX;                      // T + 1
-  int32_t* sExit = stmp + T + 1;                    // N
-
-  const int M = 2 * L;
-  for (int i = tid; i < L; i += T) {
-    int x = s + i;
-    int p0 = -1, p1 = -1, cr = 0, ix = 0;
-    if (i < cnt) {
-      p0 = t.sp[x];
-      p1 = t.op[x];
-      cr = t.creator[x];
-      ix = t.index[x];
-      int32_t* fdr = t.FD + rowoff(t, cr, ix);
-      for (int c = 0; c < N; c++) fdr[c] = INF32;
-    }
-    ssp[i] = p0;
-    sop[i] = p1;
-    scr[i] = cr;
-    sidx[i] = ix;
-    sext[2 * i] = (p0 >= 0 && p0 < s) ? p0 : INF32;
-    sext[2 * i + 1] = (p1 >= 0 && p1 < s) ? p1 : INF32;
-  }
-  __syncthreads();
-  // bitonic sort of the 2L external candidates (M is a power of two)
-  for (int size = 2; size <= M; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = tid; i < M / 2; i += T) {
-        int lo = 2 * stride * (i / stride) + (i % stride);
-        int hi = lo + stride;
-        bool up = ((lo & size) == 0);
-        int a = sext[lo], b = sext[hi];
-        if ((a > b) == up) {
-          sext[lo] = b;
-          sext[hi] = a;
-        }
-      }
-      __syncthreads();
-    }
-  }
-  for (int i = tid; i < M; i += T) {
-    int v = sext[i];
-    sflag[i] = (v != INF32 && (i == 0 || sext[i - 1] != v)) ? 1 : 0;
-  }
-  __syncthreads();
-  // keep the flags (scan overwrites): rank = exclusive prefix
-  const int nb = block_exclusive_scan(sflag, M, stmp);
-  if (nb > BMAX) {
-    if (tid == 0) atomicOr(overflow, 1);
-    return;
-  }
-  for (int i = tid; i < M; i += T) {
-    int v = sext[i];
-    int r = sflag[i];
-    int nxt = (i + 1 < M) ? sflag[i + 1] : nb;
-    if (v != INF32 && nxt != r) sbas[r] = v;  // first occurrence
-  }
-  __syncthreads();
-  // record layout (RECW ints): [basis ids BMAX | head kinds BMAX | exits N |
-  //  exit D rows N*N | exit dep words N*2BW | nb]
-  const int RECW = 2 * BMAX + N + N * N + 2 * N * BW + 1;
-  int32_t* rec = basis + (size_t)k * RECW;
-  for (int i = tid; i < nb; i += T) rec[i] = sbas[i];
-  if (tid == 0) {
-    bcount[k] = nb;
-    rec[RECW - 1] = nb;
-  }
-  // encode parents: >= 0 local offset, -1 none, -(2 + b) basis slot b
-  for (int i = tid; i < cnt; i += T) {
-    int pr[2] = {ssp[i], sop[i]};
-    for (int q = 0; q < 2; q++) {
-      int p = pr[q];
-      int code;
-      if (p < 0) code = -1;
-      else if (p >= s) code = p - s;
-      else {
-        int lo = 0, hi = nb - 1;
-        while (lo < hi) {
-          int mid = (lo + hi) >> 1;
-          if (sbas[mid] < p) lo = mid + 1;
-          else hi = mid;
-        }
-        code = -(2 + lo);
-      }
-      pr[q] = code;
-    }
-    ssp[i] = pr[0];
-    sop[i] = pr[1];
-    enc[2 * (size_t)(s - n0 + i)] = pr[0];
-    enc[2 * (size_t)(s - n0 + i) + 1] = pr[1];
-  }
-  __syncthreads();
-  // sequential in-chunk propagation: one wave.  Row i of sRow = [D (N int32) |
-  // dep (2*BW uint32)]; row L is the all-"none" row used for absent parents,
-  // so every step is one pair of independent LDS loads and one store.  Parent
-  // codes of 64 steps sit in registers (one step per lane) and are broadcast
-  // with v_readlane.
-  if (tid < 64) {
-    const int lane = tid;
-    const int RW = N + 2 * BW;
-    for (int col = lane; col < RW; col += 64) sRow[L * RW + col] = (col < N) ? -1 : 0;
-    for (int b0 = 0; b0 < cnt; b0 += 64) {
-      int msp = -1, mop = -1, mcx = 0, mix = 0;
-      if (b0 + lane < cnt) {
-        msp = ssp[b0 + lane];
-        mop = sop[b0 + lane];
-        mcx = scr[b0 + lane];
-        mix = sidx[b0 + lane];
-      }
-      const int nb = min(64, cnt - b0);
-      for (int j = 0; j < nb; j++) {
-        const int psp = __builtin_amdgcn_readlane(msp, j);
-        const int pop = __builtin_amdgcn_readlane(mop, j);
-        const int cx = __builtin_amdgcn_readlane(mcx, j);
-        const int ix = __builtin_amdgcn_readlane(mix, j);
-        const int ra = (psp >= 0 ? psp : L) * RW;
-        const int rb = (pop >= 0 ? pop : L) * RW;
-        const int bsp = psp <= -2 ? -psp - 2 : -1;  // external basis slots
-        const int bop = pop <= -2 ? -pop - 2 : -1;
-        int* dst = sRow + (b0 + j) * RW;
-        for (int col = lane; col < RW; col += 64) {
-          const int va = sRow[ra + col], vb = sRow[rb + col];
-          int v;
-          if (col < N) {
-            v = (col == cx) ? ix : max(va, vb);
-          } else {
-            const int w = col - N;  // 32-bit dep word
-            v = va | vb;
-            if (bsp >= 0 && (bsp >> 5) == w) v |= 1 << (bsp & 31);
-            if (bop >= 0 && (bop >> 5) == w) v |= 1 << (bop & 31);
-          }
-          dst[col] = v;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  const size_t base = (size_t)(s - n0);
-  const int RW = N + 2 * BW;
-  for (int item = tid; item < cnt * N; item += T) {
-    const int i = item / N, c = item - (item / N) * N;
-    Dbuf[base * N + item] = sRow[i * RW + c];
-  }
-  uint32_t* dep32 = (uint32_t*)depbuf;
-  for (int item = tid; item < cnt * 2 * BW; item += T) {
-    const int i = item / (2 * BW), w = item - (item / (2 * BW)) * (2 * BW);
-    dep32[base * 2 * BW + item] = (uint32_t)sRow[i * RW + N + w];
-  }
-  // per-chain exits (last event of each chain in the chunk) and head flags of
-  // the basis: consumed by phase B's head-table fast path
-  for (int c = tid; c < N; c += T) sExit[c] = -1;
-  __syncthreads();
-  for (int i = tid; i < cnt; i += T) atomicMax(&sExit[scr[i]], i);
-  __syncthreads();
-  for (int c = tid; c < N; c += T) rec[2 * BMAX + c] = sExit[c] >= 0 ? s + sExit[c] : -1;
-  for (int item = tid; item < N * N; item += T) {
-    const int c = item / N, i = item - (item / N) * N;
-    rec[2 * BMAX + N + item] = sExit[c] >= 0 ? sRow[sExit[c] * RW + i] : -1;
-  }
-  for (int item = tid; item < N * 2 * BW; item += T) {
-    const int c = item / (2 * BW), w = item - (item / (2 * BW)) * (2 * BW);
-    rec[2 * BMAX + N + N * N + item] = sExit[c] >= 0 ? sRow[sExit[c] * RW + N + w] : 0;
-  }
-  for (int b = tid; b < nb; b += T) {
-    const int e = sbas[b];
-    const int ce = t.creator[e], pe = t.index[e];
-    const int nxt = (pe + 1 < t.ccap) ? t.chain[(size_t)ce * t.ccap + pe + 1] : -1;
-    // kind 1 + creator: e is its chain's head at chunk start (row in phase B's
-    // head table); 0: older event (row recomputed from HBM)
-    rec[BMAX + b] = (nxt < 0 || nxt >= s) ? 1 + ce : 0;
-  }
 }
 
 // exclusive scan of a small int array by one block (n <= ~64k)
@@ -368,401 +128,17 @@ __global__ void k_scan_add(int32_t* out, int n, const int32_t* partial_scanned) 
   if (i < n) out[i] += partial_scanned[i / 1024];
 }
 
-// ---------------------------------------------------------------------------
-// Coordinates, phase B: one persistent workgroup walks the chunks in order and
-// materialises the lastAncestors rows of every basis element (the only rows a
-// later chunk needs from an earlier one).  It keeps the LA rows of all chain
-// heads in LDS: a basis element that is its chain's head at chunk start (the
-// common case: self-parents always are, gossip other-parents usually are) is an
-// LDS read; after chunk k the heads advance to the chunk's exits,
-//   LA(exit) = max(D_k[exit], max_{b in dep_k[exit]} BR_k[b]).
-// Older basis elements are recomputed from HBM.  The next chunk's packed
-// record is prefetched into registers while the current one is processed.
-// ---------------------------------------------------------------------------
-template <int BW>
-__global__ void __launch_bounds__(1024) k_coord_basis(Tables t, int n0, int L, int nchunks,
-                                                       const int32_t* Dbuf,
-                                                       const uint64_t* depbuf,
-                                                       const int32_t* rec,
-                                                       const int32_t* boff, const int32_t* olen,
-                                                       int32_t* BR) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int BMAX = BW * 64;
-  constexpr int PF = 8;
-  const int N = t.N;
-  const int tid = threadIdx.x, T = blockDim.x;
-  const int RECW = 2 * BMAX + N + N * N + 2 * N * BW + 1;
-  int32_t* sH = (int32_t*)smem;     // N*N head rows
-  int32_t* sBR = sH + N * N;        // BMAX*N basis rows of the current chunk
-  int32_t* sIn0 = sBR + BMAX * N;   // RECW
-  int32_t* sIn1 = sIn0 + RECW;      // RECW
-  for (int item = tid; item < N * N; item += T) {
-    const int c = item / N, i = item - (item / N) * N;
-    const int ol = olen[c];
-    sH[item] = ol > 0 ? t.LA[rowoff(t, c, ol - 1) + i] : -1;
-  }
-  for (int j = tid; j < RECW; j += T) sIn0[j] = rec[j];
-  __syncthreads();
-  int off = 0;
-  for (int k = 0; k < nchunks; k++) {
-    int32_t* cur = (k & 1) ? sIn1 : sIn0;
-    int32_t* nxt = (k & 1) ? sIn0 : sIn1;
-    int pf[PF];
-    const bool more = k + 1 < nchunks;
-#pragma unroll
-    for (int m = 0; m < PF; m++) {
-      const int j = tid + m * T;
-      pf[m] = (more && j < RECW) ? rec[(size_t)(k + 1) * RECW + j] : 0;
-    }
-    const int nb = cur[RECW - 1];
-    const int32_t* ids = cur;
-    const int32_t* kinds = cur + BMAX;
-    const int32_t* ex = cur + 2 * BMAX;
-    const int32_t* exD = ex + N;
-    const uint32_t* exdep = (const uint32_t*)(exD + N * N);
-    for (int item = tid; item < nb * N; item += T) {
-      const int b = item / N, c = item - (item / N) * N;
-      const int kind = kinds[b];
-      int v;
-      if (kind > 0) {
-        v = sH[(kind - 1) * N + c];
-      } else {
-        const int e = ids[b];
-        if (e < n0) {
-          v = t.LA[rowoff(t, t.creator[e], t.index[e]) + c];
-        } else {
-          const int le = e - n0;
-          const int j = le / L;
-          const int bj = boff[j];
-          v = Dbuf[(size_t)le * N + c];
-#pragma unroll
-          for (int w = 0; w < BW; w++) {
-            uint64_t msk = depbuf[(size_t)le * BW + w];
-            while (msk) {
-              const int tb = w * 64 + __builtin_ctzll(msk);
-              msk &= msk - 1;
-              v = max(v, ntload(&BR[(size_t)(bj + tb) * N + c]));
-            }
-          }
-        }
-      }
-      sBR[item] = v;
-      BR[(size_t)(off + b) * N + c] = v;
-    }
-    __syncthreads();
-    for (int item = tid; item < N * N; item += T) {
-      const int c = item / N, i = item - (item / N) * N;
-      if (ex[c] < 0) continue;
-      int v = exD[item];
-      for (int w = 0; w < 2 * BW; w++) {
-        uint32_t msk = exdep[c * 2 * BW + w];
-        while (msk) {
-          const int tb = w * 32 + __builtin_ctz(msk);
-          msk &= msk - 1;
-          v = max(v, sBR[tb * N + i]);
-        }
-      }
-      sH[item] = v;
-    }
-#pragma unroll
-    for (int m = 0; m < PF; m++) {
-      const int j = tid + m * T;
-      if (more && j < RECW) nxt[j] = pf[m];
-    }
-    if (more)
-      for (int j = tid + PF * T; j < RECW; j += T) nxt[j] = rec[(size_t)(k + 1) * RECW + j];
-    off += nb;
-    drain_stores();
-    __syncthreads();
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Coordinates, phase C: per chunk, final LA rows (to HBM, chain-major) and the
-// firstDescendants scatter (UpdateAncestorFirstDescendant, hashgraph.go:466-494):
-// event x on chain cx is the first cx-descendant of exactly the chain-j events
-// at positions (LA[sp(x)][j], LA[x][j]], so FD[j][q][cx] = index(x) there.
-// ---------------------------------------------------------------------------
-template <int BW>
-__global__ void __launch_bounds__(256) k_coord_final(Tables t, int n0, int n1, int L,
-                                                      const int32_t* Dbuf,
-                                                      const uint64_t* depbuf,
-                                                      const int32_t* enc,
-                                                      const int32_t* bcount,
-                                                      const int32_t* boff,
-                                                      const int32_t* BR, int br_in_lds) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int BMAX = BW * 64;
-  const int N = t.N;
-  const int k = blockIdx.x;
-  const int s = n0 + k * L;
-  const int e = min(n1, s + L);
-  const int cnt = e - s;
-  const int tid = threadIdx.x, T = blockDim.x;
-  const int nb = bcount[k];
-  const size_t bo = (size_t)boff[k] * N;
-  int32_t* sLA = (int32_t*)smem;  // L * N
-  const int32_t* sBR;             // BMAX * N basis rows (LDS when they fit)
-  if (br_in_lds) {
-    int32_t* b = sLA + (size_t)L * N;
-    for (int i = tid; i < nb * N; i += T) b[i] = BR[bo + i];
-    sBR = b;
-  } else {
-    sBR = BR + bo;
-  }
-  __syncthreads();
-  const size_t base = (size_t)(s - n0);
-  for (int item = tid; item < cnt * N; item += T) {
-    const int i = item / N, c = item - (item / N) * N;
-    int v = Dbuf[base * N + item];
-#pragma unroll
-    for (int w = 0; w < BW; w++) {
-      uint64_t m = depbuf[(base + i) * BW + w];
-      while (m) {
-        const int tb = w * 64 + __builtin_ctzll(m);
-        m &= m - 1;
-        v = max(v, sBR[tb * N + c]);
-      }
-    }
-    sLA[item] = v;
-    const int x = s + i;
-    t.LA[rowoff(t, t.creator[x], t.index[x]) + c] = v;
-  }
-  __syncthreads();
-  for (int item = tid; item < cnt * N; item += T) {
-    const int i = item / N, j = item - (item / N) * N;
-    const int x = s + i;
-    const int cx = t.creator[x], ix = t.index[x];
-    const int psp = enc[2 * (base + i)];
-    int lo = -1;
-    if (psp >= 0) lo = sLA[psp * N + j];
-    else if (psp <= -2) lo = sBR[(-psp - 2) * N + j];
-    const int hi = sLA[i * N + j];
-    for (int q = lo + 1; q <= hi; q++) t.FD[rowoff(t, j, q) + cx] = ix;
-  }
-}
-
 // chain table: chain[c][index] = id for the new events
 __global__ void k_chain_fill(Tables t, int n0, int n1) {
   const int x = n0 + blockIdx.x * blockDim.x + threadIdx.x;
   if (x < n1) t.chain[(size_t)t.creator[x] * t.ccap + t.index[x]] = x;
 }
 
-// ---------------------------------------------------------------------------
-// Rounds (DivideRounds/Round/RoundInc, hashgraph.go:211-305, 573-588) as a
-// frontier over rounds.  C[r][c] = first position on chain c with round >= r.
-// Proved in DESIGN.md: round(x) >= r+1  <=>  x strongly sees >= SM of
-// C_r \ {x}; the predicate is monotone along a chain, so C[r+1][c] is the first
-// position at or after max(C[r][c], old chain length) that satisfies it.
-// One persistent workgroup walks the rounds; each round probes a window of
-// candidate positions per chain against the members' FD rows staged in LDS.
-// ---------------------------------------------------------------------------
-// strongly-see test of one LA row against one FD row, both padded to NP
-// columns (LA pad -1, FD pad INF32) and 16-byte aligned in LDS
-template <int NPC>
-__device__ __forceinline__ int ss_count(const int4* la4, const int4* fd4, int NP) {
-  int cnt = 0;
-  const int nq = (NPC > 0) ? NPC / 4 : NP / 4;
-#pragma unroll
-  for (int q = 0; q < (NPC > 0 ? NPC / 4 : 1); q++) {
-    if (NPC == 0) break;
-    const int4 a = la4[q], b = fd4[q];
-    cnt += (a.x >= b.x) + (a.y >= b.y) + (a.z >= b.z) + (a.w >= b.w);
-  }
-  if (NPC == 0) {
-    for (int q = 0; q < nq; q += 4) {
-      const int4 a0 = la4[q], a1 = la4[q + 1], a2 = la4[q + 2], a3 = la4[q + 3];
-      const int4 b0 = fd4[q], b1 = fd4[q + 1], b2 = fd4[q + 2], b3 = fd4[q + 3];
-      cnt += (a0.x >= b0.x) + (a0.y >= b0.y) + (a0.z >= b0.z) + (a0.w >= b0.w);
-      cnt += (a1.x >= b1.x) + (a1.y >= b1.y) + (a1.z >= b1.z) + (a1.w >= b1.w);
-      cnt += (a2.x >= b2.x) + (a2.y >= b2.y) + (a2.z >= b2.z) + (a2.w >= b2.w);
-      cnt += (a3.x >= b3.x) + (a3.y >= b3.y) + (a3.z >= b3.z) + (a3.w >= b3.w);
-    }
-  }
-  return cnt;
-}
-
+// HGE_STAMPS diagnostics: shader-clock stamp, ordered with the code around it
 __device__ __forceinline__ uint64_t stamp() {
   uint64_t v;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");
   return v;
-}
-
-template <int NPC>
-__global__ void __launch_bounds__(1024) k_rounds_frontier(Tables t, const int32_t* olen,
-                                                          const int32_t* len, int32_t* rstate,
-                                                          int WIN, uint64_t* dbg) {
-  uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0};
-  uint64_t st_t = 0;
-#define STAMP(k)                                   \
-  if (dbg && threadIdx.x == 0) {                   \
-    const uint64_t now_ = stamp();                 \
-    if ((k) > 0) st_acc[(k) - 1] += now_ - st_t;   \
-    st_t = now_;                                   \
-  }
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int N = t.N, SM = t.SM;
-  const int NP = (N + 15) & ~15;
-  const int tid = threadIdx.x, T = blockDim.x;
-  int32_t* sFD = (int32_t*)smem;       // N*NP   member FD rows (C_r)
-  int32_t* sLAw = sFD + N * NP;        // N*WIN*NP window LA rows
-  int32_t* sP = sLAw + N * WIN * NP;   // N     C_r positions (carried in LDS across rounds)
-  int32_t* sMid = sP + N;              // N     member ids
-  int32_t* sLo = sMid + N;             // N     window start
-  int32_t* sLen = sLo + N;             // N
-  int32_t* sOlen = sLen + N;           // N
-  int32_t* sNeed = sOlen + N;          // N
-  int32_t* sCur = sNeed + N;           // N     C_{r+1} as stored before this kernel
-  int32_t* sNext = sCur + N;           // N     C_{r+1}
-  int32_t* sFlag = sNext + N;          // N*WIN probe satisfied
-  int32_t* sIdw = sFlag + N * WIN;     // N*WIN event ids of the window
-  __shared__ int s_rlo, s_any, s_more;
-
-  if (tid == 0) s_rlo = INF32;
-  __syncthreads();
-  for (int c = tid; c < N; c += T) {
-    const int ol = olen[c], ln = len[c];
-    sOlen[c] = ol;
-    sLen[c] = ln;
-    if (ln > ol) {
-      int r0 = 0;
-      if (ol == 0) t.C[c] = 0;  // initial event: first position with round >= 0
-      else r0 = t.round[t.chain[(size_t)c * t.ccap + ol - 1]];
-      atomicMin(&s_rlo, r0);
-    }
-  }
-  __syncthreads();
-  const int rlo = s_rlo;
-  if (rlo == INF32) return;  // no new events
-  // Rows this kernel writes are only re-read from LDS (a CU's L1 may keep a
-  // stale copy of a line the workgroup stored).
-  for (int c = tid; c < N; c += T) {
-    int p = t.C[(size_t)rlo * N + c];
-    if (rlo == 0 && sOlen[c] == 0 && sLen[c] > 0) p = 0;
-    sP[c] = p;
-    sMid[c] = (p != INF32) ? t.chain[(size_t)c * t.ccap + p] : -1;
-    sLo[c] = max(p, sOlen[c]);
-  }
-  __syncthreads();
-  int r = rlo;
-  for (;; r++) {
-    if (r + 1 >= t.Rcap) {
-      if (tid == 0) rstate[1] = 1;  // overflow: host grows Rcap and reruns
-      return;
-    }
-    STAMP(0);
-    // ---- one burst of independent loads: member FD rows, C_{r+1} as stored,
-    //      and the first probe window (LA rows + ids) of every chain
-    for (int item = tid; item < N * NP; item += T) {
-      const int d = item / NP, i = item - (item / NP) * NP;
-      const int p = sP[d];
-      sFD[item] = (p != INF32 && i < N) ? t.FD[rowoff(t, d, p) + i] : INF32;
-    }
-    for (int c = tid; c < N; c += T) sCur[c] = t.C[(size_t)(r + 1) * N + c];
-    bool first = true;
-    for (;;) {
-      if (tid == 0) s_more = 0;
-      // loads first (8 per thread in flight), LDS stores after: one HBM latency
-      for (int b0 = tid; b0 < N * WIN * NP; b0 += 8 * T) {
-        int v[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-          const int item = b0 + u * T;
-          v[u] = -1;
-          if (item < N * WIN * NP) {
-            const int c = item / (WIN * NP);
-            const int rem = item - c * (WIN * NP);
-            const int k = rem / NP, i = rem - (rem / NP) * NP;
-            const int p = sLo[c] + k;
-            const bool ok = sP[c] != INF32 && p < sLen[c] && (first || sNeed[c]);
-            if (ok && i < N) v[u] = t.LA[rowoff(t, c, p) + i];
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-          const int item = b0 + u * T;
-          if (item < N * WIN * NP) sLAw[item] = v[u];
-        }
-      }
-      for (int pr = tid; pr < N * WIN; pr += T) {
-        const int c = pr / WIN, k = pr - (pr / WIN) * WIN;
-        const int p = sLo[c] + k;
-        const bool ok = sP[c] != INF32 && p < sLen[c] && (first || sNeed[c]);
-        sIdw[pr] = ok ? t.chain[(size_t)c * t.ccap + p] : -1;
-      }
-      __syncthreads();
-      STAMP(1);
-      if (first) {
-        for (int c = tid; c < N; c += T) {
-          const int p = sP[c];
-          sNext[c] = sCur[c];
-          sNeed[c] = (sCur[c] == INF32 && p != INF32 && sLo[c] < sLen[c]) ? 1 : 0;
-        }
-        __syncthreads();
-        first = false;
-      }
-      // one thread per probe (c, k): x strongly sees >= SM members of C_r \ {x}?
-      for (int pr = tid; pr < N * WIN; pr += T) {
-        const int c = pr / WIN, k = pr - (pr / WIN) * WIN;
-        int flag = 0;
-        const int p = sLo[c] + k;
-        if (sNeed[c] && p < sLen[c]) {
-          const int4* la4 = (const int4*)(sLAw + (size_t)pr * NP);
-          int ss = 0;
-#pragma unroll 4
-          for (int d = 0; d < N; d++) {
-            const bool skip = sMid[d] < 0 || (d == c && p == sP[c]);
-            const int cnt = ss_count<NPC>(la4, (const int4*)(sFD + d * NP), NP);
-            ss += (!skip && cnt >= SM) ? 1 : 0;
-          }
-          flag = ss >= SM;
-        }
-        sFlag[pr] = flag;
-      }
-      __syncthreads();
-      STAMP(2);
-      for (int c = tid; c < N; c += T) {
-        if (!sNeed[c]) continue;
-        int k = 0;
-        while (k < WIN && !sFlag[c * WIN + k]) k++;
-        if (k < WIN) {
-          const int pos = sLo[c] + k;
-          sNext[c] = pos;
-          t.C[(size_t)(r + 1) * N + c] = pos;
-          sNeed[c] = 0;
-          sMid[c] = sIdw[c * WIN + k];  // next round's member
-          sCur[c] = -2;                  // marks "member id known"
-        } else if (sLo[c] + WIN >= sLen[c]) {
-          sNeed[c] = 0;
-        } else {
-          sLo[c] += WIN;
-          s_more = 1;
-        }
-      }
-      __syncthreads();
-      STAMP(3);
-      if (!s_more) break;
-    }
-    // ---- advance: C_{r+1} becomes the member set
-    if (tid == 0) s_any = 0;
-    __syncthreads();
-    for (int c = tid; c < N; c += T) {
-      const int p = sNext[c];
-      if (p != INF32) s_any = 1;
-      if (sCur[c] != -2) sMid[c] = (p != INF32) ? t.chain[(size_t)c * t.ccap + p] : -1;
-      sP[c] = p;
-      sLo[c] = max(p, sOlen[c]);
-    }
-    __syncthreads();
-    STAMP(4);
-    if (!s_any) break;
-  }
-  if (tid == 0) rstate[0] = max(rstate[0], r + 1);  // Rounds()
-  if (dbg && tid == 0) {
-    for (int q = 0; q < 4; q++) dbg[q] += st_acc[q];
-    dbg[5] += (uint64_t)(r - rlo + 1);
-  }
-#undef STAMP
 }
 
 // ---------------------------------------------------------------------------

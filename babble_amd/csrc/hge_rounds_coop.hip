@@ -1,192 +1,7 @@
-// hge_wide.hip — coordinate and round kernels for wide hashgraphs (N > 32).
-//
-// The chunked coordinate pipeline of hge_kernels.hip keeps N x N head tables
-// and per-chunk records in LDS, which stops fitting past N = 64.  Here the
-// coordinates are built from bandwidth-friendly passes instead:
-//
-//   1. lastAncestors by chain-prefix sweeps.  Along a creator chain,
-//      InitEventCoordinates (hashgraph.go:399-463) is a prefix max:
-//        LA[(j,k)] = max(own(j,k), LA[(j,k-1)], LA[op(j,k)]).
-//      A sweep recomputes every new row from the CURRENT table (in place,
-//      segments of SEG positions per workgroup, carry = the stored row before
-//      the segment).  Every value ever stored is a lower bound of the true
-//      one and the update is monotone, so a sweep that changes nothing has
-//      reached the fixed point, which for an acyclic recurrence is unique:
-//      the exact table.  ~10-20 sweeps (SURVEY §7 "windowed Jacobi").
-//      Each sweep streams op rows and own rows: coalesced 4N-byte rows.
-//   2. LA -> LAT (chain j, column c, position k) by a tiled LDS transpose.
-//   3. firstDescendants as runs (UpdateAncestorFirstDescendant,
-//      hashgraph.go:466-494): chain-j event k is the first chain-j descendant
-//      of chain-c positions (LAT[j][c][k-1], LAT[j][c][k]], so
-//      FDT[j][c][q] = k there: contiguous runs, coalesced writes.
-//   4. FDT -> FD rows (the layout every reader uses) by a tiled transpose.
-//
-// Rounds for N > 32 use a cooperative kernel: one workgroup per chain, one
-// grid barrier per round (k_rounds_coop below).
+// hge_rounds_coop.hip — DivideRounds for wide hashgraphs (N > 32): the
+// frontier recurrence evaluated by one co-resident workgroup per chain.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-
-namespace hge {
-
-// LA[(j, k)] = -1 for the new positions k in [olen_j, len_j) of every chain
-__global__ void k_la_clear(Tables t, const int32_t* olen, const int32_t* len) {
-  const int j = blockIdx.y;
-  const int N = t.N;
-  const int64_t lo = (int64_t)olen[j] * N, hi = (int64_t)len[j] * N;
-  int32_t* base = t.LA + (size_t)j * t.ccap * N;
-  for (int64_t e = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < hi;
-       e += (int64_t)gridDim.x * blockDim.x)
-    base[e] = -1;
-}
-
-// One in-place sweep.  G = 256/NP segments per workgroup, NP threads (columns)
-// per segment.  segs[s] = (chain, first position).
-template <int NP>
-__global__ void __launch_bounds__(256) k_la_sweep(Tables t, const int2* segs, int nseg, int SEG,
-                                                  const int32_t* len, int32_t* changed) {
-  constexpr int G = 256 / NP;
-  constexpr int SEGMAX = 64;
-  __shared__ int64_t s_off[G][SEGMAX];
-  const int N = t.N;
-  const int g = threadIdx.x / NP, i = threadIdx.x - (threadIdx.x / NP) * NP;
-  const int sidx = blockIdx.x * G + g;
-  const bool valid = sidx < nseg;
-  int j = 0, k0 = 0, k1 = 0;
-  if (valid) {
-    const int2 sg = segs[sidx];
-    j = sg.x;
-    k0 = sg.y;
-    k1 = min(k0 + SEG, len[j]);
-  }
-  for (int kk = i; kk < SEG; kk += NP) {
-    int64_t off = -1;
-    if (valid && k0 + kk < k1) {
-      const int x = t.chain[(size_t)j * t.ccap + k0 + kk];
-      const int o = t.op[x];
-      if (o >= 0) off = (int64_t)rowoff(t, t.creator[o], t.index[o]);
-    }
-    s_off[g][kk] = off;
-  }
-  __syncthreads();
-  const bool act = valid && i < N;
-  bool ch = false;
-  if (act) {
-    int v = (k0 > 0) ? t.LA[rowoff(t, j, k0 - 1) + i] : -1;
-    for (int kb = k0; kb < k1; kb += 8) {
-      int a[8], old[8];
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int k = kb + u;
-        a[u] = -1;
-        old[u] = -1;
-        if (k < k1) {
-          const int64_t off = s_off[g][k - k0];
-          if (off >= 0) a[u] = t.LA[off + i];
-          old[u] = t.LA[rowoff(t, j, k) + i];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int k = kb + u;
-        if (k < k1) {
-          v = max(v, a[u]);
-          if (i == j) v = max(v, k);
-          const int nv = max(v, old[u]);
-          v = nv;
-          if (nv != old[u]) {
-            t.LA[rowoff(t, j, k) + i] = nv;
-            ch = true;
-          }
-        }
-      }
-    }
-  }
-  if (__ballot(ch) && (threadIdx.x & 63) == __builtin_ctzll(__ballot(ch))) atomicOr(changed, 1);
-}
-
-// Tiled transposes through LDS (64 x 64 tiles, 256 threads).
-//   mode 0: LA[(j,k)][c] -> LAT[j][c][k] for k in [klo_j, len_j)
-//   mode 1: FDT[j][c][q] -> FD[(c,q)][j] for q in [qlo_c, len_c)
-// grid: (tiles along positions, tiles along the N columns, chain)
-__global__ void __launch_bounds__(256) k_transpose(Tables t, const int32_t* LAT_or_FDT, int32_t* out,
-                                                   const int32_t* plo, const int32_t* len, int mode) {
-  __shared__ int32_t tile[64][65];
-  const int N = t.N;
-  const size_t ccap = t.ccap;
-  const int a = blockIdx.z;  // mode 0: chain j; mode 1: source chain c
-  const int p0 = plo[a] + blockIdx.x * 64;
-  const int pend = len[a];
-  if (p0 >= pend) return;
-  const int c0 = blockIdx.y * 64;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
-  if (mode == 0) {
-    // read rows (j, p) columns [c0, c0+64): row-major, coalesced along c
-    for (int r = ty; r < 64; r += 4) {
-      const int p = p0 + r, c = c0 + tx;
-      tile[r][tx] = (p < pend && c < N) ? t.LA[rowoff(t, a, p) + c] : 0;
-    }
-    __syncthreads();
-    // write LAT[a][c][p]: coalesced along p
-    int32_t* LAT = out;
-    for (int r = ty; r < 64; r += 4) {
-      const int c = c0 + r, p = p0 + tx;
-      if (c < N && p < pend) LAT[((size_t)a * N + c) * ccap + p] = tile[tx][r];
-    }
-  } else {
-    // read FDT[j][a][q] for j in [c0, c0+64): coalesced along q
-    const int32_t* FDT = LAT_or_FDT;
-    for (int r = ty; r < 64; r += 4) {
-      const int jj = c0 + r, q = p0 + tx;
-      tile[r][tx] = (jj < N && q < pend) ? FDT[((size_t)jj * N + a) * ccap + q] : 0;
-    }
-    __syncthreads();
-    // write FD[(a, q)][j]: coalesced along j
-    for (int r = ty; r < 64; r += 4) {
-      const int q = p0 + r, jj = c0 + tx;
-      if (q < pend && jj < N) t.FD[rowoff(t, a, q) + jj] = tile[tx][r];
-    }
-  }
-}
-
-// FDT[j][c][q] = INF32 for the new positions q in [olen_c, len_c)
-__global__ void k_fdt_clear(Tables t, int32_t* FDT, const int32_t* olen, const int32_t* len) {
-  const int c = blockIdx.y, j = blockIdx.z;
-  const int lo = olen[c], hi = len[c];
-  int32_t* row = FDT + ((size_t)j * t.N + c) * t.ccap;
-  for (int q = lo + blockIdx.x * blockDim.x + threadIdx.x; q < hi; q += gridDim.x * blockDim.x)
-    row[q] = INF32;
-}
-
-// runs: chain-j event k (new) is the first chain-j descendant of chain-c
-// positions (LAT[j][c][k-1], LAT[j][c][k]]
-__global__ void k_fdt_runs(Tables t, const int32_t* LAT, int32_t* FDT, const int32_t* olen,
-                           const int32_t* len) {
-  const int c = blockIdx.y, j = blockIdx.z;
-  const int k = olen[j] + blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= len[j]) return;
-  const size_t base = ((size_t)j * t.N + c) * t.ccap;
-  const int hi = LAT[base + k];
-  const int lo = k > 0 ? LAT[base + k - 1] : -1;
-  int32_t* row = FDT + base;
-  for (int q = lo + 1; q <= hi; q++) row[q] = k;
-}
-
-// lowest chain-c position whose FD row a new event can change:
-// min over chains j with old events of LA[(j, olen_j - 1)][c] + 1
-__global__ void k_fd_qlo(Tables t, const int32_t* olen, const int32_t* len, int32_t* qlo) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= t.N) return;
-  int m = olen[c];  // the new positions themselves
-  for (int j = 0; j < t.N; j++) {
-    if (len[j] == olen[j]) continue;  // chain j got no new event
-    const int ol = olen[j];
-    const int v = ol > 0 ? t.LA[rowoff(t, j, ol - 1) + c] + 1 : 0;
-    m = min(m, v);
-  }
-  qlo[c] = max(0, m);
-}
-
-}  // namespace hge
 
 namespace hge {
 

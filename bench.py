@@ -1,20 +1,30 @@
 """Benchmark: consensus-ordered events/sec of the hashgraph ordering hot path.
 
-Workload (BASELINE.json configs[1]): synthetic random-gossip DAG, 16
-participants, 100k events, RunConsensus every K=16 inserted events (the
-caller's schedule is part of the semantics: SURVEY.md TL;DR 5).  One step =
-one full replay of the stream on the device: coordinates (InsertEvent),
-DivideRounds, DecideFame and FindOrder at all 6,250 call points, from event
-tables already resident in HBM to the complete consensus order.
+Workloads (BASELINE.json configs):
+  gossip (default, configs[1]): synthetic random-gossip DAG, 16 participants,
+      100k events, RunConsensus every K=16 inserted events (the caller's
+      schedule is part of the semantics: SURVEY.md TL;DR 5).  One step = one
+      full replay of the stream on the device: coordinates (InsertEvent),
+      DivideRounds, DecideFame and FindOrder at all 6,250 call points, from
+      event tables already resident in HBM to the complete consensus order.
+      --participants/--events/--k select configs[2] (64/1M) and configs[3]
+      (256/10M).
+  mc (configs[4]): Monte Carlo batch of independent 32-participant
+      hashgraphs with simulated Byzantine forkers (10 of 32 creators fork with
+      p=0.05), 10k submissions each, K=32; the batch is split across ranks.
+      Every graph has its own engine (HIP stream); host threads drive them
+      concurrently.
 
-Multi-GPU (torch.distributed, one process per GPU): every rank replays its own
-independent hashgraph (seed base + rank) — the Monte Carlo / independent-replay
-sharding of north_star; no data-path collective.  value = events ordered by
-all ranks per step / max-over-ranks step time ("scaling": "weak").
+Multi-GPU (torch.distributed over RCCL, one process per GPU): gossip = every
+rank replays its own independent hashgraph (seed + rank), mc = every rank
+replays its share of the batch; no data-path collective.  value = events
+ordered by all ranks per step / max-over-ranks step time ("scaling": "weak").
 
-Also reported: roofline of the dominant kernel (HIP events on the engine
-stream), and the single-core CPU baseline (the Go-faithful oracle, timed on
-the same host in the same run, rank 0 only).
+The timed steps run without per-kernel instrumentation; a separate profiled
+pass (HIP events around every launch on the engine stream) gives the
+dominant kernel's average launch time for the roofline.  The CPU baseline is
+the Go-faithful oracle on one host core over a bounded sample of the same
+workload (rank 0 only), and its order is compared with the device's.
 """
 import argparse
 import json
@@ -22,33 +32,49 @@ import os
 import platform
 import sys
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
-def algorithmic_bytes(kernel, n, events, ordered, calls):
-    """Algorithmic HBM bytes one launch of `kernel` must move.
+def algorithmic_bytes(kernel, n, events, ordered):
+    """Algorithmic HBM bytes of ONE launch of `kernel` over a whole replay
+    (B(N) = 24N + 48 per ordered event).
 
-    k_coord_final: per event LA[sp]+D rows read, LA row written, FD row
-    written once in total (16N bytes/event, SURVEY.md §8d 'coordinate kernel').
-    k_rounds_frontier: per event its LA row read once for the strongly-see
-    round test (4N bytes/event).  k_round_received: FD row of every ordered
-    event (4N) + its key.  Others: the 48-byte sort key per ordered event.
+    coordinates: k_coord_final 16N/event (read LA[sp] and D, write LA and FD),
+    k_coord_local 8N/event, k_la_sweep 12N/event (op row + own row read, own
+    row written), k_transpose 8N/event; rounds: k_fss 8N/event (FD row read,
+    fss row written), k_rounds_walk / k_rounds_coop 4N/event (the strongly-see
+    round test reads each event's LA row once); order: k_round_received /
+    k_median_wave (4N + 48)/ordered event; anything else the 48-byte sort key.
     """
-    if kernel.startswith("k_coord_final"):
-        return 16 * n * events
-    if kernel.startswith("k_coord_local"):
-        return 8 * n * events
-    if kernel.startswith("k_rounds_frontier"):
-        return 4 * n * events
-    if kernel.startswith("k_round_received"):
+    name = kernel.strip("()").split("<")[0]
+    per_event = {"k_coord_final": 16 * n, "k_coord_local": 8 * n, "k_la_sweep": 12 * n,
+                 "k_transpose": 8 * n, "k_fss": 8 * n, "k_rounds_walk": 4 * n,
+                 "k_rounds_coop": 4 * n, "k_rounds_fss": 4 * n, "k_rounds_frontier": 4 * n}
+    if name in per_event:
+        return per_event[name] * events
+    if name in ("k_round_received", "k_median_wave"):
         return (4 * n + 48) * ordered
     return 48 * ordered
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (profiles/pmc_traffic.json, made by scripts/pmc_traffic.py), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        pm = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    name = kernel.strip("()").split("<")[0]
+    v = pm.get("kernels", {}).get(name)
+    return v.get("bytes_per_launch") if isinstance(v, dict) else None
 
 
 def main():
@@ -56,13 +82,21 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--participants", type=int, default=16)
-    ap.add_argument("--events", type=int, default=100_000)
-    ap.add_argument("--k", type=int, default=16, help="RunConsensus every k inserted events")
+    ap.add_argument("--workload", choices=("gossip", "mc"), default="gossip")
+    ap.add_argument("--participants", type=int, default=None)
+    ap.add_argument("--events", type=int, default=None)
+    ap.add_argument("--k", type=int, default=None, help="RunConsensus every k submissions")
+    ap.add_argument("--graphs", type=int, default=1024, help="mc: hashgraphs in the whole batch")
+    ap.add_argument("--threads", type=int, default=8, help="mc: host threads driving engines")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-events", type=int, default=100_000)
+    ap.add_argument("--profile-steps", type=int, default=2)
     args = ap.parse_args()
+    mc = args.workload == "mc"
+    n = args.participants or (32 if mc else 16)
+    E = args.events or (10_000 if mc else 100_000)
+    K = args.k or n
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -78,17 +112,27 @@ def main():
     from babble_amd.engine import Engine, events_array
     from babble_amd.gossip import random_gossip, schedule
 
-    n, E, K = args.participants, args.events, args.k
-    dag = random_gossip(n, E, seed=args.seed + rank)
-    calls = schedule(E, K)
-    ev = events_array(dag)
-    eng = Engine(n, E, device=local_rank)
+    # ---- stage the workload in HBM (host admission + upload; not timed) ----
     t0 = time.perf_counter()
-    eng.prepare(ev, calls)  # FromParentsLatest admission on the host + staging into HBM
+    if mc:
+        per = args.graphs // world + (1 if rank < args.graphs % world else 0)
+        first = rank * (args.graphs // world) + min(rank, args.graphs % world)
+        dags = [random_gossip(n, E, seed=args.seed + first + g, forkers=10, fork_p=0.05)
+                for g in range(per)]
+        engines = [Engine(n, len(d["creator"]) + 64, device=local_rank) for d in dags]
+        for eng, d in zip(engines, dags):
+            eng.prepare(events_array(d), schedule(len(d["creator"]), K))
+    else:
+        dags = [random_gossip(n, E, seed=args.seed + rank)]
+        engines = [Engine(n, E, device=local_rank)]
+        engines[0].prepare(events_array(dags[0]), schedule(E, K))
     ingest_s = time.perf_counter() - t0
+    pool = ThreadPoolExecutor(max_workers=max(1, min(args.threads, len(engines))))
 
-    for _ in range(args.warmup):
-        eng.run()
+    def step():
+        if len(engines) == 1:
+            return engines[0].run()
+        return sum(pool.map(lambda e: e.run(), engines))
 
     def sync_all():
         if dist is not None:
@@ -96,20 +140,28 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
+    for _ in range(args.warmup):
+        step()
     sync_all()
-    eng.set_profiling(True)
     t0 = time.perf_counter()
+    ordered = 0
     for _ in range(args.steps):
-        eng.run()  # returns after the device finished (stream synchronised)
+        ordered = step()  # every engine returns after its stream drained
     t1 = time.perf_counter()
-    ordered = eng._nordered
     sync_all()
     step_s = (t1 - t0) / args.steps
-    kstats = eng.kernel_stats()
-    eng.set_profiling(False)
 
-    tot_ordered = ordered
-    max_step = step_s
+    # ---- profiled pass: per-kernel device time (HIP events on the engine stream) ----
+    eng0 = engines[0]
+    eng0.set_profiling(True)
+    for _ in range(max(1, args.profile_steps)):
+        eng0.run()
+    kstats = eng0.kernel_stats()
+    eng0.set_profiling(False)
+    ev0 = len(dags[0]["creator"])
+    ord0 = eng0._nordered
+
+    tot_ordered, max_step = ordered, step_s
     if dist is not None:
         import torch
         tt = torch.tensor([step_s], dtype=torch.float64, device=f"cuda:{local_rank}")
@@ -119,37 +171,41 @@ def main():
         dist.all_reduce(oo, op=dist.ReduceOp.SUM)
         tot_ordered = int(oo.item())
 
-    # dominant kernel (largest total device time over the timed steps)
     dom, (dom_ms, dom_n) = max(kstats.items(), key=lambda kv: kv[1][0])
     per_launch_ms = dom_ms / max(dom_n, 1)
-    launches_per_step = max(dom_n // args.steps, 1)
-    alg = algorithmic_bytes(dom, n, E, ordered, len(calls)) / launches_per_step
+    launches_per_replay = max(dom_n // max(1, args.profile_steps), 1)
+    alg = algorithmic_bytes(dom, n, ev0, ord0) / launches_per_replay
     achieved = alg / (per_launch_ms * 1e-3) / 1e9
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_path):
-        try:
-            pm = json.load(open(pmc_path))
-            if dom.split("<")[0] in pm:
-                traffic = pm[dom.split("<")[0]]
-        except Exception:
-            traffic = None
 
-    cpu = None
+    cpu, parity = None, None
     if rank == 0 and not args.no_cpu_baseline:
         from oracle.oracle import replay as oracle_replay
-        ns = min(args.cpu_sample_events, E)
-        sub = {k: (v[:ns] if isinstance(v, np.ndarray) else v) for k, v in dag.items()}
+        d = dags[0]
+        ns = min(args.cpu_sample_events, len(d["creator"]))
+        sub = {k: (v[:ns] if isinstance(v, np.ndarray) else v) for k, v in d.items()}
         t0 = time.perf_counter()
         _, _, corder, _ = oracle_replay(sub, schedule(ns, K))
         cs = time.perf_counter() - t0
-        cpu = {"value": len(corder) / cs, "unit": "events/s", "cores": 1, "kind": "port",
-               "sample": f"Go-faithful C++ oracle, first {ns} events of the same stream, K={K}, "
+        what = (f"graph 0 of the batch ({ns} submissions)" if mc else
+                f"first {ns} of {len(d['creator'])} submissions of the same stream")
+        cpu = {"value": round(len(corder) / cs, 1), "unit": "events/s", "cores": 1, "kind": "port",
+               "sample": f"Go-faithful C++ oracle (oracle/hg_oracle.cpp), {what}, K={K}, "
                          f"{cs:.2f} s on {platform.processor() or platform.machine()} "
-                         f"(nproc {os.cpu_count()})"}
+                         f"(host nproc {os.cpu_count()})"}
+        if ns == len(d["creator"]):
+            _, gorder, _ = eng0.fetch()
+            parity = ("bit-exact vs CPU oracle (full stream of graph 0)"
+                      if np.array_equal(gorder, corder) else "MISMATCH vs CPU oracle")
 
     if rank == 0:
         value = tot_ordered / max_step
+        if mc:
+            workload = (f"Monte Carlo batch: {args.graphs} independent random-gossip hashgraphs, "
+                        f"{n} participants, {E} submissions each, 10 forkers p=0.05, "
+                        f"RunConsensus every K={K}")
+        else:
+            workload = (f"random-gossip DAG, {n} participants, {E} events per GPU, "
+                        f"RunConsensus every K={K} events ({len(schedule(E, K))} calls)")
         line = {
             "metric": "consensus-ordered events/sec at N participants",
             "value": round(value, 1),
@@ -163,21 +219,24 @@ def main():
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic",
-            "config": {"workload": f"random-gossip DAG, {n} participants, {E} events per GPU, "
-                                   f"RunConsensus every K={K} events ({len(calls)} calls)",
-                       "participants": n, "events_per_gpu": E, "k": K, "calls": len(calls),
-                       "ordered_per_step": tot_ordered, "parallelism": f"replicas{world}"},
+            "config": {"workload": workload, "participants": n, "events_per_graph": E, "k": K,
+                       "graphs_per_gpu": len(engines), "ordered_per_step": tot_ordered,
+                       "parallelism": f"replicas{world}"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic(dom),
+                         "algorithmic_bytes_per_launch": int(alg),
                          "launch_ms": round(per_launch_ms, 4)},
             "cpu_baseline": cpu,
+            "parity": parity,
             "ingest_host_ms": round(ingest_s * 1e3, 2),
-            "kernels_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in
-                                    sorted(kstats.items(), key=lambda kv: -kv[1][0])},
+            "kernels_ms_per_replay": {k: round(v[0] / max(1, args.profile_steps), 4) for k, v in
+                                      sorted(kstats.items(), key=lambda kv: -kv[1][0])},
         }
-        print(json.dumps(line))
-    eng.close()
+        print(json.dumps(line), flush=True)
+    pool.shutdown()
+    for e in engines:
+        e.close()
     if dist is not None:
         dist.destroy_process_group()
 

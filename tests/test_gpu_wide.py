@@ -1,8 +1,8 @@
 """Wide hashgraphs (N > 32) on the GPU: chain-prefix sweep coordinates, the
-transposed firstDescendants runs and the cooperative rounds kernel
-(babble_amd/csrc/hge_wide.hip), bit-exact against committed oracle outputs
-(tests/golden/wide_*.npz, made by tests/golden/make_golden.py) and, at small
-N with the wide path forced (HGE_WIDE=1), against the live oracle."""
+transposed firstDescendants runs (babble_amd/csrc/hge_coords.hip) and the
+cooperative rounds kernel (hge_rounds_coop.hip), bit-exact against committed
+oracle outputs (tests/golden/wide_*.npz, made by tests/golden/make_golden.py);
+plus the sweep coordinates at small N against the live oracle."""
 import glob
 import os
 
@@ -49,15 +49,10 @@ def test_wide_golden(path):
         eng.close()
 
 
-@pytest.fixture
-def force_wide(monkeypatch):
-    monkeypatch.setenv("HGE_WIDE", "1")
-
-
 @pytest.mark.parametrize("n,events,k", [(4, 1000, 4), (16, 3000, 16), (16, 3000, 1), (32, 4000, 32),
                                         (7, 2000, 50)])
-def test_sweep_coordinates_small_n(force_wide, n, events, k):
-    """The sweep/transposes coordinate path, forced at small N, against the live oracle."""
+def test_sweep_coordinates_small_n(n, events, k):
+    """Sweeps + transposes at small N (several sweep groups, K from 1 to 50) vs the live oracle."""
     from babble_amd.engine import Engine
     eng = Engine(n, 1 << 14)
     try:
