@@ -39,12 +39,17 @@ __global__ void k_la_clear(Tables t, const int32_t* olen, const int32_t* len) {
 
 // One in-place sweep.  G = 256/NP segments per workgroup, NP threads (columns)
 // per segment.  segs[s] = (chain, first position).
+// prev: the previous sweep's changed flag (nullptr for the first): sweeps are
+// queued in groups without a host round trip, and once one changes nothing
+// the rest of its group return at once.
 template <int NP>
 __global__ void __launch_bounds__(256) k_la_sweep(Tables t, const int2* segs, int nseg, int SEG,
-                                                  const int32_t* len, int32_t* changed) {
+                                                  const int32_t* len, const int32_t* prev,
+                                                  int32_t* changed) {
   constexpr int G = 256 / NP;
   constexpr int SEGMAX = 64;
   __shared__ int64_t s_off[G][SEGMAX];
+  if (prev && *prev == 0) return;  // converged: the flag stays 0
   const int N = t.N;
   const int g = threadIdx.x / NP, i = threadIdx.x - (threadIdx.x / NP) * NP;
   const int sidx = blockIdx.x * G + g;

@@ -163,6 +163,7 @@ struct hge_engine {
   std::vector<double> prof_ms;
   std::vector<int64_t> prof_cnt;
   int R_div = 0;            // Rounds() as seen by the consensus calls (DivideRounds)
+  std::vector<int32_t> h_minw;  // first witness id per round (update_rdiv)
   float stage_ms[7] = {};
 
   Tables tables() const {
@@ -206,9 +207,12 @@ struct hge_engine {
     chain_len.assign(N, 0);
     chain_last.assign(N, -1);
     coords_len.assign(N, 0);
-    ensure_events(std::max<int64_t>(cap, 1024));
-    ensure_ccap(std::max<int64_t>(64, 2 * std::max<int64_t>(cap, 1024) / N + 64));
-    ensure_rcap(std::max<int64_t>(64, std::max<int64_t>(cap, 1024) / SM + 8));
+    // chain tables: a creator's chain is ~cap/N long (binomial, sd ~ sqrt(cap/N));
+    // rounds: a round spans >= ~4N events in gossip.  Both grow on demand.
+    const int64_t c0 = std::max<int64_t>(cap, 1024);
+    ensure_events(c0);
+    ensure_ccap(c0 / N + c0 / (8 * N) + 64);
+    ensure_rcap(c0 / (2 * N) + 64);
   }
 
   void prof_begin(const char* name) {
@@ -390,6 +394,7 @@ struct hge_engine {
     coords_len.assign(N, 0);
     n_events = n_dev = n_coords = n_divided = 0;
     R = 0;
+    h_minw.clear();
     lcr = -1;
     lcre = 0;
     ctx = 0;
@@ -522,10 +527,15 @@ struct hge_engine {
         rounds_coop();
       } else {
         // first-strong-seer rows for every event that can still be a frontier member
-        s_fst.need(N + 1);
-        KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, s_len.p, s_len.p + N, s_fst.p);
-        std::vector<int32_t> fst(N + 1);
-        readback(fst.data(), s_fst.p, N + 1);
+        // (from a fresh state the frontier starts at round 0, position 0: no round trip)
+        bool fresh = R == 0;
+        for (int c = 0; c < N; c++) fresh = fresh && coords_len[c] == 0;
+        std::vector<int32_t> fst(N + 1, 0);
+        if (!fresh) {
+          s_fst.need(N + 1);
+          KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, s_len.p, s_len.p + N, s_fst.p);
+          readback(fst.data(), s_fst.p, N + 1);
+        }
         const int rlo = fst[0];
         const int Rprev = R;  // C rows >= Rprev are empty before this batch
         if (rlo != INF32) {
@@ -575,7 +585,7 @@ struct hge_engine {
     HIPCHK(hipMemsetAsync(s_small.p + 4, 0, 4, st));
     KLAUNCH(k_round_assign, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0,
                        (int)n1, R, s_newwit.p, s_small.p + 4);
-    KLAUNCH(k_witness_bits, dim3(div_up((int64_t)m * N, 256)), dim3(256), 0, st, t, s_newwit.p,
+    KLAUNCH(k_witness_bits, dim3(std::min(div_up((int64_t)m * N, 256), 8192)), dim3(256), 0, st, t, s_newwit.p,
             s_small.p + 4, N > 32 ? (const uint64_t*)d_ssc.p : nullptr);
     KLAUNCH(k_round_minw, dim3(div_up(R, 256)), dim3(256), 0, st, t, 0, R, d_minw.p);
     n_coords = n1;
@@ -645,20 +655,22 @@ struct hge_engine {
     HIPCHK(hipMemcpyAsync(s_segs.p, segs.data(), sizeof(int2) * nseg, hipMemcpyHostToDevice, st));
     KLAUNCH(k_la_clear, dim3(std::min(64, div_up((int64_t)maxnew * N, 256)), N), dim3(256), 0, st, t,
             olen, len);
-    // sweeps until one changes nothing (checked every GROUP sweeps)
-    const int GROUP = 4, MAXSW = 4096;
+    // sweeps until one changes nothing; queued in groups, checked once per group
+    // (a sweep after a quiet one returns at once)
+    const int MAXSW = 4096;
     s_chg.need(MAXSW);
     HIPCHK(hipMemsetAsync(s_chg.p, 0, 4 * MAXSW, st));
     const int NPt = N <= 16 ? 16 : N <= 32 ? 32 : N <= 64 ? 64 : N <= 128 ? 128 : 256;
     int sw = 0;
-    for (;;) {
-      for (int g = 0; g < GROUP; g++, sw++) {
+    for (int group = 12;; group = 8) {
+      for (int g = 0; g < group; g++, sw++) {
         if (sw >= MAXSW) throw EngineError(HGE_ERR_INTERNAL, "lastAncestors sweeps did not converge");
+        const int32_t* prev = sw > 0 ? s_chg.p + sw - 1 : nullptr;
         switch (NPt) {
 #define SW(NPV)                                                                                  \
   case NPV:                                                                                      \
     KLAUNCH(k_la_sweep<NPV>, dim3(div_up(nseg, 256 / NPV)), dim3(256), 0, st, t, s_segs.p, nseg, \
-            SEG, len, s_chg.p + sw);                                                             \
+            SEG, len, prev, s_chg.p + sw);                                                       \
     break;
           SW(16)
           SW(32)
@@ -685,9 +697,16 @@ struct hge_engine {
     KLAUNCH(k_fdt_runs, dim3(div_up(maxnew, 256), N, N), dim3(256), 0, st, t, d_LAT.p, d_FDT.p,
             olen, len);
     // FDT -> FD rows for every chain-c position a new event can have touched
-    KLAUNCH(k_fd_qlo, dim3(div_up(N, 256)), dim3(256), 0, st, t, olen, len, s_plo.p + N);
-    std::vector<int32_t> qlo(N);
-    readback(qlo.data(), s_plo.p + N, N);
+    // (from a fresh state: every row; no round trip)
+    bool fresh = true;
+    for (int c = 0; c < N; c++) fresh = fresh && coords_len[c] == 0;
+    std::vector<int32_t> qlo(N, 0);
+    if (fresh) {
+      HIPCHK(hipMemsetAsync(s_plo.p + N, 0, 4 * N, st));
+    } else {
+      KLAUNCH(k_fd_qlo, dim3(div_up(N, 256)), dim3(256), 0, st, t, olen, len, s_plo.p + N);
+      readback(qlo.data(), s_plo.p + N, N);
+    }
     int span = 1;
     for (int c = 0; c < N; c++) span = std::max(span, chain_len[c] - qlo[c]);
     KLAUNCH(k_transpose, dim3(div_up(span, 64), div_up(N, 64), N), dim3(256), 0, st, t, d_FDT.p,
@@ -705,11 +724,15 @@ struct hge_engine {
     Tables t = tables();
     s_nc.need(ncalls);
     HIPCHK(hipMemcpyAsync(s_nc.p, calls.data(), 8 * ncalls, hipMemcpyHostToDevice, st));
+    // R_c = Rounds() after the DivideRounds of call c = #{r : minw[r] < n_c}
+    // (minw is on the host since update_rdiv)
     s_Rc.need(ncalls);
-    KLAUNCH(k_calls_rounds, dim3(div_up(ncalls, 256)), dim3(256), 0, st, s_nc.p,
-                       ncalls, d_minw.p, R, s_Rc.p);
     std::vector<int32_t> Rc(ncalls);
-    readback(Rc.data(), s_Rc.p, ncalls);
+    for (int c = 0; c < ncalls; c++)
+      Rc[c] = (int32_t)(std::lower_bound(h_minw.begin(), h_minw.end(), calls[c],
+                                         [](int32_t m, int64_t n) { return (int64_t)m < n; }) -
+                        h_minw.begin());
+    HIPCHK(hipMemcpyAsync(s_Rc.p, Rc.data(), 4 * ncalls, hipMemcpyHostToDevice, st));
 
     // ---- DecideFame windows (host enumeration of (round, call) pairs) ----
     std::vector<int32_t> pr_round, pr_off, pr_cf, pr_len;
@@ -945,22 +968,38 @@ struct hge_engine {
     KLAUNCH(k_scan_add, dim3(div_up(n, 256)), dim3(256), 0, st, out, n, s_part.p + nb);
   }
 
+  // lanes per round in the group-scan kernels (N <= 64); 0 = thread-per-round kernels
+  int group_lanes() const { return N <= 16 ? 16 : N <= 32 ? 32 : N <= 64 ? 64 : 0; }
+
   void fame_dispatch(int which, const Tables& t, int nrounds, int npairs, int items, int ncalls) {
+    if (which == 1) {
+      KLAUNCH(k_fame_persist, dim3(div_up((int64_t)nrounds * N, 256)), dim3(256), 0, st, t, s_pr.p,
+              s_pr.p + nrounds, s_pr.p + 2 * nrounds, s_pr.p + 3 * nrounds, nrounds, s_clast.p,
+              s_dec.p);
+      return;
+    }
+    const int G = group_lanes();
     switch (NW) {
 #define FCASE(B)                                                                                 \
   case B:                                                                                        \
-    if (which == 0) {                                                                            \
-      KLAUNCH(k_fame_decide<B>, dim3(div_up(items, 256)), dim3(256), 0, st, t,        \
-                         s_pr.p, s_pr.p + nrounds, s_pr.p + 2 * nrounds, nrounds, npairs,        \
-                         s_nc.p, s_Rc.p, s_dec.p);                                               \
-      KLAUNCH(k_fame_timeline<B>, dim3(div_up(nrounds, 64)), dim3(64), 0, st, t,      \
-                         s_pr.p, s_pr.p + nrounds, s_pr.p + 2 * nrounds, s_pr.p + 3 * nrounds,   \
-                         nrounds, s_nc.p, s_dec.p, s_decbit.p, s_Lc.p);                          \
-    } else {                                                                                     \
-      KLAUNCH(k_fame_persist<B>, dim3(div_up(nrounds, 64)), dim3(64), 0, st, t,       \
-                         s_pr.p, s_pr.p + nrounds, s_pr.p + 2 * nrounds, s_pr.p + 3 * nrounds,   \
-                         nrounds, s_clast.p, s_dec.p);                                           \
-    }                                                                                            \
+    KLAUNCH(k_fame_decide<B>, dim3(div_up(items, 256)), dim3(256), 0, st, t, s_pr.p,             \
+            s_pr.p + nrounds, s_pr.p + 2 * nrounds, nrounds, npairs, s_nc.p, s_Rc.p, s_dec.p);   \
+    if (G == 16)                                                                                 \
+      KLAUNCH(k_fame_timeline_g<16>, dim3(div_up((int64_t)nrounds * 16, 256)), dim3(256), 0, st, \
+              t, s_pr.p, s_pr.p + nrounds, s_pr.p + 2 * nrounds, s_pr.p + 3 * nrounds, nrounds,  \
+              s_nc.p, s_dec.p, s_decbit.p, s_Lc.p);                                              \
+    else if (G == 32)                                                                            \
+      KLAUNCH(k_fame_timeline_g<32>, dim3(div_up((int64_t)nrounds * 32, 256)), dim3(256), 0, st, \
+              t, s_pr.p, s_pr.p + nrounds, s_pr.p + 2 * nrounds, s_pr.p + 3 * nrounds, nrounds,  \
+              s_nc.p, s_dec.p, s_decbit.p, s_Lc.p);                                              \
+    else if (G == 64)                                                                            \
+      KLAUNCH(k_fame_timeline_g<64>, dim3(div_up((int64_t)nrounds * 64, 256)), dim3(256), 0, st, \
+              t, s_pr.p, s_pr.p + nrounds, s_pr.p + 2 * nrounds, s_pr.p + 3 * nrounds, nrounds,  \
+              s_nc.p, s_dec.p, s_decbit.p, s_Lc.p);                                              \
+    else                                                                                         \
+      KLAUNCH(k_fame_timeline<B>, dim3(div_up(nrounds, 64)), dim3(64), 0, st, t, s_pr.p,         \
+              s_pr.p + nrounds, s_pr.p + 2 * nrounds, s_pr.p + 3 * nrounds, nrounds, s_nc.p,     \
+              s_dec.p, s_decbit.p, s_Lc.p);                                                      \
     break;
       FCASE(1)
       FCASE(2)
@@ -975,12 +1014,26 @@ struct hge_engine {
 
   void seg_dispatch(int mode, const Tables& t, int rr_lo, int nr, int ncalls, const SegInfo& si,
                     int nseg) {
+    const int G = group_lanes();
     switch (NW) {
 #define SCASE(B)                                                                                 \
   case B:                                                                                        \
-    KLAUNCH(k_segments<B>, dim3(div_up(nr, 64)), dim3(64), 0, st, t, rr_lo, nr,       \
-                       s_nc.p, ncalls, si, s_arr.p, s_segcnt.p, s_segoff.p, s_segcall.p, s_seground.p,    \
-                       s_segdec.p, s_segfws.p, mode);                                            \
+    if (G == 16)                                                                                 \
+      KLAUNCH(k_segments_g<16>, dim3(div_up((int64_t)nr * 16, 256)), dim3(256), 0, st, t, rr_lo, \
+              nr, s_nc.p, ncalls, si, s_arr.p, s_segcnt.p, s_segoff.p, s_segcall.p,              \
+              s_seground.p, s_segdec.p, s_segfws.p, mode);                                       \
+    else if (G == 32)                                                                            \
+      KLAUNCH(k_segments_g<32>, dim3(div_up((int64_t)nr * 32, 256)), dim3(256), 0, st, t, rr_lo, \
+              nr, s_nc.p, ncalls, si, s_arr.p, s_segcnt.p, s_segoff.p, s_segcall.p,              \
+              s_seground.p, s_segdec.p, s_segfws.p, mode);                                       \
+    else if (G == 64)                                                                            \
+      KLAUNCH(k_segments_g<64>, dim3(div_up((int64_t)nr * 64, 256)), dim3(256), 0, st, t, rr_lo, \
+              nr, s_nc.p, ncalls, si, s_arr.p, s_segcnt.p, s_segoff.p, s_segcall.p,              \
+              s_seground.p, s_segdec.p, s_segfws.p, mode);                                       \
+    else                                                                                         \
+      KLAUNCH(k_segments<B>, dim3(div_up(nr, 64)), dim3(64), 0, st, t, rr_lo, nr, s_nc.p,        \
+              ncalls, si, s_arr.p, s_segcnt.p, s_segoff.p, s_segcall.p, s_seground.p,            \
+              s_segdec.p, s_segfws.p, mode);                                                     \
     if (mode == 1 && nseg > 0)                                                                   \
       KLAUNCH(k_seg_theta<B>, dim3(div_up(nseg * N, 256)), dim3(256), 0, st, t,       \
                          rr_lo, s_seground.p, nseg, s_segfws.p, s_theta.p);                      \
@@ -1039,14 +1092,17 @@ struct hge_engine {
     update_rdiv();
   }
 
+  // first witness id of every round (host copy: Rounds() as seen at any event count)
   void update_rdiv() {
+    h_minw.resize(R);
     if (R == 0) {
       R_div = 0;
       return;
     }
-    std::vector<int32_t> mw(R);
-    readback(mw.data(), d_minw.p, R);
-    R_div = (int)(std::lower_bound(mw.begin(), mw.end(), (int32_t)std::min<int64_t>(n_divided, INF32)) - mw.begin());
+    readback(h_minw.data(), d_minw.p, R);
+    R_div = (int)(std::lower_bound(h_minw.begin(), h_minw.end(),
+                                   (int32_t)std::min<int64_t>(n_divided, INF32)) -
+                  h_minw.begin());
   }
 };
 
@@ -1199,6 +1255,7 @@ int hge_replay_run(hge_engine* h, int64_t* n_ordered) {
   h->n_coords = h->n_divided = 0;
   h->coords_len.assign(h->N, 0);
   h->R = 0;
+  h->h_minw.clear();
   h->lcr = -1;
   h->lcre = 0;
   h->ctx = 0;

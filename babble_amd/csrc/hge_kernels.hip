@@ -183,8 +183,8 @@ template <int NPC>
 __global__ void k_fss(Tables t, const int32_t* lo, const int32_t* off, int total,
                       int32_t* FSS) {
   const int N = t.N;
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  const int ev = g / NPC, c = g - (g / NPC) * NPC;
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int ev = (int)(g / NPC), c = (int)(g - (g / NPC) * NPC);
   if (ev >= total) return;
   int cw = 0;
   while (off[cw + 1] <= ev) cw++;
@@ -536,30 +536,32 @@ __global__ void k_calls_rounds(const int64_t* nc, int ncalls, const int32_t* min
 // ssc (wide path): strongly-see bits already produced by k_rounds_coop
 __global__ void k_witness_bits(Tables t, const int32_t* newwit, const int32_t* pnnew,
                                const uint64_t* ssc) {
-  const int item = blockIdx.x * blockDim.x + threadIdx.x;
+  // grid-stride over (new witness, slot) pairs; the count lives on the device
   const int N = t.N, NW = t.NW;
-  const int nnew = *pnnew;
-  if (item >= nnew * N) return;
-  const int y = newwit[item / N];
-  const int d = item - (item / N) * N;
-  const int j = t.round[y];
-  if (j == 0) return;
-  const int w = t.W[(size_t)(j - 1) * N + d];
-  if (w < 0) return;
-  const int cy = t.creator[y];
-  const int32_t* la = t.LA + rowoff(t, cy, t.index[y]);
-  const int32_t* fd = t.FD + rowoff(t, d, t.index[w]);
-  const bool see = la[d] >= t.index[w];
-  int c = 0;
-  if (ssc) {
-    c = ((ssc[((size_t)j * N + cy) * NW + (d >> 6)] >> (d & 63)) & 1ull) ? t.SM : 0;
-  } else {
-    for (int i = 0; i < N; i++) c += (la[i] >= fd[i]) ? 1 : 0;
+  const int64_t total = (int64_t)(*pnnew) * N;
+  for (int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; item < total;
+       item += (int64_t)gridDim.x * blockDim.x) {
+    const int y = newwit[item / N];
+    const int d = (int)(item - (item / N) * N);
+    const int j = t.round[y];
+    if (j == 0) continue;
+    const int w = t.W[(size_t)(j - 1) * N + d];
+    if (w < 0) continue;
+    const int cy = t.creator[y];
+    const int32_t* la = t.LA + rowoff(t, cy, t.index[y]);
+    const int32_t* fd = t.FD + rowoff(t, d, t.index[w]);
+    const bool see = la[d] >= t.index[w];
+    int c = 0;
+    if (ssc) {
+      c = ((ssc[((size_t)j * N + cy) * NW + (d >> 6)] >> (d & 63)) & 1ull) ? t.SM : 0;
+    } else {
+      for (int i = 0; i < N; i++) c += (la[i] >= fd[i]) ? 1 : 0;
+    }
+    const size_t off = ((size_t)j * N + cy) * NW + (d >> 6);
+    const uint64_t bit = 1ull << (d & 63);
+    if (see) atomicOr((unsigned long long*)&t.seeb[off], (unsigned long long)bit);
+    if (c >= t.SM) atomicOr((unsigned long long*)&t.ssb[off], (unsigned long long)bit);
   }
-  const size_t off = ((size_t)j * N + cy) * NW + (d >> 6);
-  const uint64_t bit = 1ull << (d & 63);
-  if (see) atomicOr((unsigned long long*)&t.seeb[off], (unsigned long long)bit);
-  if (c >= t.SM) atomicOr((unsigned long long*)&t.ssb[off], (unsigned long long)bit);
 }
 
 // ---------------------------------------------------------------------------
@@ -739,23 +741,71 @@ __global__ void __launch_bounds__(1024) k_lcr_scan(const int32_t* Lc, int ncalls
   }
 }
 
-// persisted fame after the batch: decisions up to c_last(i)
-template <int NWT>
+// persisted fame after the batch: decisions up to c_last(i); one lane per
+// (processed round, witness slot), coalesced over the slots
 __global__ void k_fame_persist(Tables t, const int32_t* pr_round, const int32_t* pr_off,
                                const int32_t* pr_cf, const int32_t* pr_len, int nrounds,
                                const int32_t* clast, const uint8_t* dec) {
-  const int ri = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ri >= nrounds) return;
   const int N = t.N;
+  const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int ri = (int)(item / N), d = (int)(item - (item / N) * N);
+  if (ri >= nrounds) return;
   const int i = pr_round[ri];
   const int qend = min(pr_len[ri], clast[ri] - pr_cf[ri] + 1);
-  for (int d = 0; d < N; d++) {
-    uint8_t f = t.fame[(size_t)i * N + d];
-    for (int q = 0; q < qend; q++) {
-      const uint8_t o = dec[(size_t)(pr_off[ri] + q) * N + d];
-      if (o) f = o;
+  uint8_t f = t.fame[(size_t)i * N + d];
+  for (int q = 0; q < qend; q++) {
+    const uint8_t o = dec[(size_t)(pr_off[ri] + q) * N + d];
+    if (o) f = o;
+  }
+  t.fame[(size_t)i * N + d] = f;
+}
+
+// ---------------------------------------------------------------------------
+// N <= 64: the per-round scans below run one G-lane group per round (lane =
+// witness slot d, G = 16/32/64) instead of one thread per round, so the N-wide
+// inner loops become one coalesced load and a masked ballot per step.
+// ---------------------------------------------------------------------------
+template <int G>
+__device__ __forceinline__ uint64_t group_mask(int lane) {
+  return (G == 64) ? ~0ull : (((1ull << G) - 1) << (lane & ~(G - 1)));
+}
+
+template <int G>
+__device__ __forceinline__ int group_min(int v) {
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) v = min(v, __shfl_xor(v, o));
+  return v;
+}
+
+// k_fame_timeline with one group per processed round
+template <int G>
+__global__ void __launch_bounds__(256) k_fame_timeline_g(Tables t, const int32_t* pr_round,
+                                                         const int32_t* pr_off, const int32_t* pr_cf,
+                                                         const int32_t* pr_len, int nrounds,
+                                                         const int64_t* nc, const uint8_t* dec,
+                                                         uint8_t* decbit, int32_t* Lc) {
+  const int N = t.N;
+  const int lane = threadIdx.x & 63, d = lane & (G - 1);
+  const int ri = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G);
+  const uint64_t gm = group_mask<G>(lane);
+  const bool valid = ri < nrounds;  // uniform per group
+  const int i = valid ? pr_round[ri] : 0;
+  bool known = false;
+  int x = -1;
+  if (valid && d < N) {
+    known = t.fame[(size_t)i * N + d] != 0;
+    x = t.W[(size_t)i * N + d];
+  }
+  const int len = valid ? pr_len[ri] : 0;
+  for (int q = 0; q < len; q++) {
+    const int p = pr_off[ri] + q, c = pr_cf[ri] + q;
+    const int64_t n = nc[c];
+    if (d < N && dec[(size_t)p * N + d]) known = true;
+    const uint64_t und = __ballot(d < N && x >= 0 && x < n && !known) & gm;
+    if (d == 0) {
+      decbit[p] = und == 0 ? 1 : 0;
+      if (und == 0) atomicMax(&Lc[c], i);
     }
-    t.fame[(size_t)i * N + d] = f;
   }
 }
 
@@ -872,6 +922,71 @@ __global__ void k_segments(Tables t, int rr_lo, int nr, const int64_t* nc, int n
     c = nxt;
   }
   if (!mode) segcnt[q] = nseg;
+}
+
+// k_segments with one group per round (N <= 64: the famous set is one word)
+template <int G>
+__global__ void __launch_bounds__(256) k_segments_g(Tables t, int rr_lo, int nr, const int64_t* nc,
+                                                    int ncalls, SegInfo si, const int32_t* arr,
+                                                    int32_t* segcnt, const int32_t* segoff,
+                                                    int32_t* seg_call, int32_t* seg_round,
+                                                    uint8_t* seg_dec, uint64_t* seg_fws, int mode) {
+  const int N = t.N;
+  const int lane = threadIdx.x & 63, d = lane & (G - 1);
+  const int qi = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G);
+  const uint64_t gm = group_mask<G>(lane);
+  const int gshift = (G == 64) ? 0 : (lane & ~(G - 1));
+  const bool valid = qi < nr;  // uniform per group
+  const int i = rr_lo + (valid ? qi : 0);
+  const bool slot = valid && d < N;
+  const int a = slot ? arr[(size_t)qi * N + d] : INF32;
+  bool known = false, val = false;
+  if (slot) {
+    const uint8_t f = t.fame[(size_t)i * N + d];  // persisted BEFORE this batch's update
+    known = f != 0;
+    val = f == 1;
+  }
+  const int pi = valid ? si.pr_index[qi] : -1;
+  const int cf = pi >= 0 ? si.pr_cf[pi] : INF32;
+  const int wl = pi >= 0 ? min(si.pr_len[pi], si.clast[pi] - cf + 1) : 0;  // processed calls
+  const int poff = pi >= 0 ? si.pr_off[pi] : 0;
+  int prevdec = -1, nseg = 0;
+  uint64_t prevf = 0;
+  const int base = (mode && valid) ? segoff[qi] : 0;
+  int c = valid ? 0 : INF32;
+  while (c < ncalls) {
+    int nxt = group_min<G>((slot && a > c) ? a : INF32);
+    const bool pres = slot && a <= c;
+    if (c >= cf && c - cf < wl && slot) {
+      const uint8_t o = si.dec[(size_t)(poff + (c - cf)) * N + d];
+      if (o) {
+        known = true;
+        val = (o == 1);
+      }
+    }
+    const uint64_t bp = __ballot(pres) & gm;
+    const uint64_t und = __ballot(pres && !known) & gm;
+    const uint64_t fws = (__ballot(pres && known && val) & gm) >> gshift;
+    const bool decided = und == 0;
+    if (bp && (prevdec != (int)decided || fws != prevf)) {
+      if (mode && d == 0) {
+        const int sidx = base + nseg;
+        seg_call[sidx] = c;
+        seg_round[sidx] = i;
+        seg_dec[sidx] = decided ? 1 : 0;
+        seg_fws[sidx] = fws;
+      }
+      nseg++;
+      prevdec = decided;
+      prevf = fws;
+    }
+    // next change point: an arrival, or the next call DecideFame processes round i
+    if (c + 1 >= cf && c + 1 - cf < wl) nxt = min(nxt, c + 1);
+    else if (c + 1 < cf && wl > 0) nxt = min(nxt, cf);
+    if (nxt <= c) nxt = c + 1;
+    c = nxt;
+  }
+  if (!mode && valid && d == 0) segcnt[qi] = nseg;
 }
 
 // theta[seg][cx] = the (|fws|/2 + 1)-th largest LA[w][cx] over famous witnesses

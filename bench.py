@@ -171,11 +171,27 @@ def main():
         dist.all_reduce(oo, op=dist.ReduceOp.SUM)
         tot_ordered = int(oo.item())
 
-    dom, (dom_ms, dom_n) = max(kstats.items(), key=lambda kv: kv[1][0])
-    per_launch_ms = dom_ms / max(dom_n, 1)
-    launches_per_replay = max(dom_n // max(1, args.profile_steps), 1)
-    alg = algorithmic_bytes(dom, n, ev0, ord0) / launches_per_replay
-    achieved = alg / (per_launch_ms * 1e-3) / 1e9
+    nprof = max(1, args.profile_steps)
+
+    def kernel_gbs(name):
+        """(algorithmic bytes per launch, avg launch ms, achieved GB/s) of one kernel."""
+        ms, cnt = kstats[name]
+        per_launch = ms / max(cnt, 1)
+        launches = max(cnt // nprof, 1)
+        b = algorithmic_bytes(name, n, ev0, ord0) / launches
+        return b, per_launch, b / (per_launch * 1e-3) / 1e9
+
+    dom = max(kstats.items(), key=lambda kv: kv[1][0])[0]
+    alg, per_launch_ms, achieved = kernel_gbs(dom)
+    # the bandwidth-bound kernels (streaming passes over the N-wide tables)
+    hbm_kernels = {}
+    for name in kstats:
+        base = name.strip("()").split("<")[0]
+        if base in ("k_la_sweep", "k_transpose", "k_fss", "k_fdt_runs"):
+            b, pl, gbs = kernel_gbs(name)
+            hbm_kernels[name] = {"achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                 "launch_ms": round(pl, 4),
+                                 "launches_per_replay": kstats[name][1] // nprof}
 
     cpu, parity = None, None
     if rank == 0 and not args.no_cpu_baseline:
@@ -226,12 +242,14 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic(dom),
                          "algorithmic_bytes_per_launch": int(alg),
-                         "launch_ms": round(per_launch_ms, 4)},
+                         "launch_ms": round(per_launch_ms, 4),
+                         "hbm_kernels": hbm_kernels},
             "cpu_baseline": cpu,
             "parity": parity,
             "ingest_host_ms": round(ingest_s * 1e3, 2),
-            "kernels_ms_per_replay": {k: round(v[0] / max(1, args.profile_steps), 4) for k, v in
+            "kernels_ms_per_replay": {k: round(v[0] / nprof, 4) for k, v in
                                       sorted(kstats.items(), key=lambda kv: -kv[1][0])},
+            "kernel_launches_per_replay": {k: v[1] // nprof for k, v in kstats.items()},
         }
         print(json.dumps(line), flush=True)
     pool.shutdown()
