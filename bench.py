@@ -64,16 +64,17 @@ def algorithmic_bytes(kernel, n, events, ordered):
     return 48 * ordered
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (profiles/pmc_traffic.json, made by scripts/pmc_traffic.py), or None."""
+def pmc_traffic(config_key, kernel):
+    """HBM bytes per launch of `kernel` in this configuration from the committed
+    rocprofv3 PMC passes (profiles/pmc_traffic.json, made by
+    scripts/pmc_traffic.py on the GPU box), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         pm = json.load(open(path))
     except (OSError, ValueError):
         return None
     name = kernel.strip("()").split("<")[0]
-    v = pm.get("kernels", {}).get(name)
+    v = pm.get("configs", {}).get(config_key, {}).get(name)
     return v.get("bytes_per_launch") if isinstance(v, dict) else None
 
 
@@ -240,7 +241,8 @@ def main():
                        "parallelism": f"replicas{world}"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc_traffic(dom),
+                         "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": pmc_traffic(f"{args.workload}_n{n}_e{E}_k{K}", dom),
                          "algorithmic_bytes_per_launch": int(alg),
                          "launch_ms": round(per_launch_ms, 4),
                          "hbm_kernels": hbm_kernels},
