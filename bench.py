@@ -110,14 +110,14 @@ def main():
         dist_.init_process_group("nccl")
         dist = dist_
 
+    from babble_amd.dist import reduce_step, shard_range
     from babble_amd.engine import Engine, events_array
     from babble_amd.gossip import random_gossip, schedule
 
     # ---- stage the workload in HBM (host admission + upload; not timed) ----
     t0 = time.perf_counter()
     if mc:
-        per = args.graphs // world + (1 if rank < args.graphs % world else 0)
-        first = rank * (args.graphs // world) + min(rank, args.graphs % world)
+        first, per = shard_range(args.graphs, world, rank)
         dags = [random_gossip(n, E, seed=args.seed + first + g, forkers=10, fork_p=0.05)
                 for g in range(per)]
         engines = [Engine(n, len(d["creator"]) + 64, device=local_rank) for d in dags]
@@ -164,13 +164,7 @@ def main():
 
     tot_ordered, max_step = ordered, step_s
     if dist is not None:
-        import torch
-        tt = torch.tensor([step_s], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        max_step = float(tt.item())
-        oo = torch.tensor([ordered], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(oo, op=dist.ReduceOp.SUM)
-        tot_ordered = int(oo.item())
+        max_step, tot_ordered = reduce_step(dist, step_s, ordered, f"cuda:{local_rank}")
 
     nprof = max(1, args.profile_steps)
 
