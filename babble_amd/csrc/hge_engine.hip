@@ -643,12 +643,19 @@ struct hge_engine {
     const int32_t* len = s_len.p + N;
     int maxnew = 0, maxlen = 0;
     std::vector<int2> segs;
-    const int SEG = 64;
+    // segment length: short segments give more workgroups, long ones fewer stale carries
+    static const int SEG = getenv("HGE_SEG") ? std::max(1, std::min(64, atoi(getenv("HGE_SEG")))) : 64;
     for (int c = 0; c < N; c++) {
       maxnew = std::max(maxnew, chain_len[c] - coords_len[c] + 1);
       maxlen = std::max(maxlen, chain_len[c]);
       for (int k = coords_len[c]; k < chain_len[c]; k += SEG) segs.push_back(make_int2(c, k));
     }
+    // position-major order: workgroups are dispatched roughly in index order, so
+    // early positions of every chain are swept first and later segments read
+    // rows already updated in this sweep (Gauss-Seidel in time order)
+    if (!getenv("HGE_SEG_CHAIN_MAJOR"))
+      std::stable_sort(segs.begin(), segs.end(),
+                       [](const int2& a, const int2& b) { return a.y < b.y; });
     const int nseg = (int)segs.size();
     if (nseg == 0) return;
     s_segs.need(nseg);
@@ -680,11 +687,14 @@ struct hge_engine {
 #undef SW
         }
       }
-      int32_t last = 1;
-      readback(&last, s_chg.p + sw - 1, 1);
-      if (!last) break;
+      std::vector<int32_t> flags(sw);
+      readback(flags.data(), s_chg.p, sw);
+      if (!flags[sw - 1]) {
+        // sweeps that did work: up to and including the first one that changed nothing
+        n_sweeps = (int)(std::find(flags.begin(), flags.end(), 0) - flags.begin()) + 1;
+        break;
+      }
     }
-    n_sweeps = sw;
     // LA -> LAT for positions [olen-1, len)
     std::vector<int32_t> plo(N);
     for (int c = 0; c < N; c++) plo[c] = std::max(coords_len[c] - 1, 0);
@@ -1498,6 +1508,8 @@ int hge_kernel_stats(hge_engine* h, int k, char* name, int namecap, double* tota
   if (launches) *launches = h->prof_cnt[k];
   return n;
 }
+
+int32_t hge_coordinate_sweeps(hge_engine* h) { return h ? h->n_sweeps : -1; }
 
 int hge_stage_times(hge_engine* h, float* ms_out, int cap) {
   int n = std::min(cap, 7);

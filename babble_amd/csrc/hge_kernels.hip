@@ -481,26 +481,44 @@ __global__ void k_frontier_start(Tables t, const int32_t* olen, const int32_t* l
 }
 
 // round(x) = max r with C[r][cx] <= px; witness iff C[round][cx] == px
+// (consecutive events share a round: the per-round counts and the new-witness
+// slots are aggregated per wave before touching global atomics)
 __global__ void k_round_assign(Tables t, int n0, int n1, int R, int32_t* newwit,
                                int32_t* nnewwit) {
   const int x = n0 + blockIdx.x * blockDim.x + threadIdx.x;
-  if (x >= n1) return;
+  const bool valid = x < n1;
   const int N = t.N;
-  const int cx = t.creator[x], px = t.index[x];
-  int lo = 0, hi = R - 1;  // C[0][cx] == 0 <= px
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (t.C[(size_t)mid * N + cx] <= px) lo = mid;
-    else hi = mid - 1;
+  const int lane = threadIdx.x & 63;
+  int lo = 0;
+  bool w = false;
+  if (valid) {
+    const int cx = t.creator[x], px = t.index[x];
+    int hi = R - 1;  // C[0][cx] == 0 <= px
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (t.C[(size_t)mid * N + cx] <= px) lo = mid;
+      else hi = mid - 1;
+    }
+    t.round[x] = lo;
+    w = (t.C[(size_t)lo * N + cx] == px);
+    t.wit[x] = w ? 1 : 0;
+    if (w) t.W[(size_t)lo * N + cx] = x;
   }
-  t.round[x] = lo;
-  const bool w = (t.C[(size_t)lo * N + cx] == px);
-  t.wit[x] = w ? 1 : 0;
-  atomicAdd(&t.rcnt[lo], 1);
-  if (w) {
-    t.W[(size_t)lo * N + cx] = x;
-    const int slot = atomicAdd(nnewwit, 1);
-    newwit[slot] = x;
+  uint64_t pending = __ballot(valid);
+  while (pending) {
+    const int leader = __builtin_ctzll(pending);
+    const int r = __shfl(lo, leader);
+    const uint64_t same = __ballot(valid && lo == r);
+    if (lane == leader) atomicAdd(&t.rcnt[r], __popcll(same));
+    pending &= ~same;
+  }
+  const uint64_t wm = __ballot(w);
+  if (wm) {
+    const int leader = __builtin_ctzll(wm);
+    int base = 0;
+    if (lane == leader) base = atomicAdd(nnewwit, __popcll(wm));
+    base = __shfl(base, leader);
+    if (w) newwit[base + __popcll(wm & ((1ull << lane) - 1))] = x;
   }
 }
 

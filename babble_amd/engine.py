@@ -59,7 +59,7 @@ EXPORTS = [
     "hge_undetermined", "hge_known", "hge_round_of", "hge_is_witness", "hge_round_witness",
     "hge_fame", "hge_round_events", "hge_round_received", "hge_consensus_timestamp",
     "hge_ancestor", "hge_self_ancestor", "hge_see", "hge_strongly_see",
-    "hge_oldest_self_ancestor_to_see", "hge_coordinates", "hge_stage_times",
+    "hge_oldest_self_ancestor_to_see", "hge_coordinates", "hge_coordinate_sweeps", "hge_stage_times",
     "hge_set_profiling", "hge_reset_kernel_stats", "hge_kernel_stats",
 ]
 
@@ -119,6 +119,8 @@ def lib():
         getattr(L, f).restype = i32
     L.hge_coordinates.argtypes = [vp, i32, P(i32), P(i32)]
     L.hge_stage_times.argtypes = [vp, P(ctypes.c_float), ctypes.c_int]
+    L.hge_coordinate_sweeps.restype = ctypes.c_int32
+    L.hge_coordinate_sweeps.argtypes = [vp]
     L.hge_set_profiling.argtypes = [vp, ctypes.c_int]
     L.hge_reset_kernel_stats.argtypes = [vp]
     L.hge_kernel_stats.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
@@ -265,6 +267,10 @@ class Engine:
             self.L.hge_kernel_stats(self.h, k, buf, 128, ctypes.byref(ms), ctypes.byref(cnt))
             out[buf.value.decode()] = (ms.value, cnt.value)
         return out
+
+    def coordinate_sweeps(self):
+        """lastAncestors sweeps of the last coordinate pass (hge_coords.hip)."""
+        return self.L.hge_coordinate_sweeps(self.h)
 
     def stage_times(self):
         out = (ctypes.c_float * 7)()

@@ -134,6 +134,9 @@ int hge_coordinates(hge_engine* h, int32_t id, int32_t* la_out, int32_t* fd_out)
  * engine's stream): 0 coords, 1 rounds, 2 witness bits, 3 fame, 4 received,
  * 5 order, 6 total.  Returns the number of stages written. */
 int hge_stage_times(hge_engine* h, float* ms_out, int cap);
+/* lastAncestors sweeps the last coordinate pass needed (hge_coords.hip): each
+ * streams the new rows once; the last one confirms the fixed point. */
+int32_t hge_coordinate_sweeps(hge_engine* h);
 /* Per-kernel timing: HIP events around every launch on the engine stream. */
 int hge_set_profiling(hge_engine* h, int on);
 int hge_reset_kernel_stats(hge_engine* h);
