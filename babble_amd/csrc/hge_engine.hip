@@ -355,7 +355,9 @@ struct hge_engine {
     d_chain.n = (size_t)N * nc;
     grow_chain_table(d_LA, nc, true);
     grow_chain_table(d_FD, nc, true);
-    if (N <= 32) grow_chain_table(d_FSS, nc, true);  // first-strong-seer rows (walk, N <= 32)
+    // first-strong-seer rows (N <= 32): int32 rows of N, or uint16 rows padded to
+    // 16/32 columns for the LDS walk; rebuilt from the frontier on, never kept
+    if (N <= 32) d_FSS.need((size_t)N * nc * std::max(N, 16));
     grow_chain_table(d_LAT, nc, false, false);      // rebuilt per batch from LA
     grow_chain_table(d_FDT, nc, true, false);       // persistent: FD in run layout
     ccap = (int)nc;
@@ -555,14 +557,17 @@ struct hge_engine {
             // the LDS walk keeps chain positions as uint16; longer chains take the
             // register walk over the global fss rows
 #define FSSL(NPC, LPC, B)                                                                          \
-  KLAUNCH(k_fss<NPC>, dim3(div_up((int64_t)tot * NPC, 256)), dim3(256), 0, st, t, s_fsslo.p,       \
-          s_fsslo.p + N, tot, d_FSS.p);                                                            \
-  if (maxlen < 0xFFFF)                                                                             \
-    KLAUNCH((k_rounds_walk<NPC, LPC, B>), dim3(1), dim3(1024), 0, st, t, d_FSS.p, s_len.p,         \
-            s_len.p + N, s_small.p, rlo, Rprev);                                                   \
-  else                                                                                             \
+  if (maxlen < 0xFFFF) {                                                                           \
+    KLAUNCH(k_fss<NPC>, dim3(div_up((int64_t)tot * NPC, 256)), dim3(256), 0, st, t, s_fsslo.p,     \
+            s_fsslo.p + N, tot, (int32_t*)nullptr, (uint16_t*)d_FSS.p);                            \
+    KLAUNCH((k_rounds_walk<NPC, LPC, B>), dim3(1), dim3(1024), 0, st, t,                           \
+            (const uint16_t*)d_FSS.p, s_len.p, s_len.p + N, s_small.p, rlo, Rprev, dbg_p());       \
+  } else {                                                                                         \
+    KLAUNCH(k_fss<NPC>, dim3(div_up((int64_t)tot * NPC, 256)), dim3(256), 0, st, t, s_fsslo.p,     \
+            s_fsslo.p + N, tot, d_FSS.p, (uint16_t*)nullptr);                                      \
     KLAUNCH(k_rounds_fss<NPC>, dim3(1), dim3(64), 0, st, t, d_FSS.p, s_len.p, s_len.p + N,        \
-            s_small.p, rlo);
+            s_small.p, rlo);                                                                       \
+  }
             if (NP == 16) {
               FSSL(16, 4, 256)
             } else {

@@ -178,10 +178,13 @@ __device__ __forceinline__ int select_kth(int (&v)[NPC], int k) {
   return r;
 }
 
-// one lane per (event w, target chain c); events of chain cw from position lo[cw]
+// one lane per (event w, target chain c); events of chain cw from position lo[cw].
+// FSS16 (non-null: the LDS walk) receives uint16 rows padded to NPC columns
+// (INF and the padding = 0xFFFF) with the own-chain entry already clamped to
+// pw + 1 (an event never strongly sees itself); otherwise int32 rows of N.
 template <int NPC>
 __global__ void k_fss(Tables t, const int32_t* lo, const int32_t* off, int total,
-                      int32_t* FSS) {
+                      int32_t* FSS, uint16_t* FSS16) {
   const int N = t.N;
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int ev = (int)(g / NPC), c = (int)(g - (g / NPC) * NPC);
@@ -199,7 +202,13 @@ __global__ void k_fss(Tables t, const int32_t* lo, const int32_t* off, int total
       if (z != INF32 && c < N) v[i] = t.FD[rowoff(t, i, z) + c];
     }
   }
-  if (c < N) FSS[rowoff(t, cw, pw) + c] = select_kth<NPC>(v, t.SM);
+  int f = (c < N) ? select_kth<NPC>(v, t.SM) : INF32;
+  if (FSS16) {
+    if (c == cw && f != INF32) f = max(f, pw + 1);
+    FSS16[((size_t)cw * t.ccap + pw) * NPC + c] = (f == INF32) ? 0xFFFF : (uint16_t)f;
+  } else if (c < N) {
+    FSS[rowoff(t, cw, pw) + c] = f;
+  }
 }
 
 // the sequential frontier walk: one wave, lane = chain
@@ -247,34 +256,46 @@ __global__ void __launch_bounds__(64) k_rounds_fss(Tables t, const int32_t* FSS,
   if (c == 0) rstate[0] = max(rstate[0], r + 1);
 }
 
+// ---------------------------------------------------------------------------
 // The frontier walk (C_{r+1}[c] = SM-th smallest over d of fss_c(C_r[d])).
 // Every step depends on the previous one, so the walk is latency-bound and
 // runs in ONE wave with no barriers: lane (c, q) = chain c, quarter q of the
 // d range (LPC lanes per chain, VPL = NPC/LPC values per lane).  A step is
-// VPL LDS gathers, a bitonic network over the NPC values of each chain whose
-// in-lane stages are register min/max and whose cross-lane stages are DPP
-// quad permutes, and one LDS store of the new frontier.  Global traffic is
-// taken out of the step entirely: all 16 waves stage blocks of fss rows
-// [P_d, P_d + B) of every chain into LDS as uint16 (chain positions < 65535,
-// checked by the host) together with the already-known C rows of the next RB
-// rounds; the walk buffers its C rows in LDS and they are flushed at the next
-// restage.
+// VPL LDS gathers of uint16 fss values (0xFFFF = none), an all-ascending
+// bitonic network over the NPC values of each chain whose in-lane stages are
+// register min/max and whose cross-lane stages are DPP quad permutes, and one
+// LDS store of the new frontier.  Global traffic is taken out of the step:
+// all 16 waves stage blocks of uint16 fss rows [P_d, P_d + B) of every chain
+// into LDS (chain positions < 65535, checked by the host) together with the
+// already-known C rows of the next RB rounds; the walk buffers its C rows in
+// LDS and they are flushed at the next restage.  The own-chain clamp (an
+// event never strongly sees itself) is folded into the rows by k_fss.
 // ---------------------------------------------------------------------------
+// lane l reads lane l ^ X within its quad (X in 1..3): quad_perm DPP
 template <int X>
-__device__ __forceinline__ int dpp_xor(int v) {
-  static_assert(X == 1 || X == 2, "quad permutes only");
-  // quad_perm [1,0,3,2] = 0xB1, [2,3,0,1] = 0x4E
-  return __builtin_amdgcn_mov_dpp(v, X == 1 ? 0xB1 : 0x4E, 0xF, 0xF, false);
+__device__ __forceinline__ int dpp_flip(int v) {
+  static_assert(X >= 1 && X <= 3, "quad permutes only");
+  constexpr int ctrl = (0 ^ X) | ((1 ^ X) << 2) | ((2 ^ X) << 4) | ((3 ^ X) << 6);
+  return __builtin_amdgcn_mov_dpp(v, ctrl, 0xF, 0xF, false);
+}
+
+// the same with the distance as a value (constant after unrolling)
+__device__ __forceinline__ int dpp_flip(int x, int v) {
+  return x == 1 ? dpp_flip<1>(v) : x == 2 ? dpp_flip<2>(v) : dpp_flip<3>(v);
 }
 
 template <int NPC, int LPC, int B>
-__global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const int32_t* FSS,
+__global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* FSS,
                                                       const int32_t* olen, const int32_t* len,
-                                                      int32_t* rstate, int rlo, int Rprev) {
+                                                      int32_t* rstate, int rlo, int Rprev,
+                                                      uint64_t* dbg) {
   constexpr int VPL = NPC / LPC;
-  constexpr int RB = 64;  // C rows buffered per restage
+  constexpr int RB = 64;       // C rows buffered per restage
+  constexpr int Q8 = NPC / 8;  // int4 loads per fss row
   static_assert(NPC * LPC == 64, "one wave walks");
+  uint64_t wst[4] = {0, 0, 0, 0}, wt = 0;  // HGE_STAMPS: restage cycles, walk cycles, restages, steps
   __shared__ __attribute__((aligned(16))) uint16_t blk[NPC * B * NPC];  // [d][k][c]
+  __shared__ __attribute__((aligned(16))) uint16_t sInf[NPC];           // gathers of absent members
   __shared__ __attribute__((aligned(16))) int sP[NPC];
   __shared__ int sBase[NPC], sLen[NPC], sC[RB * NPC];
   __shared__ int s_r, s_done, s_nr;
@@ -293,6 +314,7 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const int32_t* F
     }
     sP[c] = P;
     sLen[c] = ln;
+    sInf[c] = 0xFFFF;
   }
   if (tid == 0) {
     s_r = rlo;
@@ -301,44 +323,31 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const int32_t* F
   __syncthreads();
   for (;;) {
     const int r0 = s_r;
-    // ---- restage: fss rows [P_d, P_d + B) of every chain, 4 columns per item;
-    //      all loads of a thread are in flight before the first LDS store
-    constexpr int ITEMS = NPC * B * (NPC / 4);
+    if (dbg && tid == 0) wt = stamp();
+    // ---- restage: uint16 fss rows [P_d, P_d + B) of every chain, 8 values per
+    //      int4; all loads of a thread are in flight before the first LDS store
+    constexpr int ITEMS = NPC * B * Q8;
     constexpr int PER = (ITEMS + 1023) / 1024;  // launched with 1024 threads
     int4 vals[PER];
 #pragma unroll
     for (int m = 0; m < PER; m++) {
       const int item = tid + m * 1024;
-      const int d = item / (B * (NPC / 4));
-      const int rem = item - d * (B * (NPC / 4));
-      const int k = rem / (NPC / 4), q4 = rem - k * (NPC / 4);
-      int4 w = make_int4(INF32, INF32, INF32, INF32);
-      if (item < ITEMS && d < N && sP[d] != INF32 && sP[d] + k < sLen[d]) {
-        const int32_t* row = FSS + rowoff(t, d, sP[d] + k) + 4 * q4;
-        if ((N & 3) == 0) {
-          if (4 * q4 < N) w = *(const int4*)row;
-        } else {
-          if (4 * q4 + 0 < N) w.x = row[0];
-          if (4 * q4 + 1 < N) w.y = row[1];
-          if (4 * q4 + 2 < N) w.z = row[2];
-          if (4 * q4 + 3 < N) w.w = row[3];
-        }
-      }
+      const int d = item / (B * Q8);
+      const int rem = item - d * (B * Q8);
+      const int k = rem / Q8, q8 = rem - k * Q8;
+      int4 w = make_int4(-1, -1, -1, -1);  // 0xFFFF x 8
+      if (item < ITEMS && d < N && sP[d] != INF32 && sP[d] + k < sLen[d])
+        w = *(const int4*)(FSS + ((size_t)d * t.ccap + sP[d] + k) * NPC + 8 * q8);
       vals[m] = w;
     }
 #pragma unroll
     for (int m = 0; m < PER; m++) {
       const int item = tid + m * 1024;
       if (item >= ITEMS) break;
-      const int d = item / (B * (NPC / 4));
-      const int rem = item - d * (B * (NPC / 4));
-      const int k = rem / (NPC / 4), q4 = rem - k * (NPC / 4);
-      const int4 w = vals[m];
-      const uint32_t lo = (uint32_t)(w.x == INF32 ? 0xFFFF : w.x) |
-                          ((uint32_t)(w.y == INF32 ? 0xFFFF : w.y) << 16);
-      const uint32_t hi = (uint32_t)(w.z == INF32 ? 0xFFFF : w.z) |
-                          ((uint32_t)(w.w == INF32 ? 0xFFFF : w.w) << 16);
-      *(uint2*)&blk[(d * B + k) * NPC + 4 * q4] = make_uint2(lo, hi);
+      const int d = item / (B * Q8);
+      const int rem = item - d * (B * Q8);
+      const int k = rem / Q8, q8 = rem - k * Q8;
+      *(int4*)&blk[(d * B + k) * NPC + 8 * q8] = vals[m];
     }
     // the next RB rounds' C rows as stored before this kernel (rows < Rprev)
     for (int item = tid; item < RB * NPC; item += T) {
@@ -348,6 +357,12 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const int32_t* F
     }
     if (tid < NPC) sBase[tid] = sP[tid];
     __syncthreads();
+    if (dbg && tid == 0) {
+      const uint64_t now = stamp();
+      wst[0] += now - wt;
+      wt = now;
+      wst[2]++;
+    }
     // ---- wave 0 walks from LDS only
     if (tid < 64) {
       const int lane = tid;
@@ -355,7 +370,9 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const int32_t* F
       const bool act = c < N;
       const int ln = sLen[c];
       const int base_c = sBase[c];
-      int bd[VPL];
+      const int qo = (SM - 1) / VPL, ko = (SM - 1) - qo * VPL;
+      const bool owner = act && q == qo;
+      int bd[VPL];  // per-slot block bases; absent members gather from sInf
 #pragma unroll
       for (int k = 0; k < VPL; k++) bd[k] = sBase[q * VPL + k];
       int r = r0;
@@ -367,66 +384,77 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const int32_t* F
           break;
         }
         if (r - r0 >= RB) break;  // C buffer full
-        const int Pc = sP[c];
-        if (__ballot(act && Pc != INF32 && Pc - base_c >= B)) break;  // leave the block
-        // branch-free gathers: all VPL LDS reads issue back to back
         int Pv[VPL], v[VPL];
 #pragma unroll
         for (int k = 0; k < VPL; k++) Pv[k] = sP[q * VPL + k];
 #pragma unroll
         for (int k = 0; k < VPL; k++) {
           const int d = q * VPL + k;
-          const int off = (Pv[k] != INF32) ? Pv[k] - bd[k] : 0;
-          v[k] = blk[(d * B + off) * NPC + c];
+          const uint16_t* src = (Pv[k] != INF32) ? &blk[(d * B + (Pv[k] - bd[k])) * NPC + c]
+                                                 : &sInf[c];
+          v[k] = *src;
         }
-#pragma unroll
-        for (int k = 0; k < VPL; k++) {
-          const int d = q * VPL + k;
-          int x = (Pv[k] == INF32 || v[k] == 0xFFFF) ? INF32 : v[k];
-          if (d == c && Pc != INF32) x = max(x, Pc + 1);  // x never strongly sees itself
-          v[k] = x;
-        }
-        // bitonic sort of the NPC values of chain c over its LPC lanes
+        // all-ascending bitonic network over the NPC values of chain c (LPC lanes
+        // x VPL values): each merge starts with a flip (partner e ^ (size - 1))
+        // followed by half-cleaners (partner e ^ stride), so every in-lane
+        // comparator is static and a cross-lane one needs only the lane's
+        // position in its pair
 #pragma unroll
         for (int size = 2; size <= NPC; size <<= 1) {
+          if (size <= VPL) {
 #pragma unroll
-          for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int k = 0; k < VPL; k++) {
+              const int k2 = k ^ (size - 1);
+              if (k2 > k) {
+                const int a = v[k], b = v[k2];
+                v[k] = min(a, b);
+                v[k2] = max(a, b);
+              }
+            }
+          } else {
+            const bool lower = (q & ((size >> 1) / VPL)) == 0;
+            int o[VPL];
+#pragma unroll
+            for (int k = 0; k < VPL; k++) o[k] = dpp_flip(size / VPL - 1, v[VPL - 1 - k]);
+#pragma unroll
+            for (int k = 0; k < VPL; k++) v[k] = lower ? min(v[k], o[k]) : max(v[k], o[k]);
+          }
+#pragma unroll
+          for (int stride = size >> 2; stride > 0; stride >>= 1) {
             if (stride < VPL) {
 #pragma unroll
               for (int k = 0; k < VPL; k++) {
                 const int k2 = k ^ stride;
                 if (k2 > k) {
-                  const bool up = (((q * VPL + k) & size) == 0);
                   const int a = v[k], b = v[k2];
-                  v[k] = up ? min(a, b) : max(a, b);
-                  v[k2] = up ? max(a, b) : min(a, b);
+                  v[k] = min(a, b);
+                  v[k2] = max(a, b);
                 }
               }
             } else {
-              const int ls = stride / VPL;  // lane distance: 1 or 2
-              const bool lower = ((q & ls) == 0);
+              const bool lower = (q & (stride / VPL)) == 0;
 #pragma unroll
               for (int k = 0; k < VPL; k++) {
-                const int o = (ls == 1) ? dpp_xor<1>(v[k]) : dpp_xor<2>(v[k]);
-                const bool up = (((q * VPL + k) & size) == 0);
-                v[k] = (lower == up) ? min(v[k], o) : max(v[k], o);
+                const int o = dpp_flip(stride / VPL, v[k]);
+                v[k] = lower ? min(v[k], o) : max(v[k], o);
               }
             }
           }
         }
-        const int qo = (SM - 1) / VPL, ko = (SM - 1) - qo * VPL;
         int sel = v[0];
 #pragma unroll
         for (int k = 1; k < VPL; k++) sel = (k == ko) ? v[k] : sel;
-        const bool owner = act && q == qo;
         int nxt = INF32;
-        if (owner && Pc != INF32) {
-          const int cur = sC[(r - r0) * NPC + c];
-          nxt = cur != INF32 ? cur : (sel < ln ? sel : INF32);
-        }
+        bool leave = false;
         if (owner) {
+          const int Pc = sP[c];
+          if (Pc != INF32) {
+            const int cur = sC[(r - r0) * NPC + c];
+            nxt = cur != INF32 ? cur : ((sel != 0xFFFF && sel < ln) ? sel : INF32);
+          }
           sP[c] = nxt;
           sC[(r - r0) * NPC + c] = nxt;
+          leave = nxt != INF32 && nxt - base_c >= B;  // the next step would leave the block
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -435,6 +463,7 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const int32_t* F
           break;
         }
         r++;
+        if (__ballot(leave)) break;
       }
       if (lane == 0) {
         s_nr = r - r0 + (done ? 1 : 0);  // C rows r0+1 .. r0+s_nr were produced
@@ -444,6 +473,12 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const int32_t* F
       }
     }
     __syncthreads();
+    if (dbg && tid == 0) {
+      const uint64_t now = stamp();
+      wst[1] += now - wt;
+      wt = now;
+      wst[3] += s_nr;
+    }
     // ---- flush the walked C rows (rows < Rprev are rewritten with their own values)
     const int nr = min(s_nr, RB);
     for (int item = tid; item < nr * NPC; item += T) {
@@ -453,9 +488,13 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const int32_t* F
     }
     const bool fin = s_done;
     __syncthreads();
+    if (dbg && tid == 0) wst[0] += stamp() - wt;
     if (fin) break;
   }
+  if (dbg && tid == 0)
+    for (int q = 0; q < 4; q++) dbg[q] += wst[q];
 }
+
 // frontier start: r_lo and the first position per chain that can be a member
 __global__ void k_frontier_start(Tables t, const int32_t* olen, const int32_t* len,
                                  int32_t* out /* [0] rlo, [1..N] start positions */) {
