@@ -163,7 +163,9 @@ struct hge_engine {
   std::vector<double> prof_ms;
   std::vector<int64_t> prof_cnt;
   int R_div = 0;            // Rounds() as seen by the consensus calls (DivideRounds)
-  std::vector<int32_t> h_minw;  // first witness id per round (update_rdiv)
+  std::vector<int32_t> h_minw;  // first witness id per round (read back by coords)
+  std::vector<int32_t> h_ids, h_cc;  // order readback staging
+  bool und_fresh = false;  // the candidate list is every event of a fresh replay
   float stage_ms[7] = {};
 
   Tables tables() const {
@@ -302,6 +304,9 @@ struct hge_engine {
     s_segs.free_();
     d_ssc.free_();
     s_gran.free_();
+    if (pin) (void)hipHostFree(pin);
+    pin = nullptr;
+    pin_cap = pin_used = 0;
     if (st) (void)hipStreamDestroy(st);
     st = nullptr;
   }
@@ -334,7 +339,7 @@ struct hge_engine {
     if (keep && ccap > 0 && b.p)
       HIPCHK(hipMemcpy2DAsync(q, sizeof(int32_t) * nc * w, b.p, sizeof(int32_t) * ccap * w,
                               sizeof(int32_t) * ccap * w, rows, hipMemcpyDeviceToDevice, st));
-    HIPCHK(hipStreamSynchronize(st));
+    sync();
     b.free_();
     b.p = q;
     b.n = (size_t)N * nc * N;
@@ -349,7 +354,7 @@ struct hge_engine {
     if (ccap > 0)
       HIPCHK(hipMemcpy2DAsync(chain, sizeof(int32_t) * nc, d_chain.p, sizeof(int32_t) * ccap,
                               sizeof(int32_t) * ccap, N, hipMemcpyDeviceToDevice, st));
-    HIPCHK(hipStreamSynchronize(st));
+    sync();
     d_chain.free_();
     d_chain.p = chain;
     d_chain.n = (size_t)N * nc;
@@ -377,12 +382,12 @@ struct hge_engine {
     d_minw.need(nr);
     // C must be INF32 beyond the old rows
     fill_i32(d_C.p + oldn, (int64_t)(nr - Rcap) * N, INF32);
-    HIPCHK(hipStreamSynchronize(st));
+    sync();
     Rcap = (int)nr;
   }
 
   void reset_state() {
-    HIPCHK(hipStreamSynchronize(st));
+    sync();
     h_creator.clear();
     h_index.clear();
     h_sp.clear();
@@ -410,7 +415,7 @@ struct hge_engine {
     HIPCHK(hipMemsetAsync(d_rcnt.p, 0, (size_t)Rcap * 4, st));
     HIPCHK(hipMemsetAsync(d_chain.p, 0xFF, (size_t)N * ccap * 4, st));
     HIPCHK(hipMemsetAsync(d_rr.p, 0xFF, (size_t)Ecap * 4, st));
-    HIPCHK(hipStreamSynchronize(st));
+    sync();
   }
 
   // ---------------- admission (hashgraph.go:366-396) ----------------
@@ -495,10 +500,57 @@ struct hge_engine {
     if (n > 0) KLAUNCH(k_fill_i32, dim3(div_up(n, 256)), dim3(256), 0, st, p, n, v);
   }
 
+  // ---- host <-> device staging through pinned memory ----
+  // A copy from pageable memory makes the runtime wait for the stream, so every
+  // small control upload would be a hidden round trip.  Control data goes through
+  // a pinned arena instead: uploads are enqueued without waiting, downloads are
+  // queued and land in their host destinations at the next sync(), which also
+  // recycles the arena (everything enqueued before it has completed).
+  char* pin = nullptr;
+  size_t pin_cap = 0, pin_used = 0;
+  struct Pending {
+    void* dst;
+    size_t off, bytes;
+  };
+  std::vector<Pending> pending;
+
+  char* pin_take(size_t bytes) {
+    const size_t need = (bytes + 255) & ~(size_t)255;
+    if (pin_used + need > pin_cap) {
+      sync();
+      if (need > pin_cap) {
+        if (pin) HIPCHK(hipHostFree(pin));
+        pin = nullptr;
+        pin_cap = std::max<size_t>(need, std::max<size_t>(2 * pin_cap, 1 << 16));
+        HIPCHK(hipHostMalloc((void**)&pin, pin_cap, hipHostMallocDefault));
+      }
+    }
+    char* q = pin + pin_used;
+    pin_used += need;
+    return q;
+  }
+  void h2d(void* dev, const void* host, size_t bytes) {
+    if (!bytes) return;
+    char* q = pin_take(bytes);
+    memcpy(q, host, bytes);
+    HIPCHK(hipMemcpyAsync(dev, q, bytes, hipMemcpyHostToDevice, st));
+  }
+  void d2h(void* host, const void* dev, size_t bytes) {
+    if (!bytes) return;
+    char* q = pin_take(bytes);
+    HIPCHK(hipMemcpyAsync(q, dev, bytes, hipMemcpyDeviceToHost, st));
+    pending.push_back({host, (size_t)(q - pin), bytes});
+  }
+  void sync() {
+    HIPCHK(hipStreamSynchronize(st));
+    for (const Pending& pd : pending) memcpy(pd.dst, pin + pd.off, pd.bytes);
+    pending.clear();
+    pin_used = 0;
+  }
   template <typename F>
   void readback(F* host, const F* dev, size_t n) {
-    HIPCHK(hipMemcpyAsync(host, dev, n * sizeof(F), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    d2h(host, dev, n * sizeof(F));
+    sync();
   }
 
   // ---------------- coordinates + rounds for [n_coords, n_events) ----------------
@@ -515,14 +567,14 @@ struct hge_engine {
       lens[N + c] = chain_len[c];
     }
     s_len.need(2 * N);
-    HIPCHK(hipMemcpyAsync(s_len.p, lens.data(), 8 * N, hipMemcpyHostToDevice, st));
+    h2d(s_len.p, lens.data(), 8 * N);
     KLAUNCH(k_chain_fill, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0, (int)n1);
     s_small.need(8);
     coords_sweep(t);
     // rounds frontier
     for (;;) {
       int32_t rs[2] = {R, 0};
-      HIPCHK(hipMemcpyAsync(s_small.p, rs, 8, hipMemcpyHostToDevice, st));
+      h2d(s_small.p, rs, 8);
       t = tables();
       const int NP = (N + 15) & ~15;
       if (N > 32) {
@@ -550,7 +602,7 @@ struct hge_engine {
           }
           lo_off[2 * N] = tot;
           s_fsslo.need(2 * N + 1);
-          HIPCHK(hipMemcpyAsync(s_fsslo.p, lo_off.data(), 4 * (2 * N + 1), hipMemcpyHostToDevice, st));
+          h2d(s_fsslo.p, lo_off.data(), 4 * (2 * N + 1));
           int maxlen = 0;
           for (int c = 0; c < N; c++) maxlen = std::max(maxlen, chain_len[c]);
           if (tot > 0) {
@@ -577,22 +629,30 @@ struct hge_engine {
           }
         }
       }
-      readback(rs, s_small.p, 2);
+      // rounds, witnesses and the first witness of every round, then ONE round
+      // trip for the round count and minw (the kernels stand down if the rounds
+      // table overflowed: the loop grows it and walks again)
+      t = tables();
+      s_newwit.need(m);
+      HIPCHK(hipMemsetAsync(s_small.p + 4, 0, 4, st));
+      KLAUNCH(k_round_assign, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0, (int)n1,
+              (const int32_t*)s_small.p, s_newwit.p, s_small.p + 4);
+      KLAUNCH(k_witness_bits, dim3(std::min(div_up((int64_t)m * N, 256), 8192)), dim3(256), 0, st,
+              t, s_newwit.p, s_small.p + 4, N > 32 ? (const uint64_t*)d_ssc.p : nullptr);
+      KLAUNCH(k_round_minw, dim3(div_up(Rcap, 256)), dim3(256), 0, st, t, 0,
+              (const int32_t*)s_small.p, d_minw.p);
+      h_minw.resize(Rcap);
+      d2h(rs, s_small.p, 8);
+      d2h(h_minw.data(), d_minw.p, 4 * (size_t)Rcap);
+      sync();
       if (rs[1]) {
         ensure_rcap((int64_t)Rcap * 2);
         continue;
       }
       R = rs[0];
+      h_minw.resize(R);
       break;
     }
-    t = tables();
-    s_newwit.need(m);
-    HIPCHK(hipMemsetAsync(s_small.p + 4, 0, 4, st));
-    KLAUNCH(k_round_assign, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0,
-                       (int)n1, R, s_newwit.p, s_small.p + 4);
-    KLAUNCH(k_witness_bits, dim3(std::min(div_up((int64_t)m * N, 256), 8192)), dim3(256), 0, st, t, s_newwit.p,
-            s_small.p + 4, N > 32 ? (const uint64_t*)d_ssc.p : nullptr);
-    KLAUNCH(k_round_minw, dim3(div_up(R, 256)), dim3(256), 0, st, t, 0, R, d_minw.p);
     n_coords = n1;
     coords_len = chain_len;
     prof_collect();
@@ -664,7 +724,7 @@ struct hge_engine {
     const int nseg = (int)segs.size();
     if (nseg == 0) return;
     s_segs.need(nseg);
-    HIPCHK(hipMemcpyAsync(s_segs.p, segs.data(), sizeof(int2) * nseg, hipMemcpyHostToDevice, st));
+    h2d(s_segs.p, segs.data(), sizeof(int2) * nseg);
     KLAUNCH(k_la_clear, dim3(std::min(64, div_up((int64_t)maxnew * N, 256)), N), dim3(256), 0, st, t,
             olen, len);
     // sweeps until one changes nothing; queued in groups, checked once per group
@@ -704,7 +764,7 @@ struct hge_engine {
     std::vector<int32_t> plo(N);
     for (int c = 0; c < N; c++) plo[c] = std::max(coords_len[c] - 1, 0);
     s_plo.need(2 * N);
-    HIPCHK(hipMemcpyAsync(s_plo.p, plo.data(), 4 * N, hipMemcpyHostToDevice, st));
+    h2d(s_plo.p, plo.data(), 4 * N);
     KLAUNCH(k_transpose, dim3(div_up(maxnew + 1, 64), div_up(N, 64), N), dim3(256), 0, st, t,
             (const int32_t*)nullptr, d_LAT.p, s_plo.p, len, 0);
     // FDT: clear the new positions, then the runs of the new events
@@ -738,7 +798,7 @@ struct hge_engine {
     if (ncalls == 0) return;
     Tables t = tables();
     s_nc.need(ncalls);
-    HIPCHK(hipMemcpyAsync(s_nc.p, calls.data(), 8 * ncalls, hipMemcpyHostToDevice, st));
+    h2d(s_nc.p, calls.data(), 8 * ncalls);
     // R_c = Rounds() after the DivideRounds of call c = #{r : minw[r] < n_c}
     // (minw is on the host since update_rdiv)
     s_Rc.need(ncalls);
@@ -747,7 +807,7 @@ struct hge_engine {
       Rc[c] = (int32_t)(std::lower_bound(h_minw.begin(), h_minw.end(), calls[c],
                                          [](int32_t m, int64_t n) { return (int64_t)m < n; }) -
                         h_minw.begin());
-    HIPCHK(hipMemcpyAsync(s_Rc.p, Rc.data(), 4 * ncalls, hipMemcpyHostToDevice, st));
+    h2d(s_Rc.p, Rc.data(), 4 * ncalls);
 
     // ---- DecideFame windows (host enumeration of (round, call) pairs) ----
     std::vector<int32_t> pr_round, pr_off, pr_cf, pr_len;
@@ -786,10 +846,10 @@ struct hge_engine {
         nrounds = (int)pr_round.size();
         if (nrounds == 0) break;
         s_pr.need(4 * nrounds);
-        HIPCHK(hipMemcpyAsync(s_pr.p, pr_round.data(), 4 * nrounds, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(s_pr.p + nrounds, pr_off.data(), 4 * nrounds, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(s_pr.p + 2 * nrounds, pr_cf.data(), 4 * nrounds, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(s_pr.p + 3 * nrounds, pr_len.data(), 4 * nrounds, hipMemcpyHostToDevice, st));
+        h2d(s_pr.p, pr_round.data(), 4 * nrounds);
+        h2d(s_pr.p + nrounds, pr_off.data(), 4 * nrounds);
+        h2d(s_pr.p + 2 * nrounds, pr_cf.data(), 4 * nrounds);
+        h2d(s_pr.p + 3 * nrounds, pr_len.data(), 4 * nrounds);
         s_dec.need((size_t)npairs * N);
         s_decbit.need(npairs);
         s_Lc.need(ncalls);
@@ -816,15 +876,25 @@ struct hge_engine {
     }
 
     // ---- DecideRoundReceived / FindOrder ----
+    // Everything below is enqueued without a host round trip (counts stay on the
+    // device; buffers and grids are sized by upper bounds) except the lowest
+    // candidate round of an online batch and, for N > 64, the segment count.
+    const bool fresh_und = und_fresh;
+    und_fresh = false;
+    bool got_order = false;
+    int32_t nrecv = 0, nund = 0, rcnt_r = 0, late = 0;
+    unsigned long long ntx = 0;
     if (do_order && n_und > 0) {
       const int ncand = (int)n_und;
       int32_t* cand = d_und.p;
-      // lowest candidate round
-      HIPCHK(hipMemcpyAsync(s_small.p + 7, &kInf, 4, hipMemcpyHostToDevice, st));
-      KLAUNCH(k_min_round, dim3(div_up(ncand, 256)), dim3(256), 0, st, d_round.p, cand, ncand,
-              s_small.p + 7);
-      int32_t mnr = INF32;
-      readback(&mnr, s_small.p + 7, 1);
+      // lowest candidate round (a fresh replay's candidates include event 0, round 0)
+      int32_t mnr = 0;
+      if (!fresh_und) {
+        h2d(s_small.p + 7, &kInf, 4);
+        KLAUNCH(k_min_round, dim3(div_up(ncand, 256)), dim3(256), 0, st, d_round.p, cand, ncand,
+                s_small.p + 7);
+        readback(&mnr, s_small.p + 7, 1);
+      }
       const int rr_lo = mnr + 1;
       const int R_last = Rc[ncalls - 1];
       const int nr = std::max(0, R_last - rr_lo);
@@ -836,7 +906,7 @@ struct hge_engine {
           if (i >= rr_lo && i < R_last) pidx[i - rr_lo] = k;
         }
         s_prindex.need(nr);
-        HIPCHK(hipMemcpyAsync(s_prindex.p, pidx.data(), 4 * nr, hipMemcpyHostToDevice, st));
+        h2d(s_prindex.p, pidx.data(), 4 * nr);
         SegInfo si;
         si.pr_index = s_prindex.p;
         if (nrounds > 0) {
@@ -857,14 +927,21 @@ struct hge_engine {
         seg_dispatch(0, t, rr_lo, nr, ncalls, si, 0);
         KLAUNCH(k_scan_small, dim3(1), dim3(1024), 0, st, s_segcnt.p, s_segoff.p, nr,
                            s_small.p + 6);
-        int32_t nseg = 0;
-        readback(&nseg, s_small.p + 6, 1);
-        s_segcall.need(std::max(nseg, 1));
-        s_seground.need(std::max(nseg, 1));
-        s_segdec.need(std::max(nseg, 1));
-        s_segfws.need((size_t)std::max(nseg, 1) * NW);
-        s_theta.need((size_t)std::max(nseg, 1) * N);
-        seg_dispatch(1, t, rr_lo, nr, ncalls, si, nseg);
+        // a round's segments start at call 0, at a witness arrival (<= N distinct
+        // calls), at the window start or at a processed call of its fame window
+        int64_t nseg = (int64_t)nr * (N + 2) + npairs;
+        if (!group_lanes()) {
+          int32_t v = 0;
+          readback(&v, s_small.p + 6, 1);
+          nseg = v;
+        }
+        const size_t ns = (size_t)std::max<int64_t>(nseg, 1);
+        s_segcall.need(ns);
+        s_seground.need(ns);
+        s_segdec.need(ns);
+        s_segfws.need(ns * NW);
+        s_theta.need(ns * N);
+        seg_dispatch(1, t, rr_lo, nr, ncalls, si, (int)std::min<int64_t>(nseg, INF32 / N));
         // round-received per candidate
         s_recv.need(ncand);
         s_rr.need(ncand);
@@ -874,7 +951,7 @@ struct hge_engine {
         s_recv.need(ncand);
         HIPCHK(hipMemsetAsync(s_recv.p, 0xFF, 4 * ncand, st));
       }
-      // compaction + sort
+      // compaction + sort (the received count stays on the device: s_small[2])
       s_frecv.need(ncand);
       s_fund.need(ncand);
       s_rank.need(ncand);
@@ -882,53 +959,43 @@ struct hge_engine {
       KLAUNCH(k_recv_flags, dim3(div_up(ncand, 256)), dim3(256), 0, st, s_recv.p, ncand,
                          s_frecv.p, s_fund.p, commit ? 1 : 0);
       scan_large(s_frecv.p, s_rank.p, ncand, s_small.p + 2);
-      int32_t nrecv = 0;
-      readback(&nrecv, s_small.p + 2, 1);
       s_ntx.need(1);
       HIPCHK(hipMemsetAsync(s_ntx.p, 0, 8, st));
-      if (nrecv > 0) {
-        KLAUNCH(k_set_rr, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand,
-                           s_recv.p, s_rr.p, s_cts.p, d_rr.p, d_cts.p, s_ntx.p, commit ? 1 : 0);
-      }
-      if (commit && nrecv > 0) {
-        s_keys.need((size_t)nrecv * sizeof(OKey));
-        s_keys2.need((size_t)nrecv * sizeof(OKey));
+      KLAUNCH(k_set_rr, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand, s_recv.p,
+              s_rr.p, s_cts.p, d_rr.p, d_cts.p, s_ntx.p, commit ? 1 : 0);
+      if (commit) {
+        const int32_t* pn = s_small.p + 2;
+        s_keys.need((size_t)ncand * sizeof(OKey));
+        s_keys2.need((size_t)ncand * sizeof(OKey));
         OKey* k1 = (OKey*)s_keys.p;
         OKey* k2 = (OKey*)s_keys2.p;
         KLAUNCH(k_make_keys, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand,
                            s_recv.p, s_rr.p, s_cts.p, s_rank.p, k1);
-        KLAUNCH(k_sort_tiles, dim3(div_up(nrecv, 1024)), dim3(512), 0, st, k1, nrecv);
-        for (int run = 1024; run < nrecv; run *= 2) {
-          KLAUNCH(k_merge_pass, dim3(div_up(nrecv, 256)), dim3(256), 0, st, k1, k2,
-                             nrecv, run);
+        KLAUNCH(k_sort_tiles, dim3(div_up(ncand, 1024)), dim3(512), 0, st, k1, pn);
+        // passes for the candidate count: a pass whose run covers every key copies
+        for (int run = 1024; run < ncand; run *= 2) {
+          KLAUNCH(k_merge_pass, dim3(div_up(ncand, 256)), dim3(256), 0, st, k1, k2, pn, run);
           std::swap(k1, k2);
         }
-        s_ids.need(nrecv);
+        s_ids.need(ncand);
         s_ccount.need(ncalls);
         HIPCHK(hipMemsetAsync(s_ccount.p, 0, 4 * ncalls, st));
-        KLAUNCH(k_emit_order, dim3(div_up(nrecv, 256)), dim3(256), 0, st, k1, nrecv,
-                           s_ids.p, s_ccount.p, 0);
-        std::vector<int32_t> ids(nrecv);
-        std::vector<int32_t> cc(ncalls);
-        HIPCHK(hipMemcpyAsync(ids.data(), s_ids.p, 4 * nrecv, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(cc.data(), s_ccount.p, 4 * ncalls, hipMemcpyDeviceToHost, st));
-        unsigned long long ntx = 0;
-        HIPCHK(hipMemcpyAsync(&ntx, s_ntx.p, 8, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        consensus.insert(consensus.end(), ids.begin(), ids.end());
-        ctx += (int64_t)ntx;
-        if (order_out) order_out->insert(order_out->end(), ids.begin(), ids.end());
-        if (counts_out)
-          for (int c = 0; c < ncalls; c++) counts_out->push_back(cc[c]);
-        // new undetermined list
+        KLAUNCH(k_emit_order, dim3(div_up(ncand, 256)), dim3(256), 0, st, k1, pn, s_ids.p,
+                s_ccount.p, 0);
+        // new undetermined list (in candidate order)
         scan_large(s_fund.p, s_upos.p, ncand, s_small.p + 3);
-        int32_t nund = 0;
-        readback(&nund, s_small.p + 3, 1);
-        s_und2.need(std::max(nund, 1));
+        s_und2.need(ncand);
         KLAUNCH(k_scatter_und, dim3(div_up(ncand, 256)), dim3(256), 0, st, cand, ncand,
                            s_fund.p, s_upos.p, s_und2.p);
-        HIPCHK(hipMemcpyAsync(d_und.p, s_und2.p, 4 * (size_t)nund, hipMemcpyDeviceToDevice, st));
-        n_und = nund;
+        HIPCHK(hipMemcpyAsync(d_und.p, s_und2.p, 4 * (size_t)ncand, hipMemcpyDeviceToDevice, st));
+        h_ids.resize(ncand);
+        h_cc.resize(ncalls);
+        d2h(&nrecv, s_small.p + 2, 4);
+        d2h(&nund, s_small.p + 3, 4);
+        d2h(&ntx, s_ntx.p, 8);
+        d2h(h_ids.data(), s_ids.p, 4 * (size_t)ncand);
+        d2h(h_cc.data(), s_ccount.p, 4 * (size_t)ncalls);
+        got_order = true;
       } else if (counts_out) {
         for (int c = 0; c < ncalls; c++) counts_out->push_back(0);
       }
@@ -937,29 +1004,40 @@ struct hge_engine {
     }
 
     // ---- persist fame / LCR ----
+    bool lcr_up = false;
     if (do_fame && nrounds > 0) {
       fame_dispatch(1, t, nrounds, npairs, 0, ncalls);
       if (lcr_new > lcr) {
-        // RoundEvents(lcr_new - 1) at call c_set
-        int r = lcr_new - 1;
-        int32_t cnt = 0;
+        // RoundEvents(lcr_new - 1) at call c_set: events of that round minus the
+        // ones inserted after that call
+        lcr_up = true;
+        const int r = lcr_new - 1;
         if (r >= 0) {
-          readback(&cnt, d_rcnt.p + r, 1);
+          d2h(&rcnt_r, d_rcnt.p + r, 4);
           const int64_t nfrom = calls[c_set];
           if (nfrom < n_coords) {
             HIPCHK(hipMemsetAsync(s_small.p + 5, 0, 4, st));
             KLAUNCH(k_count_late, dim3(div_up(n_coords - nfrom, 256)), dim3(256), 0, st,
                                t, (int)nfrom, (int)n_coords, r, s_small.p + 5);
-            int32_t late = 0;
-            readback(&late, s_small.p + 5, 1);
-            cnt -= late;
+            d2h(&late, s_small.p + 5, 4);
           }
         }
-        lcr = lcr_new;
-        lcre = cnt;
       }
     }
-    HIPCHK(hipStreamSynchronize(st));
+    // the batch's one closing round trip
+    sync();
+    if (got_order) {
+      consensus.insert(consensus.end(), h_ids.begin(), h_ids.begin() + nrecv);
+      ctx += (int64_t)ntx;
+      if (order_out) order_out->insert(order_out->end(), h_ids.begin(), h_ids.begin() + nrecv);
+      if (counts_out)
+        for (int c = 0; c < ncalls; c++) counts_out->push_back(h_cc[c]);
+      n_und = nund;
+    }
+    if (lcr_up) {
+      lcr = lcr_new;
+      lcre = lcr_new - 1 >= 0 ? rcnt_r - late : 0;
+    }
     prof_collect();
   }
 
@@ -1050,8 +1128,8 @@ struct hge_engine {
               ncalls, si, s_arr.p, s_segcnt.p, s_segoff.p, s_segcall.p, s_seground.p,            \
               s_segdec.p, s_segfws.p, mode);                                                     \
     if (mode == 1 && nseg > 0)                                                                   \
-      KLAUNCH(k_seg_theta<B>, dim3(div_up(nseg * N, 256)), dim3(256), 0, st, t,       \
-                         rr_lo, s_seground.p, nseg, s_segfws.p, s_theta.p);                      \
+      KLAUNCH(k_seg_theta<B>, dim3(std::min(div_up((int64_t)nseg * N, 256), 4096)), dim3(256), 0, \
+              st, t, s_seground.p, (const int32_t*)(s_small.p + 6), s_segfws.p, s_theta.p);      \
     break;
       SCASE(1)
       SCASE(2)
@@ -1109,12 +1187,12 @@ struct hge_engine {
 
   // first witness id of every round (host copy: Rounds() as seen at any event count)
   void update_rdiv() {
+    // h_minw was read back together with the round count (coords)
     h_minw.resize(R);
     if (R == 0) {
       R_div = 0;
       return;
     }
-    readback(h_minw.data(), d_minw.p, R);
     R_div = (int)(std::lower_bound(h_minw.begin(), h_minw.end(),
                                    (int32_t)std::min<int64_t>(n_divided, INF32)) -
                   h_minw.begin());
@@ -1284,7 +1362,6 @@ int hge_replay_run(hge_engine* h, int64_t* n_ordered) {
     HIPCHK(hipMemsetAsync(h->d_fame.p, 0, (size_t)h->Rcap * h->N, h->st));
     HIPCHK(hipMemsetAsync(h->d_rcnt.p, 0, (size_t)h->Rcap * 4, h->st));
     HIPCHK(hipMemsetAsync(h->d_rr.p, 0xFF, (size_t)h->Ecap * 4, h->st));
-    HIPCHK(hipStreamSynchronize(h->st));
   }
   HIPCHK(hipEventRecord(h->ev[0], h->st));
   h->coords();
@@ -1293,6 +1370,7 @@ int hge_replay_run(hge_engine* h, int64_t* n_ordered) {
   h->update_rdiv();
   if (keep > 0) h->fill_iota(h->d_und.p, keep, 0);
   h->n_und = keep;
+  h->und_fresh = keep > 0;
   h->replay_order.clear();
   h->replay_counts.clear();
   h->consensus_batch(h->replay_calls, true, true, true, &h->replay_order, &h->replay_counts);

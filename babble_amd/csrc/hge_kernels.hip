@@ -375,6 +375,7 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* 
       int bd[VPL];  // per-slot block bases; absent members gather from sInf
 #pragma unroll
       for (int k = 0; k < VPL; k++) bd[k] = sBase[q * VPL + k];
+      int myP = sP[c];  // the owner's frontier position, kept in a register
       int r = r0;
       bool done = false;
       for (;;) {
@@ -387,6 +388,8 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* 
         int Pv[VPL], v[VPL];
 #pragma unroll
         for (int k = 0; k < VPL; k++) Pv[k] = sP[q * VPL + k];
+        // the already-known C value of round r+1, read together with the members
+        const int cur = sC[(r - r0) * NPC + c];
 #pragma unroll
         for (int k = 0; k < VPL; k++) {
           const int d = q * VPL + k;
@@ -394,6 +397,8 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* 
                                                  : &sInf[c];
           v[k] = *src;
         }
+        // keep every gather in flight before the first comparator waits on one
+        __builtin_amdgcn_sched_barrier(0);
         // all-ascending bitonic network over the NPC values of chain c (LPC lanes
         // x VPL values): each merge starts with a flip (partner e ^ (size - 1))
         // followed by half-cleaners (partner e ^ stride), so every in-lane
@@ -444,18 +449,15 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* 
         int sel = v[0];
 #pragma unroll
         for (int k = 1; k < VPL; k++) sel = (k == ko) ? v[k] : sel;
-        int nxt = INF32;
-        bool leave = false;
+        // branch-free owner update: no LDS read between the network and the store
+        const int cand = (sel != 0xFFFF && sel < ln) ? sel : INF32;
+        const int nxt = myP == INF32 ? INF32 : (cur != INF32 ? cur : cand);
+        myP = nxt;
         if (owner) {
-          const int Pc = sP[c];
-          if (Pc != INF32) {
-            const int cur = sC[(r - r0) * NPC + c];
-            nxt = cur != INF32 ? cur : ((sel != 0xFFFF && sel < ln) ? sel : INF32);
-          }
           sP[c] = nxt;
           sC[(r - r0) * NPC + c] = nxt;
-          leave = nxt != INF32 && nxt - base_c >= B;  // the next step would leave the block
         }
+        const bool leave = owner && nxt != INF32 && nxt - base_c >= B;  // next step leaves the block
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (!__ballot(owner && nxt != INF32)) {
@@ -522,8 +524,10 @@ __global__ void k_frontier_start(Tables t, const int32_t* olen, const int32_t* l
 // round(x) = max r with C[r][cx] <= px; witness iff C[round][cx] == px
 // (consecutive events share a round: the per-round counts and the new-witness
 // slots are aggregated per wave before touching global atomics)
-__global__ void k_round_assign(Tables t, int n0, int n1, int R, int32_t* newwit,
+__global__ void k_round_assign(Tables t, int n0, int n1, const int32_t* rstate, int32_t* newwit,
                                int32_t* nnewwit) {
+  if (rstate[1]) return;  // the rounds table overflowed: the host grows it and walks again
+  const int R = rstate[0];
   const int x = n0 + blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = x < n1;
   const int N = t.N;
@@ -562,30 +566,15 @@ __global__ void k_round_assign(Tables t, int n0, int n1, int R, int32_t* newwit,
 }
 
 // first witness id per round (monotone increasing in r); rounds [r0, R)
-__global__ void k_round_minw(Tables t, int r0, int R, int32_t* minw) {
+__global__ void k_round_minw(Tables t, int r0, const int32_t* rstate, int32_t* minw) {
   const int r = r0 + blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= R) return;
+  if (rstate[1] || r >= rstate[0]) return;
   int m = INF32;
   for (int c = 0; c < t.N; c++) {
     const int w = t.W[(size_t)r * t.N + c];
     if (w >= 0) m = min(m, w);
   }
   minw[r] = m;
-}
-
-// R_c = Rounds() after the DivideRounds of call c = #{r : minw[r] < n_c}
-__global__ void k_calls_rounds(const int64_t* nc, int ncalls, const int32_t* minw, int R,
-                               int32_t* Rc) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= ncalls) return;
-  const int64_t n = nc[c];
-  int lo = 0, hi = R;  // count of minw < n
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if ((int64_t)minw[mid] < n) lo = mid + 1;
-    else hi = mid;
-  }
-  Rc[c] = lo;
 }
 
 // strongly-see / see bitsets of each new witness y (round j >= 1) over the
@@ -1050,33 +1039,24 @@ __global__ void __launch_bounds__(256) k_segments_g(Tables t, int rr_lo, int nr,
 // w: event x (creator cx, index ix) is seen by a strict majority of them iff
 // ix <= theta (hashgraph.go:689-697).  INT32_MIN when nobody is famous.
 template <int NWT>
-__global__ void k_seg_theta(Tables t, int rr_lo, const int32_t* seg_round, int nseg,
-                            const uint64_t* seg_fws, int32_t* theta) {
-  const int item = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ int seg_theta_one(const Tables& t, const int32_t* seg_round, const uint64_t* seg_fws,
+                             int sg, int cx) {
   const int N = t.N;
-  if (item >= nseg * N) return;
-  const int sg = item / N, cx = item - (item / N) * N;
   const int i = seg_round[sg];
-  int vals[64];
-  int m = 0;
-  int k = 0;
-  // count famous
   int nf = 0;
 #pragma unroll
   for (int w = 0; w < NWT; w++) nf += __popcll(seg_fws[(size_t)sg * NWT + w]);
-  k = nf / 2 + 1;
-  if (nf == 0) {
-    theta[item] = (int)0x80000000;
-    return;
-  }
-  // k-th largest by repeated selection over a bounded buffer (N <= 64 fast path)
+  if (nf == 0) return (int)0x80000000;
+  const int k = nf / 2 + 1;
   if (nf <= 64) {
+    // k-th largest by repeated selection over a bounded buffer
+    int vals[64];
+    int m = 0;
     for (int d = 0; d < N; d++) {
       if (!((seg_fws[(size_t)sg * NWT + (d >> 6)] >> (d & 63)) & 1ull)) continue;
       const int w = t.W[(size_t)i * N + d];
       vals[m++] = t.LA[rowoff(t, d, t.index[w]) + cx];
     }
-    // partial selection sort (descending) for k elements
     for (int a = 0; a < k; a++) {
       int best = a;
       for (int b = a + 1; b < m; b++)
@@ -1085,23 +1065,33 @@ __global__ void k_seg_theta(Tables t, int rr_lo, const int32_t* seg_round, int n
       vals[a] = vals[best];
       vals[best] = tmp;
     }
-    theta[item] = vals[k - 1];
-  } else {
-    // general: threshold search by counting (values are chain positions >= -1)
-    int lo = -1, hi = INF32 - 1;  // largest v with count(>= v) >= k
-    while (lo < hi) {
-      const int mid = lo + (int)(((int64_t)hi - lo + 1) / 2);
-      int ccount = 0;
-      for (int d = 0; d < N; d++) {
-        if (!((seg_fws[(size_t)sg * NWT + (d >> 6)] >> (d & 63)) & 1ull)) continue;
-        const int w = t.W[(size_t)i * N + d];
-        ccount += (t.LA[rowoff(t, d, t.index[w]) + cx] >= mid) ? 1 : 0;
-      }
-      if (ccount >= k) lo = mid;
-      else hi = mid - 1;
-    }
-    theta[item] = lo;
+    return vals[k - 1];
   }
+  // general: threshold search by counting (values are chain positions >= -1)
+  int lo = -1, hi = INF32 - 1;  // largest v with count(>= v) >= k
+  while (lo < hi) {
+    const int mid = lo + (int)(((int64_t)hi - lo + 1) / 2);
+    int ccount = 0;
+    for (int d = 0; d < N; d++) {
+      if (!((seg_fws[(size_t)sg * NWT + (d >> 6)] >> (d & 63)) & 1ull)) continue;
+      const int w = t.W[(size_t)i * N + d];
+      ccount += (t.LA[rowoff(t, d, t.index[w]) + cx] >= mid) ? 1 : 0;
+    }
+    if (ccount >= k) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// grid-stride over (segment, creator): the segment count lives on the device
+template <int NWT>
+__global__ void k_seg_theta(Tables t, const int32_t* seg_round, const int32_t* pnseg,
+                            const uint64_t* seg_fws, int32_t* theta) {
+  const int N = t.N;
+  const int total = *pnseg * N;
+  for (int item = blockIdx.x * blockDim.x + threadIdx.x; item < total;
+       item += gridDim.x * blockDim.x)
+    theta[item] = seg_theta_one<NWT>(t, seg_round, seg_fws, item / N, item - (item / N) * N);
 }
 
 // ---------------------------------------------------------------------------
@@ -1334,9 +1324,11 @@ __global__ void k_make_keys(Tables t, const int32_t* cand, int ncand, const int3
 }
 
 // bitonic sort of 1024-key tiles in LDS (tail padded with +inf keys)
-__global__ void __launch_bounds__(512) k_sort_tiles(OKey* keys, int n) {
+__global__ void __launch_bounds__(512) k_sort_tiles(OKey* keys, const int32_t* np) {
   __shared__ OKey sk[1024];
+  const int n = *np;  // key count on the device; the grid covers an upper bound
   const int base = blockIdx.x * 1024;
+  if (base >= n) return;
   const int tid = threadIdx.x;
   for (int i = tid; i < 1024; i += 512) {
     if (base + i < n) sk[i] = keys[base + i];
@@ -1368,8 +1360,9 @@ __global__ void __launch_bounds__(512) k_sort_tiles(OKey* keys, int n) {
 }
 
 // one merge pass of sorted runs of length `run`: rank-based (keys are unique)
-__global__ void k_merge_pass(const OKey* in, OKey* out, int n, int run) {
+__global__ void k_merge_pass(const OKey* in, OKey* out, const int32_t* np, int run) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = *np;
   if (i >= n) return;
   const int pair = i / (2 * run);
   const int a0 = pair * 2 * run;
@@ -1398,10 +1391,10 @@ __global__ void k_merge_pass(const OKey* in, OKey* out, int n, int run) {
   out[pos] = k;
 }
 
-__global__ void k_emit_order(const OKey* keys, int n, int32_t* ids, int32_t* call_counts,
-                             int32_t call_lo) {
+__global__ void k_emit_order(const OKey* keys, const int32_t* np, int32_t* ids,
+                             int32_t* call_counts, int32_t call_lo) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= *np) return;
   ids[i] = (int32_t)keys[i].id;
   atomicAdd(&call_counts[(int)(keys[i].a >> 32) - call_lo], 1);
 }
