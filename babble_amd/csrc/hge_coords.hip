@@ -42,12 +42,18 @@ __global__ void k_la_clear(Tables t, const int32_t* olen, const int32_t* len) {
 // prev: the previous sweep's changed flag (nullptr for the first): sweeps are
 // queued in groups without a host round trip, and once one changes nothing
 // the rest of its group return at once.
+// A sweep is a chain of dependent memory latencies, not of bytes at small N:
+// the other-parent coordinates come from the chain-major opcp table (one load,
+// staged in LDS), and each lane then has all U loads of a batch in flight
+// (op rows and own rows) before it folds them, so a 64-position segment costs
+// three latencies (opcp, two batches) plus the fold.
 template <int NP>
 __global__ void __launch_bounds__(256) k_la_sweep(Tables t, const int2* segs, int nseg, int SEG,
                                                   const int32_t* len, const int32_t* prev,
                                                   int32_t* changed) {
   constexpr int G = 256 / NP;
   constexpr int SEGMAX = 64;
+  constexpr int U = 32;  // loads in flight per lane and batch
   __shared__ int64_t s_off[G][SEGMAX];
   if (prev && *prev == 0) return;  // converged: the flag stays 0
   const int N = t.N;
@@ -64,9 +70,8 @@ __global__ void __launch_bounds__(256) k_la_sweep(Tables t, const int2* segs, in
   for (int kk = i; kk < SEG; kk += NP) {
     int64_t off = -1;
     if (valid && k0 + kk < k1) {
-      const int x = t.chain[(size_t)j * t.ccap + k0 + kk];
-      const int o = t.op[x];
-      if (o >= 0) off = (int64_t)rowoff(t, t.creator[o], t.index[o]);
+      const int2 o = t.opcp[(size_t)j * t.ccap + k0 + kk];
+      if (o.x >= 0) off = (int64_t)rowoff(t, o.x, o.y);
     }
     s_off[g][kk] = off;
   }
@@ -74,22 +79,23 @@ __global__ void __launch_bounds__(256) k_la_sweep(Tables t, const int2* segs, in
   const bool act = valid && i < N;
   bool ch = false;
   if (act) {
-    int v = (k0 > 0) ? t.LA[rowoff(t, j, k0 - 1) + i] : -1;
-    for (int kb = k0; kb < k1; kb += 8) {
-      int a[8], old[8];
+    const size_t own0 = rowoff(t, j, k0) + i;
+    int v = (k0 > 0) ? t.LA[own0 - N] : -1;
+    for (int kb = k0; kb < k1; kb += U) {
+      int a[U], old[U];
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
+      for (int u = 0; u < U; u++) {
         const int k = kb + u;
         a[u] = -1;
         old[u] = -1;
         if (k < k1) {
           const int64_t off = s_off[g][k - k0];
           if (off >= 0) a[u] = t.LA[off + i];
-          old[u] = t.LA[rowoff(t, j, k) + i];
+          old[u] = t.LA[own0 + (size_t)(k - k0) * N];
         }
       }
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
+      for (int u = 0; u < U; u++) {
         const int k = kb + u;
         if (k < k1) {
           v = max(v, a[u]);
@@ -97,7 +103,7 @@ __global__ void __launch_bounds__(256) k_la_sweep(Tables t, const int2* segs, in
           const int nv = max(v, old[u]);
           v = nv;
           if (nv != old[u]) {
-            t.LA[rowoff(t, j, k) + i] = nv;
+            t.LA[own0 + (size_t)(k - k0) * N] = nv;
             ch = true;
           }
         }

@@ -130,29 +130,27 @@ struct hge_engine {
   DBuf<uint64_t> d_S;
   DBuf<uint8_t> d_coin, d_wit;
   DBuf<int32_t> d_chain, d_LA, d_FD, d_FSS;
+  DBuf<int2> d_opcp;  // [N][ccap] other-parent coordinates (k_chain_fill)
   DBuf<int32_t> d_C, d_W, d_rcnt, d_minw;
   DBuf<uint64_t> d_ssb, d_seeb;
   DBuf<uint8_t> d_fame;
   // scratch
-  DBuf<int32_t> s_small, s_len, s_newwit;
-  DBuf<int64_t> s_nc;
-  DBuf<int32_t> s_Rc, s_Lc, s_LCR, s_pr, s_clast, s_flags;
+  DBuf<int32_t> s_small, s_newwit;
+  DBuf<int32_t> s_LCR, s_clast;
   DBuf<uint8_t> s_dec, s_decbit;
-  DBuf<int32_t> s_segcnt, s_segoff, s_segcall, s_seground, s_theta, s_prindex;
+  DBuf<int32_t> s_segcnt, s_segoff, s_segcall, s_seground, s_theta;
   DBuf<uint8_t> s_segdec;
   DBuf<uint64_t> s_segfws;
-  DBuf<int32_t> s_recv, s_rr, s_frecv, s_fund, s_rank, s_upos, s_und2, s_ids, s_ccount;
+  DBuf<int32_t> s_recv, s_rr, s_frecv, s_fund, s_rank, s_upos, s_und2;
   DBuf<int64_t> s_cts;
   DBuf<unsigned char> s_keys, s_keys2;
-  DBuf<unsigned long long> s_ntx;
-  DBuf<int32_t> s_part, s_arr, s_fst, s_fsslo;
+  DBuf<int32_t> s_part, s_arr, s_fst;
   // coordinate sweeps: transposed tables and scratch
   int n_sweeps = 0;
-  DBuf<int32_t> d_LAT, d_FDT, s_chg, s_plo, s_bar;
+  DBuf<int32_t> d_LAT, d_FDT, s_chg, s_bar;
   DBuf<uint64_t> d_ssc, s_gran;
   DBuf<int32_t> s_bseg;
   bool coop_checked = false;
-  DBuf<int2> s_segs;
 
   hipEvent_t ev[8] = {};
   // per-kernel HIP-event timing on the engine stream (hge_set_profiling)
@@ -164,7 +162,17 @@ struct hge_engine {
   std::vector<int64_t> prof_cnt;
   int R_div = 0;            // Rounds() as seen by the consensus calls (DivideRounds)
   std::vector<int32_t> h_minw;  // first witness id per round (read back by coords)
-  std::vector<int32_t> h_ids, h_cc;  // order readback staging
+  // consensus control block (one upload) and results block (one readback)
+  DBuf<int32_t> s_cctl, s_out;
+  std::vector<int32_t> h_cctl, h_out;
+  int64_t* c_nc = nullptr;
+  int32_t *c_Rc = nullptr, *c_Lc = nullptr, *c_flags = nullptr, *c_pr = nullptr, *c_pidx = nullptr;
+  // coordinates control block (coords): pointers into s_kctl
+  DBuf<int32_t> s_kctl;
+  std::vector<int32_t> h_kctl;
+  std::vector<int2> h_segs;
+  int32_t *k_rs = nullptr, *k_len = nullptr, *k_plo = nullptr, *k_qlo = nullptr, *k_lo = nullptr;
+  int2* k_segs = nullptr;
   bool und_fresh = false;  // the candidate list is every event of a fresh replay
   float stage_ms[7] = {};
 
@@ -184,6 +192,7 @@ struct hge_engine {
     t.coin = d_coin.p;
     t.ntx = d_ntx.p;
     t.chain = d_chain.p;
+    t.opcp = d_opcp.p;
     t.LA = d_LA.p;
     t.FD = d_FD.p;
     t.round = d_round.p;
@@ -215,6 +224,7 @@ struct hge_engine {
     ensure_events(c0);
     ensure_ccap(c0 / N + c0 / (8 * N) + 64);
     ensure_rcap(c0 / (2 * N) + 64);
+    s_small.need(8);
   }
 
   void prof_begin(const char* name) {
@@ -277,16 +287,17 @@ struct hge_engine {
       if (e) (void)hipEventDestroy(e);
     for (auto& e : prof_pool) (void)hipEventDestroy(e);
     prof_pool.clear();
-    DBuf<int32_t>* i32s[] = {&d_creator, &d_index, &d_sp, &d_op, &d_ntx, &d_round, &d_rr, &d_und,
-                             &d_chain, &d_LA, &d_FD, &d_C, &d_W, &d_rcnt, &d_minw, &s_small, &s_len, &s_newwit,
-                             &s_Rc, &s_Lc, &s_LCR, &s_pr, &s_clast, &s_flags, &s_segcnt,
-                             &s_segoff, &s_segcall, &s_seground, &s_theta, &s_prindex, &s_recv,
-                             &s_rr, &s_frecv, &s_fund, &s_rank, &s_upos, &s_und2, &s_ids, &s_part, &s_arr, &s_fst, &s_fsslo, &d_FSS, &d_LAT, &d_FDT, &s_chg, &s_plo, &s_bar, &s_bseg,
-                             &s_ccount};
+    DBuf<int32_t>* i32s[] = {&d_creator, &d_index,  &d_sp,    &d_op,     &d_ntx,     &d_round,
+                             &d_rr,      &d_und,    &d_chain, &d_LA,     &d_FD,      &d_C,
+                             &d_W,       &d_rcnt,   &d_minw,  &s_small,  &s_newwit,  &s_LCR,
+                             &s_clast,   &s_segcnt, &s_segoff, &s_segcall, &s_seground, &s_theta,
+                             &s_recv,    &s_rr,     &s_frecv, &s_fund,   &s_rank,    &s_upos,
+                             &s_und2,    &s_part,   &s_arr,   &s_fst,    &d_FSS,     &d_LAT,
+                             &d_FDT,     &s_chg,    &s_bar,   &s_bseg,   &s_kctl,    &s_cctl,
+                             &s_out};
     for (auto* b : i32s) b->free_();
     d_ts.free_();
     d_cts.free_();
-    s_nc.free_();
     s_cts.free_();
     d_S.free_();
     d_ssb.free_();
@@ -300,8 +311,7 @@ struct hge_engine {
     s_segdec.free_();
     s_keys.free_();
     s_keys2.free_();
-    s_ntx.free_();
-    s_segs.free_();
+    d_opcp.free_();
     d_ssc.free_();
     s_gran.free_();
     if (pin) (void)hipHostFree(pin);
@@ -358,6 +368,15 @@ struct hge_engine {
     d_chain.free_();
     d_chain.p = chain;
     d_chain.n = (size_t)N * nc;
+    int2* opcp = nullptr;
+    HIPCHK(hipMalloc(&opcp, sizeof(int2) * N * nc));
+    if (ccap > 0)
+      HIPCHK(hipMemcpy2DAsync(opcp, sizeof(int2) * nc, d_opcp.p, sizeof(int2) * ccap,
+                              sizeof(int2) * ccap, N, hipMemcpyDeviceToDevice, st));
+    sync();
+    d_opcp.free_();
+    d_opcp.p = opcp;
+    d_opcp.n = (size_t)N * nc;
     grow_chain_table(d_LA, nc, true);
     grow_chain_table(d_FD, nc, true);
     // first-strong-seer rows (N <= 32): int32 rows of N, or uint16 rows padded to
@@ -379,7 +398,7 @@ struct hge_engine {
     if (N > 32) d_ssc.grow_keep(nr * N * NW, oldn * NW, st, 0);
     d_fame.grow_keep(nr * N, oldn, st, 0);
     d_rcnt.grow_keep(nr, Rcap, st, 0);
-    d_minw.need(nr);
+    d_minw.need(nr + 2);  // + the round count and overflow flag (k_round_minw)
     // C must be INF32 beyond the old rows
     fill_i32(d_C.p + oldn, (int64_t)(nr - Rcap) * N, INF32);
     sync();
@@ -407,15 +426,17 @@ struct hge_engine {
     ctx = 0;
     consensus.clear();
     n_und = 0;
-    fill_i32(d_C.p, (int64_t)Rcap * N, INF32);
-    HIPCHK(hipMemsetAsync(d_W.p, 0xFF, (size_t)Rcap * N * 4, st));
-    HIPCHK(hipMemsetAsync(d_ssb.p, 0, (size_t)Rcap * N * NW * 8, st));
-    HIPCHK(hipMemsetAsync(d_seeb.p, 0, (size_t)Rcap * N * NW * 8, st));
-    HIPCHK(hipMemsetAsync(d_fame.p, 0, (size_t)Rcap * N, st));
-    HIPCHK(hipMemsetAsync(d_rcnt.p, 0, (size_t)Rcap * 4, st));
+    reset_rounds();
     HIPCHK(hipMemsetAsync(d_chain.p, 0xFF, (size_t)N * ccap * 4, st));
-    HIPCHK(hipMemsetAsync(d_rr.p, 0xFF, (size_t)Ecap * 4, st));
     sync();
+  }
+
+  // fresh per-round tables (C, W, bitsets, fame, counts) and received rounds: one launch
+  void reset_rounds() {
+    const int64_t nrow = (int64_t)Rcap * N, nbits = nrow * NW;
+    const int64_t most = std::max<int64_t>(std::max(nbits, Ecap), Rcap);
+    KLAUNCH(k_reset_rounds, dim3(std::min(div_up(most, 256), 4096)), dim3(256), 0, st, tables(), nrow,
+            nbits, Ecap, d_rr.p);
   }
 
   // ---------------- admission (hashgraph.go:366-396) ----------------
@@ -560,21 +581,53 @@ struct hge_engine {
     if (n1 == n0) return;
     Tables t = tables();
     const int m = (int)(n1 - n0);
-    std::vector<int32_t>& lens = h_lens;
-    lens.resize(2 * N);
+    // control block (one upload): round state, chain lengths, transpose bounds,
+    // fss offsets of a fresh walk and the sweep segments
+    static const int SEG = getenv("HGE_SEG") ? std::max(1, std::min(64, atoi(getenv("HGE_SEG")))) : 64;
+    std::vector<int2>& segs = h_segs;
+    segs.clear();
+    int maxnew = 0;
     for (int c = 0; c < N; c++) {
-      lens[c] = coords_len[c];
-      lens[N + c] = chain_len[c];
+      maxnew = std::max(maxnew, chain_len[c] - coords_len[c] + 1);
+      for (int k = coords_len[c]; k < chain_len[c]; k += SEG) segs.push_back(make_int2(c, k));
     }
-    s_len.need(2 * N);
-    h2d(s_len.p, lens.data(), 8 * N);
+    // position-major order: workgroups are dispatched roughly in index order, so
+    // early positions of every chain are swept first and later segments read
+    // rows already updated in this sweep (Gauss-Seidel in time order)
+    if (!getenv("HGE_SEG_CHAIN_MAJOR"))
+      std::stable_sort(segs.begin(), segs.end(),
+                       [](const int2& a, const int2& b) { return a.y < b.y; });
+    bool fresh = R == 0;
+    for (int c = 0; c < N; c++) fresh = fresh && coords_len[c] == 0;
+    const size_t o_len = 4, o_plo = o_len + 2 * N, o_qlo = o_plo + N, o_lo = o_qlo + N;
+    const size_t o_seg = (o_lo + 2 * N + 1 + 1) & ~(size_t)1;
+    std::vector<int32_t>& kc = h_kctl;
+    kc.assign(o_seg + 2 * segs.size(), 0);
+    kc[0] = R;  // rstate: {R, overflow}, new-witness count
+    int tot0 = 0;
+    for (int c = 0; c < N; c++) {
+      kc[o_len + c] = coords_len[c];
+      kc[o_len + N + c] = chain_len[c];
+      kc[o_plo + c] = std::max(coords_len[c] - 1, 0);
+      kc[o_lo + N + c] = tot0;  // fresh walk: fss rows from position 0 (qlo = 0 too)
+      tot0 += chain_len[c];
+    }
+    kc[o_lo + 2 * N] = tot0;
+    if (!segs.empty()) memcpy(&kc[o_seg], segs.data(), sizeof(int2) * segs.size());
+    s_kctl.need(kc.size());
+    h2d(s_kctl.p, kc.data(), 4 * kc.size());
+    k_rs = s_kctl.p;
+    k_len = s_kctl.p + o_len;
+    k_plo = s_kctl.p + o_plo;
+    k_qlo = s_kctl.p + o_qlo;
+    k_lo = s_kctl.p + o_lo;
+    k_segs = (int2*)(s_kctl.p + o_seg);
     KLAUNCH(k_chain_fill, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0, (int)n1);
-    s_small.need(8);
-    coords_sweep(t);
+    coords_sweep(t, (int)segs.size(), SEG, maxnew, fresh);
     // rounds frontier
-    for (;;) {
-      int32_t rs[2] = {R, 0};
-      h2d(s_small.p, rs, 8);
+    for (bool retry = false;; retry = true) {
+      int32_t rs[3] = {R, 0, 0};
+      if (retry) h2d(k_rs, rs, 12);
       t = tables();
       const int NP = (N + 15) & ~15;
       if (N > 32) {
@@ -582,27 +635,26 @@ struct hge_engine {
       } else {
         // first-strong-seer rows for every event that can still be a frontier member
         // (from a fresh state the frontier starts at round 0, position 0: no round trip)
-        bool fresh = R == 0;
-        for (int c = 0; c < N; c++) fresh = fresh && coords_len[c] == 0;
         std::vector<int32_t> fst(N + 1, 0);
         if (!fresh) {
           s_fst.need(N + 1);
-          KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, s_len.p, s_len.p + N, s_fst.p);
+          KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p);
           readback(fst.data(), s_fst.p, N + 1);
         }
         const int rlo = fst[0];
         const int Rprev = R;  // C rows >= Rprev are empty before this batch
         if (rlo != INF32) {
-          std::vector<int32_t> lo_off(2 * N + 1);
-          int tot = 0;
-          for (int c = 0; c < N; c++) {
-            lo_off[c] = fst[1 + c];
-            lo_off[N + c] = tot;
-            tot += std::max(0, chain_len[c] - fst[1 + c]);
+          int tot = fresh ? tot0 : 0;
+          if (!fresh) {
+            std::vector<int32_t> lo_off(2 * N + 1);
+            for (int c = 0; c < N; c++) {
+              lo_off[c] = fst[1 + c];
+              lo_off[N + c] = tot;
+              tot += std::max(0, chain_len[c] - fst[1 + c]);
+            }
+            lo_off[2 * N] = tot;
+            h2d(k_lo, lo_off.data(), 4 * (2 * N + 1));
           }
-          lo_off[2 * N] = tot;
-          s_fsslo.need(2 * N + 1);
-          h2d(s_fsslo.p, lo_off.data(), 4 * (2 * N + 1));
           int maxlen = 0;
           for (int c = 0; c < N; c++) maxlen = std::max(maxlen, chain_len[c]);
           if (tot > 0) {
@@ -610,15 +662,14 @@ struct hge_engine {
             // register walk over the global fss rows
 #define FSSL(NPC, LPC, B)                                                                          \
   if (maxlen < 0xFFFF) {                                                                           \
-    KLAUNCH(k_fss<NPC>, dim3(div_up((int64_t)tot * NPC, 256)), dim3(256), 0, st, t, s_fsslo.p,     \
-            s_fsslo.p + N, tot, (int32_t*)nullptr, (uint16_t*)d_FSS.p);                            \
+    KLAUNCH(k_fss<NPC>, dim3(div_up((int64_t)tot * NPC, 256)), dim3(256), 0, st, t, k_lo, k_lo + N, \
+            tot, (int32_t*)nullptr, (uint16_t*)d_FSS.p);                                           \
     KLAUNCH((k_rounds_walk<NPC, LPC, B>), dim3(1), dim3(1024), 0, st, t,                           \
-            (const uint16_t*)d_FSS.p, s_len.p, s_len.p + N, s_small.p, rlo, Rprev, dbg_p());       \
+            (const uint16_t*)d_FSS.p, k_len, k_len + N, k_rs, rlo, Rprev, dbg_p());                \
   } else {                                                                                         \
-    KLAUNCH(k_fss<NPC>, dim3(div_up((int64_t)tot * NPC, 256)), dim3(256), 0, st, t, s_fsslo.p,     \
-            s_fsslo.p + N, tot, d_FSS.p, (uint16_t*)nullptr);                                      \
-    KLAUNCH(k_rounds_fss<NPC>, dim3(1), dim3(64), 0, st, t, d_FSS.p, s_len.p, s_len.p + N,        \
-            s_small.p, rlo);                                                                       \
+    KLAUNCH(k_fss<NPC>, dim3(div_up((int64_t)tot * NPC, 256)), dim3(256), 0, st, t, k_lo, k_lo + N, \
+            tot, d_FSS.p, (uint16_t*)nullptr);                                                     \
+    KLAUNCH(k_rounds_fss<NPC>, dim3(1), dim3(64), 0, st, t, d_FSS.p, k_len, k_len + N, k_rs, rlo);  \
   }
             if (NP == 16) {
               FSSL(16, 4, 256)
@@ -634,22 +685,20 @@ struct hge_engine {
       // table overflowed: the loop grows it and walks again)
       t = tables();
       s_newwit.need(m);
-      HIPCHK(hipMemsetAsync(s_small.p + 4, 0, 4, st));
       KLAUNCH(k_round_assign, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0, (int)n1,
-              (const int32_t*)s_small.p, s_newwit.p, s_small.p + 4);
+              (const int32_t*)k_rs, s_newwit.p, k_rs + 2);
       KLAUNCH(k_witness_bits, dim3(std::min(div_up((int64_t)m * N, 256), 8192)), dim3(256), 0, st,
-              t, s_newwit.p, s_small.p + 4, N > 32 ? (const uint64_t*)d_ssc.p : nullptr);
+              t, s_newwit.p, k_rs + 2, N > 32 ? (const uint64_t*)d_ssc.p : nullptr);
       KLAUNCH(k_round_minw, dim3(div_up(Rcap, 256)), dim3(256), 0, st, t, 0,
-              (const int32_t*)s_small.p, d_minw.p);
-      h_minw.resize(Rcap);
-      d2h(rs, s_small.p, 8);
-      d2h(h_minw.data(), d_minw.p, 4 * (size_t)Rcap);
+              (const int32_t*)k_rs, d_minw.p);
+      h_minw.resize(Rcap + 2);
+      d2h(h_minw.data(), d_minw.p, 4 * ((size_t)Rcap + 2));
       sync();
-      if (rs[1]) {
+      if (h_minw[Rcap + 1]) {
         ensure_rcap((int64_t)Rcap * 2);
         continue;
       }
-      R = rs[0];
+      R = h_minw[Rcap];
       h_minw.resize(R);
       break;
     }
@@ -662,7 +711,7 @@ struct hge_engine {
   void rounds_coop() {
     Tables t = tables();
     s_fst.need(N + 1);
-    KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, s_len.p, s_len.p + N, s_fst.p);
+    KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p);
     int32_t rlo = INF32;
     readback(&rlo, s_fst.p, 1);
     if (rlo == INF32) return;
@@ -685,9 +734,9 @@ struct hge_engine {
     HIPCHK(hipMemsetAsync(s_bar.p, 0, 8, st));
     HIPCHK(hipMemsetAsync(s_gran.p, 0, 16 * (size_t)N, st));
     const int32_t* FDT = d_FDT.p;
-    const int32_t* olen = s_len.p;
-    const int32_t* len = s_len.p + N;
-    int32_t* rstate = s_small.p;
+    const int32_t* olen = k_len;
+    const int32_t* len = k_len + N;
+    int32_t* rstate = k_rs;
     uint64_t* gran = s_gran.p;
     int32_t* err = s_bar.p + 1;
     uint64_t* ssc = d_ssc.p;
@@ -703,28 +752,10 @@ struct hge_engine {
   }
 
   // coordinates: chain-prefix sweeps + transposes (hge_coords.hip)
-  void coords_sweep(Tables t) {
-    const int32_t* olen = s_len.p;
-    const int32_t* len = s_len.p + N;
-    int maxnew = 0, maxlen = 0;
-    std::vector<int2> segs;
-    // segment length: short segments give more workgroups, long ones fewer stale carries
-    static const int SEG = getenv("HGE_SEG") ? std::max(1, std::min(64, atoi(getenv("HGE_SEG")))) : 64;
-    for (int c = 0; c < N; c++) {
-      maxnew = std::max(maxnew, chain_len[c] - coords_len[c] + 1);
-      maxlen = std::max(maxlen, chain_len[c]);
-      for (int k = coords_len[c]; k < chain_len[c]; k += SEG) segs.push_back(make_int2(c, k));
-    }
-    // position-major order: workgroups are dispatched roughly in index order, so
-    // early positions of every chain are swept first and later segments read
-    // rows already updated in this sweep (Gauss-Seidel in time order)
-    if (!getenv("HGE_SEG_CHAIN_MAJOR"))
-      std::stable_sort(segs.begin(), segs.end(),
-                       [](const int2& a, const int2& b) { return a.y < b.y; });
-    const int nseg = (int)segs.size();
+  void coords_sweep(Tables t, int nseg, int SEG, int maxnew, bool fresh) {
+    const int32_t* olen = k_len;
+    const int32_t* len = k_len + N;
     if (nseg == 0) return;
-    s_segs.need(nseg);
-    h2d(s_segs.p, segs.data(), sizeof(int2) * nseg);
     KLAUNCH(k_la_clear, dim3(std::min(64, div_up((int64_t)maxnew * N, 256)), N), dim3(256), 0, st, t,
             olen, len);
     // sweeps until one changes nothing; queued in groups, checked once per group
@@ -741,7 +772,7 @@ struct hge_engine {
         switch (NPt) {
 #define SW(NPV)                                                                                  \
   case NPV:                                                                                      \
-    KLAUNCH(k_la_sweep<NPV>, dim3(div_up(nseg, 256 / NPV)), dim3(256), 0, st, t, s_segs.p, nseg, \
+    KLAUNCH(k_la_sweep<NPV>, dim3(div_up(nseg, 256 / NPV)), dim3(256), 0, st, t, k_segs, nseg,   \
             SEG, len, prev, s_chg.p + sw);                                                       \
     break;
           SW(16)
@@ -761,74 +792,77 @@ struct hge_engine {
       }
     }
     // LA -> LAT for positions [olen-1, len)
-    std::vector<int32_t> plo(N);
-    for (int c = 0; c < N; c++) plo[c] = std::max(coords_len[c] - 1, 0);
-    s_plo.need(2 * N);
-    h2d(s_plo.p, plo.data(), 4 * N);
     KLAUNCH(k_transpose, dim3(div_up(maxnew + 1, 64), div_up(N, 64), N), dim3(256), 0, st, t,
-            (const int32_t*)nullptr, d_LAT.p, s_plo.p, len, 0);
+            (const int32_t*)nullptr, d_LAT.p, k_plo, len, 0);
     // FDT: clear the new positions, then the runs of the new events
     KLAUNCH(k_fdt_clear, dim3(div_up(maxnew, 256), N, N), dim3(256), 0, st, t, d_FDT.p, olen, len);
     KLAUNCH(k_fdt_runs, dim3(div_up(maxnew, 256), N, N), dim3(256), 0, st, t, d_LAT.p, d_FDT.p,
             olen, len);
     // FDT -> FD rows for every chain-c position a new event can have touched
-    // (from a fresh state: every row; no round trip)
-    bool fresh = true;
-    for (int c = 0; c < N; c++) fresh = fresh && coords_len[c] == 0;
+    // (from a fresh state: every row, qlo = 0 as uploaded; no round trip)
     std::vector<int32_t> qlo(N, 0);
-    if (fresh) {
-      HIPCHK(hipMemsetAsync(s_plo.p + N, 0, 4 * N, st));
-    } else {
-      KLAUNCH(k_fd_qlo, dim3(div_up(N, 256)), dim3(256), 0, st, t, olen, len, s_plo.p + N);
-      readback(qlo.data(), s_plo.p + N, N);
+    if (!fresh) {
+      KLAUNCH(k_fd_qlo, dim3(div_up(N, 256)), dim3(256), 0, st, t, olen, len, k_qlo);
+      readback(qlo.data(), k_qlo, N);
     }
     int span = 1;
     for (int c = 0; c < N; c++) span = std::max(span, chain_len[c] - qlo[c]);
     KLAUNCH(k_transpose, dim3(div_up(span, 64), div_up(N, 64), N), dim3(256), 0, st, t, d_FDT.p,
-            (int32_t*)nullptr, s_plo.p + N, len, 1);
-    (void)maxlen;
+            (int32_t*)nullptr, k_qlo, len, 1);
   }
 
   // ---------------- one batch of consensus calls ----------------
   // calls: event counts n_c (<= n_divided), ascending.
+  // Host round trips: the fame-window coverage flags, the lowest candidate round
+  // of an online batch, the segment count for N > 64, and one closing readback.
+  // Control data goes up as one block (s_cctl), results come back as one block
+  // (s_out: counters, per-call counts, order).
   void consensus_batch(const std::vector<int64_t>& calls, bool do_fame, bool do_order,
                        bool commit, std::vector<int32_t>* order_out,
                        std::vector<int64_t>* counts_out) {
     const int ncalls = (int)calls.size();
     if (ncalls == 0) return;
     Tables t = tables();
-    s_nc.need(ncalls);
-    h2d(s_nc.p, calls.data(), 8 * ncalls);
     // R_c = Rounds() after the DivideRounds of call c = #{r : minw[r] < n_c}
-    // (minw is on the host since update_rdiv)
-    s_Rc.need(ncalls);
     std::vector<int32_t> Rc(ncalls);
     for (int c = 0; c < ncalls; c++)
       Rc[c] = (int32_t)(std::lower_bound(h_minw.begin(), h_minw.end(), calls[c],
                                          [](int32_t m, int64_t n) { return (int64_t)m < n; }) -
                         h_minw.begin());
-    h2d(s_Rc.p, Rc.data(), 4 * ncalls);
+    const bool fresh_und = und_fresh;
+    und_fresh = false;
+    const bool ord = do_order && n_und > 0;
+    const int ncand = (int)n_und;
+    int32_t* cand = d_und.p;
+    // lowest candidate round (a fresh replay's candidates include event 0, round 0)
+    int32_t mnr = 0;
+    if (ord && !fresh_und) {
+      h2d(s_small.p + 7, &kInf, 4);
+      KLAUNCH(k_min_round, dim3(div_up(ncand, 256)), dim3(256), 0, st, d_round.p, cand, ncand,
+              s_small.p + 7);
+      readback(&mnr, s_small.p + 7, 1);
+    }
+    const int rr_lo = mnr + 1;
+    const int R_last = Rc[ncalls - 1];
+    const int nr = ord ? std::max(0, R_last - rr_lo) : 0;
 
-    // ---- DecideFame windows (host enumeration of (round, call) pairs) ----
+    // ---- DecideFame windows (host enumeration of (round, call) pairs) + control block ----
     std::vector<int32_t> pr_round, pr_off, pr_cf, pr_len;
     int npairs = 0, nrounds = 0;
     int lcr_new = lcr, c_set = -1;
-    std::vector<int32_t> clast;
-    if (do_fame) {
-      const int i_lo = lcr + 1;
-      const int i_hi = Rc[ncalls - 1] - 2;  // processed rounds: i <= R_c - 2
-      int SPEC = 6;
-      for (;;) {
-        pr_round.clear();
-        pr_off.clear();
-        pr_cf.clear();
-        pr_len.clear();
-        npairs = 0;
+    const int i_lo = lcr + 1;
+    const int i_hi = Rc[ncalls - 1] - 2;  // processed rounds: i <= R_c - 2
+    for (int SPEC = 6;; SPEC *= 2) {
+      pr_round.clear();
+      pr_off.clear();
+      pr_cf.clear();
+      pr_len.clear();
+      npairs = 0;
+      if (do_fame) {
         int cfp = 0;
         for (int i = i_lo; i <= i_hi; i++) {
           while (cfp < ncalls && Rc[cfp] < i + 2) cfp++;
           if (cfp >= ncalls) break;
-          int ce = cfp;
           // last call with R_c <= i + 2 + SPEC
           int a = cfp, b = ncalls - 1;
           while (a < b) {
@@ -836,83 +870,74 @@ struct hge_engine {
             if (Rc[mid] <= i + 2 + SPEC) a = mid;
             else b = mid - 1;
           }
-          ce = a;
           pr_round.push_back(i);
           pr_off.push_back(npairs);
           pr_cf.push_back(cfp);
-          pr_len.push_back(ce - cfp + 1);
-          npairs += ce - cfp + 1;
+          pr_len.push_back(a - cfp + 1);
+          npairs += a - cfp + 1;
         }
-        nrounds = (int)pr_round.size();
-        if (nrounds == 0) break;
-        s_pr.need(4 * nrounds);
-        h2d(s_pr.p, pr_round.data(), 4 * nrounds);
-        h2d(s_pr.p + nrounds, pr_off.data(), 4 * nrounds);
-        h2d(s_pr.p + 2 * nrounds, pr_cf.data(), 4 * nrounds);
-        h2d(s_pr.p + 3 * nrounds, pr_len.data(), 4 * nrounds);
-        s_dec.need((size_t)npairs * N);
-        s_decbit.need(npairs);
-        s_Lc.need(ncalls);
-        s_LCR.need(ncalls);
-        s_clast.need(nrounds);
-        s_flags.need(4);
-        HIPCHK(hipMemsetAsync(s_Lc.p, 0xFF, 4 * ncalls, st));
-        HIPCHK(hipMemsetAsync(s_flags.p, 0, 16, st));
-        const int items = npairs * N;
-        fame_dispatch(0, t, nrounds, npairs, items, ncalls);
-        KLAUNCH(k_lcr_scan, dim3(1), dim3(1024), 0, st, s_Lc.p, ncalls, lcr, s_LCR.p,
-                           s_pr.p, s_pr.p + 2 * nrounds, s_pr.p + 3 * nrounds, nrounds,
-                           s_clast.p, s_flags.p);
-        int32_t fl[3];
-        readback(fl, s_flags.p, 3);
-        if (fl[0]) {
-          SPEC *= 2;
-          continue;
-        }
-        lcr_new = fl[1];
-        if (lcr_new > lcr) c_set = fl[2];
-        break;
       }
+      nrounds = (int)pr_round.size();
+      // control block: n_c (int64), R_c, L_c = -1, flags, the four window arrays,
+      // the round -> window map of the order pass
+      const size_t o_Rc = 2 * (size_t)ncalls, o_Lc = o_Rc + ncalls, o_fl = o_Lc + ncalls;
+      const size_t o_pr = o_fl + 4, o_pidx = o_pr + 4 * (size_t)nrounds;
+      std::vector<int32_t>& cc = h_cctl;
+      cc.assign(o_pidx + nr, 0);
+      memcpy(cc.data(), calls.data(), 8 * (size_t)ncalls);
+      memcpy(&cc[o_Rc], Rc.data(), 4 * (size_t)ncalls);
+      std::fill(cc.begin() + o_Lc, cc.begin() + o_fl, -1);
+      if (nrounds) {
+        memcpy(&cc[o_pr], pr_round.data(), 4 * (size_t)nrounds);
+        memcpy(&cc[o_pr + nrounds], pr_off.data(), 4 * (size_t)nrounds);
+        memcpy(&cc[o_pr + 2 * nrounds], pr_cf.data(), 4 * (size_t)nrounds);
+        memcpy(&cc[o_pr + 3 * nrounds], pr_len.data(), 4 * (size_t)nrounds);
+      }
+      for (int q = 0; q < nr; q++) cc[o_pidx + q] = -1;
+      for (int k = 0; k < nrounds; k++) {
+        const int i = pr_round[k];
+        if (i >= rr_lo && i < rr_lo + nr) cc[o_pidx + (i - rr_lo)] = k;
+      }
+      s_cctl.need(cc.size());
+      h2d(s_cctl.p, cc.data(), 4 * cc.size());
+      c_nc = (int64_t*)s_cctl.p;
+      c_Rc = s_cctl.p + o_Rc;
+      c_Lc = s_cctl.p + o_Lc;
+      c_flags = s_cctl.p + o_fl;
+      c_pr = s_cctl.p + o_pr;
+      c_pidx = s_cctl.p + o_pidx;
+      if (nrounds == 0) break;
+      s_dec.need((size_t)npairs * N);
+      s_decbit.need(npairs);
+      s_LCR.need(ncalls);
+      s_clast.need(nrounds);
+      fame_dispatch(0, t, nrounds, npairs, npairs * N, ncalls);
+      KLAUNCH(k_lcr_scan, dim3(1), dim3(1024), 0, st, c_Lc, ncalls, lcr, s_LCR.p, c_pr,
+              c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds, s_clast.p, c_flags);
+      int32_t fl[3];
+      readback(fl, c_flags, 3);
+      if (fl[0]) continue;  // a round stayed undecided past its window: widen
+      lcr_new = fl[1];
+      if (lcr_new > lcr) c_set = fl[2];
+      break;
     }
 
     // ---- DecideRoundReceived / FindOrder ----
-    // Everything below is enqueued without a host round trip (counts stay on the
-    // device; buffers and grids are sized by upper bounds) except the lowest
-    // candidate round of an online batch and, for N > 64, the segment count.
-    const bool fresh_und = und_fresh;
-    und_fresh = false;
     bool got_order = false;
-    int32_t nrecv = 0, nund = 0, rcnt_r = 0, late = 0;
-    unsigned long long ntx = 0;
-    if (do_order && n_und > 0) {
-      const int ncand = (int)n_und;
-      int32_t* cand = d_und.p;
-      // lowest candidate round (a fresh replay's candidates include event 0, round 0)
-      int32_t mnr = 0;
-      if (!fresh_und) {
-        h2d(s_small.p + 7, &kInf, 4);
-        KLAUNCH(k_min_round, dim3(div_up(ncand, 256)), dim3(256), 0, st, d_round.p, cand, ncand,
-                s_small.p + 7);
-        readback(&mnr, s_small.p + 7, 1);
-      }
-      const int rr_lo = mnr + 1;
-      const int R_last = Rc[ncalls - 1];
-      const int nr = std::max(0, R_last - rr_lo);
+    s_out.need(8 + (size_t)ncalls + (ord ? ncand : 0));
+    int32_t* o_cnt = s_out.p;  // [0] received [1] undetermined [2] LCR events [4..5] tx
+    int32_t* o_cc = s_out.p + 8;
+    int32_t* o_ids = s_out.p + 8 + ncalls;
+    unsigned long long* o_ntx = (unsigned long long*)(s_out.p + 4);
+    HIPCHK(hipMemsetAsync(s_out.p, 0, 4 * (8 + (size_t)ncalls), st));
+    if (ord) {
       if (nr > 0) {
-        // map rounds -> fame window index
-        std::vector<int32_t> pidx(nr, -1);
-        for (int k = 0; k < nrounds; k++) {
-          int i = pr_round[k];
-          if (i >= rr_lo && i < R_last) pidx[i - rr_lo] = k;
-        }
-        s_prindex.need(nr);
-        h2d(s_prindex.p, pidx.data(), 4 * nr);
         SegInfo si;
-        si.pr_index = s_prindex.p;
+        si.pr_index = c_pidx;
         if (nrounds > 0) {
-          si.pr_off = s_pr.p + nrounds;
-          si.pr_cf = s_pr.p + 2 * nrounds;
-          si.pr_len = s_pr.p + 3 * nrounds;
+          si.pr_off = c_pr + nrounds;
+          si.pr_cf = c_pr + 2 * nrounds;
+          si.pr_len = c_pr + 3 * nrounds;
           si.clast = s_clast.p;
           si.dec = s_dec.p;
         } else {
@@ -922,11 +947,11 @@ struct hge_engine {
         s_segcnt.need(nr);
         s_segoff.need(nr + 1);
         s_arr.need((size_t)nr * N);
-        KLAUNCH(k_arrivals, dim3(div_up(nr * N, 256)), dim3(256), 0, st, t, rr_lo, nr, s_nc.p,
+        KLAUNCH(k_arrivals, dim3(div_up(nr * N, 256)), dim3(256), 0, st, t, rr_lo, nr, c_nc,
                 ncalls, s_arr.p);
         seg_dispatch(0, t, rr_lo, nr, ncalls, si, 0);
         KLAUNCH(k_scan_small, dim3(1), dim3(1024), 0, st, s_segcnt.p, s_segoff.p, nr,
-                           s_small.p + 6);
+                s_small.p + 6);
         // a round's segments start at call 0, at a witness arrival (<= N distinct
         // calls), at the window start or at a processed call of its fame window
         int64_t nseg = (int64_t)nr * (N + 2) + npairs;
@@ -951,20 +976,18 @@ struct hge_engine {
         s_recv.need(ncand);
         HIPCHK(hipMemsetAsync(s_recv.p, 0xFF, 4 * ncand, st));
       }
-      // compaction + sort (the received count stays on the device: s_small[2])
+      // compaction + sort (the received count stays on the device: o_cnt[0])
       s_frecv.need(ncand);
       s_fund.need(ncand);
       s_rank.need(ncand);
       s_upos.need(ncand);
       KLAUNCH(k_recv_flags, dim3(div_up(ncand, 256)), dim3(256), 0, st, s_recv.p, ncand,
                          s_frecv.p, s_fund.p, commit ? 1 : 0);
-      scan_large(s_frecv.p, s_rank.p, ncand, s_small.p + 2);
-      s_ntx.need(1);
-      HIPCHK(hipMemsetAsync(s_ntx.p, 0, 8, st));
+      scan_large(s_frecv.p, s_rank.p, ncand, o_cnt);
       KLAUNCH(k_set_rr, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand, s_recv.p,
-              s_rr.p, s_cts.p, d_rr.p, d_cts.p, s_ntx.p, commit ? 1 : 0);
+              s_rr.p, s_cts.p, d_rr.p, d_cts.p, o_ntx, commit ? 1 : 0);
       if (commit) {
-        const int32_t* pn = s_small.p + 2;
+        const int32_t* pn = o_cnt;
         s_keys.need((size_t)ncand * sizeof(OKey));
         s_keys2.need((size_t)ncand * sizeof(OKey));
         OKey* k1 = (OKey*)s_keys.p;
@@ -977,30 +1000,15 @@ struct hge_engine {
           KLAUNCH(k_merge_pass, dim3(div_up(ncand, 256)), dim3(256), 0, st, k1, k2, pn, run);
           std::swap(k1, k2);
         }
-        s_ids.need(ncand);
-        s_ccount.need(ncalls);
-        HIPCHK(hipMemsetAsync(s_ccount.p, 0, 4 * ncalls, st));
-        KLAUNCH(k_emit_order, dim3(div_up(ncand, 256)), dim3(256), 0, st, k1, pn, s_ids.p,
-                s_ccount.p, 0);
+        KLAUNCH(k_emit_order, dim3(div_up(ncand, 256)), dim3(256), 0, st, k1, pn, o_ids, o_cc, 0);
         // new undetermined list (in candidate order)
-        scan_large(s_fund.p, s_upos.p, ncand, s_small.p + 3);
+        scan_large(s_fund.p, s_upos.p, ncand, o_cnt + 1);
         s_und2.need(ncand);
         KLAUNCH(k_scatter_und, dim3(div_up(ncand, 256)), dim3(256), 0, st, cand, ncand,
                            s_fund.p, s_upos.p, s_und2.p);
         HIPCHK(hipMemcpyAsync(d_und.p, s_und2.p, 4 * (size_t)ncand, hipMemcpyDeviceToDevice, st));
-        h_ids.resize(ncand);
-        h_cc.resize(ncalls);
-        d2h(&nrecv, s_small.p + 2, 4);
-        d2h(&nund, s_small.p + 3, 4);
-        d2h(&ntx, s_ntx.p, 8);
-        d2h(h_ids.data(), s_ids.p, 4 * (size_t)ncand);
-        d2h(h_cc.data(), s_ccount.p, 4 * (size_t)ncalls);
         got_order = true;
-      } else if (counts_out) {
-        for (int c = 0; c < ncalls; c++) counts_out->push_back(0);
       }
-    } else if (do_order && counts_out) {
-      for (int c = 0; c < ncalls; c++) counts_out->push_back(0);
     }
 
     // ---- persist fame / LCR ----
@@ -1013,30 +1021,33 @@ struct hge_engine {
         lcr_up = true;
         const int r = lcr_new - 1;
         if (r >= 0) {
-          d2h(&rcnt_r, d_rcnt.p + r, 4);
-          const int64_t nfrom = calls[c_set];
-          if (nfrom < n_coords) {
-            HIPCHK(hipMemsetAsync(s_small.p + 5, 0, 4, st));
-            KLAUNCH(k_count_late, dim3(div_up(n_coords - nfrom, 256)), dim3(256), 0, st,
-                               t, (int)nfrom, (int)n_coords, r, s_small.p + 5);
-            d2h(&late, s_small.p + 5, 4);
-          }
+          const int64_t nfrom = std::min<int64_t>(calls[c_set], n_coords);
+          KLAUNCH(k_lcre, dim3(std::max(1, div_up(n_coords - nfrom, 256))), dim3(256), 0, st, t,
+                  (int)nfrom, (int)n_coords, r, o_cnt + 2);
         }
       }
     }
     // the batch's one closing round trip
+    h_out.resize(8 + (size_t)ncalls + (got_order ? ncand : 0));
+    d2h(h_out.data(), s_out.p, 4 * h_out.size());
     sync();
+    const int32_t nrecv = h_out[0];
     if (got_order) {
-      consensus.insert(consensus.end(), h_ids.begin(), h_ids.begin() + nrecv);
+      const int32_t* ids = h_out.data() + 8 + ncalls;
+      unsigned long long ntx = 0;
+      memcpy(&ntx, &h_out[4], 8);
+      consensus.insert(consensus.end(), ids, ids + nrecv);
       ctx += (int64_t)ntx;
-      if (order_out) order_out->insert(order_out->end(), h_ids.begin(), h_ids.begin() + nrecv);
+      if (order_out) order_out->insert(order_out->end(), ids, ids + nrecv);
       if (counts_out)
-        for (int c = 0; c < ncalls; c++) counts_out->push_back(h_cc[c]);
-      n_und = nund;
+        for (int c = 0; c < ncalls; c++) counts_out->push_back(h_out[8 + c]);
+      n_und = h_out[1];
+    } else if (do_order && counts_out) {
+      for (int c = 0; c < ncalls; c++) counts_out->push_back(0);
     }
     if (lcr_up) {
       lcr = lcr_new;
-      lcre = lcr_new - 1 >= 0 ? rcnt_r - late : 0;
+      lcre = lcr_new - 1 >= 0 ? h_out[2] : 0;
     }
     prof_collect();
   }
@@ -1066,8 +1077,8 @@ struct hge_engine {
 
   void fame_dispatch(int which, const Tables& t, int nrounds, int npairs, int items, int ncalls) {
     if (which == 1) {
-      KLAUNCH(k_fame_persist, dim3(div_up((int64_t)nrounds * N, 256)), dim3(256), 0, st, t, s_pr.p,
-              s_pr.p + nrounds, s_pr.p + 2 * nrounds, s_pr.p + 3 * nrounds, nrounds, s_clast.p,
+      KLAUNCH(k_fame_persist, dim3(div_up((int64_t)nrounds * N, 256)), dim3(256), 0, st, t, c_pr,
+              c_pr + nrounds, c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds, s_clast.p,
               s_dec.p);
       return;
     }
@@ -1075,24 +1086,24 @@ struct hge_engine {
     switch (NW) {
 #define FCASE(B)                                                                                 \
   case B:                                                                                        \
-    KLAUNCH(k_fame_decide<B>, dim3(div_up(items, 256)), dim3(256), 0, st, t, s_pr.p,             \
-            s_pr.p + nrounds, s_pr.p + 2 * nrounds, nrounds, npairs, s_nc.p, s_Rc.p, s_dec.p);   \
+    KLAUNCH(k_fame_decide<B>, dim3(div_up(items, 256)), dim3(256), 0, st, t, c_pr,             \
+            c_pr + nrounds, c_pr + 2 * nrounds, nrounds, npairs, c_nc, c_Rc, s_dec.p);   \
     if (G == 16)                                                                                 \
       KLAUNCH(k_fame_timeline_g<16>, dim3(div_up((int64_t)nrounds * 16, 256)), dim3(256), 0, st, \
-              t, s_pr.p, s_pr.p + nrounds, s_pr.p + 2 * nrounds, s_pr.p + 3 * nrounds, nrounds,  \
-              s_nc.p, s_dec.p, s_decbit.p, s_Lc.p);                                              \
+              t, c_pr, c_pr + nrounds, c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds,  \
+              c_nc, s_dec.p, s_decbit.p, c_Lc);                                              \
     else if (G == 32)                                                                            \
       KLAUNCH(k_fame_timeline_g<32>, dim3(div_up((int64_t)nrounds * 32, 256)), dim3(256), 0, st, \
-              t, s_pr.p, s_pr.p + nrounds, s_pr.p + 2 * nrounds, s_pr.p + 3 * nrounds, nrounds,  \
-              s_nc.p, s_dec.p, s_decbit.p, s_Lc.p);                                              \
+              t, c_pr, c_pr + nrounds, c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds,  \
+              c_nc, s_dec.p, s_decbit.p, c_Lc);                                              \
     else if (G == 64)                                                                            \
       KLAUNCH(k_fame_timeline_g<64>, dim3(div_up((int64_t)nrounds * 64, 256)), dim3(256), 0, st, \
-              t, s_pr.p, s_pr.p + nrounds, s_pr.p + 2 * nrounds, s_pr.p + 3 * nrounds, nrounds,  \
-              s_nc.p, s_dec.p, s_decbit.p, s_Lc.p);                                              \
+              t, c_pr, c_pr + nrounds, c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds,  \
+              c_nc, s_dec.p, s_decbit.p, c_Lc);                                              \
     else                                                                                         \
-      KLAUNCH(k_fame_timeline<B>, dim3(div_up(nrounds, 64)), dim3(64), 0, st, t, s_pr.p,         \
-              s_pr.p + nrounds, s_pr.p + 2 * nrounds, s_pr.p + 3 * nrounds, nrounds, s_nc.p,     \
-              s_dec.p, s_decbit.p, s_Lc.p);                                                      \
+      KLAUNCH(k_fame_timeline<B>, dim3(div_up(nrounds, 64)), dim3(64), 0, st, t, c_pr,         \
+              c_pr + nrounds, c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds, c_nc,     \
+              s_dec.p, s_decbit.p, c_Lc);                                                      \
     break;
       FCASE(1)
       FCASE(2)
@@ -1113,18 +1124,18 @@ struct hge_engine {
   case B:                                                                                        \
     if (G == 16)                                                                                 \
       KLAUNCH(k_segments_g<16>, dim3(div_up((int64_t)nr * 16, 256)), dim3(256), 0, st, t, rr_lo, \
-              nr, s_nc.p, ncalls, si, s_arr.p, s_segcnt.p, s_segoff.p, s_segcall.p,              \
+              nr, c_nc, ncalls, si, s_arr.p, s_segcnt.p, s_segoff.p, s_segcall.p,              \
               s_seground.p, s_segdec.p, s_segfws.p, mode);                                       \
     else if (G == 32)                                                                            \
       KLAUNCH(k_segments_g<32>, dim3(div_up((int64_t)nr * 32, 256)), dim3(256), 0, st, t, rr_lo, \
-              nr, s_nc.p, ncalls, si, s_arr.p, s_segcnt.p, s_segoff.p, s_segcall.p,              \
+              nr, c_nc, ncalls, si, s_arr.p, s_segcnt.p, s_segoff.p, s_segcall.p,              \
               s_seground.p, s_segdec.p, s_segfws.p, mode);                                       \
     else if (G == 64)                                                                            \
       KLAUNCH(k_segments_g<64>, dim3(div_up((int64_t)nr * 64, 256)), dim3(256), 0, st, t, rr_lo, \
-              nr, s_nc.p, ncalls, si, s_arr.p, s_segcnt.p, s_segoff.p, s_segcall.p,              \
+              nr, c_nc, ncalls, si, s_arr.p, s_segcnt.p, s_segoff.p, s_segcall.p,              \
               s_seground.p, s_segdec.p, s_segfws.p, mode);                                       \
     else                                                                                         \
-      KLAUNCH(k_segments<B>, dim3(div_up(nr, 64)), dim3(64), 0, st, t, rr_lo, nr, s_nc.p,        \
+      KLAUNCH(k_segments<B>, dim3(div_up(nr, 64)), dim3(64), 0, st, t, rr_lo, nr, c_nc,        \
               ncalls, si, s_arr.p, s_segcnt.p, s_segoff.p, s_segcall.p, s_seground.p,            \
               s_segdec.p, s_segfws.p, mode);                                                     \
     if (mode == 1 && nseg > 0)                                                                   \
@@ -1154,7 +1165,7 @@ struct hge_engine {
 #define RCASE(B)                                                                                 \
   case B:                                                                                        \
     KLAUNCH(k_round_received<B>, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, \
-                       ncand, s_nc.p, ncalls, 0, rr_lo, R_last, s_segoff.p, s_segcnt.p,          \
+                       ncand, c_nc, ncalls, 0, rr_lo, R_last, s_segoff.p, s_segcnt.p,          \
                        s_segcall.p, s_segdec.p, s_segfws.p, s_theta.p, s_recv.p, s_rr.p,         \
                        s_cts.p, bseg);                                                           \
     if (wmed)                                                                                    \
@@ -1354,15 +1365,7 @@ int hge_replay_run(hge_engine* h, int64_t* n_ordered) {
   h->ctx = 0;
   h->consensus.clear();
   h->n_und = 0;
-  {
-    h->fill_i32(h->d_C.p, (int64_t)h->Rcap * h->N, INF32);
-    HIPCHK(hipMemsetAsync(h->d_W.p, 0xFF, (size_t)h->Rcap * h->N * 4, h->st));
-    HIPCHK(hipMemsetAsync(h->d_ssb.p, 0, (size_t)h->Rcap * h->N * h->NW * 8, h->st));
-    HIPCHK(hipMemsetAsync(h->d_seeb.p, 0, (size_t)h->Rcap * h->N * h->NW * 8, h->st));
-    HIPCHK(hipMemsetAsync(h->d_fame.p, 0, (size_t)h->Rcap * h->N, h->st));
-    HIPCHK(hipMemsetAsync(h->d_rcnt.p, 0, (size_t)h->Rcap * 4, h->st));
-    HIPCHK(hipMemsetAsync(h->d_rr.p, 0xFF, (size_t)h->Ecap * 4, h->st));
-  }
+  h->reset_rounds();
   HIPCHK(hipEventRecord(h->ev[0], h->st));
   h->coords();
   HIPCHK(hipEventRecord(h->ev[1], h->st));

@@ -35,6 +35,7 @@ struct Tables {
   const uint8_t* coin;
   const int32_t* ntx;
   int32_t* chain;
+  int2* opcp;     // [N][ccap]: (creator, index) of the other-parent, (-1, -1) if none
   int32_t* LA;
   int32_t* FD;
   int32_t* round;
@@ -131,7 +132,11 @@ __global__ void k_scan_add(int32_t* out, int n, const int32_t* partial_scanned) 
 // chain table: chain[c][index] = id for the new events
 __global__ void k_chain_fill(Tables t, int n0, int n1) {
   const int x = n0 + blockIdx.x * blockDim.x + threadIdx.x;
-  if (x < n1) t.chain[(size_t)t.creator[x] * t.ccap + t.index[x]] = x;
+  if (x >= n1) return;
+  const size_t at = (size_t)t.creator[x] * t.ccap + t.index[x];
+  t.chain[at] = x;
+  const int o = t.op[x];
+  t.opcp[at] = o >= 0 ? make_int2(t.creator[o], t.index[o]) : make_int2(-1, -1);
 }
 
 // HGE_STAMPS diagnostics: shader-clock stamp, ordered with the code around it
@@ -568,6 +573,11 @@ __global__ void k_round_assign(Tables t, int n0, int n1, const int32_t* rstate, 
 // first witness id per round (monotone increasing in r); rounds [r0, R)
 __global__ void k_round_minw(Tables t, int r0, const int32_t* rstate, int32_t* minw) {
   const int r = r0 + blockIdx.x * blockDim.x + threadIdx.x;
+  // the round count and overflow flag ride along at minw[Rcap..Rcap+1] (one readback)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    minw[t.Rcap] = rstate[0];
+    minw[t.Rcap + 1] = rstate[1];
+  }
   if (rstate[1] || r >= rstate[0]) return;
   int m = INF32;
   for (int c = 0; c < t.N; c++) {
@@ -741,16 +751,14 @@ __global__ void __launch_bounds__(1024) k_lcr_scan(const int32_t* Lc, int ncalls
   for (int i = lo; i < hi; i++) m = max(m, Lc[i]);
   tmp[tid] = m;
   __syncthreads();
-  if (tid == 0) {
-    int run = lcr_start;
-    for (int i = 0; i < T; i++) {
-      const int v = tmp[i];
-      tmp[i] = run;
-      run = max(run, v);
-    }
+  // inclusive max-scan over the threads' partial maxima (Hillis-Steele)
+  for (int off = 1; off < T; off <<= 1) {
+    const int o = (tid >= off) ? tmp[tid - off] : -1;
+    __syncthreads();
+    tmp[tid] = max(tmp[tid], o);
+    __syncthreads();
   }
-  __syncthreads();
-  int run = tmp[tid];
+  int run = max(lcr_start, tid > 0 ? tmp[tid - 1] : -1);
   for (int i = lo; i < hi; i++) {
     run = max(run, Lc[i]);
     LCR[i] = run;
@@ -1428,11 +1436,30 @@ __global__ void k_set_rr(Tables t, const int32_t* cand, int ncand, const int32_t
 }
 
 // LastCommitedRoundEvents = RoundEvents(LCR-1) at the call that set LCR
-// (hashgraph.go:666-673): events of round r minus those inserted after that call.
-__global__ void k_count_late(Tables t, int n_from, int n1, int r, int32_t* out) {
+// (hashgraph.go:666-673): events of round r minus those inserted after that
+// call (ids >= n_from).  *out starts at 0.
+__global__ void k_lcre(Tables t, int n_from, int n1, int r, int32_t* out) {
   const int x = n_from + blockIdx.x * blockDim.x + threadIdx.x;
-  if (x >= n1) return;
-  if (t.round[x] == r) atomicAdd(out, 1);
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(out, t.rcnt[r]);
+  if (x < n1 && t.round[x] == r) atomicSub(out, 1);
+}
+
+// fresh consensus state: C = INF, W = -1, bitsets / fame / counts = 0, rr = -1
+__global__ void k_reset_rounds(Tables t, int64_t nrow, int64_t nbits, int64_t nev,
+                               int32_t* rr) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nrow; i += stride) {
+    t.C[i] = INF32;
+    t.W[i] = -1;
+    t.fame[i] = 0;
+  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nbits; i += stride) {
+    t.ssb[i] = 0;
+    t.seeb[i] = 0;
+  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nev; i += stride) rr[i] = -1;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < t.Rcap; i += stride)
+    t.rcnt[i] = 0;
 }
 
 }  // namespace hge

@@ -83,6 +83,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--ramp-s", type=float, default=0.3,
+                    help="untimed clock ramp before the warmup steps (seconds)")
     ap.add_argument("--workload", choices=("gossip", "mc"), default="gossip")
     ap.add_argument("--participants", type=int, default=None)
     ap.add_argument("--events", type=int, default=None)
@@ -141,6 +143,11 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
+    # the GPU and the host thread leave their idle clocks only under sustained load:
+    # run the path for ~0.3 s before the W warmup steps (none of it is timed)
+    t_ramp = time.perf_counter()
+    while time.perf_counter() - t_ramp < args.ramp_s:
+        step()
     for _ in range(args.warmup):
         step()
     sync_all()
