@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -119,7 +120,6 @@ struct hge_engine {
 
   // replay staging
   std::vector<int64_t> replay_calls;  // n_c per call (accepted counts)
-  std::vector<int32_t> replay_order;
   std::vector<int64_t> replay_counts;
 
   // ---- device tables ----
@@ -164,7 +164,7 @@ struct hge_engine {
   std::vector<int32_t> h_minw;  // first witness id per round (read back by coords)
   // consensus control block (one upload) and results block (one readback)
   DBuf<int32_t> s_cctl, s_out;
-  std::vector<int32_t> h_cctl, h_out;
+  std::vector<int32_t> h_cctl;
   int64_t* c_nc = nullptr;
   int32_t *c_Rc = nullptr, *c_Lc = nullptr, *c_flags = nullptr, *c_pr = nullptr, *c_pidx = nullptr;
   // coordinates control block (coords): pointers into s_kctl
@@ -561,6 +561,13 @@ struct hge_engine {
     char* q = pin_take(bytes);
     HIPCHK(hipMemcpyAsync(q, dev, bytes, hipMemcpyDeviceToHost, st));
     pending.push_back({host, (size_t)(q - pin), bytes});
+  }
+  // download into the arena itself: the returned offset stays readable after the
+  // next sync() until the arena is used again (no second host copy)
+  size_t d2h_pinned(const void* dev, size_t bytes) {
+    char* q = pin_take(bytes);
+    if (bytes) HIPCHK(hipMemcpyAsync(q, dev, bytes, hipMemcpyDeviceToHost, st));
+    return (size_t)(q - pin);
   }
   void sync() {
     HIPCHK(hipStreamSynchronize(st));
@@ -1027,27 +1034,27 @@ struct hge_engine {
         }
       }
     }
-    // the batch's one closing round trip
-    h_out.resize(8 + (size_t)ncalls + (got_order ? ncand : 0));
-    d2h(h_out.data(), s_out.p, 4 * h_out.size());
+    // the batch's one closing round trip (read in place from the pinned arena)
+    const size_t off = d2h_pinned(s_out.p, 4 * (8 + (size_t)ncalls + (got_order ? ncand : 0)));
     sync();
-    const int32_t nrecv = h_out[0];
+    const int32_t* ho = (const int32_t*)(pin + off);
+    const int32_t nrecv = ho[0];
     if (got_order) {
-      const int32_t* ids = h_out.data() + 8 + ncalls;
+      const int32_t* ids = ho + 8 + ncalls;
       unsigned long long ntx = 0;
-      memcpy(&ntx, &h_out[4], 8);
+      memcpy(&ntx, ho + 4, 8);
       consensus.insert(consensus.end(), ids, ids + nrecv);
       ctx += (int64_t)ntx;
       if (order_out) order_out->insert(order_out->end(), ids, ids + nrecv);
       if (counts_out)
-        for (int c = 0; c < ncalls; c++) counts_out->push_back(h_out[8 + c]);
-      n_und = h_out[1];
+        for (int c = 0; c < ncalls; c++) counts_out->push_back(ho[8 + c]);
+      n_und = ho[1];
     } else if (do_order && counts_out) {
       for (int c = 0; c < ncalls; c++) counts_out->push_back(0);
     }
     if (lcr_up) {
       lcr = lcr_new;
-      lcre = lcr_new - 1 >= 0 ? h_out[2] : 0;
+      lcre = lcr_new - 1 >= 0 ? ho[2] : 0;
     }
     prof_collect();
   }
@@ -1365,27 +1372,38 @@ int hge_replay_run(hge_engine* h, int64_t* n_ordered) {
   h->ctx = 0;
   h->consensus.clear();
   h->n_und = 0;
+  const auto w0 = std::chrono::steady_clock::now();
   h->reset_rounds();
   HIPCHK(hipEventRecord(h->ev[0], h->st));
   h->coords();
   HIPCHK(hipEventRecord(h->ev[1], h->st));
+  const auto w1 = std::chrono::steady_clock::now();
   h->n_divided = keep;
   h->update_rdiv();
   if (keep > 0) h->fill_iota(h->d_und.p, keep, 0);
   h->n_und = keep;
   h->und_fresh = keep > 0;
-  h->replay_order.clear();
   h->replay_counts.clear();
-  h->consensus_batch(h->replay_calls, true, true, true, &h->replay_order, &h->replay_counts);
+  // the consensus log (cleared above) is the replay's order
+  h->consensus_batch(h->replay_calls, true, true, true, nullptr, &h->replay_counts);
   HIPCHK(hipEventRecord(h->ev[2], h->st));
   HIPCHK(hipEventSynchronize(h->ev[2]));
+  const auto w2 = std::chrono::steady_clock::now();
   float a = 0, b = 0;
   HIPCHK(hipEventElapsedTime(&a, h->ev[0], h->ev[1]));
   HIPCHK(hipEventElapsedTime(&b, h->ev[1], h->ev[2]));
+  auto ms = [](std::chrono::steady_clock::time_point x, std::chrono::steady_clock::time_point y) {
+    return (float)std::chrono::duration<double, std::milli>(y - x).count();
+  };
+  // [0] coordinates+rounds on the GPU, [1] their wall time, [2] consensus wall time,
+  // [3] consensus on the GPU, [4] replay wall time, [6] GPU total
   h->stage_ms[0] = a;
+  h->stage_ms[1] = ms(w0, w1);
+  h->stage_ms[2] = ms(w1, w2);
   h->stage_ms[3] = b;
+  h->stage_ms[4] = ms(w0, w2);
   h->stage_ms[6] = a + b;
-  if (n_ordered) *n_ordered = (int64_t)h->replay_order.size();
+  if (n_ordered) *n_ordered = (int64_t)h->consensus.size();
   h->dbg_dump();
   return HGE_OK;
   GUARD_END(h)
@@ -1393,8 +1411,8 @@ int hge_replay_run(hge_engine* h, int64_t* n_ordered) {
 
 int hge_replay_fetch(hge_engine* h, int32_t* order_out, int64_t cap, int64_t* call_counts_out) {
   GUARD_BEGIN
-  for (int64_t i = 0; i < (int64_t)h->replay_order.size() && i < cap && order_out; i++)
-    order_out[i] = h->replay_order[i];
+  for (int64_t i = 0; i < (int64_t)h->consensus.size() && i < cap && order_out; i++)
+    order_out[i] = h->consensus[i];
   if (call_counts_out)
     for (size_t c = 0; c < h->replay_counts.size(); c++) call_counts_out[c] = h->replay_counts[c];
   return HGE_OK;

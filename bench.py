@@ -159,8 +159,15 @@ def main():
     sync_all()
     step_s = (t1 - t0) / args.steps
 
-    # ---- profiled pass: per-kernel device time (HIP events on the engine stream) ----
+    # ---- one more unprofiled replay: GPU-busy vs wall split of a step ----
     eng0 = engines[0]
+    eng0.run()
+    st_ms = eng0.stage_times()
+    replay_ms = {"coords_gpu": st_ms[0], "coords_wall": st_ms[1], "consensus_gpu": st_ms[3],
+                 "consensus_wall": st_ms[2], "gpu": st_ms[6], "wall": st_ms[4]}
+    replay_ms = {k: round(v, 4) for k, v in replay_ms.items()}
+
+    # ---- profiled pass: per-kernel device time (HIP events on the engine stream) ----
     eng0.set_profiling(True)
     for _ in range(max(1, args.profile_steps)):
         eng0.run()
@@ -259,6 +266,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "ingest_host_ms": round(ingest_s * 1e3, 2),
+            "replay_ms": replay_ms,
             "kernels_ms_per_replay": {k: round(v[0] / nprof, 4) for k, v in
                                       sorted(kstats.items(), key=lambda kv: -kv[1][0])},
             "kernel_launches_per_replay": {k: v[1] // nprof for k, v in kstats.items()},
