@@ -266,15 +266,18 @@ __global__ void __launch_bounds__(64) k_rounds_fss(Tables t, const int32_t* FSS,
 // Every step depends on the previous one, so the walk is latency-bound and
 // runs in ONE wave with no barriers: lane (c, q) = chain c, quarter q of the
 // d range (LPC lanes per chain, VPL = NPC/LPC values per lane).  A step is
-// VPL LDS gathers of uint16 fss values (0xFFFF = none), an all-ascending
-// bitonic network over the NPC values of each chain whose in-lane stages are
-// register min/max and whose cross-lane stages are DPP quad permutes, and one
-// LDS store of the new frontier.  Global traffic is taken out of the step:
-// all 16 waves stage blocks of uint16 fss rows [P_d, P_d + B) of every chain
-// into LDS (chain positions < 65535, checked by the host) together with the
-// already-known C rows of the next RB rounds; the walk buffers its C rows in
-// LDS and they are flushed at the next restage.  The own-chain clamp (an
-// event never strongly sees itself) is folded into the rows by k_fss.
+// one LDS read of the members' block rows, VPL LDS gathers of uint16 fss
+// values (0xFFFF = none), an all-ascending bitonic network over the NPC values
+// of each chain whose in-lane stages are register min/max and whose
+// cross-lane stages are DPP quad permutes, and the owner lane's LDS stores.
+// Global traffic is taken out of the step: all 16 waves stage blocks of uint16
+// fss rows [P_d, P_d + B) of every chain into LDS (chain positions < 65535,
+// checked by the host) together with the already-known C rows of the next RB
+// rounds; the walk buffers its C rows in LDS and they are flushed at the next
+// restage.  Row B of every chain's block is all 0xFFFF: an absent member
+// (no frontier event) gathers from it, so a gather address is one shift-add of
+// the member's block row.  The own-chain clamp (an event never strongly sees
+// itself) is folded into the rows by k_fss.
 // ---------------------------------------------------------------------------
 // lane l reads lane l ^ X within its quad (X in 1..3): quad_perm DPP
 template <int X>
@@ -289,6 +292,79 @@ __device__ __forceinline__ int dpp_flip(int x, int v) {
   return x == 1 ? dpp_flip<1>(v) : x == 2 ? dpp_flip<2>(v) : dpp_flip<3>(v);
 }
 
+// packed uint16 pairs (v_pk_min_u16 / v_pk_max_u16)
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pmin(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a),
+                                                                __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ uint32_t pmax(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a),
+                                                                __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ uint32_t hswap(uint32_t a) { return __builtin_amdgcn_alignbit(a, a, 16); }
+// (lo of a, hi of b)
+__device__ __forceinline__ uint32_t lohi(uint32_t a, uint32_t b) {
+  return (a & 0xFFFFu) | (b & 0xFFFF0000u);
+}
+// in-register compare-exchange of the two halves (lo gets the min)
+__device__ __forceinline__ uint32_t cx_half(uint32_t r) {
+  const uint32_t sw = hswap(r);
+  return lohi(pmin(r, sw), pmax(r, sw));
+}
+// cross-lane stage: lower lanes keep the minima, upper lanes the maxima
+__device__ __forceinline__ uint32_t cx_lane(bool lower, uint32_t a, uint32_t o) {
+  return lower ? pmin(a, o) : pmax(a, o);
+}
+
+// All-ascending bitonic sort of the 16 values of one chain held by 4 lanes
+// (lane quarter q, values e = 4q + k) as two packed registers R0 = (v0, v2),
+// R1 = (v1, v3): stride-1 compare-exchanges are one packed min/max pair, the
+// stride-2 ones exchange register halves.  Returns the value of element k.
+__device__ __forceinline__ int net16_packed(uint32_t R0, uint32_t R1, int q, int k) {
+  uint32_t a, b, o0, o1;
+  // size 2 (flip k^1 = stride 1)
+  a = pmin(R0, R1); b = pmax(R0, R1); R0 = a; R1 = b;
+  // size 4: flip k^3 -> pairs (0,3), (1,2)
+  {
+    const uint32_t s1 = hswap(R1);
+    const uint32_t mn = pmin(R0, s1), mx = pmax(R0, s1);
+    R0 = lohi(mn, mx);
+    R1 = __builtin_amdgcn_alignbit(mx, mn, 16);  // (mn.hi, mx.lo)
+  }
+  a = pmin(R0, R1); b = pmax(R0, R1); R0 = a; R1 = b;  // stride 1
+  // size 8: flip across lanes q^1 (partner element e^7: its v[3-k])
+  {
+    const bool lower = (q & 1) == 0;
+    o0 = hswap((uint32_t)dpp_flip<1>((int)R1));  // (p.v3, p.v1)
+    o1 = hswap((uint32_t)dpp_flip<1>((int)R0));  // (p.v2, p.v0)
+    R0 = cx_lane(lower, R0, o0);
+    R1 = cx_lane(lower, R1, o1);
+  }
+  R0 = cx_half(R0); R1 = cx_half(R1);                   // stride 2
+  a = pmin(R0, R1); b = pmax(R0, R1); R0 = a; R1 = b;  // stride 1
+  // size 16: flip across lanes q^3
+  {
+    const bool lower = (q & 2) == 0;
+    o0 = hswap((uint32_t)dpp_flip<3>((int)R1));
+    o1 = hswap((uint32_t)dpp_flip<3>((int)R0));
+    R0 = cx_lane(lower, R0, o0);
+    R1 = cx_lane(lower, R1, o1);
+  }
+  // stride 4: across lanes q^1, same slot
+  {
+    const bool lower = (q & 1) == 0;
+    o0 = (uint32_t)dpp_flip<1>((int)R0);
+    o1 = (uint32_t)dpp_flip<1>((int)R1);
+    R0 = cx_lane(lower, R0, o0);
+    R1 = cx_lane(lower, R1, o1);
+  }
+  R0 = cx_half(R0); R1 = cx_half(R1);                   // stride 2
+  a = pmin(R0, R1); b = pmax(R0, R1); R0 = a; R1 = b;  // stride 1
+  const uint32_t r = (k & 1) ? R1 : R0;
+  return (int)((k & 2) ? (r >> 16) : (r & 0xFFFFu));
+}
+
 template <int NPC, int LPC, int B>
 __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* FSS,
                                                       const int32_t* olen, const int32_t* len,
@@ -297,12 +373,12 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* 
   constexpr int VPL = NPC / LPC;
   constexpr int RB = 64;       // C rows buffered per restage
   constexpr int Q8 = NPC / 8;  // int4 loads per fss row
+  constexpr int BR = B + 1;    // block rows per chain: B staged + the 0xFFFF row
   static_assert(NPC * LPC == 64, "one wave walks");
   uint64_t wst[4] = {0, 0, 0, 0}, wt = 0;  // HGE_STAMPS: restage cycles, walk cycles, restages, steps
-  __shared__ __attribute__((aligned(16))) uint16_t blk[NPC * B * NPC];  // [d][k][c]
-  __shared__ __attribute__((aligned(16))) uint16_t sInf[NPC];           // gathers of absent members
-  __shared__ __attribute__((aligned(16))) int sP[NPC];
-  __shared__ int sBase[NPC], sLen[NPC], sC[RB * NPC];
+  __shared__ __attribute__((aligned(16))) uint16_t blk[NPC * BR * NPC];  // [d][row][c]
+  __shared__ __attribute__((aligned(16))) int sA[NPC];  // member block rows (B = absent)
+  __shared__ int sP[NPC], sBase[NPC], sLen[NPC], sC[RB * NPC];
   __shared__ int s_r, s_done, s_nr;
   const int N = t.N, SM = t.SM;
   const int tid = threadIdx.x, T = blockDim.x;
@@ -319,8 +395,8 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* 
     }
     sP[c] = P;
     sLen[c] = ln;
-    sInf[c] = 0xFFFF;
   }
+  for (int i = tid; i < NPC * NPC; i += T) blk[((i / NPC) * BR + B) * NPC + (i % NPC)] = 0xFFFF;
   if (tid == 0) {
     s_r = rlo;
     s_done = 0;
@@ -352,7 +428,7 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* 
       const int d = item / (B * Q8);
       const int rem = item - d * (B * Q8);
       const int k = rem / Q8, q8 = rem - k * Q8;
-      *(int4*)&blk[(d * B + k) * NPC + 8 * q8] = vals[m];
+      *(int4*)&blk[(d * BR + k) * NPC + 8 * q8] = vals[m];
     }
     // the next RB rounds' C rows as stored before this kernel (rows < Rprev)
     for (int item = tid; item < RB * NPC; item += T) {
@@ -360,7 +436,10 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* 
       const int rr = r0 + 1 + q;
       sC[item] = (c < N && rr < Rprev && rr < t.Rcap) ? t.C[(size_t)rr * N + c] : INF32;
     }
-    if (tid < NPC) sBase[tid] = sP[tid];
+    if (tid < NPC) {
+      sBase[tid] = sP[tid];
+      sA[tid] = sP[tid] == INF32 ? B : 0;
+    }
     __syncthreads();
     if (dbg && tid == 0) {
       const uint64_t now = stamp();
@@ -377,64 +456,49 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* 
       const int base_c = sBase[c];
       const int qo = (SM - 1) / VPL, ko = (SM - 1) - qo * VPL;
       const bool owner = act && q == qo;
-      int bd[VPL];  // per-slot block bases; absent members gather from sInf
+      // byte offset of (member d = q*VPL + k, row 0, column c)
+      int gb[VPL];
 #pragma unroll
-      for (int k = 0; k < VPL; k++) bd[k] = sBase[q * VPL + k];
+      for (int k = 0; k < VPL; k++) gb[k] = 2 * (((q * VPL + k) * BR) * NPC + c);
       int myP = sP[c];  // the owner's frontier position, kept in a register
       int r = r0;
       bool done = false;
+      const int rcap1 = t.Rcap - 1;
+      const int rend = min(r0 + RB, rcap1);  // C buffer full / rounds table full
       for (;;) {
-        if (r + 1 >= t.Rcap) {
-          if (lane == 0) rstate[1] = 1;
-          done = true;
+        if (r >= rend) {
+          if (r >= rcap1) {
+            if (lane == 0) rstate[1] = 1;
+            done = true;
+          }
           break;
         }
-        if (r - r0 >= RB) break;  // C buffer full
-        int Pv[VPL], v[VPL];
+        int Av[VPL], v[VPL];
 #pragma unroll
-        for (int k = 0; k < VPL; k++) Pv[k] = sP[q * VPL + k];
+        for (int k = 0; k < VPL; k++) Av[k] = sA[q * VPL + k];
         // the already-known C value of round r+1, read together with the members
         const int cur = sC[(r - r0) * NPC + c];
 #pragma unroll
-        for (int k = 0; k < VPL; k++) {
-          const int d = q * VPL + k;
-          const uint16_t* src = (Pv[k] != INF32) ? &blk[(d * B + (Pv[k] - bd[k])) * NPC + c]
-                                                 : &sInf[c];
-          v[k] = *src;
-        }
+        for (int k = 0; k < VPL; k++)
+          v[k] = *(const uint16_t*)((const char*)blk + gb[k] + Av[k] * (2 * NPC));
         // keep every gather in flight before the first comparator waits on one
         __builtin_amdgcn_sched_barrier(0);
-        // all-ascending bitonic network over the NPC values of chain c (LPC lanes
-        // x VPL values): each merge starts with a flip (partner e ^ (size - 1))
-        // followed by half-cleaners (partner e ^ stride), so every in-lane
-        // comparator is static and a cross-lane one needs only the lane's
-        // position in its pair
+        int sel;
+        if constexpr (NPC == 16 && VPL == 4) {
+          sel = net16_packed((uint32_t)v[0] | ((uint32_t)v[2] << 16),
+                             (uint32_t)v[1] | ((uint32_t)v[3] << 16), q, ko);
+        } else {
+          // all-ascending bitonic network over the NPC values of chain c (LPC lanes
+          // x VPL values): each merge starts with a flip (partner e ^ (size - 1))
+          // followed by half-cleaners (partner e ^ stride), so every in-lane
+          // comparator is static and a cross-lane one needs only the lane's
+          // position in its pair
 #pragma unroll
-        for (int size = 2; size <= NPC; size <<= 1) {
-          if (size <= VPL) {
-#pragma unroll
-            for (int k = 0; k < VPL; k++) {
-              const int k2 = k ^ (size - 1);
-              if (k2 > k) {
-                const int a = v[k], b = v[k2];
-                v[k] = min(a, b);
-                v[k2] = max(a, b);
-              }
-            }
-          } else {
-            const bool lower = (q & ((size >> 1) / VPL)) == 0;
-            int o[VPL];
-#pragma unroll
-            for (int k = 0; k < VPL; k++) o[k] = dpp_flip(size / VPL - 1, v[VPL - 1 - k]);
-#pragma unroll
-            for (int k = 0; k < VPL; k++) v[k] = lower ? min(v[k], o[k]) : max(v[k], o[k]);
-          }
-#pragma unroll
-          for (int stride = size >> 2; stride > 0; stride >>= 1) {
-            if (stride < VPL) {
+          for (int size = 2; size <= NPC; size <<= 1) {
+            if (size <= VPL) {
 #pragma unroll
               for (int k = 0; k < VPL; k++) {
-                const int k2 = k ^ stride;
+                const int k2 = k ^ (size - 1);
                 if (k2 > k) {
                   const int a = v[k], b = v[k2];
                   v[k] = min(a, b);
@@ -442,35 +506,62 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* 
                 }
               }
             } else {
-              const bool lower = (q & (stride / VPL)) == 0;
+              const bool lower = (q & ((size >> 1) / VPL)) == 0;
+              int o[VPL];
 #pragma unroll
-              for (int k = 0; k < VPL; k++) {
-                const int o = dpp_flip(stride / VPL, v[k]);
-                v[k] = lower ? min(v[k], o) : max(v[k], o);
+              for (int k = 0; k < VPL; k++) o[k] = dpp_flip(size / VPL - 1, v[VPL - 1 - k]);
+#pragma unroll
+              for (int k = 0; k < VPL; k++) v[k] = lower ? min(v[k], o[k]) : max(v[k], o[k]);
+            }
+#pragma unroll
+            for (int stride = size >> 2; stride > 0; stride >>= 1) {
+              if (stride < VPL) {
+#pragma unroll
+                for (int k = 0; k < VPL; k++) {
+                  const int k2 = k ^ stride;
+                  if (k2 > k) {
+                    const int a = v[k], b = v[k2];
+                    v[k] = min(a, b);
+                    v[k2] = max(a, b);
+                  }
+                }
+              } else {
+                const bool lower = (q & (stride / VPL)) == 0;
+#pragma unroll
+                for (int k = 0; k < VPL; k++) {
+                  const int o = dpp_flip(stride / VPL, v[k]);
+                  v[k] = lower ? min(v[k], o) : max(v[k], o);
+                }
               }
             }
           }
-        }
-        int sel = v[0];
+          sel = v[0];
 #pragma unroll
-        for (int k = 1; k < VPL; k++) sel = (k == ko) ? v[k] : sel;
+          for (int k = 1; k < VPL; k++) sel = (k == ko) ? v[k] : sel;
+        }
         // branch-free owner update: no LDS read between the network and the store
-        const int cand = (sel != 0xFFFF && sel < ln) ? sel : INF32;
+        // (ln < 0xFFFF, so sel < ln also rules out the 0xFFFF "none")
+        const int cand = sel < ln ? sel : INF32;
         const int nxt = myP == INF32 ? INF32 : (cur != INF32 ? cur : cand);
         myP = nxt;
+        const int rowA = nxt == INF32 ? B : nxt - base_c;  // B: the 0xFFFF row
         if (owner) {
           sP[c] = nxt;
+          sA[c] = min(rowA, B);
           sC[(r - r0) * NPC + c] = nxt;
         }
-        const bool leave = owner && nxt != INF32 && nxt - base_c >= B;  // next step leaves the block
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (!__ballot(owner && nxt != INF32)) {
-          done = true;
+        // stop when no chain has a frontier event left, or when one leaves its block
+        const bool alive_l = owner && nxt != INF32;
+        const uint64_t alive = __builtin_amdgcn_ballot_w64(alive_l);
+        const uint64_t lv = __builtin_amdgcn_ballot_w64(alive_l && rowA >= B);
+        if (alive == 0 || lv != 0) {
+          if (alive == 0) done = true;
+          else r++;
           break;
         }
         r++;
-        if (__ballot(leave)) break;
       }
       if (lane == 0) {
         s_nr = r - r0 + (done ? 1 : 0);  // C rows r0+1 .. r0+s_nr were produced

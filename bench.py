@@ -262,7 +262,11 @@ def main():
                          "traffic": pmc_traffic(f"{args.workload}_n{n}_e{E}_k{K}", dom),
                          "algorithmic_bytes_per_launch": int(alg),
                          "launch_ms": round(per_launch_ms, 4),
-                         "hbm_kernels": hbm_kernels},
+                         "hbm_kernels": hbm_kernels,
+                         # the whole path against HBM, B(N) = 24N + 48 bytes/event
+                         "path": {"bytes_per_event": 24 * n + 48,
+                                  "achieved_gbs": round(value / world * (24 * n + 48) / 1e9, 2),
+                                  "frac": round(value / world * (24 * n + 48) / 1e9 / HBM_PEAK_GBS, 5)}},
             "cpu_baseline": cpu,
             "parity": parity,
             "ingest_host_ms": round(ingest_s * 1e3, 2),
