@@ -141,7 +141,7 @@ struct hge_engine {
   DBuf<int32_t> s_segcnt, s_segoff, s_segcall, s_seground, s_theta;
   DBuf<uint8_t> s_segdec;
   DBuf<uint64_t> s_segfws;
-  DBuf<int32_t> s_recv, s_rr, s_frecv, s_fund, s_rank, s_upos, s_und2;
+  DBuf<int32_t> s_recv, s_rr, s_fund, s_upos, s_und2, s_bpos;
   DBuf<int64_t> s_cts;
   DBuf<unsigned char> s_keys, s_keys2;
   DBuf<int32_t> s_part, s_arr, s_fst;
@@ -291,7 +291,7 @@ struct hge_engine {
                              &d_rr,      &d_und,    &d_chain, &d_LA,     &d_FD,      &d_C,
                              &d_W,       &d_rcnt,   &d_minw,  &s_small,  &s_newwit,  &s_LCR,
                              &s_clast,   &s_segcnt, &s_segoff, &s_segcall, &s_seground, &s_theta,
-                             &s_recv,    &s_rr,     &s_frecv, &s_fund,   &s_rank,    &s_upos,
+                             &s_recv,    &s_rr,     &s_bpos,  &s_fund,   &s_upos,
                              &s_und2,    &s_part,   &s_arr,   &s_fst,    &d_FSS,     &d_LAT,
                              &d_FDT,     &s_chg,    &s_bar,   &s_bseg,   &s_kctl,    &s_cctl,
                              &s_out};
@@ -983,31 +983,28 @@ struct hge_engine {
         s_recv.need(ncand);
         HIPCHK(hipMemsetAsync(s_recv.p, 0xFF, 4 * ncand, st));
       }
-      // compaction + sort (the received count stays on the device: o_cnt[0])
-      s_frecv.need(ncand);
+      // compaction + the order as call buckets (the received count stays on the
+      // device: o_cnt[0])
       s_fund.need(ncand);
-      s_rank.need(ncand);
       s_upos.need(ncand);
+      s_rr.need(ncand);
+      s_cts.need(ncand);
       KLAUNCH(k_recv_flags, dim3(div_up(ncand, 256)), dim3(256), 0, st, s_recv.p, ncand,
-                         s_frecv.p, s_fund.p, commit ? 1 : 0);
-      scan_large(s_frecv.p, s_rank.p, ncand, o_cnt);
+              (int32_t*)nullptr, s_fund.p, commit ? 1 : 0, commit ? o_cc : (int32_t*)nullptr);
       KLAUNCH(k_set_rr, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand, s_recv.p,
               s_rr.p, s_cts.p, d_rr.p, d_cts.p, o_ntx, commit ? 1 : 0);
       if (commit) {
-        const int32_t* pn = o_cnt;
+        s_bpos.need(ncalls);
+        KLAUNCH(k_scan_small, dim3(1), dim3(1024), 0, st, (const int32_t*)o_cc, s_bpos.p, ncalls,
+                o_cnt);
         s_keys.need((size_t)ncand * sizeof(OKey));
         s_keys2.need((size_t)ncand * sizeof(OKey));
         OKey* k1 = (OKey*)s_keys.p;
         OKey* k2 = (OKey*)s_keys2.p;
-        KLAUNCH(k_make_keys, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand,
-                           s_recv.p, s_rr.p, s_cts.p, s_rank.p, k1);
-        KLAUNCH(k_sort_tiles, dim3(div_up(ncand, 1024)), dim3(512), 0, st, k1, pn);
-        // passes for the candidate count: a pass whose run covers every key copies
-        for (int run = 1024; run < ncand; run *= 2) {
-          KLAUNCH(k_merge_pass, dim3(div_up(ncand, 256)), dim3(256), 0, st, k1, k2, pn, run);
-          std::swap(k1, k2);
-        }
-        KLAUNCH(k_emit_order, dim3(div_up(ncand, 256)), dim3(256), 0, st, k1, pn, o_ids, o_cc, 0);
+        KLAUNCH(k_bucket_keys, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand, s_recv.p,
+                s_rr.p, s_cts.p, s_bpos.p, k1);
+        KLAUNCH(k_bucket_sort, dim3(ncalls), dim3(256), 0, st, (const int32_t*)s_bpos.p,
+                (const int32_t*)o_cc, k1, k2, o_ids);
         // new undetermined list (in candidate order)
         scan_large(s_fund.p, s_upos.p, ncand, o_cnt + 1);
         s_und2.need(ncand);

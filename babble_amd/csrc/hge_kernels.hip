@@ -1404,9 +1404,40 @@ __device__ __forceinline__ bool okless(const OKey& x, const OKey& y) {
   return x.id < y.id;
 }
 
-__global__ void k_make_keys(Tables t, const int32_t* cand, int ncand, const int32_t* recv_call,
-                            const int32_t* rr, const int64_t* cts, const int32_t* rank,
-                            OKey* keys) {
+// flags for compaction: received (and committing) vs still undetermined; with
+// call_counts, the events each call receives (the order's call buckets)
+__global__ void k_recv_flags(const int32_t* recv_call, int ncand, int32_t* f_recv,
+                             int32_t* f_und, int commit, int32_t* call_counts) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  const int rc = q < ncand ? recv_call[q] : -1;
+  const bool r = rc >= 0;
+  if (q < ncand) {
+    if (f_recv) f_recv[q] = r;
+    f_und[q] = commit ? !r : 1;
+  }
+  if (!call_counts) return;
+  // neighbouring candidates are mostly received by the same call: one atomic
+  // per distinct call in the wave
+  const int lane = threadIdx.x & 63;
+  uint64_t pending = __ballot(r);
+  while (pending) {
+    const int leader = __builtin_ctzll(pending);
+    const int c = __shfl(rc, leader);
+    const uint64_t same = __ballot(r && rc == c);
+    if (lane == leader) atomicAdd(&call_counts[c], __popcll(same));
+    pending &= ~same;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// FindOrder's sort as call buckets: a counting sort by call (k_recv_flags
+// counts, one scan gives the bucket ends), the keys scattered into their
+// bucket in any order, then one workgroup per call sorts its bucket by
+// (rr, cts, S, id): an LDS bitonic index sort up to 512 keys, larger buckets
+// as 512-key chunks merged pairwise (merge path) through global scratch.
+// ---------------------------------------------------------------------------
+__global__ void k_bucket_keys(Tables t, const int32_t* cand, int ncand, const int32_t* recv_call,
+                              const int32_t* rr, const int64_t* cts, int32_t* bpos, OKey* keys) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= ncand || recv_call[q] < 0) return;
   const int x = cand[q];
@@ -1419,93 +1450,142 @@ __global__ void k_make_keys(Tables t, const int32_t* cand, int ncand, const int3
   k.s3 = t.S[4 * (size_t)x + 3];
   k.id = (uint32_t)x;
   k.pad = 0;
-  keys[rank[q]] = k;
+  keys[atomicAdd(&bpos[recv_call[q]], 1)] = k;
 }
 
-// bitonic sort of 1024-key tiles in LDS (tail padded with +inf keys)
-__global__ void __launch_bounds__(512) k_sort_tiles(OKey* keys, const int32_t* np) {
-  __shared__ OKey sk[1024];
-  const int n = *np;  // key count on the device; the grid covers an upper bound
-  const int base = blockIdx.x * 1024;
-  if (base >= n) return;
-  const int tid = threadIdx.x;
-  for (int i = tid; i < 1024; i += 512) {
-    if (base + i < n) sk[i] = keys[base + i];
-    else {
-      OKey inf;
-      inf.a = inf.b = inf.s0 = inf.s1 = inf.s2 = inf.s3 = ~0ull;
-      inf.id = 0xFFFFFFFFu;
-      inf.pad = 0;
-      sk[i] = inf;
-    }
+__device__ __forceinline__ OKey okey_inf() {
+  OKey inf;
+  inf.a = inf.b = inf.s0 = inf.s1 = inf.s2 = inf.s3 = ~0ull;
+  inf.id = 0xFFFFFFFFu;
+  inf.pad = 0;
+  return inf;
+}
+
+// first index i in [0, la] of A such that A[i..] and B[k-i..] split the merged
+// prefix of length k (keys are unique)
+__device__ int merge_corank(const OKey* A, int la, const OKey* B, int lb, int k) {
+  int lo = max(0, k - lb), hi = min(k, la);
+  while (lo < hi) {
+    const int i = (lo + hi) >> 1;  // take i from A, k - i from B
+    if (okless(A[i], B[k - i - 1])) lo = i + 1;
+    else hi = i;
   }
-  __syncthreads();
-  for (int size = 2; size <= 1024; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      const int i = tid;
-      const int lo = 2 * stride * (i / stride) + (i % stride);
-      const int hi = lo + stride;
-      const bool up = ((lo & size) == 0);
-      OKey a = sk[lo], b = sk[hi];
-      if (okless(b, a) == up) {
-        sk[lo] = b;
-        sk[hi] = a;
+  return lo;
+}
+
+// LDS chunk of keys as structure-of-arrays (conflict-free per field) sorted
+// through a uint16 index permutation: a compare-exchange reads two indices and
+// the fields up to the first difference, and swaps only the indices.
+template <int CH>
+struct SortChunk {
+  uint64_t a[CH], b[CH], s0[CH], s1[CH], s2[CH], s3[CH];
+  uint32_t id[CH];
+  uint16_t ix[CH];
+  __device__ void put(int i, const OKey& k) {
+    a[i] = k.a;
+    b[i] = k.b;
+    s0[i] = k.s0;
+    s1[i] = k.s1;
+    s2[i] = k.s2;
+    s3[i] = k.s3;
+    id[i] = k.id;
+    ix[i] = (uint16_t)i;
+  }
+  __device__ OKey get(int i) const {
+    OKey k;
+    k.a = a[i];
+    k.b = b[i];
+    k.s0 = s0[i];
+    k.s1 = s1[i];
+    k.s2 = s2[i];
+    k.s3 = s3[i];
+    k.id = id[i];
+    k.pad = 0;
+    return k;
+  }
+  __device__ bool less(int x, int y) const {
+    if (a[x] != a[y]) return a[x] < a[y];
+    if (b[x] != b[y]) return b[x] < b[y];
+    if (s0[x] != s0[y]) return s0[x] < s0[y];
+    if (s1[x] != s1[y]) return s1[x] < s1[y];
+    if (s2[x] != s2[y]) return s2[x] < s2[y];
+    if (s3[x] != s3[y]) return s3[x] < s3[y];
+    return id[x] < id[y];
+  }
+  // bitonic sort of ix[0, P) (P a power of two <= CH) by the whole block
+  __device__ void sort(int P) {
+    const int tid = threadIdx.x, T = blockDim.x;
+    for (int size = 2; size <= P; size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int i = tid; i < P / 2; i += T) {
+          const int lo = 2 * stride * (i / stride) + (i % stride);
+          const int hi = lo + stride;
+          const bool up = ((lo & size) == 0);
+          const int x = ix[lo], y = ix[hi];
+          if (less(y, x) == up) {
+            ix[lo] = (uint16_t)y;
+            ix[hi] = (uint16_t)x;
+          }
+        }
+        __syncthreads();
       }
-      __syncthreads();
     }
   }
-  for (int i = tid; i < 1024; i += 512)
-    if (base + i < n) keys[base + i] = sk[i];
-}
+};
 
-// one merge pass of sorted runs of length `run`: rank-based (keys are unique)
-__global__ void k_merge_pass(const OKey* in, OKey* out, const int32_t* np, int run) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int n = *np;
-  if (i >= n) return;
-  const int pair = i / (2 * run);
-  const int a0 = pair * 2 * run;
-  const int b0 = min(n, a0 + run);
-  const int b1 = min(n, a0 + 2 * run);
-  const OKey k = in[i];
-  int pos;
-  if (i < b0) {
-    // count of right-run keys less than k
-    int lo = b0, hi = b1;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (okless(in[mid], k)) lo = mid + 1;
-      else hi = mid;
-    }
-    pos = a0 + (i - a0) + (lo - b0);
-  } else {
-    int lo = a0, hi = b0;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (okless(in[mid], k)) lo = mid + 1;
-      else hi = mid;
-    }
-    pos = a0 + (i - b0) + (lo - a0);
+__global__ void __launch_bounds__(256) k_bucket_sort(const int32_t* bend, const int32_t* bcnt,
+                                                     OKey* keys, OKey* tmp, int32_t* ids_out) {
+  constexpr int CH = 512;  // keys per LDS chunk
+  __shared__ SortChunk<CH> sc;
+  const int b = blockIdx.x;
+  const int n = bcnt[b];
+  if (n == 0) return;
+  const int start = bend[b] - n;
+  const int tid = threadIdx.x, T = blockDim.x;
+  if (n == 1) {
+    if (tid == 0) ids_out[start] = (int32_t)keys[start].id;
+    return;
   }
-  out[pos] = k;
-}
-
-__global__ void k_emit_order(const OKey* keys, const int32_t* np, int32_t* ids,
-                             int32_t* call_counts, int32_t call_lo) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= *np) return;
-  ids[i] = (int32_t)keys[i].id;
-  atomicAdd(&call_counts[(int)(keys[i].a >> 32) - call_lo], 1);
-}
-
-// flags for compaction: received (and committing) vs still undetermined
-__global__ void k_recv_flags(const int32_t* recv_call, int ncand, int32_t* f_recv,
-                             int32_t* f_und, int commit) {
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= ncand) return;
-  const int r = recv_call[q] >= 0;
-  f_recv[q] = r;
-  f_und[q] = commit ? !r : 1;
+  if (n <= CH) {
+    int P = 2;
+    while (P < n) P <<= 1;
+    for (int i = tid; i < P; i += T) sc.put(i, i < n ? keys[start + i] : okey_inf());
+    __syncthreads();
+    sc.sort(P);
+    for (int i = tid; i < n; i += T) ids_out[start + i] = (int32_t)sc.id[sc.ix[i]];
+    return;
+  }
+  // large bucket: sorted CH-key chunks, then pairwise merges (ping-pong)
+  OKey* src = keys + start;
+  OKey* dst = tmp + start;
+  for (int c0 = 0; c0 < n; c0 += CH) {
+    const int m = min(CH, n - c0);
+    for (int i = tid; i < CH; i += T) sc.put(i, i < m ? src[c0 + i] : okey_inf());
+    __syncthreads();
+    sc.sort(CH);
+    for (int i = tid; i < m; i += T) src[c0 + i] = sc.get(sc.ix[i]);
+    __syncthreads();
+  }
+  for (int run = CH; run < n; run <<= 1) {
+    for (int a0 = 0; a0 < n; a0 += 2 * run) {
+      const int la = min(run, n - a0);
+      const int lb = max(0, min(run, n - a0 - run));
+      const OKey* A = src + a0;
+      const OKey* B = A + la;
+      const int len = la + lb;
+      const int k0 = (int)((int64_t)len * tid / T), k1 = (int)((int64_t)len * (tid + 1) / T);
+      int i = merge_corank(A, la, B, lb, k0), j = k0 - i;
+      for (int k = k0; k < k1; k++) {
+        const bool takeA = j >= lb || (i < la && okless(A[i], B[j]));
+        dst[a0 + k] = takeA ? A[i++] : B[j++];
+      }
+    }
+    __syncthreads();
+    OKey* sw = src;
+    src = dst;
+    dst = sw;
+  }
+  for (int i = tid; i < n; i += T) ids_out[start + i] = (int32_t)src[i].id;
 }
 
 __global__ void k_scatter_und(const int32_t* cand, int ncand, const int32_t* f_und,
