@@ -184,29 +184,57 @@ __device__ __forceinline__ int select_kth(int (&v)[NPC], int k) {
 }
 
 // one lane per (event w, target chain c); events of chain cw from position lo[cw].
+// Lane i of an event loads w's first descendant z_i on chain i and then the
+// whole FD row of (i, z_i) with vector loads; an LDS transpose hands lane c the
+// column c of those rows, FD[(i, z_i)][c] over i.
 // FSS16 (non-null: the LDS walk) receives uint16 rows padded to NPC columns
 // (INF and the padding = 0xFFFF) with the own-chain entry already clamped to
 // pw + 1 (an event never strongly sees itself); otherwise int32 rows of N.
 template <int NPC>
-__global__ void k_fss(Tables t, const int32_t* lo, const int32_t* off, int total,
-                      int32_t* FSS, uint16_t* FSS16) {
+__global__ void __launch_bounds__(256) k_fss(Tables t, const int32_t* lo, const int32_t* off,
+                                             int total, int32_t* FSS, uint16_t* FSS16) {
+  constexpr int EPB = 256 / NPC;  // events per block
+  __shared__ int s_off[NPC + 1], s_lo[NPC];
+  __shared__ int tr[EPB][NPC][NPC + 1];
   const int N = t.N;
-  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int ev = (int)(g / NPC), c = (int)(g - (g / NPC) * NPC);
-  if (ev >= total) return;
+  const int tid = threadIdx.x;
+  if (tid <= N) s_off[tid] = off[tid];
+  if (tid < N) s_lo[tid] = lo[tid];
+  __syncthreads();
+  const int e = tid / NPC, c = tid - (tid / NPC) * NPC;
+  const int ev = blockIdx.x * EPB + e;
+  const bool valid = ev < total;
   int cw = 0;
-  while (off[cw + 1] <= ev) cw++;
-  const int pw = lo[cw] + (ev - off[cw]);
-  const int32_t* fdw = t.FD + rowoff(t, cw, pw);
-  int v[NPC];
+  if (valid)
+    while (s_off[cw + 1] <= ev) cw++;
+  const int pw = valid ? s_lo[cw] + (ev - s_off[cw]) : 0;
+  // row of (c, z_c): FD[(c, z_c)][0..N)
+  const int z = (valid && c < N) ? t.FD[rowoff(t, cw, pw) + c] : INF32;
+  int* row = tr[e][c];
+  if (z == INF32) {
 #pragma unroll
-  for (int i = 0; i < NPC; i++) {
-    v[i] = INF32;
-    if (i < N) {
-      const int z = fdw[i];
-      if (z != INF32 && c < N) v[i] = t.FD[rowoff(t, i, z) + c];
+    for (int j = 0; j < NPC; j++) row[j] = INF32;
+  } else {
+    const int32_t* src = t.FD + rowoff(t, c, z);
+    if (N == NPC) {
+#pragma unroll
+      for (int j = 0; j < NPC; j += 4) {
+        const int4 q4 = *(const int4*)(src + j);
+        row[j] = q4.x;
+        row[j + 1] = q4.y;
+        row[j + 2] = q4.z;
+        row[j + 3] = q4.w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NPC; j++) row[j] = j < N ? src[j] : INF32;
     }
   }
+  __syncthreads();
+  if (!valid) return;
+  int v[NPC];
+#pragma unroll
+  for (int i = 0; i < NPC; i++) v[i] = tr[e][i][c];
   int f = (c < N) ? select_kth<NPC>(v, t.SM) : INF32;
   if (FSS16) {
     if (c == cw && f != INF32) f = max(f, pw + 1);
