@@ -141,7 +141,7 @@ struct hge_engine {
   DBuf<int32_t> s_segcnt, s_segoff, s_segcall, s_seground, s_theta;
   DBuf<uint8_t> s_segdec;
   DBuf<uint64_t> s_segfws;
-  DBuf<int32_t> s_recv, s_rr, s_fund, s_upos, s_und2, s_bpos;
+  DBuf<int32_t> s_recv, s_rr, s_fund, s_upos, s_und2, s_bpos, s_vis;
   DBuf<int64_t> s_cts;
   DBuf<unsigned char> s_keys, s_keys2;
   DBuf<int32_t> s_part, s_arr, s_fst;
@@ -291,7 +291,7 @@ struct hge_engine {
                              &d_rr,      &d_und,    &d_chain, &d_LA,     &d_FD,      &d_C,
                              &d_W,       &d_rcnt,   &d_minw,  &s_small,  &s_newwit,  &s_LCR,
                              &s_clast,   &s_segcnt, &s_segoff, &s_segcall, &s_seground, &s_theta,
-                             &s_recv,    &s_rr,     &s_bpos,  &s_fund,   &s_upos,
+                             &s_recv,    &s_rr,     &s_bpos,  &s_fund,   &s_upos,    &s_vis,
                              &s_und2,    &s_part,   &s_arr,   &s_fst,    &d_FSS,     &d_LAT,
                              &d_FDT,     &s_chg,    &s_bar,   &s_bseg,   &s_kctl,    &s_cctl,
                              &s_out};
@@ -954,8 +954,12 @@ struct hge_engine {
         s_segcnt.need(nr);
         s_segoff.need(nr + 1);
         s_arr.need((size_t)nr * N);
-        KLAUNCH(k_arrivals, dim3(div_up(nr * N, 256)), dim3(256), 0, st, t, rr_lo, nr, c_nc,
-                ncalls, s_arr.p);
+        // first call at which each event is visible (arrivals, round received)
+        s_vis.need(std::max<int64_t>(n_coords, 1));
+        KLAUNCH(k_visibility, dim3(div_up(n_coords, 256)), dim3(256), 0, st, (const int64_t*)c_nc,
+                ncalls, (int)n_coords, s_vis.p);
+        KLAUNCH(k_arrivals, dim3(div_up(nr * N, 256)), dim3(256), 0, st, t, rr_lo, nr,
+                (const int32_t*)s_vis.p, ncalls, s_arr.p);
         seg_dispatch(0, t, rr_lo, nr, ncalls, si, 0);
         KLAUNCH(k_scan_small, dim3(1), dim3(1024), 0, st, s_segcnt.p, s_segoff.p, nr,
                 s_small.p + 6);
@@ -1169,7 +1173,8 @@ struct hge_engine {
 #define RCASE(B)                                                                                 \
   case B:                                                                                        \
     KLAUNCH(k_round_received<B>, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, \
-                       ncand, c_nc, ncalls, 0, rr_lo, R_last, s_segoff.p, s_segcnt.p,          \
+                       ncand, (const int32_t*)s_vis.p, ncalls, 0, rr_lo, R_last, s_segoff.p,   \
+                       s_segcnt.p,                                                               \
                        s_segcall.p, s_segdec.p, s_segfws.p, s_theta.p, s_recv.p, s_rr.p,         \
                        s_cts.p, bseg);                                                           \
     if (wmed)                                                                                    \

@@ -999,7 +999,7 @@ struct SegInfo {
 };
 
 // first call of the batch at which witness W[r][d] is visible (INF32: none / later)
-__global__ void k_arrivals(Tables t, int rr_lo, int nr, const int64_t* nc, int ncalls,
+__global__ void k_arrivals(Tables t, int rr_lo, int nr, const int32_t* vis, int ncalls,
                            int32_t* arr) {
   const int item = blockIdx.x * blockDim.x + threadIdx.x;
   const int N = t.N;
@@ -1007,16 +1007,42 @@ __global__ void k_arrivals(Tables t, int rr_lo, int nr, const int64_t* nc, int n
   const int q = item / N, d = item - (item / N) * N;
   const int x = t.W[(size_t)(rr_lo + q) * N + d];
   int a = INF32;
-  if (x >= 0) {
-    int lo = 0, hi = ncalls;
+  if (x >= 0 && vis[x] < ncalls) a = vis[x];
+  arr[item] = a;
+}
+
+// vis[x] = first call whose event count exceeds x (ncalls: none), for the
+// events [0, nev): a block takes 256 consecutive events and binary-searches
+// them in an LDS window of the calls from the first one that sees its first
+// event (the global search is the fallback past the window)
+__global__ void __launch_bounds__(256) k_visibility(const int64_t* nc, int ncalls, int nev,
+                                                    int32_t* vis) {
+  __shared__ int64_t s_nc[256];
+  __shared__ int s_c0;
+  const int tid = threadIdx.x;
+  const int x0 = blockIdx.x * 256;
+  auto upper = [&](int64_t x, int lo, int hi) {
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
       if (nc[mid] > x) hi = mid;
       else lo = mid + 1;
     }
-    a = lo < ncalls ? lo : INF32;
+    return lo;
+  };
+  if (tid == 0) s_c0 = upper(x0, 0, ncalls);
+  __syncthreads();
+  const int c0 = s_c0;
+  s_nc[tid] = c0 + tid < ncalls ? nc[c0 + tid] : INT64_MAX;
+  __syncthreads();
+  const int x = x0 + tid;
+  if (x >= nev) return;
+  int lo = 0, hi = 256;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (s_nc[mid] > x) hi = mid;
+    else lo = mid + 1;
   }
-  arr[item] = a;
+  vis[x] = lo < 256 ? min(c0 + lo, ncalls) : upper(x, c0 + 256, ncalls);
 }
 
 template <int NWT>
@@ -1228,7 +1254,7 @@ __global__ void k_seg_theta(Tables t, const int32_t* seg_round, const int32_t* p
 // at c and whose famous witnesses see x by strict majority.
 // ---------------------------------------------------------------------------
 template <int NWT>
-__global__ void k_round_received(Tables t, const int32_t* cand, int ncand, const int64_t* nc,
+__global__ void k_round_received(Tables t, const int32_t* cand, int ncand, const int32_t* vis,
                                  int ncalls, int call_lo, int rr_lo, int R_last,
                                  const int32_t* segoff, const int32_t* segcnt,
                                  const int32_t* seg_call, const uint8_t* seg_dec,
@@ -1242,13 +1268,7 @@ __global__ void k_round_received(Tables t, const int32_t* cand, int ncand, const
   const int cx = t.creator[x], ix = t.index[x];
   const int rx = t.round[x];
   // first call at which x is visible
-  int a = call_lo, b = ncalls;
-  while (a < b) {
-    const int mid = (a + b) >> 1;
-    if (nc[mid] > x) b = mid;
-    else a = mid + 1;
-  }
-  const int c0 = a;
+  const int c0 = max(call_lo, vis[x]);
   int best = INF32, rr = -1, bseg = -1;
   for (int i = rx + 1; i < R_last; i++) {
     const int qi = i - rr_lo;
@@ -1281,55 +1301,55 @@ __global__ void k_round_received(Tables t, const int32_t* cand, int ncand, const
     bseg_out[q] = bseg;
     return;
   }
-  // median of the oldest-self-ancestor-to-see timestamps (OSA(w,x) = FD[x][cw])
-  int64_t tv[64];
-  int m = 0;
+  // median of the oldest-self-ancestor-to-see timestamps (OSA(w,x) = FD[x][cw]),
+  // N <= 16 (wider hashgraphs take k_median_wave): every gather of a level is
+  // issued before the next level needs it, then an int64 register sort
+  constexpr int M = 16;
+  const uint64_t fw = seg_fws[(size_t)bseg * NWT];
   const int32_t* fdx = t.FD + rowoff(t, cx, ix);
-  int64_t med = 0;
-  int nsee = 0;
-  for (int d = 0; d < N; d++) {
-    if (!((seg_fws[(size_t)bseg * NWT + (d >> 6)] >> (d & 63)) & 1ull)) continue;
-    const int w = t.W[(size_t)rr * N + d];
-    if (t.LA[rowoff(t, d, t.index[w]) + cx] < ix) continue;
-    nsee++;
+  int wid[M], wix[M], fd[M];
+#pragma unroll
+  for (int d = 0; d < M; d++) {
+    const bool fam = d < N && ((fw >> d) & 1ull);
+    wid[d] = fam ? t.W[(size_t)rr * N + d] : -1;
+    fd[d] = d < N ? fdx[d] : 0;
   }
-  if (nsee <= 64) {
-    for (int d = 0; d < N; d++) {
-      if (!((seg_fws[(size_t)bseg * NWT + (d >> 6)] >> (d & 63)) & 1ull)) continue;
-      const int w = t.W[(size_t)rr * N + d];
-      if (t.LA[rowoff(t, d, t.index[w]) + cx] < ix) continue;
-      const int osa = t.chain[(size_t)d * t.ccap + fdx[d]];
-      int64_t v = t.ts[osa];
-      int j = m++;
-      while (j > 0 && tv[j - 1] > v) {
-        tv[j] = tv[j - 1];
-        j--;
-      }
-      tv[j] = v;
-    }
-    med = tv[m / 2];
-  } else {
-    // k-th smallest by counting selection
-    const int kk = nsee / 2;  // 0-based
-    int64_t lo = INT64_MIN, hi = INT64_MAX;
-    // candidate values are the timestamps themselves: pick the smallest v with count(<= v) > kk
-    for (int d = 0; d < N; d++) {
-      if (!((seg_fws[(size_t)bseg * NWT + (d >> 6)] >> (d & 63)) & 1ull)) continue;
-      const int w = t.W[(size_t)rr * N + d];
-      if (t.LA[rowoff(t, d, t.index[w]) + cx] < ix) continue;
-      const int64_t v = t.ts[t.chain[(size_t)d * t.ccap + fdx[d]]];
-      int le = 0;
-      for (int e2 = 0; e2 < N; e2++) {
-        if (!((seg_fws[(size_t)bseg * NWT + (e2 >> 6)] >> (e2 & 63)) & 1ull)) continue;
-        const int w2 = t.W[(size_t)rr * N + e2];
-        if (t.LA[rowoff(t, e2, t.index[w2]) + cx] < ix) continue;
-        le += (t.ts[t.chain[(size_t)e2 * t.ccap + fdx[e2]]] <= v) ? 1 : 0;
-      }
-      if (le > kk && v < hi) hi = v;
-    }
-    (void)lo;
-    med = hi;
+#pragma unroll
+  for (int d = 0; d < M; d++) wix[d] = wid[d] >= 0 ? t.index[wid[d]] : 0;
+  int osa[M];
+#pragma unroll
+  for (int d = 0; d < M; d++) {
+    const bool seen = wid[d] >= 0 && t.LA[rowoff(t, d, wix[d]) + cx] >= ix;
+    osa[d] = seen ? t.chain[(size_t)d * t.ccap + fd[d]] : -1;
   }
+  int64_t tv[M];
+  int m = 0;
+#pragma unroll
+  for (int d = 0; d < M; d++) {
+    tv[d] = osa[d] >= 0 ? t.ts[osa[d]] : INT64_MAX;
+    m += osa[d] >= 0 ? 1 : 0;
+  }
+  // ascending bitonic sort (the unseen INT64_MAX pads go last), upper median
+#pragma unroll
+  for (int size = 2; size <= M; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+#pragma unroll
+      for (int i = 0; i < M; i++) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool up = (i & size) == 0;
+          const int64_t u = tv[i], w = tv[j];
+          const bool sw = up ? (w < u) : (u < w);
+          tv[i] = sw ? w : u;
+          tv[j] = sw ? u : w;
+        }
+      }
+    }
+  }
+  int64_t med = tv[0];
+#pragma unroll
+  for (int i = 1; i < M; i++) med = (i == m / 2) ? tv[i] : med;
   recv_call[q] = best;
   rr_out[q] = rr;
   cts_out[q] = med;
