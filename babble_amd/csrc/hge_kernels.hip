@@ -404,6 +404,7 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* 
   constexpr int BR = B + 1;    // block rows per chain: B staged + the 0xFFFF row
   static_assert(NPC * LPC == 64, "one wave walks");
   uint64_t wst[4] = {0, 0, 0, 0}, wt = 0;  // HGE_STAMPS: restage cycles, walk cycles, restages, steps
+  int pf = 0;                              // prefetch sink (kept live below)
   __shared__ __attribute__((aligned(16))) uint16_t blk[NPC * BR * NPC];  // [d][row][c]
   __shared__ __attribute__((aligned(16))) int sA[NPC];  // member block rows (B = absent)
   __shared__ int sP[NPC], sBase[NPC], sLen[NPC], sC[RB * NPC];
@@ -597,6 +598,17 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* 
         s_done = done;
         if (done && !rstate[1]) rstate[0] = max(rstate[0], r + 1);
       }
+    } else {
+      // the other waves pull the rows after every block ([base + B, base + 2B))
+      // into this XCD's L2 while wave 0 walks: the next block of a chain starts
+      // inside its current one, so the next restage hits L2
+      constexpr int RPL = 128 / (2 * NPC);  // fss rows per 128-byte line
+      constexpr int LPCH = B / RPL;         // lines per chain block
+      for (int item = tid - 64; item < NPC * LPCH; item += T - 64) {
+        const int d = item / LPCH, k = (item - d * LPCH) * RPL;
+        if (d < N && sBase[d] != INF32 && sBase[d] + B + k < sLen[d])
+          pf ^= *(const int*)(FSS + ((size_t)d * t.ccap + sBase[d] + B + k) * NPC);
+      }
     }
     __syncthreads();
     if (dbg && tid == 0) {
@@ -619,6 +631,7 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* 
   }
   if (dbg && tid == 0)
     for (int q = 0; q < 4; q++) dbg[q] += wst[q];
+  if (pf == 0x7fffffff && tid == 1 && rlo < 0) rstate[2] = pf;  // never true: keeps the prefetch
 }
 
 // frontier start: r_lo and the first position per chain that can be a member
