@@ -110,7 +110,8 @@ __global__ void __launch_bounds__(256) k_la_sweep(Tables t, const int2* segs, in
       }
     }
   }
-  if (__ballot(ch) && (threadIdx.x & 63) == __builtin_ctzll(__ballot(ch))) atomicOr(changed, 1);
+  // a plain store: every writer stores 1 (same-address atomics serialise at memory)
+  if (__ballot(ch) && (threadIdx.x & 63) == __builtin_ctzll(__ballot(ch))) *changed = 1;
 }
 
 // Tiled transposes through LDS (64 x 64 tiles, 256 threads).

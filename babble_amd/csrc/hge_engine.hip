@@ -692,10 +692,20 @@ struct hge_engine {
       // table overflowed: the loop grows it and walks again)
       t = tables();
       s_newwit.need(m);
-      KLAUNCH(k_round_assign, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0, (int)n1,
-              (const int32_t*)k_rs, s_newwit.p, k_rs + 2);
-      KLAUNCH(k_witness_bits, dim3(std::min(div_up((int64_t)m * N, 256), 8192)), dim3(256), 0, st,
-              t, s_newwit.p, k_rs + 2, N > 32 ? (const uint64_t*)d_ssc.p : nullptr);
+      if (fresh) {
+        s_newwit.need((size_t)Rcap * N);
+        KLAUNCH(k_round_ranges, dim3(div_up((int64_t)Rcap * N, 256)), dim3(256), 0, st, t, k_len + N,
+                (const int32_t*)k_rs, s_newwit.p, k_rs + 2);
+      } else {
+        KLAUNCH(k_round_assign, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0, (int)n1,
+                (const int32_t*)k_rs, s_newwit.p, k_rs + 2);
+      }
+      {
+        int G = 1;
+        while (G < std::min(N, 64)) G <<= 1;
+        KLAUNCH(k_witness_bits, dim3(std::min(div_up((int64_t)m * NW * G, 256), 8192)), dim3(256), 0,
+                st, t, s_newwit.p, k_rs + 2, N > 32 ? (const uint64_t*)d_ssc.p : nullptr, G);
+      }
       KLAUNCH(k_round_minw, dim3(div_up(Rcap, 256)), dim3(256), 0, st, t, 0,
               (const int32_t*)k_rs, d_minw.p);
       h_minw.resize(Rcap + 2);
@@ -931,7 +941,10 @@ struct hge_engine {
 
     // ---- DecideRoundReceived / FindOrder ----
     bool got_order = false;
-    s_out.need(8 + (size_t)ncalls + (ord ? ncand : 0));
+    // results block: counters | per-call counts | order | per-block transaction sums
+    const size_t o_tx = (8 + (size_t)ncalls + (ord ? ncand : 0) + 1) & ~(size_t)1;
+    const int ntxb = ord ? div_up(ncand, 256) : 0;
+    s_out.need(o_tx + 2 * (size_t)ntxb);
     int32_t* o_cnt = s_out.p;  // [0] received [1] undetermined [2] LCR events [4..5] tx
     int32_t* o_cc = s_out.p + 8;
     int32_t* o_ids = s_out.p + 8 + ncalls;
@@ -995,8 +1008,9 @@ struct hge_engine {
       s_cts.need(ncand);
       KLAUNCH(k_recv_flags, dim3(div_up(ncand, 256)), dim3(256), 0, st, s_recv.p, ncand,
               (int32_t*)nullptr, s_fund.p, commit ? 1 : 0, commit ? o_cc : (int32_t*)nullptr);
-      KLAUNCH(k_set_rr, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand, s_recv.p,
-              s_rr.p, s_cts.p, d_rr.p, d_cts.p, o_ntx, commit ? 1 : 0);
+      if (!commit)
+        KLAUNCH(k_set_rr, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand, s_recv.p,
+                s_rr.p, s_cts.p, d_rr.p, d_cts.p, o_ntx, 0);
       if (commit) {
         s_bpos.need(ncalls);
         KLAUNCH(k_scan_small, dim3(1), dim3(1024), 0, st, (const int32_t*)o_cc, s_bpos.p, ncalls,
@@ -1006,7 +1020,8 @@ struct hge_engine {
         OKey* k1 = (OKey*)s_keys.p;
         OKey* k2 = (OKey*)s_keys2.p;
         KLAUNCH(k_bucket_keys, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand, s_recv.p,
-                s_rr.p, s_cts.p, s_bpos.p, k1);
+                s_rr.p, s_cts.p, s_bpos.p, k1, d_rr.p, d_cts.p,
+                (unsigned long long*)(s_out.p + o_tx));
         KLAUNCH(k_bucket_sort, dim3(ncalls), dim3(256), 0, st, (const int32_t*)s_bpos.p,
                 (const int32_t*)o_cc, k1, k2, o_ids);
         // new undetermined list (in candidate order)
@@ -1036,14 +1051,18 @@ struct hge_engine {
       }
     }
     // the batch's one closing round trip (read in place from the pinned arena)
-    const size_t off = d2h_pinned(s_out.p, 4 * (8 + (size_t)ncalls + (got_order ? ncand : 0)));
+    const size_t off = d2h_pinned(s_out.p, 4 * (got_order ? o_tx + 2 * (size_t)ntxb : 8 + (size_t)ncalls));
     sync();
     const int32_t* ho = (const int32_t*)(pin + off);
     const int32_t nrecv = ho[0];
     if (got_order) {
       const int32_t* ids = ho + 8 + ncalls;
       unsigned long long ntx = 0;
-      memcpy(&ntx, ho + 4, 8);
+      for (int b2 = 0; b2 < ntxb; b2++) {
+        unsigned long long v = 0;
+        memcpy(&v, ho + o_tx + 2 * (size_t)b2, 8);
+        ntx += v;
+      }
       consensus.insert(consensus.end(), ids, ids + nrecv);
       ctx += (int64_t)ntx;
       if (order_out) order_out->insert(order_out->end(), ids, ids + nrecv);

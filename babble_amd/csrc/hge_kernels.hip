@@ -702,6 +702,59 @@ __global__ void k_round_assign(Tables t, int n0, int n1, const int32_t* rstate, 
   }
 }
 
+// The same from a fresh state, by frontier ranges: chain c's positions
+// [C[r][c], C[r+1][c]) are exactly its round-r events (rounds never decrease
+// along a chain) and the first of them is the witness.  One thread per
+// (round, chain) over the Rcap rows (R from the device).
+__global__ void k_round_ranges(Tables t, const int32_t* len, const int32_t* rstate,
+                               int32_t* newwit, int32_t* nnewwit) {
+  if (rstate[1]) return;
+  const int R = rstate[0];
+  const int N = t.N;
+  const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int r = (int)(item / N), c = (int)(item - (item / N) * N);
+  const int lane = threadIdx.x & 63;
+  int lo = INF32, hi = 0;
+  if (r < R) {
+    lo = t.C[(size_t)r * N + c];
+    hi = min(r + 1 < R ? t.C[(size_t)(r + 1) * N + c] : INF32, len[c]);
+  }
+  const bool any = lo != INF32 && lo < hi;
+  int w = -1;
+  if (any) {
+    const int32_t* ch = t.chain + (size_t)c * t.ccap;
+    for (int p = lo; p < hi; p++) {
+      const int x = ch[p];
+      t.round[x] = r;
+      t.wit[x] = p == lo ? 1 : 0;
+    }
+    w = ch[lo];
+    t.W[(size_t)r * N + c] = w;
+  }
+  // per-round counts: one atomic per distinct round in the wave
+  {
+    const int cnt = any ? hi - lo : 0;
+    uint64_t pending = __ballot(cnt > 0);
+    while (pending) {
+      const int leader = __builtin_ctzll(pending);
+      const int rl = __shfl(r, leader);
+      const uint64_t same = __ballot(cnt > 0 && r == rl);
+      int part = (cnt > 0 && r == rl) ? cnt : 0;
+      for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+      if (lane == leader) atomicAdd(&t.rcnt[rl], part);
+      pending &= ~same;
+    }
+  }
+  const uint64_t wm = __ballot(any);
+  if (wm) {
+    const int leader = __builtin_ctzll(wm);
+    int base = 0;
+    if (lane == leader) base = atomicAdd(nnewwit, __popcll(wm));
+    base = __shfl(base, leader);
+    if (any) newwit[base + __popcll(wm & ((1ull << lane) - 1))] = w;
+  }
+}
+
 // first witness id per round (monotone increasing in r); rounds [r0, R)
 __global__ void k_round_minw(Tables t, int r0, const int32_t* rstate, int32_t* minw) {
   const int r = r0 + blockIdx.x * blockDim.x + threadIdx.x;
@@ -721,34 +774,50 @@ __global__ void k_round_minw(Tables t, int r0, const int32_t* rstate, int32_t* m
 
 // strongly-see / see bitsets of each new witness y (round j >= 1) over the
 // slots of round j-1: StronglySee (hashgraph.go:189-208), See (:149-154)
-// ssc (wide path): strongly-see bits already produced by k_rounds_coop
+// ssc (wide path): strongly-see bits already produced by k_rounds_coop.
+// One group of G lanes (G = N rounded up to a power of two, at most 64) per
+// (witness, 64-slot word): the group's ballots ARE the word, stored by its
+// first lane (no global atomics: same-address atomics serialise at memory).
 __global__ void k_witness_bits(Tables t, const int32_t* newwit, const int32_t* pnnew,
-                               const uint64_t* ssc) {
-  // grid-stride over (new witness, slot) pairs; the count lives on the device
+                               const uint64_t* ssc, int G) {
   const int N = t.N, NW = t.NW;
-  const int64_t total = (int64_t)(*pnnew) * N;
+  const int lane = threadIdx.x & 63;
+  const int gl = lane & (G - 1);
+  const uint64_t gm = G == 64 ? ~0ull : ((1ull << G) - 1) << (lane & ~(G - 1));
+  const int gshift = G == 64 ? 0 : (lane & ~(G - 1));
+  // grid-stride over whole groups (the count lives on the device)
+  const int64_t total = (int64_t)(*pnnew) * NW * G;
   for (int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; item < total;
        item += (int64_t)gridDim.x * blockDim.x) {
-    const int y = newwit[item / N];
-    const int d = (int)(item - (item / N) * N);
+    const int64_t grp = item / G;
+    const int y = newwit[grp / NW];
+    const int wd = (int)(grp - (grp / NW) * NW);
+    const int d = wd * 64 + gl;
     const int j = t.round[y];
-    if (j == 0) continue;
-    const int w = t.W[(size_t)(j - 1) * N + d];
-    if (w < 0) continue;
     const int cy = t.creator[y];
-    const int32_t* la = t.LA + rowoff(t, cy, t.index[y]);
-    const int32_t* fd = t.FD + rowoff(t, d, t.index[w]);
-    const bool see = la[d] >= t.index[w];
-    int c = 0;
-    if (ssc) {
-      c = ((ssc[((size_t)j * N + cy) * NW + (d >> 6)] >> (d & 63)) & 1ull) ? t.SM : 0;
-    } else {
-      for (int i = 0; i < N; i++) c += (la[i] >= fd[i]) ? 1 : 0;
+    bool see = false, ss = false;
+    if (j > 0 && d < N) {
+      const int w = t.W[(size_t)(j - 1) * N + d];
+      if (w >= 0) {
+        const int32_t* la = t.LA + rowoff(t, cy, t.index[y]);
+        see = la[d] >= t.index[w];
+        if (ssc) {
+          ss = (ssc[((size_t)j * N + cy) * NW + wd] >> (d & 63)) & 1ull;
+        } else {
+          const int32_t* fd = t.FD + rowoff(t, d, t.index[w]);
+          int c = 0;
+          for (int i = 0; i < N; i++) c += (la[i] >= fd[i]) ? 1 : 0;
+          ss = c >= t.SM;
+        }
+      }
     }
-    const size_t off = ((size_t)j * N + cy) * NW + (d >> 6);
-    const uint64_t bit = 1ull << (d & 63);
-    if (see) atomicOr((unsigned long long*)&t.seeb[off], (unsigned long long)bit);
-    if (c >= t.SM) atomicOr((unsigned long long*)&t.ssb[off], (unsigned long long)bit);
+    const uint64_t bsee = (__ballot(see) & gm) >> gshift;
+    const uint64_t bss = (__ballot(ss) & gm) >> gshift;
+    if (gl == 0 && j > 0) {
+      const size_t off = ((size_t)j * N + cy) * NW + wd;
+      t.seeb[off] = bsee;
+      t.ssb[off] = bss;
+    }
   }
 }
 
@@ -1497,11 +1566,44 @@ __global__ void k_recv_flags(const int32_t* recv_call, int ncand, int32_t* f_rec
 // (rr, cts, S, id): an LDS bitonic index sort up to 512 keys, larger buckets
 // as 512-key chunks merged pairwise (merge path) through global scratch.
 // ---------------------------------------------------------------------------
+// (also records roundReceived / consensusTimestamp and sums the transactions,
+// as k_set_rr does outside a committing batch)
 __global__ void k_bucket_keys(Tables t, const int32_t* cand, int ncand, const int32_t* recv_call,
-                              const int32_t* rr, const int64_t* cts, int32_t* bpos, OKey* keys) {
+                              const int32_t* rr, const int64_t* cts, int32_t* bpos, OKey* keys,
+                              int32_t* ev_rr, int64_t* ev_cts, unsigned long long* ntx_sum) {
+  // ntx_sum: one partial per block (launched with 256 threads)
+  __shared__ unsigned long long s_tx[4];
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= ncand || recv_call[q] < 0) return;
-  const int x = cand[q];
+  const int lane = threadIdx.x & 63;
+  const int rc = q < ncand ? recv_call[q] : -1;
+  const bool rec = rc >= 0;
+  const int x = rec ? cand[q] : 0;
+  // transactions: a per-block partial (summed by the host), no global atomics
+  unsigned long long tx = rec ? (unsigned long long)t.ntx[x] : 0;
+  for (int o = 32; o > 0; o >>= 1) tx += __shfl_xor(tx, o);
+  if (lane == 0) s_tx[threadIdx.x >> 6] = tx;
+  // bucket slots: one atomic per distinct call in the wave
+  int slot = 0;
+  uint64_t pending = __ballot(rec);
+  while (pending) {
+    const int leader = __builtin_ctzll(pending);
+    const int c = __shfl(rc, leader);
+    const uint64_t same = __ballot(rec && rc == c);
+    int base = 0;
+    if (lane == leader) base = atomicAdd(&bpos[c], __popcll(same));
+    base = __shfl(base, leader);
+    if (rec && rc == c) slot = base + __popcll(same & ((1ull << lane) - 1));
+    pending &= ~same;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long bt = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); w++) bt += s_tx[w];
+    ntx_sum[blockIdx.x] = bt;
+  }
+  if (!rec) return;
+  ev_rr[x] = rr[q];
+  ev_cts[x] = cts[q];
   OKey k;
   k.a = ((uint64_t)(uint32_t)recv_call[q] << 32) | (uint32_t)rr[q];
   k.b = (uint64_t)cts[q] ^ 0x8000000000000000ull;
@@ -1511,7 +1613,7 @@ __global__ void k_bucket_keys(Tables t, const int32_t* cand, int ncand, const in
   k.s3 = t.S[4 * (size_t)x + 3];
   k.id = (uint32_t)x;
   k.pad = 0;
-  keys[atomicAdd(&bpos[recv_call[q]], 1)] = k;
+  keys[slot] = k;
 }
 
 __device__ __forceinline__ OKey okey_inf() {
@@ -1660,11 +1762,18 @@ __global__ void k_set_rr(Tables t, const int32_t* cand, int ncand, const int32_t
                          const int32_t* rr, const int64_t* cts, int32_t* ev_rr, int64_t* ev_cts,
                          unsigned long long* ntx_sum, int commit) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= ncand || recv_call[q] < 0) return;
-  const int x = cand[q];
-  ev_rr[x] = rr[q];
-  ev_cts[x] = cts[q];
-  if (commit) atomicAdd(ntx_sum, (unsigned long long)t.ntx[x]);
+  const bool rec = q < ncand && recv_call[q] >= 0;
+  unsigned long long tx = 0;
+  if (rec) {
+    const int x = cand[q];
+    ev_rr[x] = rr[q];
+    ev_cts[x] = cts[q];
+    tx = (unsigned long long)t.ntx[x];
+  }
+  if (!commit) return;
+  // one atomic per wave
+  for (int o = 32; o > 0; o >>= 1) tx += __shfl_xor(tx, o);
+  if ((threadIdx.x & 63) == 0 && tx) atomicAdd(ntx_sum, tx);
 }
 
 // LastCommitedRoundEvents = RoundEvents(LCR-1) at the call that set LCR
