@@ -869,7 +869,8 @@ struct hge_engine {
     int lcr_new = lcr, c_set = -1;
     const int i_lo = lcr + 1;
     const int i_hi = Rc[ncalls - 1] - 2;  // processed rounds: i <= R_c - 2
-    for (int SPEC = 6;; SPEC *= 2) {
+    static const int SPEC0 = getenv("HGE_SPEC") ? std::max(1, atoi(getenv("HGE_SPEC"))) : 3;
+    for (int SPEC = SPEC0;; SPEC *= 2) {
       pr_round.clear();
       pr_off.clear();
       pr_cf.clear();

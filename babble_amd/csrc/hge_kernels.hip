@@ -853,41 +853,67 @@ __global__ void k_fame_decide(Tables t, const int32_t* pr_round, const int32_t* 
     uint64_t votes[NWT], cur[NWT];
 #pragma unroll
     for (int w = 0; w < NWT; w++) votes[w] = 0;
+    // the witness rows are read in chunks of DC slots with every load of a chunk
+    // in flight before the first use (the d loops are latency chains otherwise)
+    constexpr int DC = 16;
     // diff == 1: vote = See(y, x)
-    for (int d = 0; d < N; d++) {
-      const int y = t.W[(size_t)(i + 1) * N + d];
-      if (y < 0 || y >= n) continue;
-      const uint64_t sb = t.seeb[((size_t)(i + 1) * N + d) * NWT + (xd >> 6)];
-      if ((sb >> (xd & 63)) & 1ull) votes[d >> 6] |= 1ull << (d & 63);
+    for (int d0 = 0; d0 < N; d0 += DC) {
+      int ys[DC];
+      uint64_t sb[DC];
+#pragma unroll
+      for (int u = 0; u < DC; u++) {
+        const int d = d0 + u;
+        ys[u] = d < N ? t.W[(size_t)(i + 1) * N + d] : -1;
+        sb[u] = d < N ? t.seeb[((size_t)(i + 1) * N + d) * NWT + (xd >> 6)] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < DC; u++) {
+        const int d = d0 + u;
+        if (ys[u] >= 0 && ys[u] < n && ((sb[u] >> (xd & 63)) & 1ull))
+          votes[d >> 6] |= 1ull << (d & 63);
+      }
     }
     for (int j = i + 2; j < R; j++) {
       const int diff = j - i;
+      bool brk = false;  // DecideFame's break leaves the y loop of this j only
       const bool coinr = (diff % N) == 0;
 #pragma unroll
       for (int w = 0; w < NWT; w++) cur[w] = 0;
-      for (int d = 0; d < N; d++) {
-        const int y = t.W[(size_t)j * N + d];
-        if (y < 0 || y >= n) continue;
-        const uint64_t* ss = t.ssb + ((size_t)j * N + d) * NWT;
-        int yays = 0, tot = 0;
+      for (int d0 = 0; d0 < N && !brk; d0 += DC) {
+        int ys[DC];
+        uint64_t ss[DC][NWT];
 #pragma unroll
-        for (int w = 0; w < NWT; w++) {
-          const uint64_t m = ss[w];
-          yays += __popcll(m & votes[w]);
-          tot += __popcll(m);
+        for (int u = 0; u < DC; u++) {
+          const int d = d0 + u;
+          ys[u] = d < N ? t.W[(size_t)j * N + d] : -1;
+#pragma unroll
+          for (int w = 0; w < NWT; w++) ss[u][w] = d < N ? t.ssb[((size_t)j * N + d) * NWT + w] : 0;
         }
-        const int nays = tot - yays;
-        const bool v = yays >= nays;
-        const int tt = v ? yays : nays;
-        if (!coinr) {
-          if (tt >= SM) {
-            out = v ? 1 : 2;
-            break;
+#pragma unroll
+        for (int u = 0; u < DC; u++) {
+          const int d = d0 + u;
+          const int y = ys[u];
+          if (brk || y < 0 || y >= n) continue;
+          int yays = 0, tot = 0;
+#pragma unroll
+          for (int w = 0; w < NWT; w++) {
+            yays += __popcll(ss[u][w] & votes[w]);
+            tot += __popcll(ss[u][w]);
           }
-          if (v) cur[d >> 6] |= 1ull << (d & 63);
-        } else {
-          const bool vv = (tt >= SM) ? v : (t.coin[y] != 0);
-          if (vv) cur[d >> 6] |= 1ull << (d & 63);
+          const int nays = tot - yays;
+          const bool v = yays >= nays;
+          const int tt = v ? yays : nays;
+          if (!coinr) {
+            if (tt >= SM) {
+              out = v ? 1 : 2;  // the last decision over j is what SetFame leaves
+              brk = true;        // later y of this j cast no vote
+              continue;
+            }
+            if (v) cur[d >> 6] |= 1ull << (d & 63);
+          } else {
+            const bool vv = (tt >= SM) ? v : (t.coin[y] != 0);
+            if (vv) cur[d >> 6] |= 1ull << (d & 63);
+          }
         }
       }
 #pragma unroll
@@ -1052,10 +1078,30 @@ __global__ void __launch_bounds__(256) k_fame_timeline_g(Tables t, const int32_t
     x = t.W[(size_t)i * N + d];
   }
   const int len = valid ? pr_len[ri] : 0;
+  const int poff = valid ? pr_off[ri] : 0, cf = valid ? pr_cf[ri] : 0;
+  // the window's loads go out QC calls at a time before the sequential scan uses them
+  constexpr int QC = 8;
+  int64_t nq[QC];
+  uint8_t oq[QC];
   for (int q = 0; q < len; q++) {
-    const int p = pr_off[ri] + q, c = pr_cf[ri] + q;
-    const int64_t n = nc[c];
-    if (d < N && dec[(size_t)p * N + d]) known = true;
+    const int u = q & (QC - 1);
+    if (u == 0) {
+#pragma unroll
+      for (int k = 0; k < QC; k++) {
+        const bool in = q + k < len;
+        nq[k] = in ? nc[cf + q + k] : 0;
+        oq[k] = (in && d < N) ? dec[(size_t)(poff + q + k) * N + d] : 0;
+      }
+    }
+    const int p = poff + q, c = cf + q;
+    int64_t n = nq[0];
+    uint8_t o = oq[0];
+#pragma unroll
+    for (int k = 1; k < QC; k++) {
+      n = (u == k) ? nq[k] : n;
+      o = (u == k) ? oq[k] : o;
+    }
+    if (o) known = true;
     const uint64_t und = __ballot(d < N && x >= 0 && x < n && !known) & gm;
     if (d == 0) {
       decbit[p] = und == 0 ? 1 : 0;
