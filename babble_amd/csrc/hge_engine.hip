@@ -167,6 +167,8 @@ struct hge_engine {
   std::vector<int32_t> h_cctl;
   int64_t* c_nc = nullptr;
   int32_t *c_Rc = nullptr, *c_Lc = nullptr, *c_flags = nullptr, *c_pr = nullptr, *c_pidx = nullptr;
+  int32_t* c_sgo = nullptr;
+  const int32_t* segoff_p = nullptr;  // segment offsets used by k_round_received
   // coordinates control block (coords): pointers into s_kctl
   DBuf<int32_t> s_kctl;
   std::vector<int32_t> h_kctl;
@@ -703,7 +705,8 @@ struct hge_engine {
       {
         int G = 1;
         while (G < std::min(N, 64)) G <<= 1;
-        KLAUNCH(k_witness_bits, dim3(std::min(div_up((int64_t)m * NW * G, 256), 8192)), dim3(256), 0,
+        const int64_t wmax = std::min<int64_t>(m, (int64_t)Rcap * N);  // witnesses <= both
+        KLAUNCH(k_witness_bits, dim3(std::min(div_up(wmax * NW * G, 256), 8192)), dim3(256), 0,
                 st, t, s_newwit.p, k_rs + 2, N > 32 ? (const uint64_t*)d_ssc.p : nullptr, G);
       }
       KLAUNCH(k_round_minw, dim3(div_up(Rcap, 256)), dim3(256), 0, st, t, 0,
@@ -866,6 +869,7 @@ struct hge_engine {
     // ---- DecideFame windows (host enumeration of (round, call) pairs) + control block ----
     std::vector<int32_t> pr_round, pr_off, pr_cf, pr_len;
     int npairs = 0, nrounds = 0;
+    int64_t nslot = 0;
     int lcr_new = lcr, c_set = -1;
     const int i_lo = lcr + 1;
     const int i_hi = Rc[ncalls - 1] - 2;  // processed rounds: i <= R_c - 2
@@ -900,8 +904,9 @@ struct hge_engine {
       // the round -> window map of the order pass
       const size_t o_Rc = 2 * (size_t)ncalls, o_Lc = o_Rc + ncalls, o_fl = o_Lc + ncalls;
       const size_t o_pr = o_fl + 4, o_pidx = o_pr + 4 * (size_t)nrounds;
+      const size_t o_sgo = o_pidx + nr;  // N <= 64: per-round segment capacity offsets
       std::vector<int32_t>& cc = h_cctl;
-      cc.assign(o_pidx + nr, 0);
+      cc.assign(o_sgo + nr + 1, 0);
       memcpy(cc.data(), calls.data(), 8 * (size_t)ncalls);
       memcpy(&cc[o_Rc], Rc.data(), 4 * (size_t)ncalls);
       std::fill(cc.begin() + o_Lc, cc.begin() + o_fl, -1);
@@ -916,6 +921,15 @@ struct hge_engine {
         const int i = pr_round[k];
         if (i >= rr_lo && i < rr_lo + nr) cc[o_pidx + (i - rr_lo)] = k;
       }
+      // a round's segments start at call 0, at a witness arrival (<= N distinct
+      // calls), at the window start or at a processed call of its fame window
+      nslot = 0;
+      for (int q = 0; q < nr; q++) {
+        cc[o_sgo + q] = (int32_t)nslot;
+        const int k = cc[o_pidx + q];
+        nslot += N + 2 + (k >= 0 ? pr_len[k] : 0);
+      }
+      cc[o_sgo + nr] = (int32_t)std::min<int64_t>(nslot, INF32);
       s_cctl.need(cc.size());
       h2d(s_cctl.p, cc.data(), 4 * cc.size());
       c_nc = (int64_t*)s_cctl.p;
@@ -924,6 +938,7 @@ struct hge_engine {
       c_flags = s_cctl.p + o_fl;
       c_pr = s_cctl.p + o_pr;
       c_pidx = s_cctl.p + o_pidx;
+      c_sgo = s_cctl.p + o_sgo;
       if (nrounds == 0) break;
       s_dec.need((size_t)npairs * N);
       s_decbit.need(npairs);
@@ -966,32 +981,51 @@ struct hge_engine {
           si.dec = nullptr;
         }
         s_segcnt.need(nr);
-        s_segoff.need(nr + 1);
-        s_arr.need((size_t)nr * N);
-        // first call at which each event is visible (arrivals, round received)
         s_vis.need(std::max<int64_t>(n_coords, 1));
+        // first call at which each event is visible (arrivals, round received)
         KLAUNCH(k_visibility, dim3(div_up(n_coords, 256)), dim3(256), 0, st, (const int64_t*)c_nc,
                 ncalls, (int)n_coords, s_vis.p);
-        KLAUNCH(k_arrivals, dim3(div_up(nr * N, 256)), dim3(256), 0, st, t, rr_lo, nr,
-                (const int32_t*)s_vis.p, ncalls, s_arr.p);
-        seg_dispatch(0, t, rr_lo, nr, ncalls, si, 0);
-        KLAUNCH(k_scan_small, dim3(1), dim3(1024), 0, st, s_segcnt.p, s_segoff.p, nr,
-                s_small.p + 6);
-        // a round's segments start at call 0, at a witness arrival (<= N distinct
-        // calls), at the window start or at a processed call of its fame window
-        int64_t nseg = (int64_t)nr * (N + 2) + npairs;
-        if (!group_lanes()) {
-          int32_t v = 0;
-          readback(&v, s_small.p + 6, 1);
-          nseg = v;
+        const int G = group_lanes();
+        if (G) {
+          // N <= 64: one pass into per-round capacity slots (no count round trip)
+          const size_t ns = (size_t)std::max<int64_t>(nslot, 1);
+          s_segcall.need(ns);
+          s_seground.need(ns);
+          s_segdec.need(ns);
+          s_segfws.need(ns * NW);
+          s_theta.need(ns * N);
+          segoff_p = c_sgo;
+#define SEG1(GG)                                                                                   \
+  KLAUNCH(k_segments_1p<GG>, dim3(div_up((int64_t)nr * GG, 256)), dim3(256), 0, st, t, rr_lo, nr,  \
+          ncalls, (const int32_t*)s_vis.p, si, (const int32_t*)c_sgo, s_segcnt.p, s_segcall.p,     \
+          s_seground.p, s_segdec.p, s_segfws.p, s_theta.p);
+          if (G == 16) {
+            SEG1(16)
+          } else if (G == 32) {
+            SEG1(32)
+          } else {
+            SEG1(64)
+          }
+#undef SEG1
+        } else {
+          s_segoff.need(nr + 1);
+          s_arr.need((size_t)nr * N);
+          segoff_p = s_segoff.p;
+          KLAUNCH(k_arrivals, dim3(div_up(nr * N, 256)), dim3(256), 0, st, t, rr_lo, nr,
+                  (const int32_t*)s_vis.p, ncalls, s_arr.p);
+          seg_dispatch(0, t, rr_lo, nr, ncalls, si, 0);
+          KLAUNCH(k_scan_small, dim3(1), dim3(1024), 0, st, s_segcnt.p, s_segoff.p, nr,
+                  s_small.p + 6);
+          int32_t nseg = 0;
+          readback(&nseg, s_small.p + 6, 1);
+          const size_t ns = (size_t)std::max(nseg, 1);
+          s_segcall.need(ns);
+          s_seground.need(ns);
+          s_segdec.need(ns);
+          s_segfws.need(ns * NW);
+          s_theta.need(ns * N);
+          seg_dispatch(1, t, rr_lo, nr, ncalls, si, nseg);
         }
-        const size_t ns = (size_t)std::max<int64_t>(nseg, 1);
-        s_segcall.need(ns);
-        s_seground.need(ns);
-        s_segdec.need(ns);
-        s_segfws.need(ns * NW);
-        s_theta.need(ns * N);
-        seg_dispatch(1, t, rr_lo, nr, ncalls, si, (int)std::min<int64_t>(nseg, INF32 / N));
         // round-received per candidate
         s_recv.need(ncand);
         s_rr.need(ncand);
@@ -1013,9 +1047,11 @@ struct hge_engine {
         KLAUNCH(k_set_rr, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand, s_recv.p,
                 s_rr.p, s_cts.p, d_rr.p, d_cts.p, o_ntx, 0);
       if (commit) {
-        s_bpos.need(ncalls);
-        KLAUNCH(k_scan_small, dim3(1), dim3(1024), 0, st, (const int32_t*)o_cc, s_bpos.p, ncalls,
-                o_cnt);
+        s_bpos.need(2 * (size_t)ncalls + 2);
+        int32_t* blist = s_bpos.p + ncalls;     // non-empty buckets
+        int32_t* nblist = s_bpos.p + 2 * ncalls;  // their count
+        KLAUNCH(k_bucket_list, dim3(1), dim3(1024), 0, st, (const int32_t*)o_cc, ncalls, s_bpos.p,
+                o_cnt, blist, nblist);
         s_keys.need((size_t)ncand * sizeof(OKey));
         s_keys2.need((size_t)ncand * sizeof(OKey));
         OKey* k1 = (OKey*)s_keys.p;
@@ -1023,8 +1059,9 @@ struct hge_engine {
         KLAUNCH(k_bucket_keys, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand, s_recv.p,
                 s_rr.p, s_cts.p, s_bpos.p, k1, d_rr.p, d_cts.p,
                 (unsigned long long*)(s_out.p + o_tx));
-        KLAUNCH(k_bucket_sort, dim3(ncalls), dim3(256), 0, st, (const int32_t*)s_bpos.p,
-                (const int32_t*)o_cc, k1, k2, o_ids);
+        KLAUNCH(k_bucket_sort, dim3(std::min(ncalls, 2048)), dim3(256), 0, st,
+                (const int32_t*)s_bpos.p, (const int32_t*)o_cc, (const int32_t*)blist,
+                (const int32_t*)nblist, k1, k2, o_ids);
         // new undetermined list (in candidate order)
         scan_large(s_fund.p, s_upos.p, ncand, o_cnt + 1);
         s_und2.need(ncand);
@@ -1193,7 +1230,7 @@ struct hge_engine {
 #define RCASE(B)                                                                                 \
   case B:                                                                                        \
     KLAUNCH(k_round_received<B>, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, \
-                       ncand, (const int32_t*)s_vis.p, ncalls, 0, rr_lo, R_last, s_segoff.p,   \
+                       ncand, (const int32_t*)s_vis.p, ncalls, 0, rr_lo, R_last, segoff_p,     \
                        s_segcnt.p,                                                               \
                        s_segcall.p, s_segdec.p, s_segfws.p, s_theta.p, s_recv.p, s_rr.p,         \
                        s_cts.p, bseg);                                                           \

@@ -1316,6 +1316,93 @@ __global__ void __launch_bounds__(256) k_segments_g(Tables t, int rr_lo, int nr,
   if (!mode && valid && d == 0) segcnt[qi] = nseg;
 }
 
+// One pass of k_segments_g for N <= 64: the witness arrivals come from the
+// visibility table, and the segments of round q are written straight into
+// [segoff[q], segoff[q+1]), a per-round capacity the host sized from the bound
+// N + 2 + (processed fame calls); unused slots get seg_round = -1.
+template <int G>
+__global__ void __launch_bounds__(256) k_segments_1p(Tables t, int rr_lo, int nr, int ncalls,
+                                                     const int32_t* vis, SegInfo si,
+                                                     const int32_t* segoff, int32_t* segcnt,
+                                                     int32_t* seg_call, int32_t* seg_round,
+                                                     uint8_t* seg_dec, uint64_t* seg_fws,
+                                                     int32_t* theta) {
+  const int N = t.N;
+  const int lane = threadIdx.x & 63, d = lane & (G - 1);
+  const int qi = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G);
+  const uint64_t gm = group_mask<G>(lane);
+  const int gshift = (G == 64) ? 0 : (lane & ~(G - 1));
+  const bool valid = qi < nr;  // uniform per group
+  const int i = rr_lo + (valid ? qi : 0);
+  const bool slot = valid && d < N;
+  int a = INF32;
+  bool known = false, val = false;
+  int row = -1;  // chain-major lastAncestors row of witness d (for theta)
+  if (slot) {
+    const int x = t.W[(size_t)i * N + d];
+    if (x >= 0 && vis[x] < ncalls) a = vis[x];
+    if (x >= 0) row = d * t.ccap + t.index[x];
+    const uint8_t f = t.fame[(size_t)i * N + d];  // persisted BEFORE this batch's update
+    known = f != 0;
+    val = f == 1;
+  }
+  const int pi = valid ? si.pr_index[qi] : -1;
+  const int cf = pi >= 0 ? si.pr_cf[pi] : INF32;
+  const int wl = pi >= 0 ? min(si.pr_len[pi], si.clast[pi] - cf + 1) : 0;  // processed calls
+  const int poff = pi >= 0 ? si.pr_off[pi] : 0;
+  int prevdec = -1, nseg = 0;
+  uint64_t prevf = 0;
+  const int base = valid ? segoff[qi] : 0;
+  int c = valid ? 0 : INF32;
+  while (c < ncalls) {
+    int nxt = group_min<G>((slot && a > c) ? a : INF32);
+    const bool pres = slot && a <= c;
+    if (c >= cf && c - cf < wl && slot) {
+      const uint8_t o = si.dec[(size_t)(poff + (c - cf)) * N + d];
+      if (o) {
+        known = true;
+        val = (o == 1);
+      }
+    }
+    const uint64_t bp = __ballot(pres) & gm;
+    const uint64_t und = __ballot(pres && !known) & gm;
+    const uint64_t fws = (__ballot(pres && known && val) & gm) >> gshift;
+    const bool decided = und == 0;
+    if (bp && (prevdec != (int)decided || fws != prevf)) {
+      const int sidx = base + nseg;
+      if (d == 0) {
+        seg_call[sidx] = c;
+        seg_round[sidx] = i;
+        seg_dec[sidx] = decided ? 1 : 0;
+        seg_fws[sidx] = fws;
+      }
+      // theta of the segment, lane = creator cx: the (|fws|/2 + 1)-th largest
+      // LA[w][cx] over its famous witnesses w (INT_MIN pads sort lowest)
+      {
+        const int cx = d;
+        int v[G];
+#pragma unroll
+        for (int dd = 0; dd < G; dd++) {
+          const int rd = __shfl(row, gshift + dd);
+          v[dd] = (((fws >> dd) & 1ull) && cx < N) ? t.LA[(size_t)rd * N + cx] : (int)0x80000000;
+        }
+        const int nf = __popcll(fws);
+        const int th = nf ? select_kth<G>(v, G - (nf / 2 + 1) + 1) : (int)0x80000000;
+        if (cx < N) theta[(size_t)sidx * N + cx] = th;
+      }
+      nseg++;
+      prevdec = decided;
+      prevf = fws;
+    }
+    // next change point: an arrival, or the next call DecideFame processes round i
+    if (c + 1 >= cf && c + 1 - cf < wl) nxt = min(nxt, c + 1);
+    else if (c + 1 < cf && wl > 0) nxt = min(nxt, cf);
+    if (nxt <= c) nxt = c + 1;
+    c = nxt;
+  }
+  if (valid && d == 0) segcnt[qi] = nseg;
+}
+
 // theta[seg][cx] = the (|fws|/2 + 1)-th largest LA[w][cx] over famous witnesses
 // w: event x (creator cx, index ix) is seen by a strict majority of them iff
 // ix <= theta (hashgraph.go:689-697).  INT32_MIN when nobody is famous.
@@ -1742,11 +1829,47 @@ struct SortChunk {
   }
 };
 
-__global__ void __launch_bounds__(256) k_bucket_sort(const int32_t* bend, const int32_t* bcnt,
-                                                     OKey* keys, OKey* tmp, int32_t* ids_out) {
+// bucket offsets (exclusive scan of the per-call counts, total = events
+// received) and the list of non-empty buckets, by one block
+__global__ void __launch_bounds__(1024) k_bucket_list(const int32_t* cnt, int n, int32_t* off,
+                                                      int32_t* total, int32_t* list,
+                                                      int32_t* nlist) {
+  __shared__ int ts[1024], tn[1024];
+  const int T = blockDim.x, tid = threadIdx.x;
+  const int per = (n + T - 1) / T;
+  const int lo = min(n, tid * per), hi = min(n, lo + per);
+  int s = 0, ne = 0;
+  for (int i = lo; i < hi; i++) {
+    s += cnt[i];
+    ne += cnt[i] > 0 ? 1 : 0;
+  }
+  ts[tid] = s;
+  tn[tid] = ne;
+  __syncthreads();
+  for (int o = 1; o < T; o <<= 1) {
+    const int a = tid >= o ? ts[tid - o] : 0, b = tid >= o ? tn[tid - o] : 0;
+    __syncthreads();
+    ts[tid] += a;
+    tn[tid] += b;
+    __syncthreads();
+  }
+  int run = ts[tid] - s, pos = tn[tid] - ne;
+  for (int i = lo; i < hi; i++) {
+    const int v = cnt[i];
+    off[i] = run;
+    run += v;
+    if (v > 0) list[pos++] = i;
+  }
+  if (tid == T - 1) {
+    *total = ts[T - 1];
+    *nlist = tn[T - 1];
+  }
+}
+
+__device__ void bucket_sort_one(int b, const int32_t* bend, const int32_t* bcnt, OKey* keys,
+                                OKey* tmp, int32_t* ids_out) {
   constexpr int CH = 512;  // keys per LDS chunk
   __shared__ SortChunk<CH> sc;
-  const int b = blockIdx.x;
   const int n = bcnt[b];
   if (n == 0) return;
   const int start = bend[b] - n;
@@ -1796,6 +1919,17 @@ __global__ void __launch_bounds__(256) k_bucket_sort(const int32_t* bend, const 
   }
   for (int i = tid; i < n; i += T) ids_out[start + i] = (int32_t)src[i].id;
 }
+
+// one block per non-empty bucket (grid-stride over the list)
+__global__ void __launch_bounds__(256) k_bucket_sort(const int32_t* bend, const int32_t* bcnt,
+                                                     const int32_t* list, const int32_t* nlist,
+                                                     OKey* keys, OKey* tmp, int32_t* ids_out) {
+  for (int li = blockIdx.x; li < *nlist; li += gridDim.x) {
+    bucket_sort_one(list[li], bend, bcnt, keys, tmp, ids_out);
+    __syncthreads();
+  }
+}
+
 
 __global__ void k_scatter_und(const int32_t* cand, int ncand, const int32_t* f_und,
                               const int32_t* pos, int32_t* und) {
