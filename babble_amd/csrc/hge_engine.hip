@@ -592,7 +592,10 @@ struct hge_engine {
     const int m = (int)(n1 - n0);
     // control block (one upload): round state, chain lengths, transpose bounds,
     // fss offsets of a fresh walk and the sweep segments
-    static const int SEG = getenv("HGE_SEG") ? std::max(1, std::min(64, atoi(getenv("HGE_SEG")))) : 64;
+    // segment length: latency-bound sweeps (small N) like short segments, bandwidth-bound
+    // ones (large N) long ones (fewer stale carries); HGE_SEG overrides
+    static const int SEG_ENV = getenv("HGE_SEG") ? std::max(1, std::min(64, atoi(getenv("HGE_SEG")))) : 0;
+    const int SEG = SEG_ENV ? SEG_ENV : (N <= 32 ? 16 : 64);
     std::vector<int2>& segs = h_segs;
     segs.clear();
     int maxnew = 0;

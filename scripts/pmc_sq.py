@@ -14,7 +14,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 COUNTERS = ["SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_INST_ANY", "SQ_INSTS_VALU",
-            "SQ_INSTS_VMEM_RD", "SQ_INSTS_SALU", "SQ_INSTS_LDS"]
+            "SQ_INSTS_VMEM_RD", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "GRBM_GUI_ACTIVE"]
 
 
 def main():
@@ -41,13 +41,14 @@ def main():
         rows.append((avg.get("SQ_WAVE_CYCLES", 0), name, n, avg))
     rows.sort(reverse=True)
     print(f"{'kernel':40s} {'launch':>6s} {'waves':>8s} {'wavecyc':>10s} {'wait%':>6s} "
-          f"{'valu/w':>7s} {'vmem/w':>7s} {'salu/w':>7s} {'lds/w':>6s}")
+          f"{'valu/w':>7s} {'vmem/w':>7s} {'salu/w':>7s} {'lds/w':>6s} {'gpu_cyc':>9s}")
     for wc, name, n, a in rows[:30]:
         w = max(a.get("SQ_WAVES", 1), 1)
         print(f"{name[:40]:40s} {n:6d} {w:8.0f} {wc:10.0f} "
               f"{100 * a.get('SQ_WAIT_INST_ANY', 0) / max(wc, 1):6.1f} "
               f"{a.get('SQ_INSTS_VALU', 0) / w:7.1f} {a.get('SQ_INSTS_VMEM_RD', 0) / w:7.1f} "
-              f"{a.get('SQ_INSTS_SALU', 0) / w:7.1f} {a.get('SQ_INSTS_LDS', 0) / w:6.1f}")
+              f"{a.get('SQ_INSTS_SALU', 0) / w:7.1f} {a.get('SQ_INSTS_LDS', 0) / w:6.1f} "
+              f"{a.get('GRBM_GUI_ACTIVE', 0):9.0f}")
 
 
 if __name__ == "__main__":
