@@ -138,13 +138,13 @@ struct hge_engine {
   DBuf<int32_t> s_small, s_newwit;
   DBuf<int32_t> s_LCR, s_clast;
   DBuf<uint8_t> s_dec, s_decbit;
-  DBuf<int32_t> s_segcnt, s_segoff, s_segcall, s_seground, s_theta;
+  DBuf<int32_t> s_segcnt, s_segcall, s_seground, s_theta;
   DBuf<uint8_t> s_segdec;
   DBuf<uint64_t> s_segfws;
   DBuf<int32_t> s_recv, s_rr, s_fund, s_upos, s_und2, s_bpos, s_vis;
   DBuf<int64_t> s_cts;
   DBuf<unsigned char> s_keys, s_keys2;
-  DBuf<int32_t> s_part, s_arr, s_fst;
+  DBuf<int32_t> s_part, s_fst;
   // coordinate sweeps: transposed tables and scratch
   int n_sweeps = 0;
   DBuf<int32_t> d_LAT, d_FDT, s_chg, s_bar;
@@ -292,9 +292,9 @@ struct hge_engine {
     DBuf<int32_t>* i32s[] = {&d_creator, &d_index,  &d_sp,    &d_op,     &d_ntx,     &d_round,
                              &d_rr,      &d_und,    &d_chain, &d_LA,     &d_FD,      &d_C,
                              &d_W,       &d_rcnt,   &d_minw,  &s_small,  &s_newwit,  &s_LCR,
-                             &s_clast,   &s_segcnt, &s_segoff, &s_segcall, &s_seground, &s_theta,
+                             &s_clast,   &s_segcnt, &s_segcall, &s_seground, &s_theta,
                              &s_recv,    &s_rr,     &s_bpos,  &s_fund,   &s_upos,    &s_vis,
-                             &s_und2,    &s_part,   &s_arr,   &s_fst,    &d_FSS,     &d_LAT,
+                             &s_und2,    &s_part,   &s_fst,    &d_FSS,     &d_LAT,
                              &d_FDT,     &s_chg,    &s_bar,   &s_bseg,   &s_kctl,    &s_cctl,
                              &s_out};
     for (auto* b : i32s) b->free_();
@@ -988,47 +988,42 @@ struct hge_engine {
         // first call at which each event is visible (arrivals, round received)
         KLAUNCH(k_visibility, dim3(div_up(n_coords, 256)), dim3(256), 0, st, (const int64_t*)c_nc,
                 ncalls, (int)n_coords, s_vis.p);
+        // one pass into per-round capacity slots (no count round trip); theta inline
+        // for N <= 64, by k_seg_theta_wide above
         const int G = group_lanes();
-        if (G) {
-          // N <= 64: one pass into per-round capacity slots (no count round trip)
-          const size_t ns = (size_t)std::max<int64_t>(nslot, 1);
-          s_segcall.need(ns);
-          s_seground.need(ns);
-          s_segdec.need(ns);
-          s_segfws.need(ns * NW);
-          s_theta.need(ns * N);
-          segoff_p = c_sgo;
-#define SEG1(GG)                                                                                   \
-  KLAUNCH(k_segments_1p<GG>, dim3(div_up((int64_t)nr * GG, 256)), dim3(256), 0, st, t, rr_lo, nr,  \
-          ncalls, (const int32_t*)s_vis.p, si, (const int32_t*)c_sgo, s_segcnt.p, s_segcall.p,     \
-          s_seground.p, s_segdec.p, s_segfws.p, s_theta.p);
-          if (G == 16) {
-            SEG1(16)
-          } else if (G == 32) {
-            SEG1(32)
-          } else {
-            SEG1(64)
-          }
-#undef SEG1
+        const size_t ns = (size_t)std::max<int64_t>(nslot, 1);
+        s_segcall.need(ns);
+        s_seground.need(ns);
+        s_segdec.need(ns);
+        s_segfws.need(ns * NW);
+        s_theta.need(ns * N);
+        segoff_p = c_sgo;
+#define SEG1(GG, SPL)                                                                              \
+  KLAUNCH((k_segments_1p<GG, SPL>), dim3(div_up((int64_t)nr * GG, 256)), dim3(256), 0, st, t,      \
+          rr_lo, nr, ncalls, (const int32_t*)s_vis.p, si, (const int32_t*)c_sgo, s_segcnt.p,       \
+          s_segcall.p, s_seground.p, s_segdec.p, s_segfws.p, s_theta.p);
+#define THW(B)                                                                                     \
+  KLAUNCH(k_seg_theta_wide<B>, dim3(std::min(nr, 4096)), dim3(256), 0, st, t,                      \
+          (const int32_t*)s_seground.p, (const int32_t*)c_sgo, (const int32_t*)s_segcnt.p, nr,     \
+          (const uint64_t*)s_segfws.p, s_theta.p);
+        if (G == 16) {
+          SEG1(16, 1)
+        } else if (G == 32) {
+          SEG1(32, 1)
+        } else if (NW == 1) {
+          SEG1(64, 1)
+        } else if (NW == 2) {
+          SEG1(64, 2)
+          THW(2)
+        } else if (NW == 3) {
+          SEG1(64, 3)
+          THW(3)
         } else {
-          s_segoff.need(nr + 1);
-          s_arr.need((size_t)nr * N);
-          segoff_p = s_segoff.p;
-          KLAUNCH(k_arrivals, dim3(div_up(nr * N, 256)), dim3(256), 0, st, t, rr_lo, nr,
-                  (const int32_t*)s_vis.p, ncalls, s_arr.p);
-          seg_dispatch(0, t, rr_lo, nr, ncalls, si, 0);
-          KLAUNCH(k_scan_small, dim3(1), dim3(1024), 0, st, s_segcnt.p, s_segoff.p, nr,
-                  s_small.p + 6);
-          int32_t nseg = 0;
-          readback(&nseg, s_small.p + 6, 1);
-          const size_t ns = (size_t)std::max(nseg, 1);
-          s_segcall.need(ns);
-          s_seground.need(ns);
-          s_segdec.need(ns);
-          s_segfws.need(ns * NW);
-          s_theta.need(ns * N);
-          seg_dispatch(1, t, rr_lo, nr, ncalls, si, nseg);
+          SEG1(64, 4)
+          THW(4)
         }
+#undef SEG1
+#undef THW
         // round-received per candidate
         s_recv.need(ncand);
         s_rr.need(ncand);
@@ -1140,8 +1135,8 @@ struct hge_engine {
     KLAUNCH(k_scan_add, dim3(div_up(n, 256)), dim3(256), 0, st, out, n, s_part.p + nb);
   }
 
-  // lanes per round in the group-scan kernels (N <= 64); 0 = thread-per-round kernels
-  int group_lanes() const { return N <= 16 ? 16 : N <= 32 ? 32 : N <= 64 ? 64 : 0; }
+  // lanes per round in the group-scan kernels (a lane holds NW slots when N > 64)
+  int group_lanes() const { return N <= 16 ? 16 : N <= 32 ? 32 : 64; }
 
   void fame_dispatch(int which, const Tables& t, int nrounds, int npairs, int items, int ncalls) {
     if (which == 1) {
@@ -1154,24 +1149,20 @@ struct hge_engine {
     switch (NW) {
 #define FCASE(B)                                                                                 \
   case B:                                                                                        \
-    KLAUNCH(k_fame_decide<B>, dim3(div_up(items, 256)), dim3(256), 0, st, t, c_pr,             \
-            c_pr + nrounds, c_pr + 2 * nrounds, nrounds, npairs, c_nc, c_Rc, s_dec.p);   \
+    KLAUNCH(k_fame_decide<B>, dim3(div_up(items, 256)), dim3(256), 0, st, t, c_pr,               \
+            c_pr + nrounds, c_pr + 2 * nrounds, nrounds, npairs, c_nc, c_Rc, s_dec.p);           \
     if (G == 16)                                                                                 \
-      KLAUNCH(k_fame_timeline_g<16>, dim3(div_up((int64_t)nrounds * 16, 256)), dim3(256), 0, st, \
-              t, c_pr, c_pr + nrounds, c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds,  \
-              c_nc, s_dec.p, s_decbit.p, c_Lc);                                              \
+      KLAUNCH((k_fame_timeline_g<16, 1>), dim3(div_up((int64_t)nrounds * 16, 256)), dim3(256), 0, \
+              st, t, c_pr, c_pr + nrounds, c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds, c_nc, \
+              s_dec.p, s_decbit.p, c_Lc);                                                        \
     else if (G == 32)                                                                            \
-      KLAUNCH(k_fame_timeline_g<32>, dim3(div_up((int64_t)nrounds * 32, 256)), dim3(256), 0, st, \
-              t, c_pr, c_pr + nrounds, c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds,  \
-              c_nc, s_dec.p, s_decbit.p, c_Lc);                                              \
-    else if (G == 64)                                                                            \
-      KLAUNCH(k_fame_timeline_g<64>, dim3(div_up((int64_t)nrounds * 64, 256)), dim3(256), 0, st, \
-              t, c_pr, c_pr + nrounds, c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds,  \
-              c_nc, s_dec.p, s_decbit.p, c_Lc);                                              \
+      KLAUNCH((k_fame_timeline_g<32, 1>), dim3(div_up((int64_t)nrounds * 32, 256)), dim3(256), 0, \
+              st, t, c_pr, c_pr + nrounds, c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds, c_nc, \
+              s_dec.p, s_decbit.p, c_Lc);                                                        \
     else                                                                                         \
-      KLAUNCH(k_fame_timeline<B>, dim3(div_up(nrounds, 64)), dim3(64), 0, st, t, c_pr,         \
-              c_pr + nrounds, c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds, c_nc,     \
-              s_dec.p, s_decbit.p, c_Lc);                                                      \
+      KLAUNCH((k_fame_timeline_g<64, B>), dim3(div_up((int64_t)nrounds * 64, 256)), dim3(256), 0, \
+              st, t, c_pr, c_pr + nrounds, c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds, c_nc, \
+              s_dec.p, s_decbit.p, c_Lc);                                                        \
     break;
       FCASE(1)
       FCASE(2)
@@ -1182,42 +1173,6 @@ struct hge_engine {
         throw EngineError(HGE_ERR_INTERNAL, "unsupported N");
     }
     (void)ncalls;
-  }
-
-  void seg_dispatch(int mode, const Tables& t, int rr_lo, int nr, int ncalls, const SegInfo& si,
-                    int nseg) {
-    const int G = group_lanes();
-    switch (NW) {
-#define SCASE(B)                                                                                 \
-  case B:                                                                                        \
-    if (G == 16)                                                                                 \
-      KLAUNCH(k_segments_g<16>, dim3(div_up((int64_t)nr * 16, 256)), dim3(256), 0, st, t, rr_lo, \
-              nr, c_nc, ncalls, si, s_arr.p, s_segcnt.p, s_segoff.p, s_segcall.p,              \
-              s_seground.p, s_segdec.p, s_segfws.p, mode);                                       \
-    else if (G == 32)                                                                            \
-      KLAUNCH(k_segments_g<32>, dim3(div_up((int64_t)nr * 32, 256)), dim3(256), 0, st, t, rr_lo, \
-              nr, c_nc, ncalls, si, s_arr.p, s_segcnt.p, s_segoff.p, s_segcall.p,              \
-              s_seground.p, s_segdec.p, s_segfws.p, mode);                                       \
-    else if (G == 64)                                                                            \
-      KLAUNCH(k_segments_g<64>, dim3(div_up((int64_t)nr * 64, 256)), dim3(256), 0, st, t, rr_lo, \
-              nr, c_nc, ncalls, si, s_arr.p, s_segcnt.p, s_segoff.p, s_segcall.p,              \
-              s_seground.p, s_segdec.p, s_segfws.p, mode);                                       \
-    else                                                                                         \
-      KLAUNCH(k_segments<B>, dim3(div_up(nr, 64)), dim3(64), 0, st, t, rr_lo, nr, c_nc,        \
-              ncalls, si, s_arr.p, s_segcnt.p, s_segoff.p, s_segcall.p, s_seground.p,            \
-              s_segdec.p, s_segfws.p, mode);                                                     \
-    if (mode == 1 && nseg > 0)                                                                   \
-      KLAUNCH(k_seg_theta<B>, dim3(std::min(div_up((int64_t)nseg * N, 256), 4096)), dim3(256), 0, \
-              st, t, s_seground.p, (const int32_t*)(s_small.p + 6), s_segfws.p, s_theta.p);      \
-    break;
-      SCASE(1)
-      SCASE(2)
-      SCASE(3)
-      SCASE(4)
-#undef SCASE
-      default:
-        throw EngineError(HGE_ERR_INTERNAL, "unsupported N");
-    }
   }
 
   void recv_dispatch(const Tables& t, const int32_t* cand, int ncand, int ncalls, int rr_lo,

@@ -923,47 +923,6 @@ __global__ void k_fame_decide(Tables t, const int32_t* pr_round, const int32_t* 
   dec[(size_t)p * N + xd] = out;
 }
 
-// Per processed round: fame state along its window of calls (persisted state
-// + decisions of each call), WitnessesDecided per call (roundInfo.go:78-85) and
-// the candidate LastConsensusRound per call (hashgraph.go:654-657).
-template <int NWT>
-__global__ void k_fame_timeline(Tables t, const int32_t* pr_round, const int32_t* pr_off,
-                                const int32_t* pr_cf, const int32_t* pr_len, int nrounds,
-                                const int64_t* nc, const uint8_t* dec, uint8_t* decbit,
-                                int32_t* Lc) {
-  const int ri = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ri >= nrounds) return;
-  const int N = t.N;
-  const int i = pr_round[ri];
-  uint64_t known[NWT], val[NWT];
-#pragma unroll
-  for (int w = 0; w < NWT; w++) known[w] = val[w] = 0;
-  for (int d = 0; d < N; d++) {
-    const uint8_t f = t.fame[(size_t)i * N + d];
-    if (f) known[d >> 6] |= 1ull << (d & 63);
-    if (f == 1) val[d >> 6] |= 1ull << (d & 63);
-  }
-  for (int q = 0; q < pr_len[ri]; q++) {
-    const int p = pr_off[ri] + q;
-    const int c = pr_cf[ri] + q;
-    const int64_t n = nc[c];
-    bool decided = true;
-    for (int d = 0; d < N; d++) {
-      const uint8_t o = dec[(size_t)p * N + d];
-      const uint64_t b = 1ull << (d & 63);
-      if (o) {
-        known[d >> 6] |= b;
-        if (o == 1) val[d >> 6] |= b;
-        else val[d >> 6] &= ~b;
-      }
-      const int x = t.W[(size_t)i * N + d];
-      if (x >= 0 && x < n && !((known[d >> 6] >> (d & 63)) & 1ull)) decided = false;
-    }
-    decbit[p] = decided ? 1 : 0;
-    if (decided) atomicMax(&Lc[c], i);
-  }
-}
-
 // LCR_c = max(LCR_start, prefix max of Lc); c_last(i) = first call with LCR >= i;
 // coverage check of each round's speculative window.
 __global__ void __launch_bounds__(1024) k_lcr_scan(const int32_t* Lc, int ncalls, int lcr_start,
@@ -1058,51 +1017,66 @@ __device__ __forceinline__ int group_min(int v) {
   return v;
 }
 
-// k_fame_timeline with one group per processed round
-template <int G>
+// k_fame_timeline with one group per processed round (G lanes; a lane holds
+// SPL witness slots d + 64k when N > 64)
+template <int G, int SPL>
 __global__ void __launch_bounds__(256) k_fame_timeline_g(Tables t, const int32_t* pr_round,
                                                          const int32_t* pr_off, const int32_t* pr_cf,
                                                          const int32_t* pr_len, int nrounds,
                                                          const int64_t* nc, const uint8_t* dec,
                                                          uint8_t* decbit, int32_t* Lc) {
+  static_assert(SPL == 1 || G == 64, "several slots per lane need full-wave groups");
   const int N = t.N;
   const int lane = threadIdx.x & 63, d = lane & (G - 1);
   const int ri = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G);
   const uint64_t gm = group_mask<G>(lane);
   const bool valid = ri < nrounds;  // uniform per group
   const int i = valid ? pr_round[ri] : 0;
-  bool known = false;
-  int x = -1;
-  if (valid && d < N) {
-    known = t.fame[(size_t)i * N + d] != 0;
-    x = t.W[(size_t)i * N + d];
+  bool known[SPL];
+  int x[SPL];
+#pragma unroll
+  for (int k = 0; k < SPL; k++) {
+    const int sl = d + 64 * k;
+    known[k] = false;
+    x[k] = -1;
+    if (valid && sl < N) {
+      known[k] = t.fame[(size_t)i * N + sl] != 0;
+      x[k] = t.W[(size_t)i * N + sl];
+    }
   }
   const int len = valid ? pr_len[ri] : 0;
   const int poff = valid ? pr_off[ri] : 0, cf = valid ? pr_cf[ri] : 0;
   // the window's loads go out QC calls at a time before the sequential scan uses them
   constexpr int QC = 8;
   int64_t nq[QC];
-  uint8_t oq[QC];
+  uint8_t oq[QC][SPL];
   for (int q = 0; q < len; q++) {
     const int u = q & (QC - 1);
     if (u == 0) {
 #pragma unroll
-      for (int k = 0; k < QC; k++) {
-        const bool in = q + k < len;
-        nq[k] = in ? nc[cf + q + k] : 0;
-        oq[k] = (in && d < N) ? dec[(size_t)(poff + q + k) * N + d] : 0;
+      for (int kq = 0; kq < QC; kq++) {
+        const bool in = q + kq < len;
+        nq[kq] = in ? nc[cf + q + kq] : 0;
+#pragma unroll
+        for (int k = 0; k < SPL; k++) {
+          const int sl = d + 64 * k;
+          oq[kq][k] = (in && sl < N) ? dec[(size_t)(poff + q + kq) * N + sl] : 0;
+        }
       }
     }
     const int p = poff + q, c = cf + q;
     int64_t n = nq[0];
-    uint8_t o = oq[0];
 #pragma unroll
-    for (int k = 1; k < QC; k++) {
-      n = (u == k) ? nq[k] : n;
-      o = (u == k) ? oq[k] : o;
+    for (int kq = 1; kq < QC; kq++) n = (u == kq) ? nq[kq] : n;
+    uint64_t und = 0;
+#pragma unroll
+    for (int k = 0; k < SPL; k++) {
+      uint8_t o = oq[0][k];
+#pragma unroll
+      for (int kq = 1; kq < QC; kq++) o = (u == kq) ? oq[kq][k] : o;
+      if (o) known[k] = true;
+      und |= __ballot(x[k] >= 0 && x[k] < n && !known[k]) & gm;
     }
-    if (o) known = true;
-    const uint64_t und = __ballot(d < N && x >= 0 && x < n && !known) & gm;
     if (d == 0) {
       decbit[p] = und == 0 ? 1 : 0;
       if (und == 0) atomicMax(&Lc[c], i);
@@ -1115,7 +1089,6 @@ __global__ void __launch_bounds__(256) k_fame_timeline_g(Tables t, const int32_t
 // round i, the calls at which (WitnessesDecided, famous set) changes.  State
 // changes only when a witness of round i becomes visible (its call of arrival)
 // or, while the round is processed by DecideFame, when a decision lands.
-// Mode 0 counts segments, mode 1 writes them.
 // ---------------------------------------------------------------------------
 struct SegInfo {
   const int32_t* pr_index;  // [rounds rr_lo..] -> index into pr_* arrays or -1
@@ -1127,18 +1100,6 @@ struct SegInfo {
 };
 
 // first call of the batch at which witness W[r][d] is visible (INF32: none / later)
-__global__ void k_arrivals(Tables t, int rr_lo, int nr, const int32_t* vis, int ncalls,
-                           int32_t* arr) {
-  const int item = blockIdx.x * blockDim.x + threadIdx.x;
-  const int N = t.N;
-  if (item >= nr * N) return;
-  const int q = item / N, d = item - (item / N) * N;
-  const int x = t.W[(size_t)(rr_lo + q) * N + d];
-  int a = INF32;
-  if (x >= 0 && vis[x] < ncalls) a = vis[x];
-  arr[item] = a;
-}
-
 // vis[x] = first call whose event count exceeds x (ncalls: none), for the
 // events [0, nev): a block takes 256 consecutive events and binary-searches
 // them in an LDS window of the calls from the first one that sees its first
@@ -1173,160 +1134,20 @@ __global__ void __launch_bounds__(256) k_visibility(const int64_t* nc, int ncall
   vis[x] = lo < 256 ? min(c0 + lo, ncalls) : upper(x, c0 + 256, ncalls);
 }
 
-template <int NWT>
-__global__ void k_segments(Tables t, int rr_lo, int nr, const int64_t* nc, int ncalls,
-                           SegInfo si, const int32_t* arr, int32_t* segcnt, const int32_t* segoff,
-                           int32_t* seg_call, int32_t* seg_round, uint8_t* seg_dec,
-                           uint64_t* seg_fws, int mode) {
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= nr) return;
-  const int N = t.N;
-  const int i = rr_lo + q;
-  const int32_t* ar = arr + (size_t)q * N;
-  uint64_t known[NWT], val[NWT], pres[NWT], prevf[NWT];
-#pragma unroll
-  for (int w = 0; w < NWT; w++) known[w] = val[w] = pres[w] = prevf[w] = 0;
-  for (int d = 0; d < N; d++) {
-    const uint8_t f = t.fame[(size_t)i * N + d];  // persisted BEFORE this batch's update
-    if (f) known[d >> 6] |= 1ull << (d & 63);
-    if (f == 1) val[d >> 6] |= 1ull << (d & 63);
-  }
-  const int pi = si.pr_index[q];
-  const int cf = pi >= 0 ? si.pr_cf[pi] : INF32;
-  const int wl = pi >= 0 ? min(si.pr_len[pi], si.clast[pi] - cf + 1) : 0;  // processed calls
-  int prevdec = -1;
-  int nseg = 0;
-  const int base = mode ? segoff[q] : 0;
-  int c = 0;
-  while (c < ncalls) {
-#pragma unroll
-    for (int w = 0; w < NWT; w++) pres[w] = 0;
-    int nxt = INF32;
-    for (int d = 0; d < N; d++) {
-      const int a = ar[d];
-      if (a <= c) pres[d >> 6] |= 1ull << (d & 63);
-      else nxt = min(nxt, a);
-    }
-    if (c >= cf && c - cf < wl) {
-      const uint8_t* dp = si.dec + (size_t)(si.pr_off[pi] + (c - cf)) * N;
-      for (int d = 0; d < N; d++) {
-        const uint8_t o = dp[d];
-        const uint64_t b = 1ull << (d & 63);
-        if (o) {
-          known[d >> 6] |= b;
-          if (o == 1) val[d >> 6] |= b;
-          else val[d >> 6] &= ~b;
-        }
-      }
-    }
-    bool exists = false, decided = true, same = true;
-    uint64_t fws[NWT];
-#pragma unroll
-    for (int w = 0; w < NWT; w++) {
-      if (pres[w]) exists = true;
-      if (pres[w] & ~known[w]) decided = false;
-      fws[w] = pres[w] & known[w] & val[w];
-      if (fws[w] != prevf[w]) same = false;
-    }
-    if (exists && (prevdec != (int)decided || !same)) {
-      if (mode) {
-        const int sidx = base + nseg;
-        seg_call[sidx] = c;
-        seg_round[sidx] = i;
-        seg_dec[sidx] = decided ? 1 : 0;
-#pragma unroll
-        for (int w = 0; w < NWT; w++) seg_fws[(size_t)sidx * NWT + w] = fws[w];
-      }
-      nseg++;
-      prevdec = decided;
-#pragma unroll
-      for (int w = 0; w < NWT; w++) prevf[w] = fws[w];
-    }
-    // next change point: an arrival, or the next call DecideFame processes round i
-    if (c + 1 >= cf && c + 1 - cf < wl) nxt = min(nxt, c + 1);
-    else if (c + 1 < cf && wl > 0) nxt = min(nxt, cf);
-    if (nxt <= c) nxt = c + 1;
-    c = nxt;
-  }
-  if (!mode) segcnt[q] = nseg;
-}
-
-// k_segments with one group per round (N <= 64: the famous set is one word)
-template <int G>
-__global__ void __launch_bounds__(256) k_segments_g(Tables t, int rr_lo, int nr, const int64_t* nc,
-                                                    int ncalls, SegInfo si, const int32_t* arr,
-                                                    int32_t* segcnt, const int32_t* segoff,
-                                                    int32_t* seg_call, int32_t* seg_round,
-                                                    uint8_t* seg_dec, uint64_t* seg_fws, int mode) {
-  const int N = t.N;
-  const int lane = threadIdx.x & 63, d = lane & (G - 1);
-  const int qi = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G);
-  const uint64_t gm = group_mask<G>(lane);
-  const int gshift = (G == 64) ? 0 : (lane & ~(G - 1));
-  const bool valid = qi < nr;  // uniform per group
-  const int i = rr_lo + (valid ? qi : 0);
-  const bool slot = valid && d < N;
-  const int a = slot ? arr[(size_t)qi * N + d] : INF32;
-  bool known = false, val = false;
-  if (slot) {
-    const uint8_t f = t.fame[(size_t)i * N + d];  // persisted BEFORE this batch's update
-    known = f != 0;
-    val = f == 1;
-  }
-  const int pi = valid ? si.pr_index[qi] : -1;
-  const int cf = pi >= 0 ? si.pr_cf[pi] : INF32;
-  const int wl = pi >= 0 ? min(si.pr_len[pi], si.clast[pi] - cf + 1) : 0;  // processed calls
-  const int poff = pi >= 0 ? si.pr_off[pi] : 0;
-  int prevdec = -1, nseg = 0;
-  uint64_t prevf = 0;
-  const int base = (mode && valid) ? segoff[qi] : 0;
-  int c = valid ? 0 : INF32;
-  while (c < ncalls) {
-    int nxt = group_min<G>((slot && a > c) ? a : INF32);
-    const bool pres = slot && a <= c;
-    if (c >= cf && c - cf < wl && slot) {
-      const uint8_t o = si.dec[(size_t)(poff + (c - cf)) * N + d];
-      if (o) {
-        known = true;
-        val = (o == 1);
-      }
-    }
-    const uint64_t bp = __ballot(pres) & gm;
-    const uint64_t und = __ballot(pres && !known) & gm;
-    const uint64_t fws = (__ballot(pres && known && val) & gm) >> gshift;
-    const bool decided = und == 0;
-    if (bp && (prevdec != (int)decided || fws != prevf)) {
-      if (mode && d == 0) {
-        const int sidx = base + nseg;
-        seg_call[sidx] = c;
-        seg_round[sidx] = i;
-        seg_dec[sidx] = decided ? 1 : 0;
-        seg_fws[sidx] = fws;
-      }
-      nseg++;
-      prevdec = decided;
-      prevf = fws;
-    }
-    // next change point: an arrival, or the next call DecideFame processes round i
-    if (c + 1 >= cf && c + 1 - cf < wl) nxt = min(nxt, c + 1);
-    else if (c + 1 < cf && wl > 0) nxt = min(nxt, cf);
-    if (nxt <= c) nxt = c + 1;
-    c = nxt;
-  }
-  if (!mode && valid && d == 0) segcnt[qi] = nseg;
-}
-
-// One pass of k_segments_g for N <= 64: the witness arrivals come from the
-// visibility table, and the segments of round q are written straight into
-// [segoff[q], segoff[q+1]), a per-round capacity the host sized from the bound
-// N + 2 + (processed fame calls); unused slots get seg_round = -1.
-template <int G>
+// One group per round (G lanes, SPL witness slots per lane when N > 64): the
+// witness arrivals come from the visibility table, the segments of round q are
+// written straight into [segoff[q], segoff[q+1]) (a per-round capacity the host
+// sized from the bound N + 2 + processed fame calls), and for N <= 64 each
+// segment's theta row is computed by the same group as it is found (lane =
+// witness slot, then = creator); wider hashgraphs take k_seg_theta_wide.
+template <int G, int SPL>
 __global__ void __launch_bounds__(256) k_segments_1p(Tables t, int rr_lo, int nr, int ncalls,
                                                      const int32_t* vis, SegInfo si,
                                                      const int32_t* segoff, int32_t* segcnt,
                                                      int32_t* seg_call, int32_t* seg_round,
                                                      uint8_t* seg_dec, uint64_t* seg_fws,
                                                      int32_t* theta) {
+  static_assert(SPL == 1 || G == 64, "several slots per lane need full-wave groups");
   const int N = t.N;
   const int lane = threadIdx.x & 63, d = lane & (G - 1);
   const int qi = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G);
@@ -1334,65 +1155,84 @@ __global__ void __launch_bounds__(256) k_segments_1p(Tables t, int rr_lo, int nr
   const int gshift = (G == 64) ? 0 : (lane & ~(G - 1));
   const bool valid = qi < nr;  // uniform per group
   const int i = rr_lo + (valid ? qi : 0);
-  const bool slot = valid && d < N;
-  int a = INF32;
-  bool known = false, val = false;
-  int row = -1;  // chain-major lastAncestors row of witness d (for theta)
-  if (slot) {
-    const int x = t.W[(size_t)i * N + d];
-    if (x >= 0 && vis[x] < ncalls) a = vis[x];
-    if (x >= 0) row = d * t.ccap + t.index[x];
-    const uint8_t f = t.fame[(size_t)i * N + d];  // persisted BEFORE this batch's update
-    known = f != 0;
-    val = f == 1;
+  int a[SPL];
+  bool known[SPL], val[SPL], slot[SPL];
+  int row = -1;  // chain-major lastAncestors row of witness d (theta, SPL == 1)
+#pragma unroll
+  for (int k = 0; k < SPL; k++) {
+    const int sl = d + 64 * k;
+    slot[k] = valid && sl < N;
+    a[k] = INF32;
+    known[k] = val[k] = false;
+    if (slot[k]) {
+      const int x = t.W[(size_t)i * N + sl];
+      if (x >= 0 && vis[x] < ncalls) a[k] = vis[x];
+      if (SPL == 1 && x >= 0) row = sl * t.ccap + t.index[x];
+      const uint8_t f = t.fame[(size_t)i * N + sl];  // persisted BEFORE this batch's update
+      known[k] = f != 0;
+      val[k] = f == 1;
+    }
   }
   const int pi = valid ? si.pr_index[qi] : -1;
   const int cf = pi >= 0 ? si.pr_cf[pi] : INF32;
   const int wl = pi >= 0 ? min(si.pr_len[pi], si.clast[pi] - cf + 1) : 0;  // processed calls
   const int poff = pi >= 0 ? si.pr_off[pi] : 0;
   int prevdec = -1, nseg = 0;
-  uint64_t prevf = 0;
+  uint64_t prevf[SPL];
+#pragma unroll
+  for (int k = 0; k < SPL; k++) prevf[k] = 0;
   const int base = valid ? segoff[qi] : 0;
   int c = valid ? 0 : INF32;
   while (c < ncalls) {
-    int nxt = group_min<G>((slot && a > c) ? a : INF32);
-    const bool pres = slot && a <= c;
-    if (c >= cf && c - cf < wl && slot) {
-      const uint8_t o = si.dec[(size_t)(poff + (c - cf)) * N + d];
-      if (o) {
-        known = true;
-        val = (o == 1);
+    int mn = INF32;
+#pragma unroll
+    for (int k = 0; k < SPL; k++) mn = min(mn, (slot[k] && a[k] > c) ? a[k] : INF32);
+    int nxt = group_min<G>(mn);
+    uint64_t bp = 0, und = 0, fws[SPL];
+    bool same = true;
+#pragma unroll
+    for (int k = 0; k < SPL; k++) {
+      const bool pres = slot[k] && a[k] <= c;
+      if (c >= cf && c - cf < wl && slot[k]) {
+        const uint8_t o = si.dec[(size_t)(poff + (c - cf)) * N + d + 64 * k];
+        if (o) {
+          known[k] = true;
+          val[k] = (o == 1);
+        }
       }
+      bp |= __ballot(pres) & gm;
+      und |= __ballot(pres && !known[k]) & gm;
+      fws[k] = (__ballot(pres && known[k] && val[k]) & gm) >> gshift;
+      same = same && fws[k] == prevf[k];
     }
-    const uint64_t bp = __ballot(pres) & gm;
-    const uint64_t und = __ballot(pres && !known) & gm;
-    const uint64_t fws = (__ballot(pres && known && val) & gm) >> gshift;
     const bool decided = und == 0;
-    if (bp && (prevdec != (int)decided || fws != prevf)) {
+    if (bp && (prevdec != (int)decided || !same)) {
       const int sidx = base + nseg;
       if (d == 0) {
         seg_call[sidx] = c;
         seg_round[sidx] = i;
         seg_dec[sidx] = decided ? 1 : 0;
-        seg_fws[sidx] = fws;
+#pragma unroll
+        for (int k = 0; k < SPL; k++) seg_fws[(size_t)sidx * SPL + k] = fws[k];
       }
-      // theta of the segment, lane = creator cx: the (|fws|/2 + 1)-th largest
-      // LA[w][cx] over its famous witnesses w (INT_MIN pads sort lowest)
-      {
+      if (SPL == 1) {
+        // theta of the segment, lane = creator cx: the (|fws|/2 + 1)-th largest
+        // LA[w][cx] over its famous witnesses w (INT_MIN pads sort lowest)
         const int cx = d;
         int v[G];
 #pragma unroll
         for (int dd = 0; dd < G; dd++) {
           const int rd = __shfl(row, gshift + dd);
-          v[dd] = (((fws >> dd) & 1ull) && cx < N) ? t.LA[(size_t)rd * N + cx] : (int)0x80000000;
+          v[dd] = (((fws[0] >> dd) & 1ull) && cx < N) ? t.LA[(size_t)rd * N + cx] : (int)0x80000000;
         }
-        const int nf = __popcll(fws);
+        const int nf = __popcll(fws[0]);
         const int th = nf ? select_kth<G>(v, G - (nf / 2 + 1) + 1) : (int)0x80000000;
         if (cx < N) theta[(size_t)sidx * N + cx] = th;
       }
       nseg++;
       prevdec = decided;
-      prevf = fws;
+#pragma unroll
+      for (int k = 0; k < SPL; k++) prevf[k] = fws[k];
     }
     // next change point: an arrival, or the next call DecideFame processes round i
     if (c + 1 >= cf && c + 1 - cf < wl) nxt = min(nxt, c + 1);
@@ -1403,63 +1243,64 @@ __global__ void __launch_bounds__(256) k_segments_1p(Tables t, int rr_lo, int nr
   if (valid && d == 0) segcnt[qi] = nseg;
 }
 
-// theta[seg][cx] = the (|fws|/2 + 1)-th largest LA[w][cx] over famous witnesses
-// w: event x (creator cx, index ix) is seen by a strict majority of them iff
-// ix <= theta (hashgraph.go:689-697).  INT32_MIN when nobody is famous.
+// theta for N > 64: one 256-thread block per round, its segments in turn
+// (thread = creator cx).
+// The famous witnesses' lastAncestors rows are staged in LDS as uint16
+// (position + 1; chains are < 65535 long on the wide path), then each thread
+// bisects the value domain of its column for the (|fws|/2 + 1)-th largest.
 template <int NWT>
-__device__ int seg_theta_one(const Tables& t, const int32_t* seg_round, const uint64_t* seg_fws,
-                             int sg, int cx) {
+__global__ void __launch_bounds__(256) k_seg_theta_wide(Tables t, const int32_t* seg_round,
+                                                        const int32_t* segoff, const int32_t* segcnt,
+                                                        int nr, const uint64_t* seg_fws,
+                                                        int32_t* theta) {
+  __shared__ uint16_t sv[256 * 256];  // [famous k][cx]
+  __shared__ int s_row[256];
+  __shared__ int s_nf;
   const int N = t.N;
-  const int i = seg_round[sg];
-  int nf = 0;
-#pragma unroll
-  for (int w = 0; w < NWT; w++) nf += __popcll(seg_fws[(size_t)sg * NWT + w]);
-  if (nf == 0) return (int)0x80000000;
-  const int k = nf / 2 + 1;
-  if (nf <= 64) {
-    // k-th largest by repeated selection over a bounded buffer
-    int vals[64];
-    int m = 0;
-    for (int d = 0; d < N; d++) {
-      if (!((seg_fws[(size_t)sg * NWT + (d >> 6)] >> (d & 63)) & 1ull)) continue;
-      const int w = t.W[(size_t)i * N + d];
-      vals[m++] = t.LA[rowoff(t, d, t.index[w]) + cx];
+  const int tid = threadIdx.x;
+  // one block per round (grid-stride), its segments [segoff[q], segoff[q] + segcnt[q]) in turn
+  for (int q = blockIdx.x; q < nr; q += gridDim.x) {
+    const int cnt = segcnt[q];
+    for (int l = 0; l < cnt; l++) {
+      const int sg = segoff[q] + l;
+      const int i = seg_round[sg];
+      if (tid == 0) {
+        int nf = 0;
+        for (int w = 0; w < NWT; w++) {
+          uint64_t m = seg_fws[(size_t)sg * NWT + w];
+          while (m) {
+            const int d = w * 64 + __builtin_ctzll(m);
+            m &= m - 1;
+            const int x = t.W[(size_t)i * N + d];
+            s_row[nf++] = d * t.ccap + t.index[x];
+          }
+        }
+        s_nf = nf;
+      }
+      __syncthreads();
+      const int nf = s_nf;
+      const int cx = tid;
+      if (cx < N) {
+        for (int k = 0; k < nf; k++)
+          sv[k * 256 + cx] = (uint16_t)(t.LA[(size_t)s_row[k] * N + cx] + 1);
+        int th = (int)0x80000000;
+        if (nf > 0) {
+          const int kk = nf / 2 + 1;  // k-th largest = largest v with count(>= v) >= kk
+          int lo = 0, hi = 65535;
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            int c2 = 0;
+            for (int k = 0; k < nf; k++) c2 += sv[k * 256 + cx] >= mid ? 1 : 0;
+            if (c2 >= kk) lo = mid;
+            else hi = mid - 1;
+          }
+          th = lo - 1;
+        }
+        theta[(size_t)sg * N + cx] = th;
+      }
+      __syncthreads();
     }
-    for (int a = 0; a < k; a++) {
-      int best = a;
-      for (int b = a + 1; b < m; b++)
-        if (vals[b] > vals[best]) best = b;
-      const int tmp = vals[a];
-      vals[a] = vals[best];
-      vals[best] = tmp;
-    }
-    return vals[k - 1];
   }
-  // general: threshold search by counting (values are chain positions >= -1)
-  int lo = -1, hi = INF32 - 1;  // largest v with count(>= v) >= k
-  while (lo < hi) {
-    const int mid = lo + (int)(((int64_t)hi - lo + 1) / 2);
-    int ccount = 0;
-    for (int d = 0; d < N; d++) {
-      if (!((seg_fws[(size_t)sg * NWT + (d >> 6)] >> (d & 63)) & 1ull)) continue;
-      const int w = t.W[(size_t)i * N + d];
-      ccount += (t.LA[rowoff(t, d, t.index[w]) + cx] >= mid) ? 1 : 0;
-    }
-    if (ccount >= k) lo = mid;
-    else hi = mid - 1;
-  }
-  return lo;
-}
-
-// grid-stride over (segment, creator): the segment count lives on the device
-template <int NWT>
-__global__ void k_seg_theta(Tables t, const int32_t* seg_round, const int32_t* pnseg,
-                            const uint64_t* seg_fws, int32_t* theta) {
-  const int N = t.N;
-  const int total = *pnseg * N;
-  for (int item = blockIdx.x * blockDim.x + threadIdx.x; item < total;
-       item += gridDim.x * blockDim.x)
-    theta[item] = seg_theta_one<NWT>(t, seg_round, seg_fws, item / N, item - (item / N) * N);
 }
 
 // ---------------------------------------------------------------------------
