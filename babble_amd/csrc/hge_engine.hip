@@ -24,6 +24,7 @@
 #include "hge_kernels.hip"
 #include "hge_coords.hip"
 #include "hge_rounds_coop.hip"
+#include "hge_walk_spec.hip"
 
 using namespace hge;
 
@@ -150,6 +151,7 @@ struct hge_engine {
   DBuf<int32_t> d_LAT, d_FDT, s_chg, s_bar;
   DBuf<uint64_t> d_ssc, s_gran;
   DBuf<int32_t> s_bseg;
+  DBuf<int32_t> s_H, s_hn, s_hres;  // speculative walk: histories, published counts, results
   bool coop_checked = false;
 
   hipEvent_t ev[8] = {};
@@ -296,7 +298,7 @@ struct hge_engine {
                              &s_recv,    &s_rr,     &s_bpos,  &s_fund,   &s_upos,    &s_vis,
                              &s_und2,    &s_part,   &s_fst,    &d_FSS,     &d_LAT,
                              &d_FDT,     &s_chg,    &s_bar,   &s_bseg,   &s_kctl,    &s_cctl,
-                             &s_out};
+                             &s_out,     &s_H,      &s_hn,    &s_hres};
     for (auto* b : i32s) b->free_();
     d_ts.free_();
     d_cts.free_();
@@ -676,8 +678,28 @@ struct hge_engine {
   if (maxlen < 0xFFFF) {                                                                           \
     KLAUNCH(k_fss<NPC>, dim3(div_up((int64_t)tot * NPC, 256)), dim3(256), 0, st, t, k_lo, k_lo + N, \
             tot, (int32_t*)nullptr, (uint16_t*)d_FSS.p);                                           \
-    KLAUNCH((k_rounds_walk<NPC, LPC, B>), dim3(1), dim3(1024), 0, st, t,                           \
-            (const uint16_t*)d_FSS.p, k_len, k_len + N, k_rs, rlo, Rprev, dbg_p());                \
+    const int nw = fresh ? spec_walkers(maxlen) : 0;                                               \
+    if (nw > 1) {                                                                                  \
+      const char* hc = getenv("HGE_WALK_HCAP"); /* tests: force the capacity fallback */          \
+      const int Hcap = hc ? std::max(2, atoi(hc))                                                  \
+                          : std::max(256, std::min(Rcap, 3 * (Rcap / nw) + 256));                  \
+      s_H.need((size_t)nw * Hcap * N);                                                             \
+      s_hres.need(4 * (size_t)nw + 1);                                                             \
+      s_hn.need(nw);                                                                               \
+      HIPCHK(hipMemsetAsync(s_hn.p, 0, 4 * (size_t)nw, st));                                       \
+      KLAUNCH((k_walk_spec<NPC, LPC, B>), dim3(nw), dim3(1024), 0, st, t,                         \
+              (const uint16_t*)d_FSS.p, k_len + N, nw, Hcap, s_H.p, s_hn.p, (int4*)s_hres.p);      \
+      int32_t* resume = s_hres.p + 4 * nw;                                                         \
+      KLAUNCH(k_walk_join, dim3(1), dim3(256), 0, st, t, (const int32_t*)s_H.p,                    \
+              (const int32_t*)s_hn.p, (const int4*)s_hres.p, nw, Hcap, k_rs, resume);              \
+      KLAUNCH((k_rounds_walk<NPC, LPC, B>), dim3(1), dim3(1024), 0, st, t,                         \
+              (const uint16_t*)d_FSS.p, k_len, k_len + N, k_rs, 0, 0, dbg_p(),                     \
+              (const int32_t*)resume);                                                             \
+    } else {                                                                                       \
+      KLAUNCH((k_rounds_walk<NPC, LPC, B>), dim3(1), dim3(1024), 0, st, t,                         \
+              (const uint16_t*)d_FSS.p, k_len, k_len + N, k_rs, rlo, Rprev, dbg_p(),               \
+              (const int32_t*)nullptr);                                                            \
+    }                                                                                              \
   } else {                                                                                         \
     KLAUNCH(k_fss<NPC>, dim3(div_up((int64_t)tot * NPC, 256)), dim3(256), 0, st, t, k_lo, k_lo + N, \
             tot, d_FSS.p, (uint16_t*)nullptr);                                                     \
@@ -728,6 +750,18 @@ struct hge_engine {
     n_coords = n1;
     coords_len = chain_len;
     prof_collect();
+  }
+
+  // Walkers of the speculative frontier walk (hge_walk_spec.hip) for a fresh
+  // state: one per ~384 positions of the longest chain, up to 32 (HGE_WALKERS
+  // overrides; 0 or 1 = the sequential walk).  Short graphs walk sequentially.
+  int spec_walkers(int maxlen) const {
+    const char* ev = getenv("HGE_WALKERS");  // read per call: the tests vary it
+    const int env = ev ? atoi(ev) : -1;
+    int minlen = INT32_MAX;
+    for (int c = 0; c < N; c++) minlen = std::min(minlen, chain_len[c]);
+    const int nw = env >= 0 ? env : (minlen >= 4 * 384 ? std::min(32, minlen / 384) : 0);
+    return std::max(0, std::min(nw, 64));
   }
 
   // rounds of a wide hashgraph: cooperative frontier kernel (hge_rounds_coop.hip)

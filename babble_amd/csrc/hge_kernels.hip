@@ -396,8 +396,12 @@ __device__ __forceinline__ int net16_packed(uint32_t R0, uint32_t R1, int q, int
 template <int NPC, int LPC, int B>
 __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* FSS,
                                                       const int32_t* olen, const int32_t* len,
-                                                      int32_t* rstate, int rlo, int Rprev,
-                                                      uint64_t* dbg) {
+                                                      int32_t* rstate, int rlo_arg, int Rprev,
+                                                      uint64_t* dbg, const int32_t* rlo_dev) {
+  // rlo_dev (non-null): the round to resume from, written by k_walk_join (-1: the
+  // speculative walk completed and there is nothing left to walk)
+  const int rlo = rlo_dev ? *rlo_dev : rlo_arg;
+  if (rlo < 0) return;
   constexpr int VPL = NPC / LPC;
   constexpr int RB = 64;       // C rows buffered per restage
   constexpr int Q8 = NPC / 8;  // int4 loads per fss row

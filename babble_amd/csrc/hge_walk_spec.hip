@@ -1,0 +1,382 @@
+// Speculative parallel frontier walk (N <= 32, fresh state).
+//
+// The frontier recurrence C_{r+1} = F(C_r) (hge_kernels.hip, k_rounds_walk;
+// DivideRounds, hashgraph.go:211-305 and 573-588) is a deterministic map of the
+// whole frontier vector, so two walks that ever reach the same vector coincide
+// from then on.  Measured on random gossip, a walk started from a guessed
+// frontier (chain positions in proportion, floor(len_c * w / nw)) lands on the
+// true trajectory within ~1-60 steps.  So nw walkers start at once, walker w
+// from guess w (walker 0 from the true start C_0), each one wave walking from
+// LDS exactly like k_rounds_walk, and each publishing its rows (local round
+// numbering, row 0 = its start) to a history buffer in HBM.  While wave 0
+// walks, waves 1-3 of the same workgroup compare the walker's newest row with
+// the published rows of the next WIN walkers; the first equal row (walker t,
+// row b) is a merge: the walker stops, since its future is walker t's from row
+// b on.  k_walk_join then follows the merges from walker 0 (whose rows are true
+// by construction) and copies the true rows into C with global round numbers.
+// Nothing is assumed: a walker that reaches its history capacity without a
+// merge ends the chain there, and the sequential k_rounds_walk resumes from the
+// last true row (k_walk_join writes its round to *resume, -1 = complete), so the
+// result is identical to the sequential walk in every case; only the time
+// depends on how soon the walkers merge.
+//
+// Cross-workgroup hand-off: history rows are written with relaxed agent-scope
+// (write-through) stores, then a release agent-scope store of the published
+// row count; readers use agent-scope loads (the "data is the flag" recipe of
+// k_rounds_coop).  A reader only ever reads rows below a count it has seen, and
+// never waits on another workgroup, so the launch needs no co-residency.
+namespace hge {
+
+template <int NPC, int LPC, int B>
+__global__ void __launch_bounds__(1024) k_walk_spec(Tables t, const uint16_t* FSS,
+                                                    const int32_t* len, int nw, int Hcap,
+                                                    int32_t* H, int32_t* hn, int4* res) {
+  constexpr int VPL = NPC / LPC;
+  constexpr int RB = 64;       // C rows buffered per flush
+  constexpr int Q8 = NPC / 8;  // int4 loads per fss row
+  constexpr int BR = B + 1;    // block rows per chain: B staged + the 0xFFFF row
+  constexpr int WIN = 8;       // later walkers a walker checks against
+  constexpr int NCHK = 192;    // checker threads (waves 1-3)
+  static_assert(NPC * LPC == 64, "one wave walks");
+  int pf = 0;  // prefetch sink
+  __shared__ __attribute__((aligned(16))) uint16_t blk[NPC * BR * NPC];  // [d][row][c]
+  __shared__ __attribute__((aligned(16))) int sA[NPC];
+  __shared__ int sP[NPC], sBase[NPC], sLen[NPC], sC[RB * NPC];
+  __shared__ int s_r, s_nr, s_lv, s_status, s_len, s_cur, s_wdone, s_mflag;
+  __shared__ unsigned long long s_mkey;
+  const int N = t.N, SM = t.SM;
+  const int tid = threadIdx.x, T = blockDim.x;
+  const int w = blockIdx.x;
+  int32_t* Hw = H + (size_t)w * Hcap * N;
+  if (tid < NPC) {
+    const int c = tid;
+    int P = INF32, ln = 0;
+    if (c < N) {
+      ln = len[c];
+      if (ln > 0) P = (int)((int64_t)ln * w / nw);  // walker 0: position 0 = C_0
+      __hip_atomic_store(Hw + c, P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    sP[c] = P;
+    sLen[c] = ln;
+  }
+  for (int i = tid; i < NPC * NPC; i += T) blk[((i / NPC) * BR + B) * NPC + (i % NPC)] = 0xFFFF;
+  if (tid == 0) {
+    s_r = 0;
+    s_lv = 1;
+    s_status = 0;
+    s_len = 0;
+    s_mflag = 0;
+    s_mkey = ~0ull;
+  }
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(hn + w, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    const int r0 = s_r;
+    if (s_lv) {
+      // restage: uint16 fss rows [P_d, P_d + B) of every chain (as k_rounds_walk)
+      constexpr int ITEMS = NPC * B * Q8;
+      constexpr int PER = (ITEMS + 1023) / 1024;
+      int4 vals[PER];
+#pragma unroll
+      for (int m = 0; m < PER; m++) {
+        const int item = tid + m * 1024;
+        const int d = item / (B * Q8);
+        const int rem = item - d * (B * Q8);
+        const int k = rem / Q8, q8 = rem - k * Q8;
+        int4 v4 = make_int4(-1, -1, -1, -1);
+        if (item < ITEMS && d < N && sP[d] != INF32 && sP[d] + k < sLen[d])
+          v4 = *(const int4*)(FSS + ((size_t)d * t.ccap + sP[d] + k) * NPC + 8 * q8);
+        vals[m] = v4;
+      }
+#pragma unroll
+      for (int m = 0; m < PER; m++) {
+        const int item = tid + m * 1024;
+        if (item >= ITEMS) break;
+        const int d = item / (B * Q8);
+        const int rem = item - d * (B * Q8);
+        const int k = rem / Q8, q8 = rem - k * Q8;
+        *(int4*)&blk[(d * BR + k) * NPC + 8 * q8] = vals[m];
+      }
+      if (tid < NPC) {
+        sBase[tid] = sP[tid];
+        sA[tid] = sP[tid] == INF32 ? B : 0;
+      }
+    }
+    for (int item = tid; item < RB * NPC; item += T) sC[item] = INF32;
+    if (tid == 0) {
+      s_cur = r0;
+      s_wdone = 0;
+    }
+    __syncthreads();
+    if (tid < 64) {
+      // ---- wave 0 walks (the k_rounds_walk step with no known rows)
+      const int lane = tid;
+      const int c = lane / LPC, q = lane - (lane / LPC) * LPC;
+      const bool act = c < N;
+      const int ln = sLen[c];
+      const int base_c = sBase[c];
+      const int qo = (SM - 1) / VPL, ko = (SM - 1) - qo * VPL;
+      const bool owner = act && q == qo;
+      int gb[VPL];
+#pragma unroll
+      for (int k = 0; k < VPL; k++) gb[k] = 2 * (((q * VPL + k) * BR) * NPC + c);
+      int myP = sP[c];
+      int r = r0, st = 0;  // st: 1 merged, 2 end of the graph, 3 history full
+      bool lvb = false;
+      const int rcap1 = Hcap - 1;
+      const int rend = min(r0 + RB, rcap1);
+      for (;;) {
+        if (r >= rend) {
+          if (r >= rcap1) st = 3;
+          break;
+        }
+        int Av[VPL], v[VPL];
+#pragma unroll
+        for (int k = 0; k < VPL; k++) Av[k] = sA[q * VPL + k];
+        const int mf = __hip_atomic_load(&s_mflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+        for (int k = 0; k < VPL; k++)
+          v[k] = *(const uint16_t*)((const char*)blk + gb[k] + Av[k] * (2 * NPC));
+        __builtin_amdgcn_sched_barrier(0);
+        if (mf) {
+          st = 1;
+          break;
+        }
+        int sel;
+        if constexpr (NPC == 16 && VPL == 4) {
+          sel = net16_packed((uint32_t)v[0] | ((uint32_t)v[2] << 16),
+                             (uint32_t)v[1] | ((uint32_t)v[3] << 16), q, ko);
+        } else {
+#pragma unroll
+          for (int size = 2; size <= NPC; size <<= 1) {
+            if (size <= VPL) {
+#pragma unroll
+              for (int k = 0; k < VPL; k++) {
+                const int k2 = k ^ (size - 1);
+                if (k2 > k) {
+                  const int a = v[k], b = v[k2];
+                  v[k] = min(a, b);
+                  v[k2] = max(a, b);
+                }
+              }
+            } else {
+              const bool lower = (q & ((size >> 1) / VPL)) == 0;
+              int o[VPL];
+#pragma unroll
+              for (int k = 0; k < VPL; k++) o[k] = dpp_flip(size / VPL - 1, v[VPL - 1 - k]);
+#pragma unroll
+              for (int k = 0; k < VPL; k++) v[k] = lower ? min(v[k], o[k]) : max(v[k], o[k]);
+            }
+#pragma unroll
+            for (int stride = size >> 2; stride > 0; stride >>= 1) {
+              if (stride < VPL) {
+#pragma unroll
+                for (int k = 0; k < VPL; k++) {
+                  const int k2 = k ^ stride;
+                  if (k2 > k) {
+                    const int a = v[k], b = v[k2];
+                    v[k] = min(a, b);
+                    v[k2] = max(a, b);
+                  }
+                }
+              } else {
+                const bool lower = (q & (stride / VPL)) == 0;
+#pragma unroll
+                for (int k = 0; k < VPL; k++) {
+                  const int o = dpp_flip(stride / VPL, v[k]);
+                  v[k] = lower ? min(v[k], o) : max(v[k], o);
+                }
+              }
+            }
+          }
+          sel = v[0];
+#pragma unroll
+          for (int k = 1; k < VPL; k++) sel = (k == ko) ? v[k] : sel;
+        }
+        const int cand = sel < ln ? sel : INF32;
+        const int nxt = myP == INF32 ? INF32 : cand;
+        myP = nxt;
+        const int rowA = nxt == INF32 ? B : nxt - base_c;
+        if (owner) {
+          sP[c] = nxt;
+          sA[c] = min(rowA, B);
+          sC[(r - r0) * NPC + c] = nxt;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const bool alive_l = owner && nxt != INF32;
+        const uint64_t alive = __builtin_amdgcn_ballot_w64(alive_l);
+        // a walker off the true trajectory can step BACK along a chain (the map is
+        // monotone, but a guessed start is not below its image): that member
+        // leaves its block too
+        const uint64_t lv = __builtin_amdgcn_ballot_w64(alive_l && (rowA >= B || rowA < 0));
+        if (alive == 0) {
+          st = 2;
+          break;
+        }
+        r++;
+        // the row r is complete in sC: hand it to the checker waves
+        if (lane == 0) __hip_atomic_store(&s_cur, r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lv != 0) {
+          lvb = true;
+          break;
+        }
+      }
+      if (lane == 0) {
+        s_nr = r - r0 + (st == 2 ? 1 : 0);  // rows r0+1 .. r0+s_nr were produced
+        s_r = r;
+        s_lv = lvb;
+        s_status = st;
+        s_len = r + 1;  // end / full: rows 0..r are this walker's rows
+        __hip_atomic_store(&s_wdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    } else if (tid < 64 + NCHK) {
+      // ---- waves 1-3 look for the walker's newest row among the published rows
+      //      of walkers w+1 .. w+WIN
+      const int ct = tid - 64;
+      int checked = r0;
+      for (;;) {
+        const int wd = __hip_atomic_load(&s_wdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const int rr = __hip_atomic_load(&s_cur, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (rr > checked &&
+            !__hip_atomic_load(&s_mflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+          int sv[NPC];
+#pragma unroll
+          for (int c = 0; c < NPC; c++) sv[c] = sC[(rr - 1 - r0) * NPC + c];
+          for (int k = 1; k <= WIN && w + k < nw; k++) {
+            const int tw = w + k;
+            const int cnt = __hip_atomic_load(hn + tw, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            const int32_t* Ht = H + (size_t)tw * Hcap * N;
+            for (int b = ct; b < cnt; b += NCHK) {
+              const int32_t* row = Ht + (size_t)b * N;
+              bool eq = true;
+#pragma unroll
+              for (int c = 0; c < NPC; c++) {
+                if (c < N && eq)
+                  eq = __hip_atomic_load(row + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == sv[c];
+              }
+              if (eq) {
+                atomicMin(&s_mkey, ((unsigned long long)rr << 40) | ((unsigned long long)k << 32) |
+                                       (unsigned long long)b);
+                __hip_atomic_store(&s_mflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              }
+            }
+          }
+          checked = rr;
+        }
+        if (wd) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+    } else {
+      // ---- the other waves pull the rows after every block into L2 (as k_rounds_walk)
+      constexpr int RPL = 128 / (2 * NPC);
+      constexpr int LPCH = B / RPL;
+      for (int item = tid - 64 - NCHK; item < NPC * LPCH; item += T - 64 - NCHK) {
+        const int d = item / LPCH, k = (item - d * LPCH) * RPL;
+        if (d < N && sBase[d] != INF32 && sBase[d] + B + k < sLen[d])
+          pf ^= *(const int*)(FSS + ((size_t)d * t.ccap + sBase[d] + B + k) * NPC);
+      }
+    }
+    __syncthreads();
+    // ---- publish the walked rows (every column, INF included)
+    const int nr = min(s_nr, RB);
+    for (int item = tid; item < nr * NPC; item += T) {
+      const int qq = item / NPC, c = item - qq * NPC;
+      if (c < N)
+        __hip_atomic_store(Hw + (size_t)(r0 + 1 + qq) * N + c, sC[item], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __threadfence();
+    __syncthreads();
+    if (tid == 0)
+      __hip_atomic_store(hn + w, r0 + nr + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    const int fin = s_status;
+    if (fin) {
+      if (tid == 0) {
+        if (fin == 1) {
+          const unsigned long long key = s_mkey;
+          res[w] = make_int4((int)(key >> 40), w + (int)((key >> 32) & 0xFF),
+                             (int)(key & 0xFFFFFFFFull), 1);
+        } else {
+          res[w] = make_int4(s_len, -1, -1, fin);
+        }
+      }
+      break;
+    }
+    __syncthreads();  // s_r / s_lv are rewritten by the next walk
+  }
+  if (pf == 0x7fffffff && tid == 1 && nw < 0) res[0].x = pf;  // never true: keeps the prefetch
+}
+
+// Follow the merges from walker 0 and copy the true rows into C (one block).
+// res[w] = {a, t, b, 1}: walker w's row a equals walker t's row b;
+//          {len, -1, -1, 2}: walker w reached the end, rows 0..len-1;
+//          {len, -1, -1, 3}: history full, rows 0..len-1 (the chain ends there).
+// rstate[0] = rounds (complete chain), rstate[1] = 1 if C overflows;
+// *resume = round of the last true row when the sequential walk must go on, else -1.
+__global__ void __launch_bounds__(256) k_walk_join(Tables t, const int32_t* H, const int32_t* hn,
+                                                   const int4* res, int nw, int Hcap,
+                                                   int32_t* rstate, int32_t* resume) {
+  constexpr int MAXSEG = 128;
+  __shared__ int s_w[MAXSEG], s_e0[MAXSEG], s_g[MAXSEG], s_n[MAXSEG];
+  __shared__ int s_ns, s_ok;
+  const int N = t.N;
+  if (threadIdx.x == 0) {
+    int wc = 0, e = 0, g = 0, ns = 0, rs_out = -1, R = -1;
+    auto emit = [&](int wv, int e0, int e1) {
+      if (e1 > e0 && ns < MAXSEG) {
+        s_w[ns] = wv;
+        s_e0[ns] = e0;
+        s_g[ns] = g;
+        s_n[ns] = e1 - e0;
+        ns++;
+        g += e1 - e0;
+      }
+    };
+    for (int it = 0; it <= nw; it++) {
+      const int4 rs = res[wc];
+      if (rs.w == 1) {
+        const int a = rs.x, tw = rs.y, b = rs.z;
+        int ne;
+        if (e <= a) {
+          emit(wc, e, a);
+          ne = b;
+        } else {
+          ne = b + (e - a);
+        }
+        if (ne < hn[tw]) {
+          wc = tw;
+          e = ne;
+          continue;
+        }
+        // the merged row is not published in walker tw: go on sequentially from
+        // the true row we stand on
+        const int cur = e <= a ? a : e;
+        emit(wc, cur, cur + 1);
+        rs_out = g - 1;
+        break;
+      }
+      emit(wc, e, rs.x);
+      if (rs.w == 2) R = g;
+      else rs_out = g - 1;
+      break;
+    }
+    const bool over = g + 1 >= t.Rcap || ns >= MAXSEG;
+    if (over) rstate[1] = 1;
+    else if (R >= 0) rstate[0] = R;
+    *resume = over ? -1 : rs_out;
+    s_ns = ns;
+    s_ok = !over;
+  }
+  __syncthreads();
+  if (!s_ok) return;
+  for (int s = 0; s < s_ns; s++) {
+    const int32_t* src = H + ((size_t)s_w[s] * Hcap + s_e0[s]) * N;
+    int32_t* dst = t.C + (size_t)s_g[s] * N;
+    const int cnt = s_n[s] * N;
+    for (int i = threadIdx.x; i < cnt; i += blockDim.x) dst[i] = src[i];
+  }
+}
+
+}  // namespace hge

@@ -42,19 +42,22 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
-def algorithmic_bytes(kernel, n, events, ordered):
+def algorithmic_bytes(kernel, n, events, ordered, sweeps=1):
     """Algorithmic HBM bytes of ONE launch of `kernel` over a whole replay
     (B(N) = 24N + 48 per ordered event).
 
     coordinates: k_coord_final 16N/event (read LA[sp] and D, write LA and FD),
-    k_coord_local 8N/event, k_la_sweep 12N/event (op row + own row read, own
-    row written), k_transpose and k_fdt_runs 8N/event; rounds: k_fss 8N/event (FD row read,
+    k_coord_local 8N/event, k_la_sweep 8N/event per sweep (op row + own row
+    read) plus the own row written once over all `sweeps` (a sweep stores only
+    the values that changed, so a converged row is not re-written), k_transpose and k_fdt_runs 8N/event; rounds: k_fss 8N/event (FD row read,
     fss row written), k_rounds_walk / k_rounds_coop 4N/event (the strongly-see
     round test reads each event's LA row once); order: k_round_received /
     k_median_wave (4N + 48)/ordered event; anything else the 48-byte sort key.
     """
     name = kernel.strip("()").split("<")[0]
-    per_event = {"k_coord_final": 16 * n, "k_coord_local": 8 * n, "k_la_sweep": 12 * n,
+    if name == "k_la_sweep":
+        return 8 * n * events + 4 * n * events / max(sweeps, 1)
+    per_event = {"k_coord_final": 16 * n, "k_coord_local": 8 * n,
                  "k_transpose": 8 * n, "k_fdt_runs": 8 * n, "k_fss": 8 * n, "k_rounds_walk": 4 * n,
                  "k_rounds_coop": 4 * n, "k_rounds_fss": 4 * n, "k_rounds_frontier": 4 * n}
     if name in per_event:
@@ -186,13 +189,14 @@ def main():
 
     def kernel_gbs(name):
         """(algorithmic bytes per launch, avg launch ms, achieved GB/s) of one kernel.
-        k_la_sweep: every sweep that does work streams the rows once (12N bytes per
-        event); the queued launches after the converged one return at once and
-        are left out of the launch count."""
+        k_la_sweep: every sweep that does work reads the own and op rows once (8N
+        bytes per event) and the row writes are spread over the sweeps; the
+        queued launches after the converged one return at once and are left out
+        of the launch count."""
         ms, cnt = kstats[name]
         if name.startswith("k_la_sweep"):
             cnt = sweeps * nprof
-            b = algorithmic_bytes(name, n, ev0, ord0)
+            b = algorithmic_bytes(name, n, ev0, ord0, sweeps)
         else:
             b = algorithmic_bytes(name, n, ev0, ord0) / max(cnt // nprof, 1)
         per_launch = ms / max(cnt, 1)
