@@ -151,7 +151,10 @@ struct hge_engine {
   DBuf<int32_t> d_LAT, d_FDT, s_chg, s_bar;
   DBuf<uint64_t> d_ssc, s_gran;
   DBuf<int32_t> s_bseg;
-  DBuf<int32_t> s_H, s_hn, s_hres;  // speculative walk: histories, published counts, results
+  DBuf<uint64_t> s_H;                // speculative walk: epoch-tagged histories
+  DBuf<int32_t> s_hn, s_hres;        // rows written + progress hints, merge results
+  uint32_t walk_epoch = 0;
+  int walk_chk[2] = {448, 2};        // checker threads, poll pause (HGE_WALK_CHK="n,s")
   bool coop_checked = false;
 
   hipEvent_t ev[8] = {};
@@ -298,7 +301,7 @@ struct hge_engine {
                              &s_recv,    &s_rr,     &s_bpos,  &s_fund,   &s_upos,    &s_vis,
                              &s_und2,    &s_part,   &s_fst,    &d_FSS,     &d_LAT,
                              &d_FDT,     &s_chg,    &s_bar,   &s_bseg,   &s_kctl,    &s_cctl,
-                             &s_out,     &s_H,      &s_hn,    &s_hres};
+                             &s_out,     &s_hn,     &s_hres};
     for (auto* b : i32s) b->free_();
     d_ts.free_();
     d_cts.free_();
@@ -306,6 +309,8 @@ struct hge_engine {
     d_S.free_();
     d_ssb.free_();
     d_seeb.free_();
+    s_H.free_();
+    s_wdbg.free_();
     s_segfws.free_();
     d_coin.free_();
     d_wit.free_();
@@ -683,18 +688,22 @@ struct hge_engine {
       const char* hc = getenv("HGE_WALK_HCAP"); /* tests: force the capacity fallback */          \
       const int Hcap = hc ? std::max(2, atoi(hc))                                                  \
                           : std::max(256, std::min(Rcap, 3 * (Rcap / nw) + 256));                  \
-      s_H.need((size_t)nw * Hcap * N);                                                             \
+      if ((size_t)nw * Hcap * N > s_H.n) {                                                         \
+        s_H.need((size_t)nw * Hcap * N); /* epoch 0 never matches a launch's tag */                \
+        HIPCHK(hipMemsetAsync(s_H.p, 0, s_H.n * sizeof(uint64_t), st));                            \
+      }                                                                                            \
       s_hres.need(4 * (size_t)nw + 1);                                                             \
-      s_hn.need(nw);                                                                               \
-      HIPCHK(hipMemsetAsync(s_hn.p, 0, 4 * (size_t)nw, st));                                       \
+      s_hn.need(2 * (size_t)nw);                                                                   \
       KLAUNCH((k_walk_spec<NPC, LPC, B>), dim3(nw), dim3(1024), 0, st, t,                         \
-              (const uint16_t*)d_FSS.p, k_len + N, nw, Hcap, s_H.p, s_hn.p, (int4*)s_hres.p);      \
+              (const uint16_t*)d_FSS.p, k_len + N, nw, Hcap, s_H.p, s_hn.p, s_hn.p + nw,          \
+              (int4*)s_hres.p, ++walk_epoch, walk_chk[0], walk_chk[1], walk_dbg(nw));              \
       int32_t* resume = s_hres.p + 4 * nw;                                                         \
-      KLAUNCH(k_walk_join, dim3(1), dim3(256), 0, st, t, (const int32_t*)s_H.p,                    \
+      KLAUNCH(k_walk_join, dim3(64), dim3(256), 0, st, t, (const uint64_t*)s_H.p,                    \
               (const int32_t*)s_hn.p, (const int4*)s_hres.p, nw, Hcap, k_rs, resume);              \
       KLAUNCH((k_rounds_walk<NPC, LPC, B>), dim3(1), dim3(1024), 0, st, t,                         \
               (const uint16_t*)d_FSS.p, k_len, k_len + N, k_rs, 0, 0, dbg_p(),                     \
               (const int32_t*)resume);                                                             \
+      if (getenv("HGE_WALK_DEBUG")) walk_debug(nw);                                               \
     } else {                                                                                       \
       KLAUNCH((k_rounds_walk<NPC, LPC, B>), dim3(1), dim3(1024), 0, st, t,                         \
               (const uint16_t*)d_FSS.p, k_len, k_len + N, k_rs, rlo, Rprev, dbg_p(),               \
@@ -753,15 +762,43 @@ struct hge_engine {
   }
 
   // Walkers of the speculative frontier walk (hge_walk_spec.hip) for a fresh
-  // state: one per ~384 positions of the longest chain, up to 32 (HGE_WALKERS
+  // state: one per ~192 positions of the shortest chain, up to 32 (HGE_WALKERS
   // overrides; 0 or 1 = the sequential walk).  Short graphs walk sequentially.
-  int spec_walkers(int maxlen) const {
+  int spec_walkers(int maxlen) {
+    if (const char* ck = getenv("HGE_WALK_CHK")) {
+      int a = 448, b = 2;
+      if (sscanf(ck, "%d,%d", &a, &b) == 2) {
+        walk_chk[0] = std::max(64, std::min(896, a / 64 * 64));
+        walk_chk[1] = std::max(0, std::min(64, b));
+      }
+    }
     const char* ev = getenv("HGE_WALKERS");  // read per call: the tests vary it
     const int env = ev ? atoi(ev) : -1;
     int minlen = INT32_MAX;
     for (int c = 0; c < N; c++) minlen = std::min(minlen, chain_len[c]);
-    const int nw = env >= 0 ? env : (minlen >= 4 * 384 ? std::min(32, minlen / 384) : 0);
+    const int nw = env >= 0 ? env : (minlen >= 4 * 192 ? std::min(32, minlen / 192) : 0);
     return std::max(0, std::min(nw, 64));
+  }
+
+  // HGE_WALK_DEBUG: per-walker rows, merge results and cycle stamps on stderr
+  DBuf<uint64_t> s_wdbg;
+  uint64_t* walk_dbg(int nw) {
+    if (!getenv("HGE_WALK_DEBUG")) return nullptr;
+    s_wdbg.need(4 * (size_t)nw);
+    return s_wdbg.p;
+  }
+  void walk_debug(int nw) {
+    std::vector<int32_t> res(4 * nw + 1), hn(nw);
+    std::vector<uint64_t> wd(4 * nw);
+    readback(res.data(), s_hres.p, res.size());
+    readback(hn.data(), s_hn.p, hn.size());
+    readback(wd.data(), s_wdbg.p, wd.size());
+    fprintf(stderr, "walk: nw=%d resume=%d |", nw, res[4 * nw]);
+    for (int w = 0; w < nw; w++)
+      fprintf(stderr, " %d:%d[%d,%d,%d,%d](%llu/%llu/%llu)", w, hn[w], res[4 * w], res[4 * w + 1],
+              res[4 * w + 2], res[4 * w + 3], (unsigned long long)wd[4 * w],
+              (unsigned long long)wd[4 * w + 1], (unsigned long long)wd[4 * w + 2]);
+    fprintf(stderr, "\n");
   }
 
   // rounds of a wide hashgraph: cooperative frontier kernel (hge_rounds_coop.hip)

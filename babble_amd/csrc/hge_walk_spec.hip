@@ -20,41 +20,54 @@
 // result is identical to the sequential walk in every case; only the time
 // depends on how soon the walkers merge.
 //
-// Cross-workgroup hand-off: history rows are written with relaxed agent-scope
-// (write-through) stores, then a release agent-scope store of the published
-// row count; readers use agent-scope loads (the "data is the flag" recipe of
-// k_rounds_coop).  A reader only ever reads rows below a count it has seen, and
-// never waits on another workgroup, so the launch needs no co-residency.
+// Cross-workgroup hand-off without fences ("data is the flag", as k_rounds_coop):
+// every history entry is 64 bits, (launch epoch << 32) | position, written by
+// the owner lane as soon as the step computes it with a relaxed agent-scope
+// (write-through) store, so publishing costs the walk no wait.  A checker
+// compares whole tagged words with relaxed agent-scope loads: an entry that is
+// stale (older epoch) or not yet visible never equals a current one, so it can
+// only delay a merge, never fake one.  Each row index is written once per
+// launch.  Lane 0 also stores a progress hint (rows so far) that bounds the
+// scan.  No workgroup ever waits on another, so the launch needs no co-residency.
 namespace hge {
+
+__device__ __forceinline__ int s_r0_rows(int r, int st) { return r + 1; }
 
 template <int NPC, int LPC, int B>
 __global__ void __launch_bounds__(1024) k_walk_spec(Tables t, const uint16_t* FSS,
                                                     const int32_t* len, int nw, int Hcap,
-                                                    int32_t* H, int32_t* hn, int4* res) {
+                                                    uint64_t* H, int32_t* hn, int32_t* hp,
+                                                    int4* res, uint32_t epoch, int nchk,
+                                                    int nsleep, uint64_t* wdbg) {
   constexpr int VPL = NPC / LPC;
-  constexpr int RB = 64;       // C rows buffered per flush
+  constexpr int RB = 64;       // rows per walk segment (the sC buffer the checkers read)
   constexpr int Q8 = NPC / 8;  // int4 loads per fss row
   constexpr int BR = B + 1;    // block rows per chain: B staged + the 0xFFFF row
-  constexpr int WIN = 8;       // later walkers a walker checks against
-  constexpr int NCHK = 192;    // checker threads (waves 1-3)
+  constexpr int WIN = 6;       // later walkers a walker checks against
+  // nchk checker threads (waves 1 .. nchk/64), each pausing nsleep x 64 cycles
+  // between polls; the rest prefetch
+  const int NCHK = nchk;
   static_assert(NPC * LPC == 64, "one wave walks");
   int pf = 0;  // prefetch sink
   __shared__ __attribute__((aligned(16))) uint16_t blk[NPC * BR * NPC];  // [d][row][c]
   __shared__ __attribute__((aligned(16))) int sA[NPC];
   __shared__ int sP[NPC], sBase[NPC], sLen[NPC], sC[RB * NPC];
-  __shared__ int s_r, s_nr, s_lv, s_status, s_len, s_cur, s_wdone, s_mflag;
+  __shared__ int s_r, s_lv, s_status, s_len, s_cur, s_wdone, s_mflag;
   __shared__ unsigned long long s_mkey;
   const int N = t.N, SM = t.SM;
   const int tid = threadIdx.x, T = blockDim.x;
   const int w = blockIdx.x;
-  int32_t* Hw = H + (size_t)w * Hcap * N;
+  uint64_t d_t0 = 0, d_rs = 0, d_nrs = 0, d_tw = 0;  // wdbg: cycles, restage cycles, restages
+  if (wdbg && tid == 0) d_t0 = stamp();
+  uint64_t* Hw = H + (size_t)w * Hcap * N;
+  const uint64_t tag = (uint64_t)epoch << 32;
   if (tid < NPC) {
     const int c = tid;
     int P = INF32, ln = 0;
     if (c < N) {
       ln = len[c];
       if (ln > 0) P = (int)((int64_t)ln * w / nw);  // walker 0: position 0 = C_0
-      __hip_atomic_store(Hw + c, P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(Hw + c, tag | (uint32_t)P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     sP[c] = P;
     sLen[c] = ln;
@@ -68,12 +81,13 @@ __global__ void __launch_bounds__(1024) k_walk_spec(Tables t, const uint16_t* FS
     s_mflag = 0;
     s_mkey = ~0ull;
   }
-  __threadfence();
+  if (tid == 0) __hip_atomic_store(hp + w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  if (tid == 0) __hip_atomic_store(hn + w, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   for (;;) {
     const int r0 = s_r;
+    if (wdbg && tid == 0) d_tw = stamp();
     if (s_lv) {
+      if (wdbg && tid == 0) d_nrs++;
       // restage: uint16 fss rows [P_d, P_d + B) of every chain (as k_rounds_walk)
       constexpr int ITEMS = NPC * B * Q8;
       constexpr int PER = (ITEMS + 1023) / 1024;
@@ -103,12 +117,12 @@ __global__ void __launch_bounds__(1024) k_walk_spec(Tables t, const uint16_t* FS
         sA[tid] = sP[tid] == INF32 ? B : 0;
       }
     }
-    for (int item = tid; item < RB * NPC; item += T) sC[item] = INF32;
     if (tid == 0) {
       s_cur = r0;
       s_wdone = 0;
     }
     __syncthreads();
+    if (wdbg && tid == 0) d_rs += stamp() - d_tw;
     if (tid < 64) {
       // ---- wave 0 walks (the k_rounds_walk step with no known rows)
       const int lane = tid;
@@ -125,7 +139,8 @@ __global__ void __launch_bounds__(1024) k_walk_spec(Tables t, const uint16_t* FS
       int r = r0, st = 0;  // st: 1 merged, 2 end of the graph, 3 history full
       bool lvb = false;
       const int rcap1 = Hcap - 1;
-      const int rend = min(r0 + RB, rcap1);
+      // a segment ends before the ring wraps onto rows not yet published
+      const int rend = min(r0 + RB - 2, rcap1);
       for (;;) {
         if (r >= rend) {
           if (r >= rcap1) st = 3;
@@ -201,7 +216,7 @@ __global__ void __launch_bounds__(1024) k_walk_spec(Tables t, const uint16_t* FS
         if (owner) {
           sP[c] = nxt;
           sA[c] = min(rowA, B);
-          sC[(r - r0) * NPC + c] = nxt;
+          sC[(r + 1) % RB * NPC + c] = nxt;  // ring of rows; the checker waves publish them
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -216,15 +231,15 @@ __global__ void __launch_bounds__(1024) k_walk_spec(Tables t, const uint16_t* FS
           break;
         }
         r++;
-        // the row r is complete in sC: hand it to the checker waves
-        if (lane == 0) __hip_atomic_store(&s_cur, r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // the row r is complete in sC (one wave's LDS writes land in order): hand
+        // it to the checker waves
+        if (lane == 0) __hip_atomic_store(&s_cur, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (lv != 0) {
           lvb = true;
           break;
         }
       }
       if (lane == 0) {
-        s_nr = r - r0 + (st == 2 ? 1 : 0);  // rows r0+1 .. r0+s_nr were produced
         s_r = r;
         s_lv = lvb;
         s_status = st;
@@ -232,41 +247,87 @@ __global__ void __launch_bounds__(1024) k_walk_spec(Tables t, const uint16_t* FS
         __hip_atomic_store(&s_wdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     } else if (tid < 64 + NCHK) {
-      // ---- waves 1-3 look for the walker's newest row among the published rows
-      //      of walkers w+1 .. w+WIN
+      // ---- waves 1-7 look for the walker's newest row among the rows of
+      //      walkers w+1 .. w+WIN (flattened over (walker, row))
       const int ct = tid - 64;
       int checked = r0;
       for (;;) {
+        // acquire: the s_cur load below may not move above it (the final pass must
+        // see the final row)
         const int wd = __hip_atomic_load(&s_wdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const int rr = __hip_atomic_load(&s_cur, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const int rr = __hip_atomic_load(&s_cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (rr > checked) {
+          // publish rows checked+1 .. rr (the walker itself never stores to HBM).
+          // Entry (q, c) belongs to thread (q*N + c) mod NCHK whatever rows the
+          // other checker threads have seen, so every entry is published once.
+          const int g0 = (checked + 1) * N, g1 = (rr + 1) * N;
+          for (int g = g0 + ((ct - g0) % NCHK + NCHK) % NCHK; g < g1; g += NCHK) {
+            const int q = g / N, c = g - q * N;
+            __hip_atomic_store(Hw + (size_t)q * N + c, tag | (uint32_t)sC[q % RB * NPC + c],
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          if (ct == 0) __hip_atomic_store(hp + w, rr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         if (rr > checked &&
             !__hip_atomic_load(&s_mflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-          int sv[NPC];
+          uint64_t sv[NPC];
 #pragma unroll
-          for (int c = 0; c < NPC; c++) sv[c] = sC[(rr - 1 - r0) * NPC + c];
-          for (int k = 1; k <= WIN && w + k < nw; k++) {
-            const int tw = w + k;
-            const int cnt = __hip_atomic_load(hn + tw, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            const int32_t* Ht = H + (size_t)tw * Hcap * N;
-            for (int b = ct; b < cnt; b += NCHK) {
-              const int32_t* row = Ht + (size_t)b * N;
-              bool eq = true;
+          for (int c = 0; c < NPC; c++) sv[c] = tag | (uint32_t)sC[rr % RB * NPC + c];
+          int cnt[WIN];
 #pragma unroll
-              for (int c = 0; c < NPC; c++) {
-                if (c < N && eq)
-                  eq = __hip_atomic_load(row + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == sv[c];
+          for (int k = 0; k < WIN; k++)
+            cnt[k] = w + 1 + k < nw
+                         ? 1 + __hip_atomic_load(hp + w + 1 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                         : 0;
+          // rows of the WIN later walkers flattened: item i -> (walker k, row b);
+          // first columns of up to MAXI items per thread in flight at once, full
+          // rows only for the items whose first column matches
+          constexpr int MAXI = 4;
+          int tot = 0;
+#pragma unroll
+          for (int k = 0; k < WIN; k++) tot += cnt[k];
+          for (int i0 = ct; i0 < tot; i0 += MAXI * NCHK) {
+            int ik[MAXI], ib[MAXI];
+            uint64_t c0[MAXI];
+#pragma unroll
+            for (int m = 0; m < MAXI; m++) {
+              int i = i0 + m * NCHK, k = 0;
+              ik[m] = -1;
+              if (i < tot) {
+                while (i >= cnt[k]) i -= cnt[k++];
+                ik[m] = k + 1;
+                ib[m] = i;
               }
-              if (eq) {
-                atomicMin(&s_mkey, ((unsigned long long)rr << 40) | ((unsigned long long)k << 32) |
-                                       (unsigned long long)b);
-                __hip_atomic_store(&s_mflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+#pragma unroll
+            for (int m = 0; m < MAXI; m++)
+              c0[m] = ik[m] > 0 ? __hip_atomic_load(H + ((size_t)(w + ik[m]) * Hcap + ib[m]) * N,
+                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                : 0;
+#pragma unroll
+            for (int m = 0; m < MAXI; m++) {
+              if (ik[m] > 0 && c0[m] == sv[0]) {
+                const uint64_t* row = H + ((size_t)(w + ik[m]) * Hcap + ib[m]) * N;
+                uint64_t rv[NPC];
+#pragma unroll
+                for (int c = 1; c < NPC; c++)
+                  rv[c] = c < N ? __hip_atomic_load(row + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                : 0;
+                bool eq = true;
+#pragma unroll
+                for (int c = 1; c < NPC; c++) eq = eq && (c >= N || rv[c] == sv[c]);
+                if (eq) {
+                  atomicMin(&s_mkey, ((unsigned long long)rr << 40) |
+                                         ((unsigned long long)ik[m] << 32) | (unsigned long long)ib[m]);
+                  __hip_atomic_store(&s_mflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
               }
             }
           }
           checked = rr;
         }
         if (wd) break;
-        __builtin_amdgcn_s_sleep(2);
+        for (int z = 0; z < nsleep; z++) __builtin_amdgcn_s_sleep(1);
       }
     } else {
       // ---- the other waves pull the rows after every block into L2 (as k_rounds_walk)
@@ -279,21 +340,17 @@ __global__ void __launch_bounds__(1024) k_walk_spec(Tables t, const uint16_t* FS
       }
     }
     __syncthreads();
-    // ---- publish the walked rows (every column, INF included)
-    const int nr = min(s_nr, RB);
-    for (int item = tid; item < nr * NPC; item += T) {
-      const int qq = item / NPC, c = item - qq * NPC;
-      if (c < N)
-        __hip_atomic_store(Hw + (size_t)(r0 + 1 + qq) * N + c, sC[item], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __threadfence();
-    __syncthreads();
-    if (tid == 0)
-      __hip_atomic_store(hn + w, r0 + nr + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     const int fin = s_status;
     if (fin) {
       if (tid == 0) {
+        // rows published: 0..r
+        hn[w] = s_r0_rows(s_r, fin);
+        if (wdbg) {
+          wdbg[4 * w] = stamp() - d_t0;
+          wdbg[4 * w + 1] = d_rs;
+          wdbg[4 * w + 2] = d_nrs;
+          wdbg[4 * w + 3] = s_r;
+        }
         if (fin == 1) {
           const unsigned long long key = s_mkey;
           res[w] = make_int4((int)(key >> 40), w + (int)((key >> 32) & 0xFF),
@@ -309,19 +366,29 @@ __global__ void __launch_bounds__(1024) k_walk_spec(Tables t, const uint16_t* FS
   if (pf == 0x7fffffff && tid == 1 && nw < 0) res[0].x = pf;  // never true: keeps the prefetch
 }
 
-// Follow the merges from walker 0 and copy the true rows into C (one block).
+// Follow the merges from walker 0 and copy the true rows into C.  Every block
+// plans the chain from the walkers' results in LDS (a few hops) and copies a
+// grid-stride share of the rows; block 0 writes the round state.
 // res[w] = {a, t, b, 1}: walker w's row a equals walker t's row b;
 //          {len, -1, -1, 2}: walker w reached the end, rows 0..len-1;
 //          {len, -1, -1, 3}: history full, rows 0..len-1 (the chain ends there).
 // rstate[0] = rounds (complete chain), rstate[1] = 1 if C overflows;
 // *resume = round of the last true row when the sequential walk must go on, else -1.
-__global__ void __launch_bounds__(256) k_walk_join(Tables t, const int32_t* H, const int32_t* hn,
+__global__ void __launch_bounds__(256) k_walk_join(Tables t, const uint64_t* H, const int32_t* hn,
                                                    const int4* res, int nw, int Hcap,
                                                    int32_t* rstate, int32_t* resume) {
-  constexpr int MAXSEG = 128;
+  constexpr int MAXSEG = 128, MAXW = 64;
   __shared__ int s_w[MAXSEG], s_e0[MAXSEG], s_g[MAXSEG], s_n[MAXSEG];
+  __shared__ int4 s_res[MAXW];
+  __shared__ int s_hn[MAXW];
   __shared__ int s_ns, s_ok;
   const int N = t.N;
+  // one parallel load of every walker's result: the chain below is a few LDS hops
+  for (int w = threadIdx.x; w < nw && w < MAXW; w += blockDim.x) {
+    s_res[w] = res[w];
+    s_hn[w] = hn[w];
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
     int wc = 0, e = 0, g = 0, ns = 0, rs_out = -1, R = -1;
     auto emit = [&](int wv, int e0, int e1) {
@@ -335,7 +402,7 @@ __global__ void __launch_bounds__(256) k_walk_join(Tables t, const int32_t* H, c
       }
     };
     for (int it = 0; it <= nw; it++) {
-      const int4 rs = res[wc];
+      const int4 rs = s_res[wc];
       if (rs.w == 1) {
         const int a = rs.x, tw = rs.y, b = rs.z;
         int ne;
@@ -345,7 +412,7 @@ __global__ void __launch_bounds__(256) k_walk_join(Tables t, const int32_t* H, c
         } else {
           ne = b + (e - a);
         }
-        if (ne < hn[tw]) {
+        if (ne < s_hn[tw]) {
           wc = tw;
           e = ne;
           continue;
@@ -363,19 +430,22 @@ __global__ void __launch_bounds__(256) k_walk_join(Tables t, const int32_t* H, c
       break;
     }
     const bool over = g + 1 >= t.Rcap || ns >= MAXSEG;
-    if (over) rstate[1] = 1;
-    else if (R >= 0) rstate[0] = R;
-    *resume = over ? -1 : rs_out;
+    if (blockIdx.x == 0) {
+      if (over) rstate[1] = 1;
+      else if (R >= 0) rstate[0] = R;
+      *resume = over ? -1 : rs_out;
+    }
     s_ns = ns;
     s_ok = !over;
   }
   __syncthreads();
   if (!s_ok) return;
+  const int gt = blockIdx.x * blockDim.x + threadIdx.x, gs = gridDim.x * blockDim.x;
   for (int s = 0; s < s_ns; s++) {
-    const int32_t* src = H + ((size_t)s_w[s] * Hcap + s_e0[s]) * N;
+    const uint64_t* src = H + ((size_t)s_w[s] * Hcap + s_e0[s]) * N;
     int32_t* dst = t.C + (size_t)s_g[s] * N;
     const int cnt = s_n[s] * N;
-    for (int i = threadIdx.x; i < cnt; i += blockDim.x) dst[i] = src[i];
+    for (int i = gt; i < cnt; i += gs) dst[i] = (int32_t)(uint32_t)src[i];
   }
 }
 
