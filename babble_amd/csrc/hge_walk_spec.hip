@@ -270,9 +270,9 @@ __global__ void __launch_bounds__(1024) k_walk_spec(Tables t, const uint16_t* FS
         }
         if (rr > checked &&
             !__hip_atomic_load(&s_mflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-          uint64_t sv[NPC];
-#pragma unroll
-          for (int c = 0; c < NPC; c++) sv[c] = tag | (uint32_t)sC[rr % RB * NPC + c];
+          // the newest row stays in LDS (registers are scarce at 1024 threads)
+          const int* svr = sC + rr % RB * NPC;
+          const uint64_t sv0 = tag | (uint32_t)svr[0];
           int cnt[WIN];
 #pragma unroll
           for (int k = 0; k < WIN; k++)
@@ -282,7 +282,7 @@ __global__ void __launch_bounds__(1024) k_walk_spec(Tables t, const uint16_t* FS
           // rows of the WIN later walkers flattened: item i -> (walker k, row b);
           // first columns of up to MAXI items per thread in flight at once, full
           // rows only for the items whose first column matches
-          constexpr int MAXI = 4;
+          constexpr int MAXI = 2;
           int tot = 0;
 #pragma unroll
           for (int k = 0; k < WIN; k++) tot += cnt[k];
@@ -306,16 +306,13 @@ __global__ void __launch_bounds__(1024) k_walk_spec(Tables t, const uint16_t* FS
                                 : 0;
 #pragma unroll
             for (int m = 0; m < MAXI; m++) {
-              if (ik[m] > 0 && c0[m] == sv[0]) {
+              if (ik[m] > 0 && c0[m] == sv0) {
+                // rare: the first column matches, compare the rest one by one
                 const uint64_t* row = H + ((size_t)(w + ik[m]) * Hcap + ib[m]) * N;
-                uint64_t rv[NPC];
-#pragma unroll
-                for (int c = 1; c < NPC; c++)
-                  rv[c] = c < N ? __hip_atomic_load(row + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                : 0;
                 bool eq = true;
-#pragma unroll
-                for (int c = 1; c < NPC; c++) eq = eq && (c >= N || rv[c] == sv[c]);
+                for (int c = 1; c < N && eq; c++)
+                  eq = __hip_atomic_load(row + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                       (tag | (uint32_t)svr[c]);
                 if (eq) {
                   atomicMin(&s_mkey, ((unsigned long long)rr << 40) |
                                          ((unsigned long long)ik[m] << 32) | (unsigned long long)ib[m]);
