@@ -26,10 +26,14 @@
 
 namespace hge {
 
-// LA[(j, k)] = -1 for the new positions k in [olen_j, len_j) of every chain
-__global__ void k_la_clear(Tables t, const int32_t* olen, const int32_t* len) {
+// LA[(j, k)] = -1 for the new positions k in [olen_j, len_j) of every chain;
+// also zeroes the sweeps' changed flags (zero[0, nzero)) in place of a memset
+__global__ void k_la_clear(Tables t, const int32_t* olen, const int32_t* len, int32_t* zero,
+                           int nzero) {
   const int j = blockIdx.y;
   const int N = t.N;
+  if (j == 0 && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < nzero; i += blockDim.x) zero[i] = 0;
   const int64_t lo = (int64_t)olen[j] * N, hi = (int64_t)len[j] * N;
   int32_t* base = t.LA + (size_t)j * t.ccap * N;
   for (int64_t e = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < hi;

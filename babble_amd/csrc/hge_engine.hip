@@ -850,13 +850,12 @@ struct hge_engine {
     const int32_t* olen = k_len;
     const int32_t* len = k_len + N;
     if (nseg == 0) return;
-    KLAUNCH(k_la_clear, dim3(std::min(64, div_up((int64_t)maxnew * N, 256)), N), dim3(256), 0, st, t,
-            olen, len);
     // sweeps until one changes nothing; queued in groups, checked once per group
-    // (a sweep after a quiet one returns at once)
+    // (a sweep after a quiet one returns at once); k_la_clear zeroes the flags
     const int MAXSW = 4096;
     s_chg.need(MAXSW);
-    HIPCHK(hipMemsetAsync(s_chg.p, 0, 4 * MAXSW, st));
+    KLAUNCH(k_la_clear, dim3(std::max(1, std::min(64, div_up((int64_t)maxnew * N, 256))), N),
+            dim3(256), 0, st, t, olen, len, s_chg.p, MAXSW);
     const int NPt = N <= 16 ? 16 : N <= 32 ? 32 : N <= 64 ? 64 : N <= 128 ? 128 : 256;
     int sw = 0;
     for (int group = 12;; group = 8) {
@@ -1133,10 +1132,11 @@ struct hge_engine {
                 (const int32_t*)nblist, k1, k2, o_ids);
         // new undetermined list (in candidate order)
         scan_large(s_fund.p, s_upos.p, ncand, o_cnt + 1);
-        s_und2.need(ncand);
+        // scatter into the spare list (same capacity) and swap: no device copy
+        s_und2.need(d_und.n);
         KLAUNCH(k_scatter_und, dim3(div_up(ncand, 256)), dim3(256), 0, st, cand, ncand,
                            s_fund.p, s_upos.p, s_und2.p);
-        HIPCHK(hipMemcpyAsync(d_und.p, s_und2.p, 4 * (size_t)ncand, hipMemcpyDeviceToDevice, st));
+        std::swap(d_und, s_und2);
         got_order = true;
       }
     }

@@ -437,12 +437,15 @@ __global__ void __launch_bounds__(256) k_walk_join(Tables t, const uint64_t* H, 
   }
   __syncthreads();
   if (!s_ok) return;
+  // flattened over (row, column): every thread's copies are independent
   const int gt = blockIdx.x * blockDim.x + threadIdx.x, gs = gridDim.x * blockDim.x;
-  for (int s = 0; s < s_ns; s++) {
-    const uint64_t* src = H + ((size_t)s_w[s] * Hcap + s_e0[s]) * N;
-    int32_t* dst = t.C + (size_t)s_g[s] * N;
-    const int cnt = s_n[s] * N;
-    for (int i = gt; i < cnt; i += gs) dst[i] = (int32_t)(uint32_t)src[i];
+  const int ns = s_ns;
+  const int rows = ns > 0 ? s_g[ns - 1] + s_n[ns - 1] : 0;
+  for (int i = gt; i < rows * N; i += gs) {
+    const int q = i / N, c = i - q * N;
+    int sg = 0;
+    while (sg + 1 < ns && s_g[sg + 1] <= q) sg++;
+    t.C[i] = (int32_t)(uint32_t)H[((size_t)s_w[sg] * Hcap + s_e0[sg] + (q - s_g[sg])) * N + c];
   }
 }
 
