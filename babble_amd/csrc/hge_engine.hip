@@ -156,6 +156,10 @@ struct hge_engine {
   uint32_t walk_epoch = 0;
   int walk_chk[2] = {448, 2};        // checker threads, poll pause (HGE_WALK_CHK="n,s")
   bool coop_checked = false;
+  int coop_nb = 0, coop_ncu = 0, coop_spec_nb = -1;
+  DBuf<uint64_t> s_cH, s_cS, s_cT, s_cM;  // speculative wide walk: rows, ssc bits, tables, merges
+  DBuf<int32_t> s_cn;
+  uint32_t coop_epoch = 0;
 
   hipEvent_t ev[8] = {};
   // per-kernel HIP-event timing on the engine stream (hge_set_profiling)
@@ -323,6 +327,11 @@ struct hge_engine {
     d_opcp.free_();
     d_ssc.free_();
     s_gran.free_();
+    s_cH.free_();
+    s_cS.free_();
+    s_cT.free_();
+    s_cM.free_();
+    s_cn.free_();
     if (pin) (void)hipHostFree(pin);
     pin = nullptr;
     pin_cap = pin_used = 0;
@@ -650,7 +659,7 @@ struct hge_engine {
       t = tables();
       const int NP = (N + 15) & ~15;
       if (N > 32) {
-        rounds_coop();
+        rounds_coop(fresh);
       } else {
         // first-strong-seer rows for every event that can still be a frontier member
         // (from a fresh state the frontier starts at round 0, position 0: no round trip)
@@ -802,7 +811,24 @@ struct hge_engine {
   }
 
   // rounds of a wide hashgraph: cooperative frontier kernel (hge_rounds_coop.hip)
-  void rounds_coop() {
+  // Speculative walkers of the wide walk (fresh state): as many N-workgroup
+  // walkers as stay co-resident, up to 8; HGE_COOP_WALKERS overrides (read per
+  // call: the tests vary it; 0 or 1 = the sequential kernel alone).
+  int coop_walkers() {
+    if (coop_spec_nb < 0)
+      HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&coop_spec_nb, (const void*)k_rounds_coop_spec,
+                                                          256, 0));
+    const int cap = (int)std::min<int64_t>(16, (int64_t)coop_spec_nb * coop_ncu / N);
+    int minlen = INT32_MAX;
+    for (int c = 0; c < N; c++) minlen = std::min(minlen, chain_len[c]);
+    const char* ev = getenv("HGE_COOP_WALKERS");
+    int nw = ev ? atoi(ev) : (minlen >= 1024 ? 8 : 0);
+    nw = std::min(nw, cap);
+    return nw >= 2 ? nw : 0;
+  }
+
+  // rounds of a wide hashgraph: cooperative frontier kernel (hge_rounds_coop.hip)
+  void rounds_coop(bool fresh) {
     Tables t = tables();
     s_fst.need(N + 1);
     KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p);
@@ -817,6 +843,8 @@ struct hge_engine {
       HIPCHK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device));
       if (!coop || (int64_t)nb * ncu < N)
         throw EngineError(HGE_ERR_DEVICE, "cooperative rounds kernel cannot be co-resident");
+      coop_nb = nb;
+      coop_ncu = ncu;
       coop_checked = true;
     }
     int maxlen = 0;
@@ -831,8 +859,59 @@ struct hge_engine {
     const int32_t* olen = k_len;
     const int32_t* len = k_len + N;
     int32_t* rstate = k_rs;
-    uint64_t* gran = s_gran.p;
     int32_t* err = s_bar.p + 1;
+    const int nw = (fresh && rlo == 0 && Rprev == 0) ? coop_walkers() : 0;
+    if (nw >= 2) {
+      const char* hc = getenv("HGE_WALK_HCAP");  // tests: force the capacity fallback
+      const int Hcap = hc ? std::max(2, std::min(0xFFFF, atoi(hc)))
+                          : std::min(0xFFFF, std::min(Rcap, std::max(256, 3 * (Rcap / nw) + 256)));
+      int TS = 64;
+      while (TS < 2 * Hcap) TS <<= 1;
+      const size_t nh = (size_t)nw * Hcap * N, nt = (size_t)nw * TS;
+      const size_t hn0 = s_cH.n, tn0 = s_cT.n;  // a new allocation holds arbitrary words
+      s_cH.need(nh);
+      s_cT.need(nt);
+      bool clear = s_cH.n != hn0 || s_cT.n != tn0;
+      if (++coop_epoch >= 0x7FFFFFFFu) {  // tags wrap: clear, restart at 1
+        coop_epoch = 1;
+        clear = true;
+      }
+      if (clear) {
+        HIPCHK(hipMemsetAsync(s_cH.p, 0, s_cH.n * sizeof(uint64_t), st));
+        HIPCHK(hipMemsetAsync(s_cT.p, 0, s_cT.n * sizeof(uint64_t), st));
+      }
+      s_cS.need(nh * NW);
+      s_cM.need(nw);
+      s_cn.need(2 * (size_t)nw + 1);
+      HIPCHK(hipMemsetAsync(s_cM.p, 0xFF, (size_t)nw * sizeof(uint64_t), st));
+      CoopSpec sp{s_cH.p, s_cS.p, s_cT.p, (unsigned long long*)s_cM.p, s_cn.p, nw, Hcap, TS,
+                  coop_epoch};
+      void* sargs[] = {&t, &FDT, &olen, &len, &sp, &err};
+      prof_begin("k_rounds_coop_spec");
+      HIPCHK(hipLaunchCooperativeKernel((const void*)k_rounds_coop_spec, dim3(nw * N), dim3(256), sargs,
+                                        0, st));
+      prof_end();
+      int32_t* resume = s_cn.p + 2 * nw;
+      KLAUNCH(k_coop_join, dim3(64), dim3(256), 0, st, t, sp, d_ssc.p, rstate, resume);
+      int32_t hres[2] = {0, 0};
+      readback(&hres[0], err, 1);
+      if (hres[0]) throw EngineError(HGE_ERR_DEVICE, "rounds frontier hand-off timed out");
+      readback(&hres[1], resume, 1);
+      if (getenv("HGE_WALK_DEBUG")) {
+        std::vector<int32_t> hn(2 * nw);
+        std::vector<uint64_t> mg(nw);
+        readback(hn.data(), s_cn.p, hn.size());
+        readback(mg.data(), s_cM.p, mg.size());
+        fprintf(stderr, "coop walk: nw=%d Hcap=%d resume=%d |", nw, Hcap, hres[1]);
+        for (int w = 0; w < nw; w++)
+          fprintf(stderr, " %d:%d%s->(%d,%d)", w, hn[w], hn[nw + w] ? "e" : "",
+                  mg[w] == ~0ull ? -1 : (int)(mg[w] >> 32), mg[w] == ~0ull ? -1 : (int)(uint32_t)mg[w]);
+        fprintf(stderr, "\n");
+      }
+      if (hres[1] < 0) return;
+      rlo = hres[1];
+    }
+    uint64_t* gran = s_gran.p;
     uint64_t* ssc = d_ssc.p;
     uint64_t* dbg = dbg_p();
     void* args[] = {&t, &FDT, &olen, &len, &rstate, &rlo, &Rprev, &gran, &err, &ssc, &dbg};
