@@ -884,8 +884,14 @@ struct hge_engine {
       s_cM.need(nw);
       s_cn.need(2 * (size_t)nw + 1);
       HIPCHK(hipMemsetAsync(s_cM.p, 0xFF, (size_t)nw * sizeof(uint64_t), st));
+      int64_t nev = 0;
+      for (int c = 0; c < N; c++) nev += chain_len[c];
+      // guesses (measured over seeds 1-3, profiles/r01p_*): time cuts at N <= 64,
+      // alternating length/time cuts above
+      const char* ge = getenv("HGE_COOP_GUESS");
+      const int guess = ge ? atoi(ge) : (N <= 64 ? 1 : 2);
       CoopSpec sp{s_cH.p, s_cS.p, s_cT.p, (unsigned long long*)s_cM.p, s_cn.p, nw, Hcap, TS,
-                  coop_epoch};
+                  coop_epoch, nev, guess};
       void* sargs[] = {&t, &FDT, &olen, &len, &sp, &err};
       prof_begin("k_rounds_coop_spec");
       HIPCHK(hipLaunchCooperativeKernel((const void*)k_rounds_coop_spec, dim3(nw * N), dim3(256), sargs,
@@ -904,8 +910,9 @@ struct hge_engine {
         readback(mg.data(), s_cM.p, mg.size());
         fprintf(stderr, "coop walk: nw=%d Hcap=%d resume=%d |", nw, Hcap, hres[1]);
         for (int w = 0; w < nw; w++)
-          fprintf(stderr, " %d:%d%s->(%d,%d)", w, hn[w], hn[nw + w] ? "e" : "",
-                  mg[w] == ~0ull ? -1 : (int)(mg[w] >> 32), mg[w] == ~0ull ? -1 : (int)(uint32_t)mg[w]);
+          fprintf(stderr, " %d:%d%s->(%d,w%d:%d)", w, hn[w], hn[nw + w] ? "e" : "",
+                  mg[w] == ~0ull ? -1 : (int)(mg[w] >> 32),
+                  mg[w] == ~0ull ? -1 : w + (int)((mg[w] >> 16) & 0xFFFF), (int)(mg[w] & 0xFFFF));
         fprintf(stderr, "\n");
       }
       if (hres[1] < 0) return;

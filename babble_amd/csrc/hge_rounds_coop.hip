@@ -401,10 +401,13 @@ struct CoopSpec {
   uint64_t* H;          // [nw][Hcap][N] tagged rows
   uint64_t* SSCH;       // [nw][Hcap][N][NW] strongly-see bits of row j vs row j-1
   uint64_t* TT;         // [nw][TS] hash -> row: (tag << 32) | (hash16 << 16) | row
-  unsigned long long* mrg;  // [nw] min over hits of (row << 32) | row of walker w+1
+  unsigned long long* mrg;  // [nw] min over hits of (row << 32) | (walker offset << 16) | row there
   int32_t* hn;          // [2 nw]: rows written (incl. the terminal row), natural end flag
   int nw, Hcap, TS;
   uint32_t epoch;       // 1 .. 2^31-1, new per launch
+  int64_t events;       // events inserted (time-cut guesses)
+  int guess;            // walker w >= 1 starts at: 0 = len_c * w / nw on every chain,
+                        // 1 = the time cut events * w / nw, 2 = 0 for odd w, 1 for even w
 };
 
 __device__ __forceinline__ uint64_t coop_mix(uint64_t z) {
@@ -414,7 +417,7 @@ __device__ __forceinline__ uint64_t coop_mix(uint64_t z) {
   return z ^ (z >> 31);
 }
 
-__global__ void __launch_bounds__(256) k_rounds_coop_spec(Tables t, const int32_t* FDT,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_rounds_coop_spec(Tables t, const int32_t* FDT,
                                                           const int32_t* olen, const int32_t* len,
                                                           CoopSpec sp, int32_t* err) {
   __shared__ CoopLDS L;
@@ -423,9 +426,6 @@ __global__ void __launch_bounds__(256) k_rounds_coop_spec(Tables t, const int32_
   const int lenc = len[c];
   const uint32_t ep = sp.epoch;
   gu64_t* Hw = (gu64_t*)(sp.H + (size_t)w * sp.Hcap * N);
-  const bool checker = w + 1 < sp.nw;
-  gu64_t* Hn = checker ? (gu64_t*)(sp.H + (size_t)(w + 1) * sp.Hcap * N) : nullptr;
-  gu64_t* Tn = checker ? (gu64_t*)(sp.TT + (size_t)(w + 1) * sp.TS) : nullptr;
   gu64_t* Tw = (gu64_t*)(sp.TT + (size_t)w * sp.TS);
   if (tid < N) {
     const int ld = len[tid];
@@ -433,8 +433,20 @@ __global__ void __launch_bounds__(256) k_rounds_coop_spec(Tables t, const int32_
     if (w == 0) {
       P = t.C[tid];
       if (olen[tid] == 0 && ld > 0) P = 0;
-    } else {
+    } else if (sp.guess == 0 || (sp.guess == 2 && (w & 1))) {
       P = ld > 0 ? (int)((int64_t)ld * w / sp.nw) : INF32;
+    } else {
+      // time cut: the first event of chain tid inserted at or after T (ids are
+      // insertion order, increasing along a chain); none = an ended chain
+      const int64_t T = sp.events * w / sp.nw;
+      const int32_t* ch = t.chain + (size_t)tid * t.ccap;
+      int lo = 0, hi = ld;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((int64_t)ch[mid] < T) lo = mid + 1;
+        else hi = mid;
+      }
+      P = lo < ld ? lo : INF32;
     }
     L.sP[tid] = P;
     if (tid == c)
@@ -530,8 +542,13 @@ __global__ void __launch_bounds__(256) k_rounds_coop_spec(Tables t, const int32_
         break;
       }
     }
-    // merge test against walker w+1 (one probe window of 64 slots)
-    if (checker && tid < 64) {
+    // merge test: against walker w+1 every step, w+2 and w+3 on alternate
+    // steps (a guessed walker can follow a trajectory that never meets the
+    // true one); one probe window of 64 slots
+    const int toff = (j & 1) ? 1 : ((j & 2) ? 2 : 3);
+    if (tid < 64 && w + toff < sp.nw) {
+      gu64_t* Tn = (gu64_t*)(sp.TT + (size_t)(w + toff) * sp.TS);
+      gu64_t* Hn = (gu64_t*)(sp.H + (size_t)(w + toff) * sp.Hcap * N);
       const uint32_t mask = (uint32_t)sp.TS - 1;
       const unsigned long long x =
           __hip_atomic_load(Tn + (((uint32_t)h + tid) & mask), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -554,7 +571,7 @@ __global__ void __launch_bounds__(256) k_rounds_coop_spec(Tables t, const int32_
       }
       if (tid == 0 && hit >= 0) {
         L.s_hit = 1;
-        atomicMin(sp.mrg + w, ((unsigned long long)(j + 1) << 32) | (uint32_t)hit);
+        atomicMin(sp.mrg + w, ((unsigned long long)(j + 1) << 32) | ((uint32_t)toff << 16) | (uint32_t)hit);
       }
     }
     __syncthreads();
@@ -574,14 +591,14 @@ __global__ void __launch_bounds__(256) k_coop_join(Tables t, CoopSpec sp, uint64
   if (threadIdx.x == 0) {
     int n = 0, v = 0, s = 0, G = 0, res = -1, R = -1;
     for (int it = 0; it < 4 * sp.nw + 4 && n < MS; it++) {
-      const unsigned long long m = v + 1 < sp.nw ? sp.mrg[v] : ~0ull;
+      const unsigned long long m = sp.mrg[v];
       const int hn = sp.hn[v];
       if (m != ~0ull) {
-        const int r = (int)(m >> 32), b = (int)(uint32_t)m;
-        if (s >= r) {  // row s of v is row b + s - r of v+1
+        const int r = (int)(m >> 32), b = (int)(m & 0xFFFF), v2 = v + (int)((m >> 16) & 0xFFFF);
+        if (s >= r) {  // row s of v is row b + s - r of v2
           const int s2 = b + (s - r);
-          if (s2 < sp.hn[v + 1] - (sp.hn[sp.nw + v + 1] ? 1 : 0)) {
-            v++;
+          if (s2 < sp.hn[v2] - (sp.hn[sp.nw + v2] ? 1 : 0)) {
+            v = v2;
             s = s2;
             continue;
           }
@@ -591,7 +608,7 @@ __global__ void __launch_bounds__(256) k_coop_join(Tables t, CoopSpec sp, uint64
         }
         sv[n] = v; ss[n] = s; se[n] = r; sG[n] = G; sE2[n] = r; n++;
         G += r - s;
-        v++;
+        v = v2;
         s = b;
         continue;
       }
