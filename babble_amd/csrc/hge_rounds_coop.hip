@@ -53,7 +53,8 @@ typedef __attribute__((address_space(1))) unsigned long long gu64_t;
 struct CoopLDS {
   int sP[256];                 // the frontier C_r (one position per chain)
   uint32_t sU[256 * 33];       // sU[d][ii] as uint16 pairs: member rows, CW columns
-  uint32_t sH[256 * 33];       // sH[d][b/2]: per-thread histograms, two 16-bit bins per word
+  uint32_t sH[32 * 256];       // sH[b/2][d]: per-member histograms, two 16-bit bins per word
+                               // (bin-major: a half-wave of members never shares a bank)
   uint32_t sH2[64];
   uint16_t sW[64][64];         // FDT window per column i: positions [wb_i, wb_i + WIN)
   int sWb[64];
@@ -67,7 +68,15 @@ struct CoopLDS {
 // (INF32 for threads that hold no member).  The result is a function of
 // L.sP alone, which is what lets speculative walkers merge (below).
 __device__ __forceinline__ int coop_select(const Tables& t, const int32_t* FDT, int c, int lenc,
-                                           CoopLDS& L, int& fss_out) {
+                                           CoopLDS& L, int& fss_out, uint64_t* sacc = nullptr) {
+  // HGE_STAMPS: cycles per section into sacc[4..7] (loads, pack, windows, gathers), sacc[8] (select)
+  uint64_t su = sacc ? stamp() : 0;
+#define SSUB(k)                          \
+  if (sacc) {                            \
+    const uint64_t now_ = stamp();       \
+    sacc[(k)] += now_ - su;              \
+    su = now_;                           \
+  }
   constexpr int NB = 64;  // histogram bins (window above C_r[c])
   constexpr int CW = 64;  // member-row columns staged per chunk
   constexpr int RS = 33;  // LDS row stride in words (odd: conflict-free per-thread rows)
@@ -83,11 +92,12 @@ __device__ __forceinline__ int coop_select(const Tables& t, const int32_t* FDT, 
   const int Pd = (d < N) ? L.sP[d] : INF32;
   const bool dact = d < N && Pd != INF32 && Pc != INF32;
   if (lead)
-    for (int w = 0; w < NB / 2; w++) L.sH[d * RS + w] = 0;
+    for (int w = 0; w < NB / 2; w++) L.sH[w * 256 + d] = 0;
   if (tid < NB) L.sH2[tid] = 0;
   for (int i0 = 0; i0 < N; i0 += CW) {
     const int ni = min(CW, N - i0);
     __syncthreads();
+    SSUB(8);
     // member rows FD[(dd, C_r[dd])][i0, i0 + CW): 4 ints per load, coalesced
     constexpr int Q = CW / 4;
     constexpr int PER = 256 * Q / 256;  // N <= 256 rows
@@ -111,6 +121,7 @@ __device__ __forceinline__ int coop_select(const Tables& t, const int32_t* FDT, 
     }
     if (tid < CW) L.sWb[tid] = INF32;
     __syncthreads();
+    SSUB(4);
     // pack to uint16 and take the per-column minimum (window base): lanes
     // l, l+16, l+32, l+48 of a wave hold the same 4 columns
     int4 mn = make_int4(INF32, INF32, INF32, INF32);
@@ -147,6 +158,7 @@ __device__ __forceinline__ int coop_select(const Tables& t, const int32_t* FDT, 
       if (mn.w != INF32) atomicMin(&L.sWb[4 * q + 3], mn.w);
     }
     __syncthreads();
+    SSUB(5);
     // FDT windows: column i's member values sit just above their minimum
     const int32_t* fdt = FDT + ((size_t)c * N + i0) * t.ccap;
     {
@@ -170,6 +182,7 @@ __device__ __forceinline__ int coop_select(const Tables& t, const int32_t* FDT, 
     // effective window base (clamped inside the table; INF32 = no window)
     if (tid < CW && L.sWb[tid] != INF32) L.sWb[tid] = min(L.sWb[tid], t.ccap - WIN);
     __syncthreads();
+    SSUB(6);
     if (dact) {
       // branch-free: all LDS reads of a batch issue back to back, window
       // misses become predicated global loads, empty values add 0.  Part p
@@ -191,6 +204,13 @@ __device__ __forceinline__ int coop_select(const Tables& t, const int32_t* FDT, 
           wv[k] = L.sW[ii][inw ? off : 0];
           if (!inw) wv[k] = -1;
         }
+        if (sacc) {  // HGE_STAMPS: batches of wave 0, and those with a window miss
+          bool miss = false;
+#pragma unroll
+          for (int k = 0; k < KB; k++) miss |= uu[k] != 0xFFFF && wv[k] < 0;
+          sacc[10] += 1;
+          sacc[9] += __ballot(miss) ? 1 : 0;
+        }
 #pragma unroll
         for (int k = 0; k < KB; k++) {
           const bool need = uu[k] != 0xFFFF && wv[k] < 0;
@@ -202,18 +222,19 @@ __device__ __forceinline__ int coop_select(const Tables& t, const int32_t* FDT, 
           if (uu[k] == 0xFFFF) v = INF32;
           const bool fin = v != INF32;
           const int b = fin ? min(max(v - Pc, 0), NB - 1) : 0;
-          atomicAdd(&L.sH[d * RS + (b >> 1)], fin ? (1u << ((b & 1) * 16)) : 0u);
+          atomicAdd(&L.sH[(b >> 1) * 256 + d], fin ? (1u << ((b & 1) * 16)) : 0u);
         }
       }
     }
   }
   __syncthreads();
+  SSUB(7);
   // first level: fss_c(m_d) = SM-th smallest gathered value (branch-free bin scan)
   int fss = INF32;
   if (dact && lead) {
     uint32_t hw[NB / 2];
 #pragma unroll
-    for (int w = 0; w < NB / 2; w++) hw[w] = L.sH[d * RS + w];
+    for (int w = 0; w < NB / 2; w++) hw[w] = L.sH[w * 256 + d];
     int cum = 0, b = NB;
 #pragma unroll
     for (int w = 0; w < NB / 2; w++) {
@@ -279,6 +300,8 @@ __device__ __forceinline__ int coop_select(const Tables& t, const int32_t* FDT, 
     if (tid == 0) L.s_sel = lo < lenc ? lo : INF32;
     __syncthreads();
   }
+  SSUB(8);
+#undef SSUB
   fss_out = fss_raw;
   return L.s_sel;
 }
@@ -289,7 +312,7 @@ __global__ void __launch_bounds__(256) k_rounds_coop(Tables t, const int32_t* FD
                                                      int Rprev, uint64_t* gran, int32_t* err,
                                                      uint64_t* ssc, uint64_t* dbg) {
   // HGE_STAMPS diagnostics (workgroup 0, thread 0): cycles per section
-  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_t = 0;
+  uint64_t st_acc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_t = 0;
 #define CSTAMP(k)                                              \
   if (dbg && blockIdx.x == 0 && threadIdx.x == 0) {            \
     const uint64_t now_ = stamp();        \
@@ -315,7 +338,7 @@ __global__ void __launch_bounds__(256) k_rounds_coop(Tables t, const int32_t* FD
     }
     CSTAMP(0);
     int fss_raw;
-    coop_select(t, FDT, c, lenc, L, fss_raw);
+    coop_select(t, FDT, c, lenc, L, fss_raw, (dbg && blockIdx.x == 0 && tid == 0) ? st_acc : nullptr);
     CSTAMP(2);
     if (tid == 0) {
       const int Pc = L.sP[c];
@@ -377,7 +400,7 @@ __global__ void __launch_bounds__(256) k_rounds_coop(Tables t, const int32_t* FD
     }
   }
   if (dbg && blockIdx.x == 0 && threadIdx.x == 0)
-    for (int q = 0; q < 8; q++) dbg[q] += st_acc[q];
+    for (int q = 0; q < 11; q++) dbg[q] += st_acc[q];
 #undef CSTAMP
 }
 
