@@ -811,9 +811,9 @@ struct hge_engine {
   }
 
   // rounds of a wide hashgraph: cooperative frontier kernel (hge_rounds_coop.hip)
-  // Speculative walkers of the wide walk (fresh state): as many N-workgroup
-  // walkers as stay co-resident, up to 8; HGE_COOP_WALKERS overrides (read per
-  // call: the tests vary it; 0 or 1 = the sequential kernel alone).
+  // Speculative walkers of the wide walk (fresh state, N <= 128): as many
+  // N-workgroup walkers as stay co-resident, up to 8; HGE_COOP_WALKERS overrides
+  // (read per call: the tests vary it; 0 or 1 = the sequential kernel alone).
   int coop_walkers() {
     if (coop_spec_nb < 0)
       HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&coop_spec_nb, (const void*)k_rounds_coop_spec,
@@ -822,7 +822,9 @@ struct hge_engine {
     int minlen = INT32_MAX;
     for (int c = 0; c < N; c++) minlen = std::min(minlen, chain_len[c]);
     const char* ev = getenv("HGE_COOP_WALKERS");
-    int nw = ev ? atoi(ev) : (minlen >= 1024 ? 8 : 0);
+    // above N = 128 only 2 walkers fit, and the 512-thread sequential kernel is faster
+    // than 2 walkers sharing each CU (22.5 vs 33.6 ms at 256/2M, profiles/r01r_*)
+    int nw = ev ? atoi(ev) : (minlen >= 1024 && N <= 128 ? 8 : 0);
     nw = std::min(nw, cap);
     return nw >= 2 ? nw : 0;
   }
@@ -838,7 +840,7 @@ struct hge_engine {
     int Rprev = R;
     if (!coop_checked) {
       int nb = 0, ncu = 0, coop = 0;
-      HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_rounds_coop, 256, 0));
+      HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_rounds_coop, COOP_BS, 0));
       HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
       HIPCHK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device));
       if (!coop || (int64_t)nb * ncu < N)
@@ -923,7 +925,7 @@ struct hge_engine {
     uint64_t* dbg = dbg_p();
     void* args[] = {&t, &FDT, &olen, &len, &rstate, &rlo, &Rprev, &gran, &err, &ssc, &dbg};
     prof_begin("k_rounds_coop");
-    HIPCHK(hipLaunchCooperativeKernel((const void*)k_rounds_coop, dim3(N), dim3(256), args, 0, st));
+    HIPCHK(hipLaunchCooperativeKernel((const void*)k_rounds_coop, dim3(N), dim3(COOP_BS), args, 0, st));
     prof_end();
     int32_t e = 0;
     readback(&e, s_bar.p + 1, 1);

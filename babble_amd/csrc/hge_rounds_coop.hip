@@ -67,6 +67,7 @@ struct CoopLDS {
 // (valid in thread 0) and, per thread, fss_c(m_d) before the own-chain clamp
 // (INF32 for threads that hold no member).  The result is a function of
 // L.sP alone, which is what lets speculative walkers merge (below).
+template <int BS>
 __device__ __forceinline__ int coop_select(const Tables& t, const int32_t* FDT, int c, int lenc,
                                            CoopLDS& L, int& fss_out, uint64_t* sacc = nullptr) {
   // HGE_STAMPS: cycles per section into sacc[4..7] (loads, pack, windows, gathers), sacc[8] (select)
@@ -84,9 +85,9 @@ __device__ __forceinline__ int coop_select(const Tables& t, const int32_t* FDT, 
   const int N = t.N, SM = t.SM;
   const int tid = threadIdx.x;
   const int Pc = L.sP[c];
-  // thread = (member d, part): TPM = 256 / NPOW threads share member d's columns
+  // thread = (member d, part): TPM = BS / NPOW threads share member d's columns
   const int NPOW = N <= 64 ? 64 : N <= 128 ? 128 : 256;
-  const int TPM = 256 / NPOW;
+  const int TPM = BS / NPOW;
   const int d = tid & (NPOW - 1), part = tid / NPOW;
   const bool lead = part == 0;
   const int Pd = (d < N) ? L.sP[d] : INF32;
@@ -100,11 +101,11 @@ __device__ __forceinline__ int coop_select(const Tables& t, const int32_t* FDT, 
     SSUB(8);
     // member rows FD[(dd, C_r[dd])][i0, i0 + CW): 4 ints per load, coalesced
     constexpr int Q = CW / 4;
-    constexpr int PER = 256 * Q / 256;  // N <= 256 rows
+    constexpr int PER = 256 * Q / BS;  // N <= 256 rows
     int4 vv[PER];
 #pragma unroll
     for (int m = 0; m < PER; m++) {
-      const int item = tid + m * 256;
+      const int item = tid + m * BS;
       const int dd = item / Q, q = item - (item / Q) * Q;
       vv[m] = make_int4(INF32, INF32, INF32, INF32);
       if (dd < N && L.sP[dd] != INF32 && 4 * q < ni) {
@@ -127,7 +128,7 @@ __device__ __forceinline__ int coop_select(const Tables& t, const int32_t* FDT, 
     int4 mn = make_int4(INF32, INF32, INF32, INF32);
 #pragma unroll
     for (int m = 0; m < PER; m++) {
-      const int item = tid + m * 256;
+      const int item = tid + m * BS;
       const int dd = item / Q, q = item - (item / Q) * Q;
       if (dd < N) {
         const int4 w = vv[m];
@@ -162,18 +163,18 @@ __device__ __forceinline__ int coop_select(const Tables& t, const int32_t* FDT, 
     // FDT windows: column i's member values sit just above their minimum
     const int32_t* fdt = FDT + ((size_t)c * N + i0) * t.ccap;
     {
-      constexpr int WPER = CW * WIN / 256;
+      constexpr int WPER = CW * WIN / BS;
       int wv[WPER];
 #pragma unroll
       for (int m = 0; m < WPER; m++) {
-        const int item = tid + m * 256;
+        const int item = tid + m * BS;
         const int ii = item / WIN, k = item - (item / WIN) * WIN;
         const int wb = min(L.sWb[ii], t.ccap - WIN);
         wv[m] = (ii < ni && L.sWb[ii] != INF32) ? fdt[(size_t)ii * t.ccap + wb + k] : INF32;
       }
 #pragma unroll
       for (int m = 0; m < WPER; m++) {
-        const int item = tid + m * 256;
+        const int item = tid + m * BS;
         const int ii = item / WIN, k = item - (item / WIN) * WIN;
         L.sW[ii][k] = (wv[m] == INF32) ? 0xFFFF : (uint16_t)wv[m];
       }
@@ -307,7 +308,9 @@ __device__ __forceinline__ int coop_select(const Tables& t, const int32_t* FDT, 
 }
 
 
-__global__ void __launch_bounds__(256) k_rounds_coop(Tables t, const int32_t* FDT, const int32_t* olen,
+// 512 threads: two waves per SIMD (the gather loop is issue/latency-bound at one)
+constexpr int COOP_BS = 512;
+__global__ void __launch_bounds__(COOP_BS) k_rounds_coop(Tables t, const int32_t* FDT, const int32_t* olen,
                                                      const int32_t* len, int32_t* rstate, int rlo,
                                                      int Rprev, uint64_t* gran, int32_t* err,
                                                      uint64_t* ssc, uint64_t* dbg) {
@@ -338,7 +341,7 @@ __global__ void __launch_bounds__(256) k_rounds_coop(Tables t, const int32_t* FD
     }
     CSTAMP(0);
     int fss_raw;
-    coop_select(t, FDT, c, lenc, L, fss_raw, (dbg && blockIdx.x == 0 && tid == 0) ? st_acc : nullptr);
+    coop_select<COOP_BS>(t, FDT, c, lenc, L, fss_raw, (dbg && blockIdx.x == 0 && tid == 0) ? st_acc : nullptr);
     CSTAMP(2);
     if (tid == 0) {
       const int Pc = L.sP[c];
@@ -487,7 +490,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       break;
     }
     int fss_raw;
-    coop_select(t, FDT, c, lenc, L, fss_raw);
+    coop_select<256>(t, FDT, c, lenc, L, fss_raw);
     if (tid == 0) {
       const int Pc = L.sP[c];
       const int nxt = (Pc != INF32 && L.s_sel < lenc) ? L.s_sel : INF32;
