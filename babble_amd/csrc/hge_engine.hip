@@ -817,7 +817,7 @@ struct hge_engine {
   int coop_walkers() {
     if (coop_spec_nb < 0)
       HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&coop_spec_nb, (const void*)k_rounds_coop_spec,
-                                                          256, 0));
+                                                          COOP_SPEC_BS, 0));
     const int cap = (int)std::min<int64_t>(16, (int64_t)coop_spec_nb * coop_ncu / N);
     int minlen = INT32_MAX;
     for (int c = 0; c < N; c++) minlen = std::min(minlen, chain_len[c]);
@@ -896,7 +896,7 @@ struct hge_engine {
                   coop_epoch, nev, guess};
       void* sargs[] = {&t, &FDT, &olen, &len, &sp, &err};
       prof_begin("k_rounds_coop_spec");
-      HIPCHK(hipLaunchCooperativeKernel((const void*)k_rounds_coop_spec, dim3(nw * N), dim3(256), sargs,
+      HIPCHK(hipLaunchCooperativeKernel((const void*)k_rounds_coop_spec, dim3(nw * N), dim3(COOP_SPEC_BS), sargs,
                                         0, st));
       prof_end();
       int32_t* resume = s_cn.p + 2 * nw;

@@ -67,7 +67,7 @@ struct CoopLDS {
 // (valid in thread 0) and, per thread, fss_c(m_d) before the own-chain clamp
 // (INF32 for threads that hold no member).  The result is a function of
 // L.sP alone, which is what lets speculative walkers merge (below).
-template <int BS>
+template <int BS, int KB>
 __device__ __forceinline__ int coop_select(const Tables& t, const int32_t* FDT, int c, int lenc,
                                            CoopLDS& L, int& fss_out, uint64_t* sacc = nullptr) {
   // HGE_STAMPS: cycles per section into sacc[4..7] (loads, pack, windows, gathers), sacc[8] (select)
@@ -189,7 +189,6 @@ __device__ __forceinline__ int coop_select(const Tables& t, const int32_t* FDT, 
       // misses become predicated global loads, empty values add 0.  Part p
       // of member d takes columns ii = p + TPM * k.
       const uint16_t* myu = (const uint16_t*)(L.sU + d * RS);
-      constexpr int KB = 16;
       for (int ib = part; ib < ni; ib += KB * TPM) {
         int uu[KB], wv[KB], gv[KB];
 #pragma unroll
@@ -308,14 +307,18 @@ __device__ __forceinline__ int coop_select(const Tables& t, const int32_t* FDT, 
 }
 
 
-// 512 threads: two waves per SIMD (the gather loop is issue/latency-bound at one)
-constexpr int COOP_BS = 512;
+// 1024 threads: four waves per SIMD (the gather loop is issue/latency-bound at
+// one); gather batches of 8 columns keep it within 128 VGPRs
+constexpr int COOP_BS = 1024;
+constexpr int COOP_SPEC_BS = 512;  // walkers: 512 threads, 2 per CU
 __global__ void __launch_bounds__(COOP_BS) k_rounds_coop(Tables t, const int32_t* FDT, const int32_t* olen,
                                                      const int32_t* len, int32_t* rstate, int rlo,
                                                      int Rprev, uint64_t* gran, int32_t* err,
                                                      uint64_t* ssc, uint64_t* dbg) {
   // HGE_STAMPS diagnostics (workgroup 0, thread 0): cycles per section
-  uint64_t st_acc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_t = 0;
+  __shared__ uint64_t st_acc[11];  // thread 0 only: kept out of every lane's registers
+  uint64_t st_t = 0;
+  if (threadIdx.x < 11) st_acc[threadIdx.x] = 0;
 #define CSTAMP(k)                                              \
   if (dbg && blockIdx.x == 0 && threadIdx.x == 0) {            \
     const uint64_t now_ = stamp();        \
@@ -341,7 +344,7 @@ __global__ void __launch_bounds__(COOP_BS) k_rounds_coop(Tables t, const int32_t
     }
     CSTAMP(0);
     int fss_raw;
-    coop_select<COOP_BS>(t, FDT, c, lenc, L, fss_raw, (dbg && blockIdx.x == 0 && tid == 0) ? st_acc : nullptr);
+    coop_select<COOP_BS, 8>(t, FDT, c, lenc, L, fss_raw, (dbg && blockIdx.x == 0 && tid == 0) ? st_acc : nullptr);
     CSTAMP(2);
     if (tid == 0) {
       const int Pc = L.sP[c];
@@ -443,7 +446,7 @@ __device__ __forceinline__ uint64_t coop_mix(uint64_t z) {
   return z ^ (z >> 31);
 }
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_rounds_coop_spec(Tables t, const int32_t* FDT,
+__global__ void __launch_bounds__(COOP_SPEC_BS) __attribute__((amdgpu_waves_per_eu(4, 4))) k_rounds_coop_spec(Tables t, const int32_t* FDT,
                                                           const int32_t* olen, const int32_t* len,
                                                           CoopSpec sp, int32_t* err) {
   __shared__ CoopLDS L;
@@ -490,7 +493,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       break;
     }
     int fss_raw;
-    coop_select<256>(t, FDT, c, lenc, L, fss_raw);
+    coop_select<COOP_SPEC_BS, 8>(t, FDT, c, lenc, L, fss_raw);
     if (tid == 0) {
       const int Pc = L.sP[c];
       const int nxt = (Pc != INF32 && L.s_sel < lenc) ? L.s_sel : INF32;
