@@ -132,6 +132,7 @@ struct hge_engine {
   DBuf<uint8_t> d_coin, d_wit;
   DBuf<int32_t> d_chain, d_LA, d_FD, d_FSS;
   DBuf<int2> d_opcp;  // [N][ccap] other-parent coordinates (k_chain_fill)
+  DBuf<int64_t> d_tsch;  // [N][ccap] timestamps in chain layout (k_chain_fill)
   DBuf<int32_t> d_C, d_W, d_rcnt, d_minw;
   DBuf<uint64_t> d_ssb, d_seeb;
   DBuf<uint8_t> d_fame;
@@ -204,6 +205,7 @@ struct hge_engine {
     t.ntx = d_ntx.p;
     t.chain = d_chain.p;
     t.opcp = d_opcp.p;
+    t.tsch = d_tsch.p;
     t.LA = d_LA.p;
     t.FD = d_FD.p;
     t.round = d_round.p;
@@ -325,6 +327,7 @@ struct hge_engine {
     s_keys.free_();
     s_keys2.free_();
     d_opcp.free_();
+    d_tsch.free_();
     d_ssc.free_();
     s_gran.free_();
     s_cH.free_();
@@ -395,6 +398,15 @@ struct hge_engine {
     d_opcp.free_();
     d_opcp.p = opcp;
     d_opcp.n = (size_t)N * nc;
+    int64_t* tsch = nullptr;
+    HIPCHK(hipMalloc(&tsch, sizeof(int64_t) * N * nc));
+    if (ccap > 0)
+      HIPCHK(hipMemcpy2DAsync(tsch, sizeof(int64_t) * nc, d_tsch.p, sizeof(int64_t) * ccap,
+                              sizeof(int64_t) * ccap, N, hipMemcpyDeviceToDevice, st));
+    sync();
+    d_tsch.free_();
+    d_tsch.p = tsch;
+    d_tsch.n = (size_t)N * nc;
     grow_chain_table(d_LA, nc, true);
     grow_chain_table(d_FD, nc, true);
     // first-strong-seer rows (N <= 32): int32 rows of N, or uint16 rows padded to

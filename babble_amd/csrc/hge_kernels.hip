@@ -36,6 +36,7 @@ struct Tables {
   const int32_t* ntx;
   int32_t* chain;
   int2* opcp;     // [N][ccap]: (creator, index) of the other-parent, (-1, -1) if none
+  int64_t* tsch;  // [N][ccap]: timestamp of the event at (chain, position)
   int32_t* LA;
   int32_t* FD;
   int32_t* round;
@@ -135,6 +136,7 @@ __global__ void k_chain_fill(Tables t, int n0, int n1) {
   if (x >= n1) return;
   const size_t at = (size_t)t.creator[x] * t.ccap + t.index[x];
   t.chain[at] = x;
+  t.tsch[at] = t.ts[x];
   const int o = t.op[x];
   t.opcp[at] = o >= 0 ? make_int2(t.creator[o], t.index[o]) : make_int2(-1, -1);
 }
@@ -1444,8 +1446,8 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
     if (d < N && ((seg_fws[(size_t)sg * NW + (d >> 6)] >> (d & 63)) & 1ull)) {
       const int w = t.W[(size_t)rr * N + d];
       if (t.LA[rowoff(t, d, t.index[w]) + cx] >= ix) {
-        const int osa = t.chain[(size_t)d * t.ccap + fdx[d]];
-        v[k] = (uint64_t)t.ts[osa] ^ 0x8000000000000000ull;
+        // ts of OSA(w, x) = the event at (d, FD[x][d]): one gather, not chain then ts
+        v[k] = (uint64_t)t.tsch[(size_t)d * t.ccap + fdx[d]] ^ 0x8000000000000000ull;
         in[k] = true;
       }
     }
