@@ -1444,8 +1444,10 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
     in[k] = false;
     v[k] = ~0ull;
     if (d < N && ((seg_fws[(size_t)sg * NW + (d >> 6)] >> (d & 63)) & 1ull)) {
-      const int w = t.W[(size_t)rr * N + d];
-      if (t.LA[rowoff(t, d, t.index[w]) + cx] >= ix) {
+      // the witness of round rr on chain d is the first event there with round >= rr,
+      // i.e. position C[rr][d]: a coalesced load instead of W then index[w]
+      const int pw = t.C[(size_t)rr * N + d];
+      if (t.LA[rowoff(t, d, pw) + cx] >= ix) {
         // ts of OSA(w, x) = the event at (d, FD[x][d]): one gather, not chain then ts
         v[k] = (uint64_t)t.tsch[(size_t)d * t.ccap + fdx[d]] ^ 0x8000000000000000ull;
         in[k] = true;
