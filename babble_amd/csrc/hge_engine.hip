@@ -157,7 +157,10 @@ struct hge_engine {
   uint32_t walk_epoch = 0;
   int walk_chk[2] = {448, 2};        // checker threads, poll pause (HGE_WALK_CHK="n,s")
   bool coop_checked = false;
-  int coop_nb = 0, coop_ncu = 0, coop_spec_nb = -1;
+  int coop_nb = 0, coop_ncu = 0, coop_spec_nb = -1, coop_spec_bs = 0;
+  const void* coop_spec_fn() const {
+    return coop_spec_bs == 1024 ? (const void*)k_rounds_coop_spec<1024> : (const void*)k_rounds_coop_spec<512>;
+  }
   DBuf<uint64_t> s_cH, s_cS, s_cT, s_cM;  // speculative wide walk: rows, ssc bits, tables, merges
   DBuf<int32_t> s_cn;
   uint32_t coop_epoch = 0;
@@ -827,9 +830,15 @@ struct hge_engine {
   // N-workgroup walkers as stay co-resident, up to 8; HGE_COOP_WALKERS overrides
   // (read per call: the tests vary it; 0 or 1 = the sequential kernel alone).
   int coop_walkers() {
-    if (coop_spec_nb < 0)
-      HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&coop_spec_nb, (const void*)k_rounds_coop_spec,
-                                                          COOP_SPEC_BS, 0));
+    // walker block size (HGE_COOP_SPEC_BS): 512 threads x 2 per CU at N <= 64, 1024 x 1
+    // above (means over seeds 1-3, profiles/r01v_specbs: 113.3 vs 106.4M ev/s at 64/1M,
+    // 60.8 vs 62.9M at 128/1M)
+    const char* bs = getenv("HGE_COOP_SPEC_BS");
+    const int sbs = bs ? (atoi(bs) == 1024 ? 1024 : 512) : (N > 64 ? 1024 : COOP_SPEC_BS);
+    if (sbs != coop_spec_bs) {
+      coop_spec_bs = sbs;
+      HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&coop_spec_nb, coop_spec_fn(), sbs, 0));
+    }
     const int cap = (int)std::min<int64_t>(16, (int64_t)coop_spec_nb * coop_ncu / N);
     int minlen = INT32_MAX;
     for (int c = 0; c < N; c++) minlen = std::min(minlen, chain_len[c]);
@@ -908,7 +917,7 @@ struct hge_engine {
                   coop_epoch, nev, guess};
       void* sargs[] = {&t, &FDT, &olen, &len, &sp, &err};
       prof_begin("k_rounds_coop_spec");
-      HIPCHK(hipLaunchCooperativeKernel((const void*)k_rounds_coop_spec, dim3(nw * N), dim3(COOP_SPEC_BS), sargs,
+      HIPCHK(hipLaunchCooperativeKernel(coop_spec_fn(), dim3(nw * N), dim3(coop_spec_bs), sargs,
                                         0, st));
       prof_end();
       int32_t* resume = s_cn.p + 2 * nw;

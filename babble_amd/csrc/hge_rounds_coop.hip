@@ -310,7 +310,7 @@ __device__ __forceinline__ int coop_select(const Tables& t, const int32_t* FDT, 
 // 1024 threads: four waves per SIMD (the gather loop is issue/latency-bound at
 // one); gather batches of 8 columns keep it within 128 VGPRs
 constexpr int COOP_BS = 1024;
-constexpr int COOP_SPEC_BS = 512;  // walkers: 512 threads, 2 per CU
+constexpr int COOP_SPEC_BS = 512;  // walkers: 512 threads, 2 per CU (1024 = 1 per CU, HGE_COOP_SPEC_BS)
 __global__ void __launch_bounds__(COOP_BS) k_rounds_coop(Tables t, const int32_t* FDT, const int32_t* olen,
                                                      const int32_t* len, int32_t* rstate, int rlo,
                                                      int Rprev, uint64_t* gran, int32_t* err,
@@ -446,7 +446,8 @@ __device__ __forceinline__ uint64_t coop_mix(uint64_t z) {
   return z ^ (z >> 31);
 }
 
-__global__ void __launch_bounds__(COOP_SPEC_BS) __attribute__((amdgpu_waves_per_eu(4, 4))) k_rounds_coop_spec(Tables t, const int32_t* FDT,
+template <int BS>
+__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4, 4))) k_rounds_coop_spec(Tables t, const int32_t* FDT,
                                                           const int32_t* olen, const int32_t* len,
                                                           CoopSpec sp, int32_t* err) {
   __shared__ CoopLDS L;
@@ -493,7 +494,7 @@ __global__ void __launch_bounds__(COOP_SPEC_BS) __attribute__((amdgpu_waves_per_
       break;
     }
     int fss_raw;
-    coop_select<COOP_SPEC_BS, 8>(t, FDT, c, lenc, L, fss_raw);
+    coop_select<BS, 8>(t, FDT, c, lenc, L, fss_raw);
     if (tid == 0) {
       const int Pc = L.sP[c];
       const int nxt = (Pc != INF32 && L.s_sel < lenc) ? L.s_sel : INF32;
@@ -691,5 +692,10 @@ __global__ void __launch_bounds__(256) k_coop_join(Tables t, CoopSpec sp, uint64
     }
   }
 }
+
+template __global__ void k_rounds_coop_spec<512>(Tables, const int32_t*, const int32_t*, const int32_t*,
+                                                 CoopSpec, int32_t*);
+template __global__ void k_rounds_coop_spec<1024>(Tables, const int32_t*, const int32_t*, const int32_t*,
+                                                  CoopSpec, int32_t*);
 
 }  // namespace hge
