@@ -113,6 +113,10 @@ struct hge_engine {
   std::vector<int32_t> h_lens;      // staging for the chain-length upload
 
   int R = 0;                // Store.Rounds()
+  int R_set = 0;            // rounds recorded by hge_set_round (Store.SetRound)
+  std::vector<std::vector<int32_t>> h_chain;  // participantEventsCache: ids per creator
+  int64_t cache_size = 0;   // Store.CacheSize() for the rolling views (0 = unbounded)
+  int32_t chain_limit = INT32_MAX;  // longest chain the rounds kernels take (admission)
   int lcr = -1;             // LastConsensusRound (-1 nil)
   int lcre = 0;             // LastCommitedRoundEvents
   int64_t ctx = 0;          // ConsensusTransactions
@@ -233,6 +237,11 @@ struct hge_engine {
     for (auto& e : ev) HIPCHK(hipEventCreate(&e));
     chain_len.assign(N, 0);
     chain_last.assign(N, -1);
+    h_chain.assign(N, {});
+    // the wide rounds kernels keep chain positions as uint16 (hge_rounds_coop.hip):
+    // longer chains are refused at admission so the engine stays usable
+    chain_limit = N > 32 ? 0xFFFE : INT32_MAX;
+    if (const char* cl = getenv("HGE_CHAIN_LIMIT")) chain_limit = std::max(1, std::min(chain_limit, atoi(cl)));
     coords_len.assign(N, 0);
     // chain tables: a creator's chain is ~cap/N long (binomial, sd ~ sqrt(cap/N));
     // rounds: a round spans >= ~4N events in gossip.  Both grow on demand.
@@ -450,9 +459,11 @@ struct hge_engine {
     h_coin.clear();
     chain_len.assign(N, 0);
     chain_last.assign(N, -1);
+    h_chain.assign(N, {});
     coords_len.assign(N, 0);
     n_events = n_dev = n_coords = n_divided = 0;
     R = 0;
+    R_set = 0;
     h_minw.clear();
     lcr = -1;
     lcre = 0;
@@ -507,6 +518,11 @@ struct hge_engine {
       err = "Event index does not match the creator's chain position";
       return HGE_ERR_INDEX;
     }
+    if (known >= chain_limit) {
+      err = "Chain capacity exceeded: the wide rounds kernels take at most " +
+            std::to_string(chain_limit) + " events per creator";
+      return HGE_ERR_CAPACITY;
+    }
     return HGE_OK;
   }
 
@@ -524,6 +540,7 @@ struct hge_engine {
       h_S.push_back(v);
     }
     h_coin.push_back(e.hash[16] != 0 ? 1 : 0);
+    h_chain[e.creator].push_back((int32_t)id);
     chain_len[e.creator]++;
     chain_last[e.creator] = (int32_t)id;
   }
@@ -850,6 +867,19 @@ struct hge_engine {
     return nw >= 2 ? nw : 0;
   }
 
+  // Launch of a grid whose workgroups hand data to each other (the frontier
+  // kernels).  Co-residency is checked once with the occupancy API
+  // (coop_checked, coop_walkers); a plain launch of such a grid gets the same
+  // residency as a cooperative one (MI355X_MICROARCH.md, Residency), and
+  // hipLaunchCooperativeKernel puts the work on a separate device queue whose
+  // teardown at process exit crashed under rocprofv3 (profiles/r02_exit_segv.md).
+  // HGE_COOP_LAUNCH=1 restores the cooperative launch.
+  hipError_t launch_resident(const void* fn, dim3 grid, dim3 block, void** args) {
+    static const bool coop = getenv("HGE_COOP_LAUNCH") && atoi(getenv("HGE_COOP_LAUNCH")) == 1;
+    if (coop) return hipLaunchCooperativeKernel(fn, grid, block, args, 0, st);
+    return hipLaunchKernel(fn, grid, block, args, 0, st);
+  }
+
   // rounds of a wide hashgraph: cooperative frontier kernel (hge_rounds_coop.hip)
   void rounds_coop(bool fresh) {
     Tables t = tables();
@@ -917,8 +947,7 @@ struct hge_engine {
                   coop_epoch, nev, guess};
       void* sargs[] = {&t, &FDT, &olen, &len, &sp, &err};
       prof_begin("k_rounds_coop_spec");
-      HIPCHK(hipLaunchCooperativeKernel(coop_spec_fn(), dim3(nw * N), dim3(coop_spec_bs), sargs,
-                                        0, st));
+      HIPCHK(launch_resident(coop_spec_fn(), dim3(nw * N), dim3(coop_spec_bs), sargs));
       prof_end();
       int32_t* resume = s_cn.p + 2 * nw;
       KLAUNCH(k_coop_join, dim3(64), dim3(256), 0, st, t, sp, d_ssc.p, rstate, resume);
@@ -946,7 +975,7 @@ struct hge_engine {
     uint64_t* dbg = dbg_p();
     void* args[] = {&t, &FDT, &olen, &len, &rstate, &rlo, &Rprev, &gran, &err, &ssc, &dbg};
     prof_begin("k_rounds_coop");
-    HIPCHK(hipLaunchCooperativeKernel((const void*)k_rounds_coop, dim3(N), dim3(COOP_BS), args, 0, st));
+    HIPCHK(launch_resident((const void*)k_rounds_coop, dim3(N), dim3(COOP_BS), args));
     prof_end();
     int32_t e = 0;
     readback(&e, s_bar.p + 1, 1);
@@ -1531,6 +1560,17 @@ int hge_run_consensus(hge_engine* h, int32_t* ids_out, int64_t cap, int64_t* n_o
 int hge_replay_prepare(hge_engine* h, const hge_event* ev, int64_t n_sub,
                        const int64_t* call_points, int64_t n_calls, int32_t* status_out) {
   GUARD_BEGIN
+  if (n_sub < 0 || (n_sub > 0 && !ev) || n_calls < 0 || (n_calls > 0 && !call_points)) {
+    h->err = "hge_replay_prepare: bad argument";
+    return HGE_ERR_ARG;
+  }
+  // call points: strictly ascending submission counts in [1, n_sub]
+  for (int64_t c = 0; c < n_calls; c++) {
+    if (call_points[c] < 1 || call_points[c] > n_sub || (c > 0 && call_points[c] <= call_points[c - 1])) {
+      h->err = "hge_replay_prepare: call points must be strictly ascending within [1, n_sub]";
+      return HGE_ERR_ARG;
+    }
+  }
   h->reset_state();
   std::vector<int32_t> idmap(n_sub, -1);
   h->replay_calls.clear();
@@ -1628,15 +1668,27 @@ int hge_replay(hge_engine* h, const hge_event* ev, int64_t n_sub, const int64_t*
 
 int64_t hge_event_count(hge_engine* h) { return h->n_events; }
 int32_t hge_participants(hge_engine* h) { return h->N; }
-int32_t hge_rounds(hge_engine* h) { return h->R_div; }
+int32_t hge_rounds(hge_engine* h) { return std::max(h->R_div, h->R_set); }
 int32_t hge_last_consensus_round(hge_engine* h) { return h->lcr; }
 int32_t hge_last_committed_round_events(hge_engine* h) { return h->lcre; }
 int64_t hge_consensus_transactions(hge_engine* h) { return h->ctx; }
 int64_t hge_consensus_count(hge_engine* h) { return (int64_t)h->consensus.size(); }
+// RollingList window (common/rolling_list.go:55-67): Add rolls the list back to
+// its last `size` items once it holds 2*size, so after `tot` adds it holds
+static int64_t window_len(int64_t tot, int64_t size) {
+  if (size <= 0 || tot <= 2 * size) return tot;
+  return size + (tot - 2 * size - 1) % size + 1;
+}
 int64_t hge_consensus_events(hge_engine* h, int32_t* ids_out, int64_t cap) {
-  for (int64_t i = 0; i < (int64_t)h->consensus.size() && i < cap && ids_out; i++)
-    ids_out[i] = h->consensus[i];
-  return (int64_t)h->consensus.size();
+  const int64_t tot = (int64_t)h->consensus.size(), w = window_len(tot, h->cache_size);
+  for (int64_t i = 0; i < w && i < cap && ids_out; i++) ids_out[i] = h->consensus[tot - w + i];
+  return w;
+}
+int64_t hge_consensus_log(hge_engine* h, int64_t from, int32_t* ids_out, int64_t cap) {
+  const int64_t tot = (int64_t)h->consensus.size();
+  if (from < 0) from = 0;
+  for (int64_t i = from; i < tot && i - from < cap && ids_out; i++) ids_out[i - from] = h->consensus[i];
+  return std::max<int64_t>(0, tot - from);
 }
 int64_t hge_undetermined(hge_engine* h, int32_t* ids_out, int64_t cap) {
   try {
@@ -1784,6 +1836,177 @@ int32_t hge_oldest_self_ancestor_to_see(hge_engine* h, int32_t x, int32_t y) {
     }
   }
   return -1;
+}
+
+// ---- Store semantics and sync-path reads ----------------------------------
+int hge_set_cache_size(hge_engine* h, int64_t size) {
+  if (!h || size < 0) return HGE_ERR_ARG;
+  h->cache_size = size;
+  return HGE_OK;
+}
+int64_t hge_cache_size(hge_engine* h) { return h->cache_size; }
+
+int hge_participant_events(hge_engine* h, int32_t creator, int64_t skip, int32_t* ids_out,
+                           int64_t cap, int64_t* n_out) {
+  if (n_out) *n_out = 0;
+  if (creator < 0 || creator >= h->N) {
+    h->err = "not found";
+    return HGE_ERR_NOT_FOUND;
+  }
+  const std::vector<int32_t>& ch = h->h_chain[creator];
+  const int64_t tot = (int64_t)ch.size();
+  if (skip >= tot) return HGE_OK;
+  const int64_t oldest = tot - window_len(tot, h->cache_size);
+  if (skip < oldest) {
+    h->err = "too late";
+    return HGE_ERR_TOO_LATE;
+  }
+  if (skip < 0) skip = 0;
+  for (int64_t k = skip; k < tot && k - skip < cap && ids_out; k++) ids_out[k - skip] = ch[k];
+  if (n_out) *n_out = tot - skip;
+  return HGE_OK;
+}
+
+int32_t hge_participant_event(hge_engine* h, int32_t creator, int64_t index) {
+  if (creator < 0 || creator >= h->N || index < 0) return HGE_ERR_NOT_FOUND;
+  const std::vector<int32_t>& ch = h->h_chain[creator];
+  const int64_t tot = (int64_t)ch.size();
+  if (index < tot - window_len(tot, h->cache_size)) return HGE_ERR_TOO_LATE;
+  if (index >= tot) return HGE_ERR_NOT_FOUND;
+  return ch[index];
+}
+
+int32_t hge_last_from(hge_engine* h, int32_t creator) {
+  if (creator < 0 || creator >= h->N) return HGE_ERR_NOT_FOUND;
+  return h->chain_last[creator];
+}
+
+int hge_diff(hge_engine* h, const int32_t* known, int32_t* ids_out, int64_t cap, int64_t* n_out) {
+  if (n_out) *n_out = 0;
+  if (!known) return HGE_ERR_ARG;
+  std::vector<int32_t> ids;
+  for (int c = 0; c < h->N; c++) {
+    const std::vector<int32_t>& ch = h->h_chain[c];
+    const int64_t tot = (int64_t)ch.size(), skip = known[c];
+    if (skip >= tot) continue;
+    if (skip < tot - window_len(tot, h->cache_size)) {
+      h->err = "too late";
+      return HGE_ERR_TOO_LATE;
+    }
+    for (int64_t k = std::max<int64_t>(skip, 0); k < tot; k++) ids.push_back(ch[k]);
+  }
+  std::sort(ids.begin(), ids.end());  // ByTopologicalOrder: ids are insertion order
+  for (int64_t i = 0; i < (int64_t)ids.size() && i < cap && ids_out; i++) ids_out[i] = ids[i];
+  if (n_out) *n_out = (int64_t)ids.size();
+  return HGE_OK;
+}
+
+int hge_wire_info(hge_engine* h, int32_t id, int32_t* out) {
+  if (id < 0 || id >= h->n_events || !out) return HGE_ERR_ARG;
+  const int32_t sp = h->h_sp[id], op = h->h_op[id];
+  out[0] = sp >= 0 ? h->h_index[sp] : -1;
+  out[1] = op >= 0 ? h->h_creator[op] : -1;
+  out[2] = op >= 0 ? h->h_index[op] : -1;
+  out[3] = h->h_creator[id];
+  return HGE_OK;
+}
+
+int hge_read_wire_parents(hge_engine* h, int32_t creator_id, int32_t self_parent_index,
+                          int32_t other_parent_creator_id, int32_t other_parent_index,
+                          int32_t* sp_out, int32_t* op_out) {
+  if (creator_id < 0 || creator_id >= h->N) return HGE_ERR_NOT_FOUND;
+  int32_t sp = HGE_NONE, op = HGE_NONE;
+  if (self_parent_index >= 0) {
+    sp = hge_participant_event(h, creator_id, self_parent_index);
+    if (sp < 0) return sp;
+  }
+  if (other_parent_index >= 0) {
+    op = hge_participant_event(h, other_parent_creator_id, other_parent_index);
+    if (op < 0) return op;
+  }
+  if (sp_out) *sp_out = sp;
+  if (op_out) *op_out = op;
+  return HGE_OK;
+}
+
+// ---- bulk state reads ------------------------------------------------------
+int hge_event_rounds(hge_engine* h, int32_t* round_out, uint8_t* witness_out, int64_t cap) {
+  GUARD_BEGIN
+  h->coords();
+  const int64_t m = std::min<int64_t>(cap, h->n_events);
+  if (m > 0 && round_out) h->d2h(round_out, h->d_round.p, 4 * (size_t)m);
+  if (m > 0 && witness_out) h->d2h(witness_out, h->d_wit.p, (size_t)m);
+  h->sync();
+  return HGE_OK;
+  GUARD_END(h)
+}
+
+int hge_event_received(hge_engine* h, int32_t* rr_out, int64_t* cts_out, int64_t cap) {
+  GUARD_BEGIN
+  const int64_t m = std::min<int64_t>(cap, h->n_events);
+  if (m > 0 && rr_out) h->d2h(rr_out, h->d_rr.p, 4 * (size_t)m);
+  if (m > 0 && cts_out) h->d2h(cts_out, h->d_cts.p, 8 * (size_t)m);
+  h->sync();
+  return HGE_OK;
+  GUARD_END(h)
+}
+
+// ---- round predicates (hashgraph.go:211-326) --------------------------------
+int32_t hge_parent_round(hge_engine* h, int32_t x) {
+  if (x < 0 || x >= h->n_events) return -1;
+  const int32_t sp = h->h_sp[x], op = h->h_op[x];
+  if (sp < 0 && op < 0) return 0;
+  if (sp < 0 || op < 0) return 0;  // a missing parent (GetEvent error) reads as 0
+  const int32_t a = hge_round_of(h, sp), b = hge_round_of(h, op);
+  return std::max(a, b);
+}
+
+int32_t hge_round_inc(hge_engine* h, int32_t x) {
+  if (x < 0 || x >= h->n_events) return 0;
+  const int32_t pr = hge_parent_round(h, x);
+  if (pr < 0 || hge_rounds(h) < pr + 1) return 0;
+  try {
+    h->coords();
+    if (pr >= h->Rcap) return 0;
+    std::vector<int32_t> w(h->N);
+    h->readback(w.data(), h->d_W.p + (size_t)pr * h->N, h->N);
+    int c = 0;
+    for (int i = 0; i < h->N; i++)
+      if (w[i] >= 0 && w[i] < h->n_events) c += hge_strongly_see(h, x, w[i]);
+    return c >= h->SM ? 1 : 0;
+  } catch (EngineError& e) {
+    h->err = e.msg;
+    return 0;
+  }
+}
+
+int hge_round_diff(hge_engine* h, int32_t x, int32_t y, int32_t* out) {
+  if (x < 0 || x >= h->n_events || y < 0 || y >= h->n_events || !out) return HGE_ERR_ARG;
+  const int32_t a = hge_round_of(h, x), b = hge_round_of(h, y);
+  if (a < 0 || b < 0) return HGE_ERR_INTERNAL;
+  *out = a - b;
+  return HGE_OK;
+}
+
+int hge_set_round(hge_engine* h, int32_t round, const int32_t* ids, const uint8_t* witness,
+                  const uint8_t* fame, int32_t n) {
+  GUARD_BEGIN
+  if (round < 0 || n < 0 || (n > 0 && !ids)) return HGE_ERR_ARG;
+  h->coords();
+  h->ensure_rcap((int64_t)round + 1);
+  for (int32_t i = 0; i < n; i++) {
+    const int32_t x = ids[i];
+    if (x < 0 || x >= h->n_events) return HGE_ERR_ARG;
+    if (witness && !witness[i]) continue;
+    const size_t slot = (size_t)round * h->N + h->h_creator[x];
+    h->h2d(h->d_W.p + slot, &ids[i], 4);
+    const uint8_t f = fame ? fame[i] : 0;
+    h->h2d(h->d_fame.p + slot, &f, 1);
+    h->sync();
+  }
+  h->R_set = std::max(h->R_set, round + 1);
+  return HGE_OK;
+  GUARD_END(h)
 }
 
 int hge_set_profiling(hge_engine* h, int on) {

@@ -25,7 +25,13 @@ ERRORS = {
     -4: "Other-parent not known",
     -5: "Self-parent not last known event by creator",
     -6: "Event index does not match the creator's chain position",
+    -7: "Chain capacity exceeded",
+    -11: "too late",
+    -12: "not found",
 }
+HGE_ERR_CAPACITY = -7
+HGE_ERR_TOO_LATE = -11
+HGE_ERR_NOT_FOUND = -12
 
 
 class HgeEvent(ctypes.Structure):
@@ -61,15 +67,23 @@ EXPORTS = [
     "hge_ancestor", "hge_self_ancestor", "hge_see", "hge_strongly_see",
     "hge_oldest_self_ancestor_to_see", "hge_coordinates", "hge_coordinate_sweeps", "hge_stage_times",
     "hge_set_profiling", "hge_reset_kernel_stats", "hge_kernel_stats",
+    "hge_consensus_log", "hge_event_rounds", "hge_event_received", "hge_set_cache_size",
+    "hge_cache_size", "hge_participant_events", "hge_participant_event", "hge_last_from",
+    "hge_diff", "hge_wire_info", "hge_read_wire_parents", "hge_parent_round", "hge_round_inc",
+    "hge_round_diff", "hge_set_round",
 ]
 
 _lib = None
 
 
 class HgeError(RuntimeError):
-    def __init__(self, code, msg):
+    """A negative hge_status.  `accepted` holds the ids the engine assigned
+    before the failing event of an insert batch (they stay inserted)."""
+
+    def __init__(self, code, msg, accepted=None):
         super().__init__(f"{msg} (hge status {code})")
         self.code = code
+        self.accepted = accepted
 
 
 def lib():
@@ -121,6 +135,27 @@ def lib():
     L.hge_stage_times.argtypes = [vp, P(ctypes.c_float), ctypes.c_int]
     L.hge_coordinate_sweeps.restype = ctypes.c_int32
     L.hge_coordinate_sweeps.argtypes = [vp]
+    L.hge_consensus_log.argtypes = [vp, i64, P(i32), i64]
+    L.hge_consensus_log.restype = i64
+    L.hge_event_rounds.argtypes = [vp, P(i32), P(ctypes.c_uint8), i64]
+    L.hge_event_received.argtypes = [vp, P(i32), P(i64), i64]
+    L.hge_set_cache_size.argtypes = [vp, i64]
+    L.hge_cache_size.argtypes = [vp]
+    L.hge_cache_size.restype = i64
+    L.hge_participant_events.argtypes = [vp, i32, i64, P(i32), i64, P(i64)]
+    L.hge_participant_event.argtypes = [vp, i32, i64]
+    L.hge_participant_event.restype = i32
+    L.hge_last_from.argtypes = [vp, i32]
+    L.hge_last_from.restype = i32
+    L.hge_diff.argtypes = [vp, P(i32), P(i32), i64, P(i64)]
+    L.hge_wire_info.argtypes = [vp, i32, P(i32)]
+    L.hge_read_wire_parents.argtypes = [vp, i32, i32, i32, i32, P(i32), P(i32)]
+    L.hge_parent_round.argtypes = [vp, i32]
+    L.hge_parent_round.restype = i32
+    L.hge_round_inc.argtypes = [vp, i32]
+    L.hge_round_inc.restype = i32
+    L.hge_round_diff.argtypes = [vp, i32, i32, P(i32)]
+    L.hge_set_round.argtypes = [vp, i32, P(i32), P(ctypes.c_uint8), P(ctypes.c_uint8), i32]
     L.hge_set_profiling.argtypes = [vp, ctypes.c_int]
     L.hge_reset_kernel_stats.argtypes = [vp]
     L.hge_kernel_stats.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
@@ -184,13 +219,14 @@ class Engine:
     # --- ingest ----------------------------------------------------------
     def insert_events(self, ev):
         """InsertEvent for each record (stops at the first rejection, like Core.Sync).
-        Returns the assigned ids; raises HgeError on the first rejected event."""
+        Returns the assigned ids; on the first rejected event raises HgeError
+        whose `accepted` holds the ids of the events inserted before it."""
         ev = np.ascontiguousarray(ev, EVENT_DTYPE)
         status = np.zeros(len(ev), np.int32)
         acc = ctypes.c_int64()
         rc = self.L.hge_insert_events(self.h, ev.ctypes.data, len(ev), _p32(status), ctypes.byref(acc))
         if rc != 0:
-            raise HgeError(rc, self.L.hge_last_error(self.h).decode())
+            raise HgeError(rc, self.L.hge_last_error(self.h).decode(), accepted=status[:acc.value].copy())
         return status[:acc.value]
 
     def insert(self, creator, index, sp, op, ts, S=b"\0" * 32, hash32=b"\1" * 32, ntx=0):
@@ -295,7 +331,9 @@ class Engine:
         return self.L.hge_consensus_transactions(self.h)
 
     def consensus_events(self):
-        m = self.L.hge_consensus_count(self.h)
+        """Store.ConsensusEvents: the rolling window (the whole list when the
+        cache size is 0, the default)."""
+        m = self.L.hge_consensus_events(self.h, None, 0)
         out = np.zeros(max(1, m), np.int32)
         self.L.hge_consensus_events(self.h, _p32(out), m)
         return out[:m]
@@ -352,6 +390,100 @@ class Engine:
     def oldest_self_ancestor_to_see(self, x, y):
         r = self.L.hge_oldest_self_ancestor_to_see(self.h, x, y)
         return None if r < 0 else r
+
+    # --- bulk reads ------------------------------------------------------
+    def event_rounds(self):
+        """(round, witness) of every event (DivideRounds state)."""
+        m = self.event_count()
+        r = np.zeros(max(m, 1), np.int32)
+        w = np.zeros(max(m, 1), np.uint8)
+        self._check(self.L.hge_event_rounds(self.h, _p32(r), w.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), m))
+        return r[:m], w[:m].astype(bool)
+
+    def event_received(self):
+        """(roundReceived (-1 nil), consensus timestamp) of every event."""
+        m = self.event_count()
+        rr = np.zeros(max(m, 1), np.int32)
+        cts = np.zeros(max(m, 1), np.int64)
+        self._check(self.L.hge_event_received(self.h, _p32(rr), _p64(cts), m))
+        return rr[:m], cts[:m]
+
+    def consensus_log(self, start=0):
+        m = self.L.hge_consensus_log(self.h, start, None, 0)
+        out = np.zeros(max(m, 1), np.int32)
+        self.L.hge_consensus_log(self.h, start, _p32(out), m)
+        return out[:m]
+
+    # --- Store semantics / sync path ---------------------------------------
+    def set_cache_size(self, size):
+        self._check(self.L.hge_set_cache_size(self.h, size))
+
+    def participant_events(self, creator, skip):
+        """Store.ParticipantEvents: ids from position `skip` (HgeError -11 = ErrTooLate)."""
+        n = ctypes.c_int64()
+        rc = self.L.hge_participant_events(self.h, creator, skip, None, 0, ctypes.byref(n))
+        if rc != 0:
+            raise HgeError(rc, self.L.hge_last_error(self.h).decode())
+        out = np.zeros(max(n.value, 1), np.int32)
+        self._check(self.L.hge_participant_events(self.h, creator, skip, _p32(out), n.value, ctypes.byref(n)))
+        return out[:n.value]
+
+    def participant_event(self, creator, index):
+        r = self.L.hge_participant_event(self.h, creator, index)
+        if r < 0:
+            raise HgeError(r, ERRORS.get(r, "error"))
+        return r
+
+    def last_from(self, creator):
+        r = self.L.hge_last_from(self.h, creator)
+        if r < -1:
+            raise HgeError(r, ERRORS.get(r, "error"))
+        return None if r == -1 else r
+
+    def diff(self, known):
+        known = np.ascontiguousarray(known, np.int32)
+        n = ctypes.c_int64()
+        rc = self.L.hge_diff(self.h, _p32(known), None, 0, ctypes.byref(n))
+        if rc != 0:
+            raise HgeError(rc, self.L.hge_last_error(self.h).decode())
+        out = np.zeros(max(n.value, 1), np.int32)
+        self._check(self.L.hge_diff(self.h, _p32(known), _p32(out), n.value, ctypes.byref(n)))
+        return out[:n.value]
+
+    def wire_info(self, x):
+        out = np.zeros(4, np.int32)
+        self._check(self.L.hge_wire_info(self.h, x, _p32(out)))
+        return tuple(int(v) for v in out)
+
+    def read_wire_parents(self, creator_id, sp_index, op_creator_id, op_index):
+        sp = ctypes.c_int32()
+        op = ctypes.c_int32()
+        rc = self.L.hge_read_wire_parents(self.h, creator_id, sp_index, op_creator_id, op_index,
+                                          ctypes.byref(sp), ctypes.byref(op))
+        if rc != 0:
+            raise HgeError(rc, ERRORS.get(rc, "error"))
+        return sp.value, op.value
+
+    # --- round predicates ----------------------------------------------------
+    def parent_round(self, x):
+        return self.L.hge_parent_round(self.h, x)
+
+    def round_inc(self, x):
+        return bool(self.L.hge_round_inc(self.h, x))
+
+    def round_diff(self, x, y):
+        out = ctypes.c_int32()
+        self._check(self.L.hge_round_diff(self.h, x, y, ctypes.byref(out)))
+        return out.value
+
+    def set_round(self, r, entries):
+        """Store.SetRound: entries = [(id, witness: bool, fame 0/1/2)]."""
+        ids = np.array([e[0] for e in entries], np.int32)
+        w = np.array([int(e[1]) for e in entries], np.uint8)
+        f = np.array([e[2] for e in entries], np.uint8)
+        u8 = ctypes.POINTER(ctypes.c_uint8)
+        self._check(self.L.hge_set_round(self.h, r, _p32(ids), w.ctypes.data_as(u8),
+                                         f.ctypes.data_as(u8), len(ids)))
 
     def coordinates(self, x):
         la = np.zeros(self.n, np.int32)

@@ -14,8 +14,17 @@ identity matter to the ordering path).
 Byzantine forkers (config 5): a subset of creators, with probability p per
 event, also submit a second event with the same (creator, index, parents) and
 a different hash/S right after the honest one.  The first-inserted branch wins;
-the fork is rejected by FromParentsLatest (hashgraph.go:366-396) and nothing
-references it.
+the fork is rejected by FromParentsLatest (hashgraph.go:366-396).
+
+Cascades (cascade_p > 0): a peer that saw the losing branch first builds on
+it.  With probability cascade_p per fork twin, a random other creator submits,
+right after the twin, an event whose other-parent IS the twin ("Other-parent
+not known", hashgraph.go:381-384); with probability 1/2 that creator then
+submits a child of the rejected event ("Self-parent not known",
+hashgraph.go:373-376), and with probability 1/2 a third creator submits an
+event whose other-parent is the rejected one (rejected again).  Rejected
+submissions are never referenced by honest ones, so the honest stream goes on
+(the node keeps syncing with everyone else).
 """
 import numpy as np
 
@@ -41,7 +50,7 @@ def _bytes32(seed, salt, n):
     return out.astype(">u8").view(np.uint8).reshape(n, 32)
 
 
-def random_gossip(n, events, seed=1, forkers=0, fork_p=0.0):
+def random_gossip(n, events, seed=1, forkers=0, fork_p=0.0, cascade_p=0.0):
     """Return a dict describing a submission stream of `events` honest events.
 
     Keys: n, creator, index, sp, op (submission indices, -1 = none), ts, S
@@ -102,6 +111,8 @@ def random_gossip(n, events, seed=1, forkers=0, fork_p=0.0):
     }
     if forkers and fork_p > 0:
         dag = _inject_forks(dag, rng, forkers, fork_p, seed)
+        if cascade_p > 0:
+            dag = _inject_cascades(dag, rng, cascade_p, seed)
     return dag
 
 
@@ -139,6 +150,99 @@ def _inject_forks(dag, rng, forkers, p, seed):
     out["hash"][is_twin] = twin_H
     out["ts"][is_twin] += 1
     out["honest"] = ~is_twin
+    return out
+
+
+def _inject_cascades(dag, rng, p, seed):
+    """Submissions that build on fork twins (see the module docstring).  Each
+    doomed record is inserted right after the twin it descends from."""
+    n = dag["n"]
+    E = len(dag["creator"])
+    twins = np.nonzero(~dag["honest"])[0]
+    chosen = twins[rng.random(len(twins)) < p]
+    if chosen.size == 0:
+        return dag
+    creator = dag["creator"]
+    honest = dag["honest"]
+    # honest positions of every creator, for "the head of creator c before position t"
+    pos_by_c = [np.nonzero((creator == c) & honest)[0] for c in range(n)]
+
+    def head(c, t):
+        k = np.searchsorted(pos_by_c[c], t) - 1
+        return int(pos_by_c[c][k]) if k >= 0 else -1
+
+    recs = []  # (insert after stream position, creator, index, sp, op) with sp/op = ("s", pos) or ("d", j)
+    for t in chosen.tolist():
+        tc = int(creator[t])
+        others = [c for c in range(n) if c != tc]
+        c2 = int(others[rng.integers(len(others))])
+        h2 = head(c2, t)
+        if h2 < 0:
+            continue
+        j0 = len(recs)
+        recs.append((t, c2, int(dag["index"][h2]) + 1, ("s", h2), ("s", t)))     # op = twin
+        if rng.random() < 0.5:                                                  # child of the doomed one
+            h_any = head(int(others[rng.integers(len(others))]), t)
+            recs.append((t, c2, int(dag["index"][h2]) + 2, ("d", j0), ("s", max(h_any, 0))))
+        if rng.random() < 0.5 and n > 2:                                        # op = the doomed one
+            c3 = int([c for c in others if c != c2][rng.integers(n - 2)])
+            h3 = head(c3, t)
+            if h3 >= 0:
+                recs.append((t, c3, int(dag["index"][h3]) + 1, ("s", h3), ("d", j0)))
+    if not recs:
+        return dag
+    after = np.array([r[0] for r in recs], np.int64)
+    m = len(recs)
+    # new position of old stream position q: q + #records inserted after positions < q
+    shift = np.searchsorted(np.sort(after), np.arange(E), side="left")
+    newpos_old = np.arange(E) + shift
+    # records after the same twin keep their relative order: position = twin's new pos + 1 + k
+    k_same = np.zeros(m, np.int64)
+    seen = {}
+    for j in range(m):
+        k_same[j] = seen.get(after[j], 0)
+        seen[after[j]] = k_same[j] + 1
+    newpos_rec = newpos_old[after] + 1 + k_same
+    tot = E + m
+    out = {"n": n}
+    sel_old = newpos_old
+    for key in ("creator", "index", "ntx", "ts", "honest"):
+        arr = np.empty(tot, dag[key].dtype)
+        arr[sel_old] = dag[key]
+        out[key] = arr
+
+    def remap_old(v):
+        return np.where(v >= 0, newpos_old[np.maximum(v, 0)], -1)
+
+    sp = np.empty(tot, np.int64)
+    op = np.empty(tot, np.int64)
+    sp[sel_old] = remap_old(dag["sp"])
+    op[sel_old] = remap_old(dag["op"])
+    S = np.empty((tot, 32), np.uint8)
+    H = np.empty((tot, 32), np.uint8)
+    S[sel_old] = dag["S"]
+    H[sel_old] = dag["hash"]
+    rS = _bytes32(seed, 5, m)
+    rH = _bytes32(seed, 6, m)
+
+    def ref(r):
+        return newpos_old[r[1]] if r[0] == "s" else newpos_rec[r[1]]
+
+    for j, (t, c, idx, rsp, rop) in enumerate(recs):
+        q = newpos_rec[j]
+        out["creator"][q] = c
+        out["index"][q] = idx
+        out["ntx"][q] = 1
+        out["ts"][q] = dag["ts"][t] + 2 + j % 997  # between the twin and the next honest event
+        out["honest"][q] = False
+        sp[q] = ref(rsp)
+        op[q] = ref(rop)
+        S[q] = rS[j]
+        H[q] = rH[j]
+    out["sp"] = sp.astype(np.int32)
+    out["op"] = op.astype(np.int32)
+    out["S"] = S
+    out["hash"] = H
     return out
 
 

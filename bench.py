@@ -1,17 +1,19 @@
 """Benchmark: consensus-ordered events/sec of the hashgraph ordering hot path.
 
 Workloads (BASELINE.json configs):
-  gossip (default, configs[1]): synthetic random-gossip DAG, 16 participants,
-      100k events, RunConsensus every K=16 inserted events (the caller's
-      schedule is part of the semantics: SURVEY.md TL;DR 5).  One step = one
-      full replay of the stream on the device: coordinates (InsertEvent),
-      DivideRounds, DecideFame and FindOrder at all 6,250 call points, from
-      event tables already resident in HBM to the complete consensus order.
-      --participants/--events/--k select configs[2] (64/1M) and configs[3]
-      (256/10M).
+  gossip (default): synthetic random-gossip DAG, 256 participants, 10M events,
+      RunConsensus every K=256 inserted events (configs[3] on one MI355X, the
+      largest single-GPU configuration; the caller's schedule is part of the
+      semantics: SURVEY.md TL;DR 5).  One step = one full replay of the stream
+      on the device: coordinates (InsertEvent), DivideRounds, DecideFame and
+      FindOrder at all 39,063 call points, from event tables already resident in
+      HBM to the complete consensus order.  --participants/--events/--k select
+      the other gossip configs (16/100k = configs[1], 64/1M = configs[2]).
   mc (configs[4]): Monte Carlo batch of independent 32-participant
       hashgraphs with simulated Byzantine forkers (10 of 32 creators fork with
-      p=0.05), 10k submissions each, K=32; the batch is split across ranks.
+      p=0.05; half of the fork twins get events built on them, which are
+      rejected in cascade), 10k submissions each, K=32; the batch is split
+      across ranks.
       Every graph has its own engine (HIP stream); host threads drive them
       concurrently.
 
@@ -21,10 +23,18 @@ replays its share of the batch; no data-path collective.  value = events
 ordered by all ranks per step / max-over-ranks step time ("scaling": "weak").
 
 The timed steps run without per-kernel instrumentation; a separate profiled
-pass (HIP events around every launch on the engine stream) gives the
-dominant kernel's average launch time for the roofline.  The CPU baseline is
-the Go-faithful oracle on one host core over a bounded sample of the same
-workload (rank 0 only), and its order is compared with the device's.
+pass (HIP events around every launch on the engine stream) gives every
+kernel's device time for the roofline.  Rank 0 also
+  * checks its order against a committed golden prefix (tests/golden/bench_*,
+    the oracle's output for the first calls of the same seeded stream): the
+    engine reproduces per-call semantics, so the first calls' batches of the
+    full replay must equal the prefix replay's;
+  * times the CPU baseline: the Go-faithful oracle on one host core over a
+    bounded prefix of the same stream, and compares its order too;
+  * with the default configuration, adds a `secondary` object: the 16/100k
+    replay (bit-exact against the oracle over the whole stream) and the online
+    per-call path (hge_insert_events of K events + hge_run_consensus per call,
+    what node/core.go:179-202 does) at 16/100k.
 """
 import argparse
 import json
@@ -40,26 +50,29 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+DEFAULT = (256, 10_000_000)
 
 
-def algorithmic_bytes(kernel, n, events, ordered, sweeps=1):
-    """Algorithmic HBM bytes of ONE launch of `kernel` over a whole replay
-    (B(N) = 24N + 48 per ordered event).
+def algorithmic_bytes(kernel, n, events, ordered):
+    """Algorithmic HBM bytes of `kernel` over ONE whole replay (all its launches),
+    int32 coordinates (B(N) = 24N + 48 per ordered event).
 
-    coordinates: k_coord_final 16N/event (read LA[sp] and D, write LA and FD),
-    k_coord_local 8N/event, k_la_sweep 8N/event per sweep (op row + own row
-    read) plus the own row written once over all `sweeps` (a sweep stores only
-    the values that changed, so a converged row is not re-written), k_transpose and k_fdt_runs 8N/event; rounds: k_fss 8N/event (FD row read,
-    fss row written), k_rounds_walk / k_rounds_coop 4N/event (the strongly-see
-    round test reads each event's LA row once); order: k_round_received /
-    k_median_wave (4N + 48)/ordered event; anything else the 48-byte sort key.
+    Each byte is counted once per replay, however many launches touch it:
+      k_la_sweep    12N/event: read LA[sp] and LA[op], write LA[x] -- once, not
+                    once per fixed-point sweep (the sweeps' re-reads are waste);
+      k_la_clear     4N/event (the new rows' -1 fill);
+      k_transpose   16N/event (LA -> LAT and FDT -> FD: each reads and writes 4N);
+      k_fdt_clear    4N/event; k_fdt_runs 8N/event (LAT read, FDT written);
+      k_fss          8N/event (FD row read, fss row written, N <= 32);
+      rounds        4N/event (the strongly-see round test reads each row once);
+      k_round_received / k_median_wave (4N + 48) per ordered event (FD row for
+                    the median, sort key); everything else the 48-byte key.
     """
     name = kernel.strip("()").split("<")[0]
-    if name == "k_la_sweep":
-        return 8 * n * events + 4 * n * events / max(sweeps, 1)
-    per_event = {"k_coord_final": 16 * n, "k_coord_local": 8 * n,
-                 "k_transpose": 8 * n, "k_fdt_runs": 8 * n, "k_fss": 8 * n, "k_rounds_walk": 4 * n,
-                 "k_rounds_coop": 4 * n, "k_rounds_fss": 4 * n, "k_rounds_frontier": 4 * n}
+    per_event = {"k_la_sweep": 12 * n, "k_la_clear": 4 * n, "k_transpose": 16 * n,
+                 "k_fdt_clear": 4 * n, "k_fdt_runs": 8 * n, "k_fss": 8 * n,
+                 "k_rounds_walk": 4 * n, "k_rounds_coop": 4 * n, "k_rounds_coop_spec": 4 * n,
+                 "k_walk_spec": 4 * n, "k_rounds_fss": 4 * n}
     if name in per_event:
         return per_event[name] * events
     if name in ("k_round_received", "k_median_wave"):
@@ -68,7 +81,7 @@ def algorithmic_bytes(kernel, n, events, ordered, sweeps=1):
 
 
 def pmc_traffic(config_key, kernel):
-    """HBM bytes per launch of `kernel` in this configuration from the committed
+    """HBM bytes per replay of `kernel` in this configuration from the committed
     rocprofv3 PMC passes (profiles/pmc_traffic.json, made by
     scripts/pmc_traffic.py on the GPU box), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -78,7 +91,82 @@ def pmc_traffic(config_key, kernel):
         return None
     name = kernel.strip("()").split("<")[0]
     v = pm.get("configs", {}).get(config_key, {}).get(name)
-    return v.get("bytes_per_launch") if isinstance(v, dict) else None
+    return v.get("bytes_per_replay") if isinstance(v, dict) else None
+
+
+def golden_prefix(n, E, K, seed):
+    """The committed oracle prefix of this exact stream, or None
+    (tests/golden/make_bench_prefix.py)."""
+    path = os.path.join(ROOT, "tests", "golden", f"bench_n{n}_e{E}_k{K}_s{seed}_prefix.npz")
+    if not os.path.exists(path):
+        return None
+    return np.load(path)
+
+
+def sub_stream(dag, ns):
+    return {k: (v[:ns] if isinstance(v, np.ndarray) else v) for k, v in dag.items()}
+
+
+def online_path(n, E, K, seed, device):
+    """The per-call production path: for every call, hge_insert_events of the
+    next K submissions, then hge_run_consensus (node/core.go:179-202).  Returns
+    per-call latency and events/s, and whether the order equals the replay's."""
+    from babble_amd.engine import Engine, events_array
+    from babble_amd.gossip import random_gossip, schedule
+    dag = random_gossip(n, E, seed=seed)
+    ev = events_array(dag)
+    calls = schedule(E, K)
+    rep = Engine(n, E, device=device)
+    _, rorder, _ = rep.replay(ev, calls)
+    rep.close()
+    eng = Engine(n, E, device=device)
+    lat = np.zeros(len(calls))
+    parts = []
+    prev = 0
+    t0 = time.perf_counter()
+    for i, c in enumerate(calls):
+        t = time.perf_counter()
+        # every submission of a gossip stream is accepted: engine id == submission index
+        eng.insert_events(ev[prev:c])
+        parts.append(eng.run_consensus())
+        lat[i] = time.perf_counter() - t
+        prev = c
+    wall = time.perf_counter() - t0
+    order = np.concatenate(parts) if parts else np.zeros(0, np.int32)
+    eng.close()
+    return {"workload": f"online per-call path, {n} participants, {E} events, "
+                        f"hge_insert_events(K={K}) + hge_run_consensus per call ({len(calls)} calls)",
+            "value": round(len(order) / wall, 1), "unit": "events/s",
+            "call_latency_us": {"mean": round(float(lat.mean()) * 1e6, 1),
+                                "p50": round(float(np.percentile(lat, 50)) * 1e6, 1),
+                                "p99": round(float(np.percentile(lat, 99)) * 1e6, 1)},
+            "parity": ("identical to the bulk replay" if np.array_equal(order, rorder)
+                       else "MISMATCH vs the bulk replay")}
+
+
+def small_replay(n, E, K, seed, device, steps=20):
+    """A second, small gossip line (configs[1]) checked bit-exact against the
+    oracle over the whole stream."""
+    from babble_amd.engine import Engine, events_array
+    from babble_amd.gossip import random_gossip, schedule
+    from oracle.oracle import replay as oracle_replay
+    dag = random_gossip(n, E, seed=seed)
+    calls = schedule(E, K)
+    eng = Engine(n, E, device=device)
+    eng.prepare(events_array(dag), calls)
+    for _ in range(5):
+        eng.run()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        nord = eng.run()
+    dt = (time.perf_counter() - t0) / steps
+    _, gorder, _ = eng.fetch()
+    eng.close()
+    _, _, corder, _ = oracle_replay(dag, calls)
+    return {"workload": f"random-gossip DAG, {n} participants, {E} events, RunConsensus every K={K}",
+            "value": round(nord / dt, 1), "unit": "events/s", "ms_per_step": round(dt * 1e3, 4),
+            "parity": ("bit-exact vs CPU oracle (full stream)" if np.array_equal(gorder, corder)
+                       else "MISMATCH vs CPU oracle")}
 
 
 def main():
@@ -96,12 +184,14 @@ def main():
     ap.add_argument("--threads", type=int, default=8, help="mc: host threads driving engines")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-events", type=int, default=100_000)
-    ap.add_argument("--profile-steps", type=int, default=2)
+    ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--cpu-sample-events", type=int, default=None,
+                    help="CPU baseline prefix (default: 20480 at N >= 128, 100k below)")
+    ap.add_argument("--profile-steps", type=int, default=1)
     args = ap.parse_args()
     mc = args.workload == "mc"
-    n = args.participants or (32 if mc else 16)
-    E = args.events or (10_000 if mc else 100_000)
+    n = args.participants or (32 if mc else DEFAULT[0])
+    E = args.events or (10_000 if mc else DEFAULT[1])
     K = args.k or n
 
     rank = int(os.environ.get("RANK", 0))
@@ -123,7 +213,7 @@ def main():
     t0 = time.perf_counter()
     if mc:
         first, per = shard_range(args.graphs, world, rank)
-        dags = [random_gossip(n, E, seed=args.seed + first + g, forkers=10, fork_p=0.05)
+        dags = [random_gossip(n, E, seed=args.seed + first + g, forkers=10, fork_p=0.05, cascade_p=0.5)
                 for g in range(per)]
         engines = [Engine(n, len(d["creator"]) + 64, device=local_rank) for d in dags]
         for eng, d in zip(engines, dags):
@@ -169,81 +259,103 @@ def main():
     replay_ms = {"coords_gpu": st_ms[0], "coords_wall": st_ms[1], "consensus_gpu": st_ms[3],
                  "consensus_wall": st_ms[2], "gpu": st_ms[6], "wall": st_ms[4]}
     replay_ms = {k: round(v, 4) for k, v in replay_ms.items()}
+    _, gorder, gcounts = eng0.fetch()
 
     # ---- profiled pass: per-kernel device time (HIP events on the engine stream) ----
+    nprof = max(1, args.profile_steps)
     eng0.set_profiling(True)
-    for _ in range(max(1, args.profile_steps)):
+    for _ in range(nprof):
         eng0.run()
     kstats = eng0.kernel_stats()
     eng0.set_profiling(False)
     ev0 = len(dags[0]["creator"])
     ord0 = eng0._nordered
+    sweeps = eng0.coordinate_sweeps()
 
     tot_ordered, max_step = ordered, step_s
     if dist is not None:
         max_step, tot_ordered = reduce_step(dist, step_s, ordered, f"cuda:{local_rank}")
 
-    nprof = max(1, args.profile_steps)
-
-    sweeps = eng0.coordinate_sweeps()
-
-    def kernel_gbs(name):
-        """(algorithmic bytes per launch, avg launch ms, achieved GB/s) of one kernel.
-        k_la_sweep: every sweep that does work reads the own and op rows once (8N
-        bytes per event) and the row writes are spread over the sweeps; the
-        queued launches after the converged one return at once and are left out
-        of the launch count."""
+    def kernel_roofline(name):
+        """(algorithmic bytes per launch, average launch ms, achieved GB/s).
+        The algorithmic bytes of a replay are spread over the launches that did
+        work: for k_la_sweep the sweeps up to the first quiet one (the queued
+        launches after it return at once and are left out)."""
         ms, cnt = kstats[name]
-        if name.startswith("k_la_sweep"):
-            cnt = sweeps * nprof
-            b = algorithmic_bytes(name, n, ev0, ord0, sweeps)
-        else:
-            b = algorithmic_bytes(name, n, ev0, ord0) / max(cnt // nprof, 1)
-        per_launch = ms / max(cnt, 1)
-        return b, per_launch, b / (per_launch * 1e-3) / 1e9
+        base = name.strip("()").split("<")[0]
+        launches = sweeps * nprof if base == "k_la_sweep" else cnt
+        per_replay = launches / nprof
+        b = algorithmic_bytes(name, n, ev0, ord0) / max(per_replay, 1)
+        per_launch = ms / max(launches, 1)
+        return b, per_launch, b / (per_launch * 1e-3) / 1e9, per_replay
 
     dom = max(kstats.items(), key=lambda kv: kv[1][0])[0]
-    alg, per_launch_ms, achieved = kernel_gbs(dom)
-    # the bandwidth-bound kernels (streaming passes over the N-wide tables)
+    alg, per_launch_ms, achieved, _ = kernel_roofline(dom)
+    # every kernel that streams the N-wide tables, with its roofline
     hbm_kernels = {}
     for name in kstats:
         base = name.strip("()").split("<")[0]
-        if base in ("k_la_sweep", "k_transpose", "k_fss", "k_fdt_runs"):
-            b, pl, gbs = kernel_gbs(name)
+        if base in ("k_la_sweep", "k_la_clear", "k_transpose", "k_fss", "k_fdt_runs",
+                    "k_fdt_clear", "k_rounds_coop", "k_rounds_coop_spec", "k_median_wave"):
+            b, pl, gbs, lpr = kernel_roofline(name)
             hbm_kernels[name] = {"achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
-                                 "launch_ms": round(pl, 4),
-                                 "launches_per_replay": (sweeps if base == "k_la_sweep"
-                                                         else kstats[name][1] // nprof)}
+                                 "alg_bytes_per_launch": int(b), "launch_ms": round(pl, 4),
+                                 "launches_per_replay": lpr}
 
-    cpu, parity = None, None
+    cpu, parity, checks = None, None, []
+    if rank == 0 and not mc:
+        gp = golden_prefix(n, E, K, args.seed)
+        if gp is not None:
+            nc = int(gp["n_calls"])
+            ok = (np.array_equal(gcounts[:nc], gp["counts"]) and
+                  np.array_equal(gorder[:len(gp["order"])], gp["order"]))
+            checks.append(f"{'bit-exact' if ok else 'MISMATCH'} vs committed oracle golden "
+                          f"(first {int(gp['prefix'])} submissions, {nc} calls, "
+                          f"{len(gp['order'])} ordered)")
     if rank == 0 and not args.no_cpu_baseline:
         from oracle.oracle import replay as oracle_replay
         d = dags[0]
-        ns = min(args.cpu_sample_events, len(d["creator"]))
-        sub = {k: (v[:ns] if isinstance(v, np.ndarray) else v) for k, v in d.items()}
+        ns = args.cpu_sample_events or (20480 if n >= 128 else 100_000)
+        ns = min(ns, len(d["creator"]))
+        if not mc:
+            ns = max(K, ns // K * K)  # whole calls only: the prefix's calls are the full run's
+        sub = sub_stream(d, ns)
+        calls = schedule(ns, K)
         t0 = time.perf_counter()
-        _, _, corder, _ = oracle_replay(sub, schedule(ns, K))
+        _, _, corder, ccounts = oracle_replay(sub, calls)
         cs = time.perf_counter() - t0
         what = (f"graph 0 of the batch ({ns} submissions)" if mc else
                 f"first {ns} of {len(d['creator'])} submissions of the same stream")
         cpu = {"value": round(len(corder) / cs, 1), "unit": "events/s", "cores": 1, "kind": "port",
                "sample": f"Go-faithful C++ oracle (oracle/hg_oracle.cpp), {what}, K={K}, "
-                         f"{cs:.2f} s on {platform.processor() or platform.machine()} "
-                         f"(host nproc {os.cpu_count()})"}
-        if ns == len(d["creator"]):
-            _, gorder, _ = eng0.fetch()
-            parity = ("bit-exact vs CPU oracle (full stream of graph 0)"
-                      if np.array_equal(gorder, corder) else "MISMATCH vs CPU oracle")
+                         f"{len(corder)} ordered in {cs:.2f} s on "
+                         f"{platform.processor() or platform.machine()} (host nproc {os.cpu_count()})"}
+        if not mc:
+            ok = (np.array_equal(gcounts[:len(calls)], ccounts) and
+                  np.array_equal(gorder[:len(corder)], corder))
+            checks.append(f"{'bit-exact' if ok else 'MISMATCH'} vs CPU oracle run live "
+                          f"(first {ns} submissions, {len(calls)} calls, {len(corder)} ordered)")
+        elif ns == len(d["creator"]):
+            ok = np.array_equal(gorder, corder)
+            checks.append(f"{'bit-exact' if ok else 'MISMATCH'} vs CPU oracle (full graph 0)")
+    if rank == 0:
+        parity = "; ".join(checks) if checks else None
+
+    secondary = None
+    if (rank == 0 and not mc and not args.no_secondary and (n, E) == DEFAULT and world == 1):
+        secondary = {"replay_16_100k": small_replay(16, 100_000, 16, args.seed, local_rank),
+                     "online_16_100k": online_path(16, 100_000, 16, args.seed, local_rank)}
 
     if rank == 0:
         value = tot_ordered / max_step
         if mc:
             workload = (f"Monte Carlo batch: {args.graphs} independent random-gossip hashgraphs, "
-                        f"{n} participants, {E} submissions each, 10 forkers p=0.05, "
+                        f"{n} participants, {E} submissions each, 10 forkers p=0.05 with cascades, "
                         f"RunConsensus every K={K}")
         else:
             workload = (f"random-gossip DAG, {n} participants, {E} events per GPU, "
                         f"RunConsensus every K={K} events ({len(schedule(E, K))} calls)")
+        cfg_key = f"{args.workload}_n{n}_e{E}_k{K}"
         line = {
             "metric": "consensus-ordered events/sec at N participants",
             "value": round(value, 1),
@@ -263,7 +375,8 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": pmc_traffic(f"{args.workload}_n{n}_e{E}_k{K}", dom),
+                         "traffic": pmc_traffic(cfg_key, dom),
+                         "traffic_unit": "HBM bytes per replay (rocprofv3 FETCH_SIZE+WRITE_SIZE)",
                          "algorithmic_bytes_per_launch": int(alg),
                          "launch_ms": round(per_launch_ms, 4),
                          "hbm_kernels": hbm_kernels,
@@ -275,14 +388,21 @@ def main():
             "parity": parity,
             "ingest_host_ms": round(ingest_s * 1e3, 2),
             "replay_ms": replay_ms,
+            "coordinate_sweeps": sweeps,
             "kernels_ms_per_replay": {k: round(v[0] / nprof, 4) for k, v in
                                       sorted(kstats.items(), key=lambda kv: -kv[1][0])},
             "kernel_launches_per_replay": {k: v[1] // nprof for k, v in kstats.items()},
         }
+        if secondary is not None:
+            line["secondary"] = secondary
         print(json.dumps(line), flush=True)
     pool.shutdown()
     for e in engines:
         e.close()
+    if os.environ.get("HGE_DUMP_MAPS"):
+        # diagnostics for crashes after main (rocprofv3 exit SIGSEGV): the library map
+        with open("/proc/self/maps") as f, open(os.environ["HGE_DUMP_MAPS"], "w") as g:
+            g.write(f.read())
     if dist is not None:
         dist.destroy_process_group()
 

@@ -34,11 +34,22 @@ enum hge_status {
   HGE_ERR_SELF_PARENT_CREATOR = -3,  /* "Self-parent has different creator"     hashgraph.go:377-379 */
   HGE_ERR_OTHER_PARENT_UNKNOWN = -4, /* "Other-parent not known"                hashgraph.go:381-384 */
   HGE_ERR_SELF_PARENT_NOT_LAST = -5, /* "Self-parent not last known event..."   hashgraph.go:390-393 */
-  HGE_ERR_INDEX = -6,      /* Body.Index != position in the creator's chain (stricter than the reference) */
-  HGE_ERR_CAPACITY = -7,   /* device allocation failed */
+  /* Body.Index != position in the creator's chain.  DELIBERATE DEVIATION: the
+   * reference accepts such an event and uses the claimed index in its coordinates
+   * (hashgraph.go:455-460); the engine's tables are indexed by chain position, so
+   * it refuses index-lying events (Byzantine input only: an honest Core always
+   * creates head.Index+1, node/core.go:87-99).  INTEGRATION.md, tests. */
+  HGE_ERR_INDEX = -6,
+  /* device allocation failed, or the event would make its creator's chain longer
+   * than the engine takes (N > 32: 65,534 events per creator; the wide rounds
+   * kernels keep chain positions as uint16).  Refused at admission: the engine
+   * stays usable. */
+  HGE_ERR_CAPACITY = -7,
   HGE_ERR_ARG = -8,        /* bad argument */
   HGE_ERR_DEVICE = -9,     /* HIP runtime error */
-  HGE_ERR_INTERNAL = -10
+  HGE_ERR_INTERNAL = -10,
+  HGE_ERR_TOO_LATE = -11,  /* ErrTooLate  (store.go:22): below the rolling window  */
+  HGE_ERR_NOT_FOUND = -12  /* ErrKeyNotFound (store.go:21)                         */
 };
 
 /* Parent reference values. */
@@ -59,8 +70,11 @@ typedef struct hge_event {
 } hge_event;
 
 /* ---- lifecycle ------------------------------------------------------------ */
-/* NewHashgraph (hashgraph.go:51-76) + NewInmemStore (inmem_store.go:27-36) with
- * unbounded capacity.  capacity_events is a sizing hint (tables grow). */
+/* NewHashgraph (hashgraph.go:51-76) + NewInmemStore (inmem_store.go:27-36).
+ * capacity_events is a sizing hint: the device tables grow on demand up to HBM.
+ * Consensus math always runs with the reference's infinite-cache contract
+ * (SURVEY.md TL;DR 8); hge_set_cache_size only shapes the rolling views below.
+ * N > 32: at most 65,534 events per creator (HGE_ERR_CAPACITY at admission). */
 int hge_create(int32_t n_participants, int64_t capacity_events, int32_t device,
                uint32_t flags, hge_engine** out);
 void hge_destroy(hge_engine* h);
@@ -71,7 +85,8 @@ int hge_reset(hge_engine* h); /* forget all events, keep allocations */
 /* InsertEvent (hashgraph.go:328-363) for n events in order.  Processing stops at
  * the first rejected event, like Core.Sync (node/core.go:137-145).  Accepted
  * events receive ids hge_event_count() .. +n_accepted-1; status_out[i] is the
- * id or a negative hge_status for the first rejection (may be NULL). */
+ * id or a negative hge_status for the first rejection (may be NULL).  The
+ * events before a rejection stay inserted: *n_accepted says how many. */
 int hge_insert_events(hge_engine* h, const hge_event* ev, int64_t n, int32_t* status_out,
                       int64_t* n_accepted);
 
@@ -89,7 +104,7 @@ int hge_run_consensus(hge_engine* h, int32_t* ids_out, int64_t cap, int64_t* n_o
 /* Replays a whole submission stream on a fresh state: parents are submission
  * indices (-1 none); rejected submissions are skipped and status_out records
  * them; RunConsensus runs after each submission count in call_points (1-based,
- * ascending).  Results are identical to calling hge_insert_events and
+ * strictly ascending, <= n_sub; anything else is HGE_ERR_ARG).  Results are identical to calling hge_insert_events and
  * hge_run_consensus at every call point.  order_out receives the full consensus
  * order, call_counts_out[c] the batch size of call c (both may be NULL). */
 int hge_replay(hge_engine* h, const hge_event* ev, int64_t n_sub, const int64_t* call_points,
@@ -109,7 +124,12 @@ int32_t hge_last_consensus_round(hge_engine* h);      /* -1 = nil               
 int32_t hge_last_committed_round_events(hge_engine* h);
 int64_t hge_consensus_transactions(hge_engine* h);
 int64_t hge_consensus_count(hge_engine* h);           /* Store.ConsensusEventsCount */
+/* Store.ConsensusEvents (inmem_store.go:88-95): the rolling window of the
+ * consensus list (common/rolling_list.go:55-67) for the configured cache size;
+ * the whole list when the cache size is 0 (unbounded).  Returns its length. */
 int64_t hge_consensus_events(hge_engine* h, int32_t* ids_out, int64_t cap);
+/* The unbounded consensus log from position `from` (commit stream; no window). */
+int64_t hge_consensus_log(hge_engine* h, int64_t from, int32_t* ids_out, int64_t cap);
 int64_t hge_undetermined(hge_engine* h, int32_t* ids_out, int64_t cap);
 int hge_known(hge_engine* h, int32_t* counts_out);    /* Known(), n_participants ints */
 int32_t hge_round_of(hge_engine* h, int32_t id);      /* Round(x) (after DivideRounds) */
@@ -119,6 +139,50 @@ int32_t hge_fame(hge_engine* h, int32_t round, int32_t creator); /* 0 undef, 1 t
 int32_t hge_round_events(hge_engine* h, int32_t round);          /* Store.RoundEvents(r) */
 int32_t hge_round_received(hge_engine* h, int32_t id);           /* -1 = nil */
 int64_t hge_consensus_timestamp(hge_engine* h, int32_t id);
+
+/* Bulk reads for ids [0, min(cap, hge_event_count)): Round/Witness of every
+ * event (DivideRounds state), and RoundReceived (-1 = nil) / consensus timestamp. */
+int hge_event_rounds(hge_engine* h, int32_t* round_out, uint8_t* witness_out, int64_t cap);
+int hge_event_received(hge_engine* h, int32_t* rr_out, int64_t* cts_out, int64_t cap);
+
+/* ---- Store semantics and the sync path (store.go:25-41, node/core.go:108-132) -- */
+/* Store.CacheSize (inmem_store.go:38-40): size of the rolling windows of
+ * ParticipantEvents / ParticipantEvent / ConsensusEvents; 0 = unbounded. */
+int hge_set_cache_size(hge_engine* h, int64_t size);
+int64_t hge_cache_size(hge_engine* h);
+/* Store.ParticipantEvents(pk, skip) (caches.go:45-76): ids of the creator's
+ * events from position `skip` on; HGE_ERR_TOO_LATE below the rolling window,
+ * HGE_ERR_NOT_FOUND for an unknown creator.  *n_out = number of ids. */
+int hge_participant_events(hge_engine* h, int32_t creator, int64_t skip, int32_t* ids_out,
+                           int64_t cap, int64_t* n_out);
+/* Store.ParticipantEvent(pk, index) (caches.go:78-84): id, or HGE_ERR_TOO_LATE /
+ * HGE_ERR_NOT_FOUND. */
+int32_t hge_participant_event(hge_engine* h, int32_t creator, int64_t index);
+/* Store.LastFrom(pk) (caches.go:86-97): id of the creator's last event, -1 = "". */
+int32_t hge_last_from(hge_engine* h, int32_t creator);
+/* Core.Diff's selection (node/core.go:108-132): every event the caller knows and
+ * `known` (n_participants counts) does not, in topological order (ByTopologicalOrder,
+ * event.go:233-239). */
+int hge_diff(hge_engine* h, const int32_t* known, int32_t* ids_out, int64_t cap, int64_t* n_out);
+/* SetWireInfo (hashgraph.go:497-524): {selfParentIndex, otherParentCreatorID,
+ * otherParentIndex, creatorID} of an event (WireBody, event.go:244-259). */
+int hge_wire_info(hge_engine* h, int32_t id, int32_t* out4);
+/* ReadWireInfo's parent resolution (hashgraph.go:526-571): (creator, index)
+ * pairs -> engine ids (HGE_NONE for index -1). */
+int hge_read_wire_parents(hge_engine* h, int32_t creator_id, int32_t self_parent_index,
+                          int32_t other_parent_creator_id, int32_t other_parent_index,
+                          int32_t* sp_out, int32_t* op_out);
+
+/* ---- round predicates (hashgraph.go:211-326) --------------------------------- */
+int32_t hge_parent_round(hge_engine* h, int32_t x);   /* ParentRound: -1 bad id, 0 no parents */
+int32_t hge_round_inc(hge_engine* h, int32_t x);      /* RoundInc (over RoundWitnesses(pr))   */
+int hge_round_diff(hge_engine* h, int32_t x, int32_t y, int32_t* out); /* RoundDiff */
+/* Store.SetRound (inmem_store.go:115-118): record witness entries (and their
+ * fame: 0 undefined, 1 true, 2 false) of round r; Rounds() >= r + 1 afterwards.
+ * The engine's own DivideRounds writes the same tables for rounds the DAG
+ * determines; the reference's round tests use SetRound in its place. */
+int hge_set_round(hge_engine* h, int32_t round, const int32_t* ids, const uint8_t* witness,
+                  const uint8_t* fame, int32_t n);
 
 /* ---- test predicates (hashgraph.go:82-208) --------------------------------- */
 int32_t hge_ancestor(hge_engine* h, int32_t x, int32_t y);

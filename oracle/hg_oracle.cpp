@@ -121,6 +121,10 @@ struct Oracle {
   int topological_index = 0;
 
   std::unordered_map<uint64_t, bool> ancestorCache, selfAncestorCache, stronglySeeCache;
+  // test instrumentation (not part of the reference): how often DecideFame took
+  // the coin branch, voted by coin, and re-decided an already decided witness
+  // (same / changed value); read by hgo_stats
+  int64_t stat_coin_evals = 0, stat_coin_votes = 0, stat_redecided = 0, stat_flipped = 0;
   std::unordered_map<uint64_t, int> oldestSelfAncestorCache;
   std::unordered_map<int, int> parentRoundCache, roundCache;
 
@@ -401,14 +405,23 @@ struct Oracle {
               // math.Mod(float64(diff), float64(N)) > 0  <=>  diff % N != 0 (diff > 0)
               if (diff % n != 0) {  // normal round
                 if (t >= SuperMajority()) {
+                  auto prev = roundInfo.events.find(x);
+                  if (prev != roundInfo.events.end() && prev->second.famous != Undefined) {
+                    stat_redecided++;
+                    if (prev->second.famous != (v ? True : False)) stat_flipped++;
+                  }
                   roundInfo.SetFame(x, v);
                   break;  // break out of y loop
                 } else {
                   setVote(y, x, v);
                 }
               } else {  // coin round
+                stat_coin_evals++;
                 if (t >= SuperMajority()) setVote(y, x, v);
-                else setVote(y, x, events[y].coin);
+                else {
+                  stat_coin_votes++;
+                  setVote(y, x, events[y].coin);
+                }
               }
             }
           }
@@ -624,6 +637,15 @@ void hgo_set_round(void* h, int r, const int32_t* ids, const int32_t* witness, c
 // position listed in call_points (ascending, 1-based counts of submissions).
 // Outputs: status[n_sub], order[cap] (consensus order), call_counts[n_calls]
 // (events committed by each call).  Returns total committed events.
+// DecideFame instrumentation: {coin-branch evaluations, coin votes, re-decided
+// witnesses, re-decisions that changed the fame value}
+int hgo_stats(void* h, int64_t* out, int cap) {
+  Oracle* o = (Oracle*)h;
+  const int64_t v[4] = {o->stat_coin_evals, o->stat_coin_votes, o->stat_redecided, o->stat_flipped};
+  for (int i = 0; i < cap && i < 4; i++) out[i] = v[i];
+  return 4;
+}
+
 int64_t hgo_replay(void* h, int64_t n_sub, const int32_t* creator, const int32_t* index,
                    const int32_t* sp, const int32_t* op, const int64_t* ts, const uint8_t* S,
                    const uint8_t* hash, const int32_t* ntx, const int64_t* call_points,

@@ -69,6 +69,7 @@ def lib():
         L.hgo_coords.argtypes = [vp, ctypes.c_int, P(i64), P(i32), P(i64), P(i32)]
         L.hgo_wire_info.argtypes = [vp, ctypes.c_int, P(i32)]
         L.hgo_set_round.argtypes = [vp, ctypes.c_int, P(i32), P(i32), P(i32), ctypes.c_int]
+        L.hgo_stats.argtypes = [vp, P(i64), ctypes.c_int]
         L.hgo_replay.restype = i64
         L.hgo_replay.argtypes = [vp, i64, P(i32), P(i32), P(i32), P(i32), P(i64),
                                  ctypes.c_char_p, ctypes.c_char_p, P(i32), P(i64), i64,
@@ -218,6 +219,13 @@ class Oracle:
         out = np.zeros(4, np.int32)
         self.L.hgo_wire_info(self.h, x, _p(out, ctypes.c_int32))
         return tuple(int(v) for v in out)
+
+    def stats(self):
+        """DecideFame instrumentation: coin-branch evaluations, coin votes,
+        re-decided witnesses, re-decisions that changed the value."""
+        out = np.zeros(4, np.int64)
+        self.L.hgo_stats(self.h, _p(out, ctypes.c_int64), 4)
+        return dict(zip(("coin_evals", "coin_votes", "redecided", "flipped"), out.tolist()))
 
     def set_round(self, r, entries):
         """entries: list of (id, witness: bool, fame: 0/1/2) (Store.SetRound)."""

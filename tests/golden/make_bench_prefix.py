@@ -1,0 +1,42 @@
+"""Golden prefix for bench.py's in-run parity check (test infrastructure).
+
+The bench replays the full seeded stream on the GPU; the engine reproduces the
+reference's per-call semantics, so the batches of the first calls depend only
+on the submissions before them.  This script runs the CPU oracle
+(oracle/hg_oracle.cpp, the Go-faithful restatement) on the first PREFIX
+submissions of the same stream with the same schedule and stores the order
+and per-call batch sizes:
+
+    python tests/golden/make_bench_prefix.py [n] [events] [k] [seed] [prefix]
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from babble_amd.gossip import random_gossip, schedule  # noqa: E402
+from oracle.oracle import replay  # noqa: E402
+
+
+def main():
+    a = [int(x) for x in sys.argv[1:]]
+    n, E, K, seed, prefix = (a + [256, 10_000_000, 256, 1, 20480][len(a):])[:5]
+    prefix = prefix // K * K
+    dag = random_gossip(n, E, seed=seed)
+    sub = {k: (v[:prefix] if isinstance(v, np.ndarray) else v) for k, v in dag.items()}
+    calls = schedule(prefix, K)
+    t = time.time()
+    _, status, order, counts = replay(sub, calls)
+    assert (status >= 0).all()
+    out = os.path.join(HERE, f"bench_n{n}_e{E}_k{K}_s{seed}_prefix.npz")
+    np.savez_compressed(out, order=order.astype(np.int32), counts=counts.astype(np.int64),
+                        n_calls=len(calls), prefix=prefix, n=n, events=E, k=K, seed=seed)
+    print(f"{out}: {len(order)} ordered over {len(calls)} calls ({time.time() - t:.1f} s)")
+
+
+if __name__ == "__main__":
+    main()

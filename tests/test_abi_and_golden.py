@@ -104,3 +104,54 @@ def test_schedule():
     assert schedule(10, 4).tolist() == [4, 8, 10]
     assert schedule(8, 4).tolist() == [4, 8]
     assert schedule(5, 100).tolist() == [5]
+
+
+def test_golden_fame_statistics():
+    """The goldens the GPU replays reach DecideFame's rare branches: coin rounds with
+    coin votes (hashgraph.go:645-649) and witnesses re-decided with a different
+    value inside one call (missing votes read as nays, SURVEY.md TL;DR 4)."""
+    stats = {os.path.basename(p): np.load(p)["fame_stats"]
+             for p in glob.glob(os.path.join(GOLD, "*.npz")) if "fame_stats" in np.load(p).files}
+    assert len(stats) >= 10
+    assert stats["gossip_n4_e1000_oneshot.npz"][0] > 0   # coin-branch evaluations
+    assert stats["gossip_n4_e1000_oneshot.npz"][1] > 0   # votes taken from the coin
+    assert sum(1 for v in stats.values() if v[3] > 0) >= 8  # fame flipped by a re-decision
+
+
+@pytest.mark.parametrize("name", ["gossip_n4_e1000_k1", "gossip_n4_e1000_oneshot"])
+def test_witness_order_invariance_flags(name):
+    """Re-run the recorded invariance check (roundInfo.go:88-96: Go iterates round
+    witnesses in random map order) and compare with the flags in the golden."""
+    g = np.load(os.path.join(GOLD, name + ".npz"))
+    dag = {k: g[k] for k in ("creator", "index", "sp", "op", "ts", "S", "hash", "ntx")}
+    dag["n"] = int(g["n"])
+    same = True
+    for sd in g["order_seeds"].tolist():
+        _, _, order, _ = replay(dag, g["calls"], order_seed=sd)
+        same &= bool(np.array_equal(order, g["order"]))
+    assert same == bool(g["order_invariant"])
+
+
+def test_cascade_generator_and_oracle():
+    d = random_gossip(16, 3000, seed=21, forkers=5, fork_p=0.08, cascade_p=0.6)
+    o, status, order, _ = replay(d, schedule(len(d["creator"]), 16))
+    assert (status[d["honest"]] >= 0).all()
+    codes = set(np.unique(status[status < 0]).tolist())
+    assert {-5, -4, -2} <= codes
+    i = np.arange(len(d["creator"]))
+    assert (d["sp"] < i).all() and (d["op"] < i).all() and (np.diff(d["ts"]) > 0).all()
+
+
+def test_property_checker_on_an_oracle_run():
+    """tests/parity.check_run (the full-size GPU checks) holds on an oracle run."""
+    from parity import check_run
+    n, E = 8, 3000
+    dag = random_gossip(n, E, seed=12, forkers=2, fork_p=0.05, cascade_p=0.5)
+    calls = schedule(len(dag["creator"]), n)
+    o, st, order, counts = replay(dag, calls)
+    m = int((st >= 0).sum())
+    rounds = np.array([o.round(x) for x in range(m)])
+    wit = np.array([o.witness(x) for x in range(m)])
+    rr = np.array([o.round_received(x) if o.round_received(x) is not None else -1 for x in range(m)])
+    cts = np.array([o.consensus_timestamp(x) if rr[x] >= 0 else 0 for x in range(m)], np.int64)
+    check_run(dag, st, order, counts, rounds, wit, rr, cts)

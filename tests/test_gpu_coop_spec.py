@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 from babble_amd.gossip import random_gossip, schedule
-from parity import run_case
+from parity import compare_golden, load_golden, run_case
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -40,20 +40,10 @@ def _state(n, dag, calls, cap):
 def test_coop_spec_golden(monkeypatch, path, walkers):
     from babble_amd.engine import Engine
     monkeypatch.setenv("HGE_COOP_WALKERS", str(walkers))
-    g = np.load(path, allow_pickle=False)
-    n = int(g["n"])
-    dag = {k: g[k] for k in ("creator", "index", "sp", "op", "ts", "S", "hash", "ntx")}
-    dag["n"] = n
-    eng = Engine(n, len(g["creator"]) + 16)
+    dag, g = load_golden(path)
+    eng = Engine(int(g["n"]), len(dag["creator"]) + 16)
     try:
-        st, order, counts = eng.replay(dag, g["calls"])
-        np.testing.assert_array_equal(st, g["status"])
-        np.testing.assert_array_equal(order, g["order"])
-        np.testing.assert_array_equal(counts, g["counts"])
-        assert eng.rounds() == int(g["scalars"][0])
-        E = len(g["rounds"])
-        np.testing.assert_array_equal(np.array([eng.round(x) for x in range(E)]), g["rounds"])
-        np.testing.assert_array_equal(np.array([eng.witness(x) for x in range(E)]), g["witness"])
+        compare_golden(eng, dag, g)
     finally:
         eng.close()
 

@@ -1,0 +1,50 @@
+"""Full-size configurations on the GPU (BASELINE.json configs[2] and configs[3]
+on one MI355X): 64 participants / 1M events and 256 / 10M, K = N.
+
+The oracle cannot replay these sizes in test time, so parity is checked by
+  * the committed oracle golden of the first calls of the SAME stream
+    (tests/golden/bench_*_prefix.npz): the engine reproduces per-call
+    semantics, so the first calls' batches must be identical;
+  * size-independent properties of the reference's algorithm on the whole run:
+    the order is a set of distinct accepted events and the per-call batches
+    add up to it; inside every call's batch the ConsensusSorter keys
+    (roundReceived, consensus timestamp, S; consensus_sorter.go:36-59) strictly
+    increase; every ordered event was received after its round
+    (hashgraph.go:680-684) and every unordered one has no roundReceived;
+    Round(x) is ParentRound(x) or ParentRound(x) + 1 (hashgraph.go:287-305);
+    witnesses are exactly the first events of their round on their chain
+    (hashgraph.go:253-266).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from babble_amd.gossip import random_gossip, schedule
+from parity import check_run
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("n,E", [(64, 1_000_000), (256, 10_000_000)])
+def test_full_size(n, E):
+    from babble_amd.engine import Engine, events_array
+    K, seed = n, 1
+    dag = random_gossip(n, E, seed=seed)
+    calls = schedule(E, K)
+    eng = Engine(n, E)
+    try:
+        st, order, counts = eng.replay(events_array(dag), calls)
+        assert (st >= 0).all()
+        assert len(order) > 0.99 * E  # all but the last rounds' events are ordered
+        gp = np.load(os.path.join(ROOT, "tests", "golden", f"bench_n{n}_e{E}_k{K}_s{seed}_prefix.npz"))
+        nc = int(gp["n_calls"])
+        np.testing.assert_array_equal(counts[:nc], gp["counts"], err_msg="golden prefix batches")
+        np.testing.assert_array_equal(order[:len(gp["order"])], gp["order"], err_msg="golden prefix order")
+        rounds, wit = eng.event_rounds()
+        rr, cts = eng.event_received()
+        check_run(dag, st, order, counts, rounds, wit, rr, cts)
+    finally:
+        eng.close()
+

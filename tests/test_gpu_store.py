@@ -1,0 +1,183 @@
+"""Coordinates, predicates, Store semantics and sync-path reads of the HIP engine
+against the oracle and the reference's container semantics.
+
+* every event's lastAncestors / firstDescendants row (hge_coordinates) equals
+  the oracle's (InitEventCoordinates / UpdateAncestorFirstDescendant,
+  hashgraph.go:399-494), on the small-N path and on the wide (N > 32) path;
+* the predicates the reference's tests call (hashgraph.go:83-326) agree with
+  the oracle on random pairs;
+* Store.ParticipantEvents / ParticipantEvent / LastFrom / ConsensusEvents follow
+  the RollingList window and ErrTooLate (caches.go:45-97,
+  common/rolling_list.go:42-67), Core.Diff's selection (node/core.go:108-132)
+  and ReadWireInfo's parent resolution (hashgraph.go:526-571);
+* admission refuses chains beyond the wide kernels' capacity and the engine
+  stays usable; replay call points are validated.
+"""
+import numpy as np
+import pytest
+
+from babble_amd.gossip import random_gossip, schedule
+from oracle.oracle import replay as oracle_replay
+
+pytestmark = pytest.mark.gpu
+INT64_MAX = np.iinfo(np.int64).max
+INT32_MAX = np.iinfo(np.int32).max
+
+
+def engine_replay(n, dag, k, cap=None):
+    from babble_amd.engine import Engine
+    eng = Engine(n, cap or len(dag["creator"]) + 64)
+    st, order, counts = eng.replay(dag, schedule(len(dag["creator"]), k))
+    return eng, st, order, counts
+
+
+@pytest.mark.parametrize("n,events,k", [(4, 600, 4), (16, 2500, 16), (40, 5000, 40), (64, 6000, 64)])
+def test_coordinates_match_oracle(n, events, k):
+    dag = random_gossip(n, events, seed=300 + n)
+    o, ost, oorder, _ = oracle_replay(dag, schedule(events, k))
+    eng, st, order, _ = engine_replay(n, dag, k)
+    try:
+        np.testing.assert_array_equal(st, ost)
+        for x in range(events):
+            la, fd = eng.coordinates(x)
+            ola, _, ofd, _ = o.coords(x)
+            np.testing.assert_array_equal(la, ola, err_msg=f"lastAncestors of {x}")
+            fd64 = np.where(fd == INT32_MAX, INT64_MAX, fd.astype(np.int64))
+            np.testing.assert_array_equal(fd64, ofd, err_msg=f"firstDescendants of {x}")
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("n,events,k", [(5, 1200, 5), (16, 3000, 16), (48, 6000, 48)])
+def test_predicates_match_oracle(n, events, k):
+    dag = random_gossip(n, events, seed=900 + n)
+    o, _, _, _ = oracle_replay(dag, schedule(events, k))
+    eng, _, _, _ = engine_replay(n, dag, k)
+    rng = np.random.default_rng(n)
+    try:
+        # pairs near each other in time (where the answers are mixed) and anywhere
+        xs = rng.integers(0, events, 1500)
+        ys = np.clip(xs - rng.integers(0, 6 * n, 1500), 0, events - 1)
+        ys[::3] = rng.integers(0, events, len(ys[::3]))
+        for x, y in zip(xs.tolist(), ys.tolist()):
+            assert eng.ancestor(x, y) == o.ancestor(x, y), ("ancestor", x, y)
+            assert eng.self_ancestor(x, y) == o.self_ancestor(x, y), ("self_ancestor", x, y)
+            assert eng.see(x, y) == o.see(x, y), ("see", x, y)
+            assert eng.strongly_see(x, y) == o.strongly_see(x, y), ("strongly_see", x, y)
+            assert eng.oldest_self_ancestor_to_see(x, y) == o.oldest_self_ancestor_to_see(x, y), ("osa", x, y)
+        for x in rng.integers(0, events, 300).tolist():
+            assert eng.parent_round(x) == o.parent_round(x), ("parent_round", x)
+            assert eng.round_inc(x) == o.round_inc(x), ("round_inc", x)
+            assert eng.round(x) == o.round(x), ("round", x)
+            assert eng.witness(x) == o.witness(x), ("witness", x)
+        # the bulk reads equal the per-event ones
+        r, w = eng.event_rounds()
+        np.testing.assert_array_equal(r, [o.round(x) for x in range(events)])
+        np.testing.assert_array_equal(w, [o.witness(x) for x in range(events)])
+        rr, cts = eng.event_received()
+        for x in o.consensus_events().tolist():
+            assert rr[x] == o.round_received(x) and cts[x] == o.consensus_timestamp(x)
+    finally:
+        eng.close()
+
+
+def rolling_model(items, size):
+    """common/rolling_list.go:55-67: (window, tot)."""
+    win, tot = [], 0
+    for it in items:
+        if size > 0 and len(win) >= 2 * size:
+            win = win[size:]
+        win.append(it)
+        tot += 1
+    return win, tot
+
+
+@pytest.mark.parametrize("size", [0, 7, 50])
+def test_store_windows_and_sync_reads(size):
+    from babble_amd.engine import HgeError
+    n, events, k = 6, 1500, 6
+    dag = random_gossip(n, events, seed=17)
+    o, _, oorder, _ = oracle_replay(dag, schedule(events, k))
+    eng, st, order, _ = engine_replay(n, dag, k)
+    try:
+        eng.set_cache_size(size)
+        chains = [np.nonzero(dag["creator"] == c)[0] for c in range(n)]
+        for c in range(n):
+            win, tot = rolling_model(chains[c].tolist(), size)
+            oldest = tot - len(win)
+            for skip in (0, oldest - 1, oldest, tot - 3, tot - 1, tot, tot + 5):
+                if skip < 0:
+                    continue
+                if skip < oldest and skip < tot:
+                    with pytest.raises(HgeError) as ei:
+                        eng.participant_events(c, skip)
+                    assert ei.value.code == -11  # ErrTooLate
+                else:
+                    assert eng.participant_events(c, skip).tolist() == chains[c][skip:].tolist()
+            assert eng.last_from(c) == chains[c][-1]
+            assert eng.participant_event(c, tot - 1) == chains[c][-1]
+            with pytest.raises(HgeError):
+                eng.participant_event(c, tot)  # not found
+        # ConsensusEvents: the rolling window of the consensus list
+        win, tot = rolling_model(oorder.tolist(), size)
+        assert eng.consensus_events().tolist() == win
+        assert eng.consensus_log().tolist() == oorder.tolist()
+        # Core.Diff: what we know beyond `known`, in topological (insertion) order
+        known = np.array([len(ch) - 3 for ch in chains], np.int32)
+        exp = sorted(x for c in range(n) for x in chains[c][known[c]:].tolist())
+        assert eng.diff(known).tolist() == exp
+        # wire info and its inverse (ReadWireInfo)
+        oldest = []
+        for c in range(n):
+            win, tot = rolling_model(chains[c].tolist(), size)
+            oldest.append(tot - len(win))
+        for x in range(0, events, 37):
+            wi = eng.wire_info(x)
+            assert wi == o.wire_info(x)
+            if (wi[0] >= 0 and wi[0] < oldest[wi[3]]) or (wi[2] >= 0 and wi[2] < oldest[wi[1]]):
+                with pytest.raises(HgeError) as ei:  # ParticipantEvent below the window
+                    eng.read_wire_parents(wi[3], wi[0], wi[1], wi[2])
+                assert ei.value.code == -11
+                continue
+            sp, op = eng.read_wire_parents(wi[3], wi[0], wi[1], wi[2])
+            assert (sp, op) == (int(dag["sp"][x]), int(dag["op"][x]))
+    finally:
+        eng.close()
+
+
+def test_chain_capacity_refused_at_admission(monkeypatch):
+    """Wide graphs keep chain positions as uint16 in the rounds kernels: a chain
+    past the limit is refused at admission (HGE_ERR_CAPACITY) and the engine
+    keeps working (HGE_CHAIN_LIMIT lowers the limit to force the boundary)."""
+    from babble_amd.engine import Engine, HgeError, events_array
+    monkeypatch.setenv("HGE_CHAIN_LIMIT", "40")
+    n, events = 36, 2000
+    dag = random_gossip(n, events, seed=5)
+    ev = events_array(dag)
+    eng = Engine(n, 4096)
+    try:
+        with pytest.raises(HgeError) as ei:
+            eng.insert_events(ev)
+        assert ei.value.code == -7
+        acc = len(ei.value.accepted)
+        assert acc > n and eng.event_count() == acc
+        first = eng.run_consensus()  # still usable after the refusal
+        assert eng.rounds() > 0
+        assert len(first) >= 0
+    finally:
+        eng.close()
+
+
+def test_replay_rejects_bad_call_points():
+    from babble_amd.engine import Engine, HgeError, events_array
+    dag = random_gossip(4, 200, seed=2)
+    eng = Engine(4, 512)
+    try:
+        for cp in ([0, 10], [10, 10], [20, 10], [10, 201]):
+            with pytest.raises(HgeError) as ei:
+                eng.prepare(events_array(dag), cp)
+            assert ei.value.code == -8
+        st, order, counts = eng.replay(dag, [50, 100, 200])
+        assert len(counts) == 3
+    finally:
+        eng.close()
