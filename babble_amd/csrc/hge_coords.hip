@@ -118,6 +118,140 @@ __global__ void __launch_bounds__(256) k_la_sweep(Tables t, const int2* segs, in
   if (__ballot(ch) && (threadIdx.x & 63) == __builtin_ctzll(__ballot(ch))) *changed = 1;
 }
 
+// ---------------------------------------------------------------------------
+// Packed 16-bit sweeps (N > 32, where chains are capped at 65,534 events):
+// the fixed-point sweeps run on LA16, a table of (LA + 1) as uint16 pairs
+// (NW2 = ceil(N / 2) words per row, -1 -> 0), so every sweep streams half the
+// bytes of the int32 sweep; k_transpose16 then writes the int32 LA rows and the
+// LAT tiles from it in one pass.  Same segments, order and fixed-point argument
+// as k_la_sweep: max over packed halves is max over each column.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ size_t rowoff16(const Tables& t, int c, int p) {
+  return ((size_t)c * t.ccap + p) * (size_t)t.NW2;
+}
+
+__global__ void k_la_clear16(Tables t, const int32_t* olen, const int32_t* len, int32_t* zero, int nzero) {
+  const int j = blockIdx.y;
+  const int W = t.NW2;
+  if (j == 0 && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < nzero; i += blockDim.x) zero[i] = 0;
+  const int64_t lo = (int64_t)olen[j] * W, hi = (int64_t)len[j] * W;
+  uint32_t* base = t.LA16 + (size_t)j * t.ccap * W;
+  for (int64_t e = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < hi;
+       e += (int64_t)gridDim.x * blockDim.x)
+    base[e] = 0u;
+}
+
+template <int NP>  // NP lanes (packed words) per segment
+__global__ void __launch_bounds__(256) k_la_sweep16(Tables t, const int2* segs, int nseg, int SEG,
+                                                    const int32_t* len, const int32_t* prev,
+                                                    int32_t* changed) {
+  constexpr int G = 256 / NP;
+  constexpr int SEGMAX = 64;
+  constexpr int U = 32;  // loads in flight per lane and batch
+  __shared__ int64_t s_off[G][SEGMAX];
+  if (prev && *prev == 0) return;  // converged: the flag stays 0
+  const int W = t.NW2;
+  const int g = threadIdx.x / NP, i = threadIdx.x - (threadIdx.x / NP) * NP;
+  const int sidx = blockIdx.x * G + g;
+  const bool valid = sidx < nseg;
+  int j = 0, k0 = 0, k1 = 0;
+  if (valid) {
+    const int2 sg = segs[sidx];
+    j = sg.x;
+    k0 = sg.y;
+    k1 = min(k0 + SEG, len[j]);
+  }
+  for (int kk = i; kk < SEG; kk += NP) {
+    int64_t off = -1;
+    if (valid && k0 + kk < k1) {
+      const int2 o = t.opcp[(size_t)j * t.ccap + k0 + kk];
+      if (o.x >= 0) off = (int64_t)rowoff16(t, o.x, o.y);
+    }
+    s_off[g][kk] = off;
+  }
+  __syncthreads();
+  const bool act = valid && i < W;
+  bool ch = false;
+  if (act) {
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    // the own column j lives in word j / 2, half j & 1
+    const bool ownw = i == (j >> 1);
+    const int own_shift = (j & 1) * 16;
+    const size_t own0 = rowoff16(t, j, k0) + i;
+    u16x2 v = (k0 > 0) ? __builtin_bit_cast(u16x2, t.LA16[own0 - W]) : u16x2{0, 0};
+    for (int kb = k0; kb < k1; kb += U) {
+      uint32_t a[U], old[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int k = kb + u;
+        a[u] = 0;
+        old[u] = 0;
+        if (k < k1) {
+          const int64_t off = s_off[g][k - k0];
+          if (off >= 0) a[u] = t.LA16[off + i];
+          old[u] = t.LA16[own0 + (size_t)(k - k0) * W];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int k = kb + u;
+        if (k < k1) {
+          v = __builtin_elementwise_max(v, __builtin_bit_cast(u16x2, a[u]));
+          if (ownw) v = __builtin_elementwise_max(v, __builtin_bit_cast(u16x2, (uint32_t)(k + 1) << own_shift));
+          const u16x2 nv = __builtin_elementwise_max(v, __builtin_bit_cast(u16x2, old[u]));
+          v = nv;
+          const uint32_t nw = __builtin_bit_cast(uint32_t, nv);
+          if (nw != old[u]) {
+            t.LA16[own0 + (size_t)(k - k0) * W] = nw;
+            ch = true;
+          }
+        }
+      }
+    }
+  }
+  if (__ballot(ch) && (threadIdx.x & 63) == __builtin_ctzll(__ballot(ch))) *changed = 1;
+}
+
+// LA16 -> LA (int32 rows) and LAT (transposed), for positions [plo_j, len_j)
+// of every chain: one pass over the packed table (k_transpose mode 0's tiles)
+__global__ void __launch_bounds__(256) k_transpose16(Tables t, int32_t* LAT, const int32_t* plo,
+                                                     const int32_t* len) {
+  __shared__ int32_t tile[64][65];
+  const int N = t.N;
+  const size_t ccap = t.ccap;
+  const int a = blockIdx.z;  // chain j
+  const int p0 = plo[a] + blockIdx.x * 64;
+  const int pend = len[a];
+  if (p0 >= pend) return;
+  const int c0 = blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+  // rows (a, p): 32 packed words = 64 columns [c0, c0 + 64); lanes 0..31 take one word
+  // of row r, lanes 32..63 the same word of row r + 1
+  for (int r = 2 * ty; r < 64; r += 8) {
+    const int rr = r + (tx >> 5), w = tx & 31;
+    const int p = p0 + rr, c = c0 + 2 * w;
+    if (p < pend && c < N) {
+      const uint32_t x = t.LA16[rowoff16(t, a, p) + (c >> 1)];
+      const int lo = (int)(x & 0xFFFFu) - 1, hi = (int)(x >> 16) - 1;
+      tile[rr][2 * w] = lo;
+      tile[rr][2 * w + 1] = hi;
+      int32_t* dst = t.LA + rowoff(t, a, p) + c;
+      if ((N & 1) == 0) {
+        *(int2*)dst = make_int2(lo, hi);  // 8-byte aligned: even row stride, even c
+      } else {
+        dst[0] = lo;
+        if (c + 1 < N) dst[1] = hi;
+      }
+    }
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const int c = c0 + r, p = p0 + tx;
+    if (c < N && p < pend) LAT[((size_t)a * N + c) * ccap + p] = tile[tx][r];
+  }
+}
+
 // Tiled transposes through LDS (64 x 64 tiles, 256 threads).
 //   mode 0: LA[(j,k)][c] -> LAT[j][c][k] for k in [klo_j, len_j)
 //   mode 1: FDT[j][c][q] -> FD[(c,q)][j] for q in [qlo_c, len_c)

@@ -24,6 +24,7 @@
 #include "hge_kernels.hip"
 #include "hge_coords.hip"
 #include "hge_rounds_coop.hip"
+#include "hge_rounds_direct.hip"
 #include "hge_walk_spec.hip"
 
 using namespace hge;
@@ -135,6 +136,7 @@ struct hge_engine {
   DBuf<uint64_t> d_S;
   DBuf<uint8_t> d_coin, d_wit;
   DBuf<int32_t> d_chain, d_LA, d_FD, d_FSS;
+  DBuf<uint32_t> d_LA16;  // N > 32: the sweeps' packed (LA + 1) table (hge_coords.hip)
   DBuf<int2> d_opcp;  // [N][ccap] other-parent coordinates (k_chain_fill)
   DBuf<int64_t> d_tsch;  // [N][ccap] timestamps in chain layout (k_chain_fill)
   DBuf<int32_t> d_C, d_W, d_rcnt, d_minw;
@@ -166,6 +168,7 @@ struct hge_engine {
     return coop_spec_bs == 1024 ? (const void*)k_rounds_coop_spec<1024> : (const void*)k_rounds_coop_spec<512>;
   }
   DBuf<uint64_t> s_cH, s_cS, s_cT, s_cM;  // speculative wide walk: rows, ssc bits, tables, merges
+  DBuf<uint32_t> s_mb;                    // direct rounds: staged member rows (two parity blocks)
   DBuf<int32_t> s_cn;
   uint32_t coop_epoch = 0;
 
@@ -214,6 +217,8 @@ struct hge_engine {
     t.opcp = d_opcp.p;
     t.tsch = d_tsch.p;
     t.LA = d_LA.p;
+    t.NW2 = (N + 1) / 2;
+    t.LA16 = d_LA16.p;
     t.FD = d_FD.p;
     t.round = d_round.p;
     t.wit = d_wit.p;
@@ -340,6 +345,7 @@ struct hge_engine {
     s_keys2.free_();
     d_opcp.free_();
     d_tsch.free_();
+    d_LA16.free_();
     d_ssc.free_();
     s_gran.free_();
     s_cH.free_();
@@ -347,6 +353,10 @@ struct hge_engine {
     s_cT.free_();
     s_cM.free_();
     s_cn.free_();
+    s_mb.free_();
+    s_hist.free_();
+    s_hstate.free_();
+    s_hssc.free_();
     if (pin) (void)hipHostFree(pin);
     pin = nullptr;
     pin_cap = pin_used = 0;
@@ -420,6 +430,18 @@ struct hge_engine {
     d_tsch.p = tsch;
     d_tsch.n = (size_t)N * nc;
     grow_chain_table(d_LA, nc, true);
+    if (sweep16()) {
+      const size_t w = (size_t)(N + 1) / 2;
+      uint32_t* q = nullptr;
+      HIPCHK(hipMalloc(&q, sizeof(uint32_t) * (size_t)N * nc * w));
+      if (ccap > 0 && d_LA16.p)
+        HIPCHK(hipMemcpy2DAsync(q, sizeof(uint32_t) * nc * w, d_LA16.p, sizeof(uint32_t) * ccap * w,
+                                sizeof(uint32_t) * ccap * w, N, hipMemcpyDeviceToDevice, st));
+      sync();
+      d_LA16.free_();
+      d_LA16.p = q;
+      d_LA16.n = (size_t)N * nc * w;
+    }
     grow_chain_table(d_FD, nc, true);
     // first-strong-seer rows (N <= 32): int32 rows of N, or uint16 rows padded to
     // 16/32 columns for the LDS walk; rebuilt from the frontier on, never kept
@@ -632,12 +654,29 @@ struct hge_engine {
   }
 
   // ---------------- coordinates + rounds for [n_coords, n_events) ----------------
+  // coordinates + rounds for [n_coords, n_events): coords_a (sweeps and
+  // transposes) then coords_b (the rounds frontier and what follows).  The
+  // cross-GPU split (hge_split_*) runs a walker between the two.
+  bool cs_pending = false, cs_fresh = false;
+  std::chrono::steady_clock::time_point w_start;
+  // cross-GPU split: the joined frontier rows of the walkers (hge_split_finish)
+  bool ext_on = false, ext_natural = false;
+  int ext_rows = 0;
+  std::vector<int32_t> ext_C;
+  std::vector<uint64_t> ext_ssc;
+  DBuf<int32_t> s_hist, s_hstate;
+  DBuf<uint64_t> s_hssc;
+  int64_t cs_n0 = 0, cs_n1 = 0;
+  int cs_tot0 = 0;
   void coords() {
+    if (!coords_a()) return;
+    coords_b();
+  }
+  bool coords_a() {
     upload();
     const int64_t n0 = n_coords, n1 = n_events;
-    if (n1 == n0) return;
+    if (n1 == n0) return false;
     Tables t = tables();
-    const int m = (int)(n1 - n0);
     // control block (one upload): round state, chain lengths, transpose bounds,
     // fss offsets of a fresh walk and the sweep segments
     // segment length: latency-bound sweeps (small N) like short segments, bandwidth-bound
@@ -682,8 +721,22 @@ struct hge_engine {
     k_qlo = s_kctl.p + o_qlo;
     k_lo = s_kctl.p + o_lo;
     k_segs = (int2*)(s_kctl.p + o_seg);
-    KLAUNCH(k_chain_fill, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0, (int)n1);
+    KLAUNCH(k_chain_fill, dim3(div_up((int)(n1 - n0), 256)), dim3(256), 0, st, t, (int)n0, (int)n1);
     coords_sweep(t, (int)segs.size(), SEG, maxnew, fresh);
+    cs_pending = true;
+    cs_fresh = fresh;
+    cs_n0 = n0;
+    cs_n1 = n1;
+    cs_tot0 = tot0;
+    return true;
+  }
+  void coords_b() {
+    cs_pending = false;
+    const bool fresh = cs_fresh;
+    const int64_t n0 = cs_n0, n1 = cs_n1;
+    const int tot0 = cs_tot0;
+    const int m = (int)(n1 - n0);
+    Tables t = tables();
     // rounds frontier
     for (bool retry = false;; retry = true) {
       int32_t rs[3] = {R, 0, 0};
@@ -880,6 +933,15 @@ struct hge_engine {
     return hipLaunchKernel(fn, grid, block, args, 0, st);
   }
 
+  // Wide rounds step: strongly-see tiles on the coordinate rows
+  // (hge_rounds_direct.hip) for N % 4 == 0, else the FDT-gather selection of
+  // hge_rounds_coop.hip; HGE_ROUNDS_STEP=fss forces the latter.
+  bool direct_rounds() const {
+    const char* e = getenv("HGE_ROUNDS_STEP");
+    if (e && strcmp(e, "fss") == 0) return false;
+    return (N & 3) == 0;
+  }
+
   // rounds of a wide hashgraph: cooperative frontier kernel (hge_rounds_coop.hip)
   void rounds_coop(bool fresh) {
     Tables t = tables();
@@ -913,6 +975,24 @@ struct hge_engine {
     const int32_t* len = k_len + N;
     int32_t* rstate = k_rs;
     int32_t* err = s_bar.p + 1;
+    if (ext_on && fresh && rlo == 0 && Rprev == 0) {
+      // frontier rows joined from the walkers of all ranks (babble_amd/dist.py)
+      const int K = ext_rows;  // true rows 0 .. K-1
+      if (K + 1 >= Rcap) {  // the rounds table must hold them: overflow, grow, come back
+        int32_t ov[2] = {0, 1};
+        h2d(rstate, ov, 8);
+        return;
+      }
+      ext_on = false;
+      h2d(d_C.p, ext_C.data(), sizeof(int32_t) * (size_t)K * N);
+      if (K > 1) h2d(d_ssc.p + (size_t)N * NW, ext_ssc.data() + (size_t)N * NW, sizeof(uint64_t) * (size_t)(K - 1) * N * NW);
+      if (ext_natural) {  // the walk ended: row K is the empty frontier
+        int32_t rs0 = K;
+        h2d(rstate, &rs0, 4);
+        return;
+      }
+      rlo = K - 1;  // the sequential walk resumes from the last true row
+    }
     const int nw = (fresh && rlo == 0 && Rprev == 0) ? coop_walkers() : 0;
     if (nw >= 2) {
       const char* hc = getenv("HGE_WALK_HCAP");  // tests: force the capacity fallback
@@ -973,14 +1053,39 @@ struct hge_engine {
     uint64_t* gran = s_gran.p;
     uint64_t* ssc = d_ssc.p;
     uint64_t* dbg = dbg_p();
-    void* args[] = {&t, &FDT, &olen, &len, &rstate, &rlo, &Rprev, &gran, &err, &ssc, &dbg};
-    prof_begin("k_rounds_coop");
-    HIPCHK(launch_resident((const void*)k_rounds_coop, dim3(N), dim3(COOP_BS), args));
-    prof_end();
+    if (direct_rounds()) {
+      // strongly-see tiles on the coordinate rows (hge_rounds_direct.hip)
+      const int npow = N <= 64 ? 64 : N <= 128 ? 128 : 256;
+      s_mb.need((size_t)npow * npow);  // two parity blocks of npow rows x npow/2 packed words
+      uint32_t* mb = s_mb.p;
+      const int32_t* nostart = nullptr;
+      int32_t* nohist = nullptr;
+      int hmax = 0, extra = 0;
+      void* dargs[] = {&t, &olen, &len, &rstate, &rlo, &Rprev, &gran, &err, &ssc, &mb, &dbg,
+                       &nostart, &nohist, &hmax, &nostart, &extra};
+      const void* fn = N <= 64 ? (const void*)k_rounds_direct<1024, 64>
+                     : N <= 128 ? (const void*)k_rounds_direct<1024, 128>
+                                : (const void*)k_rounds_direct<1024, 256>;
+      prof_begin("k_rounds_direct");
+      HIPCHK(launch_resident(fn, dim3(N), dim3(1024), dargs));
+      prof_end();
+    } else {
+      void* args[] = {&t, &FDT, &olen, &len, &rstate, &rlo, &Rprev, &gran, &err, &ssc, &dbg};
+      prof_begin("k_rounds_coop");
+      HIPCHK(launch_resident((const void*)k_rounds_coop, dim3(N), dim3(COOP_BS), args));
+      prof_end();
+    }
     int32_t e = 0;
     readback(&e, s_bar.p + 1, 1);
     if (e) throw EngineError(HGE_ERR_DEVICE, "rounds frontier hand-off timed out");
     dbg_dump();
+  }
+
+  // N > 32: the sweeps run on the packed 16-bit table (chains are capped at
+  // 65,534 events there); HGE_SWEEP16=0 keeps the int32 sweeps
+  bool sweep16() const {
+    const char* e = getenv("HGE_SWEEP16");
+    return N > 32 && !(e && atoi(e) == 0);
   }
 
   // coordinates: chain-prefix sweeps + transposes (hge_coords.hip)
@@ -992,26 +1097,46 @@ struct hge_engine {
     // (a sweep after a quiet one returns at once); k_la_clear zeroes the flags
     const int MAXSW = 4096;
     s_chg.need(MAXSW);
-    KLAUNCH(k_la_clear, dim3(std::max(1, std::min(64, div_up((int64_t)maxnew * N, 256))), N),
-            dim3(256), 0, st, t, olen, len, s_chg.p, MAXSW);
-    const int NPt = N <= 16 ? 16 : N <= 32 ? 32 : N <= 64 ? 64 : N <= 128 ? 128 : 256;
+    const bool p16 = sweep16();
+    if (p16)
+      KLAUNCH(k_la_clear16, dim3(std::max(1, std::min(64, div_up((int64_t)maxnew * t.NW2, 256))), N),
+              dim3(256), 0, st, t, olen, len, s_chg.p, MAXSW);
+    else
+      KLAUNCH(k_la_clear, dim3(std::max(1, std::min(64, div_up((int64_t)maxnew * N, 256))), N),
+              dim3(256), 0, st, t, olen, len, s_chg.p, MAXSW);
+    const int NPt = p16 ? (t.NW2 <= 32 ? 32 : t.NW2 <= 64 ? 64 : 128)
+                        : (N <= 16 ? 16 : N <= 32 ? 32 : N <= 64 ? 64 : N <= 128 ? 128 : 256);
     int sw = 0;
     for (int group = 12;; group = 8) {
       for (int g = 0; g < group; g++, sw++) {
         if (sw >= MAXSW) throw EngineError(HGE_ERR_INTERNAL, "lastAncestors sweeps did not converge");
         const int32_t* prev = sw > 0 ? s_chg.p + sw - 1 : nullptr;
-        switch (NPt) {
+        if (p16) {
+          switch (NPt) {
+#define SW16(NPV)                                                                                \
+  case NPV:                                                                                      \
+    KLAUNCH(k_la_sweep16<NPV>, dim3(div_up(nseg, 256 / NPV)), dim3(256), 0, st, t, k_segs, nseg, \
+            SEG, len, prev, s_chg.p + sw);                                                       \
+    break;
+            SW16(32)
+            SW16(64)
+            SW16(128)
+#undef SW16
+          }
+        } else {
+          switch (NPt) {
 #define SW(NPV)                                                                                  \
   case NPV:                                                                                      \
     KLAUNCH(k_la_sweep<NPV>, dim3(div_up(nseg, 256 / NPV)), dim3(256), 0, st, t, k_segs, nseg,   \
             SEG, len, prev, s_chg.p + sw);                                                       \
     break;
-          SW(16)
-          SW(32)
-          SW(64)
-          SW(128)
-          SW(256)
+            SW(16)
+            SW(32)
+            SW(64)
+            SW(128)
+            SW(256)
 #undef SW
+          }
         }
       }
       std::vector<int32_t> flags(sw);
@@ -1022,9 +1147,13 @@ struct hge_engine {
         break;
       }
     }
-    // LA -> LAT for positions [olen-1, len)
-    KLAUNCH(k_transpose, dim3(div_up(maxnew + 1, 64), div_up(N, 64), N), dim3(256), 0, st, t,
-            (const int32_t*)nullptr, d_LAT.p, k_plo, len, 0);
+    // LA -> LAT for positions [olen-1, len) (LA16 -> LA and LAT in one pass)
+    if (p16)
+      KLAUNCH(k_transpose16, dim3(div_up(maxnew + 1, 64), div_up(N, 64), N), dim3(256), 0, st, t,
+              d_LAT.p, k_plo, len);
+    else
+      KLAUNCH(k_transpose, dim3(div_up(maxnew + 1, 64), div_up(N, 64), N), dim3(256), 0, st, t,
+              (const int32_t*)nullptr, d_LAT.p, k_plo, len, 0);
     // FDT: clear the new positions, then the runs of the new events
     KLAUNCH(k_fdt_clear, dim3(div_up(maxnew, 256), N, N), dim3(256), 0, st, t, d_FDT.p, olen, len);
     KLAUNCH(k_fdt_runs, dim3(div_up(maxnew, 256), N, N), dim3(256), 0, st, t, d_LAT.p, d_FDT.p,
@@ -1236,7 +1365,7 @@ struct hge_engine {
         s_recv.need(ncand);
         s_rr.need(ncand);
         s_cts.need(ncand);
-        recv_dispatch(t, cand, ncand, ncalls, rr_lo, R_last);
+        recv_dispatch(t, cand, ncand, ncalls, rr_lo, R_last, fresh_und);
       } else {
         s_recv.need(ncand);
         HIPCHK(hipMemsetAsync(s_recv.p, 0xFF, 4 * ncand, st));
@@ -1385,9 +1514,14 @@ struct hge_engine {
   }
 
   void recv_dispatch(const Tables& t, const int32_t* cand, int ncand, int ncalls, int rr_lo,
-                     int R_last) {
-    // N > 16: the median is a wave-wide radix select (k_median_wave)
+                     int R_last, bool fresh) {
+    // N > 16: the median is a wave-wide radix select (k_median_wave).  A fresh
+    // replay's candidates are every event in id order (candidate q = event q),
+    // so the waves can walk the chain table instead (HGE_MEDIAN_ORDER=id: not)
     const bool wmed = N > 16;
+    static const bool by_id = getenv("HGE_MEDIAN_ORDER") && strcmp(getenv("HGE_MEDIAN_ORDER"), "id") == 0;
+    const bool chain_order = !by_id && fresh && cand == d_und.p && (int64_t)ncand == n_events &&
+                             (int64_t)N * ccap < INT32_MAX;
     int32_t* bseg = nullptr;
     if (wmed) {
       s_bseg.need(ncand);
@@ -1401,9 +1535,13 @@ struct hge_engine {
                        s_segcnt.p,                                                               \
                        s_segcall.p, s_segdec.p, s_segfws.p, s_theta.p, s_recv.p, s_rr.p,         \
                        s_cts.p, bseg);                                                           \
-    if (wmed)                                                                                    \
+    if (wmed && chain_order)                                                                     \
+      KLAUNCH(k_median_chain<B>, dim3(div_up((int64_t)N * div_up(ccap, MC_S), 4)), dim3(256), 0,  \
+              st, t, (const int32_t*)k_len + N, div_up(ccap, MC_S), s_recv.p, s_rr.p, bseg,      \
+              s_segfws.p, s_cts.p);                                                              \
+    else if (wmed)                                                                               \
       KLAUNCH(k_median_wave<B>, dim3(div_up(ncand, 4)), dim3(256), 0, st, t, cand, ncand,        \
-              s_recv.p, s_rr.p, bseg, s_segfws.p, s_cts.p);                                      \
+              s_recv.p, s_rr.p, bseg, s_segfws.p, s_cts.p, (const int32_t*)nullptr, ncand);      \
     break;
       RCASE(1)
       RCASE(2)
@@ -1596,10 +1734,11 @@ int hge_replay_prepare(hge_engine* h, const hge_event* ev, int64_t n_sub,
   GUARD_END(h)
 }
 
-int hge_replay_run(hge_engine* h, int64_t* n_ordered) {
-  GUARD_BEGIN
+// A fresh replay in two halves: replay_begin (reset + coordinates) and
+// replay_end (rounds frontier, DivideRounds/DecideFame/FindOrder at every call);
+// the cross-GPU split runs the walkers and their join between the two.
+static void replay_begin(hge_engine* h) {
   // fresh consensus state over the staged events (they stay resident in HBM)
-  const int64_t keep = h->n_events;
   h->n_coords = h->n_divided = 0;
   h->coords_len.assign(h->N, 0);
   h->R = 0;
@@ -1609,10 +1748,16 @@ int hge_replay_run(hge_engine* h, int64_t* n_ordered) {
   h->ctx = 0;
   h->consensus.clear();
   h->n_und = 0;
-  const auto w0 = std::chrono::steady_clock::now();
+  h->ext_on = false;
+  h->w_start = std::chrono::steady_clock::now();
   h->reset_rounds();
   HIPCHK(hipEventRecord(h->ev[0], h->st));
-  h->coords();
+  h->coords_a();
+}
+
+static void replay_end(hge_engine* h, int64_t* n_ordered) {
+  const int64_t keep = h->n_events;
+  if (h->cs_pending) h->coords_b();
   HIPCHK(hipEventRecord(h->ev[1], h->st));
   const auto w1 = std::chrono::steady_clock::now();
   h->n_divided = keep;
@@ -1635,13 +1780,133 @@ int hge_replay_run(hge_engine* h, int64_t* n_ordered) {
   // [0] coordinates+rounds on the GPU, [1] their wall time, [2] consensus wall time,
   // [3] consensus on the GPU, [4] replay wall time, [6] GPU total
   h->stage_ms[0] = a;
-  h->stage_ms[1] = ms(w0, w1);
+  h->stage_ms[1] = ms(h->w_start, w1);
   h->stage_ms[2] = ms(w1, w2);
   h->stage_ms[3] = b;
-  h->stage_ms[4] = ms(w0, w2);
+  h->stage_ms[4] = ms(h->w_start, w2);
   h->stage_ms[6] = a + b;
   if (n_ordered) *n_ordered = (int64_t)h->consensus.size();
   h->dbg_dump();
+}
+
+int hge_replay_run(hge_engine* h, int64_t* n_ordered) {
+  GUARD_BEGIN
+  replay_begin(h);
+  replay_end(h, n_ordered);
+  return HGE_OK;
+  GUARD_END(h)
+}
+
+// ---- cross-GPU split of one hashgraph's rounds walk (babble_amd/dist.py) ----
+int hge_split_begin(hge_engine* h) {
+  GUARD_BEGIN
+  if (h->N <= 32 || !h->direct_rounds()) {
+    h->err = "the split walk needs the wide direct rounds path (N > 32, N % 4 == 0)";
+    return HGE_ERR_ARG;
+  }
+  replay_begin(h);
+  if (!h->cs_pending) {
+    h->err = "nothing staged (hge_replay_prepare first)";
+    return HGE_ERR_ARG;
+  }
+  return HGE_OK;
+  GUARD_END(h)
+}
+
+int hge_frontier_guess(hge_engine* h, int32_t part, int32_t nparts, int32_t* start_out) {
+  if (!start_out || nparts < 1 || part < 0 || part >= nparts) return HGE_ERR_ARG;
+  // part 0: the true first frontier (every chain's first event); part p: the time
+  // cut at event p * E / nparts (the first event of each chain inserted at or after it)
+  const int64_t T = h->n_events * (int64_t)part / nparts;
+  for (int c = 0; c < h->N; c++) {
+    const std::vector<int32_t>& ch = h->h_chain[c];
+    const size_t k = std::lower_bound(ch.begin(), ch.end(), (int32_t)T) - ch.begin();
+    start_out[c] = k < ch.size() ? (int32_t)k : INF32;
+  }
+  return HGE_OK;
+}
+
+int hge_frontier_walk(hge_engine* h, const int32_t* start, const int32_t* stopcut, int32_t extra,
+                      int32_t hmax, int32_t* rows_out, uint64_t* ssc_out, int32_t* nrows,
+                      int32_t* natural) {
+  GUARD_BEGIN
+  if (!h->cs_pending || !start || hmax < 2) return HGE_ERR_ARG;
+  const int N = h->N, NW = h->NW;
+  h->s_hist.need((size_t)hmax * N + N);
+  h->s_hssc.need((size_t)hmax * N * NW);
+  h->s_hstate.need(N + 4);
+  h->h2d(h->s_hstate.p, start, 4 * (size_t)N);
+  int32_t* cut = nullptr;
+  if (stopcut) {
+    h->s_hist.need((size_t)hmax * N + 2 * N);
+    cut = h->s_hist.p + (size_t)hmax * N + N;
+    h->h2d(cut, stopcut, 4 * (size_t)N);
+  }
+  int32_t* rstate = h->s_hstate.p + N;
+  HIPCHK(hipMemsetAsync(rstate, 0, 16, h->st));
+  h->s_bar.need(2);
+  h->s_gran.need(2 * (size_t)N);
+  HIPCHK(hipMemsetAsync(h->s_bar.p, 0, 8, h->st));
+  HIPCHK(hipMemsetAsync(h->s_gran.p, 0, 16 * (size_t)N, h->st));
+  const int npow = N <= 64 ? 64 : N <= 128 ? 128 : 256;
+  h->s_mb.need((size_t)npow * npow);
+  Tables t = h->tables();
+  const int32_t* olen = h->k_len;
+  const int32_t* len = h->k_len + N;
+  int rlo = 0, Rprev = 0;
+  uint64_t* gran = h->s_gran.p;
+  int32_t* err = h->s_bar.p + 1;
+  uint64_t* ssc = h->s_hssc.p;
+  uint32_t* mb = h->s_mb.p;
+  uint64_t* dbg = nullptr;
+  const int32_t* st0 = h->s_hstate.p;
+  int32_t* hist = h->s_hist.p;
+  int hm = hmax, ex = std::max(0, (int)extra);
+  void* args[] = {&t, &olen, &len, &rstate, &rlo, &Rprev, &gran, &err, &ssc, &mb, &dbg,
+                  &st0, &hist, &hm, &cut, &ex};
+  const void* fn = N <= 64 ? (const void*)k_rounds_direct<1024, 64>
+                 : N <= 128 ? (const void*)k_rounds_direct<1024, 128>
+                            : (const void*)k_rounds_direct<1024, 256>;
+  h->prof_begin("k_rounds_direct_walk");
+  HIPCHK(h->launch_resident(fn, dim3(N), dim3(1024), args));
+  h->prof_end();
+  int32_t rs[2] = {0, 0}, e = 0;
+  h->d2h(rs, rstate, 8);
+  h->d2h(&e, err, 4);
+  h->sync();
+  if (e) throw EngineError(HGE_ERR_DEVICE, "rounds frontier hand-off timed out");
+  const int n = std::max(1, std::min(rs[0], hmax));
+  if (rows_out) h->readback(rows_out, h->s_hist.p, (size_t)n * N);
+  if (ssc_out) h->readback(ssc_out, h->s_hssc.p, (size_t)n * N * NW);
+  if (nrows) *nrows = n;
+  if (natural) *natural = rs[1] == 0 ? 1 : 0;
+  return HGE_OK;
+  GUARD_END(h)
+}
+
+int hge_frontier_rows(hge_engine* h, int32_t from, int32_t n, int32_t* rows_out, uint64_t* ssc_out) {
+  GUARD_BEGIN
+  const int N = h->N, NW = h->NW;
+  if (from < 0 || n < 0 || (size_t)(from + n) * N > h->s_hist.n) return HGE_ERR_ARG;
+  if (rows_out && n) h->d2h(rows_out, h->s_hist.p + (size_t)from * N, 4 * (size_t)n * N);
+  if (ssc_out && n) h->d2h(ssc_out, h->s_hssc.p + (size_t)from * N * NW, 8 * (size_t)n * N * NW);
+  h->sync();
+  return HGE_OK;
+  GUARD_END(h)
+}
+
+int hge_split_finish(hge_engine* h, const int32_t* rows, const uint64_t* ssc, int32_t nrows,
+                     int32_t natural, int64_t* n_ordered) {
+  GUARD_BEGIN
+  if (!h->cs_pending || !rows || nrows < 1 || (nrows > 1 && !ssc)) return HGE_ERR_ARG;
+  const int N = h->N, NW = h->NW;
+  h->ext_on = true;
+  h->ext_natural = natural != 0;
+  h->ext_rows = nrows;
+  h->ext_C.assign(rows, rows + (size_t)nrows * N);
+  h->ext_ssc.assign((size_t)nrows * N * NW, 0);
+  if (nrows > 1) std::copy(ssc + (size_t)N * NW, ssc + (size_t)nrows * N * NW, h->ext_ssc.begin() + (size_t)N * NW);
+  replay_end(h, n_ordered);
   return HGE_OK;
   GUARD_END(h)
 }

@@ -1,0 +1,478 @@
+// hge_rounds_direct.hip — DivideRounds for wide hashgraphs (N > 32) by batched
+// strongly-see tiles: the frontier recurrence of DESIGN.md §4.2 evaluated
+// directly on the coordinate rows, one co-resident workgroup per chain.
+//
+//   C_{r+1}[c] = min { p >= C_r[c] : #{d : StronglySee((c, p), m_d)} >= SM },
+//   StronglySee(x, m) = #{i : LA[x][i] >= FD[m][i]} >= SM   (hashgraph.go:180-208)
+//
+// where m_d = (d, C_r[d]) are the round-r frontier members.  StronglySee is
+// monotone along a chain (LA rows only grow), so the first position is found
+// by bisection over a window of candidate rows of chain c.
+//
+// Per round and workgroup (target chain c):
+//   * thread (d, part) holds its slice of member row FD[m_d] in registers as
+//     packed uint16 (FD + 1, 0xFFFF = unset / no member);
+//   * the candidate rows LA[(c, p)], p in [C_r[c], C_r[c] + W), sit in LDS as
+//     packed uint16 (LA + 2), staged while the previous round's hand-off was in
+//     flight (they are chain c's own rows: known as soon as C_{r+1}[c] is);
+//   * a probe of position p is one pass of packed saturating subtractions
+//     (la + 2 -sat m + 1 > 0  <=>  la >= m) over the member slice, a sum over
+//     the TPM lanes of a member, a wave ballot of the members that pass and
+//     one LDS add per wave: a W x N x N strongly-see tile costs log2(W) + 1
+//     probes, all compares on registers and LDS (no gathers).
+// The strongly-see bits of the selected event against every member (ssc: the
+// vote adjacency k_witness_bits consumes) are one more probe.
+//
+// The frontier hand-off between workgroups is the granule protocol of
+// hge_rounds_coop.hip (8-byte {epoch, value} granules, relaxed agent-scope
+// stores and loads, double-buffered by round parity; cdna_hip_programming.md
+// Guideline 16, R2).  Chain positions must fit uint16 with room for the +2
+// encoding: chains are capped at 65,534 events at admission.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hge {
+
+constexpr int DIR_W = 64;   // candidate rows staged per window
+constexpr int DIR_MAXP = 16;  // probe counters per window (2 + log2(DIR_W) are used)
+
+template <int BS, int NPOW>
+struct DirGeo {
+  static constexpr int TPM = BS / NPOW;       // threads per member
+  static constexpr int CPT = NPOW / TPM;      // columns per thread (NPOW^2 / BS)
+  static constexpr int CW = CPT / 2;          // packed words per thread
+  static constexpr int VW = (CW % 4 == 0) ? 4 : 2;  // words per LDS read (b128 / b64)
+  static constexpr int PS = CW + VW;          // LDS words per (row, part): parts on distinct banks
+  static constexpr int RS = TPM * PS;         // LDS words per candidate row
+  static constexpr int WIN_INTS = DIR_W * NPOW;      // ints of a full window (N = NPOW)
+  static constexpr int PREF = (WIN_INTS / 4 + BS - 1) / BS;  // int4 per thread
+  static constexpr int MBW = NPOW / 2;        // staged member row: packed words
+};
+
+template <int BS, int NPOW>
+struct DirLDS {
+  int sP[256];
+  uint32_t sLA[DIR_W * DirGeo<BS, NPOW>::RS] __attribute__((aligned(16)));
+  int sCnt[DIR_MAXP];
+  uint32_t sBits[8];
+  int s_stop, s_past;
+};
+
+__device__ __forceinline__ uint32_t dir_pack_la(int a, int b) {
+  return (uint32_t)(a + 2) | ((uint32_t)(b + 2) << 16);
+}
+__device__ __forceinline__ uint32_t dir_pack_fd(int a, int b) {
+  const uint32_t lo = a == INF32 ? 0xFFFFu : (uint32_t)(a + 1);
+  const uint32_t hi = b == INF32 ? 0xFFFFu : (uint32_t)(b + 1);
+  return lo | (hi << 16);
+}
+
+// The candidate rows live in an LDS ring of DIR_W rows: row p of chain c sits in
+// slot p % DIR_W, and the ring holds [lo, lo + DIR_W) for the current lo.  Moving
+// the window from lo to lo' only fetches rows [max(lo + W, lo'), lo' + W): ~EPR/N
+// rows per round instead of W.
+// dir_fetch: rows [p0, p0 + nr) of chain c into registers (int4 slices of the
+// contiguous chain-major rows; rows >= lenc read as -2 = "no row").  N % 4 == 0
+// (the host takes the gather path of hge_rounds_coop.hip otherwise).
+template <int BS, int NPOW>
+__device__ __forceinline__ void dir_fetch(const Tables& t, int c, int p0, int nr, int lenc,
+                                          int4 (&v)[DirGeo<BS, NPOW>::PREF]) {
+  using G = DirGeo<BS, NPOW>;
+  const int N = t.N;
+  const int have = (p0 == INF32 || nr <= 0) ? 0 : max(0, min(nr, lenc - p0));
+  if (have == 0) return;  // block-uniform
+  const int32_t* base = t.LA + ((size_t)c * t.ccap + p0) * (size_t)N;
+  // unconditional loads (rows past `have` re-read the last fetched row; dir_store
+  // drops them): no value select behind each load, so all of them stay in flight
+  const int qmax = have * N / 4 - 1;
+#pragma unroll
+  for (int m = 0; m < G::PREF; m++) {
+    const int q = min((int)threadIdx.x + m * BS, qmax);  // int4 index in the fetched rows
+    v[m] = *(const int4*)(base + 4 * (size_t)q);
+  }
+}
+
+// the fetched rows [p0, p0 + nr) -> their ring slots (caller syncs before a
+// probe); rows at or past lenc are stored as "no row" (0: never >= a member value)
+template <int BS, int NPOW>
+__device__ __forceinline__ void dir_store(const Tables& t, DirLDS<BS, NPOW>& L, int p0, int nr, int lenc,
+                                          int4 (&v)[DirGeo<BS, NPOW>::PREF]) {
+  using G = DirGeo<BS, NPOW>;
+  const int N = t.N;
+  if (p0 == INF32 || nr <= 0) return;
+  const int have = max(0, min(nr, lenc - p0));
+#pragma unroll
+  for (int m = 0; m < G::PREF; m++) {
+    const int q = threadIdx.x + m * BS;
+    const int row = (4 * q) / N;
+    if (row >= nr) continue;
+    if (row >= have) v[m] = make_int4(-2, -2, -2, -2);
+    // the 4 columns lie in one part (CPT is a multiple of 4).  Columns past N are
+    // never written: their member values are 0xFFFF, which no row value passes.
+    const int col = 4 * q - row * N;
+    const int part = col / G::CPT, w = (col - part * G::CPT) / 2;
+    const int slot = (p0 + row) & (DIR_W - 1);
+    uint2* dst = (uint2*)(L.sLA + slot * G::RS + part * G::PS + w);
+    *dst = make_uint2(dir_pack_la(v[m].x, v[m].y), dir_pack_la(v[m].z, v[m].w));
+  }
+}
+
+// member slice of thread (d, part) for the first round: FD[(d, Pd)][part * CPT, +CPT)
+// packed (FD + 1); N % 4 == 0, so every int4 is wholly inside or past the row
+template <int BS, int NPOW>
+__device__ __forceinline__ void dir_members_fd(const Tables& t, int d, int part, int Pd,
+                                               uint32_t (&mw)[DirGeo<BS, NPOW>::CW]) {
+  using G = DirGeo<BS, NPOW>;
+  const int N = t.N;
+  const int c0 = part * G::CPT;
+  const bool act = d < N && Pd != INF32;
+  const int32_t* row = t.FD + rowoff(t, act ? d : 0, act ? Pd : 0);
+#pragma unroll
+  for (int k = 0; k < G::CW / 2; k++) {
+    // unconditional loads from a valid address, then the select
+    int4 a = *(const int4*)(row + min(c0 + 4 * k, N - 4));
+    if (!act || c0 + 4 * k >= N) a = make_int4(INF32, INF32, INF32, INF32);
+    mw[2 * k] = dir_pack_fd(a.x, a.y);
+    mw[2 * k + 1] = dir_pack_fd(a.z, a.w);
+  }
+}
+
+// Member rows after the first round come from the staging block MB[parity]:
+// the workgroup of chain d packs its next frontier row FD[(d, C_{r+1}[d])] there
+// (wave 0, write-through 8-byte stores, vmcnt(0), then the granule), so every
+// consumer reads one contiguous 128 KB block (TLB- and L2-friendly) instead of
+// N rows scattered over N chain regions.  The granule poll is the flag; every
+// load of the block is an 8-byte relaxed agent-scope (sc1) load, as the
+// granule protocol requires (MI355X_MICROARCH.md, Valid forms, row 1).
+template <int BS, int NPOW>
+__device__ __forceinline__ void dir_members_mb(const uint32_t* mb, int d, int part,
+                                               uint32_t (&mw)[DirGeo<BS, NPOW>::CW]) {
+  using G = DirGeo<BS, NPOW>;
+  const gu64_t* src = (const gu64_t*)(mb + (size_t)d * G::MBW + part * G::CW);
+#pragma unroll
+  for (int k = 0; k < G::CW / 2; k++) {
+    const unsigned long long x =
+        __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    mw[2 * k] = (uint32_t)x;
+    mw[2 * k + 1] = (uint32_t)(x >> 32);
+  }
+}
+
+// wave 0 of chain c's workgroup: stage FD[(c, p)] (p = INF32: no member) into MB
+template <int BS, int NPOW>
+__device__ __forceinline__ void dir_stage_member(const Tables& t, uint32_t* mb, int c, int p) {
+  using G = DirGeo<BS, NPOW>;
+  const int lane = threadIdx.x;  // < 64
+  const int N = t.N;
+  if (4 * lane < NPOW) {
+    int4 a = make_int4(INF32, INF32, INF32, INF32);
+    if (p != INF32 && 4 * lane < N) a = *(const int4*)(t.FD + rowoff(t, c, p) + 4 * lane);
+    const unsigned long long x =
+        (unsigned long long)dir_pack_fd(a.x, a.y) | ((unsigned long long)dir_pack_fd(a.z, a.w) << 32);
+    __hip_atomic_store((gu64_t*)(mb + (size_t)c * G::MBW) + lane, x, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// strongly-see count of candidate position p (in the ring) against this
+// thread's member slice, summed over the member's TPM lanes
+template <int BS, int NPOW>
+__device__ __forceinline__ int dir_count(const DirLDS<BS, NPOW>& L, int p, int part,
+                                         const uint32_t (&mw)[DirGeo<BS, NPOW>::CW]) {
+  using G = DirGeo<BS, NPOW>;
+  const uint32_t* src = L.sLA + (p & (DIR_W - 1)) * G::RS + part * G::PS;
+  uint32_t la[G::CW];
+  if constexpr (G::VW == 4) {
+#pragma unroll
+    for (int k = 0; k < G::CW; k += 4) {
+      const uint4 q = *(const uint4*)(src + k);
+      la[k] = q.x;
+      la[k + 1] = q.y;
+      la[k + 2] = q.z;
+      la[k + 3] = q.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < G::CW; k += 2) {
+      const uint2 q = *(const uint2*)(src + k);
+      la[k] = q.x;
+      la[k + 1] = q.y;
+    }
+  }
+  uint32_t acc = 0;
+  const uint32_t ones = 0x00010001u;
+#pragma unroll
+  for (int k = 0; k < G::CW; k++) {
+    // (la + 2) -sat (m + 1) is nonzero <=> la >= m (v_pk_sub_u16 clamp saturates at 0);
+    // min(., 1) per half, then a packed add: 3 VALU ops per 2 columns
+    uint32_t df;
+    asm("v_pk_sub_u16 %0, %2, %3 clamp\n\tv_pk_min_u16 %0, %0, %4\n\tv_pk_add_u16 %1, %1, %0"
+        : "=&v"(df), "+v"(acc)
+        : "v"(la[k]), "v"(mw[k]), "v"(ones));
+  }
+  int cnt = (int)(acc & 0xFFFFu) + (int)(acc >> 16);
+#pragma unroll
+  for (int o = 1; o < G::TPM; o <<= 1) cnt += __shfl_xor(cnt, o);
+  return cnt;
+}
+
+// one probe: number of members strongly seen by candidate position p; `pass` =
+// this thread's member is strongly seen
+template <int BS, int NPOW>
+__device__ __forceinline__ int dir_probe(const Tables& t, DirLDS<BS, NPOW>& L, int p, int part, int slot,
+                                         const uint32_t (&mw)[DirGeo<BS, NPOW>::CW], bool& pass) {
+  const int cnt = dir_count<BS, NPOW>(L, p, part, mw);
+  pass = cnt >= t.SM;
+  const uint64_t b = __ballot(part == 0 && pass);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(&L.sCnt[slot], (int)__builtin_popcountll(b));
+  __syncthreads();
+  return L.sCnt[slot];
+}
+
+// C_{r+1}[c] before the end-of-chain clamp (INF32 = none yet) from the frontier
+// in L.sP, the member slice mw and the window staged at lo (== L.sP[c]);
+// pb = this thread's member pass flag at the returned row
+template <int BS, int NPOW>
+__device__ int dir_select(const Tables& t, int c, int lenc, DirLDS<BS, NPOW>& L, int part,
+                          const uint32_t (&mw)[DirGeo<BS, NPOW>::CW], int& slot,
+                          int4 (&pv)[DirGeo<BS, NPOW>::PREF], int& lo, bool& pb) {
+  const int SM = t.SM;
+  if (lo == INF32 || lo >= lenc) return INF32;
+  for (;;) {
+    const int last = min(DIR_W, lenc - lo) - 1;  // >= 0
+    const int g = min(31, last);
+    int a, b;
+    bool ps;
+    if (dir_probe<BS, NPOW>(t, L, lo + g, part, slot++, mw, ps) >= SM) {
+      a = 0;
+      b = g;
+      pb = ps;
+    } else if (g < last && dir_probe<BS, NPOW>(t, L, lo + last, part, slot++, mw, ps) >= SM) {
+      a = g + 1;
+      b = last;
+      pb = ps;
+    } else {
+      if (lo + DIR_W >= lenc) return INF32;
+      // the answer lies past the window: the whole next window, fresh counters
+      lo += DIR_W;
+      dir_fetch<BS, NPOW>(t, c, lo, DIR_W, lenc, pv);
+      __syncthreads();
+      dir_store<BS, NPOW>(t, L, lo, DIR_W, lenc, pv);
+      if (threadIdx.x < DIR_MAXP) L.sCnt[threadIdx.x] = 0;
+      slot = 0;
+      __syncthreads();
+      continue;
+    }
+    while (a < b) {  // row b passes; find the first passing row in [a, b]
+      const int mid = (a + b) >> 1;
+      if (dir_probe<BS, NPOW>(t, L, lo + mid, part, slot++, mw, ps) >= SM) {
+        b = mid;
+        pb = ps;
+      } else {
+        a = mid + 1;
+      }
+    }
+    return lo + a;
+  }
+}
+
+template <int BS, int NPOW>
+__global__ void __launch_bounds__(BS) k_rounds_direct(Tables t, const int32_t* olen, const int32_t* len,
+                                                      int32_t* rstate, int rlo, int Rprev, uint64_t* gran,
+                                                      int32_t* err, uint64_t* ssc, uint32_t* mbuf,
+                                                      uint64_t* dbg, const int32_t* start, int32_t* hist,
+                                                      int hmax, const int32_t* stopcut, int extra) {
+  // History mode (hist != nullptr; a walker of the cross-GPU split, babble_amd/dist.py):
+  // the walk starts at the frontier `start` (rlo = 0, Rprev = 0), writes frontier
+  // row j to hist[j * N + c] instead of C, the ssc bits of row j to ssc row j, and
+  // stops after row hmax - 1 (rstate[1] = 1), `extra` rows after its frontier
+  // first reached stopcut on every chain (the next walker's start; rstate[1] = 2),
+  // or at the empty frontier; rstate[0] = rows written.
+  using G = DirGeo<BS, NPOW>;
+  // HGE_STAMPS diagnostics (workgroup 0, thread 0): cycles per section into dbg[0..6]
+  uint64_t st_t = 0, st_acc[7] = {0, 0, 0, 0, 0, 0, 0};
+  const bool stamping = dbg && blockIdx.x == 0 && threadIdx.x == 0;
+#define DSTAMP(k)                             \
+  if (stamping) {                             \
+    const uint64_t now_ = stamp();            \
+    if ((k) >= 0) st_acc[(k)] += now_ - st_t; \
+    st_t = now_;                              \
+  }
+  __shared__ DirLDS<BS, NPOW> L;
+  const int N = t.N, NW = t.NW;
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const int d = tid / G::TPM, part = tid - d * G::TPM;
+  const int lenc = len[c];
+  gu64_t* gr[2] = {(gu64_t*)gran, (gu64_t*)(gran + N)};
+  uint32_t* mbp[2] = {mbuf, mbuf + (size_t)NPOW * G::MBW};
+  if (tid < N) {
+    int P;
+    if (hist) {
+      P = start[tid];
+      if (c == 0) hist[tid] = P;
+    } else {
+      P = t.C[(size_t)rlo * N + tid];
+      if (rlo == 0 && olen[tid] == 0 && len[tid] > 0) P = 0;
+      if (c == 0 && rlo == 0 && olen[tid] == 0 && len[tid] > 0) t.C[tid] = 0;
+    }
+    L.sP[tid] = P;
+  }
+  __syncthreads();
+  const int rcap = hist ? hmax : t.Rcap;
+  int extra_left = -1;  // history mode: rows still to walk after passing stopcut
+  int4 pv[G::PREF];
+  int lo = L.sP[c];
+  dir_fetch<BS, NPOW>(t, c, lo, DIR_W, lenc, pv);
+  dir_store<BS, NPOW>(t, L, lo, DIR_W, lenc, pv);
+  int f0 = INF32, fn = 0;  // rows fetched for the next round: [f0, f0 + fn)
+  for (int r = rlo;; r++) {
+    if (r + 1 >= rcap) {
+      if (c == 0 && tid == 0) {
+        rstate[1] = 1;
+        if (hist) rstate[0] = r + 1;  // rows written
+      }
+      break;
+    }
+    DSTAMP(-1);
+    uint32_t mw[G::CW];
+    if (r == rlo) dir_members_fd<BS, NPOW>(t, d, part, d < N ? L.sP[d] : INF32, mw);
+    else dir_members_mb<BS, NPOW>(mbp[r & 1], d < N ? d : 0, part, mw);
+    if (d >= N) {
+#pragma unroll
+      for (int k = 0; k < G::CW; k++) mw[k] = 0xFFFFFFFFu;
+    }
+    if (tid < DIR_MAXP) L.sCnt[tid] = 0;
+    if (tid < 8) L.sBits[tid] = 0;
+    __syncthreads();  // window stored, counters clear
+    DSTAMP(0);
+    const int Pc = L.sP[c];
+    const int cur = (r + 1 < Rprev) ? t.C[(size_t)(r + 1) * N + c] : INF32;
+    int slot = 0;
+    int nxt = INF32;
+    bool pb = false, have_bits = false;
+    if (Pc != INF32) {
+      if (cur != INF32) {
+        nxt = cur;
+      } else {
+        const int s = dir_select<BS, NPOW>(t, c, lenc, L, part, mw, slot, pv, lo, pb);
+        nxt = s < lenc ? s : INF32;
+        have_bits = nxt != INF32;
+      }
+    }
+    DSTAMP(1);
+    if (stamping) st_acc[6] += slot;
+    // publish C_{r+1}[c]: wave 0 stages the next member row, drains its stores,
+    // then lane 0 stores the granule
+    if (tid < 64) {
+      dir_stage_member<BS, NPOW>(t, mbp[(r + 1) & 1], c, nxt);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (tid == 0) {
+        if (hist) hist[(size_t)(r + 1) * N + c] = nxt;
+        else if (nxt != INF32 && cur == INF32) t.C[(size_t)(r + 1) * N + c] = nxt;
+        const uint64_t g = ((uint64_t)(uint32_t)(r - rlo + 1) << 32) | (uint32_t)nxt;
+        __hip_atomic_store(gr[(r + 1) & 1] + c, (unsigned long long)g, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    // strongly-see bits of C_{r+1}[c] against the members of round r
+    if (nxt != INF32) {
+      if (!have_bits) {  // a frontier row kept from an earlier batch: one more probe
+        if (nxt < lo || nxt >= lo + DIR_W) {
+          __syncthreads();
+          lo = nxt;
+          dir_fetch<BS, NPOW>(t, c, lo, DIR_W, lenc, pv);
+          dir_store<BS, NPOW>(t, L, lo, DIR_W, lenc, pv);
+          __syncthreads();
+        }
+        pb = dir_count<BS, NPOW>(L, nxt, part, mw) >= t.SM;
+      }
+      if (part == 0 && d < N && pb) atomicOr(&L.sBits[d >> 5], 1u << (d & 31));
+      __syncthreads();
+      if (tid < NW)
+        ssc[((size_t)(r + 1) * N + c) * NW + tid] =
+            (uint64_t)L.sBits[2 * tid] | ((uint64_t)L.sBits[2 * tid + 1] << 32);
+    }
+    DSTAMP(2);
+    // fetch the rows the next round's window [nxt, nxt + W) lacks while the
+    // other workgroups finish this round
+    if (nxt == INF32) {
+      f0 = INF32;
+      fn = 0;
+    } else {
+      f0 = (lo != INF32 && nxt < lo + DIR_W) ? lo + DIR_W : nxt;
+      fn = nxt + DIR_W - f0;
+    }
+    lo = nxt;
+    dir_fetch<BS, NPOW>(t, c, f0, fn, lenc, pv);
+    DSTAMP(3);
+    // collect C_{r+1}: wave 0 polls the N granules of epoch r - rlo + 1
+    if (tid < 64) {
+      const unsigned ep = (unsigned)(r - rlo + 1);
+      gu64_t* g = gr[(r + 1) & 1];
+      unsigned spins = 0;
+      bool any = false, fail = false;
+      for (;;) {
+        bool ok = true;
+        any = false;
+        for (int dd = tid; dd < N; dd += 64) {
+          const unsigned long long x =
+              __hip_atomic_load(g + dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok &= (unsigned)(x >> 32) == ep;
+          const int P = (int)(uint32_t)x;
+          L.sP[dd] = P;
+          any |= (P != INF32);
+        }
+        if (__all(ok)) break;
+        if (++spins > (1u << 24)) {  // never a normal wait: co-residency failure
+          fail = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      any = __ballot(any) != 0;
+      bool past = true;
+      if (stopcut)
+        for (int dd = tid; dd < N; dd += 64) past &= L.sP[dd] >= stopcut[dd];  // INF32 passes
+      past = __all(past);
+      if (tid == 0) {
+        L.s_stop = fail ? 2 : (any ? 0 : 1);
+        L.s_past = past ? 1 : 0;
+        if (fail) atomicOr(err, 1);
+      }
+    }
+    __syncthreads();  // every probe of this round has read the window
+    DSTAMP(4);
+    if (L.s_stop) {
+      if (L.s_stop == 1 && c == 0 && tid == 0) rstate[0] = hist ? r + 2 : max(rstate[0], r + 1);
+      break;
+    }
+    if (stopcut) {
+      if (extra_left < 0 && L.s_past) extra_left = extra;
+      if (extra_left >= 0 && extra_left-- == 0) {
+        if (c == 0 && tid == 0) {
+          rstate[0] = r + 2;  // rows 0 .. r + 1
+          rstate[1] = 2;
+        }
+        break;
+      }
+    }
+    dir_store<BS, NPOW>(t, L, f0, fn, lenc, pv);
+    DSTAMP(5);
+  }
+  if (stamping)
+    for (int q = 0; q < 7; q++) dbg[q] += st_acc[q];
+#undef DSTAMP
+}
+
+template __global__ void k_rounds_direct<1024, 64>(Tables, const int32_t*, const int32_t*, int32_t*, int, int,
+                                                   uint64_t*, int32_t*, uint64_t*, uint32_t*, uint64_t*,
+                                                   const int32_t*, int32_t*, int, const int32_t*, int);
+template __global__ void k_rounds_direct<1024, 128>(Tables, const int32_t*, const int32_t*, int32_t*, int, int,
+                                                    uint64_t*, int32_t*, uint64_t*, uint32_t*, uint64_t*,
+                                                   const int32_t*, int32_t*, int, const int32_t*, int);
+template __global__ void k_rounds_direct<1024, 256>(Tables, const int32_t*, const int32_t*, int32_t*, int, int,
+                                                    uint64_t*, int32_t*, uint64_t*, uint32_t*, uint64_t*,
+                                                   const int32_t*, int32_t*, int, const int32_t*, int);
+
+}  // namespace hge

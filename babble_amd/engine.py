@@ -70,7 +70,8 @@ EXPORTS = [
     "hge_consensus_log", "hge_event_rounds", "hge_event_received", "hge_set_cache_size",
     "hge_cache_size", "hge_participant_events", "hge_participant_event", "hge_last_from",
     "hge_diff", "hge_wire_info", "hge_read_wire_parents", "hge_parent_round", "hge_round_inc",
-    "hge_round_diff", "hge_set_round",
+    "hge_round_diff", "hge_set_round", "hge_split_begin", "hge_frontier_guess",
+    "hge_frontier_walk", "hge_split_finish", "hge_frontier_rows",
 ]
 
 _lib = None
@@ -156,6 +157,11 @@ def lib():
     L.hge_round_inc.restype = i32
     L.hge_round_diff.argtypes = [vp, i32, i32, P(i32)]
     L.hge_set_round.argtypes = [vp, i32, P(i32), P(ctypes.c_uint8), P(ctypes.c_uint8), i32]
+    L.hge_split_begin.argtypes = [vp]
+    L.hge_frontier_guess.argtypes = [vp, i32, i32, P(i32)]
+    L.hge_frontier_walk.argtypes = [vp, P(i32), P(i32), i32, i32, P(i32), P(ctypes.c_uint64), P(i32), P(i32)]
+    L.hge_split_finish.argtypes = [vp, P(i32), P(ctypes.c_uint64), i32, i32, P(i64)]
+    L.hge_frontier_rows.argtypes = [vp, i32, i32, P(i32), P(ctypes.c_uint64)]
     L.hge_set_profiling.argtypes = [vp, ctypes.c_int]
     L.hge_reset_kernel_stats.argtypes = [vp]
     L.hge_kernel_stats.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
@@ -287,6 +293,45 @@ class Engine:
         counts = np.zeros(max(1, self._ncalls), np.int64)
         self._check(self.L.hge_replay_fetch(self.h, _p32(order), len(order), _p64(counts)))
         return self._status, order[:self._nordered], counts[:self._ncalls]
+
+    # --- one hashgraph split across GPUs (babble_amd.dist.split_replay) ----
+    def split_begin(self):
+        self._check(self.L.hge_split_begin(self.h))
+
+    def frontier_guess(self, part, nparts):
+        out = np.zeros(self.n, np.int32)
+        self._check(self.L.hge_frontier_guess(self.h, part, nparts, _p32(out)))
+        return out
+
+    def frontier_walk(self, start, stopcut=None, extra=0, hmax=None):
+        """Rounds-frontier walk from `start`: (rows [n, N] int32, ssc [n, N, NW] uint64, natural).
+        hmax bounds the rows (default: every chain advances at least one position per
+        round, so the longest chain + 2 always suffices)."""
+        nw = (self.n + 63) // 64
+        if hmax is None:
+            hmax = int(self.known().max()) + 2
+        nr = ctypes.c_int32()
+        nat = ctypes.c_int32()
+        start = np.ascontiguousarray(start, np.int32)
+        cut = None if stopcut is None else np.ascontiguousarray(stopcut, np.int32)
+        self._check(self.L.hge_frontier_walk(self.h, _p32(start), None if cut is None else _p32(cut),
+                                             extra, hmax, None, None, ctypes.byref(nr), ctypes.byref(nat)))
+        n = nr.value
+        rows = np.zeros((n, self.n), np.int32)
+        ssc = np.zeros((n, self.n, nw), np.uint64)
+        self._check(self.L.hge_frontier_rows(self.h, 0, n, _p32(rows),
+                                             ssc.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))))
+        return rows, ssc, bool(nat.value)
+
+    def split_finish(self, rows, ssc, natural):
+        rows = np.ascontiguousarray(rows, np.int32)
+        ssc = np.ascontiguousarray(ssc, np.uint64)
+        n = ctypes.c_int64()
+        self._check(self.L.hge_split_finish(self.h, _p32(rows),
+                                            ssc.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                            len(rows), 1 if natural else 0, ctypes.byref(n)))
+        self._nordered = n.value
+        return n.value
 
     def set_profiling(self, on=True):
         self.L.hge_set_profiling(self.h, 1 if on else 0)

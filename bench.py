@@ -61,7 +61,9 @@ def algorithmic_bytes(kernel, n, events, ordered):
       k_la_sweep    12N/event: read LA[sp] and LA[op], write LA[x] -- once, not
                     once per fixed-point sweep (the sweeps' re-reads are waste);
       k_la_clear     4N/event (the new rows' -1 fill);
+      k_la_sweep16 / k_la_clear16  6N / 2N per event (N > 32: the same on packed u16);
       k_transpose   16N/event (LA -> LAT and FDT -> FD: each reads and writes 4N);
+      k_transpose16 10N/event (LA16 read, LA rows and LAT written);
       k_fdt_clear    4N/event; k_fdt_runs 8N/event (LAT read, FDT written);
       k_fss          8N/event (FD row read, fss row written, N <= 32);
       rounds        4N/event (the strongly-see round test reads each row once);
@@ -72,26 +74,30 @@ def algorithmic_bytes(kernel, n, events, ordered):
     per_event = {"k_la_sweep": 12 * n, "k_la_clear": 4 * n, "k_transpose": 16 * n,
                  "k_fdt_clear": 4 * n, "k_fdt_runs": 8 * n, "k_fss": 8 * n,
                  "k_rounds_walk": 4 * n, "k_rounds_coop": 4 * n, "k_rounds_coop_spec": 4 * n,
-                 "k_walk_spec": 4 * n, "k_rounds_fss": 4 * n}
+                 "k_walk_spec": 4 * n, "k_rounds_fss": 4 * n, "k_rounds_direct": 4 * n,
+                 "k_la_clear16": 2 * n, "k_la_sweep16": 6 * n, "k_transpose16": 10 * n}
     if name in per_event:
         return per_event[name] * events
-    if name in ("k_round_received", "k_median_wave"):
+    if name in ("k_round_received", "k_median_wave", "k_median_chain"):
         return (4 * n + 48) * ordered
     return 48 * ordered
 
 
-def pmc_traffic(config_key, kernel):
-    """HBM bytes per replay of `kernel` in this configuration from the committed
-    rocprofv3 PMC passes (profiles/pmc_traffic.json, made by
-    scripts/pmc_traffic.py on the GPU box), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def pmc_traffic(config_key, kernel, launches_per_replay):
+    """HBM bytes per launch of `kernel` in this configuration from the committed
+    rocprofv3 PMC passes (profiles/r02/pmc_traffic.json, made by
+    scripts/pmc_traffic.py on the GPU box): the kernel's bytes per replay over
+    the launches that did work (k_la_sweep: the sweeps up to the quiet one), or None."""
+    path = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
     try:
         pm = json.load(open(path))
     except (OSError, ValueError):
         return None
     name = kernel.strip("()").split("<")[0]
     v = pm.get("configs", {}).get(config_key, {}).get(name)
-    return v.get("bytes_per_replay") if isinstance(v, dict) else None
+    if not isinstance(v, dict) or "bytes_per_replay" not in v:
+        return None
+    return int(v["bytes_per_replay"] / max(launches_per_replay, 1))
 
 
 def golden_prefix(n, E, K, seed):
@@ -188,6 +194,9 @@ def main():
     ap.add_argument("--cpu-sample-events", type=int, default=None,
                     help="CPU baseline prefix (default: 20480 at N >= 128, 100k below)")
     ap.add_argument("--profile-steps", type=int, default=1)
+    ap.add_argument("--split", action="store_true",
+                    help="gossip, N > 1: ONE hashgraph per job, its rounds walk split across the "
+                         "ranks (babble_amd.dist.split_run) instead of one replica per rank")
     args = ap.parse_args()
     mc = args.workload == "mc"
     n = args.participants or (32 if mc else DEFAULT[0])
@@ -219,13 +228,23 @@ def main():
         for eng, d in zip(engines, dags):
             eng.prepare(events_array(d), schedule(len(d["creator"]), K))
     else:
-        dags = [random_gossip(n, E, seed=args.seed + rank)]
+        split = args.split and world > 1
+        # split: every rank stages the same stream (seed, not seed + rank)
+        dags = [random_gossip(n, E, seed=args.seed + (0 if split else rank))]
         engines = [Engine(n, E, device=local_rank)]
         engines[0].prepare(events_array(dags[0]), schedule(E, K))
     ingest_s = time.perf_counter() - t0
     pool = ThreadPoolExecutor(max_workers=max(1, min(args.threads, len(engines))))
 
+    split = (not mc) and args.split and world > 1
+    gather = None
+    if split:
+        from babble_amd.dist import split_run, torch_gather
+        gather = torch_gather(dist, f"cuda:{local_rank}")
+
     def step():
+        if split:
+            return split_run(engines[0], rank, world, gather)
         if len(engines) == 1:
             return engines[0].run()
         return sum(pool.map(lambda e: e.run(), engines))
@@ -275,6 +294,8 @@ def main():
     tot_ordered, max_step = ordered, step_s
     if dist is not None:
         max_step, tot_ordered = reduce_step(dist, step_s, ordered, f"cuda:{local_rank}")
+        if split:
+            tot_ordered = ordered  # one hashgraph for the whole job
 
     def kernel_roofline(name):
         """(algorithmic bytes per launch, average launch ms, achieved GB/s).
@@ -283,20 +304,22 @@ def main():
         launches after it return at once and are left out)."""
         ms, cnt = kstats[name]
         base = name.strip("()").split("<")[0]
-        launches = sweeps * nprof if base == "k_la_sweep" else cnt
+        launches = sweeps * nprof if base in ("k_la_sweep", "k_la_sweep16") else cnt
         per_replay = launches / nprof
         b = algorithmic_bytes(name, n, ev0, ord0) / max(per_replay, 1)
         per_launch = ms / max(launches, 1)
         return b, per_launch, b / (per_launch * 1e-3) / 1e9, per_replay
 
     dom = max(kstats.items(), key=lambda kv: kv[1][0])[0]
-    alg, per_launch_ms, achieved, _ = kernel_roofline(dom)
+    alg, per_launch_ms, achieved, dom_lpr = kernel_roofline(dom)
     # every kernel that streams the N-wide tables, with its roofline
     hbm_kernels = {}
     for name in kstats:
         base = name.strip("()").split("<")[0]
         if base in ("k_la_sweep", "k_la_clear", "k_transpose", "k_fss", "k_fdt_runs",
-                    "k_fdt_clear", "k_rounds_coop", "k_rounds_coop_spec", "k_median_wave"):
+                    "k_fdt_clear", "k_rounds_coop", "k_rounds_coop_spec", "k_median_wave",
+                    "k_la_clear16", "k_la_sweep16", "k_transpose16", "k_rounds_direct",
+                    "k_median_chain"):
             b, pl, gbs, lpr = kernel_roofline(name)
             hbm_kernels[name] = {"achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
                                  "alg_bytes_per_launch": int(b), "launch_ms": round(pl, 4),
@@ -365,18 +388,19 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(max_step * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if split else "weak",
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic",
             "config": {"workload": workload, "participants": n, "events_per_graph": E, "k": K,
                        "graphs_per_gpu": len(engines), "ordered_per_step": tot_ordered,
-                       "parallelism": f"replicas{world}"},
+                       "parallelism": (f"split{world}: one hashgraph, rounds walk split across "
+                                       f"{world} GPUs" if split else f"replicas{world}")},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": pmc_traffic(cfg_key, dom),
-                         "traffic_unit": "HBM bytes per replay (rocprofv3 FETCH_SIZE+WRITE_SIZE)",
+                         "traffic": pmc_traffic(cfg_key, dom, dom_lpr),
+                         "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
                          "algorithmic_bytes_per_launch": int(alg),
                          "launch_ms": round(per_launch_ms, 4),
                          "hbm_kernels": hbm_kernels,
@@ -389,6 +413,7 @@ def main():
             "ingest_host_ms": round(ingest_s * 1e3, 2),
             "replay_ms": replay_ms,
             "coordinate_sweeps": sweeps,
+            "rounds": eng0.rounds(),
             "kernels_ms_per_replay": {k: round(v[0] / nprof, 4) for k, v in
                                       sorted(kstats.items(), key=lambda kv: -kv[1][0])},
             "kernel_launches_per_replay": {k: v[1] // nprof for k, v in kstats.items()},

@@ -116,6 +116,35 @@ int hge_replay_prepare(hge_engine* h, const hge_event* ev, int64_t n_sub,
 int hge_replay_run(hge_engine* h, int64_t* n_ordered);
 int hge_replay_fetch(hge_engine* h, int32_t* order_out, int64_t cap, int64_t* call_counts_out);
 
+/* ---- one hashgraph split across GPUs (babble_amd/dist.py) ------ */
+/* Every rank stages the whole stream (hge_replay_prepare), computes the
+ * coordinates (hge_split_begin), then walks the rounds frontier recurrence
+ *  from its own start: rank 0 from the true first frontier,
+ * rank p from the time cut at p * E / nparts (hge_frontier_guess), until its
+ * rows pass `stopcut` (the next rank's start) plus `extra` rows, or hmax rows.
+ * The ranks all-gather their rows (N ints each) and strongly-see bits
+ * (N * ceil(N/64) words each); the join follows row equalities from rank 0's
+ * true trajectory (the recurrence is a function of the row alone) and
+ * hge_split_finish installs the joined rows -- the sequential walk resumes from
+ * the last joined row if the walk did not end -- and runs DivideRounds,
+ * DecideFame and FindOrder at every call point.  Results are identical to
+ * hge_replay_run.  N > 32 with N % 4 == 0 only. */
+int hge_split_begin(hge_engine* h);
+int hge_frontier_guess(hge_engine* h, int32_t part, int32_t nparts, int32_t* start_out);
+/* rows_out: hmax * N ints (row 0 = start; INT32_MAX = no event yet), ssc_out:
+ * hmax * N * ceil(N/64) words (row 0 unused); *nrows rows written; *natural = 1
+ * when the last row is the empty frontier (the walk ended). */
+int hge_frontier_walk(hge_engine* h, const int32_t* start, const int32_t* stopcut, int32_t extra,
+                      int32_t hmax, int32_t* rows_out, uint64_t* ssc_out, int32_t* nrows,
+                      int32_t* natural);
+/* rows [from, from + n) of the last walk (hge_frontier_walk with NULL outputs
+ * keeps them on the device). */
+int hge_frontier_rows(hge_engine* h, int32_t from, int32_t n, int32_t* rows_out, uint64_t* ssc_out);
+/* rows: the joined true frontier rows 0 .. nrows-1 (natural: the walk ended after
+ * them, i.e. Rounds() = nrows), ssc their strongly-see bits (row 0 unused). */
+int hge_split_finish(hge_engine* h, const int32_t* rows, const uint64_t* ssc, int32_t nrows,
+                     int32_t natural, int64_t* n_ordered);
+
 /* ---- state queries --------------------------------------------------------- */
 int64_t hge_event_count(hge_engine* h);
 int32_t hge_participants(hge_engine* h);

@@ -34,3 +34,28 @@ if [[ $WHAT == segv ]]; then
     echo "HGE_COOP_LAUNCH=$mode rocprofv3 rc=$?"
   done
 fi
+if [[ $WHAT == quick ]]; then
+  # wide-path parity + headline numbers without the CPU legs
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -k "golden or coop or fullsize or wide or store or gpu_parity or split or reference" > $OUT/pytest_quick.log 2>&1 || { echo "gpu tests failed"; tail -40 $OUT/pytest_quick.log; exit 1; }
+  tail -1 $OUT/pytest_quick.log
+  for cfg in "256 10000000" "64 1000000" "128 1000000"; do
+    set -- $cfg
+    timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-secondary --participants $1 --events $2 --steps 3 --warmup 1 > $OUT/b_$1_$2.json 2> $OUT/b_$1_$2.err || { tail -20 $OUT/b_$1_$2.err; exit 1; }
+    python -c "
+import json
+d=json.loads(open('$OUT/b_$1_$2.json').read().strip().splitlines()[-1])
+print('$1/$2', round(d['value']/1e6,2), 'Mev/s', d['ms_per_step'], 'ms', d['parity'], list(d['kernels_ms_per_replay'].items())[:6])"
+  done
+fi
+if [[ $WHAT == stamps ]]; then
+  # section cycles of the direct rounds step (workgroup 0), and median / rounds A/B
+  HGE_STAMPS=1 timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-secondary --participants 256 --events 2000000 --steps 1 --warmup 0 --ramp-s 0 --profile-steps 1 > $OUT/st.json 2> $OUT/st.err || { tail -20 $OUT/st.err; exit 1; }
+  grep "hge stamps" $OUT/st.err | tail -2
+  for env in "HGE_MEDIAN_ORDER=id" "HGE_ROUNDS_STEP=fss" "X=1"; do
+    env $env timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-secondary --participants 256 --events 2000000 --steps 3 --warmup 1 > $OUT/ab.json 2> $OUT/ab.err || { tail -20 $OUT/ab.err; exit 1; }
+    python -c "
+import json
+d=json.loads(open('$OUT/ab.json').read().strip().splitlines()[-1])
+print('$env', round(d['value']/1e6,2), d['ms_per_step'], list(d['kernels_ms_per_replay'].items())[:5])"
+  done
+fi

@@ -5,7 +5,7 @@ Runs two counter passes over `python3 bench.py <bench args>` (FETCH_SIZE, then
 WRITE_SIZE: they cannot share one pass on gfx950), each in its own rocprofv3
 run with --kernel-trace only, parses counter_collection.csv and merges
 {config-key: {kernel: {fetch_bytes, write_bytes, bytes_per_launch, launches}}}
-into profiles/pmc_traffic.json.  FETCH_SIZE is reported in KiB and, on gfx950,
+into profiles/r02/pmc_traffic.json.  FETCH_SIZE is reported in KiB and, on gfx950,
 counts half of the bytes of wide coalesced reads (MI355X_MICROARCH.md §HBM),
 so it is doubled; WRITE_SIZE (KiB) is taken as is.
 """
@@ -24,7 +24,7 @@ def run_pass(out_dir, counter, bench_args, parse_only=False):
     if not parse_only:
         cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--kernel-trace", "--pmc", counter,
                "--output-format", "csv", "-d", d, "-o", "pmc", "--", "python3", "bench.py",
-               "--no-cpu-baseline", "--profile-steps", "1"] + bench_args
+               "--no-cpu-baseline", "--no-secondary", "--profile-steps", "1"] + bench_args
         subprocess.check_call(cmd, cwd=ROOT)
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
@@ -50,15 +50,20 @@ def main():
     fetch = run_pass(out_dir, "FETCH_SIZE", bench_args, parse_only)
     write = run_pass(out_dir, "WRITE_SIZE", bench_args, parse_only)
     res = {}
+    # every replay resets its rounds tables once (k_reset_rounds): the replay count
+    replays = max(1, fetch.get("k_reset_rounds", [0.0, 0])[1])
     for name in sorted(set(fetch) | set(write)):
         fb, fl = fetch.get(name, [0.0, 0])
         wb, wl = write.get(name, [0.0, 0])
         launches = max(fl, wl, 1)
         fetch_b = 2.0 * fb * 1024 / max(fl, 1)
         write_b = wb * 1024 / max(wl, 1)
+        # per replay: every launch of the replay, the queued sweeps that returned at once included
+        per_replay = (2.0 * fb + wb) * 1024 / replays
         res[name] = {"fetch_bytes": round(fetch_b), "write_bytes": round(write_b),
-                     "bytes_per_launch": round(fetch_b + write_b), "launches": launches}
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+                     "bytes_per_launch": round(fetch_b + write_b), "launches": launches,
+                     "bytes_per_replay": round(per_replay), "replays": replays}
+    path = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
     os.makedirs(os.path.dirname(path), exist_ok=True)
     try:
         allres = json.load(open(path))

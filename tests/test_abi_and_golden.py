@@ -155,3 +155,11 @@ def test_property_checker_on_an_oracle_run():
     rr = np.array([o.round_received(x) if o.round_received(x) is not None else -1 for x in range(m)])
     cts = np.array([o.consensus_timestamp(x) if rr[x] >= 0 else 0 for x in range(m)], np.int64)
     check_run(dag, st, order, counts, rounds, wit, rr, cts)
+
+
+def test_cpp_abi_binary_cpu_checks():
+    """tests/abi/hge_abi_test.cpp: the C ABI from C++ (argument errors, null handle)."""
+    import subprocess
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tests", "abi")])
+    out = subprocess.run([os.path.join(ROOT, "build", "hge_abi_test")], capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr

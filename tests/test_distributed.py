@@ -54,3 +54,91 @@ def test_world2_gloo_reduction():
     for _, _, _, max_step, tot in out:
         assert abs(max_step - 0.015) < 1e-12       # max over ranks
         assert tot == 1000 * 1024 + 1               # sum over ranks
+
+
+# ---- one hashgraph split across ranks: the join of the walkers' rows ----------
+
+def true_frontier(n, dag, k):
+    """The rounds frontier C_r[c] (first chain-c position with round >= r; INT32_MAX
+    = none) for every round, from the oracle's per-event rounds, plus the empty row."""
+    import numpy as np
+    from babble_amd.gossip import schedule
+    from oracle.oracle import replay
+    o, st, _, _ = replay(dag, schedule(len(dag["creator"]), k))
+    E = int((st >= 0).sum())
+    rounds = np.array([o.round(x) for x in range(E)])
+    R = int(rounds.max()) + 1
+    INF = np.iinfo(np.int32).max
+    C = np.full((R + 1, n), INF, np.int32)
+    for x in range(E - 1, -1, -1):  # ids are insertion order: the last write is the first event
+        c, p = int(dag["creator"][x]), int(dag["index"][x])
+        for r in range(rounds[x] + 1):
+            if C[r, c] == INF or p < C[r, c]:
+                C[r, c] = p
+    return C
+
+
+def _marks(rows, tag):
+    import numpy as np
+    n, N = rows.shape
+    return (np.arange(n, dtype=np.uint64)[:, None, None] * 1000 + tag).repeat(N, 1).repeat(1, 2)
+
+
+def test_join_histories_follows_merges():
+    import numpy as np
+    from babble_amd.dist import join_histories
+    from babble_amd.gossip import random_gossip
+    n = 6
+    C = true_frontier(n, random_gossip(n, 3000, seed=31), n)
+    R = len(C) - 1
+    assert R > 40
+    rng = np.random.default_rng(1)
+    junk = C[20:24] + rng.integers(1, 3, (4, n)).astype(np.int32)  # a guessed start converging
+    h0 = (C[:30].copy(), None, False)                  # rank 0: true rows 0..29, then stopped
+    r1 = np.concatenate([junk, C[25:]])                # rank 1: 4 wrong rows, then true 25..R
+    h1 = (r1, None, True)
+    hists = [(h0[0], _marks(h0[0], 0), False), (h1[0], _marks(h1[0], 1), True)]
+    rows, ssc, natural = join_histories(hists)
+    assert natural and len(rows) == R
+    np.testing.assert_array_equal(rows, C[:R])
+    # rows 0..25 come from rank 0 (row 25 is where the walk hands over), 26.. from rank 1
+    assert (ssc[:26, 0, 0] % 1000 == 0).all() and (ssc[26:, 0, 0] % 1000 == 1).all()
+    assert ssc[26, 0, 0] // 1000 == 4 + 1               # rank 1's row of round 26
+    # no overlap: the join stops at rank 0's last row (the sequential walk resumes there)
+    rows, _, natural = join_histories([(C[:20].copy(), _marks(C[:20], 0), False),
+                                       (r1, _marks(r1, 1), True)])
+    assert not natural and len(rows) == 20
+    # a single rank that walked to the end
+    rows, _, natural = join_histories([(C.copy(), _marks(C, 0), True)])
+    assert natural and len(rows) == R
+
+
+def _gather_worker(rank, world, port, q):
+    import numpy as np
+    import torch.distributed as dist
+    from babble_amd.dist import torch_gather
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 5 + 3 * rank
+    rows = np.full((n, 8), rank, np.int32)
+    ssc = np.full((n, 8, 1), 10 + rank, np.uint64)
+    out = torch_gather(dist)((rows, ssc, rank == 1))
+    q.put((rank, [(r.shape, int(r[0, 0]), s.shape, int(s[0, 0, 0]), nat) for r, s, nat in out]))
+    dist.destroy_process_group()
+
+
+def test_world2_gloo_history_gather():
+    """The split's one collective (babble_amd.dist.torch_gather) with world_size 2."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    exp = [((5, 8), 0, (5, 8, 1), 10, False), ((8, 8), 1, (8, 8, 1), 11, True)]
+    assert out[0][1] == exp and out[1][1] == exp

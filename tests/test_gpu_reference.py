@@ -215,3 +215,13 @@ def test_insert_batch_error_carries_accepted_ids():
     assert ei.value.accepted.tolist() == [0, 1, 2]
     assert eng.event_count() == 3
     eng.close()
+
+
+def test_cpp_abi_binary_on_gpu():
+    """tests/abi/hge_abi_test.cpp --gpu: the consensus DAG through the C ABI from C++."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([os.path.join(root, "build", "hge_abi_test"), "--gpu"], capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode == 0, out.stderr + out.stdout
