@@ -130,11 +130,15 @@ __device__ __forceinline__ size_t rowoff16(const Tables& t, int c, int p) {
   return ((size_t)c * t.ccap + p) * (size_t)t.NW2;
 }
 
-__global__ void k_la_clear16(Tables t, const int32_t* olen, const int32_t* len, int32_t* zero, int nzero) {
+// also resets the segments' last-changed sweeps (dirty[0, ndirty) = -2: none yet)
+__global__ void k_la_clear16(Tables t, const int32_t* olen, const int32_t* len, int32_t* zero, int nzero,
+                             int32_t* dirty, int ndirty) {
   const int j = blockIdx.y;
   const int W = t.NW2;
   if (j == 0 && blockIdx.x == 0)
     for (int i = threadIdx.x; i < nzero; i += blockDim.x) zero[i] = 0;
+  if (dirty && j == (int)gridDim.y - 1 && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < ndirty; i += blockDim.x) dirty[i] = -2;
   const int64_t lo = (int64_t)olen[j] * W, hi = (int64_t)len[j] * W;
   uint32_t* base = t.LA16 + (size_t)j * t.ccap * W;
   for (int64_t e = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < hi;
@@ -142,14 +146,25 @@ __global__ void k_la_clear16(Tables t, const int32_t* olen, const int32_t* len, 
     base[e] = 0u;
 }
 
+//
+// Segment skipping (dirty != nullptr): dirty[s] = the last sweep in which
+// segment s (chain-major numbering: segbase[c] + (p - olen[c]) / SEG) changed a
+// row.  Sweep `sweep` recomputes a segment only if one of its inputs -- the
+// segment before it on its chain, or a segment holding one of its other
+// parents -- changed in the previous sweep or so far in this one (dirty >=
+// sweep - 1).  Every change to an input is then followed by a recomputation
+// that reads it, so the fixed point and its detection are unchanged; rows
+// below olen are final and never dirty.
 template <int NP>  // NP lanes (packed words) per segment
 __global__ void __launch_bounds__(256) k_la_sweep16(Tables t, const int2* segs, int nseg, int SEG,
                                                     const int32_t* len, const int32_t* prev,
-                                                    int32_t* changed) {
+                                                    int32_t* changed, const int32_t* olen,
+                                                    const int32_t* segbase, int32_t* dirty, int sweep) {
   constexpr int G = 256 / NP;
   constexpr int SEGMAX = 64;
   constexpr int U = 32;  // loads in flight per lane and batch
   __shared__ int64_t s_off[G][SEGMAX];
+  __shared__ int s_need[G];
   if (prev && *prev == 0) return;  // converged: the flag stays 0
   const int W = t.NW2;
   const int g = threadIdx.x / NP, i = threadIdx.x - (threadIdx.x / NP) * NP;
@@ -162,16 +177,30 @@ __global__ void __launch_bounds__(256) k_la_sweep16(Tables t, const int2* segs, 
     k0 = sg.y;
     k1 = min(k0 + SEG, len[j]);
   }
+  const bool skip = dirty != nullptr && sweep > 0;
+  int sid = 0;
+  if (skip) {
+    if (valid) sid = segbase[j] + (k0 - olen[j]) / SEG;
+    // the segment before this one on its chain
+    if (i == 0) s_need[g] = valid && k0 > olen[j] && dirty[sid - 1] >= sweep - 1;
+    __syncthreads();
+  }
   for (int kk = i; kk < SEG; kk += NP) {
     int64_t off = -1;
     if (valid && k0 + kk < k1) {
       const int2 o = t.opcp[(size_t)j * t.ccap + k0 + kk];
-      if (o.x >= 0) off = (int64_t)rowoff16(t, o.x, o.y);
+      if (o.x >= 0) {
+        off = (int64_t)rowoff16(t, o.x, o.y);
+        if (skip) {
+          const int ol = olen[o.x];
+          if (o.y >= ol && dirty[segbase[o.x] + (o.y - ol) / SEG] >= sweep - 1) s_need[g] = 1;
+        }
+      }
     }
     s_off[g][kk] = off;
   }
   __syncthreads();
-  const bool act = valid && i < W;
+  const bool act = valid && i < W && (!skip || s_need[g]);
   bool ch = false;
   if (act) {
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -210,7 +239,17 @@ __global__ void __launch_bounds__(256) k_la_sweep16(Tables t, const int2* segs, 
       }
     }
   }
-  if (__ballot(ch) && (threadIdx.x & 63) == __builtin_ctzll(__ballot(ch))) *changed = 1;
+  const uint64_t bal = __ballot(ch);
+  if (bal && (threadIdx.x & 63) == __builtin_ctzll(bal)) *changed = 1;
+  if (dirty) {
+    // one lane per (wave, segment) with a change: NP = 32 puts two segments in a wave
+    const int lane = threadIdx.x & 63;
+    const uint64_t grp = NP >= 64 ? ~0ull : (0xFFFFFFFFull << (lane & 32));
+    if ((bal & grp) && lane == __builtin_ctzll(bal & grp)) {
+      if (!skip) sid = segbase[j] + (k0 - olen[j]) / SEG;
+      dirty[sid] = sweep;
+    }
+  }
 }
 
 // LA16 -> LA (int32 rows) and LAT (transposed), for positions [plo_j, len_j)

@@ -155,7 +155,7 @@ struct hge_engine {
   DBuf<int32_t> s_part, s_fst;
   // coordinate sweeps: transposed tables and scratch
   int n_sweeps = 0;
-  DBuf<int32_t> d_LAT, d_FDT, s_chg, s_bar;
+  DBuf<int32_t> d_LAT, d_FDT, s_chg, s_bar, s_dirty;
   DBuf<uint64_t> d_ssc, s_gran;
   DBuf<int32_t> s_bseg;
   DBuf<uint64_t> s_H;                // speculative walk: epoch-tagged histories
@@ -195,6 +195,7 @@ struct hge_engine {
   std::vector<int2> h_segs;
   int32_t *k_rs = nullptr, *k_len = nullptr, *k_plo = nullptr, *k_qlo = nullptr, *k_lo = nullptr;
   int2* k_segs = nullptr;
+  int32_t* k_segbase = nullptr;
   bool und_fresh = false;  // the candidate list is every event of a fresh replay
   float stage_ms[7] = {};
 
@@ -324,7 +325,7 @@ struct hge_engine {
                              &s_recv,    &s_rr,     &s_bpos,  &s_fund,   &s_upos,    &s_vis,
                              &s_und2,    &s_part,   &s_fst,    &d_FSS,     &d_LAT,
                              &d_FDT,     &s_chg,    &s_bar,   &s_bseg,   &s_kctl,    &s_cctl,
-                             &s_out,     &s_hn,     &s_hres};
+                             &s_out,     &s_hn,     &s_hres,  &s_dirty};
     for (auto* b : i32s) b->free_();
     d_ts.free_();
     d_cts.free_();
@@ -700,8 +701,9 @@ struct hge_engine {
     for (int c = 0; c < N; c++) fresh = fresh && coords_len[c] == 0;
     const size_t o_len = 4, o_plo = o_len + 2 * N, o_qlo = o_plo + N, o_lo = o_qlo + N;
     const size_t o_seg = (o_lo + 2 * N + 1 + 1) & ~(size_t)1;
+    const size_t o_sb = o_seg + 2 * segs.size();  // chain-major segment bases (sweep skipping)
     std::vector<int32_t>& kc = h_kctl;
-    kc.assign(o_seg + 2 * segs.size(), 0);
+    kc.assign(o_sb + N, 0);
     kc[0] = R;  // rstate: {R, overflow}, new-witness count
     int tot0 = 0;
     for (int c = 0; c < N; c++) {
@@ -710,6 +712,10 @@ struct hge_engine {
       kc[o_plo + c] = std::max(coords_len[c] - 1, 0);
       kc[o_lo + N + c] = tot0;  // fresh walk: fss rows from position 0 (qlo = 0 too)
       tot0 += chain_len[c];
+    }
+    for (int c = 0, b = 0; c < N; c++) {
+      kc[o_sb + c] = b;
+      b += div_up(chain_len[c] - coords_len[c], SEG);
     }
     kc[o_lo + 2 * N] = tot0;
     if (!segs.empty()) memcpy(&kc[o_seg], segs.data(), sizeof(int2) * segs.size());
@@ -721,6 +727,7 @@ struct hge_engine {
     k_qlo = s_kctl.p + o_qlo;
     k_lo = s_kctl.p + o_lo;
     k_segs = (int2*)(s_kctl.p + o_seg);
+    k_segbase = s_kctl.p + o_sb;
     KLAUNCH(k_chain_fill, dim3(div_up((int)(n1 - n0), 256)), dim3(256), 0, st, t, (int)n0, (int)n1);
     coords_sweep(t, (int)segs.size(), SEG, maxnew, fresh);
     cs_pending = true;
@@ -1098,9 +1105,16 @@ struct hge_engine {
     const int MAXSW = 4096;
     s_chg.need(MAXSW);
     const bool p16 = sweep16();
+    // skip segments whose inputs did not change in the previous sweep (HGE_SWEEP_SKIP=0: off)
+    static const bool SKIP = !(getenv("HGE_SWEEP_SKIP") && atoi(getenv("HGE_SWEEP_SKIP")) == 0);
+    int32_t* dirty = nullptr;
+    if (p16 && SKIP) {
+      s_dirty.need(nseg);
+      dirty = s_dirty.p;
+    }
     if (p16)
       KLAUNCH(k_la_clear16, dim3(std::max(1, std::min(64, div_up((int64_t)maxnew * t.NW2, 256))), N),
-              dim3(256), 0, st, t, olen, len, s_chg.p, MAXSW);
+              dim3(256), 0, st, t, olen, len, s_chg.p, MAXSW, dirty, nseg);
     else
       KLAUNCH(k_la_clear, dim3(std::max(1, std::min(64, div_up((int64_t)maxnew * N, 256))), N),
               dim3(256), 0, st, t, olen, len, s_chg.p, MAXSW);
@@ -1116,7 +1130,7 @@ struct hge_engine {
 #define SW16(NPV)                                                                                \
   case NPV:                                                                                      \
     KLAUNCH(k_la_sweep16<NPV>, dim3(div_up(nseg, 256 / NPV)), dim3(256), 0, st, t, k_segs, nseg, \
-            SEG, len, prev, s_chg.p + sw);                                                       \
+            SEG, len, prev, s_chg.p + sw, olen, k_segbase, dirty, sw);                          \
     break;
             SW16(32)
             SW16(64)
@@ -1517,10 +1531,12 @@ struct hge_engine {
                      int R_last, bool fresh) {
     // N > 16: the median is a wave-wide radix select (k_median_wave).  A fresh
     // replay's candidates are every event in id order (candidate q = event q),
-    // so the waves can walk the chain table instead (HGE_MEDIAN_ORDER=id: not)
+    // so the waves could walk the chain table instead (k_median_chain,
+    // HGE_MEDIAN_ORDER=chain; measured slower than k_median_wave at 256/2M and
+    // 256/10M: 8.1 vs 6.2 ms and 48 vs 39 ms per replay, profiles/r02)
     const bool wmed = N > 16;
-    static const bool by_id = getenv("HGE_MEDIAN_ORDER") && strcmp(getenv("HGE_MEDIAN_ORDER"), "id") == 0;
-    const bool chain_order = !by_id && fresh && cand == d_und.p && (int64_t)ncand == n_events &&
+    static const bool by_chain = getenv("HGE_MEDIAN_ORDER") && strcmp(getenv("HGE_MEDIAN_ORDER"), "chain") == 0;
+    const bool chain_order = by_chain && fresh && cand == d_und.p && (int64_t)ncand == n_events &&
                              (int64_t)N * ccap < INT32_MAX;
     int32_t* bseg = nullptr;
     if (wmed) {

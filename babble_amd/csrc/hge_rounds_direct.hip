@@ -35,6 +35,7 @@ namespace hge {
 
 constexpr int DIR_W = 64;   // candidate rows staged per window
 constexpr int DIR_MAXP = 16;  // probe counters per window (2 + log2(DIR_W) are used)
+constexpr int DIR_CH = 32;    // rows per fetch chunk (a round advances ~EPR/N ~ 14 rows)
 
 template <int BS, int NPOW>
 struct DirGeo {
@@ -45,7 +46,7 @@ struct DirGeo {
   static constexpr int PS = CW + VW;          // LDS words per (row, part): parts on distinct banks
   static constexpr int RS = TPM * PS;         // LDS words per candidate row
   static constexpr int WIN_INTS = DIR_W * NPOW;      // ints of a full window (N = NPOW)
-  static constexpr int PREF = (WIN_INTS / 4 + BS - 1) / BS;  // int4 per thread
+  static constexpr int PREF = (DIR_CH * NPOW / 4 + BS - 1) / BS;  // int4 per thread and chunk
   static constexpr int MBW = NPOW / 2;        // staged member row: packed words
 };
 
@@ -71,7 +72,7 @@ __device__ __forceinline__ uint32_t dir_pack_fd(int a, int b) {
 // slot p % DIR_W, and the ring holds [lo, lo + DIR_W) for the current lo.  Moving
 // the window from lo to lo' only fetches rows [max(lo + W, lo'), lo' + W): ~EPR/N
 // rows per round instead of W.
-// dir_fetch: rows [p0, p0 + nr) of chain c into registers (int4 slices of the
+// dir_fetch: rows [p0, p0 + min(nr, DIR_CH)) of chain c into registers (int4 slices of the
 // contiguous chain-major rows; rows >= lenc read as -2 = "no row").  N % 4 == 0
 // (the host takes the gather path of hge_rounds_coop.hip otherwise).
 template <int BS, int NPOW>
@@ -79,6 +80,7 @@ __device__ __forceinline__ void dir_fetch(const Tables& t, int c, int p0, int nr
                                           int4 (&v)[DirGeo<BS, NPOW>::PREF]) {
   using G = DirGeo<BS, NPOW>;
   const int N = t.N;
+  nr = min(nr, DIR_CH);
   const int have = (p0 == INF32 || nr <= 0) ? 0 : max(0, min(nr, lenc - p0));
   if (have == 0) return;  // block-uniform
   const int32_t* base = t.LA + ((size_t)c * t.ccap + p0) * (size_t)N;
@@ -100,6 +102,7 @@ __device__ __forceinline__ void dir_store(const Tables& t, DirLDS<BS, NPOW>& L, 
   using G = DirGeo<BS, NPOW>;
   const int N = t.N;
   if (p0 == INF32 || nr <= 0) return;
+  nr = min(nr, DIR_CH);
   const int have = max(0, min(nr, lenc - p0));
 #pragma unroll
   for (int m = 0; m < G::PREF; m++) {
@@ -114,6 +117,17 @@ __device__ __forceinline__ void dir_store(const Tables& t, DirLDS<BS, NPOW>& L, 
     const int slot = (p0 + row) & (DIR_W - 1);
     uint2* dst = (uint2*)(L.sLA + slot * G::RS + part * G::PS + w);
     *dst = make_uint2(dir_pack_la(v[m].x, v[m].y), dir_pack_la(v[m].z, v[m].w));
+  }
+}
+
+// rows [p0, p0 + nr) into their ring slots, chunk by chunk (caller syncs before a probe)
+template <int BS, int NPOW>
+__device__ __forceinline__ void dir_load(const Tables& t, DirLDS<BS, NPOW>& L, int c, int p0, int nr, int lenc,
+                                         int4 (&v)[DirGeo<BS, NPOW>::PREF]) {
+  if (p0 == INF32) return;
+  for (int q = 0; q < nr; q += DIR_CH) {
+    dir_fetch<BS, NPOW>(t, c, p0 + q, nr - q, lenc, v);
+    dir_store<BS, NPOW>(t, L, p0 + q, nr - q, lenc, v);
   }
 }
 
@@ -148,13 +162,31 @@ template <int BS, int NPOW>
 __device__ __forceinline__ void dir_members_mb(const uint32_t* mb, int d, int part,
                                                uint32_t (&mw)[DirGeo<BS, NPOW>::CW]) {
   using G = DirGeo<BS, NPOW>;
-  const gu64_t* src = (const gu64_t*)(mb + (size_t)d * G::MBW + part * G::CW);
+  if constexpr (G::CW % 4 == 0) {
+    // 16-byte buffer_load_dwordx4 sc1 (aux bit 4; the table row allows 4-, 8- and
+    // 16-byte loads of 8-byte sc1 stores): 8-byte loads run at 0.54-0.70x the
+    // 16-byte rate (MI355X_MICROARCH.md)
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)mb, 0, NPOW * G::MBW * 4, 0x00020000);
+    const int off = (d * G::MBW + part * G::CW) * 4;
 #pragma unroll
-  for (int k = 0; k < G::CW / 2; k++) {
-    const unsigned long long x =
-        __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    mw[2 * k] = (uint32_t)x;
-    mw[2 * k + 1] = (uint32_t)(x >> 32);
+    for (int k = 0; k < G::CW / 4; k++) {
+      const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * k, 0, 16);
+      mw[4 * k] = x.x;
+      mw[4 * k + 1] = x.y;
+      mw[4 * k + 2] = x.z;
+      mw[4 * k + 3] = x.w;
+    }
+  } else {
+    const gu64_t* s8 = (const gu64_t*)(mb + (size_t)d * G::MBW + part * G::CW);
+#pragma unroll
+    for (int k = 0; k < G::CW / 2; k++) {
+      const unsigned long long x =
+          __hip_atomic_load(s8 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      mw[2 * k] = (uint32_t)x;
+      mw[2 * k + 1] = (uint32_t)(x >> 32);
+    }
   }
 }
 
@@ -199,20 +231,33 @@ __device__ __forceinline__ int dir_count(const DirLDS<BS, NPOW>& L, int p, int p
       la[k + 1] = q.y;
     }
   }
-  uint32_t acc = 0;
+  uint32_t acc0 = 0, acc1 = 0;
   const uint32_t ones = 0x00010001u;
+  static_assert(G::CW % 2 == 0, "member slices are whole word pairs");
 #pragma unroll
-  for (int k = 0; k < G::CW; k++) {
+  for (int k = 0; k < G::CW; k += 2) {
     // (la + 2) -sat (m + 1) is nonzero <=> la >= m (v_pk_sub_u16 clamp saturates at 0);
-    // min(., 1) per half, then a packed add: 3 VALU ops per 2 columns
-    uint32_t df;
-    asm("v_pk_sub_u16 %0, %2, %3 clamp\n\tv_pk_min_u16 %0, %0, %4\n\tv_pk_add_u16 %1, %1, %0"
-        : "=&v"(df), "+v"(acc)
-        : "v"(la[k]), "v"(mw[k]), "v"(ones));
+    // min(., 1) per half, then a packed add: 3 VALU ops per 2 columns.  Two words per
+    // asm statement and two accumulators (no dependent chain, and the compiler's
+    // hazard padding between asm statements falls on every other word pair at most)
+    uint32_t d0, d1;
+    asm("v_pk_sub_u16 %0, %4, %6 clamp\n\t"
+        "v_pk_sub_u16 %1, %5, %7 clamp\n\t"
+        "v_pk_min_u16 %0, %0, %8\n\t"
+        "v_pk_min_u16 %1, %1, %8\n\t"
+        "v_pk_add_u16 %2, %2, %0\n\t"
+        "v_pk_add_u16 %3, %3, %1"
+        : "=&v"(d0), "=&v"(d1), "+v"(acc0), "+v"(acc1)
+        : "v"(la[k]), "v"(la[k + 1]), "v"(mw[k]), "v"(mw[k + 1]), "v"(ones));
   }
-  int cnt = (int)(acc & 0xFFFFu) + (int)(acc >> 16);
-#pragma unroll
-  for (int o = 1; o < G::TPM; o <<= 1) cnt += __shfl_xor(cnt, o);
+  int cnt = (int)(acc0 & 0xFFFFu) + (int)(acc0 >> 16) + (int)(acc1 & 0xFFFFu) + (int)(acc1 >> 16);
+  // sum over the member's TPM consecutive lanes by DPP (no LDS permutes): quad_perm
+  // xor 1 and xor 2, then row_half_mirror (quads of an 8) and row_mirror (8s of a row)
+  if constexpr (G::TPM > 1) cnt += __builtin_amdgcn_mov_dpp(cnt, 0xB1, 0xF, 0xF, false);
+  if constexpr (G::TPM > 2) cnt += __builtin_amdgcn_mov_dpp(cnt, 0x4E, 0xF, 0xF, false);
+  if constexpr (G::TPM > 4) cnt += __builtin_amdgcn_mov_dpp(cnt, 0x141, 0xF, 0xF, false);
+  if constexpr (G::TPM > 8) cnt += __builtin_amdgcn_mov_dpp(cnt, 0x140, 0xF, 0xF, false);
+  static_assert(G::TPM <= 16, "a member's lanes lie in one DPP row");
   return cnt;
 }
 
@@ -255,9 +300,8 @@ __device__ int dir_select(const Tables& t, int c, int lenc, DirLDS<BS, NPOW>& L,
       if (lo + DIR_W >= lenc) return INF32;
       // the answer lies past the window: the whole next window, fresh counters
       lo += DIR_W;
-      dir_fetch<BS, NPOW>(t, c, lo, DIR_W, lenc, pv);
-      __syncthreads();
-      dir_store<BS, NPOW>(t, L, lo, DIR_W, lenc, pv);
+      __syncthreads();  // every thread has read this window's counters
+      dir_load<BS, NPOW>(t, L, c, lo, DIR_W, lenc, pv);
       if (threadIdx.x < DIR_MAXP) L.sCnt[threadIdx.x] = 0;
       slot = 0;
       __syncthreads();
@@ -289,8 +333,9 @@ __global__ void __launch_bounds__(BS) k_rounds_direct(Tables t, const int32_t* o
   // first reached stopcut on every chain (the next walker's start; rstate[1] = 2),
   // or at the empty frontier; rstate[0] = rows written.
   using G = DirGeo<BS, NPOW>;
-  // HGE_STAMPS diagnostics (workgroup 0, thread 0): cycles per section into dbg[0..6]
-  uint64_t st_t = 0, st_acc[7] = {0, 0, 0, 0, 0, 0, 0};
+  // HGE_STAMPS diagnostics (workgroup 0, thread 0): cycles per section into dbg[0..8]
+  // (6 = probes; 7, 8 = member-load issue and arrival inside section 0)
+  uint64_t st_t = 0, st_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   const bool stamping = dbg && blockIdx.x == 0 && threadIdx.x == 0;
 #define DSTAMP(k)                             \
   if (stamping) {                             \
@@ -322,8 +367,7 @@ __global__ void __launch_bounds__(BS) k_rounds_direct(Tables t, const int32_t* o
   int extra_left = -1;  // history mode: rows still to walk after passing stopcut
   int4 pv[G::PREF];
   int lo = L.sP[c];
-  dir_fetch<BS, NPOW>(t, c, lo, DIR_W, lenc, pv);
-  dir_store<BS, NPOW>(t, L, lo, DIR_W, lenc, pv);
+  dir_load<BS, NPOW>(t, L, c, lo, DIR_W, lenc, pv);
   int f0 = INF32, fn = 0;  // rows fetched for the next round: [f0, f0 + fn)
   for (int r = rlo;; r++) {
     if (r + 1 >= rcap) {
@@ -337,6 +381,11 @@ __global__ void __launch_bounds__(BS) k_rounds_direct(Tables t, const int32_t* o
     uint32_t mw[G::CW];
     if (r == rlo) dir_members_fd<BS, NPOW>(t, d, part, d < N ? L.sP[d] : INF32, mw);
     else dir_members_mb<BS, NPOW>(mbp[r & 1], d < N ? d : 0, part, mw);
+    if (stamping) {  // diagnostics only: issue, then arrival of wave 0's member loads
+      DSTAMP(7);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      DSTAMP(8);
+    }
     if (d >= N) {
 #pragma unroll
       for (int k = 0; k < G::CW; k++) mw[k] = 0xFFFFFFFFu;
@@ -380,8 +429,7 @@ __global__ void __launch_bounds__(BS) k_rounds_direct(Tables t, const int32_t* o
         if (nxt < lo || nxt >= lo + DIR_W) {
           __syncthreads();
           lo = nxt;
-          dir_fetch<BS, NPOW>(t, c, lo, DIR_W, lenc, pv);
-          dir_store<BS, NPOW>(t, L, lo, DIR_W, lenc, pv);
+          dir_load<BS, NPOW>(t, L, c, lo, DIR_W, lenc, pv);
           __syncthreads();
         }
         pb = dir_count<BS, NPOW>(L, nxt, part, mw) >= t.SM;
@@ -458,10 +506,11 @@ __global__ void __launch_bounds__(BS) k_rounds_direct(Tables t, const int32_t* o
       }
     }
     dir_store<BS, NPOW>(t, L, f0, fn, lenc, pv);
+    if (fn > DIR_CH) dir_load<BS, NPOW>(t, L, c, f0 + DIR_CH, fn - DIR_CH, lenc, pv);  // rare
     DSTAMP(5);
   }
   if (stamping)
-    for (int q = 0; q < 7; q++) dbg[q] += st_acc[q];
+    for (int q = 0; q < 9; q++) dbg[q] += st_acc[q];
 #undef DSTAMP
 }
 

@@ -51,7 +51,7 @@ if [[ $WHAT == stamps ]]; then
   # section cycles of the direct rounds step (workgroup 0), and median / rounds A/B
   HGE_STAMPS=1 timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-secondary --participants 256 --events 2000000 --steps 1 --warmup 0 --ramp-s 0 --profile-steps 1 > $OUT/st.json 2> $OUT/st.err || { tail -20 $OUT/st.err; exit 1; }
   grep "hge stamps" $OUT/st.err | tail -2
-  for env in "HGE_MEDIAN_ORDER=id" "HGE_ROUNDS_STEP=fss" "X=1"; do
+  for env in ${ABENVS:-HGE_SWEEP_SKIP=0 HGE_MEDIAN_ORDER=chain X=1}; do
     env $env timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-secondary --participants 256 --events 2000000 --steps 3 --warmup 1 > $OUT/ab.json 2> $OUT/ab.err || { tail -20 $OUT/ab.err; exit 1; }
     python -c "
 import json

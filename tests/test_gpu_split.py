@@ -54,7 +54,9 @@ def test_split_equals_replay(n, E, G, extra):
         r2, w2 = eng.event_rounds()
         np.testing.assert_array_equal(r2, r1)
         np.testing.assert_array_equal(w2, w1)
-        assert all(len(h[0]) < ref.rounds() for h in hists[:-1])  # every walker did part of it
+        # the later walkers started mid-way (rank 0 may walk to the end when the
+        # overlap `extra` reaches past the last round)
+        assert all(len(h[0]) < ref.rounds() for h in hists[1:])
     finally:
         ref.close()
         eng.close()
