@@ -156,6 +156,8 @@ struct hge_engine {
   // coordinate sweeps: transposed tables and scratch
   int n_sweeps = 0;
   DBuf<int32_t> d_LAT, d_FDT, s_chg, s_bar, s_dirty;
+  DBuf<int64_t> d_FDTS;  // N > 16: timestamps at the FD positions (the wide median)
+  DBuf<int32_t> d_WLA;   // N > 16: round frontier rows transposed (k_witness_la)
   DBuf<uint64_t> d_ssc, s_gran;
   DBuf<int32_t> s_bseg;
   DBuf<uint64_t> s_H;                // speculative walk: epoch-tagged histories
@@ -221,6 +223,8 @@ struct hge_engine {
     t.NW2 = (N + 1) / 2;
     t.LA16 = d_LA16.p;
     t.FD = d_FD.p;
+    t.FDTS = d_FDTS.p;
+    t.WLA = d_WLA.p;
     t.round = d_round.p;
     t.wit = d_wit.p;
     t.C = d_C.p;
@@ -325,9 +329,10 @@ struct hge_engine {
                              &s_recv,    &s_rr,     &s_bpos,  &s_fund,   &s_upos,    &s_vis,
                              &s_und2,    &s_part,   &s_fst,    &d_FSS,     &d_LAT,
                              &d_FDT,     &s_chg,    &s_bar,   &s_bseg,   &s_kctl,    &s_cctl,
-                             &s_out,     &s_hn,     &s_hres,  &s_dirty};
+                             &s_out,     &s_hn,     &s_hres,  &s_dirty,  &d_WLA};
     for (auto* b : i32s) b->free_();
     d_ts.free_();
+    d_FDTS.free_();
     d_cts.free_();
     s_cts.free_();
     d_S.free_();
@@ -444,6 +449,17 @@ struct hge_engine {
       d_LA16.n = (size_t)N * nc * w;
     }
     grow_chain_table(d_FD, nc, true);
+    if (N > 16) {  // FDTS rows below a batch's qlo are kept
+      int64_t* q = nullptr;
+      HIPCHK(hipMalloc(&q, sizeof(int64_t) * (size_t)N * nc * N));
+      if (ccap > 0 && d_FDTS.p)
+        HIPCHK(hipMemcpy2DAsync(q, sizeof(int64_t) * nc * N, d_FDTS.p, sizeof(int64_t) * ccap * N,
+                                sizeof(int64_t) * ccap * N, N, hipMemcpyDeviceToDevice, st));
+      sync();
+      d_FDTS.free_();
+      d_FDTS.p = q;
+      d_FDTS.n = (size_t)N * nc * N;
+    }
     // first-strong-seer rows (N <= 32): int32 rows of N, or uint16 rows padded to
     // 16/32 columns for the LDS walk; rebuilt from the frontier on, never kept
     if (N <= 32) d_FSS.need((size_t)N * nc * std::max(N, 16));
@@ -949,6 +965,7 @@ struct hge_engine {
     return (N & 3) == 0;
   }
 
+
   // rounds of a wide hashgraph: cooperative frontier kernel (hge_rounds_coop.hip)
   void rounds_coop(bool fresh) {
     Tables t = tables();
@@ -1181,8 +1198,12 @@ struct hge_engine {
     }
     int span = 1;
     for (int c = 0; c < N; c++) span = std::max(span, chain_len[c] - qlo[c]);
-    KLAUNCH(k_transpose, dim3(div_up(span, 64), div_up(N, 64), N), dim3(256), 0, st, t, d_FDT.p,
-            (int32_t*)nullptr, k_qlo, len, 1);
+    if (N > 16)
+      KLAUNCH(k_fd_transpose_ts, dim3(div_up(span, 64), div_up(N, 64), N), dim3(256), 0, st, t,
+              (const int32_t*)d_FDT.p, k_qlo, len);
+    else
+      KLAUNCH(k_transpose, dim3(div_up(span, 64), div_up(N, 64), N), dim3(256), 0, st, t, d_FDT.p,
+              (int32_t*)nullptr, k_qlo, len, 1);
   }
 
   // ---------------- one batch of consensus calls ----------------
@@ -1529,19 +1550,22 @@ struct hge_engine {
 
   void recv_dispatch(const Tables& t, const int32_t* cand, int ncand, int ncalls, int rr_lo,
                      int R_last, bool fresh) {
-    // N > 16: the median is a wave-wide radix select (k_median_wave).  A fresh
-    // replay's candidates are every event in id order (candidate q = event q),
-    // so the waves could walk the chain table instead (k_median_chain,
-    // HGE_MEDIAN_ORDER=chain; measured slower than k_median_wave at 256/2M and
-    // 256/10M: 8.1 vs 6.2 ms and 48 vs 39 ms per replay, profiles/r02)
+    // N > 16: the median is a wave-wide radix select (k_median_wave) over coalesced
+    // rows: the round frontier rows transposed (WLA, k_witness_la, for every round a
+    // candidate can receive) and the FD timestamps (FDTS).  A fresh replay's
+    // candidate list is the identity (candidate q = event q).
     const bool wmed = N > 16;
-    static const bool by_chain = getenv("HGE_MEDIAN_ORDER") && strcmp(getenv("HGE_MEDIAN_ORDER"), "chain") == 0;
-    const bool chain_order = by_chain && fresh && cand == d_und.p && (int64_t)ncand == n_events &&
-                             (int64_t)N * ccap < INT32_MAX;
+    const bool ident = fresh && cand == d_und.p && (int64_t)ncand == n_events;
     int32_t* bseg = nullptr;
     if (wmed) {
       s_bseg.need(ncand);
       bseg = s_bseg.p;
+      if (R_last > rr_lo) {
+        d_WLA.need((size_t)Rcap * N * N);
+        Tables tw = tables();
+        KLAUNCH(k_witness_la, dim3(div_up(N, 64), div_up(N, 64), R_last - rr_lo), dim3(256), 0, st, tw,
+                rr_lo);
+      }
     }
     switch (NW) {
 #define RCASE(B)                                                                                 \
@@ -1551,13 +1575,10 @@ struct hge_engine {
                        s_segcnt.p,                                                               \
                        s_segcall.p, s_segdec.p, s_segfws.p, s_theta.p, s_recv.p, s_rr.p,         \
                        s_cts.p, bseg);                                                           \
-    if (wmed && chain_order)                                                                     \
-      KLAUNCH(k_median_chain<B>, dim3(div_up((int64_t)N * div_up(ccap, MC_S), 4)), dim3(256), 0,  \
-              st, t, (const int32_t*)k_len + N, div_up(ccap, MC_S), s_recv.p, s_rr.p, bseg,      \
-              s_segfws.p, s_cts.p);                                                              \
-    else if (wmed)                                                                               \
-      KLAUNCH(k_median_wave<B>, dim3(div_up(ncand, 4)), dim3(256), 0, st, t, cand, ncand,        \
-              s_recv.p, s_rr.p, bseg, s_segfws.p, s_cts.p, (const int32_t*)nullptr, ncand);      \
+    if (wmed)                                                                                    \
+      KLAUNCH(k_median_wave<B>, dim3(div_up(ncand, 4)), dim3(256), 0, st, tables(),              \
+              ident ? (const int32_t*)nullptr : cand, ncand, s_recv.p, s_rr.p, bseg, s_segfws.p,  \
+              s_cts.p);                                                                          \
     break;
       RCASE(1)
       RCASE(2)

@@ -39,6 +39,8 @@ struct Tables {
   int32_t* chain;
   int2* opcp;     // [N][ccap]: (creator, index) of the other-parent, (-1, -1) if none
   int64_t* tsch;  // [N][ccap]: timestamp of the event at (chain, position)
+  int64_t* FDTS;  // N > 16: [N][ccap][N] timestamp of the event at FD[(c, p)][j] (0: none)
+  int32_t* WLA;   // N > 16: [Rcap][N][N] LA[(d, C[r][d])][cx] at [r][cx][d]
   int32_t* LA;
   int32_t* FD;
   int32_t* round;
@@ -1448,6 +1450,7 @@ __device__ __forceinline__ int64_t wave_upper_median(const uint64_t (&v)[VPL], c
     bool live[VPL];
 #pragma unroll
     for (int k = 0; k < VPL; k++) live[k] = in[k];
+    int nlive = n;
     for (int b = top; b >= 0; b--) {
       int c0 = 0;
 #pragma unroll
@@ -1456,162 +1459,87 @@ __device__ __forceinline__ int64_t wave_upper_median(const uint64_t (&v)[VPL], c
       if (one) {
         kk -= c0;
         prefix |= 1ull << b;
+        nlive -= c0;
+      } else {
+        nlive = c0;
       }
 #pragma unroll
       for (int k = 0; k < VPL; k++) live[k] = live[k] && (((v[k] >> b) & 1ull) == (one ? 1ull : 0ull));
+      if (nlive == 1) {
+        // one value left with this prefix: it is the answer (kk == 0), low bits and all
+        // (~8 bits in for distinct values instead of every bit below the top one)
+#pragma unroll
+        for (int k = 0; k < VPL; k++) {
+          const uint64_t m = __ballot(live[k]);
+          if (m) return (int64_t)((uint64_t)__shfl((long long)v[k], (int)__builtin_ctzll(m)) ^ 0x8000000000000000ull);
+        }
+      }
     }
   }
   return (int64_t)(prefix ^ 0x8000000000000000ull);
 }
 
+// The round-r frontier rows transposed, for every round a received event can
+// have: WLA[r][cx][d] = LA[(d, C[r][d])][cx] (-1: chain d has no event of round
+// >= r).  The witness of round r on chain d sits at C[r][d]; w_d sees x iff
+// index(x) <= WLA[r][creator(x)][d].  64 x 64 tiles through LDS.
+__global__ void __launch_bounds__(256) k_witness_la(Tables t, int rr_lo) {
+  __shared__ int32_t tile[64][65];
+  const int N = t.N;
+  const int rr = rr_lo + blockIdx.z;
+  const int d0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {
+    const int d = d0 + r, cx = c0 + tx;
+    int v = -1;
+    if (d < N && cx < N) {
+      const int pw = t.C[(size_t)rr * N + d];
+      if (pw != INF32) v = t.LA[rowoff(t, d, pw) + cx];
+    }
+    tile[r][tx] = v;
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const int cx = c0 + r, d = d0 + tx;
+    if (cx < N && d < N) t.WLA[((size_t)rr * N + cx) * N + d] = tile[tx][r];
+  }
+}
+
 // MedianTimestamp (hashgraph.go:762-770) for wide hashgraphs: one wave per
 // received event.  Lane l holds the timestamps of the famous witnesses
-// d = l, l+64, ... that see x (OSA(w, x) = FD[x][cw]); the upper median
-// (element len/2 of the sorted list) is found by a bitwise radix select over
-// the order-preserving uint64 image of the int64 timestamps, skipping the
-// high bits every candidate shares.
-//
-// Work order (order != nullptr, fresh replays where candidate q is event q):
-// wave slots walk the chain table (chain-major, holes = -1) and blocks are
-// dealt so that each XCD takes one contiguous run of slots (blocks b and b + 8
-// share an XCD; the grid is a multiple of 8).  Consecutive events of a chain
-// then run on the same XCD: the round-rr witnesses' LA cells and the tsch
-// timestamps at FD[x][d] (non-decreasing along the chain) stay in its L2
-// instead of being gathered from HBM once per event.
+// d = l, l+64, ... that see x (OSA(w, x) = FD[x][cw], its timestamp FDTS[x][cw]);
+// the upper median (element len/2 of the sorted list) is found by a bitwise
+// radix select over the order-preserving uint64 image of the int64 timestamps.
+// Every per-witness input is a coalesced row: the "sees x" thresholds
+// WLA[rr][cx][.] (k_witness_la) and the timestamps FDTS[x][.] (k_fd_transpose_ts),
+// instead of 2N scattered gathers per event.
 template <int VPL>
 __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* cand, int ncand,
                                                      const int32_t* recv_call, const int32_t* rr_in,
                                                      const int32_t* bseg, const uint64_t* seg_fws,
-                                                     int64_t* cts_out, const int32_t* order, int nslot) {
-  int q;
-  if (order) {
-    const int per = gridDim.x >> 3;
-    const int eb = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
-    const int slot = eb * 4 + (threadIdx.x >> 6);
-    if (slot >= nslot) return;
-    q = order[slot];
-    if (q < 0) return;
-  } else {
-    q = blockIdx.x * 4 + (threadIdx.x >> 6);
-  }
+                                                     int64_t* cts_out) {
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (q >= ncand || recv_call[q] < 0) return;  // wave-uniform
+  if (q >= ncand) return;  // wave-uniform
   const int N = t.N, NW = t.NW;
-  const int x = cand[q];
+  const int x = cand ? cand[q] : q;
+  const int rc = recv_call[q], rr = rr_in[q], sg = bseg[q];
   const int cx = t.creator[x], ix = t.index[x];
-  const int rr = rr_in[q], sg = bseg[q];
-  const int32_t* fdx = t.FD + rowoff(t, cx, ix);
+  if (rc < 0) return;  // wave-uniform
+  const int32_t* thr = t.WLA + ((size_t)rr * N + cx) * N;
+  const int64_t* tsr = t.FDTS + ((size_t)cx * t.ccap + ix) * N;
   uint64_t v[VPL];
   bool in[VPL];
 #pragma unroll
   for (int k = 0; k < VPL; k++) {
     const int d = lane + 64 * k;
-    in[k] = false;
-    v[k] = ~0ull;
-    if (d < N && ((seg_fws[(size_t)sg * NW + (d >> 6)] >> (d & 63)) & 1ull)) {
-      // the witness of round rr on chain d is the first event there with round >= rr,
-      // i.e. position C[rr][d]: a coalesced load instead of W then index[w]
-      const int pw = t.C[(size_t)rr * N + d];
-      if (t.LA[rowoff(t, d, pw) + cx] >= ix) {
-        // ts of OSA(w, x) = the event at (d, FD[x][d]): one gather, not chain then ts
-        v[k] = (uint64_t)t.tsch[(size_t)d * t.ccap + fdx[d]] ^ 0x8000000000000000ull;
-        in[k] = true;
-      }
-    }
+    const int dd = d < N ? d : 0;
+    const bool fam = d < N && ((seg_fws[(size_t)sg * NW + (dd >> 6)] >> (dd & 63)) & 1ull);
+    in[k] = fam && thr[dd] >= ix;
+    v[k] = in[k] ? ((uint64_t)tsr[dd] ^ 0x8000000000000000ull) : ~0ull;
   }
   const int64_t med = wave_upper_median<VPL>(v, in);
   if (lane == 0) cts_out[q] = med;
-}
-
-// MedianTimestamp for a fresh replay's candidates (candidate q = event q), one
-// wave per MC_S consecutive positions of one chain cx.  Along a chain:
-//   * the events' (call, roundReceived, segment) come in with one gather per
-//     lane for all MC_S positions up front (lane j = position p0 + j);
-//   * the round-rr witnesses' "sees x" thresholds LA[w_d][cx] are reloaded only
-//     when (rr, segment) changes (~once per EPR/N events): w_d sees x iff
-//     index(x) <= LA[w_d][cx];
-//   * the FD row of the next-but-one event and the tsch gathers of the next one
-//     are in flight while the current event's median is selected (FD[x][d] is
-//     non-decreasing along the chain, so the gathers walk forward in each
-//     chain's timestamps).
-constexpr int MC_S = 64;
-template <int VPL>
-__global__ void __launch_bounds__(256) k_median_chain(Tables t, const int32_t* len, int nseg,
-                                                      const int32_t* recv_call, const int32_t* rr_in,
-                                                      const int32_t* bseg, const uint64_t* seg_fws,
-                                                      int64_t* cts_out) {
-  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int N = t.N, NW = t.NW;
-  const int cx = wave / nseg;
-  if (cx >= N) return;
-  const int p0 = (wave - cx * nseg) * MC_S;
-  const int lenc = len[cx];
-  if (p0 >= lenc) return;
-  const int np = min(MC_S, lenc - p0);
-  // per-position scalars, lane j = position p0 + j
-  const int xj = lane < np ? t.chain[(size_t)cx * t.ccap + p0 + lane] : 0;
-  const int rcj = lane < np ? recv_call[xj] : -1;
-  const int rrj = rcj >= 0 ? rr_in[xj] : -1;
-  const int sgj = rcj >= 0 ? bseg[xj] : -1;
-  const uint64_t live = __ballot(rcj >= 0);
-  if (!live) return;
-  const int32_t* fdrow = t.FD + rowoff(t, cx, p0);
-  int thr[VPL];
-  int crr = -1, csg = -1;
-  // pipeline: fd for event j + 1 and tsch values for event j are in flight
-  int fdn[VPL];
-  uint64_t tv[VPL];
-#pragma unroll
-  for (int k = 0; k < VPL; k++) {
-    const int d = lane + 64 * k;
-    const int f = d < N ? fdrow[d] : INF32;
-    tv[k] = (d < N && f != INF32) ? (uint64_t)t.tsch[(size_t)d * t.ccap + f] : 0ull;
-    fdn[k] = (d < N && np > 1) ? fdrow[(size_t)N + d] : INF32;
-  }
-  for (int j = 0; j < np; j++) {
-    const int rr = __shfl(rrj, j), sg = __shfl(sgj, j), x = __shfl(xj, j);
-    const bool act = (live >> j) & 1ull;
-    // next event's timestamps and the one after's FD row go out before the select
-    uint64_t tn[VPL];
-    int fdn2[VPL];
-#pragma unroll
-    for (int k = 0; k < VPL; k++) {
-      const int d = lane + 64 * k;
-      tn[k] = (j + 1 < np && d < N && fdn[k] != INF32) ? (uint64_t)t.tsch[(size_t)d * t.ccap + fdn[k]] : 0ull;
-      fdn2[k] = (j + 2 < np && d < N) ? fdrow[(size_t)(j + 2) * N + d] : INF32;
-    }
-    if (act) {
-      if (rr != crr || sg != csg) {
-        crr = rr;
-        csg = sg;
-#pragma unroll
-        for (int k = 0; k < VPL; k++) {
-          const int d = lane + 64 * k;
-          thr[k] = -1;
-          if (d < N && ((seg_fws[(size_t)sg * NW + (d >> 6)] >> (d & 63)) & 1ull)) {
-            // the round-rr witness of chain d is the first event there with round >= rr
-            const int pw = t.C[(size_t)rr * N + d];
-            thr[k] = t.LA[rowoff(t, d, pw) + cx];
-          }
-        }
-      }
-      uint64_t v[VPL];
-      bool in[VPL];
-#pragma unroll
-      for (int k = 0; k < VPL; k++) {
-        in[k] = p0 + j <= thr[k];
-        v[k] = in[k] ? (tv[k] ^ 0x8000000000000000ull) : ~0ull;
-      }
-      const int64_t med = wave_upper_median<VPL>(v, in);
-      if (lane == 0) cts_out[x] = med;
-    }
-#pragma unroll
-    for (int k = 0; k < VPL; k++) {
-      tv[k] = tn[k];
-      fdn[k] = fdn2[k];
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------

@@ -48,6 +48,7 @@ struct DirGeo {
   static constexpr int WIN_INTS = DIR_W * NPOW;      // ints of a full window (N = NPOW)
   static constexpr int PREF = (DIR_CH * NPOW / 4 + BS - 1) / BS;  // int4 per thread and chunk
   static constexpr int MBW = NPOW / 2;        // staged member row: packed words
+  static constexpr int MVW = (CW % 4 == 0) ? 4 : 2;  // MB words per thread chunk (16 / 8 bytes)
 };
 
 template <int BS, int NPOW>
@@ -153,47 +154,46 @@ __device__ __forceinline__ void dir_members_fd(const Tables& t, int d, int part,
 
 // Member rows after the first round come from the staging block MB[parity]:
 // the workgroup of chain d packs its next frontier row FD[(d, C_{r+1}[d])] there
-// (wave 0, write-through 8-byte stores, vmcnt(0), then the granule), so every
-// consumer reads one contiguous 128 KB block (TLB- and L2-friendly) instead of
-// N rows scattered over N chain regions.  The granule poll is the flag; every
-// load of the block is an 8-byte relaxed agent-scope (sc1) load, as the
+// (wave 0, write-through 8-byte stores, vmcnt(0), then the granule).  MB is laid
+// out by consuming thread, chunk-major: word (k * BS + tid) * MVW + s holds word
+// k * MVW + s of thread tid's slice, so load k of a wave reads one contiguous
+// 64 * 4 * MVW bytes (a row-major block made every wave load touch 64 cache
+// lines for 16 bytes each: TA-bound, ~13k cycles per round at N = 256).  The
+// granule poll is the flag; every load of the block is an sc1 load, as the
 // granule protocol requires (MI355X_MICROARCH.md, Valid forms, row 1).
 template <int BS, int NPOW>
-__device__ __forceinline__ void dir_members_mb(const uint32_t* mb, int d, int part,
-                                               uint32_t (&mw)[DirGeo<BS, NPOW>::CW]) {
+__device__ __forceinline__ void dir_members_mb(const uint32_t* mb, uint32_t (&mw)[DirGeo<BS, NPOW>::CW]) {
   using G = DirGeo<BS, NPOW>;
-  if constexpr (G::CW % 4 == 0) {
-    // 16-byte buffer_load_dwordx4 sc1 (aux bit 4; the table row allows 4-, 8- and
-    // 16-byte loads of 8-byte sc1 stores): 8-byte loads run at 0.54-0.70x the
-    // 16-byte rate (MI355X_MICROARCH.md)
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)mb, 0, NPOW * G::MBW * 4, 0x00020000);
-    const int off = (d * G::MBW + part * G::CW) * 4;
+  constexpr int MVW = G::MVW;
+  // buffer_load sc1 (aux bit 4; the table row allows 4-, 8- and 16-byte loads of
+  // 8-byte sc1 stores); 8-byte loads run at 0.54-0.70x the 16-byte rate
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)mb, 0, BS * G::CW * 4, 0x00020000);
 #pragma unroll
-    for (int k = 0; k < G::CW / 4; k++) {
-      const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * k, 0, 16);
+  for (int k = 0; k < G::CW / MVW; k++) {
+    const int off = (k * BS + (int)threadIdx.x) * MVW * 4;
+    if constexpr (MVW == 4) {
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
       mw[4 * k] = x.x;
       mw[4 * k + 1] = x.y;
       mw[4 * k + 2] = x.z;
       mw[4 * k + 3] = x.w;
-    }
-  } else {
-    const gu64_t* s8 = (const gu64_t*)(mb + (size_t)d * G::MBW + part * G::CW);
-#pragma unroll
-    for (int k = 0; k < G::CW / 2; k++) {
-      const unsigned long long x =
-          __hip_atomic_load(s8 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      mw[2 * k] = (uint32_t)x;
-      mw[2 * k + 1] = (uint32_t)(x >> 32);
+    } else {
+      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+      const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 16);
+      mw[2 * k] = x.x;
+      mw[2 * k + 1] = x.y;
     }
   }
 }
 
-// wave 0 of chain c's workgroup: stage FD[(c, p)] (p = INF32: no member) into MB
+// wave 0 of chain c's workgroup: stage FD[(c, p)] (p = INF32: no member) into MB.
+// Lane l packs columns 4l .. 4l + 3 into row words 2l, 2l + 1 (one part, one chunk).
 template <int BS, int NPOW>
 __device__ __forceinline__ void dir_stage_member(const Tables& t, uint32_t* mb, int c, int p) {
   using G = DirGeo<BS, NPOW>;
+  constexpr int MVW = G::MVW;
   const int lane = threadIdx.x;  // < 64
   const int N = t.N;
   if (4 * lane < NPOW) {
@@ -201,8 +201,10 @@ __device__ __forceinline__ void dir_stage_member(const Tables& t, uint32_t* mb, 
     if (p != INF32 && 4 * lane < N) a = *(const int4*)(t.FD + rowoff(t, c, p) + 4 * lane);
     const unsigned long long x =
         (unsigned long long)dir_pack_fd(a.x, a.y) | ((unsigned long long)dir_pack_fd(a.z, a.w) << 32);
-    __hip_atomic_store((gu64_t*)(mb + (size_t)c * G::MBW) + lane, x, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+    const int w = 2 * lane, part = w / G::CW, wp = w - part * G::CW;
+    const int k = wp / MVW, sub = wp - k * MVW;
+    const size_t word = ((size_t)k * BS + (size_t)c * G::TPM + part) * MVW + sub;
+    __hip_atomic_store((gu64_t*)(mb + word), x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -380,7 +382,7 @@ __global__ void __launch_bounds__(BS) k_rounds_direct(Tables t, const int32_t* o
     DSTAMP(-1);
     uint32_t mw[G::CW];
     if (r == rlo) dir_members_fd<BS, NPOW>(t, d, part, d < N ? L.sP[d] : INF32, mw);
-    else dir_members_mb<BS, NPOW>(mbp[r & 1], d < N ? d : 0, part, mw);
+    else dir_members_mb<BS, NPOW>(mbp[r & 1], mw);
     if (stamping) {  // diagnostics only: issue, then arrival of wave 0's member loads
       DSTAMP(7);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

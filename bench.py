@@ -53,7 +53,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 DEFAULT = (256, 10_000_000)
 
 
-def algorithmic_bytes(kernel, n, events, ordered):
+def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
     """Algorithmic HBM bytes of `kernel` over ONE whole replay (all its launches),
     int32 coordinates (B(N) = 24N + 48 per ordered event).
 
@@ -62,23 +62,32 @@ def algorithmic_bytes(kernel, n, events, ordered):
                     once per fixed-point sweep (the sweeps' re-reads are waste);
       k_la_clear     4N/event (the new rows' -1 fill);
       k_la_sweep16 / k_la_clear16  6N / 2N per event (N > 32: the same on packed u16);
-      k_transpose   16N/event (LA -> LAT and FDT -> FD: each reads and writes 4N);
+      k_transpose   16N/event at N <= 16 (LA -> LAT and FDT -> FD: each reads and
+                    writes 4N), 8N at 16 < N <= 32 (LA -> LAT only);
+      k_fd_transpose_ts 16N/event (N > 16: FDT read, FD and the 8-byte FD
+                    timestamps written);
+      k_witness_la   8N^2 per round (frontier rows read, transposed rows written);
       k_transpose16 10N/event (LA16 read, LA rows and LAT written);
       k_fdt_clear    4N/event; k_fdt_runs 8N/event (LAT read, FDT written);
       k_fss          8N/event (FD row read, fss row written, N <= 32);
       rounds        4N/event (the strongly-see round test reads each row once);
       k_round_received / k_median_wave (4N + 48) per ordered event (FD row for
                     the median, sort key); everything else the 48-byte key.
+                    (k_median_wave reads 4N + 8N: the thresholds row and the FD
+                    timestamps row; 4N + 48 stays the SURVEY 8(d) figure.)
     """
     name = kernel.strip("()").split("<")[0]
-    per_event = {"k_la_sweep": 12 * n, "k_la_clear": 4 * n, "k_transpose": 16 * n,
+    if name == "k_witness_la":
+        return 8 * n * n * rounds
+    per_event = {"k_la_sweep": 12 * n, "k_la_clear": 4 * n, "k_transpose": 16 * n if n <= 16 else 8 * n,
+                 "k_fd_transpose_ts": 16 * n,
                  "k_fdt_clear": 4 * n, "k_fdt_runs": 8 * n, "k_fss": 8 * n,
                  "k_rounds_walk": 4 * n, "k_rounds_coop": 4 * n, "k_rounds_coop_spec": 4 * n,
                  "k_walk_spec": 4 * n, "k_rounds_fss": 4 * n, "k_rounds_direct": 4 * n,
                  "k_la_clear16": 2 * n, "k_la_sweep16": 6 * n, "k_transpose16": 10 * n}
     if name in per_event:
         return per_event[name] * events
-    if name in ("k_round_received", "k_median_wave", "k_median_chain"):
+    if name in ("k_round_received", "k_median_wave"):
         return (4 * n + 48) * ordered
     return 48 * ordered
 
@@ -306,7 +315,7 @@ def main():
         base = name.strip("()").split("<")[0]
         launches = sweeps * nprof if base in ("k_la_sweep", "k_la_sweep16") else cnt
         per_replay = launches / nprof
-        b = algorithmic_bytes(name, n, ev0, ord0) / max(per_replay, 1)
+        b = algorithmic_bytes(name, n, ev0, ord0, eng0.rounds()) / max(per_replay, 1)
         per_launch = ms / max(launches, 1)
         return b, per_launch, b / (per_launch * 1e-3) / 1e9, per_replay
 
@@ -319,7 +328,7 @@ def main():
         if base in ("k_la_sweep", "k_la_clear", "k_transpose", "k_fss", "k_fdt_runs",
                     "k_fdt_clear", "k_rounds_coop", "k_rounds_coop_spec", "k_median_wave",
                     "k_la_clear16", "k_la_sweep16", "k_transpose16", "k_rounds_direct",
-                    "k_median_chain"):
+                    "k_fd_transpose_ts", "k_witness_la"):
             b, pl, gbs, lpr = kernel_roofline(name)
             hbm_kernels[name] = {"achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
                                  "alg_bytes_per_launch": int(b), "launch_ms": round(pl, 4),

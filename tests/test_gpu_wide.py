@@ -43,3 +43,65 @@ def test_wide_online_matches_replay():
     finally:
         a.close()
         b.close()
+
+
+def _np_coords(dag, n):
+    """lastAncestors rows (insertion order) and a firstDescendants lookup, numpy."""
+    cr = np.asarray(dag["creator"], np.int64)
+    ix = np.asarray(dag["index"], np.int64)
+    sp = np.asarray(dag["sp"], np.int64)
+    op = np.asarray(dag["op"], np.int64)
+    E = len(cr)
+    LA = np.full((E, n), -1, np.int32)
+    for x in range(E):
+        row = LA[sp[x]].copy() if sp[x] >= 0 else np.full(n, -1, np.int32)
+        if op[x] >= 0:
+            np.maximum(row, LA[op[x]], out=row)
+        row[cr[x]] = ix[x]
+        LA[x] = row
+    chains = [np.flatnonzero(cr == j) for j in range(n)]  # positions in insertion order
+
+    def fd(x):
+        c, i = cr[x], ix[x]
+        out = np.full(n, np.iinfo(np.int32).max, np.int64)
+        for j in range(n):
+            col = LA[chains[j], c]  # non-decreasing along chain j
+            k = int(np.searchsorted(col, i, "left"))
+            if k < len(col):
+                out[j] = k
+        return out
+    return LA, fd
+
+
+def test_wide256_fd_rows_online_and_growth():
+    """N=256 (FD rows built straight from LAT, k_fd_rows): the online path with a
+    small starting capacity (the chain tables grow, LAT keeps its old positions)
+    equals the bulk replay, and sampled coordinates equal a numpy restatement of
+    InitEventCoordinates / UpdateAncestorFirstDescendant (hashgraph.go:399-494)."""
+    from babble_amd.engine import Engine, events_array
+    from babble_amd.gossip import schedule
+    n, E, k = 256, 12_000, 256
+    dag = random_gossip(n, E, seed=77)
+    calls = schedule(E, k)
+    a = Engine(n, E + 64)
+    b = Engine(n, 1024)
+    try:
+        _, order, _ = a.replay(dag, calls)
+        ev = events_array(dag)
+        nxt = 0
+        for c in calls:
+            b.insert_events(ev[nxt:c].copy())
+            b.run_consensus()
+            nxt = c
+        np.testing.assert_array_equal(b.consensus_events(), order)
+        assert b.rounds() == a.rounds()
+        LA, fd = _np_coords(dag, n)
+        rng = np.random.default_rng(3)
+        for x in rng.choice(E, 40, replace=False).tolist() + [0, E - 1]:
+            for eng in (a, b):
+                gla, gfd = eng.coordinates(int(x))
+                np.testing.assert_array_equal(gla, LA[x])
+                np.testing.assert_array_equal(np.asarray(gfd, np.int64), fd(x))
+    finally:
+        a.close()
+        b.close()
