@@ -381,27 +381,28 @@ __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const int32_t
   }
 }
 
-// FDT[j][c][q] = INF32 for the new positions q in [olen_c, len_c)
-__global__ void k_fdt_clear(Tables t, int32_t* FDT, const int32_t* olen, const int32_t* len) {
-  const int c = blockIdx.y, j = blockIdx.z;
-  const int lo = olen[c], hi = len[c];
-  int32_t* row = FDT + ((size_t)j * t.N + c) * t.ccap;
-  for (int q = lo + blockIdx.x * blockDim.x + threadIdx.x; q < hi; q += gridDim.x * blockDim.x)
-    row[q] = INF32;
-}
-
 // runs: chain-j event k (new) is the first chain-j descendant of chain-c
-// positions (LAT[j][c][k-1], LAT[j][c][k]]
-__global__ void k_fdt_runs(Tables t, const int32_t* LAT, int32_t* FDT, const int32_t* olen,
-                           const int32_t* len) {
+// positions (LAT[j][c][k-1], LAT[j][c][k]].  The new chain-c positions past the
+// last chain-j event's ancestor have no chain-j descendant yet (INF32); every
+// other new position lies in a new event's run (an old event cannot have a new
+// ancestor), so no separate clear pass is needed.  FDR_K events per workgroup.
+constexpr int FDR_K = 1024;
+__global__ void __launch_bounds__(256) k_fdt_runs(Tables t, const int32_t* LAT, int32_t* FDT,
+                                                  const int32_t* olen, const int32_t* len) {
   const int c = blockIdx.y, j = blockIdx.z;
-  const int k = olen[j] + blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= len[j]) return;
   const size_t base = ((size_t)j * t.N + c) * t.ccap;
-  const int hi = LAT[base + k];
-  const int lo = k > 0 ? LAT[base + k - 1] : -1;
   int32_t* row = FDT + base;
-  for (int q = lo + 1; q <= hi; q++) row[q] = k;
+  const int oj = olen[j], lj = len[j], oc = olen[c], lc = len[c];
+  const int tail0 = max(oc, lj > 0 ? LAT[base + lj - 1] + 1 : 0);
+  for (int q = tail0 + blockIdx.x * blockDim.x + threadIdx.x; q < lc; q += gridDim.x * blockDim.x)
+    row[q] = INF32;
+  const int k0 = oj + blockIdx.x * FDR_K;
+  const int k1 = min(lj, k0 + FDR_K);
+  for (int k = k0 + threadIdx.x; k < k1; k += blockDim.x) {
+    const int hi = LAT[base + k];
+    const int lo = k > 0 ? LAT[base + k - 1] : -1;
+    for (int q = lo + 1; q <= hi; q++) row[q] = k;
+  }
 }
 
 // lowest chain-c position whose FD row a new event can change:

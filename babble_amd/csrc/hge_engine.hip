@@ -1185,9 +1185,8 @@ struct hge_engine {
     else
       KLAUNCH(k_transpose, dim3(div_up(maxnew + 1, 64), div_up(N, 64), N), dim3(256), 0, st, t,
               (const int32_t*)nullptr, d_LAT.p, k_plo, len, 0);
-    // FDT: clear the new positions, then the runs of the new events
-    KLAUNCH(k_fdt_clear, dim3(div_up(maxnew, 256), N, N), dim3(256), 0, st, t, d_FDT.p, olen, len);
-    KLAUNCH(k_fdt_runs, dim3(div_up(maxnew, 256), N, N), dim3(256), 0, st, t, d_LAT.p, d_FDT.p,
+    // FDT: the runs of the new events (and the new positions with no descendant yet)
+    KLAUNCH(k_fdt_runs, dim3(div_up(maxnew, FDR_K), N, N), dim3(256), 0, st, t, d_LAT.p, d_FDT.p,
             olen, len);
     // FDT -> FD rows for every chain-c position a new event can have touched
     // (from a fresh state: every row, qlo = 0 as uploaded; no round trip)
