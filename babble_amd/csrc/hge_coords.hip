@@ -122,8 +122,8 @@ __global__ void __launch_bounds__(256) k_la_sweep(Tables t, const int2* segs, in
 // Packed 16-bit sweeps (N > 32, where chains are capped at 65,534 events):
 // the fixed-point sweeps run on LA16, a table of (LA + 1) as uint16 pairs
 // (NW2 = ceil(N / 2) words per row, -1 -> 0), so every sweep streams half the
-// bytes of the int32 sweep; k_transpose16 then writes the int32 LA rows and the
-// LAT tiles from it in one pass.  Same segments, order and fixed-point argument
+// bytes of the int32 sweep; k_la16_rows_runs then writes the int32 LA rows and
+// the FDT runs from it in one pass.  Same segments, order and fixed-point argument
 // as k_la_sweep: max over packed halves is max over each column.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ size_t rowoff16(const Tables& t, int c, int p) {
@@ -252,42 +252,77 @@ __global__ void __launch_bounds__(256) k_la_sweep16(Tables t, const int2* segs, 
   }
 }
 
-// LA16 -> LA (int32 rows) and LAT (transposed), for positions [plo_j, len_j)
-// of every chain: one pass over the packed table (k_transpose mode 0's tiles)
-__global__ void __launch_bounds__(256) k_transpose16(Tables t, int32_t* LAT, const int32_t* plo,
-                                                     const int32_t* len) {
-  __shared__ int32_t tile[64][65];
+// N > 32: LA16 -> the int32 LA rows and, from the same tile, the FDT runs
+// (a transpose to LAT + k_fdt_runs without the LAT table in between): chain-j event k
+// (new) is the first chain-j descendant of chain-c positions
+// (LA[(j, k-1)][c], LA[(j, k)][c]], written as FDT[j][c][q] = k; the new chain-c
+// positions past LA[(j, len_j - 1)][c] get INF32 (no chain-j descendant yet);
+// every other new position lies in a new event's run.  Tile: positions
+// [p0, p0 + 64) of chain j (from plo_j = olen_j - 1: the row before the first
+// new event is the first run's lower bound) x columns [c0, c0 + 64).
+__global__ void __launch_bounds__(256) k_la16_rows_runs(Tables t, int32_t* FDT, const int32_t* plo,
+                                                        const int32_t* olen, const int32_t* len) {
+  __shared__ int32_t tile[65][65];  // row 0: position p0 - 1; row 1 + r: position p0 + r
   const int N = t.N;
   const size_t ccap = t.ccap;
-  const int a = blockIdx.z;  // chain j
-  const int p0 = plo[a] + blockIdx.x * 64;
-  const int pend = len[a];
-  if (p0 >= pend) return;
+  const int j = blockIdx.z;
+  const int lj = len[j], oj = olen[j];
+  const int p0 = plo[j] + blockIdx.x * 64;
   const int c0 = blockIdx.y * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
-  // rows (a, p): 32 packed words = 64 columns [c0, c0 + 64); lanes 0..31 take one word
-  // of row r, lanes 32..63 the same word of row r + 1
-  for (int r = 2 * ty; r < 64; r += 8) {
+  if (lj == 0) {  // empty chain: every new position of every chain c has no chain-j descendant
+    if (blockIdx.x == 0)
+      for (int cc = ty; cc < 64; cc += 4) {
+        const int c = c0 + cc;
+        if (c >= N) continue;
+        int32_t* row = FDT + ((size_t)j * N + c) * ccap;
+        for (int q = olen[c] + tx; q < len[c]; q += 64) row[q] = INF32;
+      }
+    return;
+  }
+  if (p0 >= lj) return;
+  // rows p0 - 1 .. p0 + 63: 32 packed words = 64 columns; lanes 0..31 take one word of
+  // row r, lanes 32..63 the same word of row r + 1
+  for (int r = 2 * ty; r < 66; r += 8) {
     const int rr = r + (tx >> 5), w = tx & 31;
-    const int p = p0 + rr, c = c0 + 2 * w;
-    if (p < pend && c < N) {
-      const uint32_t x = t.LA16[rowoff16(t, a, p) + (c >> 1)];
+    const int p = p0 - 1 + rr, c = c0 + 2 * w;
+    if (rr < 65 && p >= 0 && p < lj && c < N) {
+      const uint32_t x = t.LA16[rowoff16(t, j, p) + (c >> 1)];
       const int lo = (int)(x & 0xFFFFu) - 1, hi = (int)(x >> 16) - 1;
       tile[rr][2 * w] = lo;
       tile[rr][2 * w + 1] = hi;
-      int32_t* dst = t.LA + rowoff(t, a, p) + c;
-      if ((N & 1) == 0) {
-        *(int2*)dst = make_int2(lo, hi);  // 8-byte aligned: even row stride, even c
-      } else {
-        dst[0] = lo;
-        if (c + 1 < N) dst[1] = hi;
+      if (rr >= 1) {  // the int32 LA row (positions from plo on)
+        int32_t* dst = t.LA + rowoff(t, j, p) + c;
+        if ((N & 1) == 0) {
+          *(int2*)dst = make_int2(lo, hi);
+        } else {
+          dst[0] = lo;
+          if (c + 1 < N) dst[1] = hi;
+        }
       }
+    } else if (rr < 65) {
+      tile[rr][2 * w] = -1;
+      tile[rr][2 * w + 1] = -1;
     }
   }
   __syncthreads();
-  for (int r = ty; r < 64; r += 4) {
-    const int c = c0 + r, p = p0 + tx;
-    if (c < N && p < pend) LAT[((size_t)a * N + c) * ccap + p] = tile[tx][r];
+  // runs: wave ty takes columns ty, ty + 4, ...; lane = position k = p0 + tx
+  const int k = p0 + tx;
+  const bool isnew = k >= oj && k < lj;
+  const bool lasttile = lj - 1 < p0 + 64;
+  for (int cc = ty; cc < 64; cc += 4) {
+    const int c = c0 + cc;
+    if (c >= N) break;
+    int32_t* row = FDT + ((size_t)j * N + c) * ccap;
+    if (isnew) {
+      const int hi = tile[tx + 1][cc];
+      const int lo = k > 0 ? tile[tx][cc] : -1;
+      for (int q = lo + 1; q <= hi; q++) row[q] = k;
+    }
+    if (lasttile) {
+      const int tail0 = max(olen[c], tile[lj - p0][cc] + 1);
+      for (int q = tail0 + tx; q < len[c]; q += 64) row[q] = INF32;
+    }
   }
 }
 

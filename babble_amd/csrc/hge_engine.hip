@@ -463,7 +463,7 @@ struct hge_engine {
     // first-strong-seer rows (N <= 32): int32 rows of N, or uint16 rows padded to
     // 16/32 columns for the LDS walk; rebuilt from the frontier on, never kept
     if (N <= 32) d_FSS.need((size_t)N * nc * std::max(N, 16));
-    grow_chain_table(d_LAT, nc, false, false);      // rebuilt per batch from LA
+    if (!sweep16()) grow_chain_table(d_LAT, nc, false, false);  // rebuilt per batch from LA
     grow_chain_table(d_FDT, nc, true, false);       // persistent: FD in run layout
     ccap = (int)nc;
   }
@@ -1178,16 +1178,18 @@ struct hge_engine {
         break;
       }
     }
-    // LA -> LAT for positions [olen-1, len) (LA16 -> LA and LAT in one pass)
-    if (p16)
-      KLAUNCH(k_transpose16, dim3(div_up(maxnew + 1, 64), div_up(N, 64), N), dim3(256), 0, st, t,
-              d_LAT.p, k_plo, len);
-    else
+    if (p16) {
+      // LA16 -> the int32 LA rows and the FDT runs from the same tiles (no LAT)
+      KLAUNCH(k_la16_rows_runs, dim3(div_up(maxnew + 1, 64), div_up(N, 64), N), dim3(256), 0, st, t,
+              d_FDT.p, k_plo, olen, len);
+    } else {
+      // LA -> LAT for positions [olen-1, len), then the runs of the new events (and
+      // the new positions with no descendant yet)
       KLAUNCH(k_transpose, dim3(div_up(maxnew + 1, 64), div_up(N, 64), N), dim3(256), 0, st, t,
               (const int32_t*)nullptr, d_LAT.p, k_plo, len, 0);
-    // FDT: the runs of the new events (and the new positions with no descendant yet)
-    KLAUNCH(k_fdt_runs, dim3(div_up(maxnew, FDR_K), N, N), dim3(256), 0, st, t, d_LAT.p, d_FDT.p,
-            olen, len);
+      KLAUNCH(k_fdt_runs, dim3(div_up(maxnew, FDR_K), N, N), dim3(256), 0, st, t, d_LAT.p, d_FDT.p,
+              olen, len);
+    }
     // FDT -> FD rows for every chain-c position a new event can have touched
     // (from a fresh state: every row, qlo = 0 as uploaded; no round trip)
     std::vector<int32_t> qlo(N, 0);

@@ -67,7 +67,7 @@ def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
       k_fd_transpose_ts 16N/event (N > 16: FDT read, FD and the 8-byte FD
                     timestamps written);
       k_witness_la   8N^2 per round (frontier rows read, transposed rows written);
-      k_transpose16 10N/event (LA16 read, LA rows and LAT written);
+      k_la16_rows_runs 10N/event (N > 32: LA16 read, LA rows and the FDT runs written);
       k_fdt_clear    4N/event; k_fdt_runs 8N/event (LAT read, FDT written);
       k_fss          8N/event (FD row read, fss row written, N <= 32);
       rounds        4N/event (the strongly-see round test reads each row once);
@@ -84,7 +84,7 @@ def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
                  "k_fdt_clear": 4 * n, "k_fdt_runs": 8 * n, "k_fss": 8 * n,
                  "k_rounds_walk": 4 * n, "k_rounds_coop": 4 * n, "k_rounds_coop_spec": 4 * n,
                  "k_walk_spec": 4 * n, "k_rounds_fss": 4 * n, "k_rounds_direct": 4 * n,
-                 "k_la_clear16": 2 * n, "k_la_sweep16": 6 * n, "k_transpose16": 10 * n}
+                 "k_la_clear16": 2 * n, "k_la_sweep16": 6 * n, "k_la16_rows_runs": 10 * n}
     if name in per_event:
         return per_event[name] * events
     if name in ("k_round_received", "k_median_wave"):
@@ -327,7 +327,7 @@ def main():
         base = name.strip("()").split("<")[0]
         if base in ("k_la_sweep", "k_la_clear", "k_transpose", "k_fss", "k_fdt_runs",
                     "k_fdt_clear", "k_rounds_coop", "k_rounds_coop_spec", "k_median_wave",
-                    "k_la_clear16", "k_la_sweep16", "k_transpose16", "k_rounds_direct",
+                    "k_la_clear16", "k_la_sweep16", "k_la16_rows_runs", "k_rounds_direct",
                     "k_fd_transpose_ts", "k_witness_la"):
             b, pl, gbs, lpr = kernel_roofline(name)
             hbm_kernels[name] = {"achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
