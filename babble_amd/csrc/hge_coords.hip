@@ -381,38 +381,43 @@ __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const int32_t
   __shared__ int64_t tts[64][65];
   const int N = t.N;
   const size_t ccap = t.ccap;
-  const int a = blockIdx.z;  // source chain c
-  const int p0 = plo[a] + blockIdx.x * 64;
+  // grid (chain, column tile, position tiles): consecutive workgroups take the same
+  // positions of different source chains, whose first descendants (and so the
+  // timestamps gathered) lie in the same stretch of each chain j -- L2 hits
+  // instead of one re-read per source chain.  Position tiles past gridDim.z loop.
+  const int a = blockIdx.x;  // source chain c
   const int pend = len[a];
-  if (p0 >= pend) return;
   const int c0 = blockIdx.y * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
-  // all 16 FDT loads of a thread in flight, then all 16 timestamp gathers
-  int kv[16];
+  for (int p0 = plo[a] + blockIdx.z * 64; p0 < pend; p0 += gridDim.z * 64) {
+    // all 16 FDT loads of a thread in flight, then all 16 timestamp gathers
+    int kv[16];
 #pragma unroll
-  for (int i = 0; i < 16; i++) {
-    const int jj = c0 + ty + 4 * i, q = p0 + tx;
-    kv[i] = (jj < N && q < pend) ? FDT[((size_t)jj * N + a) * ccap + q] : INF32;
-  }
-  int64_t tv[16];
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    const int jj = c0 + ty + 4 * i;
-    tv[i] = t.tsch[(size_t)(jj < N ? jj : 0) * ccap + (kv[i] != INF32 ? kv[i] : 0)];
-  }
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    tile[ty + 4 * i][tx] = kv[i];
-    tts[ty + 4 * i][tx] = kv[i] != INF32 ? tv[i] : 0;
-  }
-  __syncthreads();
-  for (int r = ty; r < 64; r += 4) {
-    const int q = p0 + r, jj = c0 + tx;
-    if (q < pend && jj < N) {
-      const size_t o = rowoff(t, a, q) + jj;
-      t.FD[o] = tile[tx][r];
-      t.FDTS[o] = tts[tx][r];
+    for (int i = 0; i < 16; i++) {
+      const int jj = c0 + ty + 4 * i, q = p0 + tx;
+      kv[i] = (jj < N && q < pend) ? FDT[((size_t)jj * N + a) * ccap + q] : INF32;
     }
+    int64_t tv[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int jj = c0 + ty + 4 * i;
+      tv[i] = t.tsch[(size_t)(jj < N ? jj : 0) * ccap + (kv[i] != INF32 ? kv[i] : 0)];
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      tile[ty + 4 * i][tx] = kv[i];
+      tts[ty + 4 * i][tx] = kv[i] != INF32 ? tv[i] : 0;
+    }
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4) {
+      const int q = p0 + r, jj = c0 + tx;
+      if (q < pend && jj < N) {
+        const size_t o = rowoff(t, a, q) + jj;
+        t.FD[o] = tile[tx][r];
+        t.FDTS[o] = tts[tx][r];
+      }
+    }
+    __syncthreads();
   }
 }
 

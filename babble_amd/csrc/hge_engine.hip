@@ -1200,7 +1200,7 @@ struct hge_engine {
     int span = 1;
     for (int c = 0; c < N; c++) span = std::max(span, chain_len[c] - qlo[c]);
     if (N > 16)
-      KLAUNCH(k_fd_transpose_ts, dim3(div_up(span, 64), div_up(N, 64), N), dim3(256), 0, st, t,
+      KLAUNCH(k_fd_transpose_ts, dim3(N, div_up(N, 64), std::min(div_up(span, 64), 65535)), dim3(256), 0, st, t,
               (const int32_t*)d_FDT.p, k_qlo, len);
     else
       KLAUNCH(k_transpose, dim3(div_up(span, 64), div_up(N, 64), N), dim3(256), 0, st, t, d_FDT.p,

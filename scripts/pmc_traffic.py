@@ -50,8 +50,9 @@ def main():
     fetch = run_pass(out_dir, "FETCH_SIZE", bench_args, parse_only)
     write = run_pass(out_dir, "WRITE_SIZE", bench_args, parse_only)
     res = {}
-    # every replay resets its rounds tables once (k_reset_rounds): the replay count
-    replays = max(1, fetch.get("k_reset_rounds", [0.0, 0])[1])
+    # every replay fills the chain table once (k_chain_fill): the replay count
+    # (k_reset_rounds also runs at prepare time)
+    replays = max(1, fetch.get("k_chain_fill", [0.0, 0])[1])
     for name in sorted(set(fetch) | set(write)):
         fb, fl = fetch.get(name, [0.0, 0])
         wb, wl = write.get(name, [0.0, 0])
