@@ -1523,8 +1523,12 @@ struct hge_engine {
     switch (NW) {
 #define FCASE(B)                                                                                 \
   case B:                                                                                        \
-    KLAUNCH(k_fame_decide<B>, dim3(div_up(items, 256)), dim3(256), 0, st, t, c_pr,               \
-            c_pr + nrounds, c_pr + 2 * nrounds, nrounds, npairs, c_nc, c_Rc, s_dec.p);           \
+    if (N == 64 * B)                                                                             \
+      KLAUNCH((k_fame_decide<B, true>), dim3(div_up(items, 256)), dim3(256), 0, st, t, c_pr,      \
+              c_pr + nrounds, c_pr + 2 * nrounds, nrounds, npairs, c_nc, c_Rc, s_dec.p);         \
+    else                                                                                         \
+      KLAUNCH((k_fame_decide<B, false>), dim3(div_up(items, 256)), dim3(256), 0, st, t, c_pr,     \
+              c_pr + nrounds, c_pr + 2 * nrounds, nrounds, npairs, c_nc, c_Rc, s_dec.p);         \
     if (G == 16)                                                                                 \
       KLAUNCH((k_fame_timeline_g<16, 1>), dim3(div_up((int64_t)nrounds * 16, 256)), dim3(256), 0, \
               st, t, c_pr, c_pr + nrounds, c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds, c_nc, \

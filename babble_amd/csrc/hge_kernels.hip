@@ -839,14 +839,19 @@ __global__ void k_witness_bits(Tables t, const int32_t* newwit, const int32_t* p
 // j+1), and the LAST decision over j is what SetFame leaves.  Output per
 // (pair, slot): 0 no decision in this call, 1 famous, 2 not famous.
 // ---------------------------------------------------------------------------
-template <int NWT>
+// WP (N % 64 == 0): a wave's 64 slots belong to one pair, so the pair index is
+// made wave-uniform and every witness-row load (W, ssb, seeb) becomes a scalar
+// load shared by the wave instead of 64 lanes loading the same address.
+template <int NWT, bool WP>
 __global__ void k_fame_decide(Tables t, const int32_t* pr_round, const int32_t* pr_off,
                               const int32_t* pr_cf, int nrounds, int npairs,
                               const int64_t* nc, const int32_t* Rc, uint8_t* dec) {
   const int item = blockIdx.x * blockDim.x + threadIdx.x;
   const int N = t.N, SM = t.SM;
   if (item >= npairs * N) return;
-  const int p = item / N, xd = item - (item / N) * N;
+  int p = item / N;
+  const int xd = item - p * N;
+  if constexpr (WP) p = __builtin_amdgcn_readfirstlane(p);
   int lo = 0, hi = nrounds - 1;  // last round with pr_off <= p
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
