@@ -1279,18 +1279,25 @@ __global__ void __launch_bounds__(256) k_seg_theta_wide(Tables t, const int32_t*
     for (int l = 0; l < cnt; l++) {
       const int sg = segoff[q] + l;
       const int i = seg_round[sg];
-      if (tid == 0) {
-        int nf = 0;
+      // the famous witnesses' rows, in ascending creator order: thread d places
+      // its own at its rank (a serial walk here was a chain of dependent loads)
+      {
+        uint64_t fw[NWT];
+        int nfw = 0;
+#pragma unroll
         for (int w = 0; w < NWT; w++) {
-          uint64_t m = seg_fws[(size_t)sg * NWT + w];
-          while (m) {
-            const int d = w * 64 + __builtin_ctzll(m);
-            m &= m - 1;
-            const int x = t.W[(size_t)i * N + d];
-            s_row[nf++] = d * t.ccap + t.index[x];
-          }
+          fw[w] = seg_fws[(size_t)sg * NWT + w];
+          nfw += __popcll(fw[w]);
         }
-        s_nf = nf;
+        const int d = tid;
+        if (d < N && ((fw[d >> 6] >> (d & 63)) & 1ull)) {
+          int rank = __popcll(fw[d >> 6] & ((1ull << (d & 63)) - 1));
+#pragma unroll
+          for (int w = 0; w < NWT; w++) rank += w < (d >> 6) ? __popcll(fw[w]) : 0;
+          const int x = t.W[(size_t)i * N + d];
+          s_row[rank] = d * t.ccap + t.index[x];
+        }
+        if (tid == 0) s_nf = nfw;
       }
       __syncthreads();
       const int nf = s_nf;
@@ -1447,6 +1454,51 @@ __device__ __forceinline__ int64_t wave_upper_median(const uint64_t (&v)[VPL], c
     mx = max(mx, (uint64_t)__shfl_xor((long long)mx, o));
   }
   int kk = n / 2;  // 0-based rank of the upper median
+  const bool narrow = __builtin_amdgcn_readfirstlane((int)(mx - mn < (1ull << 32))) != 0;
+  if (narrow && n > 0) {
+    // the values span < 2^32: radix-select the 32-bit offsets from the minimum
+    // with the live sets as wave masks (scalar registers), two vector
+    // instructions per value word and bit
+    uint32_t vr[VPL];
+    uint64_t lm[VPL];
+#pragma unroll
+    for (int k = 0; k < VPL; k++) {
+      vr[k] = (uint32_t)(v[k] - mn);
+      lm[k] = __ballot(in[k]);
+    }
+    const uint32_t span = __builtin_amdgcn_readfirstlane((uint32_t)(mx - mn));  // wave-uniform
+    uint32_t pre = 0;
+    int nlive = n;
+    for (int b = span ? 31 - __builtin_clz(span) : -1; b >= 0; b--) {
+      uint64_t bm[VPL];
+      int c0 = 0;
+#pragma unroll
+      for (int k = 0; k < VPL; k++) {
+        bm[k] = __ballot((vr[k] >> b) & 1u);
+        c0 += __popcll(lm[k] & ~bm[k]);
+      }
+      const bool one = kk >= c0;
+      if (one) {
+        kk -= c0;
+        pre |= 1u << b;
+        nlive -= c0;
+      } else {
+        nlive = c0;
+      }
+#pragma unroll
+      for (int k = 0; k < VPL; k++) lm[k] &= one ? bm[k] : ~bm[k];
+      if (nlive == 1) {
+        // one value left with this prefix: it is the answer (kk == 0), low bits and all
+#pragma unroll
+        for (int k = 0; k < VPL; k++)
+          if (lm[k]) {
+            const uint32_t w = (uint32_t)__shfl((int)vr[k], (int)__builtin_ctzll(lm[k]));
+            return (int64_t)((mn + w) ^ 0x8000000000000000ull);
+          }
+      }
+    }
+    return (int64_t)((mn + pre) ^ 0x8000000000000000ull);
+  }
   uint64_t prefix = mn;
   const uint64_t diff = mn ^ mx;
   if (diff) {
@@ -1523,28 +1575,54 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
                                                      const int32_t* recv_call, const int32_t* rr_in,
                                                      const int32_t* bseg, const uint64_t* seg_fws,
                                                      int64_t* cts_out) {
-  const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // MW_E events per wave (candidates q0 + e * nw, nw = the grid's wave count): all
+  // their loads are in flight together before the first select
+  constexpr int MW_E = 2;
+  const int nw = gridDim.x * 4;
+  const int q0 = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (q >= ncand) return;  // wave-uniform
   const int N = t.N, NW = t.NW;
-  const int x = cand ? cand[q] : q;
-  const int rc = recv_call[q], rr = rr_in[q], sg = bseg[q];
-  const int cx = t.creator[x], ix = t.index[x];
-  if (rc < 0) return;  // wave-uniform
-  const int32_t* thr = t.WLA + ((size_t)rr * N + cx) * N;
-  const int64_t* tsr = t.FDTS + ((size_t)cx * t.ccap + ix) * N;
-  uint64_t v[VPL];
-  bool in[VPL];
+  int qe[MW_E], ixe[MW_E];
+  bool live[MW_E];
+  uint64_t fw[MW_E][VPL];
+  int th[MW_E][VPL];
+  int64_t ts[MW_E][VPL];
 #pragma unroll
-  for (int k = 0; k < VPL; k++) {
-    const int d = lane + 64 * k;
-    const int dd = d < N ? d : 0;
-    const bool fam = d < N && ((seg_fws[(size_t)sg * NW + (dd >> 6)] >> (dd & 63)) & 1ull);
-    in[k] = fam && thr[dd] >= ix;
-    v[k] = in[k] ? ((uint64_t)tsr[dd] ^ 0x8000000000000000ull) : ~0ull;
+  for (int e = 0; e < MW_E; e++) {
+    const int q = q0 + e * nw;
+    const int qq = q < ncand ? q : ncand - 1;  // valid indices; the result is not stored
+    const int x = cand ? cand[qq] : qq;
+    const int rc = recv_call[qq], rr0 = rr_in[qq], sg0 = bseg[qq];
+    const int cx = t.creator[x], ix = t.index[x];
+    // an event not received (rc < 0) runs through with valid indices and is not
+    // stored: no branch between these loads and the row loads below
+    live[e] = q < ncand && rc >= 0;
+    const int rr = live[e] ? rr0 : 0, sg = live[e] ? sg0 : 0;
+    qe[e] = q;
+    ixe[e] = ix;
+    const int32_t* thr = t.WLA + ((size_t)rr * N + cx) * N;
+    const int64_t* tsr = t.FDTS + ((size_t)cx * t.ccap + ix) * N;
+#pragma unroll
+    for (int k = 0; k < VPL; k++) {
+      const int dd = min(lane + 64 * k, N - 1);
+      fw[e][k] = seg_fws[(size_t)sg * NW + (k < NW ? k : 0)];
+      th[e][k] = thr[dd];
+      ts[e][k] = tsr[dd];
+    }
   }
-  const int64_t med = wave_upper_median<VPL>(v, in);
-  if (lane == 0) cts_out[q] = med;
+#pragma unroll
+  for (int e = 0; e < MW_E; e++) {
+    uint64_t v[VPL];
+    bool in[VPL];
+#pragma unroll
+    for (int k = 0; k < VPL; k++) {
+      const int d = lane + 64 * k;
+      in[k] = d < N && ((fw[e][k] >> (d & 63)) & 1ull) && th[e][k] >= ixe[e];
+      v[k] = in[k] ? ((uint64_t)ts[e][k] ^ 0x8000000000000000ull) : ~0ull;
+    }
+    const int64_t med = wave_upper_median<VPL>(v, in);
+    if (lane == 0 && live[e]) cts_out[qe[e]] = med;
+  }
 }
 
 // ---------------------------------------------------------------------------
