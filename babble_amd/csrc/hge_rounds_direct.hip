@@ -57,8 +57,11 @@ struct DirLDS {
   uint32_t sLA[DIR_W * DirGeo<BS, NPOW>::RS] __attribute__((aligned(16)));
   int32_t sFD[DIR_W * NPOW] __attribute__((aligned(16)));  // the window's FD rows (int32, by LDS DMA)
   int sCnt[DIR_MAXP];
+  int sCntW[DIR_MAXP][BS / 64] __attribute__((aligned(16)));  // per-wave passing members of a probe
   uint32_t sBits[8];
   int s_stop, s_past;
+  int s_stamp;          // HGE_STAMPS: thread 0 accumulates probe phases into sdbg
+  uint64_t sdbg[2];     // [0] count (LDS reads + VALU), [1] reduce + barrier + read
 };
 
 __device__ __forceinline__ uint32_t dir_pack_la(int a, int b) {
@@ -296,12 +299,27 @@ __device__ __forceinline__ int dir_count(const DirLDS<BS, NPOW>& L, int p, int p
 template <int BS, int NPOW>
 __device__ __forceinline__ int dir_probe(const Tables& t, DirLDS<BS, NPOW>& L, int p, int part, int slot,
                                          const uint32_t (&mw)[DirGeo<BS, NPOW>::CW], bool& pass) {
+  const bool st = L.s_stamp && threadIdx.x == 0;
+  const uint64_t t0 = st ? stamp() : 0;
   const int cnt = dir_count<BS, NPOW>(L, p, part, mw);
   pass = cnt >= t.SM;
+  const uint64_t t1 = st ? stamp() : 0;
+  // each wave stores its own count (no same-address LDS atomics serialising the
+  // waves ahead of the barrier), then every thread sums the BS / 64 counts
   const uint64_t b = __ballot(part == 0 && pass);
-  if ((threadIdx.x & 63) == 0 && b) atomicAdd(&L.sCnt[slot], (int)__builtin_popcountll(b));
+  if ((threadIdx.x & 63) == 0) L.sCntW[slot][threadIdx.x >> 6] = (int)__builtin_popcountll(b);
   __syncthreads();
-  return L.sCnt[slot];
+  int r = 0;
+#pragma unroll
+  for (int w = 0; w < BS / 64; w += 4) {
+    const int4 q = *(const int4*)&L.sCntW[slot][w];
+    r += q.x + q.y + q.z + q.w;
+  }
+  if (st) {
+    L.sdbg[0] += t1 - t0;
+    L.sdbg[1] += stamp() - t1;
+  }
+  return r;
 }
 
 // C_{r+1}[c] before the end-of-chain clamp (INF32 = none yet) from the frontier
@@ -391,6 +409,10 @@ __global__ void __launch_bounds__(BS) k_rounds_direct(Tables t, const int32_t* o
       if (c == 0 && rlo == 0 && olen[tid] == 0 && len[tid] > 0) t.C[tid] = 0;
     }
     L.sP[tid] = P;
+  }
+  if (tid == 0) {
+    L.s_stamp = stamping ? 1 : 0;
+    L.sdbg[0] = L.sdbg[1] = 0;
   }
   __syncthreads();
   const int rcap = hist ? hmax : t.Rcap;
@@ -546,8 +568,11 @@ __global__ void __launch_bounds__(BS) k_rounds_direct(Tables t, const int32_t* o
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the prefetched FD rows have landed
     DSTAMP(5);
   }
-  if (stamping)
+  if (stamping) {
     for (int q = 0; q < 9; q++) dbg[q] += st_acc[q];
+    dbg[9] += L.sdbg[0];
+    dbg[10] += L.sdbg[1];
+  }
 #undef DSTAMP
 }
 
