@@ -1,0 +1,312 @@
+// hge_coords_win.hip — lastAncestors (InitEventCoordinates, hashgraph.go:399-463)
+// for 32 < N <= 256 by windowed exact propagation in insertion order.
+//
+// Column c of LA is a scalar propagation over the DAG in insertion
+// (topological) order:  LA[x][c] = max(LA[sp(x)][c], LA[op(x)][c], [creator(x)
+// == c] index(x)).  The only state it needs at any point of the order is the LA
+// row of every chain's current head (its last inserted event): N rows of N
+// uint16, 128 KB at N = 256 -- one workgroup's LDS.  So a workgroup walks a
+// window of consecutive insertion ids exactly, with no global dependence chain:
+//   * k_lw_plan cuts the ids into chunks of 64 and gives every event a level
+//     inside its chunk: above its self-parent, its other-parent when that is in
+//     the chunk, and every earlier event of the chunk that reads the head row
+//     this event replaces (so an other-parent head is still in LDS when read);
+//     the chunk's events are stored sorted by level;
+//   * a level is one read phase (self and other-parent head rows from LDS, all
+//     N columns of up to 1024 / (N/2) events at once, packed u16 max), a
+//     barrier, one write phase (the head row in LDS and the packed row to HBM:
+//     2N coalesced bytes per event), a barrier.
+// Windows run in parallel, each starting from the head rows at its first id as
+// they are stored at that moment (the windows before it are being computed
+// concurrently; in the first pass a new head row of another window is taken as
+// its own column only, so nothing unwritten is ever read).  Every stored value
+// is a lower bound of the exact one and every input only grows, so repeating
+// the pass converges to the exact table (the unique fixed point, as for the
+// sweeps of hge_coords.hip), and a pass that changes no row proves it.  A
+// window's rows stop depending on its starting rows after the information
+// horizon (the gossip spreading time, a few thousand ids), so a later pass
+// recomputes a window only until its running head rows equal the previous
+// pass's (compared through per-row sums: rows only grow, so equal sums mean
+// equal rows) and skips windows whose starting rows did not change.  Random
+// gossip converges in three passes, the last one a no-op, against ~20 Jacobi
+// sweeps of the whole table.
+//
+// An other-parent that was not its chain's head when the event was inserted
+// ("risky": possible in general DAGs, never in the synthetic gossip) is read
+// from HBM; a chunk holding one drains its stores before each barrier, and a
+// window with one after its convergence point is recomputed to its end.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hge {
+
+constexpr int LW_K = 64;          // ids per chunk (one wave plans a chunk)
+constexpr int LW_RISKY = 1;       // other-parent not the head of its chain at insertion
+constexpr int LW_INWIN = 2;       // other-parent inside the event's window
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+
+// wpos[w][c] = first chain-c position whose id is >= the window's first id
+// (the head before the window is wpos - 1); risky[w] = -1; zero[0, nzero) = 0
+__global__ void k_lw_pos(Tables t, int64_t n0, int WN, int G, const int32_t* len, int32_t* wpos,
+                         int32_t* risky, int32_t* zero, int nzero) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nzero) zero[i] = 0;
+  if (i < G) risky[i] = -1;
+  if (i >= G * t.N) return;
+  const int w = i / t.N, c = i - w * t.N;
+  const int64_t s0 = n0 + (int64_t)w * WN;
+  const int32_t* ch = t.chain + (size_t)c * t.ccap;
+  int lo = 0, hi = len[c];
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((int64_t)ch[mid] < s0) lo = mid + 1;
+    else hi = mid;
+  }
+  wpos[i] = lo;
+}
+
+// One wave per chunk of 64 ids.  plan[id - n0] for the chunk's ids, sorted by
+// level: {creator | level << 16 | flags << 24, index, opc, opp} (opc = -1: no
+// other-parent).  risky[w] = the last risky id of window w.
+__global__ void __launch_bounds__(256) k_lw_plan(Tables t, int64_t n0, int64_t n1, int WN,
+                                                 const int32_t* len, int4* plan, int32_t* risky) {
+  const int lane = threadIdx.x & 63;
+  const int64_t cs = n0 + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * LW_K;
+  if (cs >= n1) return;  // wave-uniform
+  const int64_t e = cs + lane;
+  const bool v = e < n1;
+  const int64_t wst = n0 + ((cs - n0) / WN) * WN;
+  int a = 0, k = 0, opc = -1, opp = -1, flags = 0;
+  int keysp = -2, keyop = -3;  // (chain << 16 | position) of the self- and other-parent
+  uint64_t pred = 0;           // lanes this event must follow
+  if (v) {
+    a = t.creator[e];
+    k = t.index[e];
+    if (k > 0) {
+      const int s = t.chain[(size_t)a * t.ccap + k - 1];
+      if (s >= cs) pred |= 1ull << (s - cs);
+      keysp = (a << 16) | (k - 1);
+    }
+    const int o = t.op[e];
+    if (o >= 0) {
+      opc = t.creator[o];
+      opp = t.index[o];
+      keyop = (opc << 16) | opp;
+      if (o >= cs) pred |= 1ull << (o - cs);
+      if (o >= wst) flags |= LW_INWIN;
+      if (opp + 1 < len[opc] && (int64_t)t.chain[(size_t)opc * t.ccap + opp + 1] < e) flags |= LW_RISKY;
+    }
+  }
+  // earlier readers of the head this event replaces (its self-parent as their other-parent)
+  for (int q = 0; q < 63; q++) {
+    const int kq = __builtin_amdgcn_readlane(keyop, q);
+    if (q < lane && kq == keysp) pred |= 1ull << q;
+  }
+  // levels in lane (= id) order: every predecessor has a lower lane
+  int lvl = 0;
+  for (int q = 0; q < 63; q++) {
+    const int lq = __builtin_amdgcn_readlane(lvl, q);
+    if ((pred >> q) & 1ull) lvl = max(lvl, lq + 1);
+  }
+  int maxl = v ? lvl : 0;
+  for (int off = 32; off >= 1; off >>= 1) maxl = max(maxl, __shfl_xor(maxl, off));
+  int rank = 0, base = 0;
+  const uint64_t lt = (1ull << lane) - 1;
+  for (int L = 0; L <= maxl; L++) {
+    const uint64_t m = __ballot(v && lvl == L);
+    if (v && lvl == L) rank = base + __builtin_popcountll(m & lt);
+    base += __builtin_popcountll(m);
+  }
+  if (v) plan[cs - n0 + rank] = make_int4(a | (lvl << 16) | (flags << 24), k, opc, opp);
+  const uint64_t rm = __ballot(v && (flags & LW_RISKY));
+  if (rm && lane == 63 - __builtin_clzll(rm)) atomicMax(&risky[(cs - n0) / WN], (int32_t)e);
+}
+
+// One pass over every window (one workgroup each).  pass 1 computes every new row;
+// pass > 1 recomputes a window from its current starting rows until its running
+// head rows equal the previous pass's.  rsum[plan slot] = sum of the row's 16-bit
+// values (LA + 1); initbuf[w] = the starting rows a pass used; prev / changed:
+// the previous pass's changed flag (0: converged, return at once) and this pass's.
+template <int NPOW>
+__global__ void __launch_bounds__(1024) k_la_win(Tables t, const int4* plan, int64_t n0, int64_t n1, int WN,
+                                                 const int32_t* wpos, const int32_t* olen, uint32_t* initbuf,
+                                                 const int32_t* risky, uint32_t* rsum, int pass,
+                                                 const int32_t* prev, int32_t* changed) {
+  constexpr int TPE = NPOW / 2;        // threads per event: one packed word each
+  constexpr int SL = 1024 / TPE;       // events per read/write phase
+  constexpr int MAXI = (LW_K + SL - 1) / SL;
+  constexpr int RW = TPE < 64 ? TPE : 64;  // lanes of one event inside a wave
+  __shared__ uint32_t s_st[NPOW * TPE];    // head rows [chain][word]
+  __shared__ int s_hp[NPOW], s_ol[NPOW];
+  __shared__ int4 s_ev[LW_K];
+  __shared__ uint32_t s_sum[LW_K];
+  __shared__ int s_lvoff[LW_K + 1];
+  __shared__ uint32_t s_dirty[NPOW / 32];
+  __shared__ int s_nlv, s_wait;
+  if (prev && *prev == 0) return;  // converged: the flag stays 0
+  const int N = t.N, W = t.NW2;
+  const int w = blockIdx.x;
+  const int64_t s0 = n0 + (int64_t)w * WN;
+  if (s0 >= n1) return;
+  const int64_t s1 = min(n1, s0 + (int64_t)WN);
+  const int tid = threadIdx.x;
+  const int slot = tid / TPE, wd = tid - (tid / TPE) * TPE;
+  if (tid < NPOW / 32) s_dirty[tid] = 0;
+  __syncthreads();
+  // starting rows: the heads before s0 as stored (pass 1: a new row of another
+  // window is not written yet, take its own column only)
+  uint32_t* ib = initbuf + (size_t)w * N * W;
+  for (int i = tid; i < NPOW * TPE; i += 1024) {
+    const int c = i / TPE, q = i - (i / TPE) * TPE;
+    uint32_t val = 0;
+    if (c < N && q < W) {
+      const int hp = wpos[(size_t)w * N + c] - 1;
+      if (hp >= 0) {
+        if (hp < olen[c] || pass > 1) val = t.LA16[((size_t)c * t.ccap + hp) * W + q];
+        else val = (q == (c >> 1)) ? (uint32_t)(hp + 1) << ((c & 1) * 16) : 0u;
+      }
+      if (pass > 1 && ib[(size_t)c * W + q] != val) atomicOr(&s_dirty[c >> 5], 1u << (c & 31));
+      ib[(size_t)c * W + q] = val;
+    }
+    s_st[i] = val;
+    if (q == 0) {
+      s_hp[c] = c < N ? wpos[(size_t)w * N + c] - 1 : -1;
+      s_ol[c] = c < N ? olen[c] : 0;
+    }
+  }
+  const int rl = risky[w];  // last risky id of the window (-1: none)
+  __syncthreads();
+  if (pass > 1) {
+    bool clean = rl < s0;
+    for (int q = 0; q < NPOW / 32; q++) clean &= s_dirty[q] == 0;
+    if (clean) return;  // same starting rows, nothing to revisit: the rows stand
+  }
+  // the chunk's plan entries (and, pass > 1, the previous pass's row sums) one chunk ahead
+  int4 nx = make_int4(-1, 0, -1, 0);
+  uint32_t nxs = 0, cur_s = 0;
+  if (tid < LW_K && s0 + tid < s1) {
+    nx = plan[s0 - n0 + tid];
+    if (pass > 1) nxs = rsum[s0 - n0 + tid];
+  }
+  bool anyc = false;
+  for (int64_t cs = s0; cs < s1; cs += LW_K) {
+    const int ne = (int)min((int64_t)LW_K, s1 - cs);
+    if (tid < LW_K) {
+      s_ev[tid] = nx;
+      s_sum[tid] = 0;
+      cur_s = nxs;
+      // level boundaries of the sorted entries (wave 0)
+      const int lv = tid < ne ? (nx.x >> 16) & 0xFF : 0x7FFF;
+      const int lp = __shfl(lv, tid > 0 ? tid - 1 : 0);
+      const bool start = tid < ne && (tid == 0 || lv != lp);
+      const uint64_t m = __ballot(start);
+      if (start) s_lvoff[__builtin_popcountll(m & ((1ull << tid) - 1))] = tid;
+      const bool rw = tid < ne && ((nx.x >> 24) & (LW_RISKY | LW_INWIN)) == (LW_RISKY | LW_INWIN);
+      const bool wt = __ballot(rw) != 0;
+      if (tid == 0) {
+        s_nlv = __builtin_popcountll(m);
+        s_lvoff[__builtin_popcountll(m)] = ne;
+        s_wait = wt ? 1 : 0;
+      }
+      const int64_t nc = cs + LW_K + tid;
+      nx = make_int4(-1, 0, -1, 0);
+      if (nc < s1) nx = plan[nc - n0];
+    }
+    __syncthreads();
+    if (pass > 1 && cs > s0) {
+      // the previous chunk left every head row as the previous pass had it and no
+      // risky event follows: the rest of the window is unchanged
+      bool clean = rl < cs;
+      for (int q = 0; q < NPOW / 32; q++) clean &= s_dirty[q] == 0;
+      if (clean) break;
+    }
+    const bool wt = s_wait != 0;
+    if (wt) {  // a risky read of this chunk may need rows stored by earlier chunks
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    const int nlv = s_nlv;
+    for (int L = 0; L < nlv; L++) {
+      const int lo = s_lvoff[L], hi = s_lvoff[L + 1];
+      uint32_t nv[MAXI];
+#pragma unroll
+      for (int i = 0; i < MAXI; i++) {
+        const int j = lo + slot + i * SL;
+        nv[i] = 0;
+        if (lo + i * SL < hi && j < hi && wd < W) {
+          const int4 en = s_ev[j];
+          const int a = en.x & 0xFFFF, k = en.y, opc = en.z, opp = en.w;
+          uint32_t v = s_st[a * TPE + wd];
+          if (opc >= 0) {
+            uint32_t o;
+            const size_t ro = ((size_t)opc * t.ccap + opp) * W + wd;
+            if (s_hp[opc] == opp) o = s_st[opc * TPE + wd];
+            else if (opp < s_ol[opc]) o = t.LA16[ro];  // an old, final row
+            else if ((en.x >> 24) & LW_INWIN)          // written by this workgroup this pass
+              o = __hip_atomic_load(t.LA16 + ro, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else if (pass == 1) o = (wd == (opc >> 1)) ? (uint32_t)(opp + 1) << ((opc & 1) * 16) : 0u;
+            else o = t.LA16[ro];  // another window's row: a lower bound
+            v = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2_t, v),
+                                                                         __builtin_bit_cast(u16x2_t, o)));
+          }
+          if (wd == (a >> 1)) {
+            const uint32_t own = (uint32_t)(k + 1) << ((a & 1) * 16);
+            v = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2_t, v),
+                                                                         __builtin_bit_cast(u16x2_t, own)));
+          }
+          nv[i] = v;
+        }
+      }
+      __syncthreads();  // every read of this level's head rows is done
+#pragma unroll
+      for (int i = 0; i < MAXI; i++) {
+        if (lo + i * SL >= hi) break;  // wave-uniform
+        const int j = lo + slot + i * SL;
+        uint32_t s = 0;
+        if (j < hi && wd < W) {
+          const int4 en = s_ev[j];
+          const int a = en.x & 0xFFFF, k = en.y;
+          s_st[a * TPE + wd] = nv[i];
+          t.LA16[((size_t)a * t.ccap + k) * W + wd] = nv[i];
+          if (wd == 0) s_hp[a] = k;
+          s = (nv[i] & 0xFFFFu) + (nv[i] >> 16);
+        }
+#pragma unroll
+        for (int off = RW / 2; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+        if ((tid & (RW - 1)) == 0 && j < hi && s) atomicAdd(&s_sum[j], s);
+      }
+      if (wt) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // rows a risky read may need
+      __syncthreads();
+    }
+    // chunk end (wave 0): row sums, changed rows, the head rows' dirty bits
+    if (tid < LW_K) {
+      const int4 en = s_ev[tid];
+      const bool v = tid < ne;
+      const int a = v ? (en.x & 0xFFFF) : -1, k = en.y;
+      const uint32_t sm = s_sum[tid];
+      bool chg = v;
+      if (pass > 1) {
+        chg = v && sm != cur_s;
+        bool last = v;  // the chain's last event in this chunk sets its dirty bit
+        for (int q = 0; q < LW_K; q++) {
+          const int aq = __builtin_amdgcn_readlane(a, q), kq = __builtin_amdgcn_readlane(k, q);
+          if (aq == a && kq > k) last = false;
+        }
+        if (last) {
+          if (chg) atomicOr(&s_dirty[a >> 5], 1u << (a & 31));
+          else atomicAnd(&s_dirty[a >> 5], ~(1u << (a & 31)));
+        }
+      }
+      if (chg) rsum[cs - n0 + tid] = sm;
+      anyc |= __ballot(chg) != 0;
+      // the next chunk's previous-pass sums (its plan entries have arrived)
+      if (pass > 1) {
+        const int64_t nc = cs + LW_K + tid;
+        nxs = nc < s1 ? rsum[nc - n0] : 0u;
+      }
+    }
+  }
+  if (tid == 0 && anyc) *changed = 1;
+}
+
+}  // namespace hge

@@ -23,6 +23,7 @@
 #include "../../include/hge.h"
 #include "hge_kernels.hip"
 #include "hge_coords.hip"
+#include "hge_coords_win.hip"
 #include "hge_rounds_coop.hip"
 #include "hge_rounds_direct.hip"
 #include "hge_walk_spec.hip"
@@ -156,6 +157,15 @@ struct hge_engine {
   // coordinate sweeps: transposed tables and scratch
   int n_sweeps = 0;
   DBuf<int32_t> d_LAT, d_FDT, s_chg, s_bar, s_dirty;
+  // windowed lastAncestors (hge_coords_win.hip): chunk plans, row sums, starting rows
+  DBuf<int4> s_lwplan;
+  DBuf<uint32_t> s_lwsum, s_lwinit;
+  DBuf<int32_t> s_lwpos, s_lwrisky;
+  int ncu_cache = 0;
+  int n_cu() {
+    if (!ncu_cache) HIPCHK(hipDeviceGetAttribute(&ncu_cache, hipDeviceAttributeMultiprocessorCount, device));
+    return ncu_cache;
+  }
   DBuf<int64_t> d_FDTS;  // N > 16: timestamps at the FD positions (the wide median)
   DBuf<int32_t> d_WLA;   // N > 16: round frontier rows transposed (k_witness_la)
   DBuf<uint64_t> d_ssc, s_gran;
@@ -329,8 +339,12 @@ struct hge_engine {
                              &s_recv,    &s_rr,     &s_bpos,  &s_fund,   &s_upos,    &s_vis,
                              &s_und2,    &s_part,   &s_fst,    &d_FSS,     &d_LAT,
                              &d_FDT,     &s_chg,    &s_bar,   &s_bseg,   &s_kctl,    &s_cctl,
-                             &s_out,     &s_hn,     &s_hres,  &s_dirty,  &d_WLA};
+                             &s_out,     &s_hn,     &s_hres,  &s_dirty,  &d_WLA,     &s_lwpos,
+                             &s_lwrisky};
     for (auto* b : i32s) b->free_();
+    s_lwplan.free_();
+    s_lwsum.free_();
+    s_lwinit.free_();
     d_ts.free_();
     d_FDTS.free_();
     d_cts.free_();
@@ -1112,6 +1126,64 @@ struct hge_engine {
     return N > 32 && !(e && atoi(e) == 0);
   }
 
+  // 32 < N <= 256: lastAncestors by windowed exact propagation (hge_coords_win.hip)
+  // instead of the sweeps; HGE_LA_WIN=0 keeps the sweeps
+  bool la_windows() const {
+    const char* e = getenv("HGE_LA_WIN");
+    return N > 32 && N <= 256 && !(e && atoi(e) == 0);
+  }
+
+  // passes over windows of the new ids until one changes no row (n_sweeps = passes
+  // run); one window is exact in its first pass (its starting rows are final)
+  void la_windows_run(Tables t) {
+    const int32_t* olen = k_len;
+    const int32_t* len = k_len + N;
+    const int64_t n0 = n_coords, n1 = n_events, ne = n1 - n0;
+    const int npow = N <= 64 ? 64 : N <= 128 ? 128 : 256;
+    static const int64_t WMIN = getenv("HGE_LW_MIN") ? std::max(64, atoi(getenv("HGE_LW_MIN"))) : 4096;
+    int64_t G = std::min<int64_t>((int64_t)n_cu() * (npow == 256 ? 1 : 2), std::max<int64_t>(1, ne / WMIN));
+    if (const char* g = getenv("HGE_LW_G")) G = std::max(1, atoi(g));
+    int64_t WN = (div_up(ne, G) + LW_K - 1) / LW_K * LW_K;
+    G = div_up(ne, WN);
+    const int W = t.NW2;
+    s_lwplan.need(ne);
+    s_lwsum.need(ne);
+    s_lwinit.need((size_t)G * N * W);
+    s_lwpos.need((size_t)G * N);
+    s_lwrisky.need(G);
+    const int MAXP = 64;
+    s_chg.need(MAXP);
+    KLAUNCH(k_lw_pos, dim3(div_up(std::max<int64_t>(G * N, MAXP), 256)), dim3(256), 0, st, t, n0, (int)WN, (int)G,
+            len, s_lwpos.p, s_lwrisky.p, s_chg.p, MAXP);
+    KLAUNCH(k_lw_plan, dim3(div_up(div_up(ne, LW_K), 4)), dim3(256), 0, st, t, n0, n1, (int)WN, len, s_lwplan.p,
+            s_lwrisky.p);
+    int p = 0;
+    for (int group = G == 1 ? 1 : 3;; group = 2) {
+      for (int g = 0; g < group; g++, p++) {
+        if (p >= MAXP) throw EngineError(HGE_ERR_INTERNAL, "lastAncestors windows did not converge");
+        const int32_t* prev = p > 0 ? s_chg.p + p - 1 : nullptr;
+        const int pass = p + 1;
+#define LWIN(NP)                                                                                           \
+  KLAUNCH(k_la_win<NP>, dim3(G), dim3(1024), 0, st, t, s_lwplan.p, n0, n1, (int)WN, s_lwpos.p, olen,       \
+          s_lwinit.p, s_lwrisky.p, s_lwsum.p, pass, prev, s_chg.p + p)
+        if (npow == 64) LWIN(64);
+        else if (npow == 128) LWIN(128);
+        else LWIN(256);
+#undef LWIN
+      }
+      if (G == 1) {
+        n_sweeps = 1;
+        break;
+      }
+      std::vector<int32_t> flags(p);
+      readback(flags.data(), s_chg.p, p);
+      if (!flags[p - 1]) {
+        n_sweeps = (int)(std::find(flags.begin(), flags.end(), 0) - flags.begin()) + 1;
+        break;
+      }
+    }
+  }
+
   // coordinates: chain-prefix sweeps + transposes (hge_coords.hip)
   void coords_sweep(Tables t, int nseg, int SEG, int maxnew, bool fresh) {
     const int32_t* olen = k_len;
@@ -1124,6 +1196,9 @@ struct hge_engine {
     const bool p16 = sweep16();
     // skip segments whose inputs did not change in the previous sweep (HGE_SWEEP_SKIP=0: off)
     static const bool SKIP = !(getenv("HGE_SWEEP_SKIP") && atoi(getenv("HGE_SWEEP_SKIP")) == 0);
+    if (p16 && la_windows()) {
+      la_windows_run(t);
+    } else {
     int32_t* dirty = nullptr;
     if (p16 && SKIP) {
       s_dirty.need(nseg);
@@ -1177,6 +1252,7 @@ struct hge_engine {
         n_sweeps = (int)(std::find(flags.begin(), flags.end(), 0) - flags.begin()) + 1;
         break;
       }
+    }
     }
     if (p16) {
       // LA16 -> the int32 LA rows and the FDT runs from the same tiles (no LAT)

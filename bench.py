@@ -68,6 +68,12 @@ def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
                     timestamps written);
       k_witness_la   8N^2 per round (frontier rows read, transposed rows written);
       k_la16_rows_runs 10N/event (N > 32: LA16 read, LA rows and the FDT runs written);
+      k_la_win      (2N + 20)/event (32 < N <= 256, windowed exact propagation: the
+                    head rows live in LDS, so per event only the packed row is
+                    written, the 16-byte plan entry read and the 4-byte row sum
+                    written -- once per replay, however many passes);
+      k_lw_plan     40/event (creator, index, other-parent and two chain gathers
+                    read, the plan entry written);
       k_fdt_clear    4N/event; k_fdt_runs 8N/event (LAT read, FDT written);
       k_fss          8N/event (FD row read, fss row written, N <= 32);
       rounds        4N/event (the strongly-see round test reads each row once);
@@ -84,7 +90,8 @@ def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
                  "k_fdt_clear": 4 * n, "k_fdt_runs": 8 * n, "k_fss": 8 * n,
                  "k_rounds_walk": 4 * n, "k_rounds_coop": 4 * n, "k_rounds_coop_spec": 4 * n,
                  "k_walk_spec": 4 * n, "k_rounds_fss": 4 * n, "k_rounds_direct": 4 * n,
-                 "k_la_clear16": 2 * n, "k_la_sweep16": 6 * n, "k_la16_rows_runs": 10 * n}
+                 "k_la_clear16": 2 * n, "k_la_sweep16": 6 * n, "k_la16_rows_runs": 10 * n,
+                 "k_la_win": 2 * n + 20, "k_lw_plan": 40, "k_lw_pos": 0}
     if name in per_event:
         return per_event[name] * events
     if name in ("k_round_received", "k_median_wave"):
