@@ -1101,11 +1101,15 @@ struct hge_engine {
       int hmax = 0, extra = 0;
       void* dargs[] = {&t, &olen, &len, &rstate, &rlo, &Rprev, &gran, &err, &ssc, &mb, &dbg,
                        &nostart, &nohist, &hmax, &nostart, &extra};
+      // HGE_DIRECT_BS=512: 512-thread workgroups (two per CU, 32-row windows) at N > 128
+      static const int DBS = getenv("HGE_DIRECT_BS") && atoi(getenv("HGE_DIRECT_BS")) == 512 ? 512 : 1024;
+      const int bs = N > 128 ? DBS : 1024;
       const void* fn = N <= 64 ? (const void*)k_rounds_direct<1024, 64>
                      : N <= 128 ? (const void*)k_rounds_direct<1024, 128>
-                                : (const void*)k_rounds_direct<1024, 256>;
+                     : bs == 512 ? (const void*)k_rounds_direct<512, 256>
+                                 : (const void*)k_rounds_direct<1024, 256>;
       prof_begin("k_rounds_direct");
-      HIPCHK(launch_resident(fn, dim3(N), dim3(1024), dargs));
+      HIPCHK(launch_resident(fn, dim3(N), dim3(bs), dargs));
       prof_end();
     } else {
       void* args[] = {&t, &FDT, &olen, &len, &rstate, &rlo, &Rprev, &gran, &err, &ssc, &dbg};

@@ -33,19 +33,28 @@
 
 namespace hge {
 
-constexpr int DIR_W = 64;   // candidate rows staged per window
-constexpr int DIR_MAXP = 16;  // probe counters per window (2 + log2(DIR_W) are used)
+// section stamps (HGE_STAMPS) are compiled in only with -DHGE_DIR_STAMPS: the
+// accumulators otherwise cost registers (and spills) in the round loop
+#ifdef HGE_DIR_STAMPS
+constexpr bool kDirStamps = true;
+#else
+constexpr bool kDirStamps = false;
+#endif
+constexpr int DIR_MAXP = 16;  // probe counters per window (2 + log2(W) are used)
 constexpr int DIR_CH = 32;    // rows per fetch chunk (a round advances ~EPR/N ~ 14 rows)
 
 template <int BS, int NPOW>
 struct DirGeo {
+  // candidate rows staged per window: 64 for 1024-thread workgroups (one per CU), 32 for
+  // 512-thread ones (two per CU, e.g. two walkers of one hashgraph side by side)
+  static constexpr int W = BS >= 1024 ? 64 : 32;
   static constexpr int TPM = BS / NPOW;       // threads per member
   static constexpr int CPT = NPOW / TPM;      // columns per thread (NPOW^2 / BS)
   static constexpr int CW = CPT / 2;          // packed words per thread
   static constexpr int VW = (CW % 4 == 0) ? 4 : 2;  // words per LDS read (b128 / b64)
   static constexpr int PS = CW + VW;          // LDS words per (row, part): parts on distinct banks
   static constexpr int RS = TPM * PS;         // LDS words per candidate row
-  static constexpr int WIN_INTS = DIR_W * NPOW;      // ints of a full window (N = NPOW)
+  static constexpr int WIN_INTS = W * NPOW;      // ints of a full window (N = NPOW)
   static constexpr int PREF = (DIR_CH * NPOW / 4 + BS - 1) / BS;  // int4 per thread and chunk
   static constexpr int MBW = NPOW / 2;        // staged member row: packed words
   static constexpr int MVW = (CW % 4 == 0) ? 4 : 2;  // MB words per thread chunk (16 / 8 bytes)
@@ -54,8 +63,8 @@ struct DirGeo {
 template <int BS, int NPOW>
 struct DirLDS {
   int sP[256];
-  uint32_t sLA[DIR_W * DirGeo<BS, NPOW>::RS] __attribute__((aligned(16)));
-  int32_t sFD[DIR_W * NPOW] __attribute__((aligned(16)));  // the window's FD rows (int32, by LDS DMA)
+  uint32_t sLA[DirGeo<BS, NPOW>::W * DirGeo<BS, NPOW>::RS] __attribute__((aligned(16)));
+  int32_t sFD[DirGeo<BS, NPOW>::W * NPOW] __attribute__((aligned(16)));  // the window's FD rows (int32, by LDS DMA)
   int sCnt[DIR_MAXP];
   int sCntW[DIR_MAXP][BS / 64] __attribute__((aligned(16)));  // per-wave passing members of a probe
   uint32_t sBits[8];
@@ -73,8 +82,8 @@ __device__ __forceinline__ uint32_t dir_pack_fd(int a, int b) {
   return lo | (hi << 16);
 }
 
-// The candidate rows live in an LDS ring of DIR_W rows: row p of chain c sits in
-// slot p % DIR_W, and the ring holds [lo, lo + DIR_W) for the current lo.  Moving
+// The candidate rows live in an LDS ring of W rows: row p of chain c sits in
+// slot p % W, and the ring holds [lo, lo + W) for the current lo.  Moving
 // the window from lo to lo' only fetches rows [max(lo + W, lo'), lo' + W): ~EPR/N
 // rows per round instead of W.
 // dir_fetch: rows [p0, p0 + min(nr, DIR_CH)) of chain c into registers (int4 slices of the
@@ -119,7 +128,7 @@ __device__ __forceinline__ void dir_store(const Tables& t, DirLDS<BS, NPOW>& L, 
     // never written: their member values are 0xFFFF, which no row value passes.
     const int col = 4 * q - row * N;
     const int part = col / G::CPT, w = (col - part * G::CPT) / 2;
-    const int slot = (p0 + row) & (DIR_W - 1);
+    const int slot = (p0 + row) & (DirGeo<BS, NPOW>::W - 1);
     uint2* dst = (uint2*)(L.sLA + slot * G::RS + part * G::PS + w);
     *dst = make_uint2(dir_pack_la(v[m].x, v[m].y), dir_pack_la(v[m].z, v[m].w));
   }
@@ -141,7 +150,7 @@ __device__ __forceinline__ void dir_fetch_fd(const Tables& t, DirLDS<BS, NPOW>& 
     const int p = p0 + r;
     if (4 * lane < N)
       __builtin_amdgcn_global_load_lds((const void*)(t.FD + rowoff(t, c, p) + 4 * lane),
-                                       (__attribute__((address_space(3))) void*)&L.sFD[(p & (DIR_W - 1)) * NPOW],
+                                       (__attribute__((address_space(3))) void*)&L.sFD[(p & (DirGeo<BS, NPOW>::W - 1)) * NPOW],
                                        16, 0, 0);
   }
 }
@@ -228,7 +237,7 @@ __device__ __forceinline__ void dir_stage_member(const Tables& t, const DirLDS<B
   if (4 * lane < NPOW) {
     int4 a = make_int4(INF32, INF32, INF32, INF32);
     if (p != INF32 && 4 * lane < N)
-      a = in_ring ? *(const int4*)&L.sFD[(p & (DIR_W - 1)) * NPOW + 4 * lane]
+      a = in_ring ? *(const int4*)&L.sFD[(p & (DirGeo<BS, NPOW>::W - 1)) * NPOW + 4 * lane]
                   : *(const int4*)(t.FD + rowoff(t, c, p) + 4 * lane);
     const unsigned long long x =
         (unsigned long long)dir_pack_fd(a.x, a.y) | ((unsigned long long)dir_pack_fd(a.z, a.w) << 32);
@@ -245,43 +254,43 @@ template <int BS, int NPOW>
 __device__ __forceinline__ int dir_count(const DirLDS<BS, NPOW>& L, int p, int part,
                                          const uint32_t (&mw)[DirGeo<BS, NPOW>::CW]) {
   using G = DirGeo<BS, NPOW>;
-  const uint32_t* src = L.sLA + (p & (DIR_W - 1)) * G::RS + part * G::PS;
-  uint32_t la[G::CW];
-  if constexpr (G::VW == 4) {
-#pragma unroll
-    for (int k = 0; k < G::CW; k += 4) {
-      const uint4 q = *(const uint4*)(src + k);
-      la[k] = q.x;
-      la[k + 1] = q.y;
-      la[k + 2] = q.z;
-      la[k + 3] = q.w;
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < G::CW; k += 2) {
-      const uint2 q = *(const uint2*)(src + k);
-      la[k] = q.x;
-      la[k + 1] = q.y;
-    }
-  }
+  const uint32_t* src = L.sLA + (p & (DirGeo<BS, NPOW>::W - 1)) * G::RS + part * G::PS;
   uint32_t acc0 = 0, acc1 = 0;
   const uint32_t ones = 0x00010001u;
   static_assert(G::CW % 2 == 0, "member slices are whole word pairs");
+  static_assert(G::CW % G::VW == 0, "LDS reads cover whole slices");
+  // one LDS read of VW words, then its word pairs: only VW row words are live at a
+  // time (a 512-thread workgroup holds 64 member words per thread)
 #pragma unroll
-  for (int k = 0; k < G::CW; k += 2) {
-    // (la + 2) -sat (m + 1) is nonzero <=> la >= m (v_pk_sub_u16 clamp saturates at 0);
-    // min(., 1) per half, then a packed add: 3 VALU ops per 2 columns.  Two words per
-    // asm statement and two accumulators (no dependent chain, and the compiler's
-    // hazard padding between asm statements falls on every other word pair at most)
-    uint32_t d0, d1;
-    asm("v_pk_sub_u16 %0, %4, %6 clamp\n\t"
-        "v_pk_sub_u16 %1, %5, %7 clamp\n\t"
-        "v_pk_min_u16 %0, %0, %8\n\t"
-        "v_pk_min_u16 %1, %1, %8\n\t"
-        "v_pk_add_u16 %2, %2, %0\n\t"
-        "v_pk_add_u16 %3, %3, %1"
-        : "=&v"(d0), "=&v"(d1), "+v"(acc0), "+v"(acc1)
-        : "v"(la[k]), "v"(la[k + 1]), "v"(mw[k]), "v"(mw[k + 1]), "v"(ones));
+  for (int k0 = 0; k0 < G::CW; k0 += G::VW) {
+    uint32_t la[G::VW];
+    if constexpr (G::VW == 4) {
+      const uint4 q = *(const uint4*)(src + k0);
+      la[0] = q.x;
+      la[1] = q.y;
+      la[2] = q.z;
+      la[3] = q.w;
+    } else {
+      const uint2 q = *(const uint2*)(src + k0);
+      la[0] = q.x;
+      la[1] = q.y;
+    }
+#pragma unroll
+    for (int k = 0; k < G::VW; k += 2) {
+      // (la + 2) -sat (m + 1) is nonzero <=> la >= m (v_pk_sub_u16 clamp saturates at 0);
+      // min(., 1) per half, then a packed add: 3 VALU ops per 2 columns.  Two words per
+      // asm statement and two accumulators (no dependent chain, and the compiler's
+      // hazard padding between asm statements falls on every other word pair at most)
+      uint32_t d0, d1;
+      asm("v_pk_sub_u16 %0, %4, %6 clamp\n\t"
+          "v_pk_sub_u16 %1, %5, %7 clamp\n\t"
+          "v_pk_min_u16 %0, %0, %8\n\t"
+          "v_pk_min_u16 %1, %1, %8\n\t"
+          "v_pk_add_u16 %2, %2, %0\n\t"
+          "v_pk_add_u16 %3, %3, %1"
+          : "=&v"(d0), "=&v"(d1), "+v"(acc0), "+v"(acc1)
+          : "v"(la[k]), "v"(la[k + 1]), "v"(mw[k0 + k]), "v"(mw[k0 + k + 1]), "v"(ones));
+    }
   }
   int cnt = (int)(acc0 & 0xFFFFu) + (int)(acc0 >> 16) + (int)(acc1 & 0xFFFFu) + (int)(acc1 >> 16);
   // sum over the member's TPM consecutive lanes by DPP (no LDS permutes): quad_perm
@@ -299,7 +308,7 @@ __device__ __forceinline__ int dir_count(const DirLDS<BS, NPOW>& L, int p, int p
 template <int BS, int NPOW>
 __device__ __forceinline__ int dir_probe(const Tables& t, DirLDS<BS, NPOW>& L, int p, int part, int slot,
                                          const uint32_t (&mw)[DirGeo<BS, NPOW>::CW], bool& pass) {
-  const bool st = L.s_stamp && threadIdx.x == 0;
+  const bool st = kDirStamps && L.s_stamp && threadIdx.x == 0;
   const uint64_t t0 = st ? stamp() : 0;
   const int cnt = dir_count<BS, NPOW>(L, p, part, mw);
   pass = cnt >= t.SM;
@@ -332,8 +341,8 @@ __device__ int dir_select(const Tables& t, int c, int lenc, DirLDS<BS, NPOW>& L,
   const int SM = t.SM;
   if (lo == INF32 || lo >= lenc) return INF32;
   for (;;) {
-    const int last = min(DIR_W, lenc - lo) - 1;  // >= 0
-    const int g = min(31, last);
+    const int last = min(DirGeo<BS, NPOW>::W, lenc - lo) - 1;  // >= 0
+    const int g = min(DirGeo<BS, NPOW>::W / 2 - 1, last);
     int a, b;
     bool ps;
     if (dir_probe<BS, NPOW>(t, L, lo + g, part, slot++, mw, ps) >= SM) {
@@ -345,11 +354,11 @@ __device__ int dir_select(const Tables& t, int c, int lenc, DirLDS<BS, NPOW>& L,
       b = last;
       pb = ps;
     } else {
-      if (lo + DIR_W >= lenc) return INF32;
+      if (lo + DirGeo<BS, NPOW>::W >= lenc) return INF32;
       // the answer lies past the window: the whole next window, fresh counters
-      lo += DIR_W;
+      lo += DirGeo<BS, NPOW>::W;
       __syncthreads();  // every thread has read this window's counters
-      dir_load<BS, NPOW>(t, L, c, lo, DIR_W, lenc, pv);
+      dir_load<BS, NPOW>(t, L, c, lo, DirGeo<BS, NPOW>::W, lenc, pv);
       if (threadIdx.x < DIR_MAXP) L.sCnt[threadIdx.x] = 0;
       slot = 0;
       __syncthreads();
@@ -369,7 +378,7 @@ __device__ int dir_select(const Tables& t, int c, int lenc, DirLDS<BS, NPOW>& L,
 }
 
 template <int BS, int NPOW>
-__global__ void __launch_bounds__(BS) k_rounds_direct(Tables t, const int32_t* olen, const int32_t* len,
+__global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t* olen, const int32_t* len,
                                                       int32_t* rstate, int rlo, int Rprev, uint64_t* gran,
                                                       int32_t* err, uint64_t* ssc, uint32_t* mbuf,
                                                       uint64_t* dbg, const int32_t* start, int32_t* hist,
@@ -384,7 +393,7 @@ __global__ void __launch_bounds__(BS) k_rounds_direct(Tables t, const int32_t* o
   // HGE_STAMPS diagnostics (workgroup 0, thread 0): cycles per section into dbg[0..8]
   // (6 = probes; 7, 8 = member-load issue and arrival inside section 0)
   uint64_t st_t = 0, st_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  const bool stamping = dbg && blockIdx.x == 0 && threadIdx.x == 0;
+  const bool stamping = kDirStamps && dbg && blockIdx.x == 0 && threadIdx.x == 0;
 #define DSTAMP(k)                             \
   if (stamping) {                             \
     const uint64_t now_ = stamp();            \
@@ -419,7 +428,7 @@ __global__ void __launch_bounds__(BS) k_rounds_direct(Tables t, const int32_t* o
   int extra_left = -1;  // history mode: rows still to walk after passing stopcut
   int4 pv[G::PREF];
   int lo = L.sP[c];
-  dir_load<BS, NPOW>(t, L, c, lo, DIR_W, lenc, pv);
+  dir_load<BS, NPOW>(t, L, c, lo, DirGeo<BS, NPOW>::W, lenc, pv);
   int f0 = INF32, fn = 0;  // rows fetched for the next round: [f0, f0 + fn)
   for (int r = rlo;; r++) {
     if (r + 1 >= rcap) {
@@ -465,7 +474,7 @@ __global__ void __launch_bounds__(BS) k_rounds_direct(Tables t, const int32_t* o
     // publish C_{r+1}[c]: wave 0 stages the next member row, drains its stores,
     // then lane 0 stores the granule
     if (tid < 64) {
-      dir_stage_member<BS, NPOW>(t, L, mbp[(r + 1) & 1], c, nxt, nxt >= lo && nxt - lo < DIR_W);
+      dir_stage_member<BS, NPOW>(t, L, mbp[(r + 1) & 1], c, nxt, nxt >= lo && nxt - lo < DirGeo<BS, NPOW>::W);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (tid == 0) {
         if (hist) hist[(size_t)(r + 1) * N + c] = nxt;
@@ -478,10 +487,10 @@ __global__ void __launch_bounds__(BS) k_rounds_direct(Tables t, const int32_t* o
     // strongly-see bits of C_{r+1}[c] against the members of round r
     if (nxt != INF32) {
       if (!have_bits) {  // a frontier row kept from an earlier batch: one more probe
-        if (nxt < lo || nxt >= lo + DIR_W) {
+        if (nxt < lo || nxt >= lo + DirGeo<BS, NPOW>::W) {
           __syncthreads();
           lo = nxt;
-          dir_load<BS, NPOW>(t, L, c, lo, DIR_W, lenc, pv);
+          dir_load<BS, NPOW>(t, L, c, lo, DirGeo<BS, NPOW>::W, lenc, pv);
           __syncthreads();
         }
         pb = dir_count<BS, NPOW>(L, nxt, part, mw) >= t.SM;
@@ -499,8 +508,8 @@ __global__ void __launch_bounds__(BS) k_rounds_direct(Tables t, const int32_t* o
       f0 = INF32;
       fn = 0;
     } else {
-      f0 = (lo != INF32 && nxt < lo + DIR_W) ? lo + DIR_W : nxt;
-      fn = nxt + DIR_W - f0;
+      f0 = (lo != INF32 && nxt < lo + DirGeo<BS, NPOW>::W) ? lo + DirGeo<BS, NPOW>::W : nxt;
+      fn = nxt + DirGeo<BS, NPOW>::W - f0;
     }
     lo = nxt;
     dir_fetch<BS, NPOW>(t, c, f0, fn, lenc, pv);
@@ -581,6 +590,9 @@ template __global__ void k_rounds_direct<1024, 64>(Tables, const int32_t*, const
                                                    const int32_t*, int32_t*, int, const int32_t*, int);
 template __global__ void k_rounds_direct<1024, 128>(Tables, const int32_t*, const int32_t*, int32_t*, int, int,
                                                     uint64_t*, int32_t*, uint64_t*, uint32_t*, uint64_t*,
+                                                   const int32_t*, int32_t*, int, const int32_t*, int);
+template __global__ void k_rounds_direct<512, 256>(Tables, const int32_t*, const int32_t*, int32_t*, int, int,
+                                                   uint64_t*, int32_t*, uint64_t*, uint32_t*, uint64_t*,
                                                    const int32_t*, int32_t*, int, const int32_t*, int);
 template __global__ void k_rounds_direct<1024, 256>(Tables, const int32_t*, const int32_t*, int32_t*, int, int,
                                                     uint64_t*, int32_t*, uint64_t*, uint32_t*, uint64_t*,

@@ -32,6 +32,7 @@ ERRORS = {
 HGE_ERR_CAPACITY = -7
 HGE_ERR_TOO_LATE = -11
 HGE_ERR_NOT_FOUND = -12
+HGE_ERR_SIGNATURE = -13
 
 
 class HgeEvent(ctypes.Structure):
@@ -72,6 +73,7 @@ EXPORTS = [
     "hge_diff", "hge_wire_info", "hge_read_wire_parents", "hge_parent_round", "hge_round_inc",
     "hge_round_diff", "hge_set_round", "hge_split_begin", "hge_frontier_guess",
     "hge_frontier_walk", "hge_split_finish", "hge_frontier_rows",
+    "hge_verify_events", "hge_sha256_batch", "hge_ingest",
 ]
 
 _lib = None
@@ -162,6 +164,11 @@ def lib():
     L.hge_frontier_walk.argtypes = [vp, P(i32), P(i32), i32, i32, P(i32), P(ctypes.c_uint64), P(i32), P(i32)]
     L.hge_split_finish.argtypes = [vp, P(i32), P(ctypes.c_uint64), i32, i32, P(i64)]
     L.hge_frontier_rows.argtypes = [vp, i32, i32, P(i32), P(ctypes.c_uint64)]
+    u8p = P(ctypes.c_uint8)
+    L.hge_verify_events.argtypes = [i64, u8p, P(i64), u8p, u8p, i32, u8p, P(i32)]
+    L.hge_sha256_batch.argtypes = [i64, u8p, P(i64), i32, u8p]
+    L.hge_ingest.argtypes = [vp, ctypes.c_void_p, i64, u8p, P(i64), u8p, u8p, i64, i32, P(i32), P(i64),
+                             P(ctypes.c_double)]
     L.hge_set_profiling.argtypes = [vp, ctypes.c_int]
     L.hge_reset_kernel_stats.argtypes = [vp]
     L.hge_kernel_stats.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
@@ -176,6 +183,48 @@ def _p32(a):
 
 def _p64(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+
+
+def _pu8(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+
+def _flat(bodies):
+    """(flat uint8 bytes, int64 offsets[n+1]) from a list of bytes or a (flat, off) pair."""
+    if isinstance(bodies, tuple):
+        flat, off = bodies
+        return np.ascontiguousarray(flat, np.uint8), np.ascontiguousarray(off, np.int64)
+    off = np.zeros(len(bodies) + 1, np.int64)
+    off[1:] = np.cumsum([len(b) for b in bodies])
+    flat = np.frombuffer(b"".join(bodies), np.uint8) if off[-1] else np.zeros(1, np.uint8)
+    return np.ascontiguousarray(flat), off
+
+
+def verify_events(bodies, pubs, sigs, threads=0):
+    """Event.Verify for a batch on host threads (hge_verify_events): returns
+    (ok bool[n], body hashes uint8[n, 32]).  bodies: list of bytes or (flat, off);
+    pubs uint8[n, 65]; sigs uint8[n, 64] (r || s)."""
+    flat, off = _flat(bodies)
+    n = len(off) - 1
+    pubs = np.ascontiguousarray(pubs, np.uint8).reshape(n, 65)
+    sigs = np.ascontiguousarray(sigs, np.uint8).reshape(n, 64)
+    ok = np.zeros(max(n, 1), np.int32)
+    hashes = np.zeros((max(n, 1), 32), np.uint8)
+    rc = lib().hge_verify_events(n, _pu8(flat), _p64(off), _pu8(pubs), _pu8(sigs), threads, _pu8(hashes), _p32(ok))
+    if rc != 0:
+        raise HgeError(rc, "hge_verify_events failed")
+    return ok[:n].astype(bool), hashes[:n]
+
+
+def sha256_batch(data, threads=0):
+    """SHA-256 of each byte string (hge_sha256_batch): uint8[n, 32]."""
+    flat, off = _flat(data)
+    n = len(off) - 1
+    out = np.zeros((max(n, 1), 32), np.uint8)
+    rc = lib().hge_sha256_batch(n, _pu8(flat), _p64(off), threads, _pu8(out))
+    if rc != 0:
+        raise HgeError(rc, "hge_sha256_batch failed")
+    return out[:n]
 
 
 def events_array(dag):
@@ -234,6 +283,26 @@ class Engine:
         if rc != 0:
             raise HgeError(rc, self.L.hge_last_error(self.h).decode(), accepted=status[:acc.value].copy())
         return status[:acc.value]
+
+    def ingest(self, ev, bodies, pubs, sigs, k, threads=0):
+        """hge_ingest: InsertEvent with signature checks in batches of k, RunConsensus
+        after each batch, the next batch verified on host threads meanwhile.
+        Returns (rc, status int32[n], n_accepted, times {verify_ms, device_ms, wall_ms});
+        rc is 0 or the negative status that ended the stream (HGE_ERR_SIGNATURE = -13)."""
+        ev = np.ascontiguousarray(ev, EVENT_DTYPE)
+        flat, off = _flat(bodies)
+        n = len(ev)
+        assert len(off) == n + 1
+        pubs = np.ascontiguousarray(pubs, np.uint8).reshape(n, 65)
+        sigs = np.ascontiguousarray(sigs, np.uint8).reshape(n, 64)
+        status = np.zeros(max(n, 1), np.int32)
+        acc = ctypes.c_int64()
+        tm = (ctypes.c_double * 3)()
+        rc = self.L.hge_ingest(self.h, ev.ctypes.data, n, _pu8(flat), _p64(off), _pu8(pubs), _pu8(sigs), int(k),
+                               threads, _p32(status), ctypes.byref(acc), tm)
+        if rc in (-8, -9, -10):  # argument, device or internal error (admission errors end the stream)
+            raise HgeError(rc, self.L.hge_last_error(self.h).decode())
+        return rc, status[:n], acc.value, {"verify_ms": tm[0], "device_ms": tm[1], "wall_ms": tm[2]}
 
     def insert(self, creator, index, sp, op, ts, S=b"\0" * 32, hash32=b"\1" * 32, ntx=0):
         ev = np.zeros(1, EVENT_DTYPE)

@@ -7,8 +7,9 @@
  * here; node/, net/ and proxy/ are untouched.  Plain pointers and sizes only.
  *
  * Events are identified by dense engine ids assigned in insertion order (the
- * shim keeps the hash <-> id map).  Hashing and ECDSA verification stay with
- * the caller (event.go:140-186).
+ * shim keeps the hash <-> id map).  The signature check and hashing of
+ * InsertEvent's front half run on host cores (hge_verify_events, hge_ingest
+ * below); the consensus entry points take verified hge_event records.
  *
  * Threading: one handle is used by one thread at a time (the reference
  * serialises Core under Node.coreLock, node/node.go:167-169).
@@ -49,7 +50,8 @@ enum hge_status {
   HGE_ERR_DEVICE = -9,     /* HIP runtime error */
   HGE_ERR_INTERNAL = -10,
   HGE_ERR_TOO_LATE = -11,  /* ErrTooLate  (store.go:22): below the rolling window  */
-  HGE_ERR_NOT_FOUND = -12  /* ErrKeyNotFound (store.go:21)                         */
+  HGE_ERR_NOT_FOUND = -12, /* ErrKeyNotFound (store.go:21)                         */
+  HGE_ERR_SIGNATURE = -13  /* "Invalid signature"  (hashgraph.go:330-336)            */
 };
 
 /* Parent reference values. */
@@ -89,6 +91,34 @@ int hge_reset(hge_engine* h); /* forget all events, keep allocations */
  * events before a rejection stay inserted: *n_accepted says how many. */
 int hge_insert_events(hge_engine* h, const hge_event* ev, int64_t n, int32_t* status_out,
                       int64_t* n_accepted);
+
+/* ---- host ingest pipeline (InsertEvent's front half) -------- */
+/* Event.Verify (event.go:140-150) for n events on `threads` host threads (<= 0:
+ * every core): body_hash_out[32 i] = SHA-256 of body i (EventBody.Hash, event.go:60-66:
+ * the bytes are the gob encoding EventBody.Marshal produces, event.go:44-52;
+ * bodies[body_off[i] .. body_off[i+1])), ok_out[i] = 1 iff sigs[64 i] = r || s
+ * (big-endian) is a valid ECDSA P-256 signature of that hash under pubs[65 i], the
+ * creator's uncompressed key (Body.Creator, crypto.ToECDSAPub crypto/utils.go:40-46;
+ * a key that is not a curve point verifies nothing).  body_hash_out may be NULL.
+ * Host code only: thread-safe, needs no engine, overlaps any device work. */
+int hge_verify_events(int64_t n, const uint8_t* bodies, const int64_t* body_off, const uint8_t* pubs,
+                      const uint8_t* sigs, int32_t threads, uint8_t* body_hash_out, int32_t* ok_out);
+/* SHA-256 of n byte strings data[off[i] .. off[i+1]) (Event.Hash over the gob(Event)
+ * bytes, event.go:169-179) into out[32 i], on `threads` host threads. */
+int hge_sha256_batch(int64_t n, const uint8_t* data, const int64_t* off, int32_t threads, uint8_t* out);
+/* InsertEvent with its signature check over a stream, in batches of k events with
+ * RunConsensus after each batch (node/core.go:179-202), while a pool of `threads`
+ * host threads verifies the next batch: the host crypto overlaps the device.  ev[i]
+ * is event i's record, (bodies, body_off, pubs, sigs) as for hge_verify_events.
+ * The first event whose signature fails is refused with HGE_ERR_SIGNATURE and ends
+ * the stream (the events before it stay inserted and their batch goes through
+ * consensus), like InsertEvent inside Core.Sync; admission errors end it the same
+ * way.  status_out[i] as for hge_insert_events; *n_accepted = events inserted;
+ * times_out (may be NULL): [0] host ms spent verifying that the device did not
+ * hide, [1] ms inside the insert + consensus calls, [2] wall ms. */
+int hge_ingest(hge_engine* h, const hge_event* ev, int64_t n, const uint8_t* bodies, const int64_t* body_off,
+               const uint8_t* pubs, const uint8_t* sigs, int64_t k, int32_t threads, int32_t* status_out,
+               int64_t* n_accepted, double* times_out);
 
 /* ---- consensus (node/core.go:179-202) --------------------------------------- */
 int hge_divide_rounds(hge_engine* h);          /* hashgraph.go:573-588 */
@@ -227,8 +257,9 @@ int hge_coordinates(hge_engine* h, int32_t id, int32_t* la_out, int32_t* fd_out)
  * engine's stream): 0 coords, 1 rounds, 2 witness bits, 3 fame, 4 received,
  * 5 order, 6 total.  Returns the number of stages written. */
 int hge_stage_times(hge_engine* h, float* ms_out, int cap);
-/* lastAncestors sweeps the last coordinate pass needed (hge_coords.hip): each
- * streams the new rows once; the last one confirms the fixed point. */
+/* lastAncestors passes the last coordinate step needed: window passes for
+ * 32 < N <= 256 (hge_coords_win.hip), Jacobi sweeps otherwise (hge_coords.hip);
+ * the last one confirms the fixed point (a single window needs one pass). */
 int32_t hge_coordinate_sweeps(hge_engine* h);
 /* Per-kernel timing: HIP events around every launch on the engine stream. */
 int hge_set_profiling(hge_engine* h, int on);

@@ -18,7 +18,7 @@ GOLD = os.path.join(ROOT, "tests", "golden")
 
 def header_symbols():
     src = open(os.path.join(ROOT, "include", "hge.h")).read()
-    return sorted(set(re.findall(r"\b(hge_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(hge_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_header_symbols_exported():
