@@ -1144,15 +1144,23 @@ struct hge_engine {
     const int32_t* len = k_len + N;
     const int64_t n0 = n_coords, n1 = n_events, ne = n1 - n0;
     const int npow = N <= 64 ? 64 : N <= 128 ? 128 : 256;
+    // k_la_win (default): one 1024-thread workgroup per window; HGE_LW_KERNEL=wave:
+    // k_la_wave, one wave per (window, 64-word slice), npow x 256 B of LDS each
+    static const bool BLOCK = !(getenv("HGE_LW_KERNEL") && strcmp(getenv("HGE_LW_KERNEL"), "wave") == 0);
+    const int W = t.NW2, S = (W + 63) / 64;
     static const int64_t WMIN = getenv("HGE_LW_MIN") ? std::max(64, atoi(getenv("HGE_LW_MIN"))) : 4096;
-    int64_t G = std::min<int64_t>((int64_t)n_cu() * (npow == 256 ? 1 : 2), std::max<int64_t>(1, ne / WMIN));
+    const int per_cu = BLOCK ? (npow == 256 ? 1 : 2) : std::max(1, std::min(8, (160 * 1024) / (npow * 256 + 512) / S));
+    int64_t G = std::min<int64_t>((int64_t)n_cu() * per_cu, std::max<int64_t>(1, ne / WMIN));
     if (const char* g = getenv("HGE_LW_G")) G = std::max(1, atoi(g));
     int64_t WN = (div_up(ne, G) + LW_K - 1) / LW_K * LW_K;
     G = div_up(ne, WN);
-    const int W = t.NW2;
+    const int nck = (int)(WN / LW_K);
+    if (!BLOCK) s_lwsum.need((size_t)G * S * (nck + 1));  // per (window, slice): chunk checksums
     s_lwplan.need(ne);
-    s_lwsum.need(ne);
-    s_lwinit.need((size_t)G * N * W);
+    if (BLOCK) {
+      s_lwsum.need(ne);
+      s_lwinit.need((size_t)G * N * W);
+    }
     s_lwpos.need((size_t)G * N);
     s_lwrisky.need(G);
     const int MAXP = 64;
@@ -1168,8 +1176,17 @@ struct hge_engine {
         const int32_t* prev = p > 0 ? s_chg.p + p - 1 : nullptr;
         const int pass = p + 1;
 #define LWIN(NP)                                                                                           \
-  KLAUNCH(k_la_win<NP>, dim3(G), dim3(1024), 0, st, t, s_lwplan.p, n0, n1, (int)WN, s_lwpos.p, olen,       \
-          s_lwinit.p, s_lwrisky.p, s_lwsum.p, pass, prev, s_chg.p + p)
+  do {                                                                                                     \
+    if (BLOCK)                                                                                             \
+      KLAUNCH(k_la_win<NP>, dim3(G), dim3(1024), 0, st, t, s_lwplan.p, n0, n1, (int)WN, s_lwpos.p, olen,   \
+              s_lwinit.p, s_lwrisky.p, s_lwsum.p, pass, prev, s_chg.p + p);                                \
+    else if (W % 64 == 0)                                                                                  \
+      KLAUNCH((k_la_wave<NP, true>), dim3(G * S), dim3(64), 0, st, t, s_lwplan.p, n0, n1, (int)WN,         \
+              s_lwpos.p, olen, s_lwsum.p, nck, s_lwrisky.p, pass, prev, s_chg.p + p);                      \
+    else                                                                                                   \
+      KLAUNCH((k_la_wave<NP, false>), dim3(G * S), dim3(64), 0, st, t, s_lwplan.p, n0, n1, (int)WN,        \
+              s_lwpos.p, olen, s_lwsum.p, nck, s_lwrisky.p, pass, prev, s_chg.p + p);                      \
+  } while (0)
         if (npow == 64) LWIN(64);
         else if (npow == 128) LWIN(128);
         else LWIN(256);

@@ -126,12 +126,13 @@ class Pool {
   }
 
  private:
-  static constexpr int64_t CHUNK = 64;
   void work(int w) {
+    // small pieces: a consensus-call batch is only K events (16-256); spread it over every worker
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(64, n_ / (4 * (int64_t)caches_.size())));
     for (;;) {
-      const int64_t i0 = next_.fetch_add(CHUNK);
+      const int64_t i0 = next_.fetch_add(chunk);
       if (i0 >= n_) break;
-      const int64_t i1 = std::min(n_, i0 + CHUNK);
+      const int64_t i1 = std::min(n_, i0 + chunk);
       for (int64_t i = i0; i < i1; i++) job_(w, i);
     }
   }

@@ -333,47 +333,59 @@ __device__ __forceinline__ int dir_probe(const Tables& t, DirLDS<BS, NPOW>& L, i
 
 // C_{r+1}[c] before the end-of-chain clamp (INF32 = none yet) from the frontier
 // in L.sP, the member slice mw and the window staged at lo (== L.sP[c]);
-// pb = this thread's member pass flag at the returned row
+// pb = this thread's member pass flag at the returned row.
+// A probe costs N^2 packed compares on this CU and a round lasts as long as its
+// slowest chain, so the search minimises the worst case, not the mean: the
+// advance per round is 13.8 +- 3.7 rows (max 33 over 568 x 256 at 256/2M,
+// scripts/analysis/dump_rounds.py), so the first half of the window [0, W/2) is
+// bisected on the assumption that its last row passes -- log2(W/2) probes -- and
+// that row is probed only if every probe failed.  (A search that starts at the
+// predicted advance takes fewer probes on average but more on the slowest chain
+// of a round: measured slower.)
 template <int BS, int NPOW>
 __device__ int dir_select(const Tables& t, int c, int lenc, DirLDS<BS, NPOW>& L, int part,
                           const uint32_t (&mw)[DirGeo<BS, NPOW>::CW], int& slot,
                           int4 (&pv)[DirGeo<BS, NPOW>::PREF], int& lo, bool& pb) {
+  constexpr int W = DirGeo<BS, NPOW>::W;
   const int SM = t.SM;
   if (lo == INF32 || lo >= lenc) return INF32;
   for (;;) {
-    const int last = min(DirGeo<BS, NPOW>::W, lenc - lo) - 1;  // >= 0
-    const int g = min(DirGeo<BS, NPOW>::W / 2 - 1, last);
-    int a, b;
+    const int last = min(W, lenc - lo) - 1;  // >= 0
     bool ps;
-    if (dir_probe<BS, NPOW>(t, L, lo + g, part, slot++, mw, ps) >= SM) {
-      a = 0;
-      b = g;
-      pb = ps;
-    } else if (g < last && dir_probe<BS, NPOW>(t, L, lo + last, part, slot++, mw, ps) >= SM) {
-      a = g + 1;
-      b = last;
-      pb = ps;
-    } else {
-      if (lo + DirGeo<BS, NPOW>::W >= lenc) return INF32;
-      // the answer lies past the window: the whole next window, fresh counters
-      lo += DirGeo<BS, NPOW>::W;
-      __syncthreads();  // every thread has read this window's counters
-      dir_load<BS, NPOW>(t, L, c, lo, DirGeo<BS, NPOW>::W, lenc, pv);
-      if (threadIdx.x < DIR_MAXP) L.sCnt[threadIdx.x] = 0;
-      slot = 0;
-      __syncthreads();
-      continue;
-    }
-    while (a < b) {  // row b passes; find the first passing row in [a, b]
-      const int mid = (a + b) >> 1;
-      if (dir_probe<BS, NPOW>(t, L, lo + mid, part, slot++, mw, ps) >= SM) {
-        b = mid;
-        pb = ps;
-      } else {
-        a = mid + 1;
+    int a = 0, b = min(W / 2 - 1, last);
+    bool known = false;  // row b has passed a probe
+    for (int pass2 = 0; pass2 < 2; pass2++) {
+      while (a < b) {  // the first passing row of [a, b], if row b passes
+        const int mid = (a + b) >> 1;
+        if (dir_probe<BS, NPOW>(t, L, lo + mid, part, slot++, mw, ps) >= SM) {
+          b = mid;
+          pb = ps;
+          known = true;
+        } else {
+          a = mid + 1;
+        }
       }
+      if (known) return lo + a;
+      if (dir_probe<BS, NPOW>(t, L, lo + a, part, slot++, mw, ps) >= SM) {
+        pb = ps;
+        return lo + a;
+      }
+      // every row of [0, b] fails: the second half [b + 1, last], its last row probed first
+      if (a >= last) break;
+      a = a + 1;
+      b = last;
+      if (dir_probe<BS, NPOW>(t, L, lo + b, part, slot++, mw, ps) < SM) break;
+      pb = ps;
+      known = true;
     }
-    return lo + a;
+    if (lo + W >= lenc) return INF32;
+    // the answer lies past the window: the whole next window, fresh counters
+    lo += W;
+    __syncthreads();  // every thread has read this window's counters
+    dir_load<BS, NPOW>(t, L, c, lo, W, lenc, pv);
+    if (threadIdx.x < DIR_MAXP) L.sCnt[threadIdx.x] = 0;
+    slot = 0;
+    __syncthreads();
   }
 }
 

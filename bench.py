@@ -91,7 +91,7 @@ def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
                  "k_rounds_walk": 4 * n, "k_rounds_coop": 4 * n, "k_rounds_coop_spec": 4 * n,
                  "k_walk_spec": 4 * n, "k_rounds_fss": 4 * n, "k_rounds_direct": 4 * n,
                  "k_la_clear16": 2 * n, "k_la_sweep16": 6 * n, "k_la16_rows_runs": 10 * n,
-                 "k_la_win": 2 * n + 20, "k_lw_plan": 40, "k_lw_pos": 0}
+                 "k_la_win": 2 * n + 20, "k_la_wave": 2 * n + 16, "k_lw_plan": 40, "k_lw_pos": 0}
     if name in per_event:
         return per_event[name] * events
     if name in ("k_round_received", "k_median_wave"):
