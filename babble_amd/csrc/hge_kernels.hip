@@ -1847,12 +1847,15 @@ __global__ void __launch_bounds__(1024) k_bucket_list(const int32_t* cnt, int n,
   }
 }
 
+// keys per bucket that k_bucket_sort_big sorts whole in LDS (k_bucket_sort leaves them to it)
+constexpr int BIG_SORT = 4096;
+
 __device__ void bucket_sort_one(int b, const int32_t* bend, const int32_t* bcnt, OKey* keys,
-                                OKey* tmp, int32_t* ids_out) {
+                                OKey* tmp, int32_t* ids_out, bool skip_big) {
   constexpr int CH = 512;  // keys per LDS chunk
   __shared__ SortChunk<CH> sc;
   const int n = bcnt[b];
-  if (n == 0) return;
+  if (n == 0 || (skip_big && n > CH && n <= BIG_SORT)) return;
   const int start = bend[b] - n;
   const int tid = threadIdx.x, T = blockDim.x;
   if (n == 1) {
@@ -1904,9 +1907,71 @@ __device__ void bucket_sort_one(int b, const int32_t* bend, const int32_t* bcnt,
 // one block per non-empty bucket (grid-stride over the list)
 __global__ void __launch_bounds__(256) k_bucket_sort(const int32_t* bend, const int32_t* bcnt,
                                                      const int32_t* list, const int32_t* nlist,
-                                                     OKey* keys, OKey* tmp, int32_t* ids_out) {
+                                                     OKey* keys, OKey* tmp, int32_t* ids_out, int skip_big) {
   for (int li = blockIdx.x; li < *nlist; li += gridDim.x) {
-    bucket_sort_one(list[li], bend, bcnt, keys, tmp, ids_out);
+    bucket_sort_one(list[li], bend, bcnt, keys, tmp, ids_out, skip_big != 0);
+    __syncthreads();
+  }
+}
+
+// Buckets of 513 .. BIG_SORT keys -- in a replay nearly every key sits in one: the
+// call that decides a round's fame receives that round's ~EPR events at once
+// (3,448 at N = 256).  One 1024-thread block sorts such a bucket whole in LDS: a
+// bitonic index sort over the leading 192 bits of the key (call|rr, cts, S[0..63]);
+// keys equal on those (S is uniform: ~never) are ordered by the full key from HBM.
+// k_bucket_sort's 512-key chunks + pairwise merges through global scratch moved
+// ~50x the keys' bytes for such buckets (25 GB per 256/10M replay, rocprofv3 PMC).
+__global__ void __launch_bounds__(1024) k_bucket_sort_big(const int32_t* bend, const int32_t* bcnt,
+                                                          const int32_t* list, const int32_t* nlist,
+                                                          const OKey* keys, int32_t* ids_out) {
+  __shared__ uint64_t sa[BIG_SORT], sb[BIG_SORT], ss[BIG_SORT];
+  __shared__ uint32_t sid[BIG_SORT];
+  __shared__ uint16_t ix[BIG_SORT];
+  const int tid = threadIdx.x, T = blockDim.x;
+  for (int li = blockIdx.x; li < *nlist; li += gridDim.x) {
+    const int b = list[li];
+    const int n = bcnt[b];
+    if (n <= 512 || n > BIG_SORT) continue;  // block-uniform
+    const OKey* K = keys + (bend[b] - n);
+    int P = 1024;
+    while (P < n) P <<= 1;
+    for (int i = tid; i < P; i += T) {
+      if (i < n) {
+        const OKey k = K[i];
+        sa[i] = k.a;
+        sb[i] = k.b;
+        ss[i] = k.s0;
+        sid[i] = k.id;
+      } else {
+        sa[i] = sb[i] = ss[i] = ~0ull;
+        sid[i] = 0xFFFFFFFFu;
+      }
+      ix[i] = (uint16_t)i;
+    }
+    __syncthreads();
+    for (int size = 2; size <= P; size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int i = tid; i < P / 2; i += T) {
+          const int lo = 2 * stride * (i / stride) + (i % stride);
+          const int hi = lo + stride;
+          const bool up = ((lo & size) == 0);
+          const int x = ix[lo], y = ix[hi];
+          bool yl;  // key y < key x
+          if (sa[x] != sa[y]) yl = sa[y] < sa[x];
+          else if (sb[x] != sb[y]) yl = sb[y] < sb[x];
+          else if (ss[x] != ss[y]) yl = ss[y] < ss[x];
+          else if (x >= n || y >= n) yl = y < x;  // padding (only padding ties padding)
+          else yl = okless(K[y], K[x]);          // equal leading 192 bits: the full key
+          if (yl == up) {
+            ix[lo] = (uint16_t)y;
+            ix[hi] = (uint16_t)x;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    int32_t* out = ids_out + (bend[b] - n);
+    for (int i = tid; i < n; i += T) out[i] = (int32_t)sid[ix[i]];
     __syncthreads();
   }
 }
