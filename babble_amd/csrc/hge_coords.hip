@@ -252,8 +252,8 @@ __global__ void __launch_bounds__(256) k_la_sweep16(Tables t, const int2* segs, 
   }
 }
 
-// N > 32: LA16 -> the int32 LA rows and, from the same tile, the FDT runs
-// (a transpose to LAT + k_fdt_runs without the LAT table in between): chain-j event k
+// N > 32: the FDT runs from LA16 tiles (a transpose to LAT + k_fdt_runs without the
+// LAT table in between; the int32 LA rows are never materialised): chain-j event k
 // (new) is the first chain-j descendant of chain-c positions
 // (LA[(j, k-1)][c], LA[(j, k)][c]], written as FDT[j][c][q] = k; the new chain-c
 // positions past LA[(j, len_j - 1)][c] get INF32 (no chain-j descendant yet);
@@ -291,15 +291,6 @@ __global__ void __launch_bounds__(256) k_la16_rows_runs(Tables t, int32_t* FDT, 
       const int lo = (int)(x & 0xFFFFu) - 1, hi = (int)(x >> 16) - 1;
       tile[rr][2 * w] = lo;
       tile[rr][2 * w + 1] = hi;
-      if (rr >= 1) {  // the int32 LA row (positions from plo on)
-        int32_t* dst = t.LA + rowoff(t, j, p) + c;
-        if ((N & 1) == 0) {
-          *(int2*)dst = make_int2(lo, hi);
-        } else {
-          dst[0] = lo;
-          if (c + 1 < N) dst[1] = hi;
-        }
-      }
     } else if (rr < 65) {
       tile[rr][2 * w] = -1;
       tile[rr][2 * w + 1] = -1;
@@ -454,7 +445,7 @@ __global__ void k_fd_qlo(Tables t, const int32_t* olen, const int32_t* len, int3
   for (int j = 0; j < t.N; j++) {
     if (len[j] == olen[j]) continue;  // chain j got no new event
     const int ol = olen[j];
-    const int v = ol > 0 ? t.LA[rowoff(t, j, ol - 1) + c] + 1 : 0;
+    const int v = ol > 0 ? la_at(t, j, ol - 1, c) + 1 : 0;
     m = min(m, v);
   }
   qlo[c] = max(0, m);

@@ -449,7 +449,7 @@ struct hge_engine {
     d_tsch.free_();
     d_tsch.p = tsch;
     d_tsch.n = (size_t)N * nc;
-    grow_chain_table(d_LA, nc, true);
+    if (!sweep16()) grow_chain_table(d_LA, nc, true);
     if (sweep16()) {
       const size_t w = (size_t)(N + 1) / 2;
       uint32_t* q = nullptr;
@@ -1123,12 +1123,9 @@ struct hge_engine {
     dbg_dump();
   }
 
-  // N > 32: the sweeps run on the packed 16-bit table (chains are capped at
-  // 65,534 events there); HGE_SWEEP16=0 keeps the int32 sweeps
-  bool sweep16() const {
-    const char* e = getenv("HGE_SWEEP16");
-    return N > 32 && !(e && atoi(e) == 0);
-  }
+  // N > 32: lastAncestors live only in the packed 16-bit table (chains are capped at
+  // 65,534 events there); the int32 LA rows exist for N <= 32
+  bool sweep16() const { return N > 32; }
 
   // 32 < N <= 256: lastAncestors by windowed exact propagation (hge_coords_win.hip)
   // instead of the sweeps; HGE_LA_WIN=0 keeps the sweeps
@@ -2202,7 +2199,16 @@ int hge_coordinates(hge_engine* h, int32_t id, int32_t* la_out, int32_t* fd_out)
   if (id < 0 || id >= h->n_events) return HGE_ERR_ARG;
   h->coords();
   const size_t off = ((size_t)h->h_creator[id] * h->ccap + h->h_index[id]) * h->N;
-  if (la_out) h->readback(la_out, h->d_LA.p + off, h->N);
+  if (la_out) {
+    if (h->sweep16()) {  // N > 32: unpack the LA16 row (LA + 1 as uint16 pairs)
+      const size_t w = (size_t)(h->N + 1) / 2;
+      std::vector<uint32_t> row(w);
+      h->readback(row.data(), h->d_LA16.p + ((size_t)h->h_creator[id] * h->ccap + h->h_index[id]) * w, w);
+      for (int c = 0; c < h->N; c++) la_out[c] = (int32_t)((row[c >> 1] >> ((c & 1) * 16)) & 0xFFFFu) - 1;
+    } else {
+      h->readback(la_out, h->d_LA.p + off, h->N);
+    }
+  }
   if (fd_out) h->readback(fd_out, h->d_FD.p + off, h->N);
   return HGE_OK;
   GUARD_END(h)

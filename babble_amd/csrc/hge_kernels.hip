@@ -57,6 +57,20 @@ __device__ __forceinline__ size_t rowoff(const Tables& t, int c, int p) {
   return ((size_t)c * t.ccap + p) * (size_t)t.N;
 }
 
+// lastAncestors[row][col], row = chain * ccap + position.  N > 32 keeps only the
+// packed table (LA16 = LA + 1 as uint16 pairs; chains are capped at 65,534 events
+// there): the int32 rows are never materialised, every reader unpacks.
+__device__ __forceinline__ int la_row(const Tables& t, size_t row, int col) {
+  if (t.N > 32) {
+    const uint32_t w = t.LA16[row * (size_t)t.NW2 + (col >> 1)];
+    return (int)((w >> ((col & 1) << 4)) & 0xFFFFu) - 1;
+  }
+  return t.LA[row * (size_t)t.N + col];
+}
+__device__ __forceinline__ int la_at(const Tables& t, int c, int p, int col) {
+  return la_row(t, (size_t)c * t.ccap + p, col);
+}
+
 __global__ void k_fill_i32(int32_t* p, int64_t n, int32_t v) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = v;
@@ -809,14 +823,14 @@ __global__ void k_witness_bits(Tables t, const int32_t* newwit, const int32_t* p
     if (j > 0 && d < N) {
       const int w = t.W[(size_t)(j - 1) * N + d];
       if (w >= 0) {
-        const int32_t* la = t.LA + rowoff(t, cy, t.index[y]);
-        see = la[d] >= t.index[w];
+        const size_t lrow = (size_t)cy * t.ccap + t.index[y];
+        see = la_row(t, lrow, d) >= t.index[w];
         if (ssc) {
           ss = (ssc[((size_t)j * N + cy) * NW + wd] >> (d & 63)) & 1ull;
         } else {
           const int32_t* fd = t.FD + rowoff(t, d, t.index[w]);
           int c = 0;
-          for (int i = 0; i < N; i++) c += (la[i] >= fd[i]) ? 1 : 0;
+          for (int i = 0; i < N; i++) c += (la_row(t, lrow, i) >= fd[i]) ? 1 : 0;
           ss = c >= t.SM;
         }
       }
@@ -1238,7 +1252,7 @@ __global__ void __launch_bounds__(256) k_segments_1p(Tables t, int rr_lo, int nr
 #pragma unroll
         for (int dd = 0; dd < G; dd++) {
           const int rd = __shfl(row, gshift + dd);
-          v[dd] = (((fws[0] >> dd) & 1ull) && cx < N) ? t.LA[(size_t)rd * N + cx] : (int)0x80000000;
+          v[dd] = (((fws[0] >> dd) & 1ull) && cx < N) ? la_row(t, (size_t)rd, cx) : (int)0x80000000;
         }
         const int nf = __popcll(fws[0]);
         const int th = nf ? select_kth<G>(v, G - (nf / 2 + 1) + 1) : (int)0x80000000;
@@ -1303,12 +1317,19 @@ __global__ void __launch_bounds__(256) k_seg_theta_wide(Tables t, const int32_t*
       const int nf = s_nf;
       const int cx = tid;
       if (cx < N) {
-        for (int k = 0; k < nf; k++)
-          sv[k * 256 + cx] = (uint16_t)(t.LA[(size_t)s_row[k] * N + cx] + 1);
+        // the column's values span a few dozen positions (the famous witnesses of one
+        // round see chain cx up to about the same point): bisect [min, max], not [0, 65535]
+        int vmin = 65535, vmax = 0;
+        for (int k = 0; k < nf; k++) {
+          const int v = la_row(t, (size_t)s_row[k], cx) + 1;
+          sv[k * 256 + cx] = (uint16_t)v;
+          vmin = min(vmin, v);
+          vmax = max(vmax, v);
+        }
         int th = (int)0x80000000;
         if (nf > 0) {
           const int kk = nf / 2 + 1;  // k-th largest = largest v with count(>= v) >= kk
-          int lo = 0, hi = 65535;
+          int lo = vmin, hi = vmax;
           while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
             int c2 = 0;
@@ -1397,7 +1418,7 @@ __global__ void k_round_received(Tables t, const int32_t* cand, int ncand, const
   int osa[M];
 #pragma unroll
   for (int d = 0; d < M; d++) {
-    const bool seen = wid[d] >= 0 && t.LA[rowoff(t, d, wix[d]) + cx] >= ix;
+    const bool seen = wid[d] >= 0 && la_at(t, d, wix[d], cx) >= ix;
     osa[d] = seen ? t.chain[(size_t)d * t.ccap + fd[d]] : -1;
   }
   int64_t tv[M];
@@ -1551,7 +1572,7 @@ __global__ void __launch_bounds__(256) k_witness_la(Tables t, int rr_lo) {
     int v = -1;
     if (d < N && cx < N) {
       const int pw = t.C[(size_t)rr * N + d];
-      if (pw != INF32) v = t.LA[rowoff(t, d, pw) + cx];
+      if (pw != INF32) v = la_at(t, d, pw, cx);
     }
     tile[r][tx] = v;
   }

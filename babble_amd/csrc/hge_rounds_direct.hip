@@ -86,25 +86,26 @@ __device__ __forceinline__ uint32_t dir_pack_fd(int a, int b) {
 // slot p % W, and the ring holds [lo, lo + W) for the current lo.  Moving
 // the window from lo to lo' only fetches rows [max(lo + W, lo'), lo' + W): ~EPR/N
 // rows per round instead of W.
-// dir_fetch: rows [p0, p0 + min(nr, DIR_CH)) of chain c into registers (int4 slices of the
-// contiguous chain-major rows; rows >= lenc read as -2 = "no row").  N % 4 == 0
+// dir_fetch: rows [p0, p0 + min(nr, DIR_CH)) of chain c into registers (8-byte slices of
+// the contiguous chain-major packed rows; rows >= lenc become "no row").  N % 4 == 0
 // (the host takes the gather path of hge_rounds_coop.hip otherwise).
 template <int BS, int NPOW>
 __device__ __forceinline__ void dir_fetch(const Tables& t, int c, int p0, int nr, int lenc,
-                                          int4 (&v)[DirGeo<BS, NPOW>::PREF]) {
+                                          uint2 (&v)[DirGeo<BS, NPOW>::PREF]) {
   using G = DirGeo<BS, NPOW>;
   const int N = t.N;
   nr = min(nr, DIR_CH);
   const int have = (p0 == INF32 || nr <= 0) ? 0 : max(0, min(nr, lenc - p0));
   if (have == 0) return;  // block-uniform
-  const int32_t* base = t.LA + ((size_t)c * t.ccap + p0) * (size_t)N;
+  // the packed rows (LA + 1 as uint16 pairs, N / 2 words per row): 4 columns = 8 bytes
+  const uint32_t* base = t.LA16 + ((size_t)c * t.ccap + p0) * (size_t)t.NW2;
   // unconditional loads (rows past `have` re-read the last fetched row; dir_store
   // drops them): no value select behind each load, so all of them stay in flight
   const int qmax = have * N / 4 - 1;
 #pragma unroll
   for (int m = 0; m < G::PREF; m++) {
-    const int q = min((int)threadIdx.x + m * BS, qmax);  // int4 index in the fetched rows
-    v[m] = *(const int4*)(base + 4 * (size_t)q);
+    const int q = min((int)threadIdx.x + m * BS, qmax);  // 4-column group in the fetched rows
+    v[m] = *(const uint2*)(base + 2 * (size_t)q);
   }
 }
 
@@ -112,7 +113,7 @@ __device__ __forceinline__ void dir_fetch(const Tables& t, int c, int p0, int nr
 // probe); rows at or past lenc are stored as "no row" (0: never >= a member value)
 template <int BS, int NPOW>
 __device__ __forceinline__ void dir_store(const Tables& t, DirLDS<BS, NPOW>& L, int p0, int nr, int lenc,
-                                          int4 (&v)[DirGeo<BS, NPOW>::PREF]) {
+                                          uint2 (&v)[DirGeo<BS, NPOW>::PREF]) {
   using G = DirGeo<BS, NPOW>;
   const int N = t.N;
   if (p0 == INF32 || nr <= 0) return;
@@ -123,14 +124,16 @@ __device__ __forceinline__ void dir_store(const Tables& t, DirLDS<BS, NPOW>& L, 
     const int q = threadIdx.x + m * BS;
     const int row = (4 * q) / N;
     if (row >= nr) continue;
-    if (row >= have) v[m] = make_int4(-2, -2, -2, -2);
+    // LA16 + 1 per half = the LA + 2 encoding (LA <= 65,533: no carry); a row past the
+    // chain's end is "no row" (0)
+    const bool hv = row < have;
     // the 4 columns lie in one part (CPT is a multiple of 4).  Columns past N are
     // never written: their member values are 0xFFFF, which no row value passes.
     const int col = 4 * q - row * N;
     const int part = col / G::CPT, w = (col - part * G::CPT) / 2;
     const int slot = (p0 + row) & (DirGeo<BS, NPOW>::W - 1);
     uint2* dst = (uint2*)(L.sLA + slot * G::RS + part * G::PS + w);
-    *dst = make_uint2(dir_pack_la(v[m].x, v[m].y), dir_pack_la(v[m].z, v[m].w));
+    *dst = hv ? make_uint2(v[m].x + 0x00010001u, v[m].y + 0x00010001u) : make_uint2(0u, 0u);
   }
 }
 
@@ -158,7 +161,7 @@ __device__ __forceinline__ void dir_fetch_fd(const Tables& t, DirLDS<BS, NPOW>& 
 // rows [p0, p0 + nr) into their ring slots, chunk by chunk (caller syncs before a probe)
 template <int BS, int NPOW>
 __device__ __forceinline__ void dir_load(const Tables& t, DirLDS<BS, NPOW>& L, int c, int p0, int nr, int lenc,
-                                         int4 (&v)[DirGeo<BS, NPOW>::PREF]) {
+                                         uint2 (&v)[DirGeo<BS, NPOW>::PREF]) {
   if (p0 == INF32) return;
   dir_fetch_fd<BS, NPOW>(t, L, c, p0, nr, lenc);
   for (int q = 0; q < nr; q += DIR_CH) {
@@ -345,7 +348,7 @@ __device__ __forceinline__ int dir_probe(const Tables& t, DirLDS<BS, NPOW>& L, i
 template <int BS, int NPOW>
 __device__ int dir_select(const Tables& t, int c, int lenc, DirLDS<BS, NPOW>& L, int part,
                           const uint32_t (&mw)[DirGeo<BS, NPOW>::CW], int& slot,
-                          int4 (&pv)[DirGeo<BS, NPOW>::PREF], int& lo, bool& pb) {
+                          uint2 (&pv)[DirGeo<BS, NPOW>::PREF], int& lo, bool& pb) {
   constexpr int W = DirGeo<BS, NPOW>::W;
   const int SM = t.SM;
   if (lo == INF32 || lo >= lenc) return INF32;
@@ -438,7 +441,7 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
   __syncthreads();
   const int rcap = hist ? hmax : t.Rcap;
   int extra_left = -1;  // history mode: rows still to walk after passing stopcut
-  int4 pv[G::PREF];
+  uint2 pv[G::PREF];
   int lo = L.sP[c];
   dir_load<BS, NPOW>(t, L, c, lo, DirGeo<BS, NPOW>::W, lenc, pv);
   int f0 = INF32, fn = 0;  // rows fetched for the next round: [f0, f0 + fn)

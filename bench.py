@@ -67,7 +67,7 @@ def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
       k_fd_transpose_ts 16N/event (N > 16: FDT read, FD and the 8-byte FD
                     timestamps written);
       k_witness_la   8N^2 per round (frontier rows read, transposed rows written);
-      k_la16_rows_runs 10N/event (N > 32: LA16 read, LA rows and the FDT runs written);
+      k_la16_rows_runs 6N/event (N > 32: LA16 read, the FDT runs written);
       k_la_win      (2N + 20)/event (32 < N <= 256, windowed exact propagation: the
                     head rows live in LDS, so per event only the packed row is
                     written, the 16-byte plan entry read and the 4-byte row sum
@@ -90,7 +90,7 @@ def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
                  "k_fdt_clear": 4 * n, "k_fdt_runs": 8 * n, "k_fss": 8 * n,
                  "k_rounds_walk": 4 * n, "k_rounds_coop": 4 * n, "k_rounds_coop_spec": 4 * n,
                  "k_walk_spec": 4 * n, "k_rounds_fss": 4 * n, "k_rounds_direct": 4 * n,
-                 "k_la_clear16": 2 * n, "k_la_sweep16": 6 * n, "k_la16_rows_runs": 10 * n,
+                 "k_la_clear16": 2 * n, "k_la_sweep16": 6 * n, "k_la16_rows_runs": 6 * n,
                  "k_la_win": 2 * n + 20, "k_la_wave": 2 * n + 16, "k_lw_plan": 40, "k_lw_pos": 0}
     if name in per_event:
         return per_event[name] * events
