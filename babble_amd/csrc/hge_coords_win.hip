@@ -122,6 +122,30 @@ __global__ void __launch_bounds__(256) k_lw_plan(Tables t, int64_t n0, int64_t n
   if (rm && lane == 63 - __builtin_clzll(rm)) atomicMax(&risky[(cs - n0) / WN], (int32_t)e);
 }
 
+// WPT consecutive packed words of an LDS row / to HBM (16-, 8- or 4-byte accesses)
+template <int WPT>
+__device__ __forceinline__ void lw_lds_read(const uint32_t* p, uint32_t (&v)[WPT]) {
+  if constexpr (WPT == 4) {
+    const uint4 q = *(const uint4*)p;
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  } else if constexpr (WPT == 2) {
+    const uint2 q = *(const uint2*)p;
+    v[0] = q.x; v[1] = q.y;
+  } else {
+    v[0] = *p;
+  }
+}
+template <int WPT>
+__device__ __forceinline__ void lw_lds_write(uint32_t* p, const uint32_t (&v)[WPT]) {
+  if constexpr (WPT == 4) *(uint4*)p = make_uint4(v[0], v[1], v[2], v[3]);
+  else if constexpr (WPT == 2) *(uint2*)p = make_uint2(v[0], v[1]);
+  else *p = v[0];
+}
+template <int WPT>
+__device__ __forceinline__ void lw_global_write(uint32_t* p, const uint32_t (&v)[WPT]) {
+  lw_lds_write<WPT>(p, v);
+}
+
 // One pass over every window (one workgroup each).  pass 1 computes every new row;
 // pass > 1 recomputes a window from its current starting rows until its running
 // head rows equal the previous pass's.  rsum[plan slot] = sum of the row's 16-bit
@@ -132,11 +156,14 @@ __global__ void __launch_bounds__(1024) k_la_win(Tables t, const int4* plan, int
                                                  const int32_t* wpos, const int32_t* olen, uint32_t* initbuf,
                                                  const int32_t* risky, uint32_t* rsum, int pass,
                                                  const int32_t* prev, int32_t* changed) {
-  constexpr int TPE = NPOW / 2;        // threads per event: one packed word each
-  constexpr int SL = 1024 / TPE;       // events per read/write phase
+  constexpr int RWW = NPOW / 2;         // packed words per (padded) row
+  constexpr int WPT = NPOW / 64;         // words per thread: 32 threads per event
+  constexpr int TPE = RWW / WPT;         // = 32
+  constexpr int SL = 1024 / TPE;         // events per read/write phase (32)
   constexpr int MAXI = (LW_K + SL - 1) / SL;
   constexpr int RW = TPE < 64 ? TPE : 64;  // lanes of one event inside a wave
-  __shared__ uint32_t s_st[NPOW * TPE];    // head rows [chain][word]
+  static_assert(TPE == 32, "half a wave per event");
+  __shared__ uint32_t s_st[NPOW * RWW] __attribute__((aligned(16)));  // head rows [chain][word]
   __shared__ int s_hp[NPOW], s_ol[NPOW];
   __shared__ int4 s_ev[LW_K];
   __shared__ uint32_t s_sum[LW_K];
@@ -150,14 +177,14 @@ __global__ void __launch_bounds__(1024) k_la_win(Tables t, const int4* plan, int
   if (s0 >= n1) return;
   const int64_t s1 = min(n1, s0 + (int64_t)WN);
   const int tid = threadIdx.x;
-  const int slot = tid / TPE, wd = tid - (tid / TPE) * TPE;
+  const int slot = tid / TPE, wd0 = (tid - (tid / TPE) * TPE) * WPT;  // first owned word
   if (tid < NPOW / 32) s_dirty[tid] = 0;
   __syncthreads();
   // starting rows: the heads before s0 as stored (pass 1: a new row of another
   // window is not written yet, take its own column only)
   uint32_t* ib = initbuf + (size_t)w * N * W;
-  for (int i = tid; i < NPOW * TPE; i += 1024) {
-    const int c = i / TPE, q = i - (i / TPE) * TPE;
+  for (int i = tid; i < NPOW * RWW; i += 1024) {
+    const int c = i / RWW, q = i - (i / RWW) * RWW;
     uint32_t val = 0;
     if (c < N && q < W) {
       const int hp = wpos[(size_t)w * N + c] - 1;
@@ -228,33 +255,44 @@ __global__ void __launch_bounds__(1024) k_la_win(Tables t, const int4* plan, int
     const int nlv = s_nlv;
     for (int L = 0; L < nlv; L++) {
       const int lo = s_lvoff[L], hi = s_lvoff[L + 1];
-      uint32_t nv[MAXI];
+      uint32_t nv[MAXI][WPT];
 #pragma unroll
       for (int i = 0; i < MAXI; i++) {
         const int j = lo + slot + i * SL;
-        nv[i] = 0;
-        if (lo + i * SL < hi && j < hi && wd < W) {
+        if (lo + i * SL < hi && j < hi) {
           const int4 en = s_ev[j];
           const int a = en.x & 0xFFFF, k = en.y, opc = en.z, opp = en.w;
-          uint32_t v = s_st[a * TPE + wd];
+          uint32_t v[WPT], o[WPT];
+          lw_lds_read<WPT>(&s_st[a * RWW + wd0], v);
+#pragma unroll
+          for (int u = 0; u < WPT; u++) o[u] = 0;
           if (opc >= 0) {
-            uint32_t o;
-            const size_t ro = ((size_t)opc * t.ccap + opp) * W + wd;
-            if (s_hp[opc] == opp) o = s_st[opc * TPE + wd];
-            else if (opp < s_ol[opc]) o = t.LA16[ro];  // an old, final row
-            else if ((en.x >> 24) & LW_INWIN)          // written by this workgroup this pass
-              o = __hip_atomic_load(t.LA16 + ro, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else if (pass == 1) o = (wd == (opc >> 1)) ? (uint32_t)(opp + 1) << ((opc & 1) * 16) : 0u;
-            else o = t.LA16[ro];  // another window's row: a lower bound
-            v = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2_t, v),
-                                                                         __builtin_bit_cast(u16x2_t, o)));
+            if (s_hp[opc] == opp) {
+              lw_lds_read<WPT>(&s_st[opc * RWW + wd0], o);
+            } else {
+              const uint32_t* src = t.LA16 + ((size_t)opc * t.ccap + opp) * W;
+#pragma unroll
+              for (int u = 0; u < WPT; u++) {
+                const int q = wd0 + u;
+                if (q >= W) continue;
+                if (opp < s_ol[opc]) o[u] = src[q];  // an old, final row
+                else if ((en.x >> 24) & LW_INWIN)     // written by this workgroup this pass
+                  o[u] = __hip_atomic_load(src + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else if (pass == 1) o[u] = (q == (opc >> 1)) ? (uint32_t)(opp + 1) << ((opc & 1) * 16) : 0u;
+                else o[u] = src[q];  // another window's row: a lower bound
+              }
+            }
           }
-          if (wd == (a >> 1)) {
-            const uint32_t own = (uint32_t)(k + 1) << ((a & 1) * 16);
-            v = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2_t, v),
-                                                                         __builtin_bit_cast(u16x2_t, own)));
+#pragma unroll
+          for (int u = 0; u < WPT; u++) {
+            uint32_t x = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2_t, v[u]),
+                                                                               __builtin_bit_cast(u16x2_t, o[u])));
+            if (wd0 + u == (a >> 1))
+              x = __builtin_bit_cast(uint32_t,
+                                     __builtin_elementwise_max(__builtin_bit_cast(u16x2_t, x),
+                                                               __builtin_bit_cast(u16x2_t, (uint32_t)(k + 1) << ((a & 1) * 16))));
+            nv[i][u] = x;
           }
-          nv[i] = v;
         }
       }
       __syncthreads();  // every read of this level's head rows is done
@@ -263,17 +301,33 @@ __global__ void __launch_bounds__(1024) k_la_win(Tables t, const int4* plan, int
         if (lo + i * SL >= hi) break;  // wave-uniform
         const int j = lo + slot + i * SL;
         uint32_t s = 0;
-        if (j < hi && wd < W) {
+        if (j < hi) {
           const int4 en = s_ev[j];
           const int a = en.x & 0xFFFF, k = en.y;
-          s_st[a * TPE + wd] = nv[i];
-          t.LA16[((size_t)a * t.ccap + k) * W + wd] = nv[i];
-          if (wd == 0) s_hp[a] = k;
-          s = (nv[i] & 0xFFFFu) + (nv[i] >> 16);
-        }
+          lw_lds_write<WPT>(&s_st[a * RWW + wd0], nv[i]);
+          uint32_t* dst = t.LA16 + ((size_t)a * t.ccap + k) * W + wd0;
+          if (W == RWW) {
+            lw_global_write<WPT>(dst, nv[i]);
+          } else {
 #pragma unroll
-        for (int off = RW / 2; off >= 1; off >>= 1) s += __shfl_xor(s, off);
-        if ((tid & (RW - 1)) == 0 && j < hi && s) atomicAdd(&s_sum[j], s);
+            for (int u = 0; u < WPT; u++)
+              if (wd0 + u < W) dst[u] = nv[i][u];
+          }
+          if (wd0 == 0) s_hp[a] = k;
+#pragma unroll
+          for (int u = 0; u < WPT; u++) s += (nv[i][u] & 0xFFFFu) + (nv[i][u] >> 16);
+        }
+        // sum over the event's 32 lanes: rows of 16 by DPP (quad_perm xor 1, xor 2,
+        // row_half_mirror, row_mirror), then the two rows by readlane (no LDS permutes)
+        int r = (int)s;
+        r += __builtin_amdgcn_mov_dpp(r, 0xB1, 0xF, 0xF, false);
+        r += __builtin_amdgcn_mov_dpp(r, 0x4E, 0xF, 0xF, false);
+        r += __builtin_amdgcn_mov_dpp(r, 0x141, 0xF, 0xF, false);
+        r += __builtin_amdgcn_mov_dpp(r, 0x140, 0xF, 0xF, false);
+        const uint32_t lo2 = (uint32_t)(__builtin_amdgcn_readlane(r, 0) + __builtin_amdgcn_readlane(r, 16));
+        const uint32_t hi2 = (uint32_t)(__builtin_amdgcn_readlane(r, 32) + __builtin_amdgcn_readlane(r, 48));
+        const uint32_t tot = (tid & 32) ? hi2 : lo2;
+        if ((tid & 31) == 0 && j < hi) s_sum[j] = tot;  // one half-wave per event: no atomics
       }
       if (wt) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // rows a risky read may need
       __syncthreads();
