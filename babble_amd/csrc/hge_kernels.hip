@@ -1869,7 +1869,7 @@ __global__ void __launch_bounds__(1024) k_bucket_list(const int32_t* cnt, int n,
 }
 
 // keys per bucket that k_bucket_sort_big sorts whole in LDS (k_bucket_sort leaves them to it)
-constexpr int BIG_SORT = 4096;
+constexpr int BIG_SORT = 8192;
 
 __device__ void bucket_sort_one(int b, const int32_t* bend, const int32_t* bcnt, OKey* keys,
                                 OKey* tmp, int32_t* ids_out, bool skip_big) {
@@ -1937,16 +1937,18 @@ __global__ void __launch_bounds__(256) k_bucket_sort(const int32_t* bend, const 
 
 // Buckets of 513 .. BIG_SORT keys -- in a replay nearly every key sits in one: the
 // call that decides a round's fame receives that round's ~EPR events at once
-// (3,448 at N = 256).  One 1024-thread block sorts such a bucket whole in LDS: a
-// bitonic index sort over the leading 192 bits of the key (call|rr, cts, S[0..63]);
-// keys equal on those (S is uniform: ~never) are ordered by the full key from HBM.
-// k_bucket_sort's 512-key chunks + pairwise merges through global scratch moved
-// ~50x the keys' bytes for such buckets (25 GB per 256/10M replay, rocprofv3 PMC).
+// (3,448 at N = 256; 256/2M: 422 calls of 2-4k keys, 68 of 4-8k, 4 larger,
+// scripts/analysis/call_buckets.py).  One 1024-thread block sorts such a bucket
+// whole in LDS: a bitonic index sort over (rr, cts, the top 32 bits of S) -- the
+// call is the bucket's -- 18 bytes per key, 147 KB at 8,192 keys; keys equal on
+// those bits are ordered by the full key from HBM.  k_bucket_sort's 512-key
+// chunks + pairwise merges through global scratch moved ~50x the keys' bytes for
+// such buckets (25 GB per 256/10M replay, rocprofv3 PMC).
 __global__ void __launch_bounds__(1024) k_bucket_sort_big(const int32_t* bend, const int32_t* bcnt,
                                                           const int32_t* list, const int32_t* nlist,
                                                           const OKey* keys, int32_t* ids_out) {
-  __shared__ uint64_t sa[BIG_SORT], sb[BIG_SORT], ss[BIG_SORT];
-  __shared__ uint32_t sid[BIG_SORT];
+  __shared__ uint64_t sb[BIG_SORT];
+  __shared__ uint32_t sr[BIG_SORT], ss[BIG_SORT];
   __shared__ uint16_t ix[BIG_SORT];
   const int tid = threadIdx.x, T = blockDim.x;
   for (int li = blockIdx.x; li < *nlist; li += gridDim.x) {
@@ -1959,13 +1961,13 @@ __global__ void __launch_bounds__(1024) k_bucket_sort_big(const int32_t* bend, c
     for (int i = tid; i < P; i += T) {
       if (i < n) {
         const OKey k = K[i];
-        sa[i] = k.a;
+        sr[i] = (uint32_t)k.a;  // rr (the call is the bucket's)
         sb[i] = k.b;
-        ss[i] = k.s0;
-        sid[i] = k.id;
+        ss[i] = (uint32_t)(k.s0 >> 32);
       } else {
-        sa[i] = sb[i] = ss[i] = ~0ull;
-        sid[i] = 0xFFFFFFFFu;
+        sr[i] = 0xFFFFFFFFu;
+        sb[i] = ~0ull;
+        ss[i] = 0xFFFFFFFFu;
       }
       ix[i] = (uint16_t)i;
     }
@@ -1978,11 +1980,11 @@ __global__ void __launch_bounds__(1024) k_bucket_sort_big(const int32_t* bend, c
           const bool up = ((lo & size) == 0);
           const int x = ix[lo], y = ix[hi];
           bool yl;  // key y < key x
-          if (sa[x] != sa[y]) yl = sa[y] < sa[x];
+          if (sr[x] != sr[y]) yl = sr[y] < sr[x];
           else if (sb[x] != sb[y]) yl = sb[y] < sb[x];
           else if (ss[x] != ss[y]) yl = ss[y] < ss[x];
           else if (x >= n || y >= n) yl = y < x;  // padding (only padding ties padding)
-          else yl = okless(K[y], K[x]);          // equal leading 192 bits: the full key
+          else yl = okless(K[y], K[x]);          // equal leading bits: the full key
           if (yl == up) {
             ix[lo] = (uint16_t)y;
             ix[hi] = (uint16_t)x;
@@ -1992,11 +1994,10 @@ __global__ void __launch_bounds__(1024) k_bucket_sort_big(const int32_t* bend, c
       }
     }
     int32_t* out = ids_out + (bend[b] - n);
-    for (int i = tid; i < n; i += T) out[i] = (int32_t)sid[ix[i]];
+    for (int i = tid; i < n; i += T) out[i] = (int32_t)K[ix[i]].id;
     __syncthreads();
   }
 }
-
 
 __global__ void k_scatter_und(const int32_t* cand, int ncand, const int32_t* f_und,
                               const int32_t* pos, int32_t* und) {

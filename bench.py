@@ -369,7 +369,7 @@ def main():
         if base in ("k_la_sweep", "k_la_clear", "k_transpose", "k_fss", "k_fdt_runs",
                     "k_fdt_clear", "k_rounds_coop", "k_rounds_coop_spec", "k_median_wave",
                     "k_la_clear16", "k_la_sweep16", "k_la16_rows_runs", "k_rounds_direct",
-                    "k_fd_transpose_ts", "k_witness_la"):
+                    "k_fd_transpose_ts", "k_witness_la", "k_la_win", "k_la_wave", "k_lw_plan"):
             b, pl, gbs, lpr = kernel_roofline(name)
             hbm_kernels[name] = {"achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
                                  "alg_bytes_per_launch": int(b), "launch_ms": round(pl, 4),
