@@ -1143,7 +1143,7 @@ struct hge_engine {
     const int npow = N <= 64 ? 64 : N <= 128 ? 128 : 256;
     // k_la_win (default): one 1024-thread workgroup per window; HGE_LW_KERNEL=wave:
     // k_la_wave, one wave per (window, 64-word slice), npow x 256 B of LDS each
-    static const bool BLOCK = !(getenv("HGE_LW_KERNEL") && strcmp(getenv("HGE_LW_KERNEL"), "wave") == 0);
+    const bool BLOCK = !(getenv("HGE_LW_KERNEL") && strcmp(getenv("HGE_LW_KERNEL"), "wave") == 0);
     const int W = t.NW2, S = (W + 63) / 64;
     static const int64_t WMIN = getenv("HGE_LW_MIN") ? std::max(64, atoi(getenv("HGE_LW_MIN"))) : 4096;
     const int per_cu = BLOCK ? (npow == 256 ? 1 : 2) : std::max(1, std::min(8, (160 * 1024) / (npow * 256 + 512) / S));

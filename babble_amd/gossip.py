@@ -50,8 +50,12 @@ def _bytes32(seed, salt, n):
     return out.astype(">u8").view(np.uint8).reshape(n, 32)
 
 
-def random_gossip(n, events, seed=1, forkers=0, fork_p=0.0, cascade_p=0.0):
+def random_gossip(n, events, seed=1, forkers=0, fork_p=0.0, cascade_p=0.0, op_lag=0):
     """Return a dict describing a submission stream of `events` honest events.
+
+    op_lag > 0: the other-parent is the peer's event `lag` positions before its
+    latest, lag ~ U{0..op_lag} (a stale view of the peer, as when a node inserts
+    events it learned late): other-parents that are not their chain's head.
 
     Keys: n, creator, index, sp, op (submission indices, -1 = none), ts, S
     (uint8[E,32] big-endian), hash (uint8[E,32]), ntx, honest (bool mask).
@@ -94,6 +98,8 @@ def random_gossip(n, events, seed=1, forkers=0, fork_p=0.0, cascade_p=0.0):
                 continue
             slice_ = order[starts[c]:ends[c]]
             k = np.searchsorted(slice_, subs[sel], side="left") - 1
+            if op_lag > 0:
+                k = np.maximum(0, k - rng.integers(0, op_lag + 1, len(k)))
             pos[sel] = slice_[k]
         del lo
         op[n:] = pos

@@ -105,3 +105,27 @@ def test_wide256_fd_rows_online_and_growth():
     finally:
         a.close()
         b.close()
+
+
+@pytest.mark.parametrize("n,events,G,kernel", [(64, 6000, 8, "block"), (256, 5000, 5, "block"),
+                                               (64, 6000, 8, "wave")])
+def test_stale_other_parents_in_windows(n, events, G, kernel, monkeypatch):
+    """Other-parents that are not their chain's head when the event is inserted (a
+    node inserting events it learned late; `op_lag`) are the windowed lastAncestors
+    kernels' "risky" path: read from HBM, chunk-level store drains, no early exit
+    past them.  Forced into several windows (HGE_LW_G), compared with the oracle."""
+    from babble_amd.engine import Engine
+    monkeypatch.setenv("HGE_LW_G", str(G))
+    monkeypatch.setenv("HGE_LW_KERNEL", kernel)
+    dag = random_gossip(n, events, seed=77 + n, op_lag=4)
+    eng = Engine(n, 1 << 14)
+    try:
+        run_case(eng, dag, n)
+        LA, fd = _np_coords(dag, n)
+        rng = np.random.default_rng(5)
+        for x in rng.choice(events, 30, replace=False).tolist() + [events - 1]:
+            gla, gfd = eng.coordinates(int(x))
+            np.testing.assert_array_equal(gla, LA[x])
+            np.testing.assert_array_equal(np.asarray(gfd, np.int64), fd(x))
+    finally:
+        eng.close()
