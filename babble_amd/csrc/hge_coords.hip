@@ -260,8 +260,11 @@ __global__ void __launch_bounds__(256) k_la_sweep16(Tables t, const int2* segs, 
 // every other new position lies in a new event's run.  Tile: positions
 // [p0, p0 + 64) of chain j (from plo_j = olen_j - 1: the row before the first
 // new event is the first run's lower bound) x columns [c0, c0 + 64).
-__global__ void __launch_bounds__(256) k_la16_rows_runs(Tables t, int32_t* FDT, const int32_t* plo,
+// FT = int32_t (INF32 = none) or uint16_t (0xFFFF = none; N > 128, FD transpose only)
+template <typename FT>
+__global__ void __launch_bounds__(256) k_la16_rows_runs(Tables t, FT* FDT, const int32_t* plo,
                                                         const int32_t* olen, const int32_t* len) {
+  constexpr FT FINF = sizeof(FT) == 2 ? (FT)0xFFFF : (FT)INF32;
   __shared__ int32_t tile[65][65];  // row 0: position p0 - 1; row 1 + r: position p0 + r
   const int N = t.N;
   const size_t ccap = t.ccap;
@@ -275,8 +278,8 @@ __global__ void __launch_bounds__(256) k_la16_rows_runs(Tables t, int32_t* FDT, 
       for (int cc = ty; cc < 64; cc += 4) {
         const int c = c0 + cc;
         if (c >= N) continue;
-        int32_t* row = FDT + ((size_t)j * N + c) * ccap;
-        for (int q = olen[c] + tx; q < len[c]; q += 64) row[q] = INF32;
+        FT* row = FDT + ((size_t)j * N + c) * ccap;
+        for (int q = olen[c] + tx; q < len[c]; q += 64) row[q] = FINF;
       }
     return;
   }
@@ -304,15 +307,15 @@ __global__ void __launch_bounds__(256) k_la16_rows_runs(Tables t, int32_t* FDT, 
   for (int cc = ty; cc < 64; cc += 4) {
     const int c = c0 + cc;
     if (c >= N) break;
-    int32_t* row = FDT + ((size_t)j * N + c) * ccap;
+    FT* row = FDT + ((size_t)j * N + c) * ccap;
     if (isnew) {
       const int hi = tile[tx + 1][cc];
       const int lo = k > 0 ? tile[tx][cc] : -1;
-      for (int q = lo + 1; q <= hi; q++) row[q] = k;
+      for (int q = lo + 1; q <= hi; q++) row[q] = (FT)k;
     }
     if (lasttile) {
       const int tail0 = max(olen[c], tile[lj - p0][cc] + 1);
-      for (int q = tail0 + tx; q < len[c]; q += 64) row[q] = INF32;
+      for (int q = tail0 + tx; q < len[c]; q += 64) row[q] = FINF;
     }
   }
 }
@@ -366,7 +369,8 @@ __global__ void __launch_bounds__(256) k_transpose(Tables t, const int32_t* LAT_
 // The timestamp gathers sit in the read phase, where a wave walks one chain j
 // along q and FD is non-decreasing: neighbouring lanes read neighbouring tsch
 // cells of that chain (a few cache lines per wave), not one chain per lane.
-__global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const int32_t* FDT, const int32_t* plo,
+template <typename FT>
+__global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const FT* FDT, const int32_t* plo,
                                                          const int32_t* len) {
   __shared__ int32_t tile[64][65];
   __shared__ int64_t tts[64][65];
@@ -386,7 +390,12 @@ __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const int32_t
 #pragma unroll
     for (int i = 0; i < 16; i++) {
       const int jj = c0 + ty + 4 * i, q = p0 + tx;
-      kv[i] = (jj < N && q < pend) ? FDT[((size_t)jj * N + a) * ccap + q] : INF32;
+      if (jj < N && q < pend) {
+        const FT f = FDT[((size_t)jj * N + a) * ccap + q];
+        kv[i] = (sizeof(FT) == 2 && f == (FT)0xFFFF) ? INF32 : (int)f;
+      } else {
+        kv[i] = INF32;
+      }
     }
     int64_t tv[16];
 #pragma unroll

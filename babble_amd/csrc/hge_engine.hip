@@ -157,6 +157,7 @@ struct hge_engine {
   // coordinate sweeps: transposed tables and scratch
   int n_sweeps = 0;
   DBuf<int32_t> d_LAT, d_FDT, s_chg, s_bar, s_dirty;
+  DBuf<uint16_t> d_FDT16;  // N > 128 on the direct rounds path: FDT as uint16 (INF = 0xFFFF)
   // windowed lastAncestors (hge_coords_win.hip): chunk plans, row sums, starting rows
   DBuf<int4> s_lwplan;
   DBuf<uint32_t> s_lwsum, s_lwinit;
@@ -347,6 +348,7 @@ struct hge_engine {
     s_lwinit.free_();
     d_ts.free_();
     d_FDTS.free_();
+    d_FDT16.free_();
     d_cts.free_();
     s_cts.free_();
     d_S.free_();
@@ -405,13 +407,14 @@ struct hge_engine {
 
   // chain-major tables [N][ccap][N]: grow to nc positions per chain, keeping contents
   // rowmajor: [N][ccap][N] (LA, FD, FSS); else [N][N][ccap] (LAT, FDT)
-  void grow_chain_table(DBuf<int32_t>& b, int64_t nc, bool keep, bool rowmajor = true) {
-    int32_t* q = nullptr;
-    HIPCHK(hipMalloc(&q, sizeof(int32_t) * (size_t)N * nc * N));
+  template <typename T>
+  void grow_chain_table(DBuf<T>& b, int64_t nc, bool keep, bool rowmajor = true) {
+    T* q = nullptr;
+    HIPCHK(hipMalloc(&q, sizeof(T) * (size_t)N * nc * N));
     const size_t rows = rowmajor ? N : (size_t)N * N, w = rowmajor ? N : 1;
     if (keep && ccap > 0 && b.p)
-      HIPCHK(hipMemcpy2DAsync(q, sizeof(int32_t) * nc * w, b.p, sizeof(int32_t) * ccap * w,
-                              sizeof(int32_t) * ccap * w, rows, hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipMemcpy2DAsync(q, sizeof(T) * nc * w, b.p, sizeof(T) * ccap * w,
+                              sizeof(T) * ccap * w, rows, hipMemcpyDeviceToDevice, st));
     sync();
     b.free_();
     b.p = q;
@@ -478,7 +481,8 @@ struct hge_engine {
     // 16/32 columns for the LDS walk; rebuilt from the frontier on, never kept
     if (N <= 32) d_FSS.need((size_t)N * nc * std::max(N, 16));
     if (!sweep16()) grow_chain_table(d_LAT, nc, false, false);  // rebuilt per batch from LA
-    grow_chain_table(d_FDT, nc, true, false);       // persistent: FD in run layout
+    if (fdt16()) grow_chain_table(d_FDT16, nc, true, false);  // persistent: FD in run layout
+    else grow_chain_table(d_FDT, nc, true, false);
     ccap = (int)nc;
   }
 
@@ -953,6 +957,7 @@ struct hge_engine {
     // above N = 128 only 2 walkers fit, and the 512-thread sequential kernel is faster
     // than 2 walkers sharing each CU (22.5 vs 33.6 ms at 256/2M, profiles/r01r_*)
     int nw = ev ? atoi(ev) : (minlen >= 1024 && N <= 128 ? 8 : 0);
+    if (fdt16()) nw = 0;  // the walkers gather from the int32 FDT table
     nw = std::min(nw, cap);
     return nw >= 2 ? nw : 0;
   }
@@ -1126,6 +1131,14 @@ struct hge_engine {
   // N > 32: lastAncestors live only in the packed 16-bit table (chains are capped at
   // 65,534 events there); the int32 LA rows exist for N <= 32
   bool sweep16() const { return N > 32; }
+  // HGE_FDT16=1: the firstDescendants runs table as uint16 where nothing but the FD
+  // transpose reads it (N > 128, direct rounds: no FDT-gather walkers).  Measured at
+  // 256/10M: the runs kernel 6.7 -> 5.2 ms but the transpose's 2-byte loads 8.1 -> 13.3 ms,
+  // so int32 stays the default.
+  bool fdt16() const {
+    static const bool on = getenv("HGE_FDT16") && atoi(getenv("HGE_FDT16")) == 1;
+    return on && N > 128 && direct_rounds();
+  }
 
   // 32 < N <= 256: lastAncestors by windowed exact propagation (hge_coords_win.hip)
   // instead of the sweeps; HGE_LA_WIN=0 keeps the sweeps
@@ -1274,8 +1287,12 @@ struct hge_engine {
     }
     if (p16) {
       // LA16 -> the int32 LA rows and the FDT runs from the same tiles (no LAT)
-      KLAUNCH(k_la16_rows_runs, dim3(div_up(maxnew + 1, 64), div_up(N, 64), N), dim3(256), 0, st, t,
-              d_FDT.p, k_plo, olen, len);
+      if (fdt16())
+        KLAUNCH((k_la16_rows_runs<uint16_t>), dim3(div_up(maxnew + 1, 64), div_up(N, 64), N), dim3(256), 0, st,
+                t, d_FDT16.p, k_plo, olen, len);
+      else
+        KLAUNCH((k_la16_rows_runs<int32_t>), dim3(div_up(maxnew + 1, 64), div_up(N, 64), N), dim3(256), 0, st,
+                t, d_FDT.p, k_plo, olen, len);
     } else {
       // LA -> LAT for positions [olen-1, len), then the runs of the new events (and
       // the new positions with no descendant yet)
@@ -1294,8 +1311,12 @@ struct hge_engine {
     int span = 1;
     for (int c = 0; c < N; c++) span = std::max(span, chain_len[c] - qlo[c]);
     if (N > 16)
-      KLAUNCH(k_fd_transpose_ts, dim3(N, div_up(N, 64), std::min(div_up(span, 64), 65535)), dim3(256), 0, st, t,
-              (const int32_t*)d_FDT.p, k_qlo, len);
+      if (fdt16())
+        KLAUNCH((k_fd_transpose_ts<uint16_t>), dim3(N, div_up(N, 64), std::min(div_up(span, 64), 65535)), dim3(256),
+                0, st, t, (const uint16_t*)d_FDT16.p, k_qlo, len);
+      else
+        KLAUNCH((k_fd_transpose_ts<int32_t>), dim3(N, div_up(N, 64), std::min(div_up(span, 64), 65535)), dim3(256),
+                0, st, t, (const int32_t*)d_FDT.p, k_qlo, len);
     else
       KLAUNCH(k_transpose, dim3(div_up(span, 64), div_up(N, 64), N), dim3(256), 0, st, t, d_FDT.p,
               (int32_t*)nullptr, k_qlo, len, 1);

@@ -65,9 +65,10 @@ def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
       k_transpose   16N/event at N <= 16 (LA -> LAT and FDT -> FD: each reads and
                     writes 4N), 8N at 16 < N <= 32 (LA -> LAT only);
       k_fd_transpose_ts 16N/event (N > 16: FDT read, FD and the 8-byte FD
-                    timestamps written);
+                    timestamps written; 14N with HGE_FDT16=1 above N = 128);
       k_witness_la   8N^2 per round (frontier rows read, transposed rows written);
-      k_la16_rows_runs 6N/event (N > 32: LA16 read, the FDT runs written);
+      k_la16_rows_runs 6N/event (N > 32: LA16 read, the FDT runs written; 4N with
+                    HGE_FDT16=1 above N = 128);
       k_la_win      (2N + 20)/event (32 < N <= 256, windowed exact propagation: the
                     head rows live in LDS, so per event only the packed row is
                     written, the 16-byte plan entry read and the 4-byte row sum
@@ -86,11 +87,11 @@ def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
     if name == "k_witness_la":
         return 8 * n * n * rounds
     per_event = {"k_la_sweep": 12 * n, "k_la_clear": 4 * n, "k_transpose": 16 * n if n <= 16 else 8 * n,
-                 "k_fd_transpose_ts": 16 * n,
+                 "k_fd_transpose_ts": (14 if os.environ.get("HGE_FDT16") == "1" and n > 128 else 16) * n,
                  "k_fdt_clear": 4 * n, "k_fdt_runs": 8 * n, "k_fss": 8 * n,
                  "k_rounds_walk": 4 * n, "k_rounds_coop": 4 * n, "k_rounds_coop_spec": 4 * n,
                  "k_walk_spec": 4 * n, "k_rounds_fss": 4 * n, "k_rounds_direct": 4 * n,
-                 "k_la_clear16": 2 * n, "k_la_sweep16": 6 * n, "k_la16_rows_runs": 6 * n,
+                 "k_la_clear16": 2 * n, "k_la_sweep16": 6 * n, "k_la16_rows_runs": (4 if os.environ.get("HGE_FDT16") == "1" and n > 128 else 6) * n,
                  "k_la_win": 2 * n + 20, "k_la_wave": 2 * n + 16, "k_lw_plan": 40, "k_lw_pos": 0}
     if name in per_event:
         return per_event[name] * events
