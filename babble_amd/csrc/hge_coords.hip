@@ -365,7 +365,9 @@ __global__ void __launch_bounds__(256) k_transpose(Tables t, const int32_t* LAT_
 }
 
 // k_transpose mode 1 plus the timestamps (N > 16, the wide median):
-// FDT[j][c][q] -> FD[(c, q)][j] and FDTS[(c, q)][j] = ts of the event (j, FD).
+// FDT[j][c][q] -> FD[(c, q)][j] and FDTD[(c, q)][j] = ts of the event (j, FD) - ts of
+// (c, q), as int32 (half the bytes of the timestamps themselves; a row tile with an
+// offset outside int32 is flagged in FDTW and the median gathers exact timestamps).
 // The timestamp gathers sit in the read phase, where a wave walks one chain j
 // along q and FD is non-decreasing: neighbouring lanes read neighbouring tsch
 // cells of that chain (a few cache lines per wave), not one chain per lane.
@@ -374,6 +376,7 @@ __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const FT* FDT
                                                          const int32_t* len) {
   __shared__ int32_t tile[64][65];
   __shared__ int64_t tts[64][65];
+  __shared__ int64_t rts[64];  // the tile's row events' own timestamps
   const int N = t.N;
   const size_t ccap = t.ccap;
   // grid (chain, column tile, position tiles): consecutive workgroups take the same
@@ -408,14 +411,26 @@ __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const FT* FDT
       tile[ty + 4 * i][tx] = kv[i];
       tts[ty + 4 * i][tx] = kv[i] != INF32 ? tv[i] : 0;
     }
+    if (ty == 0) rts[tx] = t.tsch[(size_t)a * ccap + min(p0 + tx, pend - 1)];
     __syncthreads();
-    for (int r = ty; r < 64; r += 4) {
+    const int NT = (N + 63) >> 6;
+    for (int r = ty; r < 64; r += 4) {  // wave ty writes rows r: the 64 columns of one row each time
       const int q = p0 + r, jj = c0 + tx;
+      bool esc = false;
       if (q < pend && jj < N) {
         const size_t o = rowoff(t, a, q) + jj;
-        t.FD[o] = tile[tx][r];
-        t.FDTS[o] = tts[tx][r];
+        const int k = tile[tx][r];
+        int32_t dv = 0;
+        if (k != INF32) {  // offset from the row event's own timestamp
+          const int64_t d = tts[tx][r] - rts[r];
+          esc = d < -(int64_t)INT32_MAX || d > (int64_t)INT32_MAX;
+          dv = esc ? INT32_MIN : (int32_t)d;
+        }
+        t.FD[o] = k;
+        t.FDTD[o] = dv;
       }
+      const bool any = __ballot(esc) != 0;
+      if (tx == 0 && q < pend) t.FDTW[((size_t)a * ccap + q) * NT + blockIdx.y] = any ? 1 : 0;
     }
     __syncthreads();
   }

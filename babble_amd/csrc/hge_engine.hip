@@ -167,7 +167,8 @@ struct hge_engine {
     if (!ncu_cache) HIPCHK(hipDeviceGetAttribute(&ncu_cache, hipDeviceAttributeMultiprocessorCount, device));
     return ncu_cache;
   }
-  DBuf<int64_t> d_FDTS;  // N > 16: timestamps at the FD positions (the wide median)
+  DBuf<int32_t> d_FDTD;  // N > 16: timestamp offsets at the FD positions (the wide median)
+  DBuf<uint8_t> d_FDTW;  // N > 16: per (row, 64-column tile) out-of-range flags of d_FDTD
   DBuf<int32_t> d_WLA;   // N > 16: round frontier rows transposed (k_witness_la)
   DBuf<uint64_t> d_ssc, s_gran;
   DBuf<int32_t> s_bseg;
@@ -234,7 +235,8 @@ struct hge_engine {
     t.NW2 = (N + 1) / 2;
     t.LA16 = d_LA16.p;
     t.FD = d_FD.p;
-    t.FDTS = d_FDTS.p;
+    t.FDTD = d_FDTD.p;
+    t.FDTW = d_FDTW.p;
     t.WLA = d_WLA.p;
     t.round = d_round.p;
     t.wit = d_wit.p;
@@ -347,7 +349,8 @@ struct hge_engine {
     s_lwsum.free_();
     s_lwinit.free_();
     d_ts.free_();
-    d_FDTS.free_();
+    d_FDTD.free_();
+    d_FDTW.free_();
     d_FDT16.free_();
     d_cts.free_();
     s_cts.free_();
@@ -466,16 +469,18 @@ struct hge_engine {
       d_LA16.n = (size_t)N * nc * w;
     }
     grow_chain_table(d_FD, nc, true);
-    if (N > 16) {  // FDTS rows below a batch's qlo are kept
-      int64_t* q = nullptr;
-      HIPCHK(hipMalloc(&q, sizeof(int64_t) * (size_t)N * nc * N));
-      if (ccap > 0 && d_FDTS.p)
-        HIPCHK(hipMemcpy2DAsync(q, sizeof(int64_t) * nc * N, d_FDTS.p, sizeof(int64_t) * ccap * N,
-                                sizeof(int64_t) * ccap * N, N, hipMemcpyDeviceToDevice, st));
+    if (N > 16) {  // FD timestamp rows below a batch's qlo are kept
+      grow_chain_table(d_FDTD, nc, true);
+      const size_t NT = (size_t)(N + 63) / 64;
+      uint8_t* q = nullptr;
+      HIPCHK(hipMalloc(&q, (size_t)N * nc * NT));
+      if (ccap > 0 && d_FDTW.p)
+        HIPCHK(hipMemcpy2DAsync(q, nc * NT, d_FDTW.p, (size_t)ccap * NT, (size_t)ccap * NT, N,
+                                hipMemcpyDeviceToDevice, st));
       sync();
-      d_FDTS.free_();
-      d_FDTS.p = q;
-      d_FDTS.n = (size_t)N * nc * N;
+      d_FDTW.free_();
+      d_FDTW.p = q;
+      d_FDTW.n = (size_t)N * nc * NT;
     }
     // first-strong-seer rows (N <= 32): int32 rows of N, or uint16 rows padded to
     // 16/32 columns for the LDS walk; rebuilt from the frontier on, never kept
@@ -1678,7 +1683,7 @@ struct hge_engine {
                      int R_last, bool fresh) {
     // N > 16: the median is a wave-wide radix select (k_median_wave) over coalesced
     // rows: the round frontier rows transposed (WLA, k_witness_la, for every round a
-    // candidate can receive) and the FD timestamps (FDTS).  A fresh replay's
+    // candidate can receive) and the FD timestamp offsets (FDTD).  A fresh replay's
     // candidate list is the identity (candidate q = event q).
     const bool wmed = N > 16;
     const bool ident = fresh && cand == d_und.p && (int64_t)ncand == n_events;

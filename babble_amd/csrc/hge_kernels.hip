@@ -39,7 +39,10 @@ struct Tables {
   int32_t* chain;
   int2* opcp;     // [N][ccap]: (creator, index) of the other-parent, (-1, -1) if none
   int64_t* tsch;  // [N][ccap]: timestamp of the event at (chain, position)
-  int64_t* FDTS;  // N > 16: [N][ccap][N] timestamp of the event at FD[(c, p)][j] (0: none)
+  // N > 16: [N][ccap][N] timestamp of the event at FD[(c, p)][j] minus that of (c, p) itself
+  // (0: none; INT32_MIN: outside int32, the row's 64-column tile flagged in FDTW)
+  int32_t* FDTD;
+  uint8_t* FDTW;  // N > 16: [N][ccap][ceil(N / 64)]: 1 = the tile holds an out-of-range delta
   int32_t* WLA;   // N > 16: [Rcap][N][N] LA[(d, C[r][d])][cx] at [r][cx][d]
   int32_t* LA;
   int32_t* FD;
@@ -1585,11 +1588,11 @@ __global__ void __launch_bounds__(256) k_witness_la(Tables t, int rr_lo) {
 
 // MedianTimestamp (hashgraph.go:762-770) for wide hashgraphs: one wave per
 // received event.  Lane l holds the timestamps of the famous witnesses
-// d = l, l+64, ... that see x (OSA(w, x) = FD[x][cw], its timestamp FDTS[x][cw]);
+// d = l, l+64, ... that see x (OSA(w, x) = FD[x][cw], its timestamp offset FDTD[x][cw]);
 // the upper median (element len/2 of the sorted list) is found by a bitwise
 // radix select over the order-preserving uint64 image of the int64 timestamps.
 // Every per-witness input is a coalesced row: the "sees x" thresholds
-// WLA[rr][cx][.] (k_witness_la) and the timestamps FDTS[x][.] (k_fd_transpose_ts),
+// WLA[rr][cx][.] (k_witness_la) and the timestamp offsets FDTD[x][.] (k_fd_transpose_ts),
 // instead of 2N scattered gathers per event.
 template <int VPL>
 __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* cand, int ncand,
@@ -1622,13 +1625,32 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
     qe[e] = q;
     ixe[e] = ix;
     const int32_t* thr = t.WLA + ((size_t)rr * N + cx) * N;
-    const int64_t* tsr = t.FDTS + ((size_t)cx * t.ccap + ix) * N;
+    const size_t rw = (size_t)cx * t.ccap + ix;
+    const int32_t* tdr = t.FDTD + rw * N;
+    // the FD timestamps as int32 offsets from x's own timestamp; a row with an offset
+    // outside int32 (flagged per 64-column tile) gathers the exact ones instead
+    const int NT = (N + 63) >> 6;
+    int wide = 0;
+    if (NT == 4) {
+      wide = *(const int32_t*)(t.FDTW + rw * 4);  // one aligned load for the 4 tiles
+    } else {
+      for (int k = 0; k < NT; k++) wide |= t.FDTW[rw * NT + k];
+    }
+    const int64_t base = t.ts[x];
 #pragma unroll
     for (int k = 0; k < VPL; k++) {
       const int dd = min(lane + 64 * k, N - 1);
       fw[e][k] = seg_fws[(size_t)sg * NW + (k < NW ? k : 0)];
       th[e][k] = thr[dd];
-      ts[e][k] = tsr[dd];
+      ts[e][k] = base + (int64_t)tdr[dd];
+    }
+    if (__builtin_amdgcn_readfirstlane(wide)) {
+#pragma unroll
+      for (int k = 0; k < VPL; k++) {
+        const int dd = min(lane + 64 * k, N - 1);
+        const int f = t.FD[rw * N + dd];
+        ts[e][k] = f != INF32 ? t.tsch[(size_t)dd * t.ccap + f] : 0;
+      }
     }
   }
 #pragma unroll

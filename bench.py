@@ -64,8 +64,8 @@ def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
       k_la_sweep16 / k_la_clear16  6N / 2N per event (N > 32: the same on packed u16);
       k_transpose   16N/event at N <= 16 (LA -> LAT and FDT -> FD: each reads and
                     writes 4N), 8N at 16 < N <= 32 (LA -> LAT only);
-      k_fd_transpose_ts 16N/event (N > 16: FDT read, FD and the 8-byte FD
-                    timestamps written; 14N with HGE_FDT16=1 above N = 128);
+      k_fd_transpose_ts 12N/event (N > 16: FDT read, FD and the 4-byte FD
+                    timestamp offsets written; 10N with HGE_FDT16=1 above N = 128);
       k_witness_la   8N^2 per round (frontier rows read, transposed rows written);
       k_la16_rows_runs 6N/event (N > 32: LA16 read, the FDT runs written; 4N with
                     HGE_FDT16=1 above N = 128);
@@ -87,7 +87,7 @@ def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
     if name == "k_witness_la":
         return 8 * n * n * rounds
     per_event = {"k_la_sweep": 12 * n, "k_la_clear": 4 * n, "k_transpose": 16 * n if n <= 16 else 8 * n,
-                 "k_fd_transpose_ts": (14 if os.environ.get("HGE_FDT16") == "1" and n > 128 else 16) * n,
+                 "k_fd_transpose_ts": (10 if os.environ.get("HGE_FDT16") == "1" and n > 128 else 12) * n,
                  "k_fdt_clear": 4 * n, "k_fdt_runs": 8 * n, "k_fss": 8 * n,
                  "k_rounds_walk": 4 * n, "k_rounds_coop": 4 * n, "k_rounds_coop_spec": 4 * n,
                  "k_walk_spec": 4 * n, "k_rounds_fss": 4 * n, "k_rounds_direct": 4 * n,

@@ -129,3 +129,19 @@ def test_stale_other_parents_in_windows(n, events, G, kernel, monkeypatch):
             np.testing.assert_array_equal(np.asarray(gfd, np.int64), fd(x))
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("n,events", [(32, 4000), (64, 6000)])
+def test_timestamp_offsets_outside_int32(n, events):
+    """The wide median reads the FD timestamps as int32 offsets from each event's own
+    timestamp; rows whose offsets do not fit (clocks 3 s apart every 500 events here)
+    are flagged per 64-column tile and gathered exactly.  Consensus timestamps and
+    order vs the oracle (MedianTimestamp, hashgraph.go:762-770)."""
+    from babble_amd.engine import Engine
+    dag = random_gossip(n, events, seed=90 + n)
+    dag["ts"] = dag["ts"] + (np.arange(events, dtype=np.int64) // 500) * 3_000_000_000
+    eng = Engine(n, 1 << 14)
+    try:
+        run_case(eng, dag, n)
+    finally:
+        eng.close()
