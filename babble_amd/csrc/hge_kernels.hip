@@ -887,7 +887,7 @@ __global__ void k_fame_decide(Tables t, const int32_t* pr_round, const int32_t* 
     for (int w = 0; w < NWT; w++) votes[w] = 0;
     // the witness rows are read in chunks of DC slots with every load of a chunk
     // in flight before the first use (the d loops are latency chains otherwise)
-    constexpr int DC = 16;
+    constexpr int DC = WP ? 8 : 16;  // WP: the chunk lives in SGPRs (16 spilled 119 of them)
     // diff == 1: vote = See(y, x)
     for (int d0 = 0; d0 < N; d0 += DC) {
       int ys[DC];
