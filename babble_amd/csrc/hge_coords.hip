@@ -300,7 +300,9 @@ __global__ void __launch_bounds__(256) k_la16_rows_runs(Tables t, FT* FDT, const
     }
   }
   __syncthreads();
-  // runs: wave ty takes columns ty, ty + 4, ...; lane = position k = p0 + tx
+  // runs: wave ty takes columns ty, ty + 4, ...; lane = position k = p0 + tx.  (Writing
+  // each column's contiguous q range with consecutive lanes, bisecting for the event
+  // of each q, measured no faster: 7.4 vs 6.7-7.3 ms at 256/10M.)
   const int k = p0 + tx;
   const bool isnew = k >= oj && k < lj;
   const bool lasttile = lj - 1 < p0 + 64;

@@ -161,7 +161,6 @@ __global__ void __launch_bounds__(1024) k_la_win(Tables t, const int4* plan, int
   constexpr int TPE = RWW / WPT;         // = 32
   constexpr int SL = 1024 / TPE;         // events per read/write phase (32)
   constexpr int MAXI = (LW_K + SL - 1) / SL;
-  constexpr int RW = TPE < 64 ? TPE : 64;  // lanes of one event inside a wave
   static_assert(TPE == 32, "half a wave per event");
   __shared__ uint32_t s_st[NPOW * RWW] __attribute__((aligned(16)));  // head rows [chain][word]
   __shared__ int s_hp[NPOW], s_ol[NPOW];
@@ -410,7 +409,6 @@ __global__ void __launch_bounds__(64) k_la_wave(Tables t, const int4* plan, int6
     wp[q] = c < N ? wpos[(size_t)w * N + c] : 0;
     ol[q] = c < N ? olen[c] : 0;
   }
-#pragma unroll
   for (int c0 = 0; c0 < NPOW; c0 += 16) {
     if (c0 >= N) break;
     uint32_t v[16];

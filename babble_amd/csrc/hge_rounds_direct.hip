@@ -409,12 +409,14 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
   // (6 = probes; 7, 8 = member-load issue and arrival inside section 0)
   uint64_t st_t = 0, st_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   const bool stamping = kDirStamps && dbg && blockIdx.x == 0 && threadIdx.x == 0;
-#define DSTAMP(k)                             \
-  if (stamping) {                             \
-    const uint64_t now_ = stamp();            \
-    if ((k) >= 0) st_acc[(k)] += now_ - st_t; \
-    st_t = now_;                              \
+#define DSTAMP(k)                  \
+  if (stamping) {                  \
+    const uint64_t now_ = stamp(); \
+    st_acc[(k)] += now_ - st_t;    \
+    st_t = now_;                   \
   }
+#define DSTAMP_START                \
+  if (stamping) st_t = stamp();
   __shared__ DirLDS<BS, NPOW> L;
   const int N = t.N, NW = t.NW;
   const int c = blockIdx.x, tid = threadIdx.x;
@@ -453,7 +455,7 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
       }
       break;
     }
-    DSTAMP(-1);
+    DSTAMP_START
     uint32_t mw[G::CW];
     if (r == rlo) dir_members_fd<BS, NPOW>(t, d, part, d < N ? L.sP[d] : INF32, mw);
     else dir_members_mb<BS, NPOW>(mbp[r & 1], mw);
@@ -598,6 +600,7 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
     dbg[10] += L.sdbg[1];
   }
 #undef DSTAMP
+#undef DSTAMP_START
 }
 
 template __global__ void k_rounds_direct<1024, 64>(Tables, const int32_t*, const int32_t*, int32_t*, int, int,
