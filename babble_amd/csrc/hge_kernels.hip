@@ -1457,6 +1457,59 @@ __global__ void k_round_received(Tables t, const int32_t* cand, int ncand, const
   cts_out[q] = med;
 }
 
+// The same select over 32-bit order-preserving images (int32 timestamp offsets ^
+// 0x80000000): one 32-bit reduction, no 64-bit arithmetic.  Returns the image.
+template <int VPL>
+__device__ __forceinline__ uint32_t wave_upper_median32(const uint32_t (&v)[VPL], const bool (&in)[VPL]) {
+  int n = 0;
+  uint32_t mn = ~0u, mx = 0;
+#pragma unroll
+  for (int k = 0; k < VPL; k++) {
+    n += __popcll(__ballot(in[k]));
+    if (in[k]) {
+      mn = min(mn, v[k]);
+      mx = max(mx, v[k]);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+  }
+  mn = __builtin_amdgcn_readfirstlane(mn);
+  int kk = n / 2;  // 0-based rank of the upper median
+  // the live set is implicit: the values whose bits above b equal the prefix so far.
+  // A value not in the list is all ones (never below mx - mn <= 2^32 - 2 in the
+  // zero branch), so the count of "bit b = 0" among the live is one compare per value.
+  uint32_t vr[VPL];
+#pragma unroll
+  for (int k = 0; k < VPL; k++) vr[k] = in[k] ? v[k] - mn : ~0u;
+  const uint32_t span = __builtin_amdgcn_readfirstlane(mx - mn);
+  uint32_t pre = 0;
+  int nlive = n;
+  for (int b = span ? 31 - __builtin_clz(span) : -1; b >= 0; b--) {
+    const uint32_t p0 = pre >> b;  // the prefix with bit b = 0
+    int c0 = 0;
+#pragma unroll
+    for (int k = 0; k < VPL; k++) c0 += __popcll(__ballot((vr[k] >> b) == p0));
+    if (kk >= c0) {
+      kk -= c0;
+      pre |= 1u << b;
+      nlive -= c0;
+    } else {
+      nlive = c0;
+    }
+    if (nlive == 1) {  // the one live value (an in value: the in-mask excludes ~0u here)
+      const uint32_t pb = pre >> b;
+#pragma unroll
+      for (int k = 0; k < VPL; k++) {
+        const uint64_t m = __ballot(in[k] && (vr[k] >> b) == pb);
+        if (m) return mn + (uint32_t)__builtin_amdgcn_readlane((int)vr[k], (int)__builtin_ctzll(m));
+      }
+    }
+  }
+  return mn + pre;
+}
+
 // Upper median (element len/2 of the sorted list, MedianTimestamp,
 // hashgraph.go:762-770) of the wave's values v[k] where in[k]: a bitwise radix
 // select over the order-preserving uint64 image (ts ^ sign bit), skipping the
@@ -1601,7 +1654,10 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
                                                      int64_t* cts_out) {
   // MW_E events per wave (candidates q0 + e * nw, nw = the grid's wave count): all
   // their loads are in flight together before the first select
-  constexpr int MW_E = 2;
+#ifndef HGE_MW_E
+#define HGE_MW_E 2
+#endif
+  constexpr int MW_E = HGE_MW_E;
   const int nw = gridDim.x * 4;
   const int q0 = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -1610,7 +1666,10 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
   bool live[MW_E];
   uint64_t fw[MW_E][VPL];
   int th[MW_E][VPL];
-  int64_t ts[MW_E][VPL];
+  int64_t ts[MW_E][VPL];   // exact timestamps (wide rows only)
+  int32_t off[MW_E][VPL];  // offsets from x's own timestamp
+  int64_t bse[MW_E];
+  int wde[MW_E];
 #pragma unroll
   for (int e = 0; e < MW_E; e++) {
     const int q = q0 + e * nw;
@@ -1636,15 +1695,16 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
     } else {
       for (int k = 0; k < NT; k++) wide |= t.FDTW[rw * NT + k];
     }
-    const int64_t base = t.ts[x];
+    bse[e] = t.ts[x];
+    wde[e] = __builtin_amdgcn_readfirstlane(wide);
 #pragma unroll
     for (int k = 0; k < VPL; k++) {
       const int dd = min(lane + 64 * k, N - 1);
       fw[e][k] = seg_fws[(size_t)sg * NW + (k < NW ? k : 0)];
       th[e][k] = thr[dd];
-      ts[e][k] = base + (int64_t)tdr[dd];
+      off[e][k] = tdr[dd];
     }
-    if (__builtin_amdgcn_readfirstlane(wide)) {
+    if (wde[e]) {
 #pragma unroll
       for (int k = 0; k < VPL; k++) {
         const int dd = min(lane + 64 * k, N - 1);
@@ -1655,15 +1715,28 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
   }
 #pragma unroll
   for (int e = 0; e < MW_E; e++) {
-    uint64_t v[VPL];
     bool in[VPL];
 #pragma unroll
     for (int k = 0; k < VPL; k++) {
       const int d = lane + 64 * k;
       in[k] = d < N && ((fw[e][k] >> (d & 63)) & 1ull) && th[e][k] >= ixe[e];
-      v[k] = in[k] ? ((uint64_t)ts[e][k] ^ 0x8000000000000000ull) : ~0ull;
     }
-    const int64_t med = wave_upper_median<VPL>(v, in);
+    int64_t med;
+    if (!wde[e]) {  // int32 offsets: the median of (base + o) is base + the median of o
+      uint32_t v[VPL];
+#pragma unroll
+      for (int k = 0; k < VPL; k++) v[k] = in[k] ? ((uint32_t)off[e][k] ^ 0x80000000u) : ~0u;
+#ifdef HGE_MED_NOSEL  // diagnostics: loads and flags only
+      med = bse[e] + (int64_t)(int32_t)(__builtin_amdgcn_readfirstlane(v[0]) ^ 0x80000000u);
+#else
+      med = bse[e] + (int64_t)(int32_t)(wave_upper_median32<VPL>(v, in) ^ 0x80000000u);
+#endif
+    } else {
+      uint64_t v[VPL];
+#pragma unroll
+      for (int k = 0; k < VPL; k++) v[k] = in[k] ? ((uint64_t)ts[e][k] ^ 0x8000000000000000ull) : ~0ull;
+      med = wave_upper_median<VPL>(v, in);
+    }
     if (lane == 0 && live[e]) cts_out[qe[e]] = med;
   }
 }

@@ -145,3 +145,25 @@ def test_timestamp_offsets_outside_int32(n, events):
         run_case(eng, dag, n)
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("n,events,kind", [(64, 5000, "spread"), (256, 3000, "spread"),
+                                           (64, 5000, "ties"), (128, 4000, "ties")])
+def test_median_select_extremes(n, events, kind):
+    """The 32-bit select on timestamp offsets at its edges: timestamps out of order
+    and spread over +-2^30 ns (offsets up to +-(2^31 - 2): spans close to 2^32, the
+    order-preserving images near 1 and 2^32 - 1), and long runs of equal timestamps
+    (ties: the select runs every bit without isolating a single value).  Consensus
+    timestamps and order vs the oracle (MedianTimestamp, hashgraph.go:762-770)."""
+    from babble_amd.engine import Engine
+    dag = random_gossip(n, events, seed=300 + n)
+    if kind == "spread":
+        rng = np.random.default_rng(n)
+        dag["ts"] = 1_700_000_000_000_000_000 + rng.integers(-(1 << 30) + 1, 1 << 30, events, dtype=np.int64)
+    else:
+        dag["ts"] = 1_700_000_000_000_000_000 + (np.arange(events, dtype=np.int64) // 97) * 1000
+    eng = Engine(n, 1 << 14)
+    try:
+        run_case(eng, dag, n)
+    finally:
+        eng.close()
