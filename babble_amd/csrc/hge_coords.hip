@@ -377,8 +377,7 @@ template <typename FT>
 __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const FT* FDT, const int32_t* plo,
                                                          const int32_t* len) {
   __shared__ int32_t tile[64][65];
-  __shared__ int64_t tts[64][65];
-  __shared__ int64_t rts[64];  // the tile's row events' own timestamps
+  __shared__ int32_t toff[64][65];  // the offsets (INT32_MIN: outside int32)
   const int N = t.N;
   const size_t ccap = t.ccap;
   // grid (chain, column tile, position tiles): consecutive workgroups take the same
@@ -390,30 +389,40 @@ __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const FT* FDT
   const int c0 = blockIdx.y * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
   for (int p0 = plo[a] + blockIdx.z * 64; p0 < pend; p0 += gridDim.z * 64) {
-    // all 16 FDT loads of a thread in flight, then all 16 timestamp gathers
-    int kv[16];
+    // read phase: lane tx walks row q = p0 + tx (its own timestamp is one load), all
+    // 16 FDT loads of a thread in flight, then all 16 timestamp gathers
+    const int64_t own = t.tsch[(size_t)a * ccap + min(p0 + tx, pend - 1)];
+#ifndef HGE_FDTS_CH
+#define HGE_FDTS_CH 16
+#endif
+    constexpr int CH = HGE_FDTS_CH;  // rows in flight per thread
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
-      const int jj = c0 + ty + 4 * i, q = p0 + tx;
-      if (jj < N && q < pend) {
-        const FT f = FDT[((size_t)jj * N + a) * ccap + q];
-        kv[i] = (sizeof(FT) == 2 && f == (FT)0xFFFF) ? INF32 : (int)f;
-      } else {
-        kv[i] = INF32;
+    for (int h = 0; h < 16; h += CH) {
+      int kv[CH];
+#pragma unroll
+      for (int i = 0; i < CH; i++) {
+        const int jj = c0 + ty + 4 * (h + i), q = p0 + tx;
+        if (jj < N && q < pend) {
+          const FT f = FDT[((size_t)jj * N + a) * ccap + q];
+          kv[i] = (sizeof(FT) == 2 && f == (FT)0xFFFF) ? INF32 : (int)f;
+        } else {
+          kv[i] = INF32;
+        }
+      }
+      int64_t tv[CH];
+#pragma unroll
+      for (int i = 0; i < CH; i++) {
+        const int jj = c0 + ty + 4 * (h + i);
+        tv[i] = t.tsch[(size_t)(jj < N ? jj : 0) * ccap + (kv[i] != INF32 ? kv[i] : 0)];
+      }
+#pragma unroll
+      for (int i = 0; i < CH; i++) {
+        tile[ty + 4 * (h + i)][tx] = kv[i];
+        const int64_t d = tv[i] - own;  // offset from the row event's own timestamp
+        const bool esc = d < -(int64_t)INT32_MAX || d > (int64_t)INT32_MAX;
+        toff[ty + 4 * (h + i)][tx] = kv[i] == INF32 ? 0 : (esc ? INT32_MIN : (int32_t)d);
       }
     }
-    int64_t tv[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-      const int jj = c0 + ty + 4 * i;
-      tv[i] = t.tsch[(size_t)(jj < N ? jj : 0) * ccap + (kv[i] != INF32 ? kv[i] : 0)];
-    }
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-      tile[ty + 4 * i][tx] = kv[i];
-      tts[ty + 4 * i][tx] = kv[i] != INF32 ? tv[i] : 0;
-    }
-    if (ty == 0) rts[tx] = t.tsch[(size_t)a * ccap + min(p0 + tx, pend - 1)];
     __syncthreads();
     const int NT = (N + 63) >> 6;
     for (int r = ty; r < 64; r += 4) {  // wave ty writes rows r: the 64 columns of one row each time
@@ -421,14 +430,9 @@ __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const FT* FDT
       bool esc = false;
       if (q < pend && jj < N) {
         const size_t o = rowoff(t, a, q) + jj;
-        const int k = tile[tx][r];
-        int32_t dv = 0;
-        if (k != INF32) {  // offset from the row event's own timestamp
-          const int64_t d = tts[tx][r] - rts[r];
-          esc = d < -(int64_t)INT32_MAX || d > (int64_t)INT32_MAX;
-          dv = esc ? INT32_MIN : (int32_t)d;
-        }
-        t.FD[o] = k;
+        const int32_t dv = toff[tx][r];
+        esc = dv == INT32_MIN;  // a real offset lies in [-INT32_MAX, INT32_MAX]
+        t.FD[o] = tile[tx][r];
         t.FDTD[o] = dv;
       }
       const bool any = __ballot(esc) != 0;
