@@ -881,7 +881,9 @@ __global__ void k_fame_decide(Tables t, const int32_t* pr_round, const int32_t* 
   const int R = Rc[c];
   uint8_t out = 0;
   const int x = t.W[(size_t)i * N + xd];
-  if (x >= 0 && x < n) {
+  // R <= i + 2: no round j in [i + 2, R) votes, so no decision (the See votes of
+  // round i + 1 are not even read)
+  if (x >= 0 && x < n && R > i + 2) {
     uint64_t votes[NWT], cur[NWT];
 #pragma unroll
     for (int w = 0; w < NWT; w++) votes[w] = 0;
