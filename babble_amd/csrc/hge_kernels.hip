@@ -1287,7 +1287,8 @@ __global__ void __launch_bounds__(256) k_seg_theta_wide(Tables t, const int32_t*
                                                         const int32_t* segoff, const int32_t* segcnt,
                                                         int nr, const uint64_t* seg_fws,
                                                         int32_t* theta) {
-  __shared__ uint16_t sv[256 * 256];  // [famous k][cx]
+  // [famous k / 8][cx]: 8 values of a column per 16 bytes, as uint16 pairs
+  __shared__ uint4 sv[32][256];
   __shared__ int s_row[256];
   __shared__ int s_nf;
   const int N = t.N;
@@ -1323,22 +1324,56 @@ __global__ void __launch_bounds__(256) k_seg_theta_wide(Tables t, const int32_t*
       const int cx = tid;
       if (cx < N) {
         // the column's values span a few dozen positions (the famous witnesses of one
-        // round see chain cx up to about the same point): bisect [min, max], not [0, 65535]
+        // round see chain cx up to about the same point): bisect [min, max], not [0, 65535].
+        // Values are LA + 1 (0: no ancestor on chain cx); the padding past nf is 0,
+        // which no probe value mid >= 1 counts.
         int vmin = 65535, vmax = 0;
-        for (int k = 0; k < nf; k++) {
-          const int v = la_row(t, (size_t)s_row[k], cx) + 1;
-          sv[k * 256 + cx] = (uint16_t)v;
-          vmin = min(vmin, v);
-          vmax = max(vmax, v);
+        for (int k0 = 0; k0 < nf; k0 += 8) {
+          uint32_t w[4];
+#pragma unroll
+          for (int u = 0; u < 8; u += 2) {
+            const int a = k0 + u < nf ? la_row(t, (size_t)s_row[k0 + u], cx) + 1 : -1;
+            const int b = k0 + u + 1 < nf ? la_row(t, (size_t)s_row[k0 + u + 1], cx) + 1 : -1;
+            if (a >= 0) { vmin = min(vmin, a); vmax = max(vmax, a); }
+            if (b >= 0) { vmin = min(vmin, b); vmax = max(vmax, b); }
+            w[u >> 1] = (uint32_t)max(a, 0) | ((uint32_t)max(b, 0) << 16);
+          }
+          sv[k0 >> 3][cx] = make_uint4(w[0], w[1], w[2], w[3]);
         }
+        if (((nf + 7) >> 3) & 1) sv[(nf + 7) >> 3][cx] = make_uint4(0, 0, 0, 0);  // even group count
         int th = (int)0x80000000;
         if (nf > 0) {
           const int kk = nf / 2 + 1;  // k-th largest = largest v with count(>= v) >= kk
+          const int ng = (nf + 7) >> 3;
           int lo = vmin, hi = vmax;
           while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
-            int c2 = 0;
-            for (int k = 0; k < nf; k++) c2 += sv[k * 256 + cx] >= mid ? 1 : 0;
+            // v >= mid <=> v -sat (mid - 1) != 0: packed saturating subtract, min 1, add
+            // (the same three packed ops as the strongly-see probe, hge_rounds_direct.hip)
+            const uint32_t m1 = (uint32_t)(mid - 1) * 0x00010001u, one = 0x00010001u;
+            uint32_t acc0 = 0, acc1 = 0;
+            for (int g = 0; g < ng; g += 2) {  // two groups per step (ng padded to even)
+#pragma unroll
+              for (int h = 0; h < 2; h++) {
+                const uint4 x = sv[g + h][cx];
+                uint32_t d0, d1, d2, d3;
+                asm("v_pk_sub_u16 %0, %6, %10 clamp\n\t"
+                    "v_pk_sub_u16 %1, %7, %10 clamp\n\t"
+                    "v_pk_sub_u16 %2, %8, %10 clamp\n\t"
+                    "v_pk_sub_u16 %3, %9, %10 clamp\n\t"
+                    "v_pk_min_u16 %0, %0, %11\n\t"
+                    "v_pk_min_u16 %1, %1, %11\n\t"
+                    "v_pk_min_u16 %2, %2, %11\n\t"
+                    "v_pk_min_u16 %3, %3, %11\n\t"
+                    "v_pk_add_u16 %4, %4, %0\n\t"
+                    "v_pk_add_u16 %5, %5, %1\n\t"
+                    "v_pk_add_u16 %4, %4, %2\n\t"
+                    "v_pk_add_u16 %5, %5, %3"
+                    : "=&v"(d0), "=&v"(d1), "=&v"(d2), "=&v"(d3), "+v"(acc0), "+v"(acc1)
+                    : "v"(x.x), "v"(x.y), "v"(x.z), "v"(x.w), "v"(m1), "v"(one));
+              }
+            }
+            const int c2 = (int)(acc0 & 0xFFFFu) + (int)(acc0 >> 16) + (int)(acc1 & 0xFFFFu) + (int)(acc1 >> 16);
             if (c2 >= kk) lo = mid;
             else hi = mid - 1;
           }
