@@ -1550,7 +1550,7 @@ struct hge_engine {
         KLAUNCH(k_bucket_keys, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand, s_recv.p,
                 s_rr.p, s_cts.p, s_bpos.p, k1, d_rr.p, d_cts.p,
                 (unsigned long long*)(s_out.p + o_tx));
-        // buckets of 513 .. BIG_SORT keys whole in LDS (HGE_BIG_SORT=0: all through k_bucket_sort)
+        // buckets of 513 .. 2 * BIG_SORT keys in LDS (HGE_BIG_SORT=0: all through k_bucket_sort)
         static const bool BIGS = !(getenv("HGE_BIG_SORT") && atoi(getenv("HGE_BIG_SORT")) == 0);
         KLAUNCH(k_bucket_sort, dim3(std::min(ncalls, 2048)), dim3(256), 0, st,
                 (const int32_t*)s_bpos.p, (const int32_t*)o_cc, (const int32_t*)blist,
@@ -1558,7 +1558,7 @@ struct hge_engine {
         if (BIGS)
           KLAUNCH(k_bucket_sort_big, dim3(std::min(ncalls, n_cu())), dim3(1024), 0, st,
                   (const int32_t*)s_bpos.p, (const int32_t*)o_cc, (const int32_t*)blist,
-                  (const int32_t*)nblist, (const OKey*)k1, o_ids);
+                  (const int32_t*)nblist, (const OKey*)k1, k2, o_ids);
         // new undetermined list (in candidate order)
         scan_large(s_fund.p, s_upos.p, ncand, o_cnt + 1);
         // scatter into the spare list (same capacity) and swap: no device copy

@@ -2008,7 +2008,7 @@ __device__ void bucket_sort_one(int b, const int32_t* bend, const int32_t* bcnt,
   constexpr int CH = 512;  // keys per LDS chunk
   __shared__ SortChunk<CH> sc;
   const int n = bcnt[b];
-  if (n == 0 || (skip_big && n > CH && n <= BIG_SORT)) return;
+  if (n == 0 || (skip_big && n > CH && n <= 2 * BIG_SORT)) return;
   const int start = bend[b] - n;
   const int tid = threadIdx.x, T = blockDim.x;
   if (n == 1) {
@@ -2024,7 +2024,8 @@ __device__ void bucket_sort_one(int b, const int32_t* bend, const int32_t* bcnt,
     for (int i = tid; i < n; i += T) ids_out[start + i] = (int32_t)sc.id[sc.ix[i]];
     return;
   }
-  // large bucket: sorted CH-key chunks, then pairwise merges (ping-pong)
+  // large bucket (past 2 * BIG_SORT, or every one with HGE_BIG_SORT=0): sorted
+  // CH-key chunks, then pairwise merges (ping-pong)
   OKey* src = keys + start;
   OKey* dst = tmp + start;
   for (int c0 = 0; c0 < n; c0 += CH) {
@@ -2076,57 +2077,94 @@ __global__ void __launch_bounds__(256) k_bucket_sort(const int32_t* bend, const 
 // those bits are ordered by the full key from HBM.  k_bucket_sort's 512-key
 // chunks + pairwise merges through global scratch moved ~50x the keys' bytes for
 // such buckets (25 GB per 256/10M replay, rocprofv3 PMC).
+// bitonic index sort of K[0, n) (n <= BIG_SORT) in LDS by (rr, cts, the top 32 bits
+// of S), then the full key from HBM on ties; ix[0, n) = the sorted local indices
+__device__ void big_bitonic(const OKey* K, int n, uint64_t* sb, uint32_t* sr, uint32_t* ss, uint16_t* ix) {
+  const int tid = threadIdx.x, T = blockDim.x;
+  int P = 1024;
+  while (P < n) P <<= 1;
+  for (int i = tid; i < P; i += T) {
+    if (i < n) {
+      const OKey k = K[i];
+      sr[i] = (uint32_t)k.a;  // rr (the call is the bucket's)
+      sb[i] = k.b;
+      ss[i] = (uint32_t)(k.s0 >> 32);
+    } else {
+      sr[i] = 0xFFFFFFFFu;
+      sb[i] = ~0ull;
+      ss[i] = 0xFFFFFFFFu;
+    }
+    ix[i] = (uint16_t)i;
+  }
+  __syncthreads();
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < P / 2; i += T) {
+        const int lo = 2 * stride * (i / stride) + (i % stride);
+        const int hi = lo + stride;
+        const bool up = ((lo & size) == 0);
+        const int x = ix[lo], y = ix[hi];
+        bool yl;  // key y < key x
+        if (sr[x] != sr[y]) yl = sr[y] < sr[x];
+        else if (sb[x] != sb[y]) yl = sb[y] < sb[x];
+        else if (ss[x] != ss[y]) yl = ss[y] < ss[x];
+        else if (x >= n || y >= n) yl = y < x;  // padding (only padding ties padding)
+        else yl = okless(K[y], K[x]);          // equal leading bits: the full key
+        if (yl == up) {
+          ix[lo] = (uint16_t)y;
+          ix[hi] = (uint16_t)x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Buckets of BIG_SORT + 1 .. 2 * BIG_SORT keys (a call that receives more than one
+// round's worth: 33 calls of 8-16k keys at 256/10M) are two halves sorted in LDS
+// the same way, then one merge-path pass over their index lists (scratch: the
+// bucket's slice of tmp), each thread placing nb / 1024 outputs from its co-rank.
 __global__ void __launch_bounds__(1024) k_bucket_sort_big(const int32_t* bend, const int32_t* bcnt,
                                                           const int32_t* list, const int32_t* nlist,
-                                                          const OKey* keys, int32_t* ids_out) {
+                                                          const OKey* keys, OKey* tmp, int32_t* ids_out) {
   __shared__ uint64_t sb[BIG_SORT];
   __shared__ uint32_t sr[BIG_SORT], ss[BIG_SORT];
   __shared__ uint16_t ix[BIG_SORT];
   const int tid = threadIdx.x, T = blockDim.x;
   for (int li = blockIdx.x; li < *nlist; li += gridDim.x) {
     const int b = list[li];
-    const int n = bcnt[b];
-    if (n <= 512 || n > BIG_SORT) continue;  // block-uniform
-    const OKey* K = keys + (bend[b] - n);
-    int P = 1024;
-    while (P < n) P <<= 1;
-    for (int i = tid; i < P; i += T) {
-      if (i < n) {
-        const OKey k = K[i];
-        sr[i] = (uint32_t)k.a;  // rr (the call is the bucket's)
-        sb[i] = k.b;
-        ss[i] = (uint32_t)(k.s0 >> 32);
-      } else {
-        sr[i] = 0xFFFFFFFFu;
-        sb[i] = ~0ull;
-        ss[i] = 0xFFFFFFFFu;
-      }
-      ix[i] = (uint16_t)i;
+    const int nb = bcnt[b];
+    if (nb <= 512 || nb > 2 * BIG_SORT) continue;  // block-uniform
+    const OKey* K = keys + (bend[b] - nb);
+    int32_t* out = ids_out + (bend[b] - nb);
+    if (nb <= BIG_SORT) {
+      big_bitonic(K, nb, sb, sr, ss, ix);
+      for (int i = tid; i < nb; i += T) out[i] = (int32_t)K[ix[i]].id;
+      __syncthreads();
+      continue;
     }
+    int32_t* S = (int32_t*)(tmp + (bend[b] - nb));  // 4 of the 48 scratch bytes per key
+    const int na = (nb + 1) >> 1, nbb = nb - na;
+    big_bitonic(K, na, sb, sr, ss, ix);
+    for (int i = tid; i < na; i += T) S[i] = ix[i];
     __syncthreads();
-    for (int size = 2; size <= P; size <<= 1) {
-      for (int stride = size >> 1; stride > 0; stride >>= 1) {
-        for (int i = tid; i < P / 2; i += T) {
-          const int lo = 2 * stride * (i / stride) + (i % stride);
-          const int hi = lo + stride;
-          const bool up = ((lo & size) == 0);
-          const int x = ix[lo], y = ix[hi];
-          bool yl;  // key y < key x
-          if (sr[x] != sr[y]) yl = sr[y] < sr[x];
-          else if (sb[x] != sb[y]) yl = sb[y] < sb[x];
-          else if (ss[x] != ss[y]) yl = ss[y] < ss[x];
-          else if (x >= n || y >= n) yl = y < x;  // padding (only padding ties padding)
-          else yl = okless(K[y], K[x]);          // equal leading bits: the full key
-          if (yl == up) {
-            ix[lo] = (uint16_t)y;
-            ix[hi] = (uint16_t)x;
-          }
-        }
-        __syncthreads();
-      }
+    big_bitonic(K + na, nbb, sb, sr, ss, ix);
+    for (int i = tid; i < nbb; i += T) S[na + i] = na + ix[i];
+    __syncthreads();
+    const int32_t* A = S;
+    const int32_t* B = S + na;
+    const int k0 = (int)((int64_t)nb * tid / T), k1 = (int)((int64_t)nb * (tid + 1) / T);
+    int lo = max(0, k0 - nbb), hi = min(k0, na);
+    while (lo < hi) {  // co-rank: take i from A, k0 - i from B
+      const int i = (lo + hi) >> 1;
+      if (okless(K[A[i]], K[B[k0 - i - 1]])) lo = i + 1;
+      else hi = i;
     }
-    int32_t* out = ids_out + (bend[b] - n);
-    for (int i = tid; i < n; i += T) out[i] = (int32_t)K[ix[i]].id;
+    int i = lo, j = k0 - lo;
+    for (int k = k0; k < k1; k++) {
+      const bool takeA = j >= nbb || (i < na && okless(K[A[i]], K[B[j]]));
+      out[k] = (int32_t)K[takeA ? A[i++] : B[j++]].id;
+    }
     __syncthreads();
   }
 }
