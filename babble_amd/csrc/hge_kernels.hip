@@ -1680,7 +1680,9 @@ __global__ void __launch_bounds__(256) k_witness_la(Tables t, int rr_lo) {
 // received event.  Lane l holds the timestamps of the famous witnesses
 // d = l, l+64, ... that see x (OSA(w, x) = FD[x][cw], its timestamp offset FDTD[x][cw]);
 // the upper median (element len/2 of the sorted list) is found by a bitwise
-// radix select over the order-preserving uint64 image of the int64 timestamps.
+// radix select over the order-preserving uint32 image of the int32 offsets
+// (wave_upper_median32; base + the median offset), or of the int64 timestamps
+// for a row flagged in FDTW (wave_upper_median).
 // Every per-witness input is a coalesced row: the "sees x" thresholds
 // WLA[rr][cx][.] (k_witness_la) and the timestamp offsets FDTD[x][.] (k_fd_transpose_ts),
 // instead of 2N scattered gathers per event.
