@@ -1691,10 +1691,11 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
                                                      const int32_t* recv_call, const int32_t* rr_in,
                                                      const int32_t* bseg, const uint64_t* seg_fws,
                                                      int64_t* cts_out) {
-  // MW_E events per wave (candidates q0 + e * nw, nw = the grid's wave count): all
+  // MW_E events per wave (candidates q0 + e * nw, nw = the grid's wave count; 1 measured
+  // fastest once the select became cheap: 6.36 vs 6.62 ms at 2, 8.19 at 3): all
   // their loads are in flight together before the first select
 #ifndef HGE_MW_E
-#define HGE_MW_E 2
+#define HGE_MW_E 1
 #endif
   constexpr int MW_E = HGE_MW_E;
   const int nw = gridDim.x * 4;
