@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -974,11 +975,38 @@ struct hge_engine {
   // hipLaunchCooperativeKernel puts the work on a separate device queue whose
   // teardown at process exit crashed under rocprofv3 (profiles/r02_exit_segv.md).
   // HGE_COOP_LAUNCH=1 restores the cooperative launch.
+  // Every such launch first checks, for the exact kernel instantiation and block
+  // size, that the whole grid fits on the device at once; a grid that cannot be
+  // co-resident is refused before anything is written.  The caller holds
+  // frontier_lock(): two of these grids on one device (two wide engines driven
+  // by different host threads) could each hold part of the CUs and wait on each
+  // other's missing workgroups, so one process runs them one at a time.  (Grids of
+  // other processes on the same device are not covered: wide engines need the
+  // device to themselves)
+  std::vector<std::pair<std::pair<const void*, int>, int>> resident_nb;
   hipError_t launch_resident(const void* fn, dim3 grid, dim3 block, void** args) {
+    const int bs = (int)(block.x * block.y * block.z);
+    int nb = -1;
+    for (auto& e : resident_nb)
+      if (e.first.first == fn && e.first.second == bs) nb = e.second;
+    if (nb < 0) {
+      HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, bs, 0));
+      resident_nb.push_back({{fn, bs}, nb});
+    }
+    const int64_t blocks = (int64_t)grid.x * grid.y * grid.z;
+    if ((int64_t)nb * n_cu() < blocks)
+      throw EngineError(HGE_ERR_DEVICE, "frontier grid of " + std::to_string(blocks) + " workgroups x " +
+                                            std::to_string(bs) + " threads cannot be co-resident (" +
+                                            std::to_string(nb) + " per CU x " + std::to_string(n_cu()) + " CUs)");
     static const bool coop = getenv("HGE_COOP_LAUNCH") && atoi(getenv("HGE_COOP_LAUNCH")) == 1;
     if (coop) return hipLaunchCooperativeKernel(fn, grid, block, args, 0, st);
     return hipLaunchKernel(fn, grid, block, args, 0, st);
   }
+  static std::mutex& frontier_mutex(int dev) {
+    static std::mutex m[64];
+    return m[dev & 63];
+  }
+  std::unique_lock<std::mutex> frontier_lock() { return std::unique_lock<std::mutex>(frontier_mutex(device)); }
 
   // Wide rounds step: strongly-see tiles on the coordinate rows
   // (hge_rounds_direct.hip) for N % 4 == 0, else the FDT-gather selection of
@@ -992,6 +1020,7 @@ struct hge_engine {
 
   // rounds of a wide hashgraph: cooperative frontier kernel (hge_rounds_coop.hip)
   void rounds_coop(bool fresh) {
+    auto lk = frontier_lock();  // until the frontier grids below have drained (last readback)
     Tables t = tables();
     s_fst.need(N + 1);
     KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p);
@@ -1982,7 +2011,12 @@ int hge_split_begin(hge_engine* h) {
 }
 
 int hge_frontier_guess(hge_engine* h, int32_t part, int32_t nparts, int32_t* start_out) {
-  if (!start_out || nparts < 1 || part < 0 || part >= nparts) return HGE_ERR_ARG;
+  if (!h) return HGE_ERR_ARG;
+  GUARD_BEGIN
+  if (!start_out || nparts < 1 || part < 0 || part >= nparts) {
+    h->err = "hge_frontier_guess: bad argument";
+    return HGE_ERR_ARG;
+  }
   // part 0: the true first frontier (every chain's first event); part p: the time
   // cut at event p * E / nparts (the first event of each chain inserted at or after it)
   const int64_t T = h->n_events * (int64_t)part / nparts;
@@ -1992,6 +2026,7 @@ int hge_frontier_guess(hge_engine* h, int32_t part, int32_t nparts, int32_t* sta
     start_out[c] = k < ch.size() ? (int32_t)k : INF32;
   }
   return HGE_OK;
+  GUARD_END(h)
 }
 
 int hge_frontier_walk(hge_engine* h, const int32_t* start, const int32_t* stopcut, int32_t extra,
@@ -2018,6 +2053,7 @@ int hge_frontier_walk(hge_engine* h, const int32_t* start, const int32_t* stopcu
   HIPCHK(hipMemsetAsync(h->s_gran.p, 0, 16 * (size_t)N, h->st));
   const int npow = N <= 64 ? 64 : N <= 128 ? 128 : 256;
   h->s_mb.need((size_t)npow * npow);
+  auto lk = h->frontier_lock();  // until the walk has drained (the sync below)
   Tables t = h->tables();
   const int32_t* olen = h->k_len;
   const int32_t* len = h->k_len + N;
@@ -2310,10 +2346,12 @@ int hge_participant_events(hge_engine* h, int32_t creator, int64_t skip, int32_t
 }
 
 int32_t hge_participant_event(hge_engine* h, int32_t creator, int64_t index) {
-  if (creator < 0 || creator >= h->N || index < 0) return HGE_ERR_NOT_FOUND;
+  if (!h || creator < 0 || creator >= h->N) return HGE_ERR_NOT_FOUND;
   const std::vector<int32_t>& ch = h->h_chain[creator];
   const int64_t tot = (int64_t)ch.size();
-  if (index < tot - window_len(tot, h->cache_size)) return HGE_ERR_TOO_LATE;
+  // RollingList.GetItem (common/rolling_list.go:42-53): index < oldestCached (>= 0),
+  // a negative index included, is ErrTooLate
+  if (index < 0 || index < tot - window_len(tot, h->cache_size)) return HGE_ERR_TOO_LATE;
   if (index >= tot) return HGE_ERR_NOT_FOUND;
   return ch[index];
 }
@@ -2390,6 +2428,23 @@ int hge_event_received(hge_engine* h, int32_t* rr_out, int64_t* cts_out, int64_t
   if (m > 0 && cts_out) h->d2h(cts_out, h->d_cts.p, 8 * (size_t)m);
   h->sync();
   return HGE_OK;
+  GUARD_END(h)
+}
+
+int32_t hge_fame_table(hge_engine* h, int32_t rounds, int8_t* fame_out) {
+  if (!h) return HGE_ERR_ARG;
+  GUARD_BEGIN
+  const int R = std::min<int>(std::max(rounds, 0), std::min(h->R, h->Rcap));
+  if (R == 0 || !fame_out) return 0;
+  const size_t n = (size_t)R * h->N;
+  std::vector<int32_t> w(n);
+  std::vector<uint8_t> f(n);
+  h->d2h(w.data(), h->d_W.p, 4 * n);
+  h->d2h(f.data(), h->d_fame.p, n);
+  h->sync();
+  for (size_t i = 0; i < n; i++)
+    fame_out[i] = (w[i] >= 0 && w[i] < h->n_divided) ? (int8_t)f[i] : (int8_t)-1;
+  return R;
   GUARD_END(h)
 }
 

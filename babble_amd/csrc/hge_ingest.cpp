@@ -198,9 +198,10 @@ int hge_sha256_batch(int64_t n, const uint8_t* data, const int64_t* off, int32_t
 }
 
 int hge_ingest(hge_engine* h, const hge_event* ev, int64_t n, const uint8_t* bodies, const int64_t* body_off,
-               const uint8_t* pubs, const uint8_t* sigs, int64_t k, int32_t threads, int32_t* status_out,
+               const uint8_t* keys, const uint8_t* sigs, int64_t k, int32_t threads, int32_t* status_out,
                int64_t* n_accepted, double* times_out) {
-  if (!h || n < 0 || k <= 0 || (n > 0 && (!ev || !bodies || !body_off || !pubs || !sigs))) return HGE_ERR_ARG;
+  if (!h || n < 0 || k <= 0 || (n > 0 && (!ev || !bodies || !body_off || !keys || !sigs))) return HGE_ERR_ARG;
+  const int N = hge_participants(h);
   for (int64_t i = 0; i < n; i++)
     if (body_off[i + 1] < body_off[i]) return HGE_ERR_ARG;
   using clk = std::chrono::steady_clock;
@@ -215,9 +216,13 @@ int hge_ingest(hge_engine* h, const hge_event* ev, int64_t n, const uint8_t* bod
     return [&, lo, hi](int w, int64_t i) {
       uint8_t hb[32];
       const int64_t e = lo + i;
-      if (e < hi)
-        ok[e] = verify_one(pool.cache(w), bodies + body_off[e], (size_t)(body_off[e + 1] - body_off[e]),
-                           pubs + 65 * e, sigs + 64 * e, hb);
+      if (e >= hi) return;
+      const int c = ev[e].creator;
+      // no key for this id: let admission refuse it ("Could not find fake creator id")
+      ok[e] = (c < 0 || c >= N) ? 1
+                                : verify_one(pool.cache(w), bodies + body_off[e],
+                                             (size_t)(body_off[e + 1] - body_off[e]), keys + 65 * (size_t)c,
+                                             sigs + 64 * e, hb);
     };
   };
   auto tv = clk::now();

@@ -67,6 +67,7 @@ struct DirLDS {
   int32_t sFD[DirGeo<BS, NPOW>::W * NPOW] __attribute__((aligned(16)));  // the window's FD rows (int32, by LDS DMA)
   int sCnt[DIR_MAXP];
   int sCntW[DIR_MAXP][BS / 64] __attribute__((aligned(16)));  // per-wave passing members of a probe
+  int sHist[DirGeo<BS, NPOW>::W / 2];  // members by first passing offset (dir_select_pm)
   uint32_t sBits[8];
   int s_stop, s_past;
   int s_stamp;          // HGE_STAMPS: thread 0 accumulates probe phases into sdbg
@@ -334,52 +335,34 @@ __device__ __forceinline__ int dir_probe(const Tables& t, DirLDS<BS, NPOW>& L, i
   return r;
 }
 
-// C_{r+1}[c] before the end-of-chain clamp (INF32 = none yet) from the frontier
-// in L.sP, the member slice mw and the window staged at lo (== L.sP[c]);
-// pb = this thread's member pass flag at the returned row.
-// A probe costs N^2 packed compares on this CU and a round lasts as long as its
-// slowest chain, so the search minimises the worst case, not the mean: the
-// advance per round is 13.8 +- 3.7 rows (max 33 over 568 x 256 at 256/2M,
-// scripts/analysis/dump_rounds.py), so the first half of the window [0, W/2) is
-// bisected on the assumption that its last row passes -- log2(W/2) probes -- and
-// that row is probed only if every probe failed.  (A search that starts at the
-// predicted advance takes fewer probes on average but more on the slowest chain
-// of a round: measured slower.)
+// Probe bisection for the first passing row at or after window offset a (the
+// fallback of dir_select: rare).  Every probe counts all members at one row (a
+// barrier each); the window's last row is probed first, and when it fails the
+// next window is loaded.  pb = this thread's member pass flag at the returned row.
 template <int BS, int NPOW>
-__device__ int dir_select(const Tables& t, int c, int lenc, DirLDS<BS, NPOW>& L, int part,
-                          const uint32_t (&mw)[DirGeo<BS, NPOW>::CW], int& slot,
-                          uint2 (&pv)[DirGeo<BS, NPOW>::PREF], int& lo, bool& pb) {
+__device__ int dir_probe_search(const Tables& t, int c, int lenc, DirLDS<BS, NPOW>& L, int part,
+                                const uint32_t (&mw)[DirGeo<BS, NPOW>::CW], int& slot,
+                                uint2 (&pv)[DirGeo<BS, NPOW>::PREF], int& lo, bool& pb, int a) {
   constexpr int W = DirGeo<BS, NPOW>::W;
   const int SM = t.SM;
-  if (lo == INF32 || lo >= lenc) return INF32;
   for (;;) {
-    const int last = min(W, lenc - lo) - 1;  // >= 0
-    bool ps;
-    int a = 0, b = min(W / 2 - 1, last);
-    bool known = false;  // row b has passed a probe
-    for (int pass2 = 0; pass2 < 2; pass2++) {
-      while (a < b) {  // the first passing row of [a, b], if row b passes
-        const int mid = (a + b) >> 1;
-        if (dir_probe<BS, NPOW>(t, L, lo + mid, part, slot++, mw, ps) >= SM) {
-          b = mid;
-          pb = ps;
-          known = true;
-        } else {
-          a = mid + 1;
-        }
-      }
-      if (known) return lo + a;
-      if (dir_probe<BS, NPOW>(t, L, lo + a, part, slot++, mw, ps) >= SM) {
+    const int last = min(W, lenc - lo) - 1;
+    if (a <= last) {
+      bool ps;
+      int b = last;
+      if (dir_probe<BS, NPOW>(t, L, lo + b, part, slot++, mw, ps) >= SM) {
         pb = ps;
+        while (a < b) {
+          const int mid = (a + b) >> 1;
+          if (dir_probe<BS, NPOW>(t, L, lo + mid, part, slot++, mw, ps) >= SM) {
+            b = mid;
+            pb = ps;
+          } else {
+            a = mid + 1;
+          }
+        }
         return lo + a;
       }
-      // every row of [0, b] fails: the second half [b + 1, last], its last row probed first
-      if (a >= last) break;
-      a = a + 1;
-      b = last;
-      if (dir_probe<BS, NPOW>(t, L, lo + b, part, slot++, mw, ps) < SM) break;
-      pb = ps;
-      known = true;
     }
     if (lo + W >= lenc) return INF32;
     // the answer lies past the window: the whole next window, fresh counters
@@ -389,7 +372,61 @@ __device__ int dir_select(const Tables& t, int c, int lenc, DirLDS<BS, NPOW>& L,
     if (threadIdx.x < DIR_MAXP) L.sCnt[threadIdx.x] = 0;
     slot = 0;
     __syncthreads();
+    a = 0;
   }
+}
+
+// C_{r+1}[c] before the end-of-chain clamp (INF32 = none yet) from the frontier
+// in L.sP, the member slice mw and the window staged at lo (== L.sP[c]).
+//
+// Per member, not per probe: C_{r+1}[c] - lo is the SM-th smallest of the
+// members' first passing offsets T_d = min{k : StronglySee((c, lo + k), m_d)}
+// (StronglySee is monotone along the chain, so "count(k) >= SM" <=> "at least
+// SM members have T_d <= k").  The TPM lanes of member d bisect T_d over the
+// first half of the window on their own -- log2(W/2) counts of their slice
+// against rows of the LDS ring, summed over the member's lanes by DPP, no
+// barrier between steps -- and one LDS histogram of the T_d plus a wave prefix
+// scan gives the SM-th smallest.  The last offset W/2 - 1 also stands for
+// "later" (not verified), so an answer there (or none) falls back to probe
+// bisection from W/2 - 1 on (dir_probe_search).  Round 2's probe bisection paid
+// a workgroup barrier, an LDS count exchange and a ballot per probe (five to
+// six per round, ~2.5k cycles each at N = 256); the counts here are the same
+// N^2 compares per step, with one barrier per round.
+// pb = this thread's member is strongly seen by the returned row.
+template <int BS, int NPOW>
+__device__ int dir_select(const Tables& t, int c, int lenc, DirLDS<BS, NPOW>& L, int d, int part,
+                          const uint32_t (&mw)[DirGeo<BS, NPOW>::CW], int& slot,
+                          uint2 (&pv)[DirGeo<BS, NPOW>::PREF], int& lo, bool& pb) {
+  constexpr int H = DirGeo<BS, NPOW>::W / 2;
+  constexpr int STEPS = H == 32 ? 5 : H == 16 ? 4 : 3;
+  static_assert((1 << STEPS) == H, "window half is a power of two");
+  const int SM = t.SM;
+  if (lo == INF32 || lo >= lenc) return INF32;
+  int a = 0, b = H - 1;
+#pragma unroll
+  for (int s = 0; s < STEPS; s++) {
+    const int mid = (a + b) >> 1;
+    if (dir_count<BS, NPOW>(L, lo + mid, part, mw) >= SM) b = mid;
+    else a = mid + 1;
+  }
+  // a == b == T_d (exact below H - 1); members past N do not count
+  if (part == 0 && d < t.N) atomicAdd(&L.sHist[a], 1);
+  __syncthreads();
+  // every wave: inclusive prefix over the H bins, the first bin reaching SM
+  const int lane = threadIdx.x & 63;
+  int v = lane < H ? L.sHist[lane] : 0;
+#pragma unroll
+  for (int o = 1; o < H; o <<= 1) {
+    const int y = __shfl_up(v, o, 64);
+    if (lane >= o) v += y;
+  }
+  const uint64_t ge = __ballot(lane < H && v >= SM);
+  const int ks = ge ? (int)__builtin_ctzll(ge) : H;
+  if (ks < H - 1) {
+    pb = a <= ks;
+    return lo + ks;
+  }
+  return dir_probe_search<BS, NPOW>(t, c, lenc, L, part, mw, slot, pv, lo, pb, H - 1);
 }
 
 template <int BS, int NPOW>
@@ -470,6 +507,7 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
     }
     if (tid < DIR_MAXP) L.sCnt[tid] = 0;
     if (tid < 8) L.sBits[tid] = 0;
+    if (tid < DirGeo<BS, NPOW>::W / 2) L.sHist[tid] = 0;
     __syncthreads();  // window stored, counters clear
     DSTAMP(0);
     const int Pc = L.sP[c];
@@ -481,7 +519,7 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
       if (cur != INF32) {
         nxt = cur;
       } else {
-        const int s = dir_select<BS, NPOW>(t, c, lenc, L, part, mw, slot, pv, lo, pb);
+        const int s = dir_select<BS, NPOW>(t, c, lenc, L, d, part, mw, slot, pv, lo, pb);
         nxt = s < lenc ? s : INF32;
         have_bits = nxt != INF32;
       }

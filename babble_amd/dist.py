@@ -50,11 +50,14 @@ def join_histories(hists):
     the end of a walker's history and the sequential walk resumes from row K-1.
     """
     G = len(hists)
+    # each row -> the FURTHEST walker that holds it: walker p runs past walker
+    # p + 1's start, so a row on the true trajectory is often in both, and the
+    # join must move on to p + 1 (a later rank overwrites an earlier one)
     index = {}
     for g in range(1, G):
         rows = hists[g][0]
         for i in range(len(rows)):
-            index.setdefault(rows[i].tobytes(), (g, i))
+            index[rows[i].tobytes()] = (g, i)
     out_r, out_s = [], []
     g, i = 0, 0
     while True:

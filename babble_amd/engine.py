@@ -73,7 +73,7 @@ EXPORTS = [
     "hge_diff", "hge_wire_info", "hge_read_wire_parents", "hge_parent_round", "hge_round_inc",
     "hge_round_diff", "hge_set_round", "hge_split_begin", "hge_frontier_guess",
     "hge_frontier_walk", "hge_split_finish", "hge_frontier_rows",
-    "hge_verify_events", "hge_sha256_batch", "hge_ingest",
+    "hge_verify_events", "hge_sha256_batch", "hge_ingest", "hge_fame_table",
 ]
 
 _lib = None
@@ -142,6 +142,8 @@ def lib():
     L.hge_consensus_log.restype = i64
     L.hge_event_rounds.argtypes = [vp, P(i32), P(ctypes.c_uint8), i64]
     L.hge_event_received.argtypes = [vp, P(i32), P(i64), i64]
+    L.hge_fame_table.argtypes = [vp, i32, P(ctypes.c_int8)]
+    L.hge_fame_table.restype = i32
     L.hge_set_cache_size.argtypes = [vp, i64]
     L.hge_cache_size.argtypes = [vp]
     L.hge_cache_size.restype = i64
@@ -284,21 +286,23 @@ class Engine:
             raise HgeError(rc, self.L.hge_last_error(self.h).decode(), accepted=status[:acc.value].copy())
         return status[:acc.value]
 
-    def ingest(self, ev, bodies, pubs, sigs, k, threads=0):
+    def ingest(self, ev, bodies, keys, sigs, k, threads=0):
         """hge_ingest: InsertEvent with signature checks in batches of k, RunConsensus
         after each batch, the next batch verified on host threads meanwhile.
+        keys: uint8[N, 65], participant c's key; event i is checked under
+        keys[ev[i].creator] (a body signed by another participant is refused).
         Returns (rc, status int32[n], n_accepted, times {verify_ms, device_ms, wall_ms});
         rc is 0 or the negative status that ended the stream (HGE_ERR_SIGNATURE = -13)."""
         ev = np.ascontiguousarray(ev, EVENT_DTYPE)
         flat, off = _flat(bodies)
         n = len(ev)
         assert len(off) == n + 1
-        pubs = np.ascontiguousarray(pubs, np.uint8).reshape(n, 65)
+        keys = np.ascontiguousarray(keys, np.uint8).reshape(self.n, 65)
         sigs = np.ascontiguousarray(sigs, np.uint8).reshape(n, 64)
         status = np.zeros(max(n, 1), np.int32)
         acc = ctypes.c_int64()
         tm = (ctypes.c_double * 3)()
-        rc = self.L.hge_ingest(self.h, ev.ctypes.data, n, _pu8(flat), _p64(off), _pu8(pubs), _pu8(sigs), int(k),
+        rc = self.L.hge_ingest(self.h, ev.ctypes.data, n, _pu8(flat), _p64(off), _pu8(keys), _pu8(sigs), int(k),
                                threads, _p32(status), ctypes.byref(acc), tm)
         if rc in (-8, -9, -10):  # argument, device or internal error (admission errors end the stream)
             raise HgeError(rc, self.L.hge_last_error(self.h).decode())
@@ -521,6 +525,16 @@ class Engine:
         cts = np.zeros(max(m, 1), np.int64)
         self._check(self.L.hge_event_received(self.h, _p32(rr), _p64(cts), m))
         return rr[:m], cts[:m]
+
+    def fame_table(self):
+        """Fame of every (round, creator) slot: int8 [Rounds(), N], -1 = no witness
+        (hge_fame's encoding: 0 undefined, 1 true, 2 false)."""
+        R = self.rounds()
+        out = np.full((max(R, 1), self.n), -1, np.int8)
+        got = self.L.hge_fame_table(self.h, R, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int8)))
+        if got < 0:
+            raise HgeError(got, self.L.hge_last_error(self.h).decode())
+        return out[:R]
 
     def consensus_log(self, start=0):
         m = self.L.hge_consensus_log(self.h, start, None, 0)

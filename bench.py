@@ -126,6 +126,20 @@ def golden_prefix(n, E, K, seed):
     return np.load(path)
 
 
+def mc_digests(n, E, K, seed):
+    """The committed oracle digests of config 5's batch (tests/golden/make_mc_digests.py)
+    when this run replays exactly that batch, else None."""
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    path = os.path.join(ROOT, "tests", "golden", f"mc_n{n}_e{E}_k{K}_digests.json")
+    if not os.path.exists(path):
+        return None
+    d = json.load(open(path))
+    p = d["params"]
+    if (p["seed0"], p["forkers"], p["fork_p"], p["cascade_p"]) != (seed, 10, 0.05, 0.5):
+        return None
+    return d["digests"]
+
+
 def sub_stream(dag, ns):
     return {k: (v[:ns] if isinstance(v, np.ndarray) else v) for k, v in dag.items()}
 
@@ -179,15 +193,14 @@ def ingest_path(n, E, K, seed, device, threads=16):
     dag = random_gossip(n, E, seed=seed)
     pubs, bodies, sigs = signing.signed_stream(dag, seed=seed, threads=threads)
     ev = events_array(dag)
-    cpubs = pubs[dag["creator"]]
     t0 = time.perf_counter()
-    ok, _ = verify_events(bodies, cpubs, sigs, threads=threads)
+    ok, _ = verify_events(bodies, pubs[dag["creator"]], sigs, threads=threads)
     vdt = time.perf_counter() - t0
     rep = Engine(n, E, device=device)
     _, rorder, _ = rep.replay(ev, schedule(E, K))
     rep.close()
     eng = Engine(n, E, device=device)
-    rc, _, acc, tm = eng.ingest(ev, bodies, cpubs, sigs, K, threads=threads)
+    rc, _, acc, tm = eng.ingest(ev, bodies, pubs, sigs, K, threads=threads)
     order = eng.consensus_log()
     eng.close()
     return {"workload": f"online path with signature checks, {n} participants, {E} events, hge_ingest "
@@ -377,41 +390,81 @@ def main():
                                  "launches_per_replay": lpr}
 
     cpu, parity, checks = None, None, []
+    if mc:
+        # every graph of this rank against the oracle's full-state digest
+        # (tests/golden/make_mc_digests.py): order, batches, rounds, witnesses,
+        # fame, round received, timestamps, undetermined list, scalars
+        dg = mc_digests(n, E, K, args.seed)
+        bad, nchk = 0, 0
+        if dg is not None:
+            from digest import digest, engine_state
+            for g, eng in enumerate(engines):
+                gi = first + g
+                if gi >= len(dg):
+                    continue
+                st_, ord_, cnt_ = eng.fetch()
+                nchk += 1
+                bad += digest(engine_state(eng, st_, ord_, cnt_)) != dg[gi]
+        if dist is not None:
+            import torch
+            t_ = torch.tensor([nchk, bad], dtype=torch.int64, device=f"cuda:{local_rank}")
+            dist.all_reduce(t_)
+            nchk, bad = int(t_[0].item()), int(t_[1].item())
+        if nchk:
+            checks.append(f"{'bit-exact' if bad == 0 else f'MISMATCH on {bad} graphs'} vs the oracle's "
+                          f"full-state digests on {nchk} of {args.graphs} graphs (order, batches, rounds, "
+                          f"witnesses, fame, round received, timestamps; tests/golden/mc_*_digests.json)")
     if rank == 0 and not mc:
         gp = golden_prefix(n, E, K, args.seed)
         if gp is not None:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            from parity import check_prefix
             nc = int(gp["n_calls"])
-            ok = (np.array_equal(gcounts[:nc], gp["counts"]) and
-                  np.array_equal(gorder[:len(gp["order"])], gp["order"]))
-            checks.append(f"{'bit-exact' if ok else 'MISMATCH'} vs committed oracle golden "
-                          f"(first {int(gp['prefix'])} submissions, {nc} calls, "
+            rounds_, wit_ = eng0.event_rounds()
+            rr_, cts_ = eng0.event_received()
+            bad = check_prefix(gp, gorder, gcounts, rounds_, wit_, rr_, cts_, eng0.fame_table())
+            full = "rounds" in gp.files
+            what = ("order, batches, rounds, witnesses, round received, timestamps, fame to LCR "
+                    f"{int(gp['scalars'][1])}" if full else "order and batches")
+            checks.append(f"{'bit-exact' if not bad else 'MISMATCH in ' + ','.join(bad)} vs committed oracle "
+                          f"golden ({what}; first {int(gp['prefix'])} submissions, {nc} calls, "
                           f"{len(gp['order'])} ordered)")
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline and mc:
+        # the oracle on whole graphs of the batch, one core, until ~10 s of work
+        from oracle.oracle import replay as oracle_replay
+        t0 = time.perf_counter()
+        tot, ng = 0, 0
+        for d in dags:
+            _, _, corder, _ = oracle_replay(d, schedule(len(d["creator"]), K))
+            tot += len(corder)
+            ng += 1
+            if time.perf_counter() - t0 > 10.0:
+                break
+        cs = time.perf_counter() - t0
+        cpu = {"value": round(tot / cs, 1), "unit": "events/s", "cores": 1, "kind": "port",
+               "sample": f"Go-faithful C++ oracle (oracle/hg_oracle.cpp), the first {ng} graphs of the batch "
+                         f"(whole graphs, K={K}), {tot} ordered in {cs:.2f} s on "
+                         f"{platform.processor() or platform.machine()} (host nproc {os.cpu_count()})"}
+    elif rank == 0 and not args.no_cpu_baseline:
         from oracle.oracle import replay as oracle_replay
         d = dags[0]
         ns = args.cpu_sample_events or (20480 if n >= 128 else 100_000)
         ns = min(ns, len(d["creator"]))
-        if not mc:
-            ns = max(K, ns // K * K)  # whole calls only: the prefix's calls are the full run's
+        ns = max(K, ns // K * K)  # whole calls only: the prefix's calls are the full run's
         sub = sub_stream(d, ns)
         calls = schedule(ns, K)
         t0 = time.perf_counter()
         _, _, corder, ccounts = oracle_replay(sub, calls)
         cs = time.perf_counter() - t0
-        what = (f"graph 0 of the batch ({ns} submissions)" if mc else
-                f"first {ns} of {len(d['creator'])} submissions of the same stream")
+        what = f"first {ns} of {len(d['creator'])} submissions of the same stream"
         cpu = {"value": round(len(corder) / cs, 1), "unit": "events/s", "cores": 1, "kind": "port",
                "sample": f"Go-faithful C++ oracle (oracle/hg_oracle.cpp), {what}, K={K}, "
                          f"{len(corder)} ordered in {cs:.2f} s on "
                          f"{platform.processor() or platform.machine()} (host nproc {os.cpu_count()})"}
-        if not mc:
-            ok = (np.array_equal(gcounts[:len(calls)], ccounts) and
-                  np.array_equal(gorder[:len(corder)], corder))
-            checks.append(f"{'bit-exact' if ok else 'MISMATCH'} vs CPU oracle run live "
-                          f"(first {ns} submissions, {len(calls)} calls, {len(corder)} ordered)")
-        elif ns == len(d["creator"]):
-            ok = np.array_equal(gorder, corder)
-            checks.append(f"{'bit-exact' if ok else 'MISMATCH'} vs CPU oracle (full graph 0)")
+        ok = (np.array_equal(gcounts[:len(calls)], ccounts) and
+              np.array_equal(gorder[:len(corder)], corder))
+        checks.append(f"{'bit-exact' if ok else 'MISMATCH'} vs CPU oracle run live "
+                      f"(first {ns} submissions, {len(calls)} calls, {len(corder)} ordered)")
     if rank == 0:
         parity = "; ".join(checks) if checks else None
 

@@ -109,7 +109,16 @@ int hge_sha256_batch(int64_t n, const uint8_t* data, const int64_t* off, int32_t
 /* InsertEvent with its signature check over a stream, in batches of k events with
  * RunConsensus after each batch (node/core.go:179-202), while a pool of `threads`
  * host threads verifies the next batch: the host crypto overlaps the device.  ev[i]
- * is event i's record, (bodies, body_off, pubs, sigs) as for hge_verify_events.
+ * is event i's record, (bodies, body_off, sigs) as for hge_verify_events, and
+ * keys[65 c] is participant c's uncompressed P-256 key: event i's signature is
+ * checked under keys[65 * ev[i].creator], the key its creator id stands for.  In
+ * the reference Body.Creator IS the key and the creator id is looked up from it
+ * (hashgraph.go:51-76 Participants, :366-370), so a body signed by another
+ * participant's key cannot pass as this creator's event: it is refused with
+ * HGE_ERR_SIGNATURE here.  The caller derives ev[i] (creator, index, parents,
+ * timestamp, hash) from the body it passes; the engine does not decode the body.
+ * A creator id outside [0, N) is refused with HGE_ERR_CREATOR, as by
+ * hge_insert_events.
  * The first event whose signature fails is refused with HGE_ERR_SIGNATURE and ends
  * the stream (the events before it stay inserted and their batch goes through
  * consensus), like InsertEvent inside Core.Sync; admission errors end it the same
@@ -117,7 +126,7 @@ int hge_sha256_batch(int64_t n, const uint8_t* data, const int64_t* off, int32_t
  * times_out (may be NULL): [0] host ms spent verifying that the device did not
  * hide, [1] ms inside the insert + consensus calls, [2] wall ms. */
 int hge_ingest(hge_engine* h, const hge_event* ev, int64_t n, const uint8_t* bodies, const int64_t* body_off,
-               const uint8_t* pubs, const uint8_t* sigs, int64_t k, int32_t threads, int32_t* status_out,
+               const uint8_t* keys, const uint8_t* sigs, int64_t k, int32_t threads, int32_t* status_out,
                int64_t* n_accepted, double* times_out);
 
 /* ---- consensus (node/core.go:179-202) --------------------------------------- */
@@ -203,6 +212,10 @@ int64_t hge_consensus_timestamp(hge_engine* h, int32_t id);
  * event (DivideRounds state), and RoundReceived (-1 = nil) / consensus timestamp. */
 int hge_event_rounds(hge_engine* h, int32_t* round_out, uint8_t* witness_out, int64_t cap);
 int hge_event_received(hge_engine* h, int32_t* rr_out, int64_t* cts_out, int64_t cap);
+/* Fame of every round slot, rounds [0, min(rounds, hge_rounds)) x n_participants,
+ * row-major: hge_fame's encoding (RoundInfo.Events[w].Famous, roundInfo.go:24-36,
+ * -1 = no witness of that creator in that round).  Returns the rounds written. */
+int32_t hge_fame_table(hge_engine* h, int32_t rounds, int8_t* fame_out);
 
 /* ---- Store semantics and the sync path (store.go:25-41, node/core.go:108-132) -- */
 /* Store.CacheSize (inmem_store.go:38-40): size of the rolling windows of

@@ -1,0 +1,59 @@
+"""Full-state digests of a replay (test infrastructure).
+
+One SHA-256 over everything the parity contract calls bit-exact:
+admission status, the order, per-call batch sizes, every event's round and
+witness flag, the fame of every (round, creator) slot, every event's round
+received, the consensus timestamp of every ordered event, the undetermined list
+and the scalars (Rounds(), LastConsensusRound, LastCommitedRoundEvents,
+ConsensusTransactions).  The same canonical byte layout is built from the CPU
+oracle (make_mc_digests.py, make_golden.py's `describe`) and from the engine
+(`engine_state`), so equal digests mean equal state, field by field.
+"""
+import hashlib
+
+import numpy as np
+
+FIELDS = (("status", "<i4"), ("order", "<i4"), ("counts", "<i8"), ("rounds", "<i4"),
+          ("witness", "u1"), ("fame", "i1"), ("rr", "<i4"), ("cts", "<i8"),
+          ("undetermined", "<i4"), ("scalars", "<i8"))
+
+
+def canonical(state):
+    """The state dict with canonical dtypes; cts kept for ordered events only."""
+    out = {k: np.ascontiguousarray(np.asarray(state[k]).astype(dt)) for k, dt in FIELDS}
+    cts = np.zeros_like(out["cts"])
+    cts[out["order"]] = out["cts"][out["order"]]
+    out["cts"] = cts
+    return out
+
+
+def digest(state):
+    s = canonical(state)
+    h = hashlib.sha256()
+    for k, _ in FIELDS:
+        a = s[k]
+        h.update(k.encode())
+        h.update(np.array(a.shape, "<i8").tobytes())
+        h.update(a.tobytes())
+    return h.hexdigest()
+
+
+def engine_state(eng, status, order, counts):
+    """The engine's side of `canonical` after a replay (status/order/counts from
+    Engine.fetch)."""
+    rounds, wit = eng.event_rounds()
+    rr, cts = eng.event_received()
+    lcr = eng.last_consensus_round()
+    return dict(status=status, order=order, counts=counts, rounds=rounds, witness=wit, fame=eng.fame_table(),
+                rr=rr, cts=cts, undetermined=eng.undetermined(),
+                scalars=np.array([eng.rounds(), -1 if lcr is None else lcr, eng.last_committed_round_events(),
+                                  eng.consensus_transactions()], np.int64))
+
+
+def first_difference(a, b):
+    """Name of the first field where two states differ (None if equal)."""
+    ca, cb = canonical(a), canonical(b)
+    for k, _ in FIELDS:
+        if ca[k].shape != cb[k].shape or not np.array_equal(ca[k], cb[k]):
+            return k
+    return None

@@ -4,8 +4,10 @@ The bench replays the full seeded stream on the GPU; the engine reproduces the
 reference's per-call semantics, so the batches of the first calls depend only
 on the submissions before them.  This script runs the CPU oracle
 (oracle/hg_oracle.cpp, the Go-faithful restatement) on the first PREFIX
-submissions of the same stream with the same schedule and stores the order
-and per-call batch sizes:
+submissions of the same stream with the same schedule and stores every field
+of the parity contract (make_golden.describe: status, order, per-call batch
+sizes, rounds, witness flags, fame of every round slot, round received,
+consensus timestamps, undetermined list, scalars):
 
     python tests/golden/make_bench_prefix.py [n] [events] [k] [seed] [prefix]
 """
@@ -17,8 +19,11 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, HERE)
 
 from babble_amd.gossip import random_gossip, schedule  # noqa: E402
+from make_golden import describe  # noqa: E402
 from oracle.oracle import replay  # noqa: E402
 
 
@@ -30,11 +35,15 @@ def main():
     sub = {k: (v[:prefix] if isinstance(v, np.ndarray) else v) for k, v in dag.items()}
     calls = schedule(prefix, K)
     t = time.time()
-    _, status, order, counts = replay(sub, calls)
+    o, status, order, counts = replay(sub, calls)
     assert (status >= 0).all()
+    d = describe(o, sub, status, order, counts, calls)
+    d.pop("status")  # every submission of a gossip stream is accepted: status = iota
+    d.pop("calls")
+    d["order"] = d["order"].astype(np.int32)
+    d["counts"] = d["counts"].astype(np.int64)
     out = os.path.join(HERE, f"bench_n{n}_e{E}_k{K}_s{seed}_prefix.npz")
-    np.savez_compressed(out, order=order.astype(np.int32), counts=counts.astype(np.int64),
-                        n_calls=len(calls), prefix=prefix, n=n, events=E, k=K, seed=seed)
+    np.savez_compressed(out, n_calls=len(calls), prefix=prefix, n=n, events=E, k=K, seed=seed, **d)
     print(f"{out}: {len(order)} ordered over {len(calls)} calls ({time.time() - t:.1f} s)")
 
 

@@ -171,3 +171,37 @@ def check_run(dag, st, order, counts, rounds, wit, rr, cts):
         less |= eq & (S[a, limb] < S[b, limb])
         eq &= S[a, limb] == S[b, limb]
     assert (less | ~same_batch).all(), "ConsensusSorter order violated inside a batch"
+
+
+def check_prefix(gp, order, counts, rounds, wit, rr, cts, fame):
+    """Fields of a full replay that a committed oracle prefix golden pins
+    (tests/golden/make_bench_prefix.py: the oracle on the first P submissions of
+    the same stream, same schedule).  The engine reproduces per-call semantics,
+    so in the full run: the first calls' batches and order equal the prefix's;
+    every prefix event's round and witness flag are the prefix's (a round
+    depends only on ancestors); every event the prefix ordered has the prefix's
+    round received and consensus timestamp; fame of every round up to the
+    prefix's LastConsensusRound is final (DecideFame restarts at LCR + 1,
+    hashgraph.go:590-595).  Returns the names of the fields that differ."""
+    bad = []
+    nc = int(gp["n_calls"])
+    if not np.array_equal(counts[:nc], gp["counts"]):
+        bad.append("counts")
+    go = gp["order"]
+    if not np.array_equal(order[:len(go)], go):
+        bad.append("order")
+    if "rounds" not in gp.files:
+        return bad
+    P = len(gp["rounds"])
+    if not np.array_equal(rounds[:P], gp["rounds"]):
+        bad.append("rounds")
+    if not np.array_equal(np.asarray(wit[:P]).astype(bool), gp["witness"].astype(bool)):
+        bad.append("witness")
+    if not np.array_equal(rr[go], gp["rr"][go]):
+        bad.append("rr")
+    if not np.array_equal(cts[go], gp["cts"][go]):
+        bad.append("cts")
+    lcr = int(gp["scalars"][1])
+    if lcr >= 0 and (fame.shape[0] <= lcr or not np.array_equal(fame[:lcr + 1], gp["fame"][:lcr + 1])):
+        bad.append("fame")
+    return bad

@@ -113,6 +113,32 @@ def test_join_histories_follows_merges():
     assert natural and len(rows) == R
 
 
+def test_join_histories_three_walkers_overlapping():
+    """Walker p runs past walker p + 1's start, so rows of the true trajectory are
+    in both: the join must move on to the furthest walker holding a row (1 -> 2
+    here), not stop at the end of walker 1's history."""
+    import numpy as np
+    from babble_amd.dist import join_histories
+    from babble_amd.gossip import random_gossip
+    n = 6
+    C = true_frontier(n, random_gossip(n, 4000, seed=32), n)
+    R = len(C) - 1
+    assert R > 70
+    rng = np.random.default_rng(2)
+    j1 = C[20:23] + rng.integers(1, 3, (3, n)).astype(np.int32)
+    j2 = C[40:43] + rng.integers(1, 3, (3, n)).astype(np.int32)
+    h = [C[:30].copy(),                      # rank 0: true rows 0..29
+         np.concatenate([j1, C[25:60]]),     # rank 1: converges at 25, walks past rank 2's merge
+         np.concatenate([j2, C[45:]])]       # rank 2: converges at 45, walks to the end
+    hists = [(r, _marks(r, g), g == 2) for g, r in enumerate(h)]
+    rows, ssc, natural = join_histories(hists)
+    assert natural and len(rows) == R
+    np.testing.assert_array_equal(rows, C[:R])
+    # rank 0 up to its hand-over row 25, rank 1 up to 45, rank 2 after
+    tags = ssc[:, 0, 0] % 1000
+    assert (tags[:26] == 0).all() and (tags[26:46] == 1).all() and (tags[46:] == 2).all()
+
+
 def _gather_worker(rank, world, port, q):
     import numpy as np
     import torch.distributed as dist

@@ -3,8 +3,11 @@ on one MI355X): 64 participants / 1M events and 256 / 10M, K = N.
 
 The oracle cannot replay these sizes in test time, so parity is checked by
   * the committed oracle golden of the first calls of the SAME stream
-    (tests/golden/bench_*_prefix.npz): the engine reproduces per-call
-    semantics, so the first calls' batches must be identical;
+    (tests/golden/bench_*_prefix.npz, every field of the parity contract): the
+    engine reproduces per-call semantics, so the first calls' batches and
+    order, the prefix events' rounds and witness flags, the round received and
+    timestamp of every event the prefix ordered and the fame of every round up
+    to the prefix's LastConsensusRound must be identical (parity.check_prefix);
   * size-independent properties of the reference's algorithm on the whole run:
     the order is a set of distinct accepted events and the per-call batches
     add up to it; inside every call's batch the ConsensusSorter keys
@@ -21,7 +24,7 @@ import numpy as np
 import pytest
 
 from babble_amd.gossip import random_gossip, schedule
-from parity import check_run
+from parity import check_prefix, check_run
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -39,11 +42,10 @@ def test_full_size(n, E):
         assert (st >= 0).all()
         assert len(order) > 0.99 * E  # all but the last rounds' events are ordered
         gp = np.load(os.path.join(ROOT, "tests", "golden", f"bench_n{n}_e{E}_k{K}_s{seed}_prefix.npz"))
-        nc = int(gp["n_calls"])
-        np.testing.assert_array_equal(counts[:nc], gp["counts"], err_msg="golden prefix batches")
-        np.testing.assert_array_equal(order[:len(gp["order"])], gp["order"], err_msg="golden prefix order")
         rounds, wit = eng.event_rounds()
         rr, cts = eng.event_received()
+        bad = check_prefix(gp, order, counts, rounds, wit, rr, cts, eng.fame_table())
+        assert not bad, f"fields differing from the oracle prefix golden: {bad}"
         check_run(dag, st, order, counts, rounds, wit, rr, cts)
     finally:
         eng.close()

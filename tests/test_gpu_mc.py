@@ -2,6 +2,9 @@
 Byzantine forkers (and fork cascades), one engine (HIP stream) each, driven
 concurrently by host threads on one device -- the shape bench.py --workload mc
 times.  Every graph is compared bit-exact with the oracle."""
+import json
+import os
+import sys
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -40,6 +43,45 @@ def test_monte_carlo_batch_threads():
             codes |= set(np.unique(st[st < 0]).tolist())
         assert rejected > graphs  # forks and cascades were generated and refused
         assert {-5, -4, -2} <= codes  # fork, op on a rejected event, child of a rejected event
+    finally:
+        for e in engines:
+            e.close()
+
+
+def test_monte_carlo_config5_size():
+    """Config 5 at its stated size: 256 of the batch's 1024 graphs x 10k
+    submissions (graphs 0-255 of bench.py --workload mc), 8 host threads, each
+    graph's FULL state (order, batches, rounds, witnesses, fame, round received,
+    timestamps, undetermined list, scalars) against the oracle digests committed
+    in tests/golden/mc_n32_e10000_k32_digests.json, and 8 graphs also against the
+    oracle run live, field by field."""
+    from babble_amd.engine import Engine, events_array
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    sys.path.insert(0, here)
+    from digest import digest, engine_state, first_difference
+    from make_mc_digests import OUT, graph_stream, oracle_state
+    ref = json.load(open(OUT))
+    graphs, threads = 256, 8
+    streams = [graph_stream(g) for g in range(graphs)]
+    engines = [Engine(32, len(d["creator"]) + 64) for d, _ in streams]
+    try:
+        for e, (d, calls) in zip(engines, streams):
+            e.prepare(events_array(d), calls)
+
+        def run(i):
+            engines[i].run()
+            st, order, counts = engines[i].fetch()
+            return engine_state(engines[i], st, order, counts)
+
+        with ThreadPoolExecutor(threads) as pool:
+            got = list(pool.map(run, range(graphs)))
+            live = list(pool.map(lambda g: oracle_state(*streams[g]), range(0, graphs, graphs // 8)))
+        bad = [g for g in range(graphs) if digest(got[g]) != ref["digests"][g]]
+        assert not bad, f"graphs differing from the oracle digests: {bad[:16]}"
+        for j, g in enumerate(range(0, graphs, graphs // 8)):
+            assert first_difference(got[g], live[j]) is None, f"graph {g}: {first_difference(got[g], live[j])}"
+        assert sum(int((s["status"] < 0).sum()) for s in got) == sum(ref["rejected"][:graphs])
+        assert sum(len(s["order"]) for s in got) == sum(ref["ordered"][:graphs])
     finally:
         for e in engines:
             e.close()

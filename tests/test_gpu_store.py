@@ -116,8 +116,12 @@ def test_store_windows_and_sync_reads(size):
                     assert eng.participant_events(c, skip).tolist() == chains[c][skip:].tolist()
             assert eng.last_from(c) == chains[c][-1]
             assert eng.participant_event(c, tot - 1) == chains[c][-1]
-            with pytest.raises(HgeError):
+            with pytest.raises(HgeError) as ei:
                 eng.participant_event(c, tot)  # not found
+            assert ei.value.code == -12
+            with pytest.raises(HgeError) as ei:
+                eng.participant_event(c, -1)  # below oldestCached (>= 0): ErrTooLate
+            assert ei.value.code == -11
         # ConsensusEvents: the rolling window of the consensus list
         win, tot = rolling_model(oorder.tolist(), size)
         assert eng.consensus_events().tolist() == win

@@ -182,3 +182,32 @@ def test_oversized_call_buckets(n, events):
         run_case(eng, random_gossip(n, events, seed=500 + n), events)
     finally:
         eng.close()
+
+
+def test_two_wide_engines_concurrently():
+    """Two N > 32 engines replaying at the same time from two host threads on one
+    device: their frontier grids (one co-resident 1024-thread workgroup per
+    chain) are serialised inside the process, so neither waits on workgroups
+    the other holds; both results equal the sequential replays."""
+    from concurrent.futures import ThreadPoolExecutor
+    from babble_amd.engine import Engine
+    from babble_amd.gossip import schedule
+    cases = [(128, 12_000, 128, 61), (256, 20_000, 256, 62)]
+    dags = [random_gossip(n, E, seed=s) for n, E, _, s in cases]
+    engines = [Engine(n, E) for n, E, _, _ in cases]
+    try:
+        want = [e.replay(d, schedule(len(d["creator"]), k))[1] for e, d, (_, _, k, _) in zip(engines, dags, cases)]
+
+        def run(i):
+            out = None
+            for _ in range(3):
+                out = engines[i].replay(dags[i], schedule(len(dags[i]["creator"]), cases[i][2]))[1]
+            return out
+
+        with ThreadPoolExecutor(2) as pool:
+            got = list(pool.map(run, range(2)))
+        for g, w in zip(got, want):
+            np.testing.assert_array_equal(g, w)
+    finally:
+        for e in engines:
+            e.close()
