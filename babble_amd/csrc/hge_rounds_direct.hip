@@ -386,9 +386,9 @@ __device__ int dir_probe_search(const Tables& t, int c, int lenc, DirLDS<BS, NPO
 // first half of the window on their own -- log2(W/2) counts of their slice
 // against rows of the LDS ring, summed over the member's lanes by DPP, no
 // barrier between steps -- and one LDS histogram of the T_d plus a wave prefix
-// scan gives the SM-th smallest.  The last offset W/2 - 1 also stands for
-// "later" (not verified), so an answer there (or none) falls back to probe
-// bisection from W/2 - 1 on (dir_probe_search).  Round 2's probe bisection paid
+// scan gives the SM-th smallest.  The last offset searched, e = min(W/2, rows
+// left on the chain) - 1, also stands for "later" (not verified), so an answer
+// there (or none) falls back to probe bisection from e on (dir_probe_search).  Round 2's probe bisection paid
 // a workgroup barrier, an LDS count exchange and a ballot per probe (five to
 // six per round, ~2.5k cycles each at N = 256); the counts here are the same
 // N^2 compares per step, with one barrier per round.
@@ -402,14 +402,17 @@ __device__ int dir_select(const Tables& t, int c, int lenc, DirLDS<BS, NPOW>& L,
   static_assert((1 << STEPS) == H, "window half is a power of two");
   const int SM = t.SM;
   if (lo == INF32 || lo >= lenc) return INF32;
-  int a = 0, b = H - 1;
+  // bisect over real rows only: the ring's "no row" entries past the chain's end
+  // fail every count, which would break the monotonicity the bisection needs
+  const int e = min(H - 1, lenc - lo - 1);
+  int a = 0, b = e;
 #pragma unroll
   for (int s = 0; s < STEPS; s++) {
     const int mid = (a + b) >> 1;
     if (dir_count<BS, NPOW>(L, lo + mid, part, mw) >= SM) b = mid;
     else a = mid + 1;
   }
-  // a == b == T_d (exact below H - 1); members past N do not count
+  // a == b == T_d, exact below e (e stands for "e or later"); members past N do not count
   if (part == 0 && d < t.N) atomicAdd(&L.sHist[a], 1);
   __syncthreads();
   // every wave: inclusive prefix over the H bins, the first bin reaching SM
@@ -422,11 +425,11 @@ __device__ int dir_select(const Tables& t, int c, int lenc, DirLDS<BS, NPOW>& L,
   }
   const uint64_t ge = __ballot(lane < H && v >= SM);
   const int ks = ge ? (int)__builtin_ctzll(ge) : H;
-  if (ks < H - 1) {
+  if (ks < e) {
     pb = a <= ks;
     return lo + ks;
   }
-  return dir_probe_search<BS, NPOW>(t, c, lenc, L, part, mw, slot, pv, lo, pb, H - 1);
+  return dir_probe_search<BS, NPOW>(t, c, lenc, L, part, mw, slot, pv, lo, pb, e);
 }
 
 template <int BS, int NPOW>
