@@ -69,7 +69,7 @@ struct DirLDS {
   int sCntW[DIR_MAXP][BS / 64] __attribute__((aligned(16)));  // per-wave passing members of a probe
   int sHist[DirGeo<BS, NPOW>::W / 2];  // members by first passing offset (dir_select_pm)
   uint32_t sBits[8];
-  int s_stop, s_past;
+  int sFlag[2];          // per round parity: 1 = some member exists, 2 = some chain below stopcut, 4 = hand-off failed
   int s_stamp;          // HGE_STAMPS: thread 0 accumulates probe phases into sdbg
   uint64_t sdbg[2];     // [0] count (LDS reads + VALU), [1] reduce + barrier + read
 };
@@ -405,6 +405,8 @@ __device__ int dir_select(const Tables& t, int c, int lenc, DirLDS<BS, NPOW>& L,
   // bisect over real rows only: the ring's "no row" entries past the chain's end
   // fail every count, which would break the monotonicity the bisection needs
   const int e = min(H - 1, lenc - lo - 1);
+  const bool st = kDirStamps && L.s_stamp && threadIdx.x == 0;
+  const uint64_t t0 = st ? stamp() : 0;
   int a = 0, b = e;
 #pragma unroll
   for (int s = 0; s < STEPS; s++) {
@@ -414,7 +416,16 @@ __device__ int dir_select(const Tables& t, int c, int lenc, DirLDS<BS, NPOW>& L,
   }
   // a == b == T_d, exact below e (e stands for "e or later"); members past N do not count
   if (part == 0 && d < t.N) atomicAdd(&L.sHist[a], 1);
+  uint64_t t1 = 0;
+  if (st) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    t1 = stamp();
+  }
   __syncthreads();
+  if (st) {  // HGE_STAMPS: [9] this wave's steps, [10] the wait for the other waves
+    L.sdbg[0] += t1 - t0;
+    L.sdbg[1] += stamp() - t1;
+  }
   // every wave: inclusive prefix over the H bins, the first bin reaching SM
   const int lane = threadIdx.x & 63;
   int v = lane < H ? L.sHist[lane] : 0;
@@ -487,6 +498,10 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
   int lo = L.sP[c];
   dir_load<BS, NPOW>(t, L, c, lo, DirGeo<BS, NPOW>::W, lenc, pv);
   int f0 = INF32, fn = 0;  // rows fetched for the next round: [f0, f0 + fn)
+  // members of the first round from the FD table; later rounds' members are loaded
+  // by each wave right after its own poll of the previous round (below)
+  uint32_t mw[G::CW];
+  dir_members_fd<BS, NPOW>(t, d, part, d < N ? L.sP[d] : INF32, mw);
   for (int r = rlo;; r++) {
     if (r + 1 >= rcap) {
       if (c == 0 && tid == 0) {
@@ -496,14 +511,6 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
       break;
     }
     DSTAMP_START
-    uint32_t mw[G::CW];
-    if (r == rlo) dir_members_fd<BS, NPOW>(t, d, part, d < N ? L.sP[d] : INF32, mw);
-    else dir_members_mb<BS, NPOW>(mbp[r & 1], mw);
-    if (stamping) {  // diagnostics only: issue, then arrival of wave 0's member loads
-      DSTAMP(7);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      DSTAMP(8);
-    }
     if (d >= N) {
 #pragma unroll
       for (int k = 0; k < G::CW; k++) mw[k] = 0xFFFFFFFFu;
@@ -511,6 +518,7 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
     if (tid < DIR_MAXP) L.sCnt[tid] = 0;
     if (tid < 8) L.sBits[tid] = 0;
     if (tid < DirGeo<BS, NPOW>::W / 2) L.sHist[tid] = 0;
+    if (tid == 0) L.sFlag[(r + 1) & 1] = 0;  // read after the previous round's poll barrier
     __syncthreads();  // window stored, counters clear
     DSTAMP(0);
     const int Pc = L.sP[c];
@@ -554,14 +562,15 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
         pb = dir_count<BS, NPOW>(L, nxt, part, mw) >= t.SM;
       }
       if (part == 0 && d < N && pb) atomicOr(&L.sBits[d >> 5], 1u << (d & 31));
-      __syncthreads();
+      __syncthreads();  // also: every wave is done with this round's window
       if (tid < NW)
         ssc[((size_t)(r + 1) * N + c) * NW + tid] =
             (uint64_t)L.sBits[2 * tid] | ((uint64_t)L.sBits[2 * tid + 1] << 32);
     }
     DSTAMP(2);
-    // fetch the rows the next round's window [nxt, nxt + W) lacks while the
-    // other workgroups finish this round
+    // the rows the next round's window [nxt, nxt + W) lacks, into their ring slots
+    // (slots of rows below nxt: no wave reads them again; fn > 0 only if nxt is
+    // a row, and then the barrier above has passed)
     if (nxt == INF32) {
       f0 = INF32;
       fn = 0;
@@ -572,23 +581,33 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
     lo = nxt;
     dir_fetch<BS, NPOW>(t, c, f0, fn, lenc, pv);
     dir_fetch_fd<BS, NPOW>(t, L, c, f0, fn, lenc);
+    dir_store<BS, NPOW>(t, L, f0, fn, lenc, pv);
+    if (fn > DIR_CH) {  // rare: the LA rows past the first chunk (the FD rows are in flight)
+      for (int q = DIR_CH; q < fn; q += DIR_CH) {
+        dir_fetch<BS, NPOW>(t, c, f0 + q, fn - q, lenc, pv);
+        dir_store<BS, NPOW>(t, L, f0 + q, fn - q, lenc, pv);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's FD rows have landed
     DSTAMP(3);
-    // collect C_{r+1}: wave 0 polls the N granules of epoch r - rlo + 1
-    if (tid < 64) {
+    // collect C_{r+1}: every wave polls the granules (epoch r - rlo + 1) of its OWN
+    // members and, once they match, loads their staged rows for the next round
+    // right away -- the rows of early chains load while the late ones are still
+    // being selected (round 2's single polling wave let the whole 128 KB block
+    // load only after the slowest chain had published).  Each wave loads only
+    // bytes whose flags it polled itself (MI355X_MICROARCH.md, Valid forms, row 1).
+    {
       const unsigned ep = (unsigned)(r - rlo + 1);
-      gu64_t* g = gr[(r + 1) & 1];
+      const gu64_t* g = gr[(r + 1) & 1];
       unsigned spins = 0;
-      bool any = false, fail = false;
+      bool fail = false;
+      int P = INF32;
       for (;;) {
         bool ok = true;
-        any = false;
-        for (int dd = tid; dd < N; dd += 64) {
-          const unsigned long long x =
-              __hip_atomic_load(g + dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ok &= (unsigned)(x >> 32) == ep;
-          const int P = (int)(uint32_t)x;
-          L.sP[dd] = P;
-          any |= (P != INF32);
+        if (d < N) {
+          const unsigned long long x = __hip_atomic_load(g + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = (unsigned)(x >> 32) == ep;
+          P = (int)(uint32_t)x;
         }
         if (__all(ok)) break;
         if (++spins > (1u << 24)) {  // never a normal wait: co-residency failure
@@ -598,25 +617,24 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
         __builtin_amdgcn_s_sleep(1);
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      any = __ballot(any) != 0;
-      bool past = true;
-      if (stopcut)
-        for (int dd = tid; dd < N; dd += 64) past &= L.sP[dd] >= stopcut[dd];  // INF32 passes
-      past = __all(past);
-      if (tid == 0) {
-        L.s_stop = fail ? 2 : (any ? 0 : 1);
-        L.s_past = past ? 1 : 0;
-        if (fail) atomicOr(err, 1);
-      }
+      if (part == 0 && d < N) L.sP[d] = P;
+      const bool any = __ballot(d < N && P != INF32) != 0;
+      const bool notpast = stopcut && __ballot(part == 0 && d < N && P < stopcut[d]) != 0;  // INF32 passes
+      if ((threadIdx.x & 63) == 0 && (any || notpast || fail))
+        atomicOr(&L.sFlag[(r + 1) & 1], (any ? 1 : 0) | (notpast ? 2 : 0) | (fail ? 4 : 0));
+      if (fail && (threadIdx.x & 63) == 0) atomicOr(err, 1);
+      if (!fail) dir_members_mb<BS, NPOW>(mbp[(r + 1) & 1], mw);
     }
-    __syncthreads();  // every probe of this round has read the window
+    __syncthreads();  // every wave has polled (and stored its window rows)
     DSTAMP(4);
-    if (L.s_stop) {
-      if (L.s_stop == 1 && c == 0 && tid == 0) rstate[0] = hist ? r + 2 : max(rstate[0], r + 1);
+    const int fl = L.sFlag[(r + 1) & 1];
+    const int stop = (fl & 4) ? 2 : ((fl & 1) ? 0 : 1);
+    if (stop) {
+      if (stop == 1 && c == 0 && tid == 0) rstate[0] = hist ? r + 2 : max(rstate[0], r + 1);
       break;
     }
     if (stopcut) {
-      if (extra_left < 0 && L.s_past) extra_left = extra;
+      if (extra_left < 0 && !(fl & 2)) extra_left = extra;
       if (extra_left >= 0 && extra_left-- == 0) {
         if (c == 0 && tid == 0) {
           rstate[0] = r + 2;  // rows 0 .. r + 1
@@ -625,15 +643,6 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
         break;
       }
     }
-    dir_store<BS, NPOW>(t, L, f0, fn, lenc, pv);
-    if (fn > DIR_CH) {  // rare: the LA rows past the first chunk (the FD rows are in flight)
-      for (int q = DIR_CH; q < fn; q += DIR_CH) {
-        dir_fetch<BS, NPOW>(t, c, f0 + q, fn - q, lenc, pv);
-        dir_store<BS, NPOW>(t, L, f0 + q, fn - q, lenc, pv);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the prefetched FD rows have landed
-    DSTAMP(5);
   }
   if (stamping) {
     for (int q = 0; q < 9; q++) dbg[q] += st_acc[q];

@@ -1,6 +1,6 @@
 """Per-kernel SQ counters from one rocprofv3 PMC pass (run on the GPU box).
 
-usage: python scripts/pmc_sq.py <out_dir> [--parse-only] -- <bench args...>
+usage: python scripts/pmc_sq.py <out_dir> [--parse-only] [--counters A,B,..] -- <bench args...>
 One pass of 8 SQ counters over `python3 bench.py <bench args>` with --kernel-trace
 only; prints, per kernel and launch, waves, wave-cycles, the share of wave-cycles
 spent waiting on an instruction dependency (SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES) and
@@ -21,9 +21,12 @@ def main():
     out_dir = sys.argv[1]
     bench_args = sys.argv[sys.argv.index("--") + 1:] if "--" in sys.argv else []
     parse_only = "--parse-only" in sys.argv
+    counters = COUNTERS
+    if "--counters" in sys.argv:
+        counters = sys.argv[sys.argv.index("--counters") + 1].split(",")
     d = os.path.join(out_dir, "sq")
     if not parse_only:
-        cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--kernel-trace", "--pmc"] + COUNTERS + [
+        cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--kernel-trace", "--pmc"] + counters + [
             "--output-format", "csv", "-d", d, "-o", "pmc", "--", "python3", "bench.py",
             "--no-cpu-baseline", "--profile-steps", "1", "--ramp-s", "0"] + bench_args
         subprocess.check_call(cmd, cwd=ROOT)
@@ -42,7 +45,11 @@ def main():
     rows.sort(reverse=True)
     print(f"{'kernel':40s} {'launch':>6s} {'waves':>8s} {'wavecyc':>10s} {'wait%':>6s} "
           f"{'valu/w':>7s} {'vmem/w':>7s} {'salu/w':>7s} {'lds/w':>6s} {'gpu_cyc':>9s}")
+    extra = [c for c in counters if c not in COUNTERS]
     for wc, name, n, a in rows[:30]:
+        if extra:
+            print(f"{name[:40]:40s} " + " ".join(f"{c}={a.get(c, 0):.0f}" for c in ["SQ_WAVES", "SQ_WAVE_CYCLES"] + extra))
+            continue
         w = max(a.get("SQ_WAVES", 1), 1)
         print(f"{name[:40]:40s} {n:6d} {w:8.0f} {wc:10.0f} "
               f"{100 * a.get('SQ_WAIT_INST_ANY', 0) / max(wc, 1):6.1f} "
