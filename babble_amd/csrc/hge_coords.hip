@@ -373,9 +373,12 @@ __global__ void __launch_bounds__(256) k_transpose(Tables t, const int32_t* LAT_
 // The timestamp gathers sit in the read phase, where a wave walks one chain j
 // along q and FD is non-decreasing: neighbouring lanes read neighbouring tsch
 // cells of that chain (a few cache lines per wave), not one chain per lane.
+// tlo/thi (a split part, may be null): the timestamp rows are written for chain
+// positions [tlo_c, thi_c) only -- the part's own candidates; FD rows for all.
 template <typename FT>
 __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const FT* FDT, const int32_t* plo,
-                                                         const int32_t* len) {
+                                                         const int32_t* len, const int32_t* tlo,
+                                                         const int32_t* thi) {
   __shared__ int32_t tile[64][65];
   __shared__ int32_t toff[64][65];  // the offsets (INT32_MIN: outside int32)
   const int N = t.N;
@@ -386,6 +389,7 @@ __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const FT* FDT
   // instead of one re-read per source chain.  Position tiles past gridDim.z loop.
   const int a = blockIdx.x;  // source chain c
   const int pend = len[a];
+  const int ts0 = tlo ? tlo[a] : 0, ts1 = thi ? thi[a] : pend;
   const int c0 = blockIdx.y * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
   for (int p0 = plo[a] + blockIdx.z * 64; p0 < pend; p0 += gridDim.z * 64) {
@@ -410,10 +414,11 @@ __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const FT* FDT
         }
       }
       int64_t tv[CH];
+      const bool tson = p0 + tx >= ts0 && p0 + tx < ts1;
 #pragma unroll
       for (int i = 0; i < CH; i++) {
         const int jj = c0 + ty + 4 * (h + i);
-        tv[i] = t.tsch[(size_t)(jj < N ? jj : 0) * ccap + (kv[i] != INF32 ? kv[i] : 0)];
+        tv[i] = tson ? t.tsch[(size_t)(jj < N ? jj : 0) * ccap + (kv[i] != INF32 ? kv[i] : 0)] : own;
       }
 #pragma unroll
       for (int i = 0; i < CH; i++) {
@@ -427,16 +432,17 @@ __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const FT* FDT
     const int NT = (N + 63) >> 6;
     for (int r = ty; r < 64; r += 4) {  // wave ty writes rows r: the 64 columns of one row each time
       const int q = p0 + r, jj = c0 + tx;
+      const bool tsrow = q >= ts0 && q < ts1;  // wave-uniform
       bool esc = false;
       if (q < pend && jj < N) {
         const size_t o = rowoff(t, a, q) + jj;
         const int32_t dv = toff[tx][r];
         esc = dv == INT32_MIN;  // a real offset lies in [-INT32_MAX, INT32_MAX]
         t.FD[o] = tile[tx][r];
-        t.FDTD[o] = dv;
+        if (tsrow) t.FDTD[o] = dv;
       }
       const bool any = __ballot(esc) != 0;
-      if (tx == 0 && q < pend) t.FDTW[((size_t)a * ccap + q) * NT + blockIdx.y] = any ? 1 : 0;
+      if (tx == 0 && q < pend && tsrow) t.FDTW[((size_t)a * ccap + q) * NT + blockIdx.y] = any ? 1 : 0;
     }
     __syncthreads();
   }

@@ -362,172 +362,4 @@ __global__ void __launch_bounds__(1024) k_la_win(Tables t, const int4* plan, int
   if (tid == 0 && anyc) *changed = 1;
 }
 
-// ---------------------------------------------------------------------------
-// The same passes with no barrier at all: the columns of LA never interact, so
-// workgroup (window w, slice s) is ONE wave that owns packed words
-// [64 s, 64 s + 64) of every row (lane = word) and walks every event of the
-// window in plan order for them: per event two LDS reads (the self-parent and
-// other-parent head words), a packed max, one LDS write and one coalesced
-// 256-byte store, event fields broadcast by readlane from the chunk's plan
-// entries (one per lane).  A level's events read no word another event of the
-// level writes, so a group of up to 8 events issues all its LDS reads before
-// its writes; different levels are kept in order by LDS's in-order issue.
-// For an event whose other-parent was its chain's head when it was inserted
-// (every event but the "risky" ones) the plan's ordering guarantees that row is
-// still the head in LDS when the event is taken.
-//
-// Convergence test per (window, slice): every lane keeps the sum of the 16-bit
-// values of all N head words it owns (updated by the difference at every
-// event); at a chunk end its wave total is the chunk's checksum.  Head rows
-// only grow from pass to pass, so equal checksums at the same chunk end mean
-// equal head rows: the rest of the window (with no risky event left) repeats
-// the previous pass exactly and the wave stops.  cks[(w * S + s) * (nck + 1)]:
-// the starting rows' checksum, then one per chunk.
-template <int NPOW, bool FULL>
-__global__ void __launch_bounds__(64) k_la_wave(Tables t, const int4* plan, int64_t n0, int64_t n1, int WN,
-                                                const int32_t* wpos, const int32_t* olen, uint32_t* cks, int nck,
-                                                const int32_t* risky, int pass, const int32_t* prev,
-                                                int32_t* changed) {
-  __shared__ uint32_t s_st[NPOW * 64];  // head rows: [chain][this slice's 64 words]
-  if (prev && *prev == 0) return;
-  const int N = t.N, W = t.NW2;
-  const int S = (W + 63) / 64;
-  const int w = blockIdx.x / S, sl = blockIdx.x - (blockIdx.x / S) * S;
-  const int64_t s0 = n0 + (int64_t)w * WN;
-  if (s0 >= n1) return;
-  const int64_t s1 = min(n1, s0 + (int64_t)WN);
-  const int lane = threadIdx.x;
-  const int wd = sl * 64 + lane;  // the packed word this lane owns
-  const bool live = FULL || wd < W;  // FULL: W % 64 == 0, every lane owns a word
-  uint32_t* ck = cks + (size_t)blockIdx.x * (nck + 1);
-  // starting rows (pass 1: a new row of another window is its own column only)
-  uint32_t T = 0;  // sum of this lane's head halves
-  int wp[NPOW / 64], ol[NPOW / 64];  // chain l + 64 q: head before the window + 1, olen
-#pragma unroll
-  for (int q = 0; q < NPOW / 64; q++) {
-    const int c = q * 64 + lane;
-    wp[q] = c < N ? wpos[(size_t)w * N + c] : 0;
-    ol[q] = c < N ? olen[c] : 0;
-  }
-  for (int c0 = 0; c0 < NPOW; c0 += 16) {
-    if (c0 >= N) break;
-    uint32_t v[16];
-#pragma unroll
-    for (int u = 0; u < 16; u++) {  // 16 head rows in flight
-      const int c = c0 + u;
-      const int hp = __builtin_amdgcn_readlane(wp[c >> 6], c & 63) - 1;
-      const int oc = __builtin_amdgcn_readlane(ol[c >> 6], c & 63);
-      v[u] = 0;
-      if (c < N && hp >= 0 && live) {
-        if (hp < oc || pass > 1) v[u] = t.LA16[((size_t)c * t.ccap + hp) * W + wd];
-        else v[u] = (wd == (c >> 1)) ? (uint32_t)(hp + 1) << ((c & 1) * 16) : 0u;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 16; u++) {
-      s_st[(c0 + u) * 64 + lane] = v[u];
-      T += (v[u] & 0xFFFFu) + (v[u] >> 16);
-    }
-  }
-  const int rl = risky[w];
-  bool anyc = false;
-  {
-    uint32_t tot = T;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) tot += __shfl_xor(tot, off);
-    if (pass > 1) {
-      const bool same = tot == ck[0];
-      anyc = !same;
-      if (same && rl < s0) return;  // same starting rows, nothing risky: the rows stand
-    }
-    if (lane == 0) ck[0] = tot;
-  }
-  int4 cur = make_int4(-1, 0, -1, 0), nx = make_int4(-1, 0, -1, 0);
-  if (s0 + lane < s1) nx = plan[s0 - n0 + lane];
-  int chunk = 0;
-  for (int64_t cs = s0; cs < s1; cs += LW_K, chunk++) {
-    const int ne = (int)min((int64_t)LW_K, s1 - cs);
-    cur = nx;
-    if (cs + LW_K + lane < s1) nx = plan[cs + LW_K - n0 + lane];  // next chunk, in flight
-    // level boundaries of the sorted entries
-    const int lv = lane < ne ? (cur.x >> 16) & 0xFF : 0x7FFF;
-    const int lp = __shfl(lv, lane > 0 ? lane - 1 : 0);
-    uint64_t starts = __ballot(lane < ne && (lane == 0 || lv != lp));
-    const bool risky_chunk = __ballot(lane < ne && ((cur.x >> 24) & LW_RISKY)) != 0;
-    const int ea = cur.x & 0xFFFF, ek = cur.y, eo = cur.z, ep = cur.w, ef = cur.x >> 24;
-    while (starts) {
-      const int lo = __builtin_ctzll(starts);
-      starts &= starts - 1;
-      const int hi = starts ? __builtin_ctzll(starts) : ne;
-      for (int g0 = lo; g0 < hi; g0 += 8) {
-        const int m = min(8, hi - g0);
-        uint32_t sv[8], ov[8];
-        int aa[8], kk[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-          if (u < m) {
-            const int j = g0 + u;
-            const int a = __builtin_amdgcn_readlane(ea, j), k = __builtin_amdgcn_readlane(ek, j);
-            const int opc = __builtin_amdgcn_readlane(eo, j), opp = __builtin_amdgcn_readlane(ep, j);
-            const int fl = __builtin_amdgcn_readlane(ef, j);
-            aa[u] = a;
-            kk[u] = k;
-            sv[u] = s_st[a * 64 + lane];
-            uint32_t o = 0;
-            if (opc >= 0 && live) {
-              if (!(fl & LW_RISKY)) {
-                o = s_st[opc * 64 + lane];  // the other-parent is its chain's head
-              } else {
-                const uint32_t* src = t.LA16 + ((size_t)opc * t.ccap + opp) * W + wd;
-                if (opp < olen[opc]) {
-                  o = *src;  // old, final
-                } else if (fl & LW_INWIN) {
-                  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's own earlier store
-                  o = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                } else if (pass == 1) {
-                  o = (wd == (opc >> 1)) ? (uint32_t)(opp + 1) << ((opc & 1) * 16) : 0u;
-                } else {
-                  o = *src;  // another window's row: a lower bound
-                }
-              }
-            }
-            ov[u] = o;
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-          if (u < m && live) {
-            const int a = aa[u], k = kk[u];
-            u16x2_t v = __builtin_elementwise_max(__builtin_bit_cast(u16x2_t, sv[u]),
-                                                  __builtin_bit_cast(u16x2_t, ov[u]));
-            if (wd == (a >> 1))
-              v = __builtin_elementwise_max(v, __builtin_bit_cast(u16x2_t, (uint32_t)(k + 1) << ((a & 1) * 16)));
-            const uint32_t nv = __builtin_bit_cast(uint32_t, v);
-            // the head word grows from sv to nv: both halves without borrow
-            T += ((nv & 0xFFFFu) + (nv >> 16)) - ((sv[u] & 0xFFFFu) + (sv[u] >> 16));
-            s_st[a * 64 + lane] = nv;
-            t.LA16[((size_t)a * t.ccap + k) * W + wd] = nv;
-          }
-        }
-      }
-    }
-    if (risky_chunk) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // the chunk's checksum against the previous pass's at the same point
-    uint32_t tot = T;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) tot += __shfl_xor(tot, off);
-    bool stop = false;
-    if (pass > 1 && chunk + 1 <= nck) {
-      const bool same = tot == ck[1 + chunk];
-      anyc |= !same;
-      stop = same && rl < cs + LW_K;
-    } else {
-      anyc = true;
-    }
-    if (lane == 0 && chunk + 1 <= nck) ck[1 + chunk] = tot;
-    if (stop) break;
-  }
-  if (lane == 0 && anyc) *changed = 1;
-}
-
 }  // namespace hge

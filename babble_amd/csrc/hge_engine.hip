@@ -158,7 +158,6 @@ struct hge_engine {
   // coordinate sweeps: transposed tables and scratch
   int n_sweeps = 0;
   DBuf<int32_t> d_LAT, d_FDT, s_chg, s_bar, s_dirty;
-  DBuf<uint16_t> d_FDT16;  // N > 128 on the direct rounds path: FDT as uint16 (INF = 0xFFFF)
   // windowed lastAncestors (hge_coords_win.hip): chunk plans, row sums, starting rows
   DBuf<int4> s_lwplan;
   DBuf<uint32_t> s_lwsum, s_lwinit;
@@ -176,7 +175,7 @@ struct hge_engine {
   DBuf<uint64_t> s_H;                // speculative walk: epoch-tagged histories
   DBuf<int32_t> s_hn, s_hres;        // rows written + progress hints, merge results
   uint32_t walk_epoch = 0;
-  int walk_chk[2] = {448, 2};        // checker threads, poll pause (HGE_WALK_CHK="n,s")
+  int walk_chk[2] = {448, 2};        // checker threads, poll pause
   bool coop_checked = false;
   int coop_nb = 0, coop_ncu = 0, coop_spec_nb = -1, coop_spec_bs = 0;
   const void* coop_spec_fn() const {
@@ -211,6 +210,7 @@ struct hge_engine {
   int32_t *k_rs = nullptr, *k_len = nullptr, *k_plo = nullptr, *k_qlo = nullptr, *k_lo = nullptr;
   int2* k_segs = nullptr;
   int32_t* k_segbase = nullptr;
+  int32_t* k_fd = nullptr;  // split: the candidates' chain positions [lo N, hi N)
   bool und_fresh = false;  // the candidate list is every event of a fresh replay
   float stage_ms[7] = {};
 
@@ -273,7 +273,7 @@ struct hge_engine {
     ensure_events(c0);
     ensure_ccap(c0 / N + c0 / (8 * N) + 64);
     ensure_rcap(c0 / (2 * N) + 64);
-    s_small.need(8);
+    s_small.need(16);
   }
 
   void prof_begin(const char* name) {
@@ -352,7 +352,6 @@ struct hge_engine {
     d_ts.free_();
     d_FDTD.free_();
     d_FDTW.free_();
-    d_FDT16.free_();
     d_cts.free_();
     s_cts.free_();
     d_S.free_();
@@ -487,8 +486,7 @@ struct hge_engine {
     // 16/32 columns for the LDS walk; rebuilt from the frontier on, never kept
     if (N <= 32) d_FSS.need((size_t)N * nc * std::max(N, 16));
     if (!sweep16()) grow_chain_table(d_LAT, nc, false, false);  // rebuilt per batch from LA
-    if (fdt16()) grow_chain_table(d_FDT16, nc, true, false);  // persistent: FD in run layout
-    else grow_chain_table(d_FDT, nc, true, false);
+    grow_chain_table(d_FDT, nc, true, false);  // persistent: FD in run layout
     ccap = (int)nc;
   }
 
@@ -707,6 +705,54 @@ struct hge_engine {
   std::vector<uint64_t> ext_ssc;
   DBuf<int32_t> s_hist, s_hstate;
   DBuf<uint64_t> s_hssc;
+  // One hashgraph sharded across GPUs by time (hge_split_plan): part
+  // p owns the events [a_p, a_{p+1}) and the calls [cb_p, cb_{p+1}).  Every part
+  // computes the coordinates and walks the rounds recurrence (sequential: it cannot
+  // be split exactly); part p then decides the fame of the rounds whose
+  // first witness it owns and commits the events its calls receive (candidates from
+  // cand_lo_p, the only FD timestamp rows it writes), and the parts exchange fame
+  // decisions and ordered slices through the caller's all-gather (hge_split_exchange).
+  struct SplitPlan {
+    int part = 0, nparts = 0;
+    std::vector<int64_t> a;     // event bounds, nparts + 1
+    std::vector<int32_t> cb;    // call bounds, nparts + 1
+    std::vector<int64_t> clo;   // first candidate of every part
+  } sp;
+  bool sp_active = false;  // during hge_split_run
+  bool split_on() const { return sp_active && sp.nparts > 1; }
+  hge_exchange_fn x_fn = nullptr;
+  void* x_ctx = nullptr;
+  DBuf<int32_t> s_sord;   // split: every part's ordered ids
+  DBuf<int64_t> s_soff;   // split: their offsets
+  // a device buffer of nparts slots of `bytes` (the caller's memory: its collectives
+  // write into it), then the all-gather: this part's slot is filled and the stream drained
+  void* x_buf(int64_t bytes) {
+    sync();  // the caller may hand out (or move) the memory of the previous exchange
+    void* b = nullptr;
+    if (!x_fn) throw EngineError(HGE_ERR_ARG, "split replay: no exchange (hge_split_exchange)");
+    if (x_fn(x_ctx, 0, bytes, &b) != 0 || !b) throw EngineError(HGE_ERR_DEVICE, "split exchange: no buffer");
+    return b;
+  }
+  void x_gather(int64_t bytes, void* b) {
+    sync();
+    if (x_fn(x_ctx, 1, bytes, &b) != 0) throw EngineError(HGE_ERR_DEVICE, "split exchange failed");
+  }
+  // fame rounds of part g: the pr_* indices [k_lo, k_hi) whose round's first witness
+  // lies in the part's events (h_minw is ascending in the round)
+  void split_rounds_of(int g, const std::vector<int32_t>& pr_round, int& k_lo, int& k_hi) const {
+    const int nr = (int)pr_round.size();
+    auto first_at = [&](int64_t ev) {
+      int lo = 0, hi = nr;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((int64_t)h_minw[pr_round[mid]] < ev) lo = mid + 1;
+        else hi = mid;
+      }
+      return lo;
+    };
+    k_lo = g == 0 ? 0 : first_at(sp.a[g]);
+    k_hi = g == sp.nparts - 1 ? nr : first_at(sp.a[g + 1]);
+  }
   int64_t cs_n0 = 0, cs_n1 = 0;
   int cs_tot0 = 0;
   void coords() {
@@ -721,9 +767,8 @@ struct hge_engine {
     // control block (one upload): round state, chain lengths, transpose bounds,
     // fss offsets of a fresh walk and the sweep segments
     // segment length: latency-bound sweeps (small N) like short segments, bandwidth-bound
-    // ones (large N) long ones (fewer stale carries); HGE_SEG overrides
-    static const int SEG_ENV = getenv("HGE_SEG") ? std::max(1, std::min(64, atoi(getenv("HGE_SEG")))) : 0;
-    const int SEG = SEG_ENV ? SEG_ENV : (N <= 32 ? 16 : 64);
+    // ones (large N) long ones (fewer stale carries)
+    const int SEG = N <= 32 ? 16 : 64;
     std::vector<int2>& segs = h_segs;
     segs.clear();
     int maxnew = 0;
@@ -734,16 +779,25 @@ struct hge_engine {
     // position-major order: workgroups are dispatched roughly in index order, so
     // early positions of every chain are swept first and later segments read
     // rows already updated in this sweep (Gauss-Seidel in time order)
-    if (!getenv("HGE_SEG_CHAIN_MAJOR"))
-      std::stable_sort(segs.begin(), segs.end(),
+    std::stable_sort(segs.begin(), segs.end(),
                        [](const int2& a, const int2& b) { return a.y < b.y; });
     bool fresh = R == 0;
     for (int c = 0; c < N; c++) fresh = fresh && coords_len[c] == 0;
     const size_t o_len = 4, o_plo = o_len + 2 * N, o_qlo = o_plo + N, o_lo = o_qlo + N;
     const size_t o_seg = (o_lo + 2 * N + 1 + 1) & ~(size_t)1;
     const size_t o_sb = o_seg + 2 * segs.size();  // chain-major segment bases (sweep skipping)
+    const size_t o_fd = o_sb + N;  // split: the chain positions of the part's candidates
     std::vector<int32_t>& kc = h_kctl;
-    kc.assign(o_sb + N, 0);
+    kc.assign(o_fd + 2 * N, 0);
+    if (split_on()) {
+      // FD timestamp rows (the median's input) of the ids [cand_lo, the part's end)
+      const int64_t A = sp.clo[sp.part], B = sp.a[sp.part + 1];
+      for (int c = 0; c < N; c++) {
+        const std::vector<int32_t>& ch = h_chain[c];
+        kc[o_fd + c] = (int)(std::lower_bound(ch.begin(), ch.end(), (int32_t)A) - ch.begin());
+        kc[o_fd + N + c] = (int)(std::lower_bound(ch.begin(), ch.end(), (int32_t)B) - ch.begin());
+      }
+    }
     kc[0] = R;  // rstate: {R, overflow}, new-witness count
     int tot0 = 0;
     for (int c = 0; c < N; c++) {
@@ -768,6 +822,7 @@ struct hge_engine {
     k_lo = s_kctl.p + o_lo;
     k_segs = (int2*)(s_kctl.p + o_seg);
     k_segbase = s_kctl.p + o_sb;
+    k_fd = split_on() ? s_kctl.p + o_fd : nullptr;
     KLAUNCH(k_chain_fill, dim3(div_up((int)(n1 - n0), 256)), dim3(256), 0, st, t, (int)n0, (int)n1);
     coords_sweep(t, (int)segs.size(), SEG, maxnew, fresh);
     cs_pending = true;
@@ -906,13 +961,6 @@ struct hge_engine {
   // state: one per ~192 positions of the shortest chain, up to 32 (HGE_WALKERS
   // overrides; 0 or 1 = the sequential walk).  Short graphs walk sequentially.
   int spec_walkers(int maxlen) {
-    if (const char* ck = getenv("HGE_WALK_CHK")) {
-      int a = 448, b = 2;
-      if (sscanf(ck, "%d,%d", &a, &b) == 2) {
-        walk_chk[0] = std::max(64, std::min(896, a / 64 * 64));
-        walk_chk[1] = std::max(0, std::min(64, b));
-      }
-    }
     const char* ev = getenv("HGE_WALKERS");  // read per call: the tests vary it
     const int env = ev ? atoi(ev) : -1;
     int minlen = INT32_MAX;
@@ -947,11 +995,9 @@ struct hge_engine {
   // N-workgroup walkers as stay co-resident, up to 8; HGE_COOP_WALKERS overrides
   // (read per call: the tests vary it; 0 or 1 = the sequential kernel alone).
   int coop_walkers() {
-    // walker block size (HGE_COOP_SPEC_BS): 512 threads x 2 per CU at N <= 64, 1024 x 1
-    // above (means over seeds 1-3, profiles/r01v_specbs: 113.3 vs 106.4M ev/s at 64/1M,
-    // 60.8 vs 62.9M at 128/1M)
-    const char* bs = getenv("HGE_COOP_SPEC_BS");
-    const int sbs = bs ? (atoi(bs) == 1024 ? 1024 : 512) : (N > 64 ? 1024 : COOP_SPEC_BS);
+    // walker block size: 512 threads x 2 per CU at N <= 64, 1024 x 1 above (means over
+    // seeds 1-3, profiles/r01/specbs: 113.3 vs 106.4M ev/s at 64/1M, 60.8 vs 62.9M at 128/1M)
+    const int sbs = N > 64 ? 1024 : COOP_SPEC_BS;
     if (sbs != coop_spec_bs) {
       coop_spec_bs = sbs;
       HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&coop_spec_nb, coop_spec_fn(), sbs, 0));
@@ -963,7 +1009,6 @@ struct hge_engine {
     // above N = 128 only 2 walkers fit, and the 512-thread sequential kernel is faster
     // than 2 walkers sharing each CU (22.5 vs 33.6 ms at 256/2M, profiles/r01r_*)
     int nw = ev ? atoi(ev) : (minlen >= 1024 && N <= 128 ? 8 : 0);
-    if (fdt16()) nw = 0;  // the walkers gather from the int32 FDT table
     nw = std::min(nw, cap);
     return nw >= 2 ? nw : 0;
   }
@@ -974,7 +1019,6 @@ struct hge_engine {
   // residency as a cooperative one (MI355X_MICROARCH.md, Residency), and
   // hipLaunchCooperativeKernel puts the work on a separate device queue whose
   // teardown at process exit crashed under rocprofv3 (profiles/r02_exit_segv.md).
-  // HGE_COOP_LAUNCH=1 restores the cooperative launch.
   // Every such launch first checks, for the exact kernel instantiation and block
   // size, that the whole grid fits on the device at once; a grid that cannot be
   // co-resident is refused before anything is written.  The caller holds
@@ -998,8 +1042,6 @@ struct hge_engine {
       throw EngineError(HGE_ERR_DEVICE, "frontier grid of " + std::to_string(blocks) + " workgroups x " +
                                             std::to_string(bs) + " threads cannot be co-resident (" +
                                             std::to_string(nb) + " per CU x " + std::to_string(n_cu()) + " CUs)");
-    static const bool coop = getenv("HGE_COOP_LAUNCH") && atoi(getenv("HGE_COOP_LAUNCH")) == 1;
-    if (coop) return hipLaunchCooperativeKernel(fn, grid, block, args, 0, st);
     return hipLaunchKernel(fn, grid, block, args, 0, st);
   }
   static std::mutex& frontier_mutex(int dev) {
@@ -1010,12 +1052,8 @@ struct hge_engine {
 
   // Wide rounds step: strongly-see tiles on the coordinate rows
   // (hge_rounds_direct.hip) for N % 4 == 0, else the FDT-gather selection of
-  // hge_rounds_coop.hip; HGE_ROUNDS_STEP=fss forces the latter.
-  bool direct_rounds() const {
-    const char* e = getenv("HGE_ROUNDS_STEP");
-    if (e && strcmp(e, "fss") == 0) return false;
-    return (N & 3) == 0;
-  }
+  // hge_rounds_coop.hip.
+  bool direct_rounds() const { return (N & 3) == 0; }
 
 
   // rounds of a wide hashgraph: cooperative frontier kernel (hge_rounds_coop.hip)
@@ -1096,18 +1134,17 @@ struct hge_engine {
       HIPCHK(hipMemsetAsync(s_cM.p, 0xFF, (size_t)nw * sizeof(uint64_t), st));
       int64_t nev = 0;
       for (int c = 0; c < N; c++) nev += chain_len[c];
-      // guesses (measured over seeds 1-3, profiles/r01p_*): time cuts at N <= 64,
+      // guesses (measured over seeds 1-3, profiles/r01/guess128): time cuts at N <= 64,
       // alternating length/time cuts above
-      const char* ge = getenv("HGE_COOP_GUESS");
-      const int guess = ge ? atoi(ge) : (N <= 64 ? 1 : 2);
-      CoopSpec sp{s_cH.p, s_cS.p, s_cT.p, (unsigned long long*)s_cM.p, s_cn.p, nw, Hcap, TS,
+      const int guess = N <= 64 ? 1 : 2;
+      CoopSpec cs{s_cH.p, s_cS.p, s_cT.p, (unsigned long long*)s_cM.p, s_cn.p, nw, Hcap, TS,
                   coop_epoch, nev, guess};
-      void* sargs[] = {&t, &FDT, &olen, &len, &sp, &err};
+      void* sargs[] = {&t, &FDT, &olen, &len, &cs, &err};
       prof_begin("k_rounds_coop_spec");
       HIPCHK(launch_resident(coop_spec_fn(), dim3(nw * N), dim3(coop_spec_bs), sargs));
       prof_end();
       int32_t* resume = s_cn.p + 2 * nw;
-      KLAUNCH(k_coop_join, dim3(64), dim3(256), 0, st, t, sp, d_ssc.p, rstate, resume);
+      KLAUNCH(k_coop_join, dim3(64), dim3(256), 0, st, t, cs, d_ssc.p, rstate, resume);
       int32_t hres[2] = {0, 0};
       readback(&hres[0], err, 1);
       if (hres[0]) throw EngineError(HGE_ERR_DEVICE, "rounds frontier hand-off timed out");
@@ -1140,15 +1177,11 @@ struct hge_engine {
       int hmax = 0, extra = 0;
       void* dargs[] = {&t, &olen, &len, &rstate, &rlo, &Rprev, &gran, &err, &ssc, &mb, &dbg,
                        &nostart, &nohist, &hmax, &nostart, &extra};
-      // HGE_DIRECT_BS=512: 512-thread workgroups (two per CU, 32-row windows) at N > 128
-      static const int DBS = getenv("HGE_DIRECT_BS") && atoi(getenv("HGE_DIRECT_BS")) == 512 ? 512 : 1024;
-      const int bs = N > 128 ? DBS : 1024;
       const void* fn = N <= 64 ? (const void*)k_rounds_direct<1024, 64>
                      : N <= 128 ? (const void*)k_rounds_direct<1024, 128>
-                     : bs == 512 ? (const void*)k_rounds_direct<512, 256>
-                                 : (const void*)k_rounds_direct<1024, 256>;
+                                : (const void*)k_rounds_direct<1024, 256>;
       prof_begin("k_rounds_direct");
-      HIPCHK(launch_resident(fn, dim3(N), dim3(bs), dargs));
+      HIPCHK(launch_resident(fn, dim3(N), dim3(1024), dargs));
       prof_end();
     } else {
       void* args[] = {&t, &FDT, &olen, &len, &rstate, &rlo, &Rprev, &gran, &err, &ssc, &dbg};
@@ -1165,21 +1198,10 @@ struct hge_engine {
   // N > 32: lastAncestors live only in the packed 16-bit table (chains are capped at
   // 65,534 events there); the int32 LA rows exist for N <= 32
   bool sweep16() const { return N > 32; }
-  // HGE_FDT16=1: the firstDescendants runs table as uint16 where nothing but the FD
-  // transpose reads it (N > 128, direct rounds: no FDT-gather walkers).  Measured at
-  // 256/10M: the runs kernel 6.7 -> 5.2 ms but the transpose's 2-byte loads 8.1 -> 13.3 ms,
-  // so int32 stays the default.
-  bool fdt16() const {
-    static const bool on = getenv("HGE_FDT16") && atoi(getenv("HGE_FDT16")) == 1;
-    return on && N > 128 && direct_rounds();
-  }
 
   // 32 < N <= 256: lastAncestors by windowed exact propagation (hge_coords_win.hip)
-  // instead of the sweeps; HGE_LA_WIN=0 keeps the sweeps
-  bool la_windows() const {
-    const char* e = getenv("HGE_LA_WIN");
-    return N > 32 && N <= 256 && !(e && atoi(e) == 0);
-  }
+  // instead of the sweeps
+  bool la_windows() const { return N > 32 && N <= 256; }
 
   // passes over windows of the new ids until one changes no row (n_sweeps = passes
   // run); one window is exact in its first pass (its starting rows are final)
@@ -1188,23 +1210,18 @@ struct hge_engine {
     const int32_t* len = k_len + N;
     const int64_t n0 = n_coords, n1 = n_events, ne = n1 - n0;
     const int npow = N <= 64 ? 64 : N <= 128 ? 128 : 256;
-    // k_la_win (default): one 1024-thread workgroup per window; HGE_LW_KERNEL=wave:
-    // k_la_wave, one wave per (window, 64-word slice), npow x 256 B of LDS each
-    const bool BLOCK = !(getenv("HGE_LW_KERNEL") && strcmp(getenv("HGE_LW_KERNEL"), "wave") == 0);
-    const int W = t.NW2, S = (W + 63) / 64;
-    static const int64_t WMIN = getenv("HGE_LW_MIN") ? std::max(64, atoi(getenv("HGE_LW_MIN"))) : 4096;
-    const int per_cu = BLOCK ? (npow == 256 ? 1 : 2) : std::max(1, std::min(8, (160 * 1024) / (npow * 256 + 512) / S));
+    // k_la_win: one 1024-thread workgroup per window (a barrier-free wave-per-slice
+    // variant measured 2x slower: DESIGN.md §4.1)
+    const int W = t.NW2;
+    const int64_t WMIN = 4096;  // ids per window at least
+    const int per_cu = npow == 256 ? 1 : 2;
     int64_t G = std::min<int64_t>((int64_t)n_cu() * per_cu, std::max<int64_t>(1, ne / WMIN));
     if (const char* g = getenv("HGE_LW_G")) G = std::max(1, atoi(g));
     int64_t WN = (div_up(ne, G) + LW_K - 1) / LW_K * LW_K;
     G = div_up(ne, WN);
-    const int nck = (int)(WN / LW_K);
-    if (!BLOCK) s_lwsum.need((size_t)G * S * (nck + 1));  // per (window, slice): chunk checksums
     s_lwplan.need(ne);
-    if (BLOCK) {
-      s_lwsum.need(ne);
-      s_lwinit.need((size_t)G * N * W);
-    }
+    s_lwsum.need(ne);
+    s_lwinit.need((size_t)G * N * W);
     s_lwpos.need((size_t)G * N);
     s_lwrisky.need(G);
     const int MAXP = 64;
@@ -1219,18 +1236,9 @@ struct hge_engine {
         if (p >= MAXP) throw EngineError(HGE_ERR_INTERNAL, "lastAncestors windows did not converge");
         const int32_t* prev = p > 0 ? s_chg.p + p - 1 : nullptr;
         const int pass = p + 1;
-#define LWIN(NP)                                                                                           \
-  do {                                                                                                     \
-    if (BLOCK)                                                                                             \
-      KLAUNCH(k_la_win<NP>, dim3(G), dim3(1024), 0, st, t, s_lwplan.p, n0, n1, (int)WN, s_lwpos.p, olen,   \
-              s_lwinit.p, s_lwrisky.p, s_lwsum.p, pass, prev, s_chg.p + p);                                \
-    else if (W % 64 == 0)                                                                                  \
-      KLAUNCH((k_la_wave<NP, true>), dim3(G * S), dim3(64), 0, st, t, s_lwplan.p, n0, n1, (int)WN,         \
-              s_lwpos.p, olen, s_lwsum.p, nck, s_lwrisky.p, pass, prev, s_chg.p + p);                      \
-    else                                                                                                   \
-      KLAUNCH((k_la_wave<NP, false>), dim3(G * S), dim3(64), 0, st, t, s_lwplan.p, n0, n1, (int)WN,        \
-              s_lwpos.p, olen, s_lwsum.p, nck, s_lwrisky.p, pass, prev, s_chg.p + p);                      \
-  } while (0)
+#define LWIN(NP)                                                                                         \
+  KLAUNCH(k_la_win<NP>, dim3(G), dim3(1024), 0, st, t, s_lwplan.p, n0, n1, (int)WN, s_lwpos.p, olen,     \
+          s_lwinit.p, s_lwrisky.p, s_lwsum.p, pass, prev, s_chg.p + p)
         if (npow == 64) LWIN(64);
         else if (npow == 128) LWIN(128);
         else LWIN(256);
@@ -1259,8 +1267,8 @@ struct hge_engine {
     const int MAXSW = 4096;
     s_chg.need(MAXSW);
     const bool p16 = sweep16();
-    // skip segments whose inputs did not change in the previous sweep (HGE_SWEEP_SKIP=0: off)
-    static const bool SKIP = !(getenv("HGE_SWEEP_SKIP") && atoi(getenv("HGE_SWEEP_SKIP")) == 0);
+    // skip segments whose inputs did not change in the previous sweep
+    const bool SKIP = true;
     if (p16 && la_windows()) {
       la_windows_run(t);
     } else {
@@ -1321,12 +1329,8 @@ struct hge_engine {
     }
     if (p16) {
       // LA16 -> the int32 LA rows and the FDT runs from the same tiles (no LAT)
-      if (fdt16())
-        KLAUNCH((k_la16_rows_runs<uint16_t>), dim3(div_up(maxnew + 1, 64), div_up(N, 64), N), dim3(256), 0, st,
-                t, d_FDT16.p, k_plo, olen, len);
-      else
-        KLAUNCH((k_la16_rows_runs<int32_t>), dim3(div_up(maxnew + 1, 64), div_up(N, 64), N), dim3(256), 0, st,
-                t, d_FDT.p, k_plo, olen, len);
+      KLAUNCH((k_la16_rows_runs<int32_t>), dim3(div_up(maxnew + 1, 64), div_up(N, 64), N), dim3(256), 0, st, t,
+              d_FDT.p, k_plo, olen, len);
     } else {
       // LA -> LAT for positions [olen-1, len), then the runs of the new events (and
       // the new positions with no descendant yet)
@@ -1344,13 +1348,11 @@ struct hge_engine {
     }
     int span = 1;
     for (int c = 0; c < N; c++) span = std::max(span, chain_len[c] - qlo[c]);
+    // (a split part writes the timestamp rows of its own candidates only)
     if (N > 16)
-      if (fdt16())
-        KLAUNCH((k_fd_transpose_ts<uint16_t>), dim3(N, div_up(N, 64), std::min(div_up(span, 64), 65535)), dim3(256),
-                0, st, t, (const uint16_t*)d_FDT16.p, k_qlo, len);
-      else
-        KLAUNCH((k_fd_transpose_ts<int32_t>), dim3(N, div_up(N, 64), std::min(div_up(span, 64), 65535)), dim3(256),
-                0, st, t, (const int32_t*)d_FDT.p, k_qlo, len);
+      KLAUNCH((k_fd_transpose_ts<int32_t>), dim3(N, div_up(N, 64), std::min(div_up(span, 64), 65535)), dim3(256),
+              0, st, t, (const int32_t*)d_FDT.p, k_qlo, len, (const int32_t*)k_fd,
+              (const int32_t*)(k_fd ? k_fd + N : nullptr));
     else
       KLAUNCH(k_transpose, dim3(div_up(span, 64), div_up(N, 64), N), dim3(256), 0, st, t, d_FDT.p,
               (int32_t*)nullptr, k_qlo, len, 1);
@@ -1377,18 +1379,25 @@ struct hge_engine {
     const bool fresh_und = und_fresh;
     und_fresh = false;
     const bool ord = do_order && n_und > 0;
-    const int ncand = (int)n_und;
+    int ncand = (int)n_und;
     int32_t* cand = d_und.p;
+    // a split part's candidates: the events [cand_lo, its end) of the fresh list (identity)
+    const bool spl = split_on() && ord && fresh_und;
+    if (spl) {
+      cand = d_und.p + sp.clo[sp.part];
+      ncand = (int)(sp.a[sp.part + 1] - sp.clo[sp.part]);
+    }
     // lowest candidate round (a fresh replay's candidates include event 0, round 0)
     int32_t mnr = 0;
-    if (ord && !fresh_und) {
+    if (ord && (!fresh_und || spl)) {
       h2d(s_small.p + 7, &kInf, 4);
       KLAUNCH(k_min_round, dim3(div_up(ncand, 256)), dim3(256), 0, st, d_round.p, cand, ncand,
               s_small.p + 7);
       readback(&mnr, s_small.p + 7, 1);
     }
     const int rr_lo = mnr + 1;
-    const int R_last = Rc[ncalls - 1];
+    // a split part's calls end at its last one: later rounds receive nothing it commits
+    const int R_last = spl ? Rc[sp.cb[sp.part + 1] - 1] : Rc[ncalls - 1];
     const int nr = ord ? std::max(0, R_last - rr_lo) : 0;
 
     // ---- DecideFame windows (host enumeration of (round, call) pairs) + control block ----
@@ -1398,8 +1407,9 @@ struct hge_engine {
     int lcr_new = lcr, c_set = -1;
     const int i_lo = lcr + 1;
     const int i_hi = Rc[ncalls - 1] - 2;  // processed rounds: i <= R_c - 2
-    static const int SPEC0 = getenv("HGE_SPEC") ? std::max(1, atoi(getenv("HGE_SPEC"))) : 3;
-    for (int SPEC = SPEC0;; SPEC *= 2) {
+    // speculative fame window: calls up to R_c <= i + 2 + SPEC, widened when a round
+    // stays undecided past it (narrower windows re-dispatch more often: slower)
+    for (int SPEC = 3;; SPEC *= 2) {
       pr_round.clear();
       pr_off.clear();
       pr_cf.clear();
@@ -1469,7 +1479,7 @@ struct hge_engine {
       s_decbit.need(npairs);
       s_LCR.need(ncalls);
       s_clast.need(nrounds);
-      fame_dispatch(0, t, nrounds, npairs, npairs * N, ncalls);
+      fame_dispatch(0, t, nrounds, npairs, ncalls, &pr_round, &pr_off);
       KLAUNCH(k_lcr_scan, dim3(1), dim3(1024), 0, st, c_Lc, ncalls, lcr, s_LCR.p, c_pr,
               c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds, s_clast.p, c_flags);
       int32_t fl[3];
@@ -1555,6 +1565,13 @@ struct hge_engine {
         s_recv.need(ncand);
         HIPCHK(hipMemsetAsync(s_recv.p, 0xFF, 4 * ncand, st));
       }
+      if (spl) {  // keep what this part's calls receive (k_split_filter)
+        const int p = sp.part;
+        const int32_t guard = p + 1 < sp.nparts ? (int32_t)sp.clo[p + 1] : INT32_MIN;
+        HIPCHK(hipMemsetAsync(s_small.p + 8, 0, 4, st));
+        KLAUNCH(k_split_filter, dim3(div_up(ncand, 256)), dim3(256), 0, st, (const int32_t*)cand, ncand,
+                s_recv.p, sp.cb[p], sp.cb[p + 1] - 1, guard, s_small.p + 8);
+      }
       // compaction + the order as call buckets (the received count stays on the
       // device: o_cnt[0])
       s_fund.need(ncand);
@@ -1579,15 +1596,13 @@ struct hge_engine {
         KLAUNCH(k_bucket_keys, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand, s_recv.p,
                 s_rr.p, s_cts.p, s_bpos.p, k1, d_rr.p, d_cts.p,
                 (unsigned long long*)(s_out.p + o_tx));
-        // buckets of 513 .. 2 * BIG_SORT keys in LDS (HGE_BIG_SORT=0: all through k_bucket_sort)
-        static const bool BIGS = !(getenv("HGE_BIG_SORT") && atoi(getenv("HGE_BIG_SORT")) == 0);
+        // buckets of 513 .. 2 * BIG_SORT keys in LDS (k_bucket_sort_big), the rest here
         KLAUNCH(k_bucket_sort, dim3(std::min(ncalls, 2048)), dim3(256), 0, st,
                 (const int32_t*)s_bpos.p, (const int32_t*)o_cc, (const int32_t*)blist,
-                (const int32_t*)nblist, k1, k2, o_ids, BIGS ? 1 : 0);
-        if (BIGS)
-          KLAUNCH(k_bucket_sort_big, dim3(std::min(ncalls, n_cu())), dim3(1024), 0, st,
-                  (const int32_t*)s_bpos.p, (const int32_t*)o_cc, (const int32_t*)blist,
-                  (const int32_t*)nblist, (const OKey*)k1, k2, o_ids);
+                (const int32_t*)nblist, k1, k2, o_ids, 1);
+        KLAUNCH(k_bucket_sort_big, dim3(std::min(ncalls, n_cu())), dim3(1024), 0, st,
+                (const int32_t*)s_bpos.p, (const int32_t*)o_cc, (const int32_t*)blist,
+                (const int32_t*)nblist, (const OKey*)k1, k2, o_ids);
         // new undetermined list (in candidate order)
         scan_large(s_fund.p, s_upos.p, ncand, o_cnt + 1);
         // scatter into the spare list (same capacity) and swap: no device copy
@@ -1602,7 +1617,7 @@ struct hge_engine {
     // ---- persist fame / LCR ----
     bool lcr_up = false;
     if (do_fame && nrounds > 0) {
-      fame_dispatch(1, t, nrounds, npairs, 0, ncalls);
+      fame_dispatch(1, t, nrounds, npairs, ncalls);
       if (lcr_new > lcr) {
         // RoundEvents(lcr_new - 1) at call c_set: events of that round minus the
         // ones inserted after that call
@@ -1614,6 +1629,12 @@ struct hge_engine {
                   (int)nfrom, (int)n_coords, r, o_cnt + 2);
         }
       }
+    }
+    bool split_done = false;
+    if (spl && got_order) {  // the parts' ordered slices, joined in call order
+      split_commit(o_cnt, o_cc, o_ids, ntxb, (const unsigned long long*)(s_out.p + o_tx), order_out, counts_out);
+      got_order = false;
+      split_done = true;
     }
     // the batch's one closing round trip (read in place from the pinned arena)
     const size_t off = d2h_pinned(s_out.p, 4 * (got_order ? o_tx + 2 * (size_t)ntxb : 8 + (size_t)ncalls));
@@ -1634,7 +1655,7 @@ struct hge_engine {
       if (counts_out)
         for (int c = 0; c < ncalls; c++) counts_out->push_back(ho[8 + c]);
       n_und = ho[1];
-    } else if (do_order && counts_out) {
+    } else if (do_order && counts_out && !split_done) {
       for (int c = 0; c < ncalls; c++) counts_out->push_back(0);
     }
     if (lcr_up) {
@@ -1642,6 +1663,89 @@ struct hge_engine {
       lcre = lcr_new - 1 >= 0 ? ho[2] : 0;
     }
     prof_collect();
+  }
+
+  // split replay: the parts' fame decisions (each part's pairs [P0, P1)) all-gathered
+  void split_exchange_dec(const std::vector<int32_t>& pr_round, const std::vector<int32_t>& pr_off, int npairs) {
+    const int G = sp.nparts, nr = (int)pr_round.size();
+    std::vector<int64_t> P0(G), P1(G);
+    int64_t mx = 1;
+    for (int g = 0; g < G; g++) {
+      int klo = 0, khi = 0;
+      split_rounds_of(g, pr_round, klo, khi);
+      P0[g] = klo < nr ? pr_off[klo] : npairs;
+      P1[g] = khi < nr ? pr_off[khi] : npairs;
+      mx = std::max(mx, P1[g] - P0[g]);
+    }
+    const int64_t bytes = (mx * N + 255) / 256 * 256;
+    uint8_t* buf = (uint8_t*)x_buf(bytes);
+    const int p = sp.part;
+    if (P1[p] > P0[p])
+      HIPCHK(hipMemcpyAsync(buf + (size_t)p * bytes, s_dec.p + (size_t)P0[p] * N, (size_t)(P1[p] - P0[p]) * N,
+                            hipMemcpyDeviceToDevice, st));
+    x_gather(bytes, buf);
+    for (int g = 0; g < G; g++)
+      if (g != p && P1[g] > P0[g])
+        HIPCHK(hipMemcpyAsync(s_dec.p + (size_t)P0[g] * N, buf + (size_t)g * bytes, (size_t)(P1[g] - P0[g]) * N,
+                              hipMemcpyDeviceToDevice, st));
+  }
+
+  // split replay: this part's ordered slice (its calls' buckets, round received,
+  // consensus timestamps, left candidates) all-gathered; every part then holds the
+  // whole order, the per-call batches and the undetermined list (the last part's)
+  void split_commit(const int32_t* o_cnt, const int32_t* o_cc, const int32_t* o_ids, int ntxb,
+                    const unsigned long long* ntx_part, std::vector<int32_t>* order_out,
+                    std::vector<int64_t>* counts_out) {
+    const int G = sp.nparts, p = sp.part;
+    int maxcalls = 0;
+    int64_t cap = 1;
+    for (int g = 0; g < G; g++) {
+      maxcalls = std::max(maxcalls, sp.cb[g + 1] - sp.cb[g]);
+      cap = std::max(cap, sp.a[g + 1] - sp.clo[g]);
+    }
+    const SplitSlot L = SplitSlot::make(maxcalls, cap);
+    const int64_t bytes = 4 * L.words;
+    int32_t* buf = (int32_t*)x_buf(bytes);
+    KLAUNCH(k_split_pack, dim3(std::min(div_up(cap, 256), 4096)), dim3(256), 0, st, o_cnt, o_cc, sp.cb[p],
+            sp.cb[p + 1] - sp.cb[p], o_ids, (const int32_t*)d_und.p, (const int32_t*)d_rr.p,
+            (const int64_t*)d_cts.p, ntx_part, ntxb, (const int32_t*)(s_small.p + 8), L,
+            buf + (size_t)p * L.words);
+    x_gather(bytes, buf);
+    // every part's header and call counts
+    std::vector<int32_t> hd((size_t)G * L.ids);
+    for (int g = 0; g < G; g++) d2h(&hd[(size_t)g * L.ids], buf + (size_t)g * L.words, 4 * (size_t)L.ids);
+    sync();
+    std::vector<int64_t> off(G + 1, 0);
+    bool bad = false;
+    unsigned long long ntx = 0;
+    for (int g = 0; g < G; g++) {
+      const int32_t* h0 = &hd[(size_t)g * L.ids];
+      bad = bad || h0[2] != 0;
+      off[g + 1] = off[g] + h0[0];
+      ntx += (unsigned long long)(uint32_t)h0[4] | ((unsigned long long)(uint32_t)h0[5] << 32);
+    }
+    if (bad) throw EngineError(HGE_ERR_SPLIT, "split replay: an event is received outside every part's range");
+    const int64_t tot = off[G];
+    s_sord.need((size_t)std::max<int64_t>(tot, 1));
+    s_soff.need((size_t)G + 1);
+    h2d(s_soff.p, off.data(), 8 * ((size_t)G + 1));
+    KLAUNCH(k_split_unpack, dim3(std::min(div_up(cap, 256), 1024), G), dim3(256), 0, st, (const int32_t*)buf, L, G,
+            (const int64_t*)s_soff.p, s_sord.p, d_rr.p, d_cts.p);
+    // the undetermined list: the last part's left candidates
+    const int nleft = hd[(size_t)(G - 1) * L.ids + 1];
+    if (nleft > 0)
+      HIPCHK(hipMemcpyAsync(d_und.p, buf + (size_t)(G - 1) * L.words + L.left, 4 * (size_t)nleft,
+                            hipMemcpyDeviceToDevice, st));
+    const size_t po = d2h_pinned(s_sord.p, 4 * (size_t)tot);
+    sync();
+    const int32_t* ids = (const int32_t*)(pin + po);
+    consensus.insert(consensus.end(), ids, ids + tot);
+    if (order_out) order_out->insert(order_out->end(), ids, ids + tot);
+    ctx += (int64_t)ntx;
+    n_und = nleft;
+    if (counts_out)
+      for (int g = 0; g < G; g++)
+        for (int c = sp.cb[g]; c < sp.cb[g + 1]; c++) counts_out->push_back(hd[(size_t)g * L.ids + 8 + (c - sp.cb[g])]);
   }
 
   void gather_rounds(const std::vector<int32_t>& ids, std::vector<int32_t>& out) {
@@ -1667,7 +1771,10 @@ struct hge_engine {
   // lanes per round in the group-scan kernels (a lane holds NW slots when N > 64)
   int group_lanes() const { return N <= 16 ? 16 : N <= 32 ? 32 : 64; }
 
-  void fame_dispatch(int which, const Tables& t, int nrounds, int npairs, int items, int ncalls) {
+  // which 0: k_fame_decide (a split part: the pairs of its rounds, then the parts'
+  // decisions all-gathered) and the per-round timeline; which 1: persist
+  void fame_dispatch(int which, const Tables& t, int nrounds, int npairs, int ncalls,
+                     const std::vector<int32_t>* pr_round = nullptr, const std::vector<int32_t>* pr_off = nullptr) {
     if (which == 1) {
       KLAUNCH(k_fame_persist, dim3(div_up((int64_t)nrounds * N, 256)), dim3(256), 0, st, t, c_pr,
               c_pr + nrounds, c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds, s_clast.p,
@@ -1675,15 +1782,37 @@ struct hge_engine {
       return;
     }
     const int G = group_lanes();
+    int k_lo = 0, k_hi = nrounds;
+    if (split_on() && pr_round) split_rounds_of(sp.part, *pr_round, k_lo, k_hi);
+    const int p0 = k_lo < nrounds && pr_off ? (*pr_off)[k_lo] : (k_lo < nrounds ? 0 : npairs);
+    const int p1 = k_hi < nrounds && pr_off ? (*pr_off)[k_hi] : npairs;
+    const int items = (p1 - p0) * N;
+    if (items > 0) {
+      switch (NW) {
+#define DCASE(B)                                                                                     \
+  case B:                                                                                            \
+    if (N == 64 * B)                                                                                 \
+      KLAUNCH((k_fame_decide<B, true>), dim3(div_up(items, 256)), dim3(256), 0, st, t, c_pr + k_lo,   \
+              c_pr + nrounds + k_lo, c_pr + 2 * nrounds + k_lo, k_hi - k_lo, p0, p1, c_nc, c_Rc,      \
+              s_dec.p);                                                                              \
+    else                                                                                             \
+      KLAUNCH((k_fame_decide<B, false>), dim3(div_up(items, 256)), dim3(256), 0, st, t, c_pr + k_lo,  \
+              c_pr + nrounds + k_lo, c_pr + 2 * nrounds + k_lo, k_hi - k_lo, p0, p1, c_nc, c_Rc,      \
+              s_dec.p);                                                                              \
+    break;
+        DCASE(1)
+        DCASE(2)
+        DCASE(3)
+        DCASE(4)
+#undef DCASE
+        default:
+          throw EngineError(HGE_ERR_INTERNAL, "unsupported N");
+      }
+    }
+    if (split_on() && pr_round) split_exchange_dec(*pr_round, *pr_off, npairs);
     switch (NW) {
 #define FCASE(B)                                                                                 \
   case B:                                                                                        \
-    if (N == 64 * B)                                                                             \
-      KLAUNCH((k_fame_decide<B, true>), dim3(div_up(items, 256)), dim3(256), 0, st, t, c_pr,      \
-              c_pr + nrounds, c_pr + 2 * nrounds, nrounds, npairs, c_nc, c_Rc, s_dec.p);         \
-    else                                                                                         \
-      KLAUNCH((k_fame_decide<B, false>), dim3(div_up(items, 256)), dim3(256), 0, st, t, c_pr,     \
-              c_pr + nrounds, c_pr + 2 * nrounds, nrounds, npairs, c_nc, c_Rc, s_dec.p);         \
     if (G == 16)                                                                                 \
       KLAUNCH((k_fame_timeline_g<16, 1>), dim3(div_up((int64_t)nrounds * 16, 256)), dim3(256), 0, \
               st, t, c_pr, c_pr + nrounds, c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds, c_nc, \
@@ -1907,6 +2036,8 @@ int hge_replay_prepare(hge_engine* h, const hge_event* ev, int64_t n_sub,
     }
   }
   h->reset_state();
+  h->sp = hge_engine::SplitPlan();  // a plan belongs to the stream it was made for
+  h->sp_active = false;
   std::vector<int32_t> idmap(n_sub, -1);
   h->replay_calls.clear();
   int64_t nc = 0;
@@ -1988,6 +2119,7 @@ static void replay_end(hge_engine* h, int64_t* n_ordered) {
 
 int hge_replay_run(hge_engine* h, int64_t* n_ordered) {
   GUARD_BEGIN
+  h->sp_active = false;
   replay_begin(h);
   replay_end(h, n_ordered);
   return HGE_OK;
@@ -1995,12 +2127,76 @@ int hge_replay_run(hge_engine* h, int64_t* n_ordered) {
 }
 
 // ---- cross-GPU split of one hashgraph's rounds walk (babble_amd/dist.py) ----
+int hge_split_plan(hge_engine* h, int32_t part, int32_t nparts, const int64_t* ev_bounds,
+                   const int32_t* call_bounds, const int64_t* cand_lo) {
+  if (!h) return HGE_ERR_ARG;
+  GUARD_BEGIN
+  if (nparts <= 1) {
+    h->sp = hge_engine::SplitPlan();
+    return HGE_OK;
+  }
+  auto bad = [&](const char* why) {
+    h->err = std::string("hge_split_plan: ") + why;
+    return HGE_ERR_ARG;
+  };
+  if (h->N <= 32 || !h->direct_rounds()) return bad("needs the wide direct rounds path");
+  if (part < 0 || part >= nparts || !ev_bounds || !call_bounds || !cand_lo) return bad("bad argument");
+  const int64_t E = h->n_events;
+  const int ncalls = (int)h->replay_calls.size();
+  if (ev_bounds[0] != 0 || ev_bounds[nparts] != E || call_bounds[0] != 0 || call_bounds[nparts] != ncalls)
+    return bad("the bounds must cover the staged stream and its calls");
+  for (int g = 0; g < nparts; g++) {
+    if (ev_bounds[g + 1] < ev_bounds[g] || call_bounds[g + 1] <= call_bounds[g])
+      return bad("bounds must ascend and every part needs a call");
+    if (cand_lo[g] < 0 || cand_lo[g] > ev_bounds[g] || cand_lo[g] >= ev_bounds[g + 1])
+      return bad("cand_lo[p] must lie in [0, ev_bounds[p]] below ev_bounds[p + 1]");
+  }
+  if (E > INT32_MAX) return bad("stream too long");
+  h->sp.part = part;
+  h->sp.nparts = nparts;
+  h->sp.a.assign(ev_bounds, ev_bounds + nparts + 1);
+  h->sp.cb.assign(call_bounds, call_bounds + nparts + 1);
+  h->sp.clo.assign(cand_lo, cand_lo + nparts);
+  return HGE_OK;
+  GUARD_END(h)
+}
+
+int hge_split_exchange(hge_engine* h, hge_exchange_fn fn, void* ctx) {
+  if (!h) return HGE_ERR_ARG;
+  h->x_fn = fn;
+  h->x_ctx = ctx;
+  return HGE_OK;
+}
+
+int hge_split_run(hge_engine* h, int64_t* n_ordered) {
+  if (!h) return HGE_ERR_ARG;
+  GUARD_BEGIN
+  if (h->sp.nparts <= 1) {
+    h->err = "hge_split_run: no split plan (hge_split_plan)";
+    return HGE_ERR_ARG;
+  }
+  if (!h->x_fn) {
+    h->err = "hge_split_run: no exchange (hge_split_exchange)";
+    return HGE_ERR_ARG;
+  }
+  struct Off {  // the plan applies to this replay only
+    hge_engine* h;
+    ~Off() { h->sp_active = false; }
+  } off{h};
+  h->sp_active = true;
+  replay_begin(h);
+  replay_end(h, n_ordered);
+  return HGE_OK;
+  GUARD_END(h)
+}
+
 int hge_split_begin(hge_engine* h) {
   GUARD_BEGIN
   if (h->N <= 32 || !h->direct_rounds()) {
     h->err = "the split walk needs the wide direct rounds path (N > 32, N % 4 == 0)";
     return HGE_ERR_ARG;
   }
+  h->sp_active = false;  // the walk-only split: every part computes everything else
   replay_begin(h);
   if (!h->cs_pending) {
     h->err = "nothing staged (hge_replay_prepare first)";
@@ -2019,7 +2215,8 @@ int hge_frontier_guess(hge_engine* h, int32_t part, int32_t nparts, int32_t* sta
   }
   // part 0: the true first frontier (every chain's first event); part p: the time
   // cut at event p * E / nparts (the first event of each chain inserted at or after it)
-  const int64_t T = h->n_events * (int64_t)part / nparts;
+  // with a split plan of nparts parts: its event bound of the part
+  const int64_t T = h->sp.nparts == nparts ? h->sp.a[part] : h->n_events * (int64_t)part / nparts;
   for (int c = 0; c < h->N; c++) {
     const std::vector<int32_t>& ch = h->h_chain[c];
     const size_t k = std::lower_bound(ch.begin(), ch.end(), (int32_t)T) - ch.begin();

@@ -861,13 +861,16 @@ __global__ void k_witness_bits(Tables t, const int32_t* newwit, const int32_t* p
 // load shared by the wave instead of 64 lanes loading the same address.
 template <int NWT, bool WP>
 __global__ void k_fame_decide(Tables t, const int32_t* pr_round, const int32_t* pr_off,
-                              const int32_t* pr_cf, int nrounds, int npairs,
+                              const int32_t* pr_cf, int nrounds, int p0, int npairs,
                               const int64_t* nc, const int32_t* Rc, uint8_t* dec) {
+  // pairs [p0, npairs): a part of a split replay decides the pairs of its rounds only
+  // (pr_* then start at its first round; pair indices stay absolute)
   const int item = blockIdx.x * blockDim.x + threadIdx.x;
   const int N = t.N, SM = t.SM;
-  if (item >= npairs * N) return;
+  if (item >= (npairs - p0) * N) return;
   int p = item / N;
   const int xd = item - p * N;
+  p += p0;
   if constexpr (WP) p = __builtin_amdgcn_readfirstlane(p);
   int lo = 0, hi = nrounds - 1;  // last round with pr_off <= p
   while (lo < hi) {
@@ -1813,7 +1816,8 @@ __global__ void k_recv_flags(const int32_t* recv_call, int ncand, int32_t* f_rec
   const bool r = rc >= 0;
   if (q < ncand) {
     if (f_recv) f_recv[q] = r;
-    f_und[q] = commit ? !r : 1;
+    // -1: not received (stays undetermined); below -1: another part's (split replay)
+    f_und[q] = commit ? rc == -1 : 1;
   }
   if (!call_counts) return;
   // neighbouring candidates are mostly received by the same call: one atomic
@@ -2195,6 +2199,99 @@ __global__ void k_set_rr(Tables t, const int32_t* cand, int ncand, const int32_t
   // one atomic per wave
   for (int o = 32; o > 0; o >>= 1) tx += __shfl_xor(tx, o);
   if ((threadIdx.x & 63) == 0 && tx) atomicAdd(ntx_sum, tx);
+}
+
+// ---------------------------------------------------------------------------
+// One hashgraph split across GPUs: part p commits the events its
+// calls [c_lo, c_hi] receive.  A candidate received before c_lo is the previous
+// part's (-2: neither ordered nor left here); one received after c_hi, or not at
+// all, is left (-1).  A left candidate below `guard` (the next part's first
+// candidate) is one no part covers: the flag makes the whole split fall back.
+// ---------------------------------------------------------------------------
+__global__ void k_split_filter(const int32_t* cand, int ncand, int32_t* recv_call, int c_lo, int c_hi,
+                               int32_t guard, int32_t* flag) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  bool bad = false;
+  if (q < ncand) {
+    int rc = recv_call[q];
+    if (rc >= 0 && rc < c_lo) rc = -2;
+    else if (rc > c_hi) rc = -1;
+    recv_call[q] = rc;
+    bad = rc == -1 && cand[q] < guard;
+  }
+  if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+// Slot of a part in the order exchange (int32 words): header [nord, nleft, flag,
+// 0, ntx lo, ntx hi, 0, 0], the counts of its calls, then ids, rr, cts (int64)
+// and the left (undetermined) ids, each region `cap` entries.
+struct SplitSlot {
+  int64_t counts, ids, rr, cts, left, words;
+  __host__ __device__ static SplitSlot make(int ncalls_max, int64_t cap) {
+    SplitSlot s;
+    s.counts = 8;
+    s.ids = (s.counts + ncalls_max + 1) & ~(int64_t)1;
+    s.rr = s.ids + cap;
+    s.cts = (s.rr + cap + 1) & ~(int64_t)1;
+    s.left = s.cts + 2 * cap;
+    s.words = (s.left + cap + 1) & ~(int64_t)1;
+    return s;
+  }
+};
+
+// pack this part's results into its slot (one grid over max(nord, nleft, ncalls));
+// block 0 also sums the per-block transaction partials and writes the header
+__global__ void k_split_pack(const int32_t* cnt, const int32_t* call_counts, int c_lo, int ncalls_p,
+                             const int32_t* ids, const int32_t* left, const int32_t* ev_rr,
+                             const int64_t* ev_cts, const unsigned long long* ntx_part, int ntxb,
+                             const int32_t* flag, SplitSlot L, int32_t* slot) {
+  const int nord = cnt[0], nleft = cnt[1];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nord; i += stride) {
+    const int x = ids[i];
+    slot[L.ids + i] = x;
+    slot[L.rr + i] = ev_rr[x];
+    ((int64_t*)(slot + L.cts))[i] = ev_cts[x];
+  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nleft; i += stride)
+    slot[L.left + i] = left[i];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ncalls_p; i += stride)
+    slot[L.counts + i] = call_counts[c_lo + i];
+  if (blockIdx.x == 0) {
+    __shared__ unsigned long long s_tx[256];
+    unsigned long long tx = 0;
+    for (int b = threadIdx.x; b < ntxb; b += blockDim.x) tx += ntx_part[b];
+    s_tx[threadIdx.x] = tx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long tot = 0;
+      for (int k = 0; k < (int)blockDim.x; k++) tot += s_tx[k];
+      slot[0] = nord;
+      slot[1] = nleft;
+      slot[2] = *flag;
+      slot[3] = 0;
+      slot[4] = (int32_t)(uint32_t)tot;
+      slot[5] = (int32_t)(uint32_t)(tot >> 32);
+      slot[6] = slot[7] = 0;
+    }
+  }
+}
+
+// every part's ordered ids into one list (part g's at off[g]) and their round
+// received / consensus timestamp into the event tables
+__global__ void k_split_unpack(const int32_t* buf, SplitSlot L, int nparts, const int64_t* off,
+                               int32_t* ids_out, int32_t* ev_rr, int64_t* ev_cts) {
+  const int g = blockIdx.y;
+  const int32_t* slot = buf + (size_t)g * L.words;
+  const int nord = slot[0];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nord;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int x = slot[L.ids + i];
+    ids_out[off[g] + i] = x;
+    ev_rr[x] = slot[L.rr + i];
+    ev_cts[x] = ((const int64_t*)(slot + L.cts))[i];
+  }
+  (void)nparts;
 }
 
 // LastCommitedRoundEvents = RoundEvents(LCR-1) at the call that set LCR

@@ -33,6 +33,12 @@ HGE_ERR_CAPACITY = -7
 HGE_ERR_TOO_LATE = -11
 HGE_ERR_NOT_FOUND = -12
 HGE_ERR_SIGNATURE = -13
+HGE_ERR_SPLIT = -14
+
+# hge_exchange_fn (include/hge.h): op 0 -> *buf = device memory for nparts slots of
+# bytes_per_part bytes; op 1 -> all-gather the slots in place
+EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
+                               ctypes.POINTER(ctypes.c_void_p))
 
 
 class HgeEvent(ctypes.Structure):
@@ -72,7 +78,7 @@ EXPORTS = [
     "hge_cache_size", "hge_participant_events", "hge_participant_event", "hge_last_from",
     "hge_diff", "hge_wire_info", "hge_read_wire_parents", "hge_parent_round", "hge_round_inc",
     "hge_round_diff", "hge_set_round", "hge_split_begin", "hge_frontier_guess",
-    "hge_frontier_walk", "hge_split_finish", "hge_frontier_rows",
+    "hge_frontier_walk", "hge_split_finish", "hge_frontier_rows", "hge_split_plan", "hge_split_exchange", "hge_split_run",
     "hge_verify_events", "hge_sha256_batch", "hge_ingest", "hge_fame_table",
 ]
 
@@ -95,6 +101,13 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"HIP engine library not built: {LIB_PATH} (run __graft_entry__.build())")
+    # torch (the collectives' plumbing, babble_amd.dist) ships its own HIP runtime; it
+    # must be mapped before this library maps /opt/rocm's, or torch's runtime finds no
+    # GPU in this process (measured on the MI355X box)
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     P = ctypes.POINTER
@@ -166,6 +179,9 @@ def lib():
     L.hge_frontier_walk.argtypes = [vp, P(i32), P(i32), i32, i32, P(i32), P(ctypes.c_uint64), P(i32), P(i32)]
     L.hge_split_finish.argtypes = [vp, P(i32), P(ctypes.c_uint64), i32, i32, P(i64)]
     L.hge_frontier_rows.argtypes = [vp, i32, i32, P(i32), P(ctypes.c_uint64)]
+    L.hge_split_plan.argtypes = [vp, i32, i32, P(i64), P(i32), P(i64)]
+    L.hge_split_run.argtypes = [vp, P(i64)]
+    L.hge_split_exchange.argtypes = [vp, EXCHANGE_FN, vp]
     u8p = P(ctypes.c_uint8)
     L.hge_verify_events.argtypes = [i64, u8p, P(i64), u8p, u8p, i32, u8p, P(i32)]
     L.hge_sha256_batch.argtypes = [i64, u8p, P(i64), i32, u8p]
@@ -270,6 +286,9 @@ class Engine:
 
     def _check(self, rc):
         if rc != 0:
+            xe, self._xerr = getattr(self, "_xerr", None), None
+            if xe is not None:
+                raise HgeError(rc, self.L.hge_last_error(self.h).decode()) from xe
             raise HgeError(rc, self.L.hge_last_error(self.h).decode())
         return rc
 
@@ -351,6 +370,7 @@ class Engine:
         cp = np.ascontiguousarray(call_points, np.int64)
         self._status = np.zeros(len(ev), np.int32)
         self._ncalls = len(cp)
+        self._calls = cp.copy()
         self._check(self.L.hge_replay_prepare(self.h, ev.ctypes.data, len(ev), _p64(cp), len(cp),
                                               _p32(self._status)))
         return self._status
@@ -367,7 +387,46 @@ class Engine:
         self._check(self.L.hge_replay_fetch(self.h, _p32(order), len(order), _p64(counts)))
         return self._status, order[:self._nordered], counts[:self._ncalls]
 
-    # --- one hashgraph split across GPUs (babble_amd.dist.split_replay) ----
+    # --- one hashgraph split across GPUs (babble_amd.dist.split_run) ----
+    def call_events(self):
+        """Events accepted at each call point of the staged replay (hge_replay_prepare)."""
+        acc = np.cumsum(self._status >= 0)
+        return acc[self._calls - 1].astype(np.int64)
+
+    def split_plan(self, part, nparts, plan=None):
+        """hge_split_plan: shard the staged replay by time (babble_amd.dist.split_plan);
+        nparts <= 1 clears the plan."""
+        if nparts <= 1 or plan is None:
+            self._check(self.L.hge_split_plan(self.h, 0, 0, None, None, None))
+            return
+        evb = np.ascontiguousarray(plan["ev_bounds"], np.int64)
+        cb = np.ascontiguousarray(plan["call_bounds"], np.int32)
+        clo = np.ascontiguousarray(plan["cand_lo"], np.int64)
+        self._check(self.L.hge_split_plan(self.h, part, nparts, _p64(evb), _p32(cb), _p64(clo)))
+
+    def split_run(self):
+        """hge_split_run: this part of the sharded replay (plan + exchange set);
+        returns the number of events ordered by the whole replay."""
+        n = ctypes.c_int64()
+        self._check(self.L.hge_split_run(self.h, ctypes.byref(n)))
+        self._nordered = n.value
+        return n.value
+
+    def set_exchange(self, fn):
+        """fn(op, bytes_per_part) -> device pointer (op 0) / None (op 1): the
+        all-gather of a split replay (hge_split_exchange)."""
+        def cb(_ctx, op, nbytes, bufp):
+            try:
+                r = fn(int(op), int(nbytes))
+                if op == 0:
+                    bufp[0] = r
+                return 0
+            except Exception as e:  # the engine fails the replay with HGE_ERR_DEVICE
+                self._xerr = e
+                return 1
+        self._xcb = EXCHANGE_FN(cb)  # kept alive with the engine
+        self._check(self.L.hge_split_exchange(self.h, self._xcb, None))
+
     def split_begin(self):
         self._check(self.L.hge_split_begin(self.h))
 

@@ -17,10 +17,16 @@ Workloads (BASELINE.json configs):
       Every graph has its own engine (HIP stream); host threads drive them
       concurrently.
 
-Multi-GPU (torch.distributed over RCCL, one process per GPU): gossip = every
-rank replays its own independent hashgraph (seed + rank), mc = every rank
-replays its share of the batch; no data-path collective.  value = events
-ordered by all ranks per step / max-over-ranks step time ("scaling": "weak").
+Multi-GPU (torch.distributed over RCCL, one process per GPU):
+  gossip (default): ONE hashgraph sharded by time across the ranks
+      (babble_amd.dist.split_run, DESIGN.md §6: every rank computes the
+      coordinates and the sequential rounds walk, then decides the fame of its
+      rounds and orders its calls' events; fame decisions and ordered slices are
+      all-gathered over RCCL), "scaling": "strong": value = the one hashgraph's
+      ordered events / max-over-ranks step time.  --replicas: every rank replays its own independent hashgraph
+      (seed + rank), no data-path collective, "scaling": "weak".
+  mc: every rank replays its share of the batch; no data-path collective
+      ("scaling": "weak").
 
 The timed steps run without per-kernel instrumentation; a separate profiled
 pass (HIP events around every launch on the engine stream) gives every
@@ -65,10 +71,9 @@ def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
       k_transpose   16N/event at N <= 16 (LA -> LAT and FDT -> FD: each reads and
                     writes 4N), 8N at 16 < N <= 32 (LA -> LAT only);
       k_fd_transpose_ts 12N/event (N > 16: FDT read, FD and the 4-byte FD
-                    timestamp offsets written; 10N with HGE_FDT16=1 above N = 128);
+                    timestamp offsets written);
       k_witness_la   8N^2 per round (frontier rows read, transposed rows written);
-      k_la16_rows_runs 6N/event (N > 32: LA16 read, the FDT runs written; 4N with
-                    HGE_FDT16=1 above N = 128);
+      k_la16_rows_runs 6N/event (N > 32: LA16 read, the FDT runs written);
       k_la_win      (2N + 20)/event (32 < N <= 256, windowed exact propagation: the
                     head rows live in LDS, so per event only the packed row is
                     written, the 16-byte plan entry read and the 4-byte row sum
@@ -87,12 +92,12 @@ def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
     if name == "k_witness_la":
         return 8 * n * n * rounds
     per_event = {"k_la_sweep": 12 * n, "k_la_clear": 4 * n, "k_transpose": 16 * n if n <= 16 else 8 * n,
-                 "k_fd_transpose_ts": (10 if os.environ.get("HGE_FDT16") == "1" and n > 128 else 12) * n,
+                 "k_fd_transpose_ts": 12 * n,
                  "k_fdt_clear": 4 * n, "k_fdt_runs": 8 * n, "k_fss": 8 * n,
                  "k_rounds_walk": 4 * n, "k_rounds_coop": 4 * n, "k_rounds_coop_spec": 4 * n,
                  "k_walk_spec": 4 * n, "k_rounds_fss": 4 * n, "k_rounds_direct": 4 * n,
-                 "k_la_clear16": 2 * n, "k_la_sweep16": 6 * n, "k_la16_rows_runs": (4 if os.environ.get("HGE_FDT16") == "1" and n > 128 else 6) * n,
-                 "k_la_win": 2 * n + 20, "k_la_wave": 2 * n + 16, "k_lw_plan": 40, "k_lw_pos": 0}
+                 "k_la_clear16": 2 * n, "k_la_sweep16": 6 * n, "k_la16_rows_runs": 6 * n,
+                 "k_la_win": 2 * n + 20, "k_lw_plan": 40, "k_lw_pos": 0}
     if name in per_event:
         return per_event[name] * events
     if name in ("k_round_received", "k_median_wave"):
@@ -258,9 +263,12 @@ def main():
     ap.add_argument("--cpu-sample-events", type=int, default=None,
                     help="CPU baseline prefix (default: 20480 at N >= 128, 100k below)")
     ap.add_argument("--profile-steps", type=int, default=1)
-    ap.add_argument("--split", action="store_true",
-                    help="gossip, N > 1: ONE hashgraph per job, its rounds walk split across the "
-                         "ranks (babble_amd.dist.split_run) instead of one replica per rank")
+    ap.add_argument("--replicas", action="store_true",
+                    help="gossip, N > 1: one independent hashgraph per rank (weak scaling) instead of "
+                         "ONE hashgraph sharded across the ranks (babble_amd.dist.split_run)")
+    ap.add_argument("--walk-only", action="store_true",
+                    help="gossip, N > 1: round 2's walk-only split (walkers from time cuts joined by row "
+                         "equality; every rank computes the rest) instead of the sharded replay")
     args = ap.parse_args()
     mc = args.workload == "mc"
     n = args.participants or (32 if mc else DEFAULT[0])
@@ -292,7 +300,7 @@ def main():
         for eng, d in zip(engines, dags):
             eng.prepare(events_array(d), schedule(len(d["creator"]), K))
     else:
-        split = args.split and world > 1
+        split = not args.replicas and world > 1
         # split: every rank stages the same stream (seed, not seed + rank)
         dags = [random_gossip(n, E, seed=args.seed + (0 if split else rank))]
         engines = [Engine(n, E, device=local_rank)]
@@ -300,15 +308,18 @@ def main():
     ingest_s = time.perf_counter() - t0
     pool = ThreadPoolExecutor(max_workers=max(1, min(args.threads, len(engines))))
 
-    split = (not mc) and args.split and world > 1
-    gather = None
+    split = (not mc) and not args.replicas and world > 1
+    gather, exchange, split_stats = None, None, {}
     if split:
-        from babble_amd.dist import split_run, torch_gather
+        from babble_amd.dist import TorchExchange, split_run, torch_gather, walk_split_run
         gather = torch_gather(dist, f"cuda:{local_rank}")
+        exchange = TorchExchange(dist, f"cuda:{local_rank}")
 
     def step():
+        if split and args.walk_only:
+            return walk_split_run(engines[0], rank, world, gather)
         if split:
-            return split_run(engines[0], rank, world, gather)
+            return split_run(engines[0], rank, world, exchange, stats=split_stats)
         if len(engines) == 1:
             return engines[0].run()
         return sum(pool.map(lambda e: e.run(), engines))
@@ -327,6 +338,7 @@ def main():
     for _ in range(args.warmup):
         step()
     sync_all()
+    f0 = split_stats.get("fallback", 0)
     t0 = time.perf_counter()
     ordered = 0
     for _ in range(args.steps):
@@ -337,7 +349,12 @@ def main():
 
     # ---- one more unprofiled replay: GPU-busy vs wall split of a step ----
     eng0 = engines[0]
-    eng0.run()
+    nfall = split_stats.get("fallback", 0) - f0
+    if split:
+        sync_all()
+        step()
+    else:
+        eng0.run()
     st_ms = eng0.stage_times()
     replay_ms = {"coords_gpu": st_ms[0], "coords_wall": st_ms[1], "consensus_gpu": st_ms[3],
                  "consensus_wall": st_ms[2], "gpu": st_ms[6], "wall": st_ms[4]}
@@ -348,7 +365,7 @@ def main():
     nprof = max(1, args.profile_steps)
     eng0.set_profiling(True)
     for _ in range(nprof):
-        eng0.run()
+        step() if split else eng0.run()
     kstats = eng0.kernel_stats()
     eng0.set_profiling(False)
     ev0 = len(dags[0]["creator"])
@@ -383,7 +400,7 @@ def main():
         if base in ("k_la_sweep", "k_la_clear", "k_transpose", "k_fss", "k_fdt_runs",
                     "k_fdt_clear", "k_rounds_coop", "k_rounds_coop_spec", "k_median_wave",
                     "k_la_clear16", "k_la_sweep16", "k_la16_rows_runs", "k_rounds_direct",
-                    "k_fd_transpose_ts", "k_witness_la", "k_la_win", "k_la_wave", "k_lw_plan"):
+                    "k_fd_transpose_ts", "k_witness_la", "k_la_win", "k_lw_plan"):
             b, pl, gbs, lpr = kernel_roofline(name)
             hbm_kernels[name] = {"achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
                                  "alg_bytes_per_launch": int(b), "launch_ms": round(pl, 4),
@@ -481,7 +498,8 @@ def main():
                         f"{n} participants, {E} submissions each, 10 forkers p=0.05 with cascades, "
                         f"RunConsensus every K={K}")
         else:
-            workload = (f"random-gossip DAG, {n} participants, {E} events per GPU, "
+            workload = (f"random-gossip DAG, {n} participants, {E} events "
+                        f"{'in one hashgraph' if split else 'per GPU'}, "
                         f"RunConsensus every K={K} events ({len(schedule(E, K))} calls)")
         cfg_key = f"{args.workload}_n{n}_e{E}_k{K}"
         line = {
@@ -499,8 +517,12 @@ def main():
             "data": "synthetic",
             "config": {"workload": workload, "participants": n, "events_per_graph": E, "k": K,
                        "graphs_per_gpu": len(engines), "ordered_per_step": tot_ordered,
-                       "parallelism": (f"split{world}: one hashgraph, rounds walk split across "
-                                       f"{world} GPUs" if split else f"replicas{world}")},
+                       "parallelism": ((f"split{world}: one hashgraph, rounds walk split across {world} GPUs"
+                                        if args.walk_only else
+                                        f"shard{world}: one hashgraph sharded by time across {world} GPUs "
+                                        f"(fame by round, round received / median / order by call; RCCL "
+                                        f"all-gathers; coordinates and the sequential rounds walk on every "
+                                        f"rank)") if split else f"replicas{world}")},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
@@ -523,6 +545,10 @@ def main():
                                       sorted(kstats.items(), key=lambda kv: -kv[1][0])},
             "kernel_launches_per_replay": {k: v[1] // nprof for k, v in kstats.items()},
         }
+        if split:
+            # timed steps that fell back to the unsplit replay (HGE_ERR_SPLIT): 0 means
+            # every timed step ran sharded
+            line["split_fallbacks"] = nfall
         if secondary is not None:
             line["secondary"] = secondary
         print(json.dumps(line), flush=True)

@@ -51,7 +51,11 @@ enum hge_status {
   HGE_ERR_INTERNAL = -10,
   HGE_ERR_TOO_LATE = -11,  /* ErrTooLate  (store.go:22): below the rolling window  */
   HGE_ERR_NOT_FOUND = -12, /* ErrKeyNotFound (store.go:21)                         */
-  HGE_ERR_SIGNATURE = -13  /* "Invalid signature"  (hashgraph.go:330-336)            */
+  HGE_ERR_SIGNATURE = -13, /* "Invalid signature"  (hashgraph.go:330-336)            */
+  /* a split replay's parts did not cover the stream (walkers that never met, or an
+   * event received outside every part's range): every part returns it together,
+   * and the caller replays unsplit (babble_amd/dist.py).  Engine-only. */
+  HGE_ERR_SPLIT = -14
 };
 
 /* Parent reference values. */
@@ -156,18 +160,45 @@ int hge_replay_run(hge_engine* h, int64_t* n_ordered);
 int hge_replay_fetch(hge_engine* h, int32_t* order_out, int64_t cap, int64_t* call_counts_out);
 
 /* ---- one hashgraph split across GPUs (babble_amd/dist.py) ------ */
-/* Every rank stages the whole stream (hge_replay_prepare), computes the
- * coordinates (hge_split_begin), then walks the rounds frontier recurrence
- *  from its own start: rank 0 from the true first frontier,
- * rank p from the time cut at p * E / nparts (hge_frontier_guess), until its
- * rows pass `stopcut` (the next rank's start) plus `extra` rows, or hmax rows.
- * The ranks all-gather their rows (N ints each) and strongly-see bits
- * (N * ceil(N/64) words each); the join follows row equalities from rank 0's
- * true trajectory (the recurrence is a function of the row alone) and
- * hge_split_finish installs the joined rows -- the sequential walk resumes from
- * the last joined row if the walk did not end -- and runs DivideRounds,
- * DecideFame and FindOrder at every call point.  Results are identical to
- * hge_replay_run.  N > 32 with N % 4 == 0 only. */
+/* Sharded replay.  Every rank stages the whole stream (hge_replay_prepare) and
+ * makes the same plan: part p owns the events [ev_bounds[p], ev_bounds[p+1]) and
+ * the calls [call_bounds[p], call_bounds[p+1]) (both ascending, covering the
+ * staged stream and its calls).  hge_split_run replays with the plan:
+ *  - every part computes the coordinates and walks the rounds frontier recurrence
+ *    (DESIGN.md §4.2): the recurrence is sequential and cannot be split exactly
+ *    (walkers started mid-stream rarely meet the true trajectory, §6); the
+ *    firstDescendants timestamp rows are written for the part's candidates only;
+ *  - DecideFame: the part decides the (round, call) pairs of the rounds whose first
+ *    witness it owns, and the parts all-gather the decisions;
+ *  - DecideRoundReceived / FindOrder: round received, consensus timestamp and the
+ *    call buckets of the candidates [cand_lo[p], ev_bounds[p+1]) that its calls
+ *    receive (cand_lo[p] <= ev_bounds[p]: events received late, from before the
+ *    part's own range), then the parts all-gather their ordered slices;
+ * every rank ends with the whole replay's state, identical to hge_replay_run.  A
+ * candidate that no part covers makes every part return HGE_ERR_SPLIT (the caller
+ * replays unsplit).  nparts <= 1 clears the plan.  N > 32 with N % 4 == 0 only.
+ * The exchange: op 0 asks the caller for device memory of nparts slots of
+ * bytes_per_part bytes (*buf, valid until the next op 0), op 1 all-gathers it in
+ * place once this part's slot is filled and the engine stream is drained; the
+ * callback returns 0, or nonzero to fail the replay.  Every part makes the same
+ * calls with the same sizes (torch.distributed all_gather_into_tensor on RCCL). */
+typedef int (*hge_exchange_fn)(void* ctx, int32_t op, int64_t bytes_per_part, void** buf);
+int hge_split_plan(hge_engine* h, int32_t part, int32_t nparts, const int64_t* ev_bounds,
+                   const int32_t* call_bounds, const int64_t* cand_lo);
+int hge_split_exchange(hge_engine* h, hge_exchange_fn fn, void* ctx);
+int hge_split_run(hge_engine* h, int64_t* n_ordered);
+
+/* Walk-only split (measured, kept for the record: DESIGN.md §6).  Every rank
+ * computes everything; the rounds walk is walked by one walker per rank from its
+ * own start: rank 0 from the true first frontier, rank p from the time cut at
+ * p * E / nparts (hge_frontier_guess), until its rows pass `stopcut` (the next
+ * rank's start) plus `extra` rows, or hmax rows.  The ranks all-gather their rows
+ * (N ints each) and strongly-see bits (N * ceil(N/64) words each); the join
+ * follows row equalities from rank 0's true trajectory (the recurrence is a
+ * function of the row alone) and hge_split_finish installs the joined rows -- the
+ * sequential walk resumes from the last joined row if the walkers did not meet
+ * (at N = 256 they rarely do) -- and runs DivideRounds, DecideFame and FindOrder
+ * at every call point.  Results are identical to hge_replay_run. */
 int hge_split_begin(hge_engine* h);
 int hge_frontier_guess(hge_engine* h, int32_t part, int32_t nparts, int32_t* start_out);
 /* rows_out: hmax * N ints (row 0 = start; INT32_MAX = no event yet), ssc_out:

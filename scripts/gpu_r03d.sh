@@ -1,0 +1,24 @@
+#!/bin/bash
+# round 3: full GPU suite (minus the new sharded split), smoke, bench, rocprofv3 stats,
+# then the sharded split tests and the walkers' convergence data
+set -o pipefail
+export TMPDIR=/tmp
+OUT=gpurun_out/${1:-r03d}
+mkdir -p $OUT
+PYT="python -u -m pytest -x -v --timeout 240 --timeout-method thread"
+timeout -k 10 900 $PYT tests -m gpu -k "not sharded" > $OUT/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -40 $OUT/pytest_gpu.log; exit 1; }
+tail -1 $OUT/pytest_gpu.log
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
+tail -1 $OUT/smoke.log
+timeout -k 10 400 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
+python -c "
+import json
+d=json.loads(open('$OUT/bench.json').read().strip().splitlines()[-1])
+print(round(d['value']/1e6,2), d['ms_per_step'], d['parity'], d['roofline']['kernel'], d['roofline']['frac'], d['cpu_baseline'])
+print(list(d['kernels_ms_per_replay'].items())[:8])"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --no-cpu-baseline --no-secondary --steps 2 --warmup 1 > $OUT/prof.log 2>&1
+echo "rocprofv3 rc=$?"
+timeout -k 10 600 $PYT tests/test_gpu_split.py -k sharded > $OUT/pytest_sharded.log 2>&1 || { echo "sharded tests failed"; tail -60 $OUT/pytest_sharded.log; exit 1; }
+tail -1 $OUT/pytest_sharded.log
+timeout -k 10 300 python -u scripts/analysis/split_converge.py 256 10000000 2 4 8 > $OUT/converge.log 2>&1 || { tail -20 $OUT/converge.log; exit 1; }
+tail -3 $OUT/converge.log

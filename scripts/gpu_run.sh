@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-2 GPU pass: parity tests, smoke, default bench (256/10M), rocprofv3 kernel stats.
+# GPU pass (round 3): parity tests, smoke, default bench (256/10M), rocprofv3 kernel stats.
 # usage: scripts/gpu_r02.sh <tag> [tests|bench|prof|segv|all] [pytest -k expr]
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/${1:-r02}
+OUT=gpurun_out/${1:-r03}
 WHAT=${2:-all}
 mkdir -p $OUT
 if [[ $WHAT == all || $WHAT == tests ]]; then
@@ -58,4 +58,9 @@ import json
 d=json.loads(open('$OUT/ab.json').read().strip().splitlines()[-1])
 print('$env', round(d['value']/1e6,2), d['ms_per_step'], list(d['kernels_ms_per_replay'].items())[:5])"
   done
+fi
+if [[ $WHAT == all || $WHAT == converge ]]; then
+  # how far split walkers must overlap
+  timeout -k 10 300 python -u scripts/analysis/split_converge.py 256 10000000 2 4 8 > $OUT/converge.log 2>&1 || { tail -20 $OUT/converge.log; exit 1; }
+  tail -3 $OUT/converge.log
 fi

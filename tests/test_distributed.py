@@ -168,3 +168,69 @@ def test_world2_gloo_history_gather():
         assert p.exitcode == 0
     exp = [((5, 8), 0, (5, 8, 1), 10, False), ((8, 8), 1, (8, 8, 1), 11, True)]
     assert out[0][1] == exp and out[1][1] == exp
+
+
+# ---- one hashgraph sharded by time (split_plan) -----------------
+@pytest.mark.parametrize("world,ncalls,K,tail", [(2, 10, 64, 0), (3, 100, 256, 17), (8, 39063, 256, 128),
+                                                  (4, 4, 16, 0)])
+def test_split_plan_covers_the_stream(world, ncalls, K, tail):
+    """Parts own disjoint call ranges and event ranges that tile the stream; the
+    candidate halo stays inside it; the last part ends at E."""
+    import numpy as np
+    from babble_amd.dist import split_plan
+    calls = K * np.arange(1, ncalls + 1, dtype=np.int64)
+    E = int(calls[-1]) + tail
+    plan = split_plan(calls, E, world, 3 * K)
+    ev, cb, clo = plan["ev_bounds"], plan["call_bounds"], plan["cand_lo"]
+    assert ev[0] == 0 and ev[-1] == E and cb[0] == 0 and cb[-1] == ncalls
+    for g in range(world):
+        assert cb[g + 1] > cb[g] and ev[g + 1] > ev[g]
+        # a part's events are those inserted during its calls
+        if g > 0:
+            assert ev[g] == calls[cb[g] - 1]
+        if g < world - 1:
+            assert ev[g + 1] == calls[cb[g + 1] - 1]
+        assert clo[g] == max(0, ev[g] - 3 * K) and clo[g] <= ev[g]
+    # call shares differ by at most one
+    sizes = np.diff(cb)
+    assert sizes.max() - sizes.min() <= 1
+    with pytest.raises(ValueError):
+        split_plan(calls[:1], E, 2, 0)
+
+
+def _exchange_worker(rank, world, port, q):
+    import ctypes
+
+    import numpy as np
+    import torch.distributed as dist
+    from babble_amd.dist import TorchExchange
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ex = TorchExchange(dist, "cpu")
+    out = []
+    for nbytes in (16, 1000, 64):  # the engine's op 0 / op 1 sequence, sizes varying
+        ptr = ex(0, nbytes)
+        slot = np.ctypeslib.as_array((ctypes.c_uint8 * (nbytes * world)).from_address(ptr))
+        slot[rank * nbytes:(rank + 1) * nbytes] = (rank + 1) * 7 % 256
+        ex(1, nbytes)
+        out.append([int(slot[g * nbytes]) for g in range(world)] + [int(slot[(g + 1) * nbytes - 1]) for g in range(world)])
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def test_world2_gloo_engine_exchange():
+    """The engine's all-gather (hge_split_exchange) over torch.distributed: op 0
+    hands out the slots' memory, op 1 leaves every rank's slot in every buffer."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    exp = [[7, 14, 7, 14]] * 3
+    assert out[0][1] == exp and out[1][1] == exp

@@ -1,11 +1,14 @@
-"""One hashgraph split across GPUs (babble_amd/dist.py): the
-rounds walk by several walkers from different starts, joined by row equality,
-must give exactly the single-GPU replay -- order, batches, rounds, witnesses.
+"""One hashgraph split across GPUs (babble_amd/dist.py) must give
+exactly the single-GPU replay -- order, batches, rounds, witnesses, fame, round
+received, timestamps, LastConsensusRound, the undetermined list.
 
-* single process: the walkers of G "ranks" run one after the other on one
-  engine (the real kernels and join, no collective);
-* two processes on the one GPU of the box, over gloo (the real collective
-  path, world_size 2), each with its own engine and the whole stream.
+* walk-only split, single process: the walkers of G "ranks" run one after the
+  other on one engine (the real kernels and join, no collective);
+* sharded split (hge_split_plan / hge_split_run): G parts, one engine and host
+  thread each on the one GPU of the box, exchanging through device memory
+  (ThreadExchange): each part decides its rounds' fame and its calls' order;
+* two processes on the one GPU, over gloo (the real torch.distributed path,
+  world_size 2), each with its own engine and the whole stream.
 """
 import os
 import socket
@@ -21,6 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def walk_all(eng, G, extra):
+    """The walk-only split (dist.walk_split_run) with G walkers on one engine."""
     from babble_amd.dist import join_histories
     eng.split_begin()
     hists = []
@@ -78,6 +82,106 @@ def test_split_on_golden():
         eng.close()
 
 
+def compare_state(ref, eng, order, counts, o2, c2):
+    np.testing.assert_array_equal(o2, order)
+    np.testing.assert_array_equal(c2, counts)
+    assert eng.rounds() == ref.rounds()
+    r1, w1 = ref.event_rounds()
+    r2, w2 = eng.event_rounds()
+    np.testing.assert_array_equal(r2, r1)
+    np.testing.assert_array_equal(w2, w1)
+    np.testing.assert_array_equal(eng.fame_table(), ref.fame_table())
+    rr1, ct1 = ref.event_received()
+    rr2, ct2 = eng.event_received()
+    np.testing.assert_array_equal(rr2[order], rr1[order])
+    np.testing.assert_array_equal(ct2[order], ct1[order])
+    assert eng.last_consensus_round() == ref.last_consensus_round()
+    assert eng.consensus_transactions() == ref.consensus_transactions()
+    np.testing.assert_array_equal(eng.undetermined(), ref.undetermined())
+
+
+def run_parts(engs, G, halo_rounds):
+    """The G parts of a sharded split replay, one host thread per engine."""
+    import threading
+    from babble_amd.dist import ThreadExchange, split_run
+    xg = ThreadExchange(G)
+    res, stats = [None] * G, [{} for _ in range(G)]
+
+    def run(p):
+        try:
+            res[p] = split_run(engs[p], p, G, xg.make(p), halo_rounds, stats[p])
+        except BaseException as e:  # noqa: BLE001 -- release the other parts
+            res[p] = e
+            xg.bar.abort()
+
+    ths = [threading.Thread(target=run, args=(p,)) for p in range(G)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=300)
+    for r in res:
+        if isinstance(r, BaseException):
+            raise r
+    return res, stats
+
+
+@pytest.mark.parametrize("n,E,G,halo,fallback", [
+    (64, 60_000, 3, 8, False),
+    (128, 80_000, 2, 4, False),
+    (64, 40_000, 4, 8, False),
+    (256, 60_000, 3, 8, False),
+    (64, 30_000, 2, 0, True),   # no candidate halo: events received late are nobody's -> unsplit replay
+])
+def test_sharded_split_equals_replay(n, E, G, halo, fallback):
+    from babble_amd.engine import Engine, events_array
+    dag = random_gossip(n, E, seed=170 + n + G)
+    ev = events_array(dag)
+    calls = schedule(E, n)
+    ref = Engine(n, E + 64)
+    engs = [Engine(n, E + 64) for _ in range(G)]
+    try:
+        _, order, counts = ref.replay(ev, calls)
+        for e in engs:
+            e.prepare(ev, calls)
+        res, stats = run_parts(engs, G, halo)
+        assert all(r == len(order) for r in res)
+        assert any(s.get("fallback", 0) for s in stats) == fallback, stats
+        for e in engs:
+            _, o2, c2 = e.fetch()
+            compare_state(ref, e, order, counts, o2, c2)
+        # a second replay of the same engines (buffers reused) gives the same again
+        res, _ = run_parts(engs, G, halo)
+        for e in engs:
+            _, o2, c2 = e.fetch()
+            np.testing.assert_array_equal(o2, order)
+    finally:
+        ref.close()
+        for e in engs:
+            e.close()
+
+
+def test_sharded_split_on_golden():
+    """The sharded split against the oracle's golden (64 participants, 100k events)."""
+    from babble_amd.engine import Engine, events_array
+    dag, g = load_golden(os.path.join(ROOT, "tests", "golden", "wide_n64_e100000_k64.npz"))
+    n, G = int(g["n"]), 3
+    engs = [Engine(n, len(dag["creator"]) + 64) for _ in range(G)]
+    try:
+        for e in engs:
+            e.prepare(events_array(dag), g["calls"])
+        _, stats = run_parts(engs, G, 8)
+        assert not any(s.get("fallback", 0) for s in stats)
+        for e in engs:
+            _, order, counts = e.fetch()
+            np.testing.assert_array_equal(order, g["order"])
+            np.testing.assert_array_equal(counts, g["counts"])
+            rounds, wit = e.event_rounds()
+            np.testing.assert_array_equal(rounds, g["rounds"])
+    finally:
+        for e in engs:
+            e.close()
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -86,7 +190,7 @@ def _free_port():
 
 def _rank(rank, world, port, q):
     import torch.distributed as dist
-    from babble_amd.dist import split_run, torch_gather
+    from babble_amd.dist import TorchExchange, split_run
     from babble_amd.engine import Engine, events_array
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -97,17 +201,19 @@ def _rank(rank, world, port, q):
     calls = schedule(E, n)
     eng = Engine(n, E + 64, device=0)
     eng.prepare(ev, calls)
-    split_run(eng, rank, world, torch_gather(dist))
+    stats = {}
+    split_run(eng, rank, world, TorchExchange(dist, "cuda:0"), 8, stats)
     _, order, counts = eng.fetch()
     ref = Engine(n, E + 64, device=0)
     _, rorder, rcounts = ref.replay(ev, calls)
-    q.put((rank, bool(np.array_equal(order, rorder) and np.array_equal(counts, rcounts)), len(order)))
+    q.put((rank, bool(np.array_equal(order, rorder) and np.array_equal(counts, rcounts)) and not stats,
+           len(order), len(rorder), stats))
     eng.close()
     ref.close()
     dist.destroy_process_group()
 
 
-def test_split_two_ranks_gloo_one_gpu():
+def test_sharded_split_two_ranks_gloo_one_gpu():
     import torch.multiprocessing as mp
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")

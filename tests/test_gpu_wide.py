@@ -107,16 +107,14 @@ def test_wide256_fd_rows_online_and_growth():
         b.close()
 
 
-@pytest.mark.parametrize("n,events,G,kernel", [(64, 6000, 8, "block"), (256, 5000, 5, "block"),
-                                               (64, 6000, 8, "wave")])
-def test_stale_other_parents_in_windows(n, events, G, kernel, monkeypatch):
+@pytest.mark.parametrize("n,events,G", [(64, 6000, 8), (256, 5000, 5), (128, 6000, 3)])
+def test_stale_other_parents_in_windows(n, events, G, monkeypatch):
     """Other-parents that are not their chain's head when the event is inserted (a
     node inserting events it learned late; `op_lag`) are the windowed lastAncestors
     kernels' "risky" path: read from HBM, chunk-level store drains, no early exit
     past them.  Forced into several windows (HGE_LW_G), compared with the oracle."""
     from babble_amd.engine import Engine
     monkeypatch.setenv("HGE_LW_G", str(G))
-    monkeypatch.setenv("HGE_LW_KERNEL", kernel)
     dag = random_gossip(n, events, seed=77 + n, op_lag=4)
     eng = Engine(n, 1 << 14)
     try:
