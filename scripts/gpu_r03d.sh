@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 3: full GPU suite (minus the new sharded split), smoke, bench, rocprofv3 stats,
-# then the sharded split tests and the walkers' convergence data
+# then the sharded split tests
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r03d}
@@ -20,5 +20,3 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
 echo "rocprofv3 rc=$?"
 timeout -k 10 600 $PYT tests/test_gpu_split.py -k sharded > $OUT/pytest_sharded.log 2>&1 || { echo "sharded tests failed"; tail -60 $OUT/pytest_sharded.log; exit 1; }
 tail -1 $OUT/pytest_sharded.log
-timeout -k 10 300 python -u scripts/analysis/split_converge.py 256 10000000 2 4 8 > $OUT/converge.log 2>&1 || { tail -20 $OUT/converge.log; exit 1; }
-tail -3 $OUT/converge.log
