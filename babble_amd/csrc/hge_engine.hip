@@ -347,6 +347,9 @@ struct hge_engine {
                              &s_lwrisky};
     for (auto* b : i32s) b->free_();
     s_lwplan.free_();
+    s_xbuf.free_();
+    s_sord.free_();
+    s_soff.free_();
     s_lwsum.free_();
     s_lwinit.free_();
     d_ts.free_();
@@ -722,12 +725,28 @@ struct hge_engine {
   bool split_on() const { return sp_active && sp.nparts > 1; }
   hge_exchange_fn x_fn = nullptr;
   void* x_ctx = nullptr;
+  // measurement aid (hge_split_emulate): an unsplit replay records what every part
+  // of a split contributes to the exchanges (the fame decisions of every fame
+  // iteration, the order, per-call batches, round received / timestamps, the
+  // undetermined list); a split part run without an exchange then takes the other
+  // parts' slots from the record, so one GPU times each part of a G-way split alone
+  bool rec_on = false, rec_have = false;
+  std::vector<std::vector<uint8_t>> rec_dec;
+  std::vector<int32_t> rec_order, rec_rr, rec_left;
+  std::vector<int64_t> rec_counts, rec_cts;
+  int x_iter = 0;  // fame iteration of the current batch (the record's index)
+  DBuf<uint8_t> s_xbuf;
+  bool emulating() const { return split_on() && !x_fn && rec_have; }
   DBuf<int32_t> s_sord;   // split: every part's ordered ids
   DBuf<int64_t> s_soff;   // split: their offsets
   // a device buffer of nparts slots of `bytes` (the caller's memory: its collectives
   // write into it), then the all-gather: this part's slot is filled and the stream drained
   void* x_buf(int64_t bytes) {
     sync();  // the caller may hand out (or move) the memory of the previous exchange
+    if (emulating()) {
+      s_xbuf.need((size_t)bytes * sp.nparts);
+      return s_xbuf.p;
+    }
     void* b = nullptr;
     if (!x_fn) throw EngineError(HGE_ERR_ARG, "split replay: no exchange (hge_split_exchange)");
     if (x_fn(x_ctx, 0, bytes, &b) != 0 || !b) throw EngineError(HGE_ERR_DEVICE, "split exchange: no buffer");
@@ -735,6 +754,7 @@ struct hge_engine {
   }
   void x_gather(int64_t bytes, void* b) {
     sync();
+    if (emulating()) return;  // the caller fills the other parts' slots from the record
     if (x_fn(x_ctx, 1, bytes, &b) != 0) throw EngineError(HGE_ERR_DEVICE, "split exchange failed");
   }
   // fame rounds of part g: the pr_* indices [k_lo, k_hi) whose round's first witness
@@ -1370,6 +1390,7 @@ struct hge_engine {
     const int ncalls = (int)calls.size();
     if (ncalls == 0) return;
     Tables t = tables();
+    x_iter = 0;
     // R_c = Rounds() after the DivideRounds of call c = #{r : minw[r] < n_c}
     std::vector<int32_t> Rc(ncalls);
     for (int c = 0; c < ncalls; c++)
@@ -1480,6 +1501,11 @@ struct hge_engine {
       s_LCR.need(ncalls);
       s_clast.need(nrounds);
       fame_dispatch(0, t, nrounds, npairs, ncalls, &pr_round, &pr_off);
+      if (rec_on && !split_on()) {
+        rec_dec.emplace_back((size_t)npairs * N);
+        readback(rec_dec.back().data(), s_dec.p, (size_t)npairs * N);
+      }
+      x_iter++;
       KLAUNCH(k_lcr_scan, dim3(1), dim3(1024), 0, st, c_Lc, ncalls, lcr, s_LCR.p, c_pr,
               c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds, s_clast.p, c_flags);
       int32_t fl[3];
@@ -1684,6 +1710,11 @@ struct hge_engine {
       HIPCHK(hipMemcpyAsync(buf + (size_t)p * bytes, s_dec.p + (size_t)P0[p] * N, (size_t)(P1[p] - P0[p]) * N,
                             hipMemcpyDeviceToDevice, st));
     x_gather(bytes, buf);
+    if (emulating()) {  // the other parts' decisions of this fame iteration, from the record
+      const std::vector<uint8_t>& rd = rec_dec.at((size_t)x_iter);
+      for (int g = 0; g < G; g++)
+        if (g != p && P1[g] > P0[g]) h2d(buf + (size_t)g * bytes, rd.data() + (size_t)P0[g] * N, (size_t)(P1[g] - P0[g]) * N);
+    }
     for (int g = 0; g < G; g++)
       if (g != p && P1[g] > P0[g])
         HIPCHK(hipMemcpyAsync(s_dec.p + (size_t)P0[g] * N, buf + (size_t)g * bytes, (size_t)(P1[g] - P0[g]) * N,
@@ -1711,6 +1742,34 @@ struct hge_engine {
             (const int64_t*)d_cts.p, ntx_part, ntxb, (const int32_t*)(s_small.p + 8), L,
             buf + (size_t)p * L.words);
     x_gather(bytes, buf);
+    if (emulating()) {  // the other parts' slots from the record
+      int64_t off0 = 0;
+      for (int g = 0; g < G; g++) {
+        int64_t nord = 0;
+        for (int c = sp.cb[g]; c < sp.cb[g + 1]; c++) nord += rec_counts[c];
+        if (g != p) {
+          const bool last = g == G - 1;
+          std::vector<int32_t> sl((size_t)L.words, 0);
+          unsigned long long tx = 0;
+          for (int64_t i = 0; i < nord; i++) {
+            const int32_t x = rec_order[off0 + i];
+            sl[L.ids + i] = x;
+            sl[L.rr + i] = rec_rr[x];
+            memcpy(&sl[L.cts + 2 * i], &rec_cts[x], 8);
+            tx += (unsigned long long)h_ntx[x];
+          }
+          const int64_t nleft = last ? (int64_t)rec_left.size() : 0;
+          for (int64_t i = 0; i < nleft; i++) sl[L.left + i] = rec_left[i];
+          for (int c = sp.cb[g]; c < sp.cb[g + 1]; c++) sl[L.counts + (c - sp.cb[g])] = (int32_t)rec_counts[c];
+          sl[0] = (int32_t)nord;
+          sl[1] = (int32_t)nleft;
+          sl[4] = (int32_t)(uint32_t)tx;
+          sl[5] = (int32_t)(uint32_t)(tx >> 32);
+          h2d(buf + (size_t)g * L.words, sl.data(), 4 * (size_t)L.words);
+        }
+        off0 += nord;
+      }
+    }
     // every part's header and call counts
     std::vector<int32_t> hd((size_t)G * L.ids);
     for (int g = 0; g < G; g++) d2h(&hd[(size_t)g * L.ids], buf + (size_t)g * L.words, 4 * (size_t)L.ids);
@@ -2120,8 +2179,22 @@ static void replay_end(hge_engine* h, int64_t* n_ordered) {
 int hge_replay_run(hge_engine* h, int64_t* n_ordered) {
   GUARD_BEGIN
   h->sp_active = false;
+  if (h->rec_on) h->rec_dec.clear();
   replay_begin(h);
   replay_end(h, n_ordered);
+  if (h->rec_on) {  // hge_split_emulate: the rest of the record
+    const int64_t E = h->n_events;
+    h->rec_order = h->consensus;
+    h->rec_counts = h->replay_counts;
+    h->rec_rr.resize(E);
+    h->rec_cts.resize(E);
+    h->readback(h->rec_rr.data(), h->d_rr.p, (size_t)E);
+    h->readback(h->rec_cts.data(), h->d_cts.p, (size_t)E);
+    h->rec_left.resize(h->n_und);
+    if (h->n_und) h->readback(h->rec_left.data(), h->d_und.p, (size_t)h->n_und);
+    h->rec_on = false;
+    h->rec_have = true;
+  }
   return HGE_OK;
   GUARD_END(h)
 }
@@ -2168,6 +2241,14 @@ int hge_split_exchange(hge_engine* h, hge_exchange_fn fn, void* ctx) {
   return HGE_OK;
 }
 
+int hge_split_emulate(hge_engine* h, int32_t on) {
+  if (!h) return HGE_ERR_ARG;
+  h->rec_on = on != 0;
+  h->rec_have = false;
+  h->rec_dec.clear();
+  return HGE_OK;
+}
+
 int hge_split_run(hge_engine* h, int64_t* n_ordered) {
   if (!h) return HGE_ERR_ARG;
   GUARD_BEGIN
@@ -2175,8 +2256,8 @@ int hge_split_run(hge_engine* h, int64_t* n_ordered) {
     h->err = "hge_split_run: no split plan (hge_split_plan)";
     return HGE_ERR_ARG;
   }
-  if (!h->x_fn) {
-    h->err = "hge_split_run: no exchange (hge_split_exchange)";
+  if (!h->x_fn && !h->rec_have) {
+    h->err = "hge_split_run: no exchange (hge_split_exchange) and no record (hge_split_emulate)";
     return HGE_ERR_ARG;
   }
   struct Off {  // the plan applies to this replay only
@@ -2432,6 +2513,38 @@ int32_t hge_round_events(hge_engine* h, int32_t round) {
     return e.code;
   }
 }
+// Store.GetRound's events (RoundInfo.Events, roundInfo.go:24-60): every event of
+// round r in insertion order with its witness flag (the first event of round r is
+// its first witness: ids below h_minw[r] are not scanned)
+int hge_round_event_ids(hge_engine* h, int32_t round, int32_t* ids_out, uint8_t* witness_out, int64_t cap,
+                        int64_t* n_out) {
+  if (!h || !n_out) return HGE_ERR_ARG;
+  GUARD_BEGIN
+  *n_out = 0;
+  h->coords();
+  if (round < 0 || round >= h->R || h->n_coords == 0) return HGE_OK;
+  const int64_t lo = round < (int)h->h_minw.size() ? std::max<int64_t>(0, h->h_minw[round]) : 0;
+  const int64_t n = h->n_coords - lo;
+  if (n <= 0) return HGE_OK;
+  std::vector<int32_t> rd((size_t)n);
+  std::vector<uint8_t> wd((size_t)n);
+  h->d2h(rd.data(), h->d_round.p + lo, 4 * (size_t)n);
+  h->d2h(wd.data(), h->d_wit.p + lo, (size_t)n);
+  h->sync();
+  int64_t k = 0;
+  for (int64_t i = 0; i < n; i++) {
+    if (rd[(size_t)i] != round) continue;
+    if (k < cap) {
+      if (ids_out) ids_out[k] = (int32_t)(lo + i);
+      if (witness_out) witness_out[k] = wd[(size_t)i];
+    }
+    k++;
+  }
+  *n_out = k;
+  return HGE_OK;
+  GUARD_END(h)
+}
+
 int32_t hge_round_received(hge_engine* h, int32_t id) {
   try {
     if (id < 0 || id >= h->n_events) return -1;

@@ -60,6 +60,7 @@ __device__ __forceinline__ size_t rowoff(const Tables& t, int c, int p) {
   return ((size_t)c * t.ccap + p) * (size_t)t.N;
 }
 
+
 // lastAncestors[row][col], row = chain * ccap + position.  N > 32 keeps only the
 // packed table (LA16 = LA + 1 as uint16 pairs; chains are capped at 65,534 events
 // there): the int32 rows are never materialised, every reader unpacks.

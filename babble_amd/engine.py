@@ -77,9 +77,15 @@ EXPORTS = [
     "hge_consensus_log", "hge_event_rounds", "hge_event_received", "hge_set_cache_size",
     "hge_cache_size", "hge_participant_events", "hge_participant_event", "hge_last_from",
     "hge_diff", "hge_wire_info", "hge_read_wire_parents", "hge_parent_round", "hge_round_inc",
-    "hge_round_diff", "hge_set_round", "hge_split_begin", "hge_frontier_guess",
-    "hge_frontier_walk", "hge_split_finish", "hge_frontier_rows", "hge_split_plan", "hge_split_exchange", "hge_split_run",
+    "hge_round_diff", "hge_set_round", "hge_round_event_ids", "hge_split_begin", "hge_frontier_guess",
+    "hge_frontier_walk", "hge_split_finish", "hge_frontier_rows", "hge_split_plan", "hge_split_exchange", "hge_split_run", "hge_split_emulate",
     "hge_verify_events", "hge_sha256_batch", "hge_ingest", "hge_fame_table",
+    # the standalone Store (host only; the Go shim's NewInmemStore, tests/abi/hge_store_test.cpp)
+    "hge_store_create", "hge_store_destroy", "hge_store_set_event", "hge_store_has_event",
+    "hge_store_participant_events", "hge_store_participant_event", "hge_store_last_from",
+    "hge_store_known", "hge_store_add_consensus_event", "hge_store_consensus_events",
+    "hge_store_consensus_count", "hge_store_set_round", "hge_store_get_round", "hge_store_rounds",
+    "hge_store_round_witnesses", "hge_store_round_events",
 ]
 
 _lib = None
@@ -174,14 +180,19 @@ def lib():
     L.hge_round_inc.restype = i32
     L.hge_round_diff.argtypes = [vp, i32, i32, P(i32)]
     L.hge_set_round.argtypes = [vp, i32, P(i32), P(ctypes.c_uint8), P(ctypes.c_uint8), i32]
+    if hasattr(L, "hge_round_event_ids"):
+        L.hge_round_event_ids.argtypes = [vp, i32, P(i32), P(ctypes.c_uint8), i64, P(i64)]
     L.hge_split_begin.argtypes = [vp]
     L.hge_frontier_guess.argtypes = [vp, i32, i32, P(i32)]
     L.hge_frontier_walk.argtypes = [vp, P(i32), P(i32), i32, i32, P(i32), P(ctypes.c_uint64), P(i32), P(i32)]
     L.hge_split_finish.argtypes = [vp, P(i32), P(ctypes.c_uint64), i32, i32, P(i64)]
     L.hge_frontier_rows.argtypes = [vp, i32, i32, P(i32), P(ctypes.c_uint64)]
-    L.hge_split_plan.argtypes = [vp, i32, i32, P(i64), P(i32), P(i64)]
-    L.hge_split_run.argtypes = [vp, P(i64)]
-    L.hge_split_exchange.argtypes = [vp, EXCHANGE_FN, vp]
+    if hasattr(L, "hge_split_run"):  # (a diagnostic build of an older tree, HGE_LIB, may lack them)
+        L.hge_split_plan.argtypes = [vp, i32, i32, P(i64), P(i32), P(i64)]
+        L.hge_split_run.argtypes = [vp, P(i64)]
+        L.hge_split_exchange.argtypes = [vp, EXCHANGE_FN, vp]
+    if hasattr(L, "hge_split_emulate"):
+        L.hge_split_emulate.argtypes = [vp, i32]
     u8p = P(ctypes.c_uint8)
     L.hge_verify_events.argtypes = [i64, u8p, P(i64), u8p, u8p, i32, u8p, P(i32)]
     L.hge_sha256_batch.argtypes = [i64, u8p, P(i64), i32, u8p]
@@ -404,6 +415,15 @@ class Engine:
         clo = np.ascontiguousarray(plan["cand_lo"], np.int64)
         self._check(self.L.hge_split_plan(self.h, part, nparts, _p64(evb), _p32(cb), _p64(clo)))
 
+    def clear_exchange(self):
+        self._xcb = None
+        self._check(self.L.hge_split_exchange(self.h, ctypes.cast(None, EXCHANGE_FN), None))
+
+    def split_emulate(self, on=True):
+        """hge_split_emulate: the next run() records every part's exchange slots; a
+        split_run() without an exchange then takes the other parts' from the record."""
+        self._check(self.L.hge_split_emulate(self.h, 1 if on else 0))
+
     def split_run(self):
         """hge_split_run: this part of the sharded replay (plan + exchange set);
         returns the number of events ordered by the whole replay."""
@@ -584,6 +604,15 @@ class Engine:
         cts = np.zeros(max(m, 1), np.int64)
         self._check(self.L.hge_event_received(self.h, _p32(rr), _p64(cts), m))
         return rr[:m], cts[:m]
+
+    def round_event_ids(self, r):
+        """Every event of round r (insertion order) and its witness flag (hge_round_event_ids)."""
+        n = ctypes.c_int64()
+        self._check(self.L.hge_round_event_ids(self.h, r, None, None, 0, ctypes.byref(n)))
+        ids = np.zeros(max(1, n.value), np.int32)
+        wit = np.zeros(max(1, n.value), np.uint8)
+        self._check(self.L.hge_round_event_ids(self.h, r, _p32(ids), _pu8(wit), n.value, ctypes.byref(n)))
+        return ids[:n.value], wit[:n.value].astype(bool)
 
     def fame_table(self):
         """Fame of every (round, creator) slot: int8 [Rounds(), N], -1 = no witness

@@ -451,11 +451,9 @@ func (h *Hashgraph) syncFields() {
 	h.ConsensusTransactions = int(C.hge_consensus_transactions(h.eng))
 }
 
-// MedianTimestamp (hashgraph.go:762-770) over Store events (host-side helper).
+// MedianTimestamp (hashgraph.go:762-770) over Store events (host-side helper).  Like
+// the reference it indexes events[len/2], so an empty list panics there too.
 func (h *Hashgraph) MedianTimestamp(eventHashes []string) time.Time {
-	if len(eventHashes) == 0 {
-		return time.Time{}
-	}
 	events := []Event{}
 	for _, x := range eventHashes {
 		ex, _ := h.Store.GetEvent(x)

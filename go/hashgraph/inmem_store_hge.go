@@ -3,14 +3,22 @@ package hashgraph
 // The engine-backed Store (replaces /root/reference/hashgraph/inmem_store.go
 // and caches.go).
 //
-// * Full Events live in an UNBOUNDED map: GetEvent never misses an inserted
-//   event (the reference's LRU eventCache could evict, and FindOrder's
-//   GetEvent would then fail; SURVEY.md TL;DR 8).
-// * The per-creator lists, Known, the consensus list and the rounds live in
-//   the engine.  ParticipantEvents / ParticipantEvent / ConsensusEvents keep the
-//   reference's RollingList windows and ErrTooLate for the configured
-//   cacheSize (caches.go:45-97, common/rolling_list.go:42-67); consensus math
-//   itself always runs with infinite caches.
+// A store serves two callers, like the reference's:
+//   * on its own (NewInmemStore, then SetEvent / SetRound / ... directly, as the
+//     reference's store tests and tools do): the standalone Store of the C ABI
+//     (hge_store_*: per-participant and consensus RollingLists, an LRU of
+//     RoundInfos; include/hge.h) keeps the reference's containers for events that
+//     were never inserted into a hashgraph and RoundInfos with any entries;
+//   * bound to a Hashgraph (NewHashgraph): the per-creator lists, Known, the
+//     consensus list and the rounds live in the engine, and the views keep the
+//     reference's RollingList windows and ErrTooLate for the configured cacheSize
+//     (caches.go:45-97, common/rolling_list.go:42-67); consensus math itself always
+//     runs with infinite caches.  A RoundInfo set with SetRound is kept in the
+//     standalone containers too, so GetRound returns exactly what was set (entries
+//     the engine does not know included); rounds nobody set come from the engine.
+// Full Events live in an UNBOUNDED map: GetEvent never misses an inserted event
+// (the reference's LRU eventCache could evict, and FindOrder's GetEvent would then
+// fail; SURVEY.md TL;DR 8).
 
 /*
 #include "hge.h"
@@ -25,25 +33,38 @@ import (
 type InmemStore struct {
 	cacheSize    int
 	events       map[string]Event    // hash => full Event, never evicted
-	ids          map[string]C.int32_t // hash => engine id
+	ids          map[string]C.int32_t // hash => engine id (bound)
 	hashes       []string             // engine id => hash
-	eng          *C.hge_engine
+	keys         map[string]int64     // hash => standalone key
+	keyHash      []string             // standalone key => hash
+	st           *C.hge_store         // the standalone containers
+	eng          *C.hge_engine        // the bound Hashgraph's engine, or nil
 	participants map[string]int
 }
 
-// NewInmemStore (inmem_store.go:27-36).  The store is bound to its engine by NewHashgraph.
+// NewInmemStore (inmem_store.go:27-36): usable on its own at once; NewHashgraph
+// binds it to its engine.
 func NewInmemStore(participants map[string]int, cacheSize int) *InmemStore {
-	return &InmemStore{
+	s := &InmemStore{
 		cacheSize:    cacheSize,
 		events:       make(map[string]Event),
 		ids:          make(map[string]C.int32_t),
+		keys:         make(map[string]int64),
 		participants: participants,
 	}
+	if rc := C.hge_store_create(C.int32_t(len(participants)), C.int64_t(cacheSize), &s.st); rc != C.HGE_OK {
+		panic(fmt.Sprintf("hge_store_create: status %d", int(rc)))
+	}
+	return s
 }
 
 func (s *InmemStore) bind(eng *C.hge_engine, participants map[string]int) {
 	s.eng = eng
 	s.participants = participants
+}
+
+func (s *InmemStore) bound() bool {
+	return s.eng != nil
 }
 
 func (s *InmemStore) remember(hash string, id C.int32_t) {
@@ -60,6 +81,24 @@ func (s *InmemStore) hash(id C.int32_t) string {
 		return ""
 	}
 	return s.hashes[id]
+}
+
+// standalone key of a hash (a new one for a hash never seen)
+func (s *InmemStore) key(hash string) C.int64_t {
+	if k, ok := s.keys[hash]; ok {
+		return C.int64_t(k)
+	}
+	k := int64(len(s.keyHash))
+	s.keys[hash] = k
+	s.keyHash = append(s.keyHash, hash)
+	return C.int64_t(k)
+}
+
+func (s *InmemStore) keyToHash(k C.int64_t) string {
+	if k < 0 || int(k) >= len(s.keyHash) {
+		return ""
+	}
+	return s.keyHash[k]
 }
 
 func storeErr(rc C.int) error {
@@ -90,11 +129,20 @@ func (s *InmemStore) GetEvent(key string) (Event, error) {
 	return ev, nil
 }
 
-// SetEvent keeps the full Event; the engine already holds its coordinates and
-// its place in the creator's list (hge_insert_events).
+// SetEvent (inmem_store.go:51-64) keeps the full Event.  Bound, the engine already
+// holds its coordinates and its place in the creator's list (hge_insert_events);
+// on its own, the first SetEvent of a hash appends it to its creator's list.
 func (s *InmemStore) SetEvent(event Event) error {
-	s.events[event.Hex()] = event
-	return nil
+	key := event.Hex()
+	s.events[key] = event
+	if s.bound() {
+		return nil
+	}
+	c, err := s.creatorID(event.Creator())
+	if err != nil {
+		return err
+	}
+	return storeErr(C.hge_store_set_event(s.st, s.key(key), c))
 }
 
 func (s *InmemStore) creatorID(participant string) (C.int32_t, error) {
@@ -111,11 +159,26 @@ func (s *InmemStore) ParticipantEvents(participant string, skip int) ([]string, 
 	if err != nil {
 		return []string{}, err
 	}
+	res := []string{}
+	if !s.bound() {
+		var n C.int64_t
+		if err := storeErr(C.hge_store_participant_events(s.st, c, C.int64_t(skip), nil, 0, &n)); err != nil {
+			return []string{}, err
+		}
+		if n == 0 {
+			return res, nil
+		}
+		keys := make([]C.int64_t, int(n))
+		C.hge_store_participant_events(s.st, c, C.int64_t(skip), &keys[0], n, &n)
+		for _, k := range keys {
+			res = append(res, s.keyToHash(k))
+		}
+		return res, nil
+	}
 	var n C.int64_t
 	if err := storeErr(C.hge_participant_events(s.eng, c, C.int64_t(skip), nil, 0, &n)); err != nil {
 		return []string{}, err
 	}
-	res := []string{}
 	if n == 0 {
 		return res, nil
 	}
@@ -135,6 +198,13 @@ func (s *InmemStore) ParticipantEvent(participant string, index int) (string, er
 	if err != nil {
 		return "", err
 	}
+	if !s.bound() {
+		var k C.int64_t
+		if err := storeErr(C.hge_store_participant_event(s.st, c, C.int64_t(index), &k)); err != nil {
+			return "", err
+		}
+		return s.keyToHash(k), nil
+	}
 	id := C.hge_participant_event(s.eng, c, C.int64_t(index))
 	if id < 0 {
 		return "", storeErr(C.int(id))
@@ -148,6 +218,17 @@ func (s *InmemStore) LastFrom(participant string) (string, error) {
 	if err != nil {
 		return "", err
 	}
+	if !s.bound() {
+		var k C.int64_t
+		var found C.int32_t
+		if err := storeErr(C.hge_store_last_from(s.st, c, &k, &found)); err != nil {
+			return "", err
+		}
+		if found == 0 {
+			return "", nil
+		}
+		return s.keyToHash(k), nil
+	}
 	return s.hash(C.hge_last_from(s.eng, c)), nil
 }
 
@@ -158,7 +239,11 @@ func (s *InmemStore) Known() map[int]int {
 		return known
 	}
 	counts := make([]C.int32_t, n)
-	C.hge_known(s.eng, &counts[0])
+	if s.bound() {
+		C.hge_known(s.eng, &counts[0])
+	} else {
+		C.hge_store_known(s.st, &counts[0])
+	}
 	for i, c := range counts {
 		known[i] = int(c)
 	}
@@ -168,6 +253,18 @@ func (s *InmemStore) Known() map[int]int {
 // ConsensusEvents (inmem_store.go:88-95): the rolling window of the list.
 func (s *InmemStore) ConsensusEvents() []string {
 	res := []string{}
+	if !s.bound() {
+		n := C.hge_store_consensus_events(s.st, nil, 0)
+		if n <= 0 {
+			return res
+		}
+		keys := make([]C.int64_t, int(n))
+		C.hge_store_consensus_events(s.st, &keys[0], n)
+		for _, k := range keys {
+			res = append(res, s.keyToHash(k))
+		}
+		return res
+	}
 	n := C.hge_consensus_events(s.eng, nil, 0)
 	if n <= 0 {
 		return res
@@ -181,52 +278,107 @@ func (s *InmemStore) ConsensusEvents() []string {
 }
 
 func (s *InmemStore) ConsensusEventsCount() int {
+	if !s.bound() {
+		return int(C.hge_store_consensus_count(s.st))
+	}
 	return int(C.hge_consensus_count(s.eng))
 }
 
-// AddConsensusEvent: the engine appends to its consensus list in FindOrder.
+// AddConsensusEvent (inmem_store.go:102-105).  Bound, the engine appends to its
+// consensus list in FindOrder.
 func (s *InmemStore) AddConsensusEvent(key string) error {
+	if !s.bound() {
+		return storeErr(C.hge_store_add_consensus_event(s.st, s.key(key)))
+	}
 	if _, ok := s.ids[key]; !ok {
 		return ErrKeyNotFound
 	}
 	return nil
 }
 
-// GetRound (inmem_store.go:107-113): the round's witnesses with their fame.
-// (RoundEvents(r) counts all of the round's events.)
+// the RoundInfo set with SetRound for round r, if any
+func (s *InmemStore) setRound(r int) (RoundInfo, bool) {
+	var n C.int32_t
+	if C.hge_store_get_round(s.st, C.int32_t(r), nil, nil, nil, 0, &n) != C.HGE_OK {
+		return *NewRoundInfo(), false
+	}
+	ri := NewRoundInfo()
+	if n == 0 {
+		return *ri, true
+	}
+	keys := make([]C.int64_t, int(n))
+	wit := make([]C.uint8_t, int(n))
+	fame := make([]C.uint8_t, int(n))
+	C.hge_store_get_round(s.st, C.int32_t(r), &keys[0], &wit[0], &fame[0], n, &n)
+	for i := range keys {
+		ri.Events[s.keyToHash(keys[i])] = RoundEvent{Witness: wit[i] != 0, Famous: Trilean(fame[i])}
+	}
+	return *ri, true
+}
+
+// GetRound (inmem_store.go:107-113): the RoundInfo set with SetRound, as set; bound,
+// a round nobody set is the engine's: every event of the round, the witnesses with
+// their fame.
 func (s *InmemStore) GetRound(r int) (RoundInfo, error) {
-	if r < 0 || r >= s.Rounds() {
+	if ri, ok := s.setRound(r); ok {
+		return ri, nil
+	}
+	if !s.bound() || r < 0 || r >= s.Rounds() {
 		return *NewRoundInfo(), ErrKeyNotFound
 	}
 	ri := NewRoundInfo()
-	for c := 0; c < len(s.participants); c++ {
-		w := C.hge_round_witness(s.eng, C.int32_t(r), C.int32_t(c))
-		if w < 0 {
-			continue
+	var n C.int64_t
+	C.hge_round_event_ids(s.eng, C.int32_t(r), nil, nil, 0, &n)
+	if n > 0 {
+		ids := make([]C.int32_t, int(n))
+		wit := make([]C.uint8_t, int(n))
+		C.hge_round_event_ids(s.eng, C.int32_t(r), &ids[0], &wit[0], n, &n)
+		for i, id := range ids {
+			re := RoundEvent{Witness: wit[i] != 0}
+			if re.Witness {
+				ev := s.events[s.hash(id)]
+				if c, err := s.creatorID(ev.Creator()); err == nil {
+					re.Famous = Trilean(C.hge_fame(s.eng, C.int32_t(r), c))
+				}
+			}
+			ri.Events[s.hash(id)] = re
 		}
-		ri.Events[s.hash(w)] = RoundEvent{Witness: true,
-			Famous: Trilean(C.hge_fame(s.eng, C.int32_t(r), C.int32_t(c)))}
 	}
 	return *ri, nil
 }
 
-// SetRound (inmem_store.go:115-118): records the round's witnesses and fame.
+// SetRound (inmem_store.go:115-118): any RoundInfo -- non-witness entries and hashes
+// the store never saw included -- round-trips through GetRound.  Bound, its
+// witness entries of inserted events also go to the engine's round tables.
 func (s *InmemStore) SetRound(r int, round RoundInfo) error {
+	keys := []C.int64_t{}
+	kwit := []C.uint8_t{}
+	kfame := []C.uint8_t{}
 	ids := []C.int32_t{}
 	wit := []C.uint8_t{}
 	fame := []C.uint8_t{}
 	for hash, re := range round.Events {
-		id, ok := s.ids[hash]
-		if !ok {
-			return ErrKeyNotFound
-		}
 		w := C.uint8_t(0)
 		if re.Witness {
 			w = 1
 		}
-		ids = append(ids, id)
-		wit = append(wit, w)
-		fame = append(fame, C.uint8_t(re.Famous))
+		keys = append(keys, s.key(hash))
+		kwit = append(kwit, w)
+		kfame = append(kfame, C.uint8_t(re.Famous))
+		if id, ok := s.ids[hash]; ok && s.bound() && re.Witness {
+			ids = append(ids, id)
+			wit = append(wit, w)
+			fame = append(fame, C.uint8_t(re.Famous))
+		}
+	}
+	var err error
+	if len(keys) == 0 {
+		err = storeErr(C.hge_store_set_round(s.st, C.int32_t(r), nil, nil, nil, 0))
+	} else {
+		err = storeErr(C.hge_store_set_round(s.st, C.int32_t(r), &keys[0], &kwit[0], &kfame[0], C.int32_t(len(keys))))
+	}
+	if err != nil || !s.bound() {
+		return err
 	}
 	if len(ids) == 0 {
 		return storeErr(C.hge_set_round(s.eng, C.int32_t(r), nil, nil, nil, 0))
@@ -234,24 +386,38 @@ func (s *InmemStore) SetRound(r int, round RoundInfo) error {
 	return storeErr(C.hge_set_round(s.eng, C.int32_t(r), &ids[0], &wit[0], &fame[0], C.int32_t(len(ids))))
 }
 
+// Rounds (inmem_store.go:120-122): on its own, the RoundInfos kept (the LRU's
+// length); bound, the engine's Rounds().
 func (s *InmemStore) Rounds() int {
+	if !s.bound() {
+		return int(C.hge_store_rounds(s.st))
+	}
 	return int(C.hge_rounds(s.eng))
 }
 
 func (s *InmemStore) RoundWitnesses(r int) []string {
 	res := []string{}
-	for c := 0; c < len(s.participants); c++ {
-		if w := C.hge_round_witness(s.eng, C.int32_t(r), C.int32_t(c)); w >= 0 {
-			res = append(res, s.hash(w))
-		}
+	round, err := s.GetRound(r)
+	if err != nil {
+		return res
 	}
-	return res
+	return round.Witnesses()
 }
 
 func (s *InmemStore) RoundEvents(r int) int {
+	if ri, ok := s.setRound(r); ok {
+		return len(ri.Events)
+	}
+	if !s.bound() {
+		return 0
+	}
 	return int(C.hge_round_events(s.eng, C.int32_t(r)))
 }
 
 func (s *InmemStore) Close() error {
+	if s.st != nil {
+		C.hge_store_destroy(s.st)
+		s.st = nil
+	}
 	return nil
 }

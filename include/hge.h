@@ -187,6 +187,12 @@ int hge_split_plan(hge_engine* h, int32_t part, int32_t nparts, const int64_t* e
                    const int32_t* call_bounds, const int64_t* cand_lo);
 int hge_split_exchange(hge_engine* h, hge_exchange_fn fn, void* ctx);
 int hge_split_run(hge_engine* h, int64_t* n_ordered);
+/* Measurement aid: on = 1 makes the next hge_replay_run record what every part of a
+ * split contributes to the exchanges; afterwards hge_split_run without an exchange
+ * (hge_split_exchange(h, NULL, NULL)) takes the other parts' slots from that record,
+ * so one GPU runs and times each part of a G-way split alone (results identical to
+ * the replay; scripts/analysis/split_emulate.py).  on = 0 drops the record. */
+int hge_split_emulate(hge_engine* h, int32_t on);
 
 /* Walk-only split (measured, kept for the record: DESIGN.md §6).  Every rank
  * computes everything; the rounds walk is walked by one walker per rank from its
@@ -236,6 +242,10 @@ int32_t hge_is_witness(hge_engine* h, int32_t id);    /* Witness(x)             
 int32_t hge_round_witness(hge_engine* h, int32_t round, int32_t creator); /* id or -1 */
 int32_t hge_fame(hge_engine* h, int32_t round, int32_t creator); /* 0 undef, 1 true, 2 false, -1 none */
 int32_t hge_round_events(hge_engine* h, int32_t round);          /* Store.RoundEvents(r) */
+/* Store.GetRound's events: every event of round r (insertion order) and its witness
+ * flag; *n_out = their number (ids beyond cap are dropped). */
+int hge_round_event_ids(hge_engine* h, int32_t round, int32_t* ids_out, uint8_t* witness_out, int64_t cap,
+                        int64_t* n_out);
 int32_t hge_round_received(hge_engine* h, int32_t id);           /* -1 = nil */
 int64_t hge_consensus_timestamp(hge_engine* h, int32_t id);
 
@@ -275,6 +285,40 @@ int hge_wire_info(hge_engine* h, int32_t id, int32_t* out4);
 int hge_read_wire_parents(hge_engine* h, int32_t creator_id, int32_t self_parent_index,
                           int32_t other_parent_creator_id, int32_t other_parent_index,
                           int32_t* sp_out, int32_t* op_out);
+
+/* ---- standalone Store (host only: no device, no Hashgraph) -------------------- */
+/* The reference's InmemStore for a store used on its own -- its own tests and tools
+ * call SetEvent / SetRound directly, with events that were never inserted into a
+ * hashgraph and RoundInfos holding any entries (inmem_store_test.go:48-159,
+ * caches_test.go:22-131).  Same containers: per-participant RollingLists and a
+ * consensus RollingList of cache_size (ErrTooLate / ErrKeyNotFound as the
+ * reference's, caches.go:45-115, common/rolling_list.go:25-67) and an LRU of
+ * cache_size RoundInfos (Rounds() = its length, common/lru.go); cache_size <= 0 =
+ * unbounded.  Events are the caller's int64 keys (the shim's hash <-> key map);
+ * event bodies stay with the caller, kept without eviction.  The engine-bound Store
+ * (the hge_* views above) serves a Hashgraph; this one serves NewInmemStore until a
+ * Hashgraph binds it (go/hashgraph/inmem_store_hge.go). */
+typedef struct hge_store hge_store;
+int hge_store_create(int32_t n_participants, int64_t cache_size, hge_store** out);
+void hge_store_destroy(hge_store* s);
+int hge_store_set_event(hge_store* s, int64_t key, int32_t creator);   /* SetEvent */
+int32_t hge_store_has_event(hge_store* s, int64_t key);
+int hge_store_participant_events(hge_store* s, int32_t creator, int64_t skip, int64_t* keys_out, int64_t cap,
+                                 int64_t* n_out);                       /* ParticipantEvents */
+int hge_store_participant_event(hge_store* s, int32_t creator, int64_t index, int64_t* key_out);
+int hge_store_last_from(hge_store* s, int32_t creator, int64_t* key_out, int32_t* found);
+int hge_store_known(hge_store* s, int32_t* counts_out);
+int hge_store_add_consensus_event(hge_store* s, int64_t key);
+int64_t hge_store_consensus_events(hge_store* s, int64_t* keys_out, int64_t cap);
+int64_t hge_store_consensus_count(hge_store* s);
+/* SetRound / GetRound: entries (key, witness, famous 0 undefined 1 true 2 false) */
+int hge_store_set_round(hge_store* s, int32_t round, const int64_t* keys, const uint8_t* witness,
+                        const uint8_t* famous, int32_t n);
+int hge_store_get_round(hge_store* s, int32_t round, int64_t* keys_out, uint8_t* witness_out,
+                        uint8_t* famous_out, int32_t cap, int32_t* n_out);
+int32_t hge_store_rounds(hge_store* s);
+int hge_store_round_witnesses(hge_store* s, int32_t round, int64_t* keys_out, int32_t cap, int32_t* n_out);
+int32_t hge_store_round_events(hge_store* s, int32_t round);
 
 /* ---- round predicates (hashgraph.go:211-326) --------------------------------- */
 int32_t hge_parent_round(hge_engine* h, int32_t x);   /* ParentRound: -1 bad id, 0 no parents */

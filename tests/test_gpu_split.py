@@ -227,3 +227,33 @@ def test_sharded_split_two_ranks_gloo_one_gpu():
         assert p.exitcode == 0
     assert out[0][1] and out[1][1], out
     assert out[0][2] == out[1][2] > 0
+
+
+@pytest.mark.parametrize("n,E,G", [(64, 40_000, 3), (256, 40_000, 2)])
+def test_sharded_split_emulated_parts(n, E, G):
+    """hge_split_emulate: one engine records an unsplit replay, then runs every part
+    of a G-way split alone (the other parts' exchange slots from the record); every
+    part ends with the replay's state (the measurement path of
+    scripts/analysis/split_emulate.py)."""
+    from babble_amd.dist import ROUND_EVENTS_PER_PARTICIPANT, split_plan
+    from babble_amd.engine import Engine, events_array
+    dag = random_gossip(n, E, seed=270 + n)
+    ev = events_array(dag)
+    calls = schedule(E, n)
+    ref = Engine(n, E + 64)
+    eng = Engine(n, E + 64)
+    try:
+        _, order, counts = ref.replay(ev, calls)
+        eng.prepare(ev, calls)
+        eng.split_emulate(True)
+        eng.run()
+        plan = split_plan(eng.call_events(), eng.event_count(), G, 8 * ROUND_EVENTS_PER_PARTICIPANT * n)
+        for p in range(G):
+            eng.split_plan(p, G, plan)
+            eng.clear_exchange()
+            assert eng.split_run() == len(order)
+            _, o2, c2 = eng.fetch()
+            compare_state(ref, eng, order, counts, o2, c2)
+    finally:
+        ref.close()
+        eng.close()

@@ -185,3 +185,26 @@ def test_replay_rejects_bad_call_points():
         assert len(counts) == 3
     finally:
         eng.close()
+
+
+def test_round_event_ids_match_event_rounds():
+    """hge_round_event_ids (Store.GetRound's RoundInfo.Events): every event of the
+    round with its witness flag, in insertion order."""
+    from babble_amd.engine import Engine, events_array
+    from babble_amd.gossip import random_gossip, schedule
+    n, E = 64, 20_000
+    dag = random_gossip(n, E, seed=41)
+    eng = Engine(n, E + 64)
+    try:
+        eng.replay(events_array(dag), schedule(E, n))
+        rounds, wit = eng.event_rounds()
+        R = eng.rounds()
+        for r in [0, 1, R // 2, R - 2, R - 1]:
+            ids, w = eng.round_event_ids(r)
+            exp = np.flatnonzero(rounds == r)
+            np.testing.assert_array_equal(ids, exp)
+            np.testing.assert_array_equal(w, wit[exp].astype(bool))
+            assert w.sum() == (eng.fame_table()[r] >= 0).sum()
+        assert len(eng.round_event_ids(R)[0]) == 0
+    finally:
+        eng.close()
