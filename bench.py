@@ -266,6 +266,8 @@ def main():
     ap.add_argument("--replicas", action="store_true",
                     help="gossip, N > 1: one independent hashgraph per rank (weak scaling) instead of "
                          "ONE hashgraph sharded across the ranks (babble_amd.dist.split_run)")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="torch.distributed backend (nccl = RCCL; gloo: rehearsing N ranks on one GPU)")
     ap.add_argument("--walk-only", action="store_true",
                     help="gossip, N > 1: round 2's walk-only split (walkers from time cuts joined by row "
                          "equality; every rank computes the rest) instead of the sharded replay")
@@ -282,8 +284,10 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist_
+        # one GPU per rank; ranks past the box's GPU count share them (--dist-backend gloo)
+        local_rank = local_rank % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local_rank)
-        dist_.init_process_group("nccl")
+        dist_.init_process_group(args.dist_backend)
         dist = dist_
 
     from babble_amd.dist import reduce_step, shard_range
@@ -486,6 +490,20 @@ def main():
         parity = "; ".join(checks) if checks else None
 
     secondary = None
+    if split and not args.walk_only:
+        # the same job as independent replicas (every rank replays the whole stream on
+        # its own GPU, no collective): the weak-scaling line next to the strong one
+        sync_all()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            rep_ordered = eng0.run()
+        t1 = time.perf_counter()
+        sync_all()
+        rep_step, rep_tot = reduce_step(dist, (t1 - t0) / args.steps, rep_ordered, f"cuda:{local_rank}")
+        secondary = {"replicas": {
+            "workload": f"{world} independent replays of the same stream, one per GPU (no collective)",
+            "value": round(rep_tot / rep_step, 1), "unit": "events/s", "ms_per_step": round(rep_step * 1e3, 4),
+            "scaling": "weak"}}
     if (rank == 0 and not mc and not args.no_secondary and (n, E) == DEFAULT and world == 1):
         secondary = {"replay_16_100k": small_replay(16, 100_000, 16, args.seed, local_rank),
                      "online_16_100k": online_path(16, 100_000, 16, args.seed, local_rank),
