@@ -332,11 +332,11 @@ __global__ void __launch_bounds__(256) k_transpose(Tables t, const int32_t* LAT_
   const int N = t.N;
   const size_t ccap = t.ccap;
   const int a = blockIdx.z;  // mode 0: chain j; mode 1: source chain c
-  const int p0 = plo[a] + blockIdx.x * 64;
   const int pend = len[a];
-  if (p0 >= pend) return;
   const int c0 = blockIdx.y * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+  // position tiles past the grid loop (the host sizes it without reading plo)
+  for (int p0 = plo[a] + blockIdx.x * 64; p0 < pend; p0 += gridDim.x * 64) {
   if (mode == 0) {
     // read rows (j, p) columns [c0, c0+64): row-major, coalesced along c
     for (int r = ty; r < 64; r += 4) {
@@ -363,6 +363,8 @@ __global__ void __launch_bounds__(256) k_transpose(Tables t, const int32_t* LAT_
       const int q = p0 + r, jj = c0 + tx;
       if (q < pend && jj < N) t.FD[rowoff(t, a, q) + jj] = tile[tx][r];
     }
+  }
+  __syncthreads();
   }
 }
 

@@ -683,7 +683,9 @@ struct hge_engine {
     if (bytes) HIPCHK(hipMemcpyAsync(q, dev, bytes, hipMemcpyDeviceToHost, st));
     return (size_t)(q - pin);
   }
+  int64_t n_syncs = 0;  // host waits on the stream (hge_host_syncs)
   void sync() {
+    n_syncs++;
     HIPCHK(hipStreamSynchronize(st));
     for (const Pending& pd : pending) memcpy(pd.dst, pin + pd.off, pd.bytes);
     pending.clear();
@@ -774,6 +776,11 @@ struct hge_engine {
     k_hi = g == sp.nparts - 1 ? nr : first_at(sp.a[g + 1]);
   }
   int64_t cs_n0 = 0, cs_n1 = 0;
+  // the candidates' lowest round, read back with the round count (coords_b) for the
+  // undetermined list of n_und = key[0] + key[2] - key[1] events after the divide
+  // that raises n_divided from key[1] to key[2] (key[0] < 0: none)
+  int32_t mnr_pre = 0;
+  int64_t mnr_key[3] = {-1, 0, 0};
   int cs_tot0 = 0;
   void coords() {
     if (!coords_a()) return;
@@ -861,6 +868,10 @@ struct hge_engine {
     Tables t = tables();
     // rounds frontier
     for (bool retry = false;; retry = true) {
+      // the wide frontier grids stay on the device until the sync below: two such
+      // grids on one device must not overlap (frontier_lock)
+      std::unique_lock<std::mutex> flk;
+      if (N > 32) flk = frontier_lock();
       int32_t rs[3] = {R, 0, 0};
       if (retry) h2d(k_rs, rs, 12);
       t = tables();
@@ -963,7 +974,28 @@ struct hge_engine {
               (const int32_t*)k_rs, d_minw.p);
       h_minw.resize(Rcap + 2);
       d2h(h_minw.data(), d_minw.p, 4 * ((size_t)Rcap + 2));
+      // the lowest round of the next batch's candidates (the undetermined list and the
+      // events the next divide appends), read with the round count
+      // (a fresh replay's candidates start at event 0, round 0: nothing to read)
+      if (!fresh) {
+        s_small.need(16);
+        h2d(s_small.p + 9, &kInf, 4);
+        if (n_und > 0)
+          KLAUNCH(k_min_round, dim3(div_up(n_und, 256)), dim3(256), 0, st, d_round.p, d_und.p, (int)n_und,
+                  s_small.p + 9);
+        if (n1 > n_divided)
+          KLAUNCH(k_min_round_range, dim3(div_up(n1 - n_divided, 256)), dim3(256), 0, st, d_round.p,
+                  (int)n_divided, (int)n1, s_small.p + 9);
+        d2h(&mnr_pre, s_small.p + 9, 4);
+      }
       sync();
+      mnr_key[0] = fresh ? -1 : n_und;
+      mnr_key[1] = n_divided;
+      mnr_key[2] = n1;
+      if (coop_err_check) {
+        coop_err_check = false;
+        if (coop_err) throw EngineError(HGE_ERR_DEVICE, "rounds frontier hand-off timed out");
+      }
       if (h_minw[Rcap + 1]) {
         ensure_rcap((int64_t)Rcap * 2);
         continue;
@@ -1077,14 +1109,25 @@ struct hge_engine {
 
 
   // rounds of a wide hashgraph: cooperative frontier kernel (hge_rounds_coop.hip)
+  // (the caller holds frontier_lock() until the stream has drained)
+  int32_t coop_err = 0;
+  bool coop_err_check = false;
   void rounds_coop(bool fresh) {
-    auto lk = frontier_lock();  // until the frontier grids below have drained (last readback)
     Tables t = tables();
     s_fst.need(N + 1);
     KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p);
-    int32_t rlo = INF32;
-    readback(&rlo, s_fst.p, 1);
-    if (rlo == INF32) return;
+    // the lowest round to recompute: read back for a fresh state (the walkers and the
+    // joined rows need it on the host), else read by the frontier kernel itself,
+    // which stands down at INF32 (no round trip)
+    int32_t rlo = 0;
+    const int32_t* rlo_dev = nullptr;
+    if (fresh) {
+      rlo = INF32;
+      readback(&rlo, s_fst.p, 1);
+      if (rlo == INF32) return;
+    } else {
+      rlo_dev = s_fst.p;
+    }
     int Rprev = R;
     if (!coop_checked) {
       int nb = 0, ncu = 0, coop = 0;
@@ -1195,7 +1238,7 @@ struct hge_engine {
       const int32_t* nostart = nullptr;
       int32_t* nohist = nullptr;
       int hmax = 0, extra = 0;
-      void* dargs[] = {&t, &olen, &len, &rstate, &rlo, &Rprev, &gran, &err, &ssc, &mb, &dbg,
+      void* dargs[] = {&t, &olen, &len, &rstate, &rlo, &rlo_dev, &Rprev, &gran, &err, &ssc, &mb, &dbg,
                        &nostart, &nohist, &hmax, &nostart, &extra};
       const void* fn = N <= 64 ? (const void*)k_rounds_direct<1024, 64>
                      : N <= 128 ? (const void*)k_rounds_direct<1024, 128>
@@ -1204,14 +1247,14 @@ struct hge_engine {
       HIPCHK(launch_resident(fn, dim3(N), dim3(1024), dargs));
       prof_end();
     } else {
-      void* args[] = {&t, &FDT, &olen, &len, &rstate, &rlo, &Rprev, &gran, &err, &ssc, &dbg};
+      void* args[] = {&t, &FDT, &olen, &len, &rstate, &rlo, &rlo_dev, &Rprev, &gran, &err, &ssc, &dbg};
       prof_begin("k_rounds_coop");
       HIPCHK(launch_resident((const void*)k_rounds_coop, dim3(N), dim3(COOP_BS), args));
       prof_end();
     }
-    int32_t e = 0;
-    readback(&e, s_bar.p + 1, 1);
-    if (e) throw EngineError(HGE_ERR_DEVICE, "rounds frontier hand-off timed out");
+    // the hand-off error flag comes back with the round count (coords_b)
+    d2h(&coop_err, s_bar.p + 1, 4);
+    coop_err_check = true;
     dbg_dump();
   }
 
@@ -1361,13 +1404,15 @@ struct hge_engine {
     }
     // FDT -> FD rows for every chain-c position a new event can have touched
     // (from a fresh state: every row, qlo = 0 as uploaded; no round trip)
-    std::vector<int32_t> qlo(N, 0);
+    // (the rows' lower bounds stay on the device: the transposes loop over position
+    // tiles past their grid, sized here for the new positions plus a tile)
+    int span = 1;
     if (!fresh) {
       KLAUNCH(k_fd_qlo, dim3(div_up(N, 256)), dim3(256), 0, st, t, olen, len, k_qlo);
-      readback(qlo.data(), k_qlo, N);
+      span = maxnew + 64;
+    } else {
+      for (int c = 0; c < N; c++) span = std::max(span, chain_len[c]);
     }
-    int span = 1;
-    for (int c = 0; c < N; c++) span = std::max(span, chain_len[c] - qlo[c]);
     // (a split part writes the timestamp rows of its own candidates only)
     if (N > 16)
       KLAUNCH((k_fd_transpose_ts<int32_t>), dim3(N, div_up(N, 64), std::min(div_up(span, 64), 65535)), dim3(256),
@@ -1410,7 +1455,12 @@ struct hge_engine {
     }
     // lowest candidate round (a fresh replay's candidates include event 0, round 0)
     int32_t mnr = 0;
-    if (ord && (!fresh_und || spl)) {
+    const bool pre = mnr_key[0] >= 0 && !spl && n_divided == mnr_key[2] &&
+                     n_und == mnr_key[0] + (mnr_key[2] - mnr_key[1]);
+    mnr_key[0] = -1;
+    if (ord && !fresh_und && pre) {
+      mnr = mnr_pre;
+    } else if (ord && (!fresh_und || spl)) {
       h2d(s_small.p + 7, &kInf, 4);
       KLAUNCH(k_min_round, dim3(div_up(ncand, 256)), dim3(256), 0, st, d_round.p, cand, ncand,
               s_small.p + 7);
@@ -1426,6 +1476,10 @@ struct hge_engine {
     int npairs = 0, nrounds = 0;
     int64_t nslot = 0;
     int lcr_new = lcr, c_set = -1;
+    // every round's window reaching the last call (always so for one call: the
+    // online path) cannot widen: the coverage flags stay on the device, and the new
+    // LastConsensusRound comes back with the batch's closing readback
+    bool lcr_dev = false;
     const int i_lo = lcr + 1;
     const int i_hi = Rc[ncalls - 1] - 2;  // processed rounds: i <= R_c - 2
     // speculative fame window: calls up to R_c <= i + 2 + SPEC, widened when a round
@@ -1508,6 +1562,12 @@ struct hge_engine {
       x_iter++;
       KLAUNCH(k_lcr_scan, dim3(1), dim3(1024), 0, st, c_Lc, ncalls, lcr, s_LCR.p, c_pr,
               c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds, s_clast.p, c_flags);
+      bool full = true;
+      for (int k = 0; k < nrounds && full; k++) full = pr_cf[k] + pr_len[k] == ncalls;
+      if (full) {
+        lcr_dev = true;
+        break;
+      }
       int32_t fl[3];
       readback(fl, c_flags, 3);
       if (fl[0]) continue;  // a round stayed undecided past its window: widen
@@ -1527,6 +1587,8 @@ struct hge_engine {
     int32_t* o_ids = s_out.p + 8 + ncalls;
     unsigned long long* o_ntx = (unsigned long long*)(s_out.p + 4);
     HIPCHK(hipMemsetAsync(s_out.p, 0, 4 * (8 + (size_t)ncalls), st));
+    if (lcr_dev)  // the new LastConsensusRound into the results block (o_cnt[3])
+      HIPCHK(hipMemcpyAsync(s_out.p + 3, c_flags + 1, 4, hipMemcpyDeviceToDevice, st));
     if (ord) {
       if (nr > 0) {
         SegInfo si;
@@ -1644,7 +1706,12 @@ struct hge_engine {
     bool lcr_up = false;
     if (do_fame && nrounds > 0) {
       fame_dispatch(1, t, nrounds, npairs, ncalls);
-      if (lcr_new > lcr) {
+      if (lcr_dev) {
+        // RoundEvents(LCR - 1) as below, the new LCR and its call read on the device
+        const int64_t nfrom = std::min<int64_t>(calls[0], n_coords);
+        KLAUNCH(k_lcre_dev, dim3(std::max(1, div_up(n_coords - nfrom, 256))), dim3(256), 0, st, t,
+                (const int64_t*)c_nc, (const int32_t*)c_flags, lcr, (int)nfrom, (int)n_coords, o_cnt + 2);
+      } else if (lcr_new > lcr) {
         // RoundEvents(lcr_new - 1) at call c_set: events of that round minus the
         // ones inserted after that call
         lcr_up = true;
@@ -1683,6 +1750,10 @@ struct hge_engine {
       n_und = ho[1];
     } else if (do_order && counts_out && !split_done) {
       for (int c = 0; c < ncalls; c++) counts_out->push_back(0);
+    }
+    if (lcr_dev && ho[3] > lcr) {
+      lcr_up = true;
+      lcr_new = ho[3];
     }
     if (lcr_up) {
       lcr = lcr_new;
@@ -2336,6 +2407,7 @@ int hge_frontier_walk(hge_engine* h, const int32_t* start, const int32_t* stopcu
   const int32_t* olen = h->k_len;
   const int32_t* len = h->k_len + N;
   int rlo = 0, Rprev = 0;
+  const int32_t* rlo_dev = nullptr;
   uint64_t* gran = h->s_gran.p;
   int32_t* err = h->s_bar.p + 1;
   uint64_t* ssc = h->s_hssc.p;
@@ -2344,7 +2416,7 @@ int hge_frontier_walk(hge_engine* h, const int32_t* start, const int32_t* stopcu
   const int32_t* st0 = h->s_hstate.p;
   int32_t* hist = h->s_hist.p;
   int hm = hmax, ex = std::max(0, (int)extra);
-  void* args[] = {&t, &olen, &len, &rstate, &rlo, &Rprev, &gran, &err, &ssc, &mb, &dbg,
+  void* args[] = {&t, &olen, &len, &rstate, &rlo, &rlo_dev, &Rprev, &gran, &err, &ssc, &mb, &dbg,
                   &st0, &hist, &hm, &cut, &ex};
   const void* fn = N <= 64 ? (const void*)k_rounds_direct<1024, 64>
                  : N <= 128 ? (const void*)k_rounds_direct<1024, 128>
@@ -2841,6 +2913,8 @@ int hge_kernel_stats(hge_engine* h, int k, char* name, int namecap, double* tota
 }
 
 int32_t hge_coordinate_sweeps(hge_engine* h) { return h ? h->n_sweeps : -1; }
+
+int64_t hge_host_syncs(hge_engine* h) { return h ? h->n_syncs : -1; }
 
 int hge_stage_times(hge_engine* h, float* ms_out, int cap) {
   int n = std::min(cap, 7);

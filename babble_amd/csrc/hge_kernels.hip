@@ -94,6 +94,15 @@ __global__ void k_min_round(const int32_t* round, const int32_t* cand, int n, in
   if ((threadIdx.x & 63) == 0 && v != INF32) atomicMin(out, v);
 }
 
+// k_min_round over the ids [lo, hi)
+__global__ void k_min_round_range(const int32_t* round, int lo, int hi, int32_t* out) {
+  const int i = lo + blockIdx.x * blockDim.x + threadIdx.x;
+  int v = INF32;
+  if (i < hi) v = round[i];
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+  if ((threadIdx.x & 63) == 0 && v != INF32) atomicMin(out, v);
+}
+
 // exclusive scan of a small int array by one block (n <= ~64k)
 __global__ void __launch_bounds__(1024) k_scan_small(const int32_t* in, int32_t* out, int n,
                                                      int32_t* total) {
@@ -2302,6 +2311,20 @@ __global__ void k_lcre(Tables t, int n_from, int n1, int r, int32_t* out) {
   const int x = n_from + blockIdx.x * blockDim.x + threadIdx.x;
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(out, t.rcnt[r]);
   if (x < n1 && t.round[x] == r) atomicSub(out, 1);
+}
+
+// k_lcre with the new LastConsensusRound L = flags[1] and its call flags[2] read
+// on the device: nothing unless L > lcr_old; the blocks before the call's event
+// count n_c stand down
+__global__ void k_lcre_dev(Tables t, const int64_t* nc, const int32_t* flags, int lcr_old, int n_lo, int n1,
+                           int32_t* out) {
+  const int L = flags[1];
+  if (L <= lcr_old || L < 1) return;
+  const int r = L - 1;
+  const int n_from = (int)min<int64_t>(nc[flags[2]], (int64_t)n1);
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(out, t.rcnt[r]);
+  const int x = n_lo + blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= n_from && x < n1 && t.round[x] == r) atomicSub(out, 1);
 }
 
 // fresh consensus state: C = INF, W = -1, bitsets / fame / counts = 0, rr = -1

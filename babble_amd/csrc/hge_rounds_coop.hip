@@ -313,8 +313,13 @@ constexpr int COOP_BS = 1024;
 constexpr int COOP_SPEC_BS = 512;  // walkers: 512 threads, 2 per CU (1024 = 1 per CU, HGE_COOP_SPEC_BS)
 __global__ void __launch_bounds__(COOP_BS) k_rounds_coop(Tables t, const int32_t* FDT, const int32_t* olen,
                                                      const int32_t* len, int32_t* rstate, int rlo,
-                                                     int Rprev, uint64_t* gran, int32_t* err,
-                                                     uint64_t* ssc, uint64_t* dbg) {
+                                                     const int32_t* rlo_dev, int Rprev, uint64_t* gran,
+                                                     int32_t* err, uint64_t* ssc, uint64_t* dbg) {
+  // rlo_dev: the first round to recompute, read here (INF32: nothing to do)
+  if (rlo_dev) {
+    rlo = *rlo_dev;
+    if (rlo == INF32) return;
+  }
   // HGE_STAMPS diagnostics (workgroup 0, thread 0): cycles per section
   __shared__ uint64_t st_acc[11];  // thread 0 only: kept out of every lane's registers
   uint64_t st_t = 0;

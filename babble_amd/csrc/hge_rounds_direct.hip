@@ -445,7 +445,8 @@ __device__ int dir_select(const Tables& t, int c, int lenc, DirLDS<BS, NPOW>& L,
 
 template <int BS, int NPOW>
 __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t* olen, const int32_t* len,
-                                                      int32_t* rstate, int rlo, int Rprev, uint64_t* gran,
+                                                      int32_t* rstate, int rlo, const int32_t* rlo_dev,
+                                                      int Rprev, uint64_t* gran,
                                                       int32_t* err, uint64_t* ssc, uint32_t* mbuf,
                                                       uint64_t* dbg, const int32_t* start, int32_t* hist,
                                                       int hmax, const int32_t* stopcut, int extra) {
@@ -456,6 +457,11 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
   // first reached stopcut on every chain (the next walker's start; rstate[1] = 2),
   // or at the empty frontier; rstate[0] = rows written.
   using G = DirGeo<BS, NPOW>;
+  // rlo_dev: the first round to recompute, read here (INF32: nothing to do)
+  if (rlo_dev) {
+    rlo = *rlo_dev;
+    if (rlo == INF32) return;
+  }
   // HGE_STAMPS diagnostics (workgroup 0, thread 0): cycles per section into dbg[0..8]
   // (6 = probes; 7, 8 = member-load issue and arrival inside section 0)
   uint64_t st_t = 0, st_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -653,17 +659,11 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
 #undef DSTAMP_START
 }
 
-template __global__ void k_rounds_direct<1024, 64>(Tables, const int32_t*, const int32_t*, int32_t*, int, int,
-                                                   uint64_t*, int32_t*, uint64_t*, uint32_t*, uint64_t*,
-                                                   const int32_t*, int32_t*, int, const int32_t*, int);
-template __global__ void k_rounds_direct<1024, 128>(Tables, const int32_t*, const int32_t*, int32_t*, int, int,
-                                                    uint64_t*, int32_t*, uint64_t*, uint32_t*, uint64_t*,
-                                                   const int32_t*, int32_t*, int, const int32_t*, int);
-template __global__ void k_rounds_direct<512, 256>(Tables, const int32_t*, const int32_t*, int32_t*, int, int,
-                                                   uint64_t*, int32_t*, uint64_t*, uint32_t*, uint64_t*,
-                                                   const int32_t*, int32_t*, int, const int32_t*, int);
-template __global__ void k_rounds_direct<1024, 256>(Tables, const int32_t*, const int32_t*, int32_t*, int, int,
-                                                    uint64_t*, int32_t*, uint64_t*, uint32_t*, uint64_t*,
-                                                   const int32_t*, int32_t*, int, const int32_t*, int);
+template __global__ void k_rounds_direct<1024, 64>(Tables, const int32_t*, const int32_t*, int32_t*, int, const int32_t*, int,
+    uint64_t*, int32_t*, uint64_t*, uint32_t*, uint64_t*, const int32_t*, int32_t*, int, const int32_t*, int);
+template __global__ void k_rounds_direct<1024, 128>(Tables, const int32_t*, const int32_t*, int32_t*, int, const int32_t*, int,
+    uint64_t*, int32_t*, uint64_t*, uint32_t*, uint64_t*, const int32_t*, int32_t*, int, const int32_t*, int);
+template __global__ void k_rounds_direct<1024, 256>(Tables, const int32_t*, const int32_t*, int32_t*, int, const int32_t*, int,
+    uint64_t*, int32_t*, uint64_t*, uint32_t*, uint64_t*, const int32_t*, int32_t*, int, const int32_t*, int);
 
 }  // namespace hge

@@ -57,6 +57,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 DEFAULT = (256, 10_000_000)
+ONLINE_PREFIX = 512_000  # online per-call line at the default width
 
 
 def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
@@ -149,39 +150,48 @@ def sub_stream(dag, ns):
     return {k: (v[:ns] if isinstance(v, np.ndarray) else v) for k, v in dag.items()}
 
 
-def online_path(n, E, K, seed, device):
+def online_path(n, E, K, seed, device, dag=None, what=None):
     """The per-call production path: for every call, hge_insert_events of the
     next K submissions, then hge_run_consensus (node/core.go:179-202).  Returns
-    per-call latency and events/s, and whether the order equals the replay's."""
+    per-call latency (p50/p99), the host admission share, host round trips per
+    call, events/s, and whether the order equals the replay's.  `dag`: a stream
+    to take (else a fresh random_gossip(n, E, seed))."""
     from babble_amd.engine import Engine, events_array
     from babble_amd.gossip import random_gossip, schedule
-    dag = random_gossip(n, E, seed=seed)
-    ev = events_array(dag)
+    if dag is None:
+        dag = random_gossip(n, E, seed=seed)
+    ev = events_array(dag)[:E]
     calls = schedule(E, K)
     rep = Engine(n, E, device=device)
     _, rorder, _ = rep.replay(ev, calls)
     rep.close()
     eng = Engine(n, E, device=device)
     lat = np.zeros(len(calls))
+    adm = np.zeros(len(calls))
     parts = []
     prev = 0
+    s0 = eng.host_syncs()
     t0 = time.perf_counter()
     for i, c in enumerate(calls):
         t = time.perf_counter()
         # every submission of a gossip stream is accepted: engine id == submission index
         eng.insert_events(ev[prev:c])
+        ta = time.perf_counter()
         parts.append(eng.run_consensus())
         lat[i] = time.perf_counter() - t
+        adm[i] = ta - t
         prev = c
     wall = time.perf_counter() - t0
+    syncs = eng.host_syncs() - s0
     order = np.concatenate(parts) if parts else np.zeros(0, np.int32)
     eng.close()
-    return {"workload": f"online per-call path, {n} participants, {E} events, "
-                        f"hge_insert_events(K={K}) + hge_run_consensus per call ({len(calls)} calls)",
+    us = lambda a, q: round(float(np.percentile(a, q)) * 1e6, 1)
+    return {"workload": what or (f"online per-call path, {n} participants, {E} events, "
+                                 f"hge_insert_events(K={K}) + hge_run_consensus per call ({len(calls)} calls)"),
             "value": round(len(order) / wall, 1), "unit": "events/s",
-            "call_latency_us": {"mean": round(float(lat.mean()) * 1e6, 1),
-                                "p50": round(float(np.percentile(lat, 50)) * 1e6, 1),
-                                "p99": round(float(np.percentile(lat, 99)) * 1e6, 1)},
+            "call_latency_us": {"mean": round(float(lat.mean()) * 1e6, 1), "p50": us(lat, 50), "p99": us(lat, 99)},
+            "admission_us": {"p50": us(adm, 50), "p99": us(adm, 99)},
+            "host_round_trips_per_call": round(syncs / max(1, len(calls)), 2),
             "parity": ("identical to the bulk replay" if np.array_equal(order, rorder)
                        else "MISMATCH vs the bulk replay")}
 
@@ -296,6 +306,7 @@ def main():
 
     # ---- stage the workload in HBM (host admission + upload; not timed) ----
     t0 = time.perf_counter()
+    admission_s = None
     if mc:
         first, per = shard_range(args.graphs, world, rank)
         dags = [random_gossip(n, E, seed=args.seed + first + g, forkers=10, fork_p=0.05, cascade_p=0.5)
@@ -308,7 +319,11 @@ def main():
         # split: every rank stages the same stream (seed, not seed + rank)
         dags = [random_gossip(n, E, seed=args.seed + (0 if split else rank))]
         engines = [Engine(n, E, device=local_rank)]
-        engines[0].prepare(events_array(dags[0]), schedule(E, K))
+        ev0 = events_array(dags[0])
+        t_adm = time.perf_counter()
+        engines[0].prepare(ev0, schedule(E, K))
+        admission_s = time.perf_counter() - t_adm
+        del ev0
     ingest_s = time.perf_counter() - t0
     pool = ThreadPoolExecutor(max_workers=max(1, min(args.threads, len(engines))))
 
@@ -507,6 +522,12 @@ def main():
     if (rank == 0 and not mc and not args.no_secondary and (n, E) == DEFAULT and world == 1):
         secondary = {"replay_16_100k": small_replay(16, 100_000, 16, args.seed, local_rank),
                      "online_16_100k": online_path(16, 100_000, 16, args.seed, local_rank),
+                     "online_64_1m": online_path(64, 1_000_000, 64, args.seed, local_rank),
+                     "online_256_prefix": online_path(
+                         n, ONLINE_PREFIX, K, args.seed, local_rank, dag=dags[0],
+                         what=f"online per-call path on the first {ONLINE_PREFIX} submissions of the bench's own "
+                              f"{n}-participant stream, hge_insert_events(K={K}) + hge_run_consensus per call "
+                              f"({len(schedule(ONLINE_PREFIX, K))} calls)"),
                      "ingest_16_100k": ingest_path(16, 100_000, 16, args.seed, local_rank)}
 
     if rank == 0:
@@ -556,6 +577,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "ingest_host_ms": round(ingest_s * 1e3, 2),
+            "admission_ms": None if admission_s is None else round(admission_s * 1e3, 2),
             "replay_ms": replay_ms,
             "coordinate_sweeps": sweeps,
             "rounds": eng0.rounds(),

@@ -349,6 +349,9 @@ int hge_stage_times(hge_engine* h, float* ms_out, int cap);
  * 32 < N <= 256 (hge_coords_win.hip), Jacobi sweeps otherwise (hge_coords.hip);
  * the last one confirms the fixed point (a single window needs one pass). */
 int32_t hge_coordinate_sweeps(hge_engine* h);
+/* Host round trips so far: the number of times the host has waited on the
+ * engine's stream (each readback of a control value or result is one). */
+int64_t hge_host_syncs(hge_engine* h);
 /* Per-kernel timing: HIP events around every launch on the engine stream. */
 int hge_set_profiling(hge_engine* h, int on);
 int hge_reset_kernel_stats(hge_engine* h);
