@@ -389,12 +389,17 @@ __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const FT* FDT
   // positions of different source chains, whose first descendants (and so the
   // timestamps gathered) lie in the same stretch of each chain j -- L2 hits
   // instead of one re-read per source chain.  Position tiles past gridDim.z loop.
-  const int a = blockIdx.x;  // source chain c
+  // (in XCD-aware order: the neighbouring source chains of a position tile run on one
+  // XCD, so the gathers they share hit its L2)
+  const int64_t nbk = (int64_t)gridDim.x * gridDim.y * gridDim.z;
+  const int64_t lb = xcd_block(blockIdx.x + (int64_t)gridDim.x * (blockIdx.y + (int64_t)gridDim.y * blockIdx.z), nbk);
+  const int bx = (int)(lb % gridDim.x), by = (int)((lb / gridDim.x) % gridDim.y), bz = (int)(lb / ((int64_t)gridDim.x * gridDim.y));
+  const int a = bx;  // source chain c
   const int pend = len[a];
   const int ts0 = tlo ? tlo[a] : 0, ts1 = thi ? thi[a] : pend;
-  const int c0 = blockIdx.y * 64;
+  const int c0 = by * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
-  for (int p0 = plo[a] + blockIdx.z * 64; p0 < pend; p0 += gridDim.z * 64) {
+  for (int p0 = plo[a] + bz * 64; p0 < pend; p0 += gridDim.z * 64) {
     // read phase: lane tx walks row q = p0 + tx (its own timestamp is one load), all
     // 16 FDT loads of a thread in flight, then all 16 timestamp gathers
     const int64_t own = t.tsch[(size_t)a * ccap + min(p0 + tx, pend - 1)];
@@ -444,7 +449,7 @@ __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const FT* FDT
         if (tsrow) t.FDTD[o] = dv;
       }
       const bool any = __ballot(esc) != 0;
-      if (tx == 0 && q < pend && tsrow) t.FDTW[((size_t)a * ccap + q) * NT + blockIdx.y] = any ? 1 : 0;
+      if (tx == 0 && q < pend && tsrow) t.FDTW[((size_t)a * ccap + q) * NT + by] = any ? 1 : 0;
     }
     __syncthreads();
   }

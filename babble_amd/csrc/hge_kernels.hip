@@ -60,6 +60,16 @@ __device__ __forceinline__ size_t rowoff(const Tables& t, int c, int p) {
   return ((size_t)c * t.ccap + p) * (size_t)t.N;
 }
 
+// XCD-aware block order: the dispatcher deals workgroup ids round-robin to the 8
+// XCDs (each with its own L2), so neighbouring ids -- which a kernel gives
+// neighbouring work that shares rows -- land on different L2s and every XCD
+// fetches every shared row.  xcd_block maps the id to one of 8 contiguous ranges
+// of the grid, one per XCD (a bijection on [0, nb) for any nb).
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
+  const int64_t q = nb >> 3, r = nb & 7, x = b & 7, i = b >> 3;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
 
 // lastAncestors[row][col], row = chain * ccap + position.  N > 32 keeps only the
 // packed table (LA16 = LA + 1 as uint16 pairs; chains are capped at 65,534 events
@@ -875,7 +885,8 @@ __global__ void k_fame_decide(Tables t, const int32_t* pr_round, const int32_t* 
                               const int64_t* nc, const int32_t* Rc, uint8_t* dec) {
   // pairs [p0, npairs): a part of a split replay decides the pairs of its rounds only
   // (pr_* then start at its first round; pair indices stay absolute)
-  const int item = blockIdx.x * blockDim.x + threadIdx.x;
+  // (XCD-aware order: neighbouring pairs read the same rounds' witness rows)
+  const int item = (int)xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   const int N = t.N, SM = t.SM;
   if (item >= (npairs - p0) * N) return;
   int p = item / N;
@@ -1712,6 +1723,7 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
 #endif
   constexpr int MW_E = HGE_MW_E;
   const int nw = gridDim.x * 4;
+  // (the XCD-aware order of k_fame_decide measured 0.2 ms slower here)
   const int q0 = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int N = t.N, NW = t.NW;
