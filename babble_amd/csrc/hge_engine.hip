@@ -23,6 +23,7 @@
 
 #include "../../include/hge.h"
 #include "hge_kernels.hip"
+#include "hge_wide32.hip"
 #include "hge_coords.hip"
 #include "hge_coords_win.hip"
 #include "hge_rounds_coop.hip"
@@ -119,7 +120,11 @@ struct hge_engine {
   int R_set = 0;            // rounds recorded by hge_set_round (Store.SetRound)
   std::vector<std::vector<int32_t>> h_chain;  // participantEventsCache: ids per creator
   int64_t cache_size = 0;   // Store.CacheSize() for the rolling views (0 = unbounded)
-  int32_t chain_limit = INT32_MAX;  // longest chain the rounds kernels take (admission)
+  int32_t chain_limit = INT32_MAX;  // longest chain of the uint16 wide path (then: to_wide32)
+  int32_t chain_limit0 = INT32_MAX;
+  // N > 32 past chain_limit: int32 positions for good (hge_wide32.hip); pending until
+  // the next coordinate step converts the packed table
+  bool wide32 = false, wide32_pending = false;
   int lcr = -1;             // LastConsensusRound (-1 nil)
   int lcre = 0;             // LastCommitedRoundEvents
   int64_t ctx = 0;          // ConsensusTransactions
@@ -138,6 +143,7 @@ struct hge_engine {
   DBuf<uint64_t> d_S;
   DBuf<uint8_t> d_coin, d_wit;
   DBuf<int32_t> d_chain, d_LA, d_FD, d_FSS;
+  DBuf<int32_t> s_w32, s_w32a;  // to_wide32 / rounds_step32 scratch
   DBuf<uint32_t> d_LA16;  // N > 32: the sweeps' packed (LA + 1) table (hge_coords.hip)
   DBuf<int2> d_opcp;  // [N][ccap] other-parent coordinates (k_chain_fill)
   DBuf<int64_t> d_tsch;  // [N][ccap] timestamps in chain layout (k_chain_fill)
@@ -234,7 +240,7 @@ struct hge_engine {
     t.tsch = d_tsch.p;
     t.LA = d_LA.p;
     t.NW2 = (N + 1) / 2;
-    t.LA16 = d_LA16.p;
+    t.LA16 = sweep16() ? d_LA16.p : nullptr;  // null: int32 rows (la_row)
     t.FD = d_FD.p;
     t.FDTD = d_FDTD.p;
     t.FDTW = d_FDTW.p;
@@ -262,10 +268,12 @@ struct hge_engine {
     chain_len.assign(N, 0);
     chain_last.assign(N, -1);
     h_chain.assign(N, {});
-    // the wide rounds kernels keep chain positions as uint16 (hge_rounds_coop.hip):
-    // longer chains are refused at admission so the engine stays usable
+    // the wide kernels keep chain positions as uint16 (LA16, the rounds walk, theta):
+    // a longer chain switches the engine to int32 positions (to_wide32).
+    // HGE_CHAIN_LIMIT (tests) lowers the switch point.
     chain_limit = N > 32 ? 0xFFFE : INT32_MAX;
     if (const char* cl = getenv("HGE_CHAIN_LIMIT")) chain_limit = std::max(1, std::min(chain_limit, atoi(cl)));
+    chain_limit0 = chain_limit;
     coords_len.assign(N, 0);
     // chain tables: a creator's chain is ~cap/N long (binomial, sd ~ sqrt(cap/N));
     // rounds: a round spans >= ~4N events in gossip.  Both grow on demand.
@@ -459,7 +467,7 @@ struct hge_engine {
     d_tsch.p = tsch;
     d_tsch.n = (size_t)N * nc;
     if (!sweep16()) grow_chain_table(d_LA, nc, true);
-    if (sweep16()) {
+    if (N > 32) {  // (kept across a switch to int32: a later stream starts packed again)
       const size_t w = (size_t)(N + 1) / 2;
       uint32_t* q = nullptr;
       HIPCHK(hipMalloc(&q, sizeof(uint32_t) * (size_t)N * nc * w));
@@ -534,6 +542,8 @@ struct hge_engine {
     ctx = 0;
     consensus.clear();
     n_und = 0;
+    wide32 = wide32_pending = false;  // a new stream starts on the packed path
+    chain_limit = chain_limit0;
     reset_rounds();
     HIPCHK(hipMemsetAsync(d_chain.p, 0xFF, (size_t)N * ccap * 4, st));
     sync();
@@ -583,9 +593,13 @@ struct hge_engine {
       return HGE_ERR_INDEX;
     }
     if (known >= chain_limit) {
-      err = "Chain capacity exceeded: the wide rounds kernels take at most " +
-            std::to_string(chain_limit) + " events per creator";
-      return HGE_ERR_CAPACITY;
+      if (N > 32 && N <= 256 && !wide32) {  // past the uint16 positions: int32 from here on
+        wide32_pending = true;
+        chain_limit = INT32_MAX;
+      } else {
+        err = "Chain capacity exceeded: at most " + std::to_string(chain_limit) + " events per creator";
+        return HGE_ERR_CAPACITY;
+      }
     }
     return HGE_OK;
   }
@@ -788,6 +802,7 @@ struct hge_engine {
   }
   bool coords_a() {
     upload();
+    if (wide32_pending) to_wide32();
     const int64_t n0 = n_coords, n1 = n_events;
     if (n1 == n0) return false;
     Tables t = tables();
@@ -876,7 +891,9 @@ struct hge_engine {
       if (retry) h2d(k_rs, rs, 12);
       t = tables();
       const int NP = (N + 15) & ~15;
-      if (N > 32) {
+      if (N > 32 && wide32) {
+        rounds_step32();
+      } else if (N > 32) {
         rounds_coop(fresh);
       } else {
         // first-strong-seer rows for every event that can still be a frontier member
@@ -1260,11 +1277,62 @@ struct hge_engine {
 
   // N > 32: lastAncestors live only in the packed 16-bit table (chains are capped at
   // 65,534 events there); the int32 LA rows exist for N <= 32
-  bool sweep16() const { return N > 32; }
+  bool sweep16() const { return N > 32 && !wide32; }
+
+  // the switch to int32 positions (hge_wide32.hip): the int32 LA rows of every event
+  // with coordinates, unpacked from LA16; from here on the N <= 32 sweeps and
+  // transposes, k_round_step32 and k_seg_theta32 take the wide path's place
+  void to_wide32() {
+    wide32_pending = false;
+    grow_chain_table(d_LA, ccap, false);
+    grow_chain_table(d_LAT, ccap, false, false);
+    s_w32.need(N);
+    h2d(s_w32.p, coords_len.data(), 4 * (size_t)N);
+    wide32 = true;
+    Tables t = tables();
+    int64_t most = 1;
+    for (int c = 0; c < N; c++) most = std::max<int64_t>(most, (int64_t)coords_len[c] * N);
+    KLAUNCH(k_la16_to_la32, dim3((unsigned)std::min<int64_t>(div_up(most, 256), 4096), N), dim3(256), 0, st, t,
+            (const uint32_t*)d_LA16.p, (const int32_t*)s_w32.p);
+  }
+
+  // rounds with int32 positions: k_round_step32 round by round from the first round
+  // to recompute, 32 launches between readbacks of their "row exists" flags
+  void rounds_step32() {
+    Tables t = tables();
+    s_fst.need(N + 1);
+    KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p);
+    int32_t rlo = INF32;
+    readback(&rlo, s_fst.p, 1);
+    if (rlo == INF32) return;
+    const int Rprev = R, NB = 32;
+    s_w32a.need(NB);
+    for (int r = rlo;;) {
+      HIPCHK(hipMemsetAsync(s_w32a.p, 0, 4 * NB, st));
+      int k = 0;
+      for (; k < NB && r + k + 1 < Rcap; k++)
+        KLAUNCH(k_round_step32, dim3(N), dim3(256), 0, st, t, (const int32_t*)k_len, (const int32_t*)(k_len + N),
+                r + k, Rprev, d_ssc.p, s_w32a.p + k);
+      std::vector<int32_t> alive(NB, 0);
+      readback(alive.data(), s_w32a.p, NB);
+      for (int q = 0; q < k; q++)
+        if (!alive[q]) {  // row r + q + 1 is empty: the rounds end there
+          const int32_t rs[2] = {std::max(R, r + q + 1), 0};
+          h2d(k_rs, rs, 8);
+          return;
+        }
+      r += k;
+      if (k < NB) {  // the rounds table is full: grown by the caller, walked again
+        const int32_t rs[2] = {R, 1};
+        h2d(k_rs, rs, 8);
+        return;
+      }
+    }
+  }
 
   // 32 < N <= 256: lastAncestors by windowed exact propagation (hge_coords_win.hip)
   // instead of the sweeps
-  bool la_windows() const { return N > 32 && N <= 256; }
+  bool la_windows() const { return N > 32 && N <= 256 && !wide32; }
 
   // passes over windows of the new ids until one changes no row (n_sweeps = passes
   // run); one window is exact in its first pass (its starting rows are final)
@@ -1623,9 +1691,14 @@ struct hge_engine {
           rr_lo, nr, ncalls, (const int32_t*)s_vis.p, si, (const int32_t*)c_sgo, s_segcnt.p,       \
           s_segcall.p, s_seground.p, s_segdec.p, s_segfws.p, s_theta.p);
 #define THW(B)                                                                                     \
-  KLAUNCH(k_seg_theta_wide<B>, dim3(std::min(nr, 4096)), dim3(256), 0, st, t,                      \
-          (const int32_t*)s_seground.p, (const int32_t*)c_sgo, (const int32_t*)s_segcnt.p, nr,     \
-          (const uint64_t*)s_segfws.p, s_theta.p);
+  if (wide32)                                                                                      \
+    KLAUNCH(k_seg_theta32<B>, dim3(std::min(nr, 4096)), dim3(256), 0, st, t,                       \
+            (const int32_t*)s_seground.p, (const int32_t*)c_sgo, (const int32_t*)s_segcnt.p, nr,   \
+            (const uint64_t*)s_segfws.p, s_theta.p);                                               \
+  else                                                                                             \
+    KLAUNCH(k_seg_theta_wide<B>, dim3(std::min(nr, 4096)), dim3(256), 0, st, t,                    \
+            (const int32_t*)s_seground.p, (const int32_t*)c_sgo, (const int32_t*)s_segcnt.p, nr,   \
+            (const uint64_t*)s_segfws.p, s_theta.p);
         if (G == 16) {
           SEG1(16, 1)
         } else if (G == 32) {
@@ -2283,7 +2356,8 @@ int hge_split_plan(hge_engine* h, int32_t part, int32_t nparts, const int64_t* e
     h->err = std::string("hge_split_plan: ") + why;
     return HGE_ERR_ARG;
   };
-  if (h->N <= 32 || !h->direct_rounds()) return bad("needs the wide direct rounds path");
+  if (h->N <= 32 || !h->direct_rounds() || h->wide32 || h->wide32_pending)
+    return bad("needs the wide direct rounds path (N > 32, N % 4 == 0, chains below 65,535 events)");
   if (part < 0 || part >= nparts || !ev_bounds || !call_bounds || !cand_lo) return bad("bad argument");
   const int64_t E = h->n_events;
   const int ncalls = (int)h->replay_calls.size();
@@ -2344,7 +2418,7 @@ int hge_split_run(hge_engine* h, int64_t* n_ordered) {
 
 int hge_split_begin(hge_engine* h) {
   GUARD_BEGIN
-  if (h->N <= 32 || !h->direct_rounds()) {
+  if (h->N <= 32 || !h->direct_rounds() || h->wide32 || h->wide32_pending) {
     h->err = "the split walk needs the wide direct rounds path (N > 32, N % 4 == 0)";
     return HGE_ERR_ARG;
   }

@@ -72,10 +72,11 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
 
 
 // lastAncestors[row][col], row = chain * ccap + position.  N > 32 keeps only the
-// packed table (LA16 = LA + 1 as uint16 pairs; chains are capped at 65,534 events
-// there): the int32 rows are never materialised, every reader unpacks.
+// packed table (LA16 = LA + 1 as uint16 pairs, chains below 65,535 events): the
+// int32 rows are not materialised, every reader unpacks.  Past that length the
+// engine switches to the int32 rows (LA16 = null: hge_engine.hip, to_wide32).
 __device__ __forceinline__ int la_row(const Tables& t, size_t row, int col) {
-  if (t.N > 32) {
+  if (t.LA16) {
     const uint32_t w = t.LA16[row * (size_t)t.NW2 + (col >> 1)];
     return (int)((w >> ((col & 1) << 4)) & 0xFFFFu) - 1;
   }

@@ -18,6 +18,7 @@ import pytest
 
 from babble_amd.gossip import random_gossip, schedule
 from oracle.oracle import replay as oracle_replay
+from parity import run_case
 
 pytestmark = pytest.mark.gpu
 INT64_MAX = np.iinfo(np.int64).max
@@ -149,27 +150,59 @@ def test_store_windows_and_sync_reads(size):
         eng.close()
 
 
-def test_chain_capacity_refused_at_admission(monkeypatch):
-    """Wide graphs keep chain positions as uint16 in the rounds kernels: a chain
-    past the limit is refused at admission (HGE_ERR_CAPACITY) and the engine
-    keeps working (HGE_CHAIN_LIMIT lowers the limit to force the boundary)."""
-    from babble_amd.engine import Engine, HgeError, events_array
-    monkeypatch.setenv("HGE_CHAIN_LIMIT", "40")
-    n, events = 36, 2000
-    dag = random_gossip(n, events, seed=5)
-    ev = events_array(dag)
-    eng = Engine(n, 4096)
+@pytest.mark.parametrize("n,events,limit", [(36, 2000, 40), (64, 6000, 60), (128, 12000, 70), (256, 20000, 60)])
+def test_chain_past_uint16_switches_to_int32_replay(monkeypatch, n, events, limit):
+    """Wide graphs keep chain positions as uint16 until a chain reaches the limit,
+    then switch to int32 positions for good (hge_wide32.hip; the reference has no
+    cap, hashgraph.go:328-363).  HGE_CHAIN_LIMIT lowers the switch point so a small
+    stream crosses it: the replay (switched at admission) equals the live oracle."""
+    from babble_amd.engine import Engine
+    monkeypatch.setenv("HGE_CHAIN_LIMIT", str(limit))
+    dag = random_gossip(n, events, seed=5 + n)
+    assert np.bincount(np.asarray(dag["creator"]), minlength=n).max() > limit
+    eng = Engine(n, events + 64)
     try:
-        with pytest.raises(HgeError) as ei:
-            eng.insert_events(ev)
-        assert ei.value.code == -7
-        acc = len(ei.value.accepted)
-        assert acc > n and eng.event_count() == acc
-        first = eng.run_consensus()  # still usable after the refusal
-        assert eng.rounds() > 0
-        assert len(first) >= 0
+        run_case(eng, dag, n)
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("n,events,limit", [(40, 4000, 50), (256, 24000, 50)])
+def test_chain_past_uint16_switches_mid_stream_online(monkeypatch, n, events, limit):
+    """The online path crosses the limit mid-stream (the packed table is unpacked
+    into int32 rows at the next coordinate step): the order, batches, rounds and
+    round received equal an engine that never switched (the bulk replay of the
+    packed path, no limit) and the fork-free stream stays fully accepted."""
+    from babble_amd.engine import Engine, events_array
+    from babble_amd.gossip import schedule
+    dag = random_gossip(n, events, seed=90 + n)
+    ev = events_array(dag)
+    calls = schedule(events, n)
+    ref = Engine(n, events + 64)  # created before the limit is set: packed all the way
+    monkeypatch.setenv("HGE_CHAIN_LIMIT", str(limit))
+    eng = Engine(n, events + 64)
+    try:
+        _, order, counts = ref.replay(ev, calls)
+        nxt, per = 0, []
+        for c in calls:
+            eng.insert_events(ev[nxt:c].copy())
+            per.append(len(eng.run_consensus()))
+            nxt = c
+        np.testing.assert_array_equal(eng.consensus_events(), order)
+        np.testing.assert_array_equal(np.asarray(per), counts)
+        assert eng.rounds() == ref.rounds()
+        assert eng.last_consensus_round() == ref.last_consensus_round()
+        for x, y in zip(eng.event_rounds(), ref.event_rounds()):
+            np.testing.assert_array_equal(x, y)
+        for x, y in zip(eng.event_received(), ref.event_received()):
+            np.testing.assert_array_equal(x, y)
+        # the coordinates read back from the int32 rows equal the packed ones
+        for i in (0, events // 2, events - 1):
+            for x, y in zip(eng.coordinates(i), ref.coordinates(i)):
+                np.testing.assert_array_equal(x, y)
+    finally:
+        eng.close()
+        ref.close()
 
 
 def test_replay_rejects_bad_call_points():
