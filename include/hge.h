@@ -41,10 +41,9 @@ enum hge_status {
    * it refuses index-lying events (Byzantine input only: an honest Core always
    * creates head.Index+1, node/core.go:87-99).  INTEGRATION.md, tests. */
   HGE_ERR_INDEX = -6,
-  /* device allocation failed, or the event would make its creator's chain longer
-   * than the engine takes (N > 32: 65,534 events per creator; the wide rounds
-   * kernels keep chain positions as uint16).  Refused at admission: the engine
-   * stays usable. */
+  /* device allocation failed.  (Chains have no length cap: at N > 32 a chain
+   * reaching 65,534 events switches the engine from its uint16 position tables
+   * to int32 ones) */
   HGE_ERR_CAPACITY = -7,
   HGE_ERR_ARG = -8,        /* bad argument */
   HGE_ERR_DEVICE = -9,     /* HIP runtime error */
@@ -80,7 +79,7 @@ typedef struct hge_event {
  * capacity_events is a sizing hint: the device tables grow on demand up to HBM.
  * Consensus math always runs with the reference's infinite-cache contract
  * (SURVEY.md TL;DR 8); hge_set_cache_size only shapes the rolling views below.
- * N > 32: at most 65,534 events per creator (HGE_ERR_CAPACITY at admission). */
+ * No cap on events per creator (N > 32 switches to int32 positions past 65,534). */
 int hge_create(int32_t n_participants, int64_t capacity_events, int32_t device,
                uint32_t flags, hge_engine** out);
 void hge_destroy(hge_engine* h);
