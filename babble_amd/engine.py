@@ -86,6 +86,8 @@ EXPORTS = [
     "hge_store_known", "hge_store_add_consensus_event", "hge_store_consensus_events",
     "hge_store_consensus_count", "hge_store_set_round", "hge_store_get_round", "hge_store_rounds",
     "hge_store_round_witnesses", "hge_store_round_events",
+    # the wire / hashing format (host only, hge_gob.cpp)
+    "hge_gob_encode_wire_events", "hge_gob_decode_wire_events", "hge_gob_encode_event_body",
 ]
 
 _lib = None
@@ -157,6 +159,13 @@ def lib():
     L.hge_stage_times.argtypes = [vp, P(ctypes.c_float), ctypes.c_int]
     L.hge_coordinate_sweeps.restype = ctypes.c_int32
     L.hge_coordinate_sweeps.argtypes = [vp]
+    if hasattr(L, "hge_gob_encode_wire_events"):
+        L.hge_gob_encode_wire_events.argtypes = [vp, i64, P(ctypes.c_uint8), P(i64), i32, P(ctypes.c_uint8), i64,
+                                                 P(i64)]
+        L.hge_gob_decode_wire_events.argtypes = [P(ctypes.c_uint8), i64, vp, i64, P(ctypes.c_uint8), i64, P(i64),
+                                                 i64, P(i64), P(i64), P(i64)]
+        L.hge_gob_encode_event_body.argtypes = [vp, P(ctypes.c_uint8), P(i64), P(ctypes.c_uint8), P(i64), i32,
+                                                P(ctypes.c_uint8), i64, P(i64)]
     if hasattr(L, "hge_host_syncs"):
         L.hge_host_syncs.restype = i64
         L.hge_host_syncs.argtypes = [vp]
@@ -246,6 +255,120 @@ def verify_events(bodies, pubs, sigs, threads=0):
     if rc != 0:
         raise HgeError(rc, "hge_verify_events failed")
     return ok[:n].astype(bool), hashes[:n]
+
+
+class GobTime(ctypes.Structure):
+    _fields_ = [("unix_sec", ctypes.c_int64), ("nsec", ctypes.c_int32), ("offset_min", ctypes.c_int16),
+                ("set", ctypes.c_int16)]
+
+
+class WireEvent(ctypes.Structure):
+    """hge_wire_event (include/hge.h): a babble WireEvent (hashgraph/event.go:244-259)."""
+    _fields_ = [("self_parent_index", ctypes.c_int64), ("other_parent_creator_id", ctypes.c_int64),
+                ("other_parent_index", ctypes.c_int64), ("creator_id", ctypes.c_int64), ("index", ctypes.c_int64),
+                ("timestamp", GobTime), ("r", ctypes.c_uint8 * 32), ("s", ctypes.c_uint8 * 32),
+                ("r_set", ctypes.c_int32), ("s_set", ctypes.c_int32), ("tx_first", ctypes.c_int64),
+                ("tx_count", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
+class GobBody(ctypes.Structure):
+    _fields_ = [("tx_count", ctypes.c_int32), ("n_parents", ctypes.c_int32),
+                ("creator", ctypes.POINTER(ctypes.c_uint8)), ("creator_len", ctypes.c_int64),
+                ("timestamp", GobTime), ("index", ctypes.c_int64)]
+
+
+WIRE_INT_FIELDS = ("self_parent_index", "other_parent_creator_id", "other_parent_index", "creator_id", "index")
+
+
+def _gob_time(ts):
+    """(unix_sec, nsec, offset_min) or None (the zero time.Time)."""
+    if ts is None:
+        return GobTime(0, 0, 0, 0)
+    return GobTime(int(ts[0]), int(ts[1]), int(ts[2]), 1)
+
+
+def gob_encode_wire_events(events, first_type_id=65):
+    """One gob encoder's stream of WireEvents (hge_gob_encode_wire_events).  events:
+    dicts with the WIRE_INT_FIELDS, "timestamp" (unix_sec, nsec, offset_min | None),
+    "r" / "s" (non-negative ints < 2**256 | None), "transactions" (list of bytes)."""
+    n = len(events)
+    arr = (WireEvent * max(n, 1))()
+    txs = []
+    for k, e in enumerate(events):
+        w = arr[k]
+        for f in WIRE_INT_FIELDS:
+            setattr(w, f, int(e.get(f, 0)))
+        w.timestamp = _gob_time(e.get("timestamp"))
+        for name in ("r", "s"):
+            v = e.get(name)
+            if v is not None:
+                getattr(w, name)[:] = list(int(v).to_bytes(32, "big"))
+                setattr(w, name + "_set", 1)
+        w.tx_first = len(txs)
+        w.tx_count = len(e.get("transactions", []))
+        txs.extend(e.get("transactions", []))
+    flat, off = _flat(txs)
+    L = lib()
+    nout = ctypes.c_int64()
+    rc = L.hge_gob_encode_wire_events(arr, n, _pu8(flat), _p64(off), first_type_id, None, 0, ctypes.byref(nout))
+    if rc != 0:
+        raise HgeError(rc, "hge_gob_encode_wire_events failed")
+    out = np.zeros(max(1, nout.value), np.uint8)
+    rc = L.hge_gob_encode_wire_events(arr, n, _pu8(flat), _p64(off), first_type_id, _pu8(out), nout.value,
+                                      ctypes.byref(nout))
+    if rc != 0:
+        raise HgeError(rc, "hge_gob_encode_wire_events failed")
+    return out[:nout.value].tobytes()
+
+
+def gob_decode_wire_events(buf):
+    """Every WireEvent in a gob stream (hge_gob_decode_wire_events), as the dicts
+    gob_encode_wire_events takes."""
+    b = np.frombuffer(bytes(buf), np.uint8) if len(buf) else np.zeros(1, np.uint8)
+    L = lib()
+    ne, nt, nb = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    rc = L.hge_gob_decode_wire_events(_pu8(b), len(buf), None, 0, None, 0, None, 0, ctypes.byref(ne),
+                                      ctypes.byref(nt), ctypes.byref(nb))
+    if rc not in (0, -12):
+        raise HgeError(rc, "not a gob stream of WireEvents")
+    arr = (WireEvent * max(1, ne.value))()
+    tx = np.zeros(max(1, nb.value), np.uint8)
+    off = np.zeros(nt.value + 1, np.int64)
+    rc = L.hge_gob_decode_wire_events(_pu8(b), len(buf), arr, ne.value, _pu8(tx), nb.value, _p64(off), len(off),
+                                      ctypes.byref(ne), ctypes.byref(nt), ctypes.byref(nb))
+    if rc != 0:
+        raise HgeError(rc, "not a gob stream of WireEvents")
+    out = []
+    for k in range(ne.value):
+        w = arr[k]
+        e = {f: int(getattr(w, f)) for f in WIRE_INT_FIELDS}
+        t = w.timestamp
+        e["timestamp"] = (int(t.unix_sec), int(t.nsec), int(t.offset_min)) if t.set else None
+        e["r"] = int.from_bytes(bytes(w.r), "big") if w.r_set else None
+        e["s"] = int.from_bytes(bytes(w.s), "big") if w.s_set else None
+        e["transactions"] = [tx[off[w.tx_first + j]:off[w.tx_first + j + 1]].tobytes() for j in range(w.tx_count)]
+        out.append(e)
+    return out
+
+
+def gob_encode_event_body(transactions, parents, creator, timestamp, index, first_type_id=65):
+    """EventBody.Marshal (hge_gob_encode_event_body): the bytes Sign/Verify hash."""
+    tflat, toff = _flat(list(transactions))
+    pflat, poff = _flat([p.encode() for p in parents])
+    cr = np.frombuffer(bytes(creator), np.uint8) if len(creator) else np.zeros(1, np.uint8)
+    body = GobBody(len(transactions), len(parents), _pu8(cr), len(creator), _gob_time(timestamp), int(index))
+    L = lib()
+    nout = ctypes.c_int64()
+    rc = L.hge_gob_encode_event_body(ctypes.byref(body), _pu8(tflat), _p64(toff), _pu8(pflat), _p64(poff),
+                                     first_type_id, None, 0, ctypes.byref(nout))
+    if rc != 0:
+        raise HgeError(rc, "hge_gob_encode_event_body failed")
+    out = np.zeros(max(1, nout.value), np.uint8)
+    rc = L.hge_gob_encode_event_body(ctypes.byref(body), _pu8(tflat), _p64(toff), _pu8(pflat), _p64(poff),
+                                     first_type_id, _pu8(out), nout.value, ctypes.byref(nout))
+    if rc != 0:
+        raise HgeError(rc, "hge_gob_encode_event_body failed")
+    return out[:nout.value].tobytes()
 
 
 def sha256_batch(data, threads=0):

@@ -339,6 +339,55 @@ int32_t hge_oldest_self_ancestor_to_see(hge_engine* h, int32_t x, int32_t y); /*
 /* lastAncestors / firstDescendants indices of x (FD unset = INT32_MAX), N ints each. */
 int hge_coordinates(hge_engine* h, int32_t id, int32_t* la_out, int32_t* fd_out);
 
+/* ---- wire and hashing format: encoding/gob, hge_gob.cpp --------
+ * Host only.  WireEvent (hashgraph/event.go:244-259) as babble puts it on the wire
+ * (SyncResponse.Events, net/commands.go; framing net/net_transport.go:297-395), and
+ * EventBody.Marshal (event.go:44-58), the bytes Sign/Verify hash.  Timestamps are
+ * Go time.Time values: Unix seconds, nanoseconds, zone offset in minutes (-1 =
+ * UTC; set = 0: the zero Time, omitted).  R, S: 32-byte big-endian magnitudes of
+ * the non-negative signature halves (r_set / s_set = 0: nil).  Transactions of
+ * event k are tx[tx_off[tx_first + j] .. tx_off[tx_first + j + 1]), j < tx_count.
+ * Gob type ids are process-global in Go: first_type_id is the id the first type
+ * defined takes (65 in a fresh process whose first gob type is this one). */
+typedef struct {
+  int64_t unix_sec;
+  int32_t nsec;
+  int16_t offset_min;
+  int16_t set;
+} hge_gob_time;
+typedef struct {
+  int64_t self_parent_index, other_parent_creator_id, other_parent_index, creator_id, index;
+  hge_gob_time timestamp;
+  uint8_t r[32], s[32];
+  int32_t r_set, s_set;
+  int64_t tx_first;
+  int32_t tx_count, pad;
+} hge_wire_event;
+typedef struct {
+  int32_t tx_count, n_parents;
+  const uint8_t* creator;
+  int64_t creator_len;
+  hge_gob_time timestamp;
+  int64_t index;
+} hge_gob_body;
+/* One encoder's stream: the type definitions, then one message per event (like
+ * successive gob Encoder.Encode(WireEvent) calls).  *n_out = bytes; out = NULL
+ * with cap = 0 asks for the size. */
+int hge_gob_encode_wire_events(const hge_wire_event* ev, int64_t n, const uint8_t* tx, const int64_t* tx_off,
+                               int32_t first_type_id, uint8_t* out, int64_t cap, int64_t* n_out);
+/* Every WireEvent in a gob stream (top-level values or nested, e.g. a
+ * SyncResponse's Events), any type ids, fields matched by name.  tx_off gets
+ * n_tx + 1 offsets.  HGE_ERR_NOT_FOUND: a capacity was too small (the counts say
+ * what is needed); HGE_ERR_ARG: not a well-formed stream of these types. */
+int hge_gob_decode_wire_events(const uint8_t* buf, int64_t len, hge_wire_event* ev, int64_t cap_ev, uint8_t* tx,
+                               int64_t cap_bytes, int64_t* tx_off, int64_t cap_tx, int64_t* n_ev, int64_t* n_tx,
+                               int64_t* n_bytes);
+/* EventBody.Marshal: a fresh encoder's stream of one EventBody (Parents: hex
+ * strings parents[parent_off[k] .. parent_off[k + 1])). */
+int hge_gob_encode_event_body(const hge_gob_body* body, const uint8_t* tx, const int64_t* tx_off,
+                              const uint8_t* parents, const int64_t* parent_off, int32_t first_type_id,
+                              uint8_t* out, int64_t cap, int64_t* n_out);
+
 /* ---- profiling ------------------------------------------------------------- */
 /* Device milliseconds of the last replay/batch by stage (HIP events on the
  * engine's stream): 0 coords, 1 rounds, 2 witness bits, 3 fame, 4 received,
