@@ -5,7 +5,7 @@ Runs two counter passes over `python3 bench.py <bench args>` (FETCH_SIZE, then
 WRITE_SIZE: they cannot share one pass on gfx950), each in its own rocprofv3
 run with --kernel-trace only, parses counter_collection.csv and merges
 {config-key: {kernel: {fetch_bytes, write_bytes, bytes_per_launch, launches}}}
-into profiles/r02/pmc_traffic.json.  FETCH_SIZE is reported in KiB and, on gfx950,
+into profiles/r03/pmc_traffic.json.  FETCH_SIZE is reported in KiB and, on gfx950,
 counts half of the bytes of wide coalesced reads (MI355X_MICROARCH.md §HBM),
 so it is doubled; WRITE_SIZE (KiB) is taken as is.
 """
@@ -64,7 +64,7 @@ def main():
         res[name] = {"fetch_bytes": round(fetch_b), "write_bytes": round(write_b),
                      "bytes_per_launch": round(fetch_b + write_b), "launches": launches,
                      "bytes_per_replay": round(per_replay), "replays": replays}
-    path = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
+    path = os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json")
     os.makedirs(os.path.dirname(path), exist_ok=True)
     try:
         allres = json.load(open(path))
