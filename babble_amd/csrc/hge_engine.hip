@@ -1995,7 +1995,7 @@ struct hge_engine {
 #define DCASE(B)                                                                                     \
   case B:                                                                                            \
     if (N == 64 * B)                                                                                 \
-      KLAUNCH((k_fame_decide<B, true>), dim3(div_up(items, 256)), dim3(256), 0, st, t, c_pr + k_lo,   \
+      KLAUNCH((k_fame_decide_blk<B>), dim3(p1 - p0), dim3(N), 0, st, t, c_pr + k_lo,                  \
               c_pr + nrounds + k_lo, c_pr + 2 * nrounds + k_lo, k_hi - k_lo, p0, p1, c_nc, c_Rc,      \
               s_dec.p);                                                                              \
     else                                                                                             \

@@ -982,6 +982,97 @@ __global__ void k_fame_decide(Tables t, const int32_t* pr_round, const int32_t* 
   dec[(size_t)p * N + xd] = out;
 }
 
+// k_fame_decide for N = 64 * NWT, one (round i, call c) pair per block of N
+// threads (thread = witness slot x of round i): the rows every lane of the pair
+// reads -- round j's witnesses W[j][.], their strongly-see bitsets ssb[j][.] and
+// coins -- are staged in LDS once per j by one coalesced load of the block, and
+// the y loop reads them as LDS broadcasts (the per-lane k_fame_decide reads them
+// as chains of scalar loads, 8 slots at a time).  Same decisions, same output.
+template <int NWT>
+__global__ void __launch_bounds__(256) k_fame_decide_blk(Tables t, const int32_t* pr_round, const int32_t* pr_off,
+                                                         const int32_t* pr_cf, int nrounds, int p0, int npairs,
+                                                         const int64_t* nc, const int32_t* Rc, uint8_t* dec) {
+  __shared__ int sY[64 * NWT];    // witness y of slot d, -1 if none or not yet inserted at call c
+  __shared__ int sTot[64 * NWT];  // |ssb[y]|: the same for every lane
+  __shared__ uint64_t sS[64 * NWT][NWT];
+  __shared__ uint8_t sCoin[64 * NWT];
+  const int N = t.N, SM = t.SM;
+  const int p = p0 + (int)xcd_block(blockIdx.x, gridDim.x);  // (XCD-aware: neighbouring pairs share rows)
+  if (p >= npairs) return;
+  const int xd = threadIdx.x;
+  int lo = 0, hi = nrounds - 1;  // last round with pr_off <= p
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (pr_off[mid] <= p) lo = mid;
+    else hi = mid - 1;
+  }
+  const int i = pr_round[lo];
+  const int c = pr_cf[lo] + (p - pr_off[lo]);
+  const int64_t n = nc[c];
+  const int R = Rc[c];
+  const int x = t.W[(size_t)i * N + xd];
+  const bool act = x >= 0 && x < n;
+  if (R <= i + 2) {  // no round j in [i + 2, R) votes: no decision (block-uniform)
+    dec[(size_t)p * N + xd] = 0;
+    return;
+  }
+  auto stage = [&](int j, const uint64_t* bits) {
+    __syncthreads();  // every lane is done with the previous round's rows
+    const int y = t.W[(size_t)j * N + xd];
+    sY[xd] = (y >= 0 && y < n) ? y : -1;
+    int tot = 0;
+#pragma unroll
+    for (int w = 0; w < NWT; w++) {
+      const uint64_t b = bits[((size_t)j * N + xd) * NWT + w];
+      sS[xd][w] = b;
+      tot += __popcll(b);
+    }
+    sTot[xd] = tot;
+    sCoin[xd] = y >= 0 ? t.coin[y] : 0;
+    __syncthreads();
+  };
+  uint64_t votes[NWT], cur[NWT];
+#pragma unroll
+  for (int w = 0; w < NWT; w++) votes[w] = 0;
+  // diff == 1: vote = See(y, x)
+  stage(i + 1, t.seeb);
+  if (act)
+    for (int d = 0; d < N; d++) {
+      if (sY[d] >= 0 && ((sS[d][xd >> 6] >> (xd & 63)) & 1ull)) votes[d >> 6] |= 1ull << (d & 63);
+    }
+  uint8_t out = 0;
+  for (int j = i + 2; j < R; j++) {
+    stage(j, t.ssb);
+    if (!act) continue;
+    const int diff = j - i;
+    const bool coinr = (diff % N) == 0;
+#pragma unroll
+    for (int w = 0; w < NWT; w++) cur[w] = 0;
+    for (int d = 0; d < N; d++) {
+      if (sY[d] < 0) continue;
+      int yays = 0;
+#pragma unroll
+      for (int w = 0; w < NWT; w++) yays += __popcll(sS[d][w] & votes[w]);
+      const int nays = sTot[d] - yays;
+      const bool v = yays >= nays;
+      const int tt = v ? yays : nays;
+      if (!coinr) {
+        if (tt >= SM) {
+          out = v ? 1 : 2;  // the last decision over j is what SetFame leaves
+          break;            // later y of this j cast no vote
+        }
+        if (v) cur[d >> 6] |= 1ull << (d & 63);
+      } else {
+        const bool vv = (tt >= SM) ? v : (sCoin[d] != 0);
+        if (vv) cur[d >> 6] |= 1ull << (d & 63);
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < NWT; w++) votes[w] = cur[w];
+  }
+  dec[(size_t)p * N + xd] = act ? out : 0;
+}
+
 // LCR_c = max(LCR_start, prefix max of Lc); c_last(i) = first call with LCR >= i;
 // coverage check of each round's speculative window.
 __global__ void __launch_bounds__(1024) k_lcr_scan(const int32_t* Lc, int ncalls, int lcr_start,
