@@ -1999,7 +1999,7 @@ struct hge_engine {
               c_pr + nrounds + k_lo, c_pr + 2 * nrounds + k_lo, k_hi - k_lo, p0, p1, c_nc, c_Rc,      \
               s_dec.p);                                                                              \
     else                                                                                             \
-      KLAUNCH((k_fame_decide<B, false>), dim3(div_up(items, 256)), dim3(256), 0, st, t, c_pr + k_lo,  \
+      KLAUNCH((k_fame_decide<B>), dim3(div_up(items, 256)), dim3(256), 0, st, t, c_pr + k_lo,         \
               c_pr + nrounds + k_lo, c_pr + 2 * nrounds + k_lo, k_hi - k_lo, p0, p1, c_nc, c_Rc,      \
               s_dec.p);                                                                              \
     break;

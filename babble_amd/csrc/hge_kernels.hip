@@ -877,10 +877,8 @@ __global__ void k_witness_bits(Tables t, const int32_t* newwit, const int32_t* p
 // j+1), and the LAST decision over j is what SetFame leaves.  Output per
 // (pair, slot): 0 no decision in this call, 1 famous, 2 not famous.
 // ---------------------------------------------------------------------------
-// WP (N % 64 == 0): a wave's 64 slots belong to one pair, so the pair index is
-// made wave-uniform and every witness-row load (W, ssb, seeb) becomes a scalar
-// load shared by the wave instead of 64 lanes loading the same address.
-template <int NWT, bool WP>
+// (N % 64 == 0 takes k_fame_decide_blk below: one pair per block, rows in LDS.)
+template <int NWT>
 __global__ void k_fame_decide(Tables t, const int32_t* pr_round, const int32_t* pr_off,
                               const int32_t* pr_cf, int nrounds, int p0, int npairs,
                               const int64_t* nc, const int32_t* Rc, uint8_t* dec) {
@@ -893,7 +891,6 @@ __global__ void k_fame_decide(Tables t, const int32_t* pr_round, const int32_t* 
   int p = item / N;
   const int xd = item - p * N;
   p += p0;
-  if constexpr (WP) p = __builtin_amdgcn_readfirstlane(p);
   int lo = 0, hi = nrounds - 1;  // last round with pr_off <= p
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -914,7 +911,7 @@ __global__ void k_fame_decide(Tables t, const int32_t* pr_round, const int32_t* 
     for (int w = 0; w < NWT; w++) votes[w] = 0;
     // the witness rows are read in chunks of DC slots with every load of a chunk
     // in flight before the first use (the d loops are latency chains otherwise)
-    constexpr int DC = WP ? 8 : 16;  // WP: the chunk lives in SGPRs (16 spilled 119 of them)
+    constexpr int DC = 16;
     // diff == 1: vote = See(y, x)
     for (int d0 = 0; d0 < N; d0 += DC) {
       int ys[DC];
