@@ -48,6 +48,10 @@ type Hashgraph struct {
 
 	eng   *C.hge_engine
 	store *InmemStore // the engine-backed store (owns the hash <-> id maps)
+	// the Body.Timestamp of an inserted event per instant (UnixNano): a consensus
+	// timestamp is one of them (MedianTimestamp returns a source event's Time,
+	// hashgraph.go:762-770), so FindOrder hands back that Time value, zone included
+	tsByNano map[int64]time.Time
 
 	logger *logrus.Logger
 }
@@ -75,6 +79,7 @@ func NewHashgraph(participants map[string]int, store Store, commitCh chan []Even
 		commitCh:            commitCh,
 		store:               s,
 		logger:              logger,
+		tsByNano:            make(map[int64]time.Time),
 	}
 	capacity := C.int64_t(s.cacheSize)
 	if capacity < 1<<16 {
@@ -247,6 +252,9 @@ func (h *Hashgraph) insert(event *Event) error {
 	}
 	hex := event.Hex()
 	h.store.remember(hex, status)
+	if _, seen := h.tsByNano[int64(ev.timestamp_ns)]; !seen {
+		h.tsByNano[int64(ev.timestamp_ns)] = event.Body.Timestamp
+	}
 	if err := h.SetWireInfo(event); err != nil {
 		return err
 	}
@@ -420,7 +428,12 @@ func (h *Hashgraph) FindOrder() error {
 				return err
 			}
 			ev.SetRoundReceived(int(C.hge_round_received(h.eng, id)))
-			ev.consensusTimestamp = time.Unix(0, int64(C.hge_consensus_timestamp(h.eng, id)))
+			cts := int64(C.hge_consensus_timestamp(h.eng, id))
+			if t, ok := h.tsByNano[cts]; ok {
+				ev.consensusTimestamp = t // the source event's Time (location included)
+			} else {
+				ev.consensusTimestamp = time.Unix(0, cts)
+			}
 			h.store.events[hex] = ev
 			batch = append(batch, ev)
 		}
