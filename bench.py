@@ -270,7 +270,8 @@ def main():
     ap.add_argument("--events", type=int, default=None)
     ap.add_argument("--k", type=int, default=None, help="RunConsensus every k submissions")
     ap.add_argument("--graphs", type=int, default=1024, help="mc: hashgraphs in the whole batch")
-    ap.add_argument("--threads", type=int, default=8, help="mc: host threads driving engines")
+    ap.add_argument("--threads", type=int, default=16,
+                    help="mc: host threads driving engines (the box's CPU share per GPU; 4 / 8 / 16 threads: 44.3 / 53.1 / 58.3M ev/s, profiles/r03/configs/mc_threads)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")

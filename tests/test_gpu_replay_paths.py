@@ -1,7 +1,7 @@
 """The fresh replay at N = 256 against the engine's other paths: the online
 per-call path, a replay whose rounds table overflows and grows mid-walk, and
 repeated replays of the staged stream (the bench's steps).  The 256-participant
-goldens (test_gpu_golden.py) and the bench's 409,600-submission prefix check the
+goldens (test_gpu_golden.py) and the bench's 819,200-submission prefix check the
 replay against the oracle."""
 import numpy as np
 import pytest
