@@ -136,6 +136,15 @@ def golden_prefix(n, E, K, seed):
     return np.load(path)
 
 
+def golden_full(n, E, K, seed):
+    """The committed whole-stream oracle digests of this exact stream, or None
+    (tests/golden/make_bench_full.py)."""
+    path = os.path.join(ROOT, "tests", "golden", f"bench_n{n}_e{E}_k{K}_s{seed}_full.json")
+    if not os.path.exists(path):
+        return None
+    return json.load(open(path))
+
+
 def mc_digests(n, E, K, seed):
     """The committed oracle digests of config 5's batch (tests/golden/make_mc_digests.py)
     when this run replays exactly that batch, else None."""
@@ -383,7 +392,7 @@ def main():
     replay_ms = {"coords_gpu": st_ms[0], "coords_wall": st_ms[1], "consensus_gpu": st_ms[3],
                  "consensus_wall": st_ms[2], "gpu": st_ms[6], "wall": st_ms[4]}
     replay_ms = {k: round(v, 4) for k, v in replay_ms.items()}
-    _, gorder, gcounts = eng0.fetch()
+    gstatus, gorder, gcounts = eng0.fetch()
 
     # ---- profiled pass: per-kernel device time (HIP events on the engine stream) ----
     nprof = max(1, args.profile_steps)
@@ -470,6 +479,21 @@ def main():
             checks.append(f"{'bit-exact' if not bad else 'MISMATCH in ' + ','.join(bad)} vs committed oracle "
                           f"golden ({what}; first {int(gp['prefix'])} submissions, {nc} calls, "
                           f"{len(gp['order'])} ordered)")
+        gf = golden_full(n, E, K, args.seed)
+        if gf is not None:
+            # the whole stream: every field of the parity contract against the
+            # oracle's digests (tests/golden/make_bench_full.py); a sharded run
+            # holds the whole order and batches on every rank, the per-event
+            # fields only for its own slice
+            sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+            from digest import compare_full, engine_state
+            only = ("order", "counts") if split else None
+            bad = compare_full(engine_state(eng0, gstatus, gorder, gcounts), gf, only)
+            what = "order, batches" if split else ("status, order, batches, rounds, witnesses, fame, round "
+                                                   "received, timestamps, undetermined, scalars")
+            checks.append(f"{'bit-exact' if not bad else 'MISMATCH in ' + ','.join(bad)} vs the oracle's "
+                          f"whole-stream digests ({what}; all {gf['n_calls']} calls, {gf['ordered']} ordered, "
+                          f"{gf['scalars'][0]} rounds, LCR {gf['scalars'][1]})")
     if rank == 0 and not args.no_cpu_baseline and mc:
         # the oracle on whole graphs of the batch, one core, until ~10 s of work
         from oracle.oracle import replay as oracle_replay

@@ -16,6 +16,35 @@
 // or a seeded random permutation per iteration to emulate Go's randomised
 // map order.
 //
+// Two modes over the same store:
+//  * faithful (default): the Go loops as written, with the memo caches.  The
+//    bench's CPU baseline times this mode.
+//  * scale (hgo_create2 flag 1; canonical witness order, no SetRound seeding):
+//    the same functions computed without re-deriving what cannot change within
+//    one call, so that whole 1M-10M-event streams fit in the container:
+//      - the pure-memo caches (ancestor, selfAncestor, stronglySee,
+//        oldestSelfAncestor) are not kept: their answers never change once both
+//        events exist (SURVEY TL;DR 7), so recomputing gives the same value;
+//        roundCache / parentRoundCache, whose first-computed values ARE the
+//        semantics (Round depends on Rounds() when first asked), are kept as
+//        dense arrays;
+//      - DecideFame's `votes` map becomes, per (round i, witness x), a bitset
+//        over the witnesses of round j (set only when the vote is true, as a
+//        missing vote reads as false), and the ssWitnesses of (y, j-1) a bitset
+//        built once per call: yays / nays are popcounts of their intersection;
+//      - WitnessesDecided is a counter of undecided witness entries;
+//      - DecideRoundReceived's "more than half of the famous witnesses see x"
+//        is x.index <= theta(round, creator(x)), the (|F|/2+1)-th largest
+//        lastAncestor index among the famous witnesses, recomputed when the
+//        round's fame changes; the median is taken over the same set;
+//      - optional release of the coordinates of events ordered long ago (any
+//        later read of them aborts the process, so a completed run used none).
+//    tests/test_oracle_fast.py checks both modes field by field, and every
+//    golden regenerated in scale mode is byte-identical to the faithful one.
+//
+// Coordinates (event.go:68-71, EventCoordinates{hash, index}) are stored as
+// 4-byte event ids and indexes; an index outside int32 is refused.
+//
 // Parity pinning: there are no fixed-byte golden vectors in the reference
 // (keys/signatures come from crypto/rand).  This oracle is pinned by the
 // reference's own known-answer tests restated as fixtures in tests/golden/
@@ -23,9 +52,13 @@
 //
 // Citations are /root/reference relative paths.
 #include <algorithm>
+#include <climits>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <random>
 #include <string>
 #include <unordered_map>
@@ -35,12 +68,8 @@ namespace {
 
 constexpr int64_t kMaxInt64 = INT64_MAX;     // hashgraph.go:404-406 sentinel
 constexpr int64_t kZeroTime = INT64_MIN;     // Go zero time.Time (never reached)
-
-// EventCoordinates{hash, index} — event.go:68-71. hash is the event id (-1 = "").
-struct Coord {
-  int hash;
-  int64_t index;
-};
+constexpr int32_t kFdUnset = INT32_MAX;      // the MaxInt64 sentinel in 4 bytes
+constexpr int kUnset = INT_MIN;              // dense round memo: not computed yet
 
 // Event — event.go:73-88 (fields the ordering path reads).
 struct Event {
@@ -57,7 +86,9 @@ struct Event {
   bool has_rr = false;
   int rr = 0;
   int64_t cts = 0;
-  std::vector<Coord> la, fd;
+  // lastAncestors / firstDescendants (event.go:84-85): 4 rows of n int32,
+  // [la index | fd index | la event id | fd event id]; null once released.
+  std::unique_ptr<int32_t[]> co;
 };
 
 // RoundEvent / RoundInfo — roundInfo.go:24-60.
@@ -67,17 +98,24 @@ struct RoundEvent {
   Trilean famous;
 };
 
-struct Oracle;
-
 struct RoundInfo {
   std::unordered_map<int, RoundEvent> events;  // Events map[hash]RoundEvent
   std::vector<int> keys;                       // insertion order (for determinism)
+  // derived views kept in step with `events` (read by the scale mode only)
+  std::vector<int> wkeys;  // keys whose entry is a witness, in insertion order
+  int undecided = 0;       // witness entries with famous == Undefined
+  int version = 0;         // bumped whenever a witness entry or a fame value changes
 
   // roundInfo.go:53-60
   void AddEvent(int x, bool witness) {
     if (events.find(x) == events.end()) {
       events[x] = RoundEvent{witness, Undefined};
       keys.push_back(x);
+      if (witness) {
+        wkeys.push_back(x);
+        undecided++;
+        version++;
+      }
     }
   }
   // roundInfo.go:62-75
@@ -87,11 +125,14 @@ struct RoundInfo {
     if (it == events.end()) {
       e = RoundEvent{true, Undefined};
       keys.push_back(x);
+      wkeys.push_back(x);
     } else {
       e = it->second;
+      if (e.witness && e.famous == Undefined) undecided--;
     }
     e.famous = f ? True : False;
     events[x] = e;
+    version++;
   }
   // roundInfo.go:78-85
   bool WitnessesDecided() const {
@@ -101,10 +142,20 @@ struct RoundInfo {
   }
 };
 
+[[noreturn]] void die(const char* what, long long v) {
+  std::fprintf(stderr, "hg_oracle: %s (%lld)\n", what, v);
+  std::fflush(stderr);
+  std::abort();
+}
+
 struct Oracle {
   int n = 0;             // len(Participants)
   uint64_t order_seed;   // 0 = canonical (ascending creator) map order
   std::mt19937_64 rng;
+  bool scale = false;    // scale mode requested (see the header)
+  bool seeded = false;   // Store.SetRound was called from outside: faithful path only
+  int release_lag = -1;  // scale mode: release ordered events' coordinates this many rounds behind LCR
+  size_t release_next = 0;
 
   // InmemStore (inmem_store.go:20-36), infinite cache contract (SURVEY TL;DR 8)
   std::vector<Event> events;                    // eventCache
@@ -127,15 +178,38 @@ struct Oracle {
   int64_t stat_coin_evals = 0, stat_coin_votes = 0, stat_redecided = 0, stat_flipped = 0;
   std::unordered_map<uint64_t, int> oldestSelfAncestorCache;
   std::unordered_map<int, int> parentRoundCache, roundCache;
+  // scale mode: the same two caches, dense; `added` = DivideRounds already added x
+  std::vector<int> parentRoundMemo, roundMemo;
+  std::vector<uint8_t> added;
+  // scale mode, DecideRoundReceived: per round, thresholds valid for `version`
+  struct Theta {
+    int version = -1;
+    std::vector<int> famous;
+    std::vector<int32_t> th;  // [creator]
+  };
+  std::vector<Theta> thetas;
 
   std::string last_error;
   std::vector<int> last_batch;  // events committed by the last FindOrder
 
   Oracle(int n_, uint64_t seed) : n(n_), order_seed(seed), rng(seed), participant(n_) {}
 
+  bool fast() const { return scale && order_seed == 0 && !seeded; }
+
   static uint64_t key(int x, int y) { return (uint64_t)(uint32_t)x << 32 | (uint32_t)y; }
   bool getEvent(int x) const { return x >= 0 && x < (int)events.size(); }
   int SuperMajority() const { return 2 * n / 3 + 1; }  // hashgraph.go:78-80
+
+  // coordinate rows of event x
+  int32_t* co(int x) const {
+    int32_t* p = events[x].co.get();
+    if (!p) die("coordinates of a released event were read; raise the release lag", x);
+    return p;
+  }
+  const int32_t* laIx(int x) const { return co(x); }
+  const int32_t* fdIx(int x) const { return co(x) + n; }
+  const int32_t* laId(int x) const { return co(x) + 2 * n; }
+  const int32_t* fdId(int x) const { return co(x) + 3 * n; }
 
   // Go map iteration emulation for RoundInfo.Witnesses()/FamousWitnesses().
   std::vector<int> ordered(std::vector<int> v) {
@@ -180,6 +254,7 @@ struct Oracle {
 
   // ---------------- predicates (hashgraph.go:82-305) ----------------
   bool Ancestor(int x, int y) {
+    if (fast()) return ancestor(x, y);
     auto k = key(x, y);
     auto it = ancestorCache.find(k);
     if (it != ancestorCache.end()) return it->second;
@@ -191,11 +266,11 @@ struct Oracle {
     if (x < 0) return false;
     if (x == y) return true;
     if (!getEvent(x) || !getEvent(y)) return false;
-    const Event& ex = events[x];
     const Event& ey = events[y];
-    return ex.la[ey.creator].index >= ey.index;
+    return laIx(x)[ey.creator] >= ey.index;
   }
   bool SelfAncestor(int x, int y) {
+    if (fast()) return selfAncestor(x, y);
     auto k = key(x, y);
     auto it = selfAncestorCache.find(k);
     if (it != selfAncestorCache.end()) return it->second;
@@ -211,6 +286,7 @@ struct Oracle {
   }
   bool See(int x, int y) { return Ancestor(x, y); }  // hashgraph.go:149-154
   int OldestSelfAncestorToSee(int x, int y) {
+    if (fast()) return oldestSelfAncestorToSee(x, y);
     auto k = key(x, y);
     auto it = oldestSelfAncestorCache.find(k);
     if (it != oldestSelfAncestorCache.end()) return it->second;
@@ -220,11 +296,12 @@ struct Oracle {
   }
   int oldestSelfAncestorToSee(int x, int y) {  // hashgraph.go:166-177
     if (!getEvent(x) || !getEvent(y)) return -1;
-    const Coord& a = events[y].fd[events[x].creator];
-    if (a.index <= events[x].index) return a.hash;
+    const int cx = events[x].creator;
+    if (fdIx(y)[cx] <= events[x].index) return fdId(y)[cx];
     return -1;
   }
   bool StronglySee(int x, int y) {
+    if (fast()) return stronglySee(x, y);
     auto k = key(x, y);
     auto it = stronglySeeCache.find(k);
     if (it != stronglySeeCache.end()) return it->second;
@@ -234,14 +311,18 @@ struct Oracle {
   }
   bool stronglySee(int x, int y) {  // hashgraph.go:189-208
     if (!getEvent(x) || !getEvent(y)) return false;
-    const Event& ex = events[x];
-    const Event& ey = events[y];
+    const int32_t* la = laIx(x);
+    const int32_t* fd = fdIx(y);
     int c = 0;
-    for (int i = 0; i < (int)ex.la.size(); i++)
-      if (ex.la[i].index >= ey.fd[i].index) c++;
+    for (int i = 0; i < n; i++) c += la[i] >= fd[i];
     return c >= SuperMajority();
   }
   int ParentRound(int x) {
+    if (fast() && getEvent(x)) {
+      int& m = parentRoundMemo[x];
+      if (m == kUnset) m = parentRound(x);
+      return m;
+    }
     auto it = parentRoundCache.find(x);
     if (it != parentRoundCache.end()) return it->second;
     int pr = parentRound(x);
@@ -269,12 +350,30 @@ struct Oracle {
     int pr = ParentRound(x);
     if (pr < 0) return false;
     if (Rounds() < pr + 1) return false;
+    if (fast()) {  // the count of RoundWitnesses(pr) x strongly sees; order-free, so from wkeys
+      auto it = rounds.find(pr);
+      if (it == rounds.end()) return false;
+      const std::vector<int>& w = it->second.wkeys;
+      const int sm = SuperMajority(), m = (int)w.size();
+      int c = 0;
+      for (int k = 0; k < m && c < sm && c + (m - k) >= sm; k++) c += stronglySee(x, w[k]);
+      return c >= sm;
+    }
     int c = 0;
     for (int w : RoundWitnesses(pr))
       if (StronglySee(x, w)) c++;
     return c >= SuperMajority();
   }
   int Round(int x) {
+    if (fast() && getEvent(x)) {
+      int& m = roundMemo[x];
+      if (m == kUnset) {
+        int r = round(x);
+        roundMemo[x] = r;  // round() may grow nothing, but keep the write after it
+        return r;
+      }
+      return m;
+    }
     auto it = roundCache.find(x);
     if (it != roundCache.end()) return it->second;
     int r = round(x);
@@ -290,7 +389,8 @@ struct Oracle {
   // ---------------- insertion (hashgraph.go:328-494) ----------------
   // Returns new id >= 0, or a negative error code:
   //  -1 bad creator, -2 self-parent not known, -3 self-parent different creator,
-  //  -4 other-parent not known, -5 self-parent not last known.
+  //  -4 other-parent not known, -5 self-parent not last known,
+  //  -6 index outside this oracle's int32 coordinate range (not a reference error).
   int FromParentsLatest(const Event& e) {  // hashgraph.go:366-396
     int known = (int)participant[e.creator].size();
     if (e.sp < 0 && e.op < 0 && known == 0) return 0;
@@ -306,6 +406,10 @@ struct Oracle {
     if (e.creator < 0 || e.creator >= n) { last_error = "Could not find fake creator id"; return -1; }
     int err = FromParentsLatest(e);
     if (err) return err;
+    if (e.index < INT32_MIN || e.index >= kFdUnset) {
+      last_error = "Index outside the oracle's int32 coordinate range";
+      return -6;
+    }
     e.topo = topological_index++;
     // SetWireInfo (hashgraph.go:496-524)
     e.sp_index = e.sp >= 0 ? (int)events[e.sp].index : -1;
@@ -317,40 +421,65 @@ struct Oracle {
     // Store.SetEvent (inmem_store.go:51-65): new key -> participant list
     participant[e.creator].push_back(id);
     events.push_back(std::move(e));
+    if (scale) {
+      parentRoundMemo.push_back(kUnset);
+      roundMemo.push_back(kUnset);
+      added.push_back(0);
+    }
     UpdateAncestorFirstDescendant(id);
     undetermined.push_back(id);
     return id;
   }
 
   void InitEventCoordinates(Event& e, int id) {  // hashgraph.go:399-463
-    e.fd.assign(n, Coord{-1, kMaxInt64});
-    e.la.assign(n, Coord{-1, -1});
+    e.co.reset(new int32_t[4 * (size_t)n]);
+    int32_t* la = e.co.get();
+    int32_t* fd = la + n;
+    int32_t* lah = la + 2 * n;
+    int32_t* fdh = la + 3 * n;
+    for (int i = 0; i < n; i++) {
+      la[i] = -1;
+      lah[i] = -1;
+      fd[i] = kFdUnset;
+      fdh[i] = -1;
+    }
     if (e.sp < 0 && e.op < 0) {
       // all -1
     } else if (e.sp < 0) {
-      e.la = events[e.op].la;
+      std::memcpy(la, laIx(e.op), n * 4);
+      std::memcpy(lah, laId(e.op), n * 4);
     } else if (e.op < 0) {
-      e.la = events[e.sp].la;
+      std::memcpy(la, laIx(e.sp), n * 4);
+      std::memcpy(lah, laId(e.sp), n * 4);
     } else {
-      e.la = events[e.sp].la;
-      const auto& opla = events[e.op].la;
+      std::memcpy(la, laIx(e.sp), n * 4);
+      std::memcpy(lah, laId(e.sp), n * 4);
+      const int32_t* opla = laIx(e.op);
+      const int32_t* oplah = laId(e.op);
       for (int i = 0; i < n; i++)
-        if (e.la[i].index < opla[i].index) e.la[i] = opla[i];
+        if (la[i] < opla[i]) {
+          la[i] = opla[i];
+          lah[i] = oplah[i];
+        }
     }
-    e.fd[e.creator] = Coord{id, e.index};
-    e.la[e.creator] = Coord{id, e.index};
+    fd[e.creator] = (int32_t)e.index;
+    fdh[e.creator] = id;
+    la[e.creator] = (int32_t)e.index;
+    lah[e.creator] = id;
   }
 
   void UpdateAncestorFirstDescendant(int id) {  // hashgraph.go:466-494
     const int c = events[id].creator;
-    const int64_t index = events[id].index;
+    const int32_t index = (int32_t)events[id].index;
+    const int32_t* lah = laId(id);
     for (int i = 0; i < n; i++) {
-      int ah = events[id].la[i].hash;
+      int ah = lah[i];
       while (ah >= 0) {
-        Event& a = events[ah];
-        if (a.fd[c].index == kMaxInt64) {
-          a.fd[c] = Coord{id, index};
-          ah = a.sp;
+        int32_t* a = co(ah);
+        if (a[n + c] == kFdUnset) {
+          a[n + c] = index;
+          a[3 * n + c] = id;
+          ah = events[ah].sp;
         } else {
           break;
         }
@@ -360,6 +489,17 @@ struct Oracle {
 
   // ---------------- consensus (hashgraph.go:573-760) ----------------
   void DivideRounds() {  // hashgraph.go:573-588
+    if (fast()) {
+      for (int x : undetermined) {
+        int r = Round(x);
+        bool w = Witness(x);
+        if (!added[x]) {  // AddEvent of an event already in its round is a no-op
+          rounds[r].AddEvent(x, w);
+          added[x] = 1;
+        }
+      }
+      return;
+    }
     for (int x : undetermined) {
       int r = Round(x);
       bool w = Witness(x);
@@ -374,6 +514,7 @@ struct Oracle {
   }
 
   void DecideFame() {  // hashgraph.go:598-664
+    if (fast()) return DecideFameScale();
     // votes[y][x] => vote(y, x); rebuilt every call (hashgraph.go:599)
     std::unordered_map<uint64_t, bool> votes;
     auto setVote = [&](int y, int x, bool v) { votes[key(y, x)] = v; };
@@ -431,6 +572,101 @@ struct Oracle {
     }
   }
 
+  // Scale mode DecideFame: the loops above with the votes of one (i, x) as a
+  // bitset over round j's witnesses (bit set iff vote(y, x) was set true in this
+  // call; unset and false both read as nay) and ssWitnesses(y) as a bitset over
+  // round j-1's witnesses.  Rounds are contiguous here (no external SetRound),
+  // so rounds[i] exists for every i < Rounds().
+  void DecideFameScale() {
+    const int start = has_lcr ? lcr + 1 : 0;
+    const int R = Rounds();
+    if (start >= R - 1) return;
+    if (rounds.begin()->first != 0 || rounds.rbegin()->first != R - 1) die("rounds not contiguous", R);
+    const int SM = SuperMajority();
+    const int nr = R - start;
+    std::vector<std::vector<int>> W(nr);
+    for (int j = start; j < R; j++) W[j - start] = ordered(rounds.at(j).wkeys);
+    // ssb[j][ys]: the witnesses of round j-1 that witness ys of round j strongly sees
+    std::vector<std::vector<uint64_t>> ssb(nr);
+    std::vector<std::vector<uint8_t>> ssOk(nr);
+    auto ss = [&](int j, int ys) -> const uint64_t* {
+      const int jj = j - start;
+      const std::vector<int>& Wp = W[jj - 1];
+      const int pw = ((int)Wp.size() + 63) / 64;
+      if (ssb[jj].empty()) {
+        ssb[jj].assign(W[jj].size() * (size_t)pw + 1, 0);
+        ssOk[jj].assign(W[jj].size(), 0);
+      }
+      uint64_t* s = &ssb[jj][(size_t)ys * pw];
+      if (!ssOk[jj][ys]) {
+        const int y = W[jj][ys];
+        for (int ws = 0; ws < (int)Wp.size(); ws++)
+          if (stronglySee(y, Wp[ws])) s[ws >> 6] |= 1ull << (ws & 63);
+        ssOk[jj][ys] = 1;
+      }
+      return s;
+    };
+    std::vector<uint64_t> prev, cur;
+    for (int i = start; i < R - 1; i++) {
+      RoundInfo& roundInfo = rounds.at(i);
+      const std::vector<int>& Wi = W[i - start];
+      const int nx = (int)Wi.size();
+      int prevWords = 0;
+      for (int j = i + 1; j < R; j++) {
+        const std::vector<int>& Wj = W[j - start];
+        const int ny = (int)Wj.size();
+        const int cw = (ny + 63) / 64;
+        const int diff = j - i;
+        cur.assign((size_t)nx * cw + 1, 0);
+        for (int xs = 0; xs < nx; xs++) {
+          const int x = Wi[xs];
+          uint64_t* cv = &cur[(size_t)xs * cw];
+          const uint64_t* pv = prev.data() + (size_t)xs * prevWords;
+          for (int ys = 0; ys < ny; ys++) {
+            const int y = Wj[ys];
+            if (diff == 1) {
+              if (ancestor(y, x)) cv[ys >> 6] |= 1ull << (ys & 63);
+              continue;
+            }
+            const uint64_t* s = ss(j, ys);
+            int yays = 0, tot = 0;
+            for (int k = 0; k < prevWords; k++) {
+              yays += __builtin_popcountll(s[k] & pv[k]);
+              tot += __builtin_popcountll(s[k]);
+            }
+            const int nays = tot - yays;
+            bool v = false;
+            int t = nays;
+            if (yays >= nays) { v = true; t = yays; }
+            if (diff % n != 0) {  // normal round
+              if (t >= SM) {
+                auto prevE = roundInfo.events.find(x);
+                if (prevE != roundInfo.events.end() && prevE->second.famous != Undefined) {
+                  stat_redecided++;
+                  if (prevE->second.famous != (v ? True : False)) stat_flipped++;
+                }
+                roundInfo.SetFame(x, v);
+                break;  // break out of y loop
+              } else if (v) {
+                cv[ys >> 6] |= 1ull << (ys & 63);
+              }
+            } else {  // coin round
+              stat_coin_evals++;
+              if (t < SM) {
+                stat_coin_votes++;
+                v = events[y].coin;
+              }
+              if (v) cv[ys >> 6] |= 1ull << (ys & 63);
+            }
+          }
+        }
+        prev.swap(cur);
+        prevWords = cw;
+      }
+      if (roundInfo.undecided == 0 && (!has_lcr || i > lcr)) setLastConsensusRound(i);
+    }
+  }
+
   int64_t MedianTimestamp(const std::vector<int>& hashes) {  // hashgraph.go:762-770
     std::vector<int64_t> t;
     for (int x : hashes) t.push_back(getEvent(x) ? events[x].ts : kZeroTime);
@@ -439,6 +675,7 @@ struct Oracle {
   }
 
   void DecideRoundReceived() {  // hashgraph.go:676-721
+    if (fast()) return DecideRoundReceivedScale();
     for (int x : undetermined) {
       int r = Round(x);
       for (int i = r + 1; i < Rounds(); i++) {
@@ -457,6 +694,63 @@ struct Oracle {
           ex.cts = MedianTimestamp(t);
           break;
         }
+      }
+    }
+  }
+
+  // Scale mode DecideRoundReceived: See(w, x) is laIx(w)[creator(x)] >= index(x),
+  // so |{w in F : See(w, x)}| > |F|/2 iff index(x) <= theta(creator(x)), the
+  // (|F|/2+1)-th largest of laIx(w)[creator(x)] over the famous witnesses F.
+  // The median is order-free, so F's iteration order does not matter.
+  void DecideRoundReceivedScale() {
+    const int R = Rounds();
+    if ((int)thetas.size() < R) thetas.resize(R);
+    std::vector<int32_t> col;
+    auto prep = [&](int i) -> Theta& {
+      RoundInfo& tr = rounds.at(i);
+      Theta& T = thetas[i];
+      if (T.version != tr.version) {
+        T.version = tr.version;
+        T.famous.clear();
+        for (int w : tr.wkeys)
+          if (tr.events.at(w).famous == True) T.famous.push_back(w);
+        T.th.assign(n, INT32_MIN);
+        const int m = (int)T.famous.size();
+        if (m > 0) {
+          const int need = m / 2 + 1;  // count > m/2
+          col.resize(m);
+          for (int c = 0; c < n; c++) {
+            for (int k = 0; k < m; k++) col[k] = laIx(T.famous[k])[c];
+            std::nth_element(col.begin(), col.begin() + (need - 1), col.end(), std::greater<int32_t>());
+            T.th[c] = col[need - 1];
+          }
+        }
+      }
+      return T;
+    };
+    std::vector<int64_t> t;
+    for (int x : undetermined) {
+      int r = Round(x);
+      Event& ex = events[x];
+      const int cx = ex.creator;
+      for (int i = r + 1; i < R; i++) {
+        if (rounds.at(i).undecided != 0) continue;
+        Theta& T = prep(i);
+        if (T.famous.empty() || (int64_t)T.th[cx] < ex.index) continue;
+        ex.has_rr = true;
+        ex.rr = i;
+        const int32_t* xfd = fdIx(x);
+        const int32_t* xfdh = fdId(x);
+        t.clear();
+        for (int a : T.famous) {
+          if ((int64_t)laIx(a)[cx] < ex.index) continue;  // !See(a, x)
+          const int ca = events[a].creator;
+          const int o = xfd[ca] <= events[a].index ? xfdh[ca] : -1;  // OldestSelfAncestorToSee(a, x)
+          t.push_back(getEvent(o) ? events[o].ts : kZeroTime);
+        }
+        std::sort(t.begin(), t.end());
+        ex.cts = t[t.size() / 2];
+        break;
       }
     }
   }
@@ -495,6 +789,20 @@ struct Oracle {
     DivideRounds();
     DecideFame();
     FindOrder();
+    if (fast() && release_lag >= 0) Release();
+  }
+
+  // Scale mode: drop the coordinates of a prefix of ordered events whose round
+  // lies release_lag rounds behind LastConsensusRound.  Nothing on the path reads
+  // them again in a gossip stream; a read aborts (co()), so a finished run is exact.
+  void Release() {
+    if (!has_lcr) return;
+    while (release_next < events.size()) {
+      Event& e = events[release_next];
+      if (!e.has_rr || roundMemo[release_next] == kUnset || roundMemo[release_next] + release_lag >= lcr) break;
+      e.co.reset();
+      release_next++;
+    }
   }
 };
 
@@ -521,6 +829,15 @@ Event makeEvent(int creator, int64_t index, int sp, int op, int64_t ts, const ui
 extern "C" {
 
 void* hgo_create(int n, uint64_t order_seed) { return new Oracle(n, order_seed); }
+// flags: bit 0 = scale mode (see the header; applies with order_seed 0 only)
+void* hgo_create2(int n, uint64_t order_seed, int flags) {
+  Oracle* o = new Oracle(n, order_seed);
+  o->scale = (flags & 1) != 0;
+  return o;
+}
+// Scale mode: release the coordinates of ordered events `lag` rounds behind LCR (-1: never).
+void hgo_set_release(void* h, int lag) { ((Oracle*)h)->release_lag = lag; }
+int hgo_is_scale(void* h) { return ((Oracle*)h)->fast(); }
 void hgo_destroy(void* h) { delete (Oracle*)h; }
 const char* hgo_last_error(void* h) { return ((Oracle*)h)->last_error.c_str(); }
 
@@ -604,11 +921,13 @@ int64_t hgo_consensus_timestamp(void* h, int x) { return ((Oracle*)h)->events[x]
 // lastAncestors / firstDescendants indices (FD MaxInt64 reported as INT64_MAX).
 void hgo_coords(void* h, int x, int64_t* la_idx, int32_t* la_hash, int64_t* fd_idx, int32_t* fd_hash) {
   Oracle* o = (Oracle*)h;
+  const int32_t* la = o->laIx(x);
+  const int32_t* fd = o->fdIx(x);
   for (int i = 0; i < o->n; i++) {
-    if (la_idx) la_idx[i] = o->events[x].la[i].index;
-    if (la_hash) la_hash[i] = o->events[x].la[i].hash;
-    if (fd_idx) fd_idx[i] = o->events[x].fd[i].index;
-    if (fd_hash) fd_hash[i] = o->events[x].fd[i].hash;
+    if (la_idx) la_idx[i] = la[i];
+    if (la_hash) la_hash[i] = o->laId(x)[i];
+    if (fd_idx) fd_idx[i] = fd[i] == kFdUnset ? kMaxInt64 : fd[i];
+    if (fd_hash) fd_hash[i] = o->fdId(x)[i];
   }
 }
 void hgo_wire_info(void* h, int x, int32_t* out4) {
@@ -624,10 +943,46 @@ void hgo_set_round(void* h, int r, const int32_t* ids, const int32_t* witness, c
   Oracle* o = (Oracle*)h;
   RoundInfo ri;
   for (int i = 0; i < m; i++) {
-    ri.events[ids[i]] = RoundEvent{witness[i] != 0, (Trilean)fame[i]};
+    RoundEvent e{witness[i] != 0, (Trilean)fame[i]};
+    ri.events[ids[i]] = e;
     ri.keys.push_back(ids[i]);
+    if (e.witness) {
+      ri.wkeys.push_back(ids[i]);
+      if (e.famous == Undefined) ri.undecided++;
+    }
   }
   o->rounds[r] = ri;
+  o->seeded = true;
+}
+
+// Bulk reads for the golden generators: Round / Witness of ids [0, E), round
+// received and consensus timestamp (0 when not received), and the fame of every
+// (round, creator) witness slot (-1 = no witness; 0/1/2 = Undefined/True/False).
+void hgo_event_rounds(void* h, int32_t* round, uint8_t* wit) {
+  Oracle* o = (Oracle*)h;
+  for (int x = 0; x < (int)o->events.size(); x++) {
+    round[x] = o->Round(x);
+    wit[x] = o->Witness(x);
+  }
+}
+void hgo_event_received(void* h, int32_t* rr, int64_t* cts) {
+  Oracle* o = (Oracle*)h;
+  for (size_t x = 0; x < o->events.size(); x++) {
+    rr[x] = o->events[x].has_rr ? o->events[x].rr : -1;
+    cts[x] = o->events[x].has_rr ? o->events[x].cts : 0;
+  }
+}
+void hgo_fame_table(void* h, int8_t* out, int R) {
+  Oracle* o = (Oracle*)h;
+  std::memset(out, -1, (size_t)R * o->n);
+  for (int r = 0; r < R; r++) {
+    auto it = o->rounds.find(r);
+    if (it == o->rounds.end()) continue;
+    for (int w : it->second.keys) {
+      const RoundEvent& e = it->second.events.at(w);
+      if (e.witness) out[(size_t)r * o->n + o->events[w].creator] = (int8_t)e.famous;
+    }
+  }
 }
 
 // Whole-schedule replay (the bench's CPU baseline and the fixture generator).

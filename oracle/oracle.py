@@ -31,6 +31,14 @@ def lib():
         P = ctypes.POINTER
         L.hgo_create.restype = vp
         L.hgo_create.argtypes = [ctypes.c_int, u64]
+        L.hgo_create2.restype = vp
+        L.hgo_create2.argtypes = [ctypes.c_int, u64, ctypes.c_int]
+        L.hgo_set_release.argtypes = [vp, ctypes.c_int]
+        L.hgo_is_scale.argtypes = [vp]
+        L.hgo_is_scale.restype = ctypes.c_int
+        L.hgo_event_rounds.argtypes = [vp, P(i32), P(ctypes.c_uint8)]
+        L.hgo_event_received.argtypes = [vp, P(i32), P(i64)]
+        L.hgo_fame_table.argtypes = [vp, P(ctypes.c_int8), ctypes.c_int]
         L.hgo_destroy.argtypes = [vp]
         L.hgo_last_error.restype = ctypes.c_char_p
         L.hgo_last_error.argtypes = [vp]
@@ -87,12 +95,19 @@ class Oracle:
 
     order_seed=0 iterates round witnesses in ascending creator id (the parity
     contract); any other seed emulates Go's randomised map iteration.
+
+    scale=True selects the scale mode of hg_oracle.cpp (same results, computed
+    without the memo caches and with bitset votes; canonical order only), and
+    release_lag >= 0 lets it drop the coordinates of events ordered that many
+    rounds behind LastConsensusRound (a later read of them aborts).
     """
 
-    def __init__(self, n, order_seed=0):
+    def __init__(self, n, order_seed=0, scale=False, release_lag=-1):
         self.L = lib()
         self.n = n
-        self.h = self.L.hgo_create(n, order_seed)
+        self.h = self.L.hgo_create2(n, order_seed, 1 if scale else 0)
+        if release_lag >= 0:
+            self.L.hgo_set_release(self.h, release_lag)
 
     def close(self):
         if self.h:
@@ -227,6 +242,32 @@ class Oracle:
         self.L.hgo_stats(self.h, _p(out, ctypes.c_int64), 4)
         return dict(zip(("coin_evals", "coin_votes", "redecided", "flipped"), out.tolist()))
 
+    def is_scale(self):
+        return bool(self.L.hgo_is_scale(self.h))
+
+    def event_rounds(self):
+        """Round and witness flag of every event (bulk Round / Witness)."""
+        E = self.L.hgo_event_count(self.h)
+        r = np.zeros(max(E, 1), np.int32)
+        w = np.zeros(max(E, 1), np.uint8)
+        self.L.hgo_event_rounds(self.h, _p(r, ctypes.c_int32), _p(w, ctypes.c_uint8))
+        return r[:E], w[:E]
+
+    def event_received(self):
+        """Round received (-1 = none) and consensus timestamp (0 = none) of every event."""
+        E = self.L.hgo_event_count(self.h)
+        rr = np.zeros(max(E, 1), np.int32)
+        cts = np.zeros(max(E, 1), np.int64)
+        self.L.hgo_event_received(self.h, _p(rr, ctypes.c_int32), _p(cts, ctypes.c_int64))
+        return rr[:E], cts[:E]
+
+    def fame_table(self):
+        """fame[r, creator] of every witness slot: -1 none, 0 undefined, 1 true, 2 false."""
+        R = self.rounds()
+        out = np.zeros((max(R, 1), self.n), np.int8)
+        self.L.hgo_fame_table(self.h, _p(out, ctypes.c_int8), R)
+        return out[:R]
+
     def set_round(self, r, entries):
         """entries: list of (id, witness: bool, fame: 0/1/2) (Store.SetRound)."""
         ids = np.array([e[0] for e in entries], np.int32)
@@ -236,14 +277,15 @@ class Oracle:
                              _p(f, ctypes.c_int32), len(ids))
 
 
-def replay(dag, call_points, order_seed=0):
+def replay(dag, call_points, order_seed=0, scale=False, release_lag=-1):
     """Run the Go-shaped path over a whole submission stream.
 
     dag: dict of numpy arrays (creator, index, sp, op, ts, S[n,32] u8, hash[n,32] u8, ntx)
     call_points: ascending 1-based submission counts after which RunConsensus runs.
+    scale / release_lag: see Oracle.
     Returns (oracle, status, order, call_counts).
     """
-    o = Oracle(int(dag["n"]), order_seed)
+    o = Oracle(int(dag["n"]), order_seed, scale=scale, release_lag=release_lag)
     n_sub = len(dag["creator"])
     cp = np.ascontiguousarray(call_points, np.int64)
     status = np.zeros(n_sub, np.int32)

@@ -38,6 +38,52 @@ def digest(state):
     return h.hexdigest()
 
 
+EVENT_CHUNK = 1 << 20   # events per chunk digest of rounds / witness / rr / cts
+ORDER_CHUNK = 1 << 20   # order positions per chunk digest
+CALL_CHUNK = 1 << 12    # calls per chunk digest of counts
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()[:32]
+
+
+def _chunks(a, step):
+    return [_sha(a[i:i + step]) for i in range(0, max(len(a), 1), step)]
+
+
+def field_digests(state):
+    """Per-field and per-chunk digests of a state (the `canonical` layout), and
+    the whole-state digest: what tests/golden/*_full.json hold."""
+    s = canonical(state)
+    out = {"fields": {k: _sha(s[k]) for k, _ in FIELDS},
+           "chunks": {"order": _chunks(s["order"], ORDER_CHUNK), "counts": _chunks(s["counts"], CALL_CHUNK)}}
+    for k in ("rounds", "witness", "rr", "cts"):
+        out["chunks"][k] = _chunks(s[k], EVENT_CHUNK)
+    out["digest"] = digest(state)
+    return out
+
+
+def compare_full(state, golden, fields=None):
+    """Fields of `state` whose digest differs from a *_full.json golden, each with
+    the first differing chunk where the field is chunked: [] when identical.
+    `fields`: only these (e.g. order and counts for a sharded run)."""
+    got = field_digests(state)
+    bad = []
+    for k, _ in FIELDS:
+        if fields is not None and k not in fields:
+            continue
+        if got["fields"][k] != golden["fields"][k]:
+            ch = golden["chunks"].get(k)
+            if ch is not None:
+                gc = got["chunks"][k]
+                first = next((i for i in range(max(len(ch), len(gc)))
+                              if i >= len(ch) or i >= len(gc) or ch[i] != gc[i]), None)
+                bad.append(f"{k}[chunk {first}]")
+            else:
+                bad.append(k)
+    return bad
+
+
 def engine_state(eng, status, order, counts):
     """The engine's side of `canonical` after a replay (status/order/counts from
     Engine.fetch)."""

@@ -3,7 +3,9 @@
 The bench replays the full seeded stream on the GPU; the engine reproduces the
 reference's per-call semantics, so the batches of the first calls depend only
 on the submissions before them.  This script runs the CPU oracle
-(oracle/hg_oracle.cpp, the Go-faithful restatement) on the first PREFIX
+(oracle/hg_oracle.cpp, the Go-faithful restatement, in its scale mode: same
+results, pinned to the faithful mode by tests/test_oracle_scale.py and by
+tests/golden/regen_check.py over every committed golden) on the first PREFIX
 submissions of the same stream with the same schedule and stores every field
 of the parity contract (make_golden.describe: status, order, per-call batch
 sizes, rounds, witness flags, fame of every round slot, round received,
@@ -11,7 +13,10 @@ consensus timestamps, undetermined list, scalars):
 
     python tests/golden/make_bench_prefix.py [n] [events] [k] [seed] [prefix]
 
-The committed 256/10M golden was made with prefix 819200 (1,850 s of oracle time, ~26 GB of host memory).
+Committed: 256/10M with prefix 2,560,000 (10,000 calls) and 64/1M with the whole
+stream (prefix 1,000,000).  Round 3's faithful-mode oracle took 1,850 s and
+~26 GB for an 819,200 prefix; the scale mode takes ~35 s for that.  The whole
+streams are pinned by digests as well (make_bench_full.py).
 """
 import os
 import sys
@@ -37,7 +42,7 @@ def main():
     sub = {k: (v[:prefix] if isinstance(v, np.ndarray) else v) for k, v in dag.items()}
     calls = schedule(prefix, K)
     t = time.time()
-    o, status, order, counts = replay(sub, calls)
+    o, status, order, counts = replay(sub, calls, scale=True, release_lag=12)
     assert (status >= 0).all()
     d = describe(o, sub, status, order, counts, calls)
     d.pop("status")  # every submission of a gossip stream is accepted: status = iota

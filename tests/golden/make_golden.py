@@ -54,26 +54,14 @@ CASES = [
 
 
 def describe(o, dag, status, order, counts, calls):
-    acc = status >= 0
-    ids = status[acc]
-    E = len(ids)
-    rounds = np.array([o.round(int(x)) for x in range(E)], np.int32)
-    wit = np.array([o.witness(int(x)) for x in range(E)], np.int8)
-    creators = dag["creator"][acc]
-    R = o.rounds()
-    fame = np.full((R, dag["n"]), -1, np.int8)
-    for r in range(R):
-        for w in o.round_witnesses(r):
-            fame[r, creators[w]] = o.round_fame(r, w)
-    rr = np.array([o.round_received(int(x)) if o.round_received(int(x)) is not None else -1
-                   for x in range(E)], np.int32)
-    cts = np.array([o.consensus_timestamp(int(x)) if rr[x] >= 0 else 0 for x in range(E)], np.int64)
+    rounds, wit = o.event_rounds()
+    rr, cts = o.event_received()
     st = o.stats()
-    return dict(status=status, order=order, counts=counts, calls=calls, rounds=rounds, witness=wit,
-                fame=fame, rr=rr, cts=cts, undetermined=o.undetermined(),
+    return dict(status=status, order=order, counts=counts, calls=calls, rounds=rounds, witness=wit.astype(np.int8),
+                fame=o.fame_table(), rr=rr, cts=cts, undetermined=o.undetermined(),
                 fame_stats=np.array([st["coin_evals"], st["coin_votes"], st["redecided"], st["flipped"]],
                                     np.int64),
-                scalars=np.array([R, -1 if o.last_consensus_round() is None else o.last_consensus_round(),
+                scalars=np.array([o.rounds(), -1 if o.last_consensus_round() is None else o.last_consensus_round(),
                                   o.last_committed_round_events(), o.consensus_transactions()],
                                  np.int64))
 

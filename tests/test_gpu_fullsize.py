@@ -1,7 +1,13 @@
 """Full-size configurations on the GPU (BASELINE.json configs[2] and configs[3]
 on one MI355X): 64 participants / 1M events and 256 / 10M, K = N.
 
-The oracle cannot replay these sizes in test time, so parity is checked by
+Parity is checked by
+  * the oracle's digests of the WHOLE stream (tests/golden/*_full.json, made by
+    tests/golden/make_bench_full.py with the oracle's scale mode): every field
+    of the parity contract -- status, order, per-call batches, every event's
+    round, witness flag, round received and consensus timestamp, the fame of
+    every (round, creator) slot, the undetermined list and the scalars -- must
+    hash identically; a mismatch names the first differing chunk;
   * the committed oracle golden of the first calls of the SAME stream
     (tests/golden/bench_*_prefix.npz, every field of the parity contract): the
     engine reproduces per-call semantics, so the first calls' batches and
@@ -18,7 +24,9 @@ The oracle cannot replay these sizes in test time, so parity is checked by
     witnesses are exactly the first events of their round on their chain
     (hashgraph.go:253-266).
 """
+import json
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -28,6 +36,7 @@ from parity import check_prefix, check_run
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
 
 
 @pytest.mark.parametrize("n,E", [(64, 1_000_000), (256, 10_000_000)])
@@ -47,6 +56,10 @@ def test_full_size(n, E):
         bad = check_prefix(gp, order, counts, rounds, wit, rr, cts, eng.fame_table())
         assert not bad, f"fields differing from the oracle prefix golden: {bad}"
         check_run(dag, st, order, counts, rounds, wit, rr, cts)
+        gf = json.load(open(os.path.join(ROOT, "tests", "golden", f"bench_n{n}_e{E}_k{K}_s{seed}_full.json")))
+        from digest import compare_full, engine_state
+        bad = compare_full(engine_state(eng, st, order, counts), gf)
+        assert not bad, f"fields differing from the oracle's whole-stream digests: {bad}"
     finally:
         eng.close()
 
