@@ -1,0 +1,1152 @@
+// hge_batch.hip — many independent small hashgraphs replayed together
+// (BASELINE config 5: a Monte Carlo batch of 32-participant graphs with
+// Byzantine forkers).  C ABI: hge_batch_* in include/hge.h.
+//
+// The single-graph engine (hge_engine.hip) sizes its grids from one graph and
+// makes a few host round trips per replay; driving 1,024 of them means ~50k
+// launches per batch from host threads (58M ev/s, the
+// host bound).  Here every stage is ONE launch over the whole batch, one
+// 64-lane wavefront per graph (N <= 64: lane = participant column / witness
+// slot), and the graph's whole call schedule runs inside the consensus kernel:
+//
+//   kb_coords     lastAncestors rows in insertion order (hashgraph.go:399-463);
+//                 the chain heads' rows live in LDS, a row is a max of the
+//                 self-parent head and the other-parent row.
+//   kb_fd         firstDescendants in run layout FDT[j][c][p]: chain-j event k is
+//                 the first chain-j descendant of chain-c positions
+//                 (LA[(j,k-1)][c], LA[(j,k)][c]] (hashgraph.go:466-494).
+//   kb_rounds     Round / Witness of every event in insertion order
+//                 (hashgraph.go:220-305): ParentRound from the parents' rounds,
+//                 RoundInc = strongly seeing >= SM witnesses of the parent round
+//                 present so far (the last rounds' witness FD rows in an LDS ring);
+//                 each new witness gets its strongly-see / see bitsets over the
+//                 previous round's witnesses (the vote adjacency of DecideFame).
+//   kb_consensus  for every call point in order: DivideRounds' bookkeeping,
+//                 DecideFame (hashgraph.go:598-664: lane = witness x of round i,
+//                 its votes over round j's witnesses a 64-bit mask, the `break`,
+//                 missing votes as nays, coin rounds), DecideRoundReceived
+//                 (hashgraph.go:676-721: x is seen by more than half of the famous
+//                 witnesses iff index(x) <= theta(round, creator(x)), the
+//                 (|F|/2+1)-th largest lastAncestor of the famous witnesses),
+//                 MedianTimestamp (:762-770) and the ConsensusSorter sort of the
+//                 call's batch (consensus_sorter.go:36-59, PRN = 0) in LDS.
+//
+// Everything on the path is integer; results are bit-exact with the oracle
+// (tests/test_gpu_batch.py, tests/test_gpu_mc.py: every graph's full-state digest).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/hge.h"
+
+namespace hgb {
+
+constexpr int32_t INF = 0x7fffffff;
+constexpr int64_t TS_MAX = INT64_MAX;
+constexpr int64_t ZERO_TIME = INT64_MIN;  // Go's zero time.Time (hashgraph.go:765: a missing event)
+constexpr int LB = 512;                   // call batch sorted in LDS (larger: global scratch)
+
+struct GDesc {
+  int64_t eo;    // first event of the graph in the per-event pools
+  int32_t E;     // accepted events
+  int32_t co;    // first call in the per-call pools
+  int32_t K;     // calls
+  int32_t ro;    // first round row in the per-round pools
+  int32_t Rcap;  // rounds the graph may reach (E / SM + 2)
+  int32_t pad;
+};
+
+// batch tables (device pointers); per-graph blocks are addressed through GDesc
+struct BT {
+  int N, SM, ccap;
+  const GDesc* gd;
+  const int32_t *cr, *ix, *sp, *op, *ntx, *clen;
+  const int64_t* ts;
+  const uint64_t* S;  // 4 limbs per event, most significant first
+  const uint8_t* coin;
+  const int32_t* chain;  // [g][N][ccap] local event ids
+  const int64_t* tsch;   // [g][N][ccap] timestamps in chain layout
+  const int64_t* calls;  // accepted-event count at each call point
+  int32_t* LA;           // [eo + x][N] lastAncestors (positions; -1 none)
+  int32_t* FDT;          // [g][j][c][ccap] firstDescendants in run layout (INF none)
+  int32_t* round;
+  uint8_t* wit;
+  int32_t* rr;
+  int64_t* cts;
+  int32_t *W, *WIX, *WFD;      // [ro + r][N] witness id / its index, [ro + r][N][N] its FD row
+  uint64_t *ssb, *seeb;        // [ro + r][N] bitsets over round r-1's witness creators
+  int8_t* fame;                // [ro + r][N] 0 undefined, 1 true, 2 false (persisted)
+  int32_t *rcnt, *ver, *thv;   // [ro + r] events in the round so far, fame/witness version, theta's version
+  int32_t* th;                 // [ro + r][N] receive thresholds
+  int32_t* U;                  // [eo + k] undetermined list
+  int32_t* order;              // [eo + k] consensus order
+  int64_t* counts;             // [co + c] batch size of call c
+  int64_t* scal;               // [g][8] R, LCR, LCRE, transactions, ordered, undetermined, error
+  int32_t* krr;                // [eo + k] sort scratch for batches past LB keys
+  int64_t* kct;
+  uint64_t* ks0;
+  int32_t* kid;
+};
+
+__device__ __forceinline__ int rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return (uint64_t)hi << 32 | lo;
+}
+__device__ __forceinline__ int64_t rl64s(int64_t v, int l) { return (int64_t)rl64((uint64_t)v, l); }
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ int wave_max(int v) {
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ int wave_min(int v) {
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ int64_t wave_sum64(int64_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+// mutable per-graph state in global memory is written and read by different
+// lanes of the graph's wave: device-coherent loads bypass a stale L1 line
+template <typename T>
+__device__ __forceinline__ T ld(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T, typename V>
+__device__ __forceinline__ void st(T* p, V v) {
+  __hip_atomic_store(p, (T)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void wsync() { __builtin_amdgcn_wave_barrier(); }
+
+// ---------------------------------------------------------------------------
+// lastAncestors (InitEventCoordinates, hashgraph.go:399-463): in insertion order,
+// LA[x] = max(LA[sp], LA[op]) with LA[x][creator] = index.  The self-parent is the
+// creator's head (admission: "Self-parent not last known", hashgraph.go:390-393),
+// so its row is in LDS; so is the other-parent's when it is its chain's head.
+template <int NM>
+__global__ __launch_bounds__(64) void kb_coords(BT t) {
+  const GDesc d = t.gd[blockIdx.x];
+  const int N = t.N, k = threadIdx.x;
+  __shared__ int32_t head[NM][NM];
+  __shared__ int32_t headid[NM];
+  if (k < N) {
+    for (int c = 0; c < N; c++) head[c][k] = -1;
+    headid[k] = -1;
+  }
+  __syncthreads();
+  int32_t* LA = t.LA + d.eo * N;
+  for (int base = 0; base < d.E; base += 64) {
+    const int i = base + k;
+    int mcr = 0, mix = 0, msp = -1, mop = -1, moc = 0;
+    if (i < d.E) {
+      mcr = t.cr[d.eo + i];
+      mix = t.ix[d.eo + i];
+      msp = t.sp[d.eo + i];
+      mop = t.op[d.eo + i];
+      moc = mop >= 0 ? t.cr[d.eo + mop] : 0;
+    }
+    const int cnt = min(64, d.E - base);
+    for (int u = 0; u < cnt; u++) {
+      const int cr = rl(mcr, u), ix = rl(mix, u), sp = rl(msp, u), op = rl(mop, u), oc = rl(moc, u);
+      const bool oph = op >= 0 && headid[oc] == op;
+      if (k < N) {
+        int v = sp >= 0 ? head[cr][k] : -1;
+        if (op >= 0) v = max(v, oph ? head[oc][k] : ld(&LA[(int64_t)op * N + k]));
+        if (k == cr) v = ix;
+        head[cr][k] = v;
+        LA[(int64_t)(base + u) * N + k] = v;
+      }
+      wsync();
+      if (k == 0) headid[cr] = base + u;
+      wsync();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// firstDescendants in run layout (UpdateAncestorFirstDescendant, hashgraph.go:466-494):
+// lane c walks chain j and hands positions (LA[(j,k-1)][c], LA[(j,k)][c]] of chain c
+// the first descendant k; positions no chain-j event sees keep INF (MaxInt64).
+template <int NM>
+__global__ __launch_bounds__(64) void kb_fd(BT t) {
+  const int g = blockIdx.x;
+  const GDesc d = t.gd[g];
+  const int N = t.N, c = threadIdx.x, cc = t.ccap;
+  const int32_t* LA = t.LA + d.eo * N;
+  const int lenc = c < N ? t.clen[g * N + c] : 0;
+  for (int j = 0; j < N; j++) {
+    const int lenj = t.clen[g * N + j];
+    const int32_t* ch = t.chain + ((int64_t)g * N + j) * cc;
+    int32_t* out = t.FDT + (((int64_t)g * N + j) * N + c) * cc;
+    int prev = -1;
+    for (int base = 0; base < lenj; base += 64) {
+      const int mx = base + c < lenj ? ch[base + c] : 0;
+      const int cnt = min(64, lenj - base);
+      int nxt = c < N && cnt > 0 ? LA[(int64_t)rl(mx, 0) * N + c] : -1;
+      for (int u = 0; u < cnt; u++) {
+        const int cur = nxt;
+        if (u + 1 < cnt && c < N) nxt = LA[(int64_t)rl(mx, u + 1) * N + c];
+        if (c < N) {
+          for (int p = prev + 1; p <= cur; p++) out[p] = base + u;
+          prev = max(prev, cur);
+        }
+      }
+    }
+    if (c < N)
+      for (int p = prev + 1; p < lenc; p++) out[p] = INF;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Round / Witness in insertion order (hashgraph.go:220-305).  DivideRounds computes
+// Round(x) in insertion order, so when x is computed the store holds exactly the
+// events before it: Rounds() = 1 + their highest round, and RoundWitnesses(pr) are
+// the witnesses of round pr among them.  StronglySee(x, w) counts the columns with
+// LA[x][k] >= FD[w][k] (hashgraph.go:189-208); FD here is final, which gives the same
+// count (a descendant of w that x sees precedes x).
+template <int NM, int RING>
+__global__ __launch_bounds__(64) void kb_rounds(BT t) {
+  const int g = blockIdx.x;
+  const GDesc d = t.gd[g];
+  const int N = t.N, SM = t.SM, k = threadIdx.x, cc = t.ccap;
+  __shared__ int32_t rhead[NM], headid[NM];
+  __shared__ int32_t wid[RING][NM], wixr[RING][NM];
+  __shared__ int32_t wfd[RING][NM][NM];  // [slot][column k][witness creator]
+  if (k < N) {
+    rhead[k] = -1;
+    headid[k] = -1;
+    for (int s = 0; s < RING; s++) wid[s][k] = -1;
+  }
+  __syncthreads();
+  const int32_t* LA = t.LA + d.eo * N;
+  const int32_t* FDTg = t.FDT + (int64_t)g * N * N * cc;
+  int top = -1;   // highest round with a ring slot
+  int maxr = -1;  // highest round so far (Rounds() - 1)
+  int err = 0;
+  // count of lanes d whose witness of round r is strongly seen by the LA row `la`
+  auto ss_mask = [&](int r, int la, bool ring) -> uint64_t {
+    bool ss = false;
+    if (k < N) {
+      if (ring) {
+        const int s = r % RING;
+        if (wid[s][k] >= 0) {
+          int cnt = 0;
+          for (int q = 0; q < N; q++) cnt += rl(la, q) >= wfd[s][q][k];
+          ss = cnt >= SM;
+        }
+      } else {
+        const int w = ld(&t.W[(int64_t)(d.ro + r) * N + k]);
+        if (w >= 0) {
+          const int32_t* f = t.WFD + ((int64_t)(d.ro + r) * N + k) * N;
+          int cnt = 0;
+          for (int q = 0; q < N; q++) cnt += rl(la, q) >= ld(&f[q]);
+          ss = cnt >= SM;
+        }
+      }
+    }
+    return ballot(ss);
+  };
+  for (int base = 0; base < d.E && !err; base += 64) {
+    const int i = base + k;
+    int mcr = 0, mix = 0, msp = -1, mop = -1, moc = 0;
+    if (i < d.E) {
+      mcr = t.cr[d.eo + i];
+      mix = t.ix[d.eo + i];
+      msp = t.sp[d.eo + i];
+      mop = t.op[d.eo + i];
+      moc = mop >= 0 ? t.cr[d.eo + mop] : 0;
+    }
+    const int cnt = min(64, d.E - base);
+    int la = k < N && cnt > 0 ? LA[(int64_t)base * N + k] : -1;
+    for (int u = 0; u < cnt; u++) {
+      const int x = base + u;
+      const int cr = rl(mcr, u), ix = rl(mix, u), sp = rl(msp, u), op = rl(mop, u), oc = rl(moc, u);
+      const int lax = la;
+      if (u + 1 < cnt) la = k < N ? LA[(int64_t)(x + 1) * N + k] : -1;
+      // ParentRound (hashgraph.go:220-244): 0 without both parents
+      const int rsp = sp >= 0 ? rhead[cr] : -1;
+      int pr = 0;
+      if (sp >= 0 && op >= 0) {
+        const int rop = headid[oc] == op ? rhead[oc] : ld(&t.round[d.eo + op]);
+        pr = max(rsp, rop);
+      }
+      // RoundInc (hashgraph.go:263-285): Rounds() < pr + 1 -> false
+      bool inc = false;
+      if (maxr + 1 >= pr + 1) {
+        const bool ring = pr <= top && pr > top - RING;
+        inc = __popcll(ss_mask(pr, lax, ring)) >= SM;
+      }
+      const int r = pr + (inc ? 1 : 0);
+      const bool w = sp < 0 || r > rsp;  // Witness (hashgraph.go:247-260)
+      if (k == 0) {
+        st(&t.round[d.eo + x], r);
+        t.wit[d.eo + x] = w;
+      }
+      wsync();
+      if (k == 0) {
+        rhead[cr] = r;
+        headid[cr] = x;
+      }
+      maxr = max(maxr, r);
+      if (w) {
+        if (r >= d.Rcap) {
+          err = 1;
+          break;
+        }
+        while (top < r) {  // a new round takes the oldest ring slot
+          top++;
+          if (k < N) wid[top % RING][k] = -1;
+        }
+        const bool inring = r > top - RING;
+        const int fdk = k < N ? FDTg[((int64_t)k * N + cr) * cc + ix] : INF;
+        if (k < N) st(&t.WFD[((int64_t)(d.ro + r) * N + cr) * N + k], fdk);
+        if (k == 0) {
+          st(&t.W[(int64_t)(d.ro + r) * N + cr], x);
+          st(&t.WIX[(int64_t)(d.ro + r) * N + cr], ix);
+        }
+        if (inring && k < N) wfd[r % RING][k][cr] = fdk;
+        wsync();
+        if (inring && k == 0) {
+          wid[r % RING][cr] = x;
+          wixr[r % RING][cr] = ix;
+        }
+        wsync();
+        if (r >= 1) {
+          // the vote adjacency: x's strongly-see / see bits over the witnesses of
+          // round r-1 inserted before it (later ones are not its ancestors: bits 0)
+          const bool ring1 = r - 1 <= top && r - 1 > top - RING;
+          const uint64_t ssm = ss_mask(r - 1, lax, ring1);
+          bool see = false;
+          if (k < N) {
+            const int wr = ring1 ? wid[(r - 1) % RING][k] : ld(&t.W[(int64_t)(d.ro + r - 1) * N + k]);
+            const int wix = ring1 ? wixr[(r - 1) % RING][k] : ld(&t.WIX[(int64_t)(d.ro + r - 1) * N + k]);
+            see = wr >= 0 && lax >= wix;
+          }
+          const uint64_t sem = ballot(see);
+          if (k == 0) {
+            t.ssb[(int64_t)(d.ro + r) * N + cr] = ssm;
+            t.seeb[(int64_t)(d.ro + r) * N + cr] = sem;
+          }
+        }
+      }
+      wsync();
+    }
+  }
+  if (k == 0 && err) t.scal[(int64_t)blockIdx.x * 8 + 6] = 1;
+}
+
+// ---------------------------------------------------------------------------
+// consensus sorter keys (consensus_sorter.go:36-59 with PRN = 0): roundReceived,
+// consensus timestamp, S (4 limbs), then the id (S never ties for real signatures)
+__device__ __forceinline__ bool key_less(const BT& t, int64_t eo, int ra, int64_t ca, uint64_t sa, int ia,
+                                         int rb, int64_t cb, uint64_t sb, int ib) {
+  if (ra != rb) return ra < rb;
+  if (ca != cb) return ca < cb;
+  if (sa != sb) return sa < sb;
+  for (int l = 1; l < 4; l++) {
+    const uint64_t a = t.S[(eo + ia) * 4 + l], b = t.S[(eo + ib) * 4 + l];
+    if (a != b) return a < b;
+  }
+  return ia < ib;
+}
+
+// a key slot of the call's batch: LDS (plain accesses) or global scratch
+// (device-coherent accesses: lanes exchange keys between stages)
+template <bool G, typename T>
+__device__ __forceinline__ T kget(const T* p) {
+  if constexpr (G) return ld(p);
+  else return *p;
+}
+template <bool G, typename T>
+__device__ __forceinline__ void kput(T* p, T v) {
+  if constexpr (G) st(p, v);
+  else *p = v;
+}
+
+// bitonic sort of n keys (padded to a power of two with sentinels, id INF, that
+// order after every key) by one wavefront
+template <bool G>
+__device__ void sort_keys(const BT& t, int64_t eo, int n, int32_t* kr, int64_t* kc, uint64_t* ks, int32_t* ki) {
+  const int lane = threadIdx.x;
+  int P = 1;
+  while (P < n) P <<= 1;
+  for (int p = n + lane; p < P; p += 64) kput<G>(ki + p, INF);
+  wsync();
+  __threadfence_block();
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int q = lane; q < P / 2; q += 64) {
+        const int a = 2 * q - (q & (stride - 1));
+        const int b = a + stride;
+        const bool up = (a & size) == 0;
+        const int ia = kget<G>(ki + a), ib = kget<G>(ki + b);
+        if (ia == INF && ib == INF) continue;
+        int ra = 0, rb = 0;
+        int64_t ca = 0, cb = 0;
+        uint64_t sa = 0, sb = 0;
+        if (ia != INF) {
+          ra = kget<G>(kr + a);
+          ca = kget<G>(kc + a);
+          sa = kget<G>(ks + a);
+        }
+        if (ib != INF) {
+          rb = kget<G>(kr + b);
+          cb = kget<G>(kc + b);
+          sb = kget<G>(ks + b);
+        }
+        // b < a ?
+        const bool b_lt_a = ib == INF ? false : (ia == INF ? true : key_less(t, eo, rb, cb, sb, ib, ra, ca, sa, ia));
+        const bool a_lt_b = ia == INF ? false : (ib == INF ? true : key_less(t, eo, ra, ca, sa, ia, rb, cb, sb, ib));
+        if (up ? b_lt_a : a_lt_b) {
+          kput<G>(kr + a, rb);
+          kput<G>(kr + b, ra);
+          kput<G>(kc + a, cb);
+          kput<G>(kc + b, ca);
+          kput<G>(ks + a, sb);
+          kput<G>(ks + b, sa);
+          kput<G>(ki + a, ib);
+          kput<G>(ki + b, ia);
+        }
+      }
+      wsync();
+      __threadfence_block();
+    }
+  }
+}
+
+template <int NM>
+__global__ __launch_bounds__(64) void kb_consensus(BT t) {
+  const int g = blockIdx.x;
+  const GDesc d = t.gd[g];
+  const int N = t.N, SM = t.SM, lane = threadIdx.x, cc = t.ccap;
+  const int64_t eo = d.eo;
+  const int32_t* LA = t.LA + eo * N;
+  const int32_t* FDTg = t.FDT + (int64_t)g * N * N * cc;
+  const int64_t* tschg = t.tsch + (int64_t)g * N * cc;
+  __shared__ int32_t kr[LB], ki[LB];
+  __shared__ int64_t kc[LB];
+  __shared__ uint64_t ks[LB];
+  if (t.scal[(int64_t)g * 8 + 6]) return;  // the rounds pass failed: nothing to decide
+  int R = 0, lcr = -1, lcre = 0, nord = 0, nU = 0, n_prev = 0;
+  int64_t ctx = 0;
+  for (int c = 0; c < d.K; c++) {
+    const int n_c = (int)t.calls[d.co + c];
+    // ---- DivideRounds (hashgraph.go:573-588): the new events join the store ----
+    {
+      int rmax = -1;
+      for (int b0 = n_prev; b0 < n_c; b0 += 64) {
+        const int i = b0 + lane;
+        const bool on = i < n_c;
+        const int r = on ? t.round[eo + i] : -1;
+        const bool w = on && t.wit[eo + i];
+        if (on) st(&t.U[eo + nU + (i - n_prev)], i);
+        rmax = max(rmax, r);
+        // per-round event counts (RoundEvents) and witness versions, one writer per round
+        uint64_t rem = ballot(on);
+        while (rem) {
+          const int r0 = rl(r, __ffsll((unsigned long long)rem) - 1);
+          const uint64_t same = ballot(on && r == r0);
+          const int nw = __popcll(ballot(on && r == r0 && w));
+          if (lane == 0) {
+            st(&t.rcnt[d.ro + r0], ld(&t.rcnt[d.ro + r0]) + __popcll(same));
+            if (nw) st(&t.ver[d.ro + r0], ld(&t.ver[d.ro + r0]) + 1);
+          }
+          rem &= ~same;
+        }
+      }
+      rmax = wave_max(rmax);
+      if (n_c > n_prev) R = max(R, rmax + 1);
+      nU += n_c - n_prev;
+      n_prev = n_c;
+    }
+    wsync();
+    // ---- DecideFame (hashgraph.go:598-664) ----
+    for (int i = lcr + 1; i < R - 1; i++) {
+      const int xid = lane < N ? t.W[(int64_t)(d.ro + i) * N + lane] : -1;
+      const bool px = xid >= 0 && xid < n_c;
+      const int fv0 = px ? ld(&t.fame[(int64_t)(d.ro + i) * N + lane]) : 0;
+      int fv = fv0;
+      uint64_t prev = 0;
+      for (int j = i + 1; j < R; j++) {
+        const int diff = j - i;
+        const int64_t row = (int64_t)(d.ro + j) * N;
+        const int yid = lane < N ? t.W[row + lane] : -1;
+        const bool py = yid >= 0 && yid < n_c;
+        const uint64_t ybits = lane < N ? (diff == 1 ? t.seeb[row + lane] : t.ssb[row + lane]) : 0;
+        const int ycoin = py ? t.coin[eo + yid] : 0;
+        uint64_t mm = ballot(py);
+        uint64_t cur = 0;
+        bool on = px;
+        while (mm) {
+          const int dd = __ffsll((unsigned long long)mm) - 1;
+          mm &= mm - 1;
+          const uint64_t s = rl64(ybits, dd);
+          if (diff == 1) {
+            if (on && ((s >> lane) & 1)) cur |= 1ull << dd;  // setVote(y, x, See(y, x))
+          } else if (on) {
+            const int yays = __popcll(s & prev), tot = __popcll(s), nays = tot - yays;
+            bool v = yays >= nays;
+            const int tt = v ? yays : nays;
+            if (diff % N != 0) {  // normal round
+              if (tt >= SM) {
+                fv = v ? 1 : 2;  // SetFame(x, v); break out of the y loop
+                on = false;
+              } else if (v) {
+                cur |= 1ull << dd;
+              }
+            } else {  // coin round
+              if (tt < SM) v = rl(ycoin, dd) != 0;
+              if (v) cur |= 1ull << dd;
+            }
+          }
+        }
+        prev = cur;
+      }
+      const bool chg = px && fv != fv0;
+      if (chg) st(&t.fame[(int64_t)(d.ro + i) * N + lane], (int8_t)fv);
+      if (ballot(chg) && lane == 0) st(&t.ver[d.ro + i], ld(&t.ver[d.ro + i]) + 1);
+      const bool decided = ballot(px && fv == 0) == 0;  // WitnessesDecided (roundInfo.go:78-85)
+      if (decided && (lcr < 0 || i > lcr)) {           // setLastConsensusRound (hashgraph.go:666-673)
+        lcr = i;
+        lcre = i >= 1 ? ld(&t.rcnt[d.ro + i - 1]) : 0;
+      }
+    }
+    wsync();
+    // ---- DecideRoundReceived (hashgraph.go:676-721) ----
+    // the rounds the undetermined events can be received in: (min round, R)
+    int rmin = INF;
+    for (int b0 = 0; b0 < nU; b0 += 64) {
+      const int x = b0 + lane < nU ? ld(&t.U[eo + b0 + lane]) : -1;
+      rmin = min(rmin, x >= 0 ? t.round[eo + x] : INF);
+    }
+    rmin = wave_min(rmin);
+    if (rmin == INF) rmin = R;  // nothing undetermined
+    // per round: decided, the famous witnesses, the thresholds (kept across calls
+    // while the round's fame and witnesses are unchanged)
+    for (int i = rmin + 1; i < R; i++) {
+      const int64_t row = (int64_t)(d.ro + i) * N;
+      const int w = lane < N ? t.W[row + lane] : -1;
+      const bool pw = w >= 0 && w < n_c;
+      const int f = pw ? ld(&t.fame[row + lane]) : 0;
+      if (ballot(pw && f == 0)) continue;  // not decided: thresholds unused
+      const int v = ld(&t.ver[d.ro + i]);
+      if (ld(&t.thv[d.ro + i]) == v) continue;
+      const uint64_t fm = ballot(pw && f == 1);
+      const int m = __popcll(fm);
+      int th = -1;
+      if (lane < N && m > 0) {
+        const int need = m / 2 + 1;  // len(s) > len(fws)/2
+        int lo = -1, hi = t.clen[g * N + lane] - 1;  // count_ge(lo) = m >= need
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          int cnt = 0;
+          uint64_t q = fm;
+          while (q) {
+            const int dd = __ffsll((unsigned long long)q) - 1;
+            q &= q - 1;
+            cnt += LA[(int64_t)rl(w, dd) * N + lane] >= mid;
+          }
+          if (cnt >= need) lo = mid;
+          else hi = mid - 1;
+        }
+        th = lo;
+      }
+      if (lane < N) st(&t.th[row + lane], m > 0 ? th : -2);
+      wsync();
+      if (lane == 0) st(&t.thv[d.ro + i], v);
+    }
+    wsync();
+    __threadfence_block();
+    // the undetermined events in order: received ones become the call's batch (keys
+    // to LDS, and to global scratch past LB), the rest stay undetermined (compacted)
+    int nb = 0, nk = 0;
+    for (int b0 = 0; b0 < nU; b0 += 64) {
+      const bool on = b0 + lane < nU;
+      const int x = on ? ld(&t.U[eo + b0 + lane]) : -1;
+      int found = -1;
+      int cx = 0, px = 0;
+      if (on) {
+        const int r = t.round[eo + x];
+        cx = t.cr[eo + x];
+        px = t.ix[eo + x];
+        for (int i = r + 1; i < R; i++) {
+          const int64_t row = (int64_t)(d.ro + i) * N;
+          // decided rounds have thresholds of the current version; -2: no famous witness
+          if (ld(&t.thv[d.ro + i]) != ld(&t.ver[d.ro + i])) continue;
+          const int th = ld(&t.th[row + cx]);
+          if (th == -2) continue;
+          if (px <= th) {
+            found = i;
+            break;
+          }
+        }
+      }
+      int64_t med = 0;
+      if (found >= 0) {
+        // MedianTimestamp over OldestSelfAncestorToSee(w, x) of the famous witnesses
+        // w that see x (hashgraph.go:704-709, 762-770): the upper median
+        const int64_t row = (int64_t)(d.ro + found) * N;
+        int64_t vals[NM];
+        int m = 0;
+#pragma unroll
+        for (int dd = 0; dd < NM; dd++) {
+          vals[dd] = TS_MAX;
+          if (dd < N) {
+            const int w = t.W[row + dd];
+            if (w >= 0 && w < n_c && ld(&t.fame[row + dd]) == 1 && LA[(int64_t)w * N + cx] >= px) {
+              const int q = FDTg[((int64_t)dd * N + cx) * cc + px];
+              vals[dd] = q <= t.WIX[row + dd] ? tschg[(int64_t)dd * cc + q] : ZERO_TIME;
+              m++;
+            }
+          }
+        }
+        const int want = m / 2;
+        bool got = false;
+#pragma unroll
+        for (int a = 0; a < NM; a++) {
+          if (a < N && vals[a] != TS_MAX && !got) {
+            int rank = 0;
+#pragma unroll
+            for (int b = 0; b < NM; b++)
+              rank += (b < N) && vals[b] != TS_MAX && (vals[b] < vals[a] || (vals[b] == vals[a] && b < a));
+            if (rank == want) {
+              med = vals[a];
+              got = true;
+            }
+          }
+        }
+        t.rr[eo + x] = found;
+        t.cts[eo + x] = med;
+      }
+      const uint64_t rec = ballot(found >= 0);
+      const uint64_t keep = ballot(on && found < 0);
+      const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+      if (found >= 0) {
+        const int p = nb + __popcll(rec & below);
+        const uint64_t s0 = t.S[(eo + x) * 4];
+        if (p < LB) {
+          kr[p] = found;
+          kc[p] = med;
+          ks[p] = s0;
+          ki[p] = x;
+        }
+        st(&t.krr[2 * eo + nord + p], found);
+        st(&t.kct[2 * eo + nord + p], med);
+        st(&t.ks0[2 * eo + nord + p], s0);
+        st(&t.kid[2 * eo + nord + p], x);
+      }
+      if (on && found < 0) st(&t.U[eo + nk + __popcll(keep & below)], x);
+      nb += __popcll(rec);
+      nk += __popcll(keep);
+      wsync();
+    }
+    nU = nk;
+    wsync();
+    __threadfence_block();
+    // ---- FindOrder (hashgraph.go:723-760): sort the batch, append it ----
+    if (nb > 0) {
+      if (nb <= LB) {
+        sort_keys<false>(t, eo, nb, kr, kc, ks, ki);
+        for (int p = lane; p < nb; p += 64) t.order[eo + nord + p] = ki[p];
+      } else {
+        // past LB keys: the same network on the graph's global scratch (2E entries from
+        // 2 eo: nord + the padded size stays below 2E)
+        const int64_t so = 2 * eo + nord;
+        sort_keys<true>(t, eo, nb, t.krr + so, t.kct + so, t.ks0 + so, t.kid + so);
+        for (int p = lane; p < nb; p += 64) t.order[eo + nord + p] = ld(&t.kid[so + p]);
+      }
+      int64_t tx = 0;
+      for (int p = lane; p < nb; p += 64) tx += t.ntx[eo + (nb <= LB ? ki[p] : ld(&t.kid[2 * eo + nord + p]))];
+      ctx += wave_sum64(tx);
+    }
+    if (lane == 0) t.counts[d.co + c] = nb;
+    nord += nb;
+    wsync();
+    __threadfence_block();
+  }
+  if (lane == 0) {
+    int64_t* s = t.scal + (int64_t)g * 8;
+    s[0] = R;
+    s[1] = lcr;
+    s[2] = lcre;
+    s[3] = ctx;
+    s[4] = nord;
+    s[5] = nU;
+  }
+}
+
+}  // namespace hgb
+
+// ===========================================================================
+// host side
+// ===========================================================================
+using namespace hgb;
+
+namespace {
+
+struct BatchError {
+  int code;
+  std::string msg;
+};
+
+#define BCHK(x)                                                                                \
+  do {                                                                                         \
+    hipError_t e_ = (x);                                                                       \
+    if (e_ != hipSuccess) throw BatchError{HGE_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_)}; \
+  } while (0)
+
+template <typename T>
+struct Buf {
+  T* p = nullptr;
+  size_t n = 0;
+  void need(size_t m) {
+    if (m <= n && p) return;
+    free_();
+    BCHK(hipMalloc(&p, std::max<size_t>(m, 1) * sizeof(T)));
+    n = m;
+  }
+  void free_() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+}  // namespace
+
+struct hge_batch {
+  int N = 0, SM = 1, device = 0;
+  hipStream_t st = nullptr;
+  hipEvent_t ev[5] = {};
+  std::string err;
+  struct Graph {
+    std::vector<int32_t> cr, ix, sp, op, ntx;
+    std::vector<int64_t> ts;
+    std::vector<uint64_t> S;
+    std::vector<uint8_t> coin;
+    std::vector<int64_t> calls;  // accepted counts at the call points
+    std::vector<std::vector<int32_t>> chain;
+  };
+  std::vector<Graph> gs;
+  bool staged = false, ran = false;
+  std::vector<GDesc> hd;
+  int64_t Etot = 0;
+  int64_t Ktot = 0, Rtot = 0;
+  int ccap = 0;
+  std::vector<int64_t> h_scal;
+  float kms[4] = {};
+  // device tables
+  Buf<GDesc> d_gd;
+  Buf<int32_t> d_cr, d_ix, d_sp, d_op, d_ntx, d_clen, d_chain, d_LA, d_FDT, d_round, d_rr, d_W, d_WIX, d_WFD;
+  Buf<int32_t> d_rcnt, d_ver, d_thv, d_th, d_U, d_order, d_krr, d_kid;
+  Buf<int64_t> d_ts, d_tsch, d_calls, d_cts, d_counts, d_scal, d_kct;
+  Buf<uint64_t> d_S, d_ssb, d_seeb, d_ks0;
+  Buf<uint8_t> d_coin, d_wit;
+  Buf<int8_t> d_fame;
+
+  void free_all() {
+    d_gd.free_();
+    for (auto* b : {&d_cr, &d_ix, &d_sp, &d_op, &d_ntx, &d_clen, &d_chain, &d_LA, &d_FDT, &d_round, &d_rr, &d_W,
+                    &d_WIX, &d_WFD, &d_rcnt, &d_ver, &d_thv, &d_th, &d_U, &d_order, &d_krr, &d_kid})
+      b->free_();
+    for (auto* b : {&d_ts, &d_tsch, &d_calls, &d_cts, &d_counts, &d_scal, &d_kct}) b->free_();
+    for (auto* b : {&d_S, &d_ssb, &d_seeb, &d_ks0}) b->free_();
+    d_coin.free_();
+    d_wit.free_();
+    d_fame.free_();
+  }
+
+  // FromParentsLatest (hashgraph.go:366-396) and the index rule of the engine
+  // (hge_engine.hip admit: index-lying events are refused, HGE_ERR_INDEX)
+  int admit(Graph& G, const std::vector<int32_t>& last, const hge_event& e, int32_t sp, int32_t op) {
+    const int c = e.creator;
+    if (c < 0 || c >= N) return HGE_ERR_CREATOR;
+    const int known = (int)G.chain[c].size();
+    const int64_t E = (int64_t)G.cr.size();
+    if (sp == HGE_NONE && op == HGE_NONE && known == 0) return e.index == 0 ? HGE_OK : HGE_ERR_INDEX;
+    if (sp < 0 || sp >= E) return HGE_ERR_SELF_PARENT_UNKNOWN;
+    if (G.cr[sp] != c) return HGE_ERR_SELF_PARENT_CREATOR;
+    if (op < 0 || op >= E) return HGE_ERR_OTHER_PARENT_UNKNOWN;
+    if (sp != last[c]) return HGE_ERR_SELF_PARENT_NOT_LAST;
+    if (e.index != known) return HGE_ERR_INDEX;
+    return HGE_OK;
+  }
+
+  int add(const hge_event* ev, int64_t n_sub, const int64_t* cp, int64_t n_calls, int32_t* status) {
+    for (int64_t c = 0; c < n_calls; c++)
+      if (cp[c] < 1 || cp[c] > n_sub || (c > 0 && cp[c] <= cp[c - 1]))
+        throw BatchError{HGE_ERR_ARG, "hge_batch_add: call points must be strictly ascending within [1, n_sub]"};
+    if (n_sub >= INT32_MAX / 2) throw BatchError{HGE_ERR_ARG, "hge_batch_add: stream too long for a batch graph"};
+    gs.emplace_back();
+    Graph& G = gs.back();
+    G.chain.assign(N, {});
+    std::vector<int32_t> last(N, -1), idmap(n_sub, -1);
+    int64_t nc = 0;
+    for (int64_t i = 0; i < n_sub; i++) {
+      const int32_t s = ev[i].self_parent, o = ev[i].other_parent;
+      const int32_t sp = s < 0 ? HGE_NONE : (s < i && idmap[s] >= 0 ? idmap[s] : HGE_UNKNOWN);
+      const int32_t op = o < 0 ? HGE_NONE : (o < i && idmap[o] >= 0 ? idmap[o] : HGE_UNKNOWN);
+      const int r = admit(G, last, ev[i], sp, op);
+      if (r == HGE_OK) {
+        const int32_t id = (int32_t)G.cr.size();
+        idmap[i] = id;
+        G.cr.push_back(ev[i].creator);
+        G.ix.push_back(ev[i].index);
+        G.sp.push_back(sp);
+        G.op.push_back(op);
+        G.ntx.push_back(ev[i].n_tx);
+        G.ts.push_back(ev[i].timestamp_ns);
+        for (int k = 0; k < 4; k++) {
+          uint64_t v = 0;
+          for (int b = 0; b < 8; b++) v = (v << 8) | ev[i].s[8 * k + b];
+          G.S.push_back(v);
+        }
+        G.coin.push_back(ev[i].hash[16] != 0);
+        G.chain[ev[i].creator].push_back(id);
+        last[ev[i].creator] = id;
+      }
+      if (status) status[i] = r == HGE_OK ? idmap[i] : r;
+      while (nc < n_calls && cp[nc] == i + 1) {
+        G.calls.push_back((int64_t)G.cr.size());
+        nc++;
+      }
+    }
+    staged = false;
+    ran = false;
+    return (int)gs.size() - 1;
+  }
+
+  template <typename T>
+  void up(Buf<T>& b, const std::vector<T>& h) {
+    b.need(h.size());
+    if (!h.empty()) BCHK(hipMemcpyAsync(b.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, st));
+  }
+
+  void stage() {
+    if (staged) return;
+    BCHK(hipSetDevice(device));
+    const int G = (int)gs.size();
+    hd.assign(G, GDesc{});
+    Etot = Ktot = Rtot = 0;
+    ccap = 1;
+    for (int g = 0; g < G; g++) {
+      const Graph& gr = gs[g];
+      GDesc& d = hd[g];
+      d.eo = Etot;
+      d.E = (int32_t)gr.cr.size();
+      d.co = (int32_t)Ktot;
+      d.K = (int32_t)gr.calls.size();
+      d.ro = (int32_t)Rtot;
+      // a round r + 1 exists only once >= SM witnesses of round r do: R <= E / SM + 1
+      d.Rcap = d.E / SM + 2;
+      Etot += d.E;
+      Ktot += d.K;
+      Rtot += d.Rcap;
+      for (int c = 0; c < N; c++) ccap = std::max(ccap, (int)gr.chain[c].size());
+    }
+    if (Rtot >= INT32_MAX || Ktot >= INT32_MAX) throw BatchError{HGE_ERR_CAPACITY, "batch too large"};
+    std::vector<int32_t> cr, ix, sp, op, ntx, clen((size_t)G * N), chain((size_t)G * N * ccap, -1);
+    std::vector<int64_t> ts, tsch((size_t)G * N * ccap, 0), calls;
+    std::vector<uint64_t> S;
+    std::vector<uint8_t> coin;
+    cr.reserve(Etot);
+    for (int g = 0; g < G; g++) {
+      const Graph& gr = gs[g];
+      cr.insert(cr.end(), gr.cr.begin(), gr.cr.end());
+      ix.insert(ix.end(), gr.ix.begin(), gr.ix.end());
+      sp.insert(sp.end(), gr.sp.begin(), gr.sp.end());
+      op.insert(op.end(), gr.op.begin(), gr.op.end());
+      ntx.insert(ntx.end(), gr.ntx.begin(), gr.ntx.end());
+      ts.insert(ts.end(), gr.ts.begin(), gr.ts.end());
+      S.insert(S.end(), gr.S.begin(), gr.S.end());
+      coin.insert(coin.end(), gr.coin.begin(), gr.coin.end());
+      calls.insert(calls.end(), gr.calls.begin(), gr.calls.end());
+      for (int c = 0; c < N; c++) {
+        clen[(size_t)g * N + c] = (int32_t)gr.chain[c].size();
+        for (size_t p = 0; p < gr.chain[c].size(); p++) {
+          chain[((size_t)g * N + c) * ccap + p] = gr.chain[c][p];
+          tsch[((size_t)g * N + c) * ccap + p] = gr.ts[gr.chain[c][p]];
+        }
+      }
+    }
+    up(d_cr, cr);
+    up(d_ix, ix);
+    up(d_sp, sp);
+    up(d_op, op);
+    up(d_ntx, ntx);
+    up(d_ts, ts);
+    up(d_S, S);
+    up(d_coin, coin);
+    up(d_calls, calls);
+    up(d_clen, clen);
+    up(d_chain, chain);
+    up(d_tsch, tsch);
+    d_gd.need(G);
+    BCHK(hipMemcpyAsync(d_gd.p, hd.data(), sizeof(GDesc) * G, hipMemcpyHostToDevice, st));
+    const size_t E1 = (size_t)std::max<int64_t>(Etot, 1);
+    d_LA.need(E1 * N);
+    d_FDT.need((size_t)G * N * N * ccap);
+    d_round.need(E1);
+    d_wit.need(E1);
+    d_rr.need(E1);
+    d_cts.need(E1);
+    d_U.need(E1);
+    d_order.need(E1);
+    d_krr.need(2 * E1 + 64);
+    d_kct.need(2 * E1 + 64);
+    d_ks0.need(2 * E1 + 64);
+    d_kid.need(2 * E1 + 64);
+    const size_t RN = (size_t)std::max<int64_t>(Rtot, 1) * N;
+    d_W.need(RN);
+    d_WIX.need(RN);
+    d_WFD.need(RN * N);
+    d_ssb.need(RN);
+    d_seeb.need(RN);
+    d_fame.need(RN);
+    d_th.need(RN);
+    d_rcnt.need(RN / N);
+    d_ver.need(RN / N);
+    d_thv.need(RN / N);
+    d_counts.need(std::max<int64_t>(Ktot, 1));
+    d_scal.need((size_t)G * 8);
+    BCHK(hipStreamSynchronize(st));
+    staged = true;
+  }
+
+  BT tables() const {
+    BT t;
+    t.N = N;
+    t.SM = SM;
+    t.ccap = ccap;
+    t.gd = d_gd.p;
+    t.cr = d_cr.p;
+    t.ix = d_ix.p;
+    t.sp = d_sp.p;
+    t.op = d_op.p;
+    t.ntx = d_ntx.p;
+    t.clen = d_clen.p;
+    t.ts = d_ts.p;
+    t.S = d_S.p;
+    t.coin = d_coin.p;
+    t.chain = d_chain.p;
+    t.tsch = d_tsch.p;
+    t.calls = d_calls.p;
+    t.LA = d_LA.p;
+    t.FDT = d_FDT.p;
+    t.round = d_round.p;
+    t.wit = d_wit.p;
+    t.rr = d_rr.p;
+    t.cts = d_cts.p;
+    t.W = d_W.p;
+    t.WIX = d_WIX.p;
+    t.WFD = d_WFD.p;
+    t.ssb = d_ssb.p;
+    t.seeb = d_seeb.p;
+    t.fame = d_fame.p;
+    t.rcnt = d_rcnt.p;
+    t.ver = d_ver.p;
+    t.thv = d_thv.p;
+    t.th = d_th.p;
+    t.U = d_U.p;
+    t.order = d_order.p;
+    t.counts = d_counts.p;
+    t.scal = d_scal.p;
+    t.krr = d_krr.p;
+    t.kct = d_kct.p;
+    t.ks0 = d_ks0.p;
+    t.kid = d_kid.p;
+    return t;
+  }
+
+  template <typename K>
+  void launch(K kern, int G, const BT& t) {
+    hipLaunchKernelGGL(kern, dim3(G), dim3(64), 0, st, t);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) throw BatchError{HGE_ERR_DEVICE, std::string("batch launch: ") + hipGetErrorString(e)};
+  }
+
+  int64_t run() {
+    stage();
+    const int G = (int)gs.size();
+    if (G == 0) return 0;
+    const size_t RN = (size_t)std::max<int64_t>(Rtot, 1) * N;
+    const size_t E1 = (size_t)std::max<int64_t>(Etot, 1);
+    BCHK(hipMemsetAsync(d_W.p, 0xFF, RN * 4, st));
+    BCHK(hipMemsetAsync(d_WIX.p, 0xFF, RN * 4, st));
+    BCHK(hipMemsetAsync(d_ssb.p, 0, RN * 8, st));
+    BCHK(hipMemsetAsync(d_seeb.p, 0, RN * 8, st));
+    BCHK(hipMemsetAsync(d_fame.p, 0, RN, st));
+    BCHK(hipMemsetAsync(d_rcnt.p, 0, RN / N * 4, st));
+    BCHK(hipMemsetAsync(d_ver.p, 0, RN / N * 4, st));
+    BCHK(hipMemsetAsync(d_thv.p, 0xFF, RN / N * 4, st));
+    BCHK(hipMemsetAsync(d_rr.p, 0xFF, E1 * 4, st));
+    BCHK(hipMemsetAsync(d_cts.p, 0, E1 * 8, st));
+    BCHK(hipMemsetAsync(d_scal.p, 0, (size_t)G * 64, st));
+    const BT t = tables();
+    BCHK(hipEventRecord(ev[0], st));
+    if (N <= 32) {
+      launch(kb_coords<32>, G, t);
+      BCHK(hipEventRecord(ev[1], st));
+      launch(kb_fd<32>, G, t);
+      BCHK(hipEventRecord(ev[2], st));
+      launch(kb_rounds<32, 4>, G, t);
+      BCHK(hipEventRecord(ev[3], st));
+      launch(kb_consensus<32>, G, t);
+    } else {
+      launch(kb_coords<64>, G, t);
+      BCHK(hipEventRecord(ev[1], st));
+      launch(kb_fd<64>, G, t);
+      BCHK(hipEventRecord(ev[2], st));
+      launch(kb_rounds<64, 2>, G, t);
+      BCHK(hipEventRecord(ev[3], st));
+      launch(kb_consensus<64>, G, t);
+    }
+    BCHK(hipEventRecord(ev[4], st));
+    h_scal.resize((size_t)G * 8);
+    BCHK(hipMemcpyAsync(h_scal.data(), d_scal.p, (size_t)G * 64, hipMemcpyDeviceToHost, st));
+    BCHK(hipStreamSynchronize(st));
+    for (int k = 0; k < 4; k++) BCHK(hipEventElapsedTime(&kms[k], ev[k], ev[k + 1]));
+    int64_t tot = 0;
+    for (int g = 0; g < G; g++) {
+      if (h_scal[(size_t)g * 8 + 6])
+        throw BatchError{HGE_ERR_INTERNAL, "batch graph " + std::to_string(g) + ": round capacity exceeded"};
+      tot += h_scal[(size_t)g * 8 + 4];
+    }
+    ran = true;
+    return tot;
+  }
+
+  template <typename T>
+  void down(T* host, const T* dev, size_t n) {
+    if (host && n) BCHK(hipMemcpy(host, dev, n * sizeof(T), hipMemcpyDeviceToHost));
+  }
+};
+
+#define BGUARD_BEGIN try {
+#define BGUARD_END(b)                 \
+  }                                   \
+  catch (BatchError & e) {            \
+    (b)->err = e.msg;                 \
+    return e.code;                    \
+  }                                   \
+  catch (std::exception & e) {        \
+    (b)->err = e.what();              \
+    return HGE_ERR_INTERNAL;          \
+  }
+
+extern "C" {
+
+int hge_batch_create(int32_t n_participants, int32_t device, hge_batch** out) {
+  if (!out || n_participants < 1 || n_participants > 64) return HGE_ERR_ARG;
+  hge_batch* b = new hge_batch();
+  b->N = n_participants;
+  b->SM = 2 * n_participants / 3 + 1;  // hashgraph.go:78-80
+  b->device = device;
+  try {
+    BCHK(hipSetDevice(device));
+    BCHK(hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking));
+    for (auto& e : b->ev) BCHK(hipEventCreate(&e));
+  } catch (BatchError& e) {
+    delete b;
+    return e.code;
+  }
+  *out = b;
+  return HGE_OK;
+}
+
+void hge_batch_destroy(hge_batch* b) {
+  if (!b) return;
+  if (b->st) (void)hipStreamSynchronize(b->st);
+  b->free_all();
+  for (auto& e : b->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (b->st) (void)hipStreamDestroy(b->st);
+  delete b;
+}
+
+const char* hge_batch_last_error(hge_batch* b) { return b ? b->err.c_str() : "null handle"; }
+
+int hge_batch_add(hge_batch* b, const hge_event* ev, int64_t n_sub, const int64_t* call_points, int64_t n_calls,
+                  int32_t* status_out, int32_t* graph_out) {
+  if (!b) return HGE_ERR_ARG;
+  BGUARD_BEGIN
+  if (n_sub < 0 || (n_sub > 0 && !ev) || n_calls < 0 || (n_calls > 0 && !call_points))
+    throw BatchError{HGE_ERR_ARG, "hge_batch_add: bad argument"};
+  const int g = b->add(ev, n_sub, call_points, n_calls, status_out);
+  if (graph_out) *graph_out = g;
+  return HGE_OK;
+  BGUARD_END(b)
+}
+
+int hge_batch_stage(hge_batch* b) {
+  if (!b) return HGE_ERR_ARG;
+  BGUARD_BEGIN
+  b->stage();
+  return HGE_OK;
+  BGUARD_END(b)
+}
+
+int hge_batch_run(hge_batch* b, int64_t* n_ordered) {
+  if (!b) return HGE_ERR_ARG;
+  BGUARD_BEGIN
+  const int64_t m = b->run();
+  if (n_ordered) *n_ordered = m;
+  return HGE_OK;
+  BGUARD_END(b)
+}
+
+int32_t hge_batch_graphs(hge_batch* b) { return b ? (int32_t)b->gs.size() : -1; }
+
+int hge_batch_info(hge_batch* b, int32_t g, int64_t* info) {
+  if (!b || !info || g < 0 || g >= (int)b->gs.size()) return HGE_ERR_ARG;
+  if (!b->ran) {
+    b->err = "hge_batch_info: no replay yet (hge_batch_run)";
+    return HGE_ERR_ARG;
+  }
+  const int64_t* s = &b->h_scal[(size_t)g * 8];
+  info[0] = (int64_t)b->gs[g].cr.size();
+  info[1] = (int64_t)b->gs[g].calls.size();
+  for (int k = 0; k < 6; k++) info[2 + k] = s[k];
+  return HGE_OK;
+}
+
+int hge_batch_results(hge_batch* b, int32_t g, int32_t* order, int64_t* counts, int32_t* round, uint8_t* witness,
+                      int32_t* rr, int64_t* cts, int8_t* fame, int32_t* undetermined) {
+  if (!b || g < 0 || g >= (int)b->gs.size()) return HGE_ERR_ARG;
+  BGUARD_BEGIN
+  if (!b->ran) throw BatchError{HGE_ERR_ARG, "hge_batch_results: no replay yet (hge_batch_run)"};
+  const GDesc& d = b->hd[g];
+  const int64_t* s = &b->h_scal[(size_t)g * 8];
+  const int N = b->N;
+  b->down(order, b->d_order.p + d.eo, (size_t)s[4]);
+  b->down(counts, b->d_counts.p + d.co, (size_t)d.K);
+  b->down(round, b->d_round.p + d.eo, (size_t)d.E);
+  b->down(witness, b->d_wit.p + d.eo, (size_t)d.E);
+  b->down(rr, b->d_rr.p + d.eo, (size_t)d.E);
+  b->down(cts, b->d_cts.p + d.eo, (size_t)d.E);
+  b->down(undetermined, b->d_U.p + d.eo, (size_t)s[5]);
+  if (fame && s[0] > 0) {
+    const size_t RN = (size_t)s[0] * N;
+    std::vector<int32_t> w(RN);
+    std::vector<int8_t> f(RN);
+    b->down(w.data(), b->d_W.p + (size_t)d.ro * N, RN);
+    b->down(f.data(), b->d_fame.p + (size_t)d.ro * N, RN);
+    for (size_t k = 0; k < RN; k++) fame[k] = w[k] >= 0 ? f[k] : (int8_t)-1;
+  }
+  return HGE_OK;
+  BGUARD_END(b)
+}
+
+int hge_batch_kernel_ms(hge_batch* b, float* ms4) {
+  if (!b || !ms4) return HGE_ERR_ARG;
+  for (int k = 0; k < 4; k++) ms4[k] = b->kms[k];
+  return HGE_OK;
+}
+
+}  // extern "C"

@@ -13,8 +13,18 @@
 //     evicting the least recently used past `size`; Get moves to the front;
 //     Rounds() is the LRU's length.  A RoundInfo is any set of (event, witness,
 //     famous) entries -- non-witnesses and events the store never saw included.
+//   * events: an LRU of `size` keys (the eventCache, inmem_store.go:28-49): SetEvent
+//     appends a key to its creator's list unless GetEvent finds it, then adds it;
+//     a key evicted from the LRU is appended again by its next SetEvent, as in the
+//     reference.
 // Events are identified by the caller's int64 keys (the Go shim's hash <-> key map);
-// event bodies stay with the caller.  A cache size <= 0 is taken as unbounded.
+// event bodies stay with the caller.  Cache size 0 is the reference's NewLRU(0) /
+// NewRollingList(0): the LRUs (events, rounds) keep nothing, the rolling lists never
+// roll.  A negative size is refused (the reference's make() panics on it).
+// A creator id >= n_participants is a participant the store was not created with:
+// ParticipantEventsCache.Add creates its list on first use (caches.go:99-106); Known
+// reports the n_participants registered ones only (the reference writes such an
+// entry over participant 0's in map order, caches.go:108-115).
 #include <cstdint>
 #include <list>
 #include <map>
@@ -58,9 +68,28 @@ struct RoundEntry {
 struct hge_store {
   int32_t n = 0;
   int64_t size = 0;
-  std::vector<RollingList> part;  // ParticipantEventsCache
+  std::vector<RollingList> part;  // ParticipantEventsCache (lists past n: unknown participants)
+  std::vector<uint8_t> has_part;  // a list exists for the participant
   RollingList consensus;          // consensusCache
-  std::unordered_map<int64_t, int32_t> seen;  // eventCache keys (SetEvent of a stored key adds nothing)
+  // eventCache (LRU of keys): most recent first
+  std::list<int64_t> ev_lru;
+  std::unordered_map<int64_t, std::list<int64_t>::iterator> ev_where;
+
+  bool ev_get(int64_t key) {  // LRU.Get: refreshes
+    auto it = ev_where.find(key);
+    if (it == ev_where.end()) return false;
+    ev_lru.splice(ev_lru.begin(), ev_lru, it->second);
+    return true;
+  }
+  void ev_add(int64_t key) {  // LRU.Add
+    if (ev_get(key)) return;
+    ev_lru.push_front(key);
+    ev_where[key] = ev_lru.begin();
+    if ((int64_t)ev_lru.size() > size) {
+      ev_where.erase(ev_lru.back());
+      ev_lru.pop_back();
+    }
+  }
   // roundCache (LRU): most recent first
   std::list<std::pair<int32_t, std::vector<RoundEntry>>> lru;
   std::map<int32_t, std::list<std::pair<int32_t, std::vector<RoundEntry>>>::iterator> where;
@@ -80,7 +109,7 @@ struct hge_store {
     }
     lru.emplace_front(r, std::move(v));
     where[r] = lru.begin();
-    if (size > 0 && (int64_t)lru.size() > size) {  // removeOldest
+    if ((int64_t)lru.size() > size) {  // removeOldest (size 0: the entry just added)
       where.erase(lru.back().first);
       lru.pop_back();
     }
@@ -90,11 +119,12 @@ struct hge_store {
 extern "C" {
 
 int hge_store_create(int32_t n_participants, int64_t cache_size, hge_store** out) {
-  if (!out || n_participants < 0) return HGE_ERR_ARG;
+  if (!out || n_participants < 0 || cache_size < 0) return HGE_ERR_ARG;
   hge_store* s = new hge_store();
   s->n = n_participants;
   s->size = cache_size;
   s->part.resize((size_t)n_participants);
+  s->has_part.assign((size_t)n_participants, 1);
   for (auto& p : s->part) p.size = cache_size;
   s->consensus.size = cache_size;
   *out = s;
@@ -103,24 +133,40 @@ int hge_store_create(int32_t n_participants, int64_t cache_size, hge_store** out
 
 void hge_store_destroy(hge_store* s) { delete s; }
 
-// SetEvent (inmem_store.go:51-64): a key not stored yet joins its creator's list
+static bool known_participant(const hge_store* s, int32_t c) {
+  return c >= 0 && c < (int32_t)s->part.size() && s->has_part[(size_t)c];
+}
+
+// SetEvent (inmem_store.go:51-64): a key GetEvent does not find joins its creator's
+// list (created for a participant not registered, caches.go:99-106), then the
+// eventCache adds it
 int hge_store_set_event(hge_store* s, int64_t key, int32_t creator) {
-  if (!s) return HGE_ERR_ARG;
-  if (s->seen.count(key)) return HGE_OK;
-  if (creator < 0 || creator >= s->n) return HGE_ERR_NOT_FOUND;
-  s->seen[key] = creator;
-  s->part[(size_t)creator].add(key);
+  if (!s || creator < 0) return HGE_ERR_ARG;
+  if (!s->ev_get(key)) {
+    if (creator >= (int32_t)s->part.size()) {
+      s->part.resize((size_t)creator + 1);
+      s->has_part.resize((size_t)creator + 1, 0);
+    }
+    if (!s->has_part[(size_t)creator]) {
+      s->part[(size_t)creator] = RollingList();
+      s->part[(size_t)creator].size = s->size;
+      s->has_part[(size_t)creator] = 1;
+    }
+    s->part[(size_t)creator].add(key);
+  }
+  s->ev_add(key);
   return HGE_OK;
 }
 
-int32_t hge_store_has_event(hge_store* s, int64_t key) { return s && s->seen.count(key) ? 1 : 0; }
+// GetEvent's success (inmem_store.go:41-49; refreshes the LRU entry)
+int32_t hge_store_has_event(hge_store* s, int64_t key) { return s && s->ev_get(key) ? 1 : 0; }
 
 // ParticipantEventsCache.Get (caches.go:45-76)
 int hge_store_participant_events(hge_store* s, int32_t creator, int64_t skip, int64_t* keys_out, int64_t cap,
                                  int64_t* n_out) {
   if (!s || !n_out) return HGE_ERR_ARG;
   *n_out = 0;
-  if (creator < 0 || creator >= s->n) return HGE_ERR_NOT_FOUND;
+  if (!known_participant(s, creator)) return HGE_ERR_NOT_FOUND;
   const RollingList& pe = s->part[(size_t)creator];
   if (skip >= pe.tot) return HGE_OK;
   if (skip < pe.oldest()) return HGE_ERR_TOO_LATE;
@@ -134,14 +180,14 @@ int hge_store_participant_events(hge_store* s, int32_t creator, int64_t skip, in
 // ParticipantEventsCache.GetItem (caches.go:78-84)
 int hge_store_participant_event(hge_store* s, int32_t creator, int64_t index, int64_t* key_out) {
   if (!s || !key_out) return HGE_ERR_ARG;
-  if (creator < 0 || creator >= s->n) return HGE_ERR_NOT_FOUND;
+  if (!known_participant(s, creator)) return HGE_ERR_NOT_FOUND;
   return s->part[(size_t)creator].get_item(index, key_out);
 }
 
 // ParticipantEventsCache.GetLast (caches.go:86-97): *found = 0 for "" (no event yet)
 int hge_store_last_from(hge_store* s, int32_t creator, int64_t* key_out, int32_t* found) {
   if (!s || !key_out || !found) return HGE_ERR_ARG;
-  if (creator < 0 || creator >= s->n) return HGE_ERR_NOT_FOUND;
+  if (!known_participant(s, creator)) return HGE_ERR_NOT_FOUND;
   const RollingList& pe = s->part[(size_t)creator];
   *found = pe.items.empty() ? 0 : 1;
   if (*found) *key_out = pe.items.back();

@@ -86,6 +86,9 @@ EXPORTS = [
     "hge_store_known", "hge_store_add_consensus_event", "hge_store_consensus_events",
     "hge_store_consensus_count", "hge_store_set_round", "hge_store_get_round", "hge_store_rounds",
     "hge_store_round_witnesses", "hge_store_round_events",
+    # a batch of independent hashgraphs (config 5, hge_batch.hip)
+    "hge_batch_create", "hge_batch_destroy", "hge_batch_last_error", "hge_batch_add", "hge_batch_stage",
+    "hge_batch_run", "hge_batch_graphs", "hge_batch_info", "hge_batch_results", "hge_batch_kernel_ms",
     # the wire / hashing format (host only, hge_gob.cpp)
     "hge_gob_encode_wire_events", "hge_gob_decode_wire_events", "hge_gob_encode_event_body",
 ]
@@ -214,6 +217,20 @@ def lib():
     L.hge_reset_kernel_stats.argtypes = [vp]
     L.hge_kernel_stats.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
                                    P(ctypes.c_double), P(i64)]
+    L.hge_batch_create.argtypes = [i32, i32, P(vp)]
+    L.hge_batch_destroy.argtypes = [vp]
+    L.hge_batch_destroy.restype = None
+    L.hge_batch_last_error.argtypes = [vp]
+    L.hge_batch_last_error.restype = ctypes.c_char_p
+    L.hge_batch_add.argtypes = [vp, ctypes.c_void_p, i64, P(i64), i64, P(i32), P(i32)]
+    L.hge_batch_stage.argtypes = [vp]
+    L.hge_batch_run.argtypes = [vp, P(i64)]
+    L.hge_batch_graphs.argtypes = [vp]
+    L.hge_batch_graphs.restype = i32
+    L.hge_batch_info.argtypes = [vp, i32, P(i64)]
+    L.hge_batch_results.argtypes = [vp, i32, P(i32), P(i64), P(i32), P(ctypes.c_uint8), P(i32), P(i64),
+                                    P(ctypes.c_int8), P(i32)]
+    L.hge_batch_kernel_ms.argtypes = [vp, P(ctypes.c_float)]
     _lib = L
     return L
 
@@ -836,3 +853,90 @@ class Engine:
         fd = np.zeros(self.n, np.int32)
         self._check(self.L.hge_coordinates(self.h, x, _p32(la), _p32(fd)))
         return la, fd
+
+
+class Batch:
+    """Many independent hashgraphs of N <= 64 participants replayed together on one
+    GPU (hge_batch_*: one launch per stage for the whole batch).  add() admits a
+    graph's stream (hge_replay's conventions), run() replays every graph, state(g)
+    gives graph g's full state in tests/golden/digest.py's layout."""
+
+    def __init__(self, n_participants, device=0):
+        self.L = lib()
+        h = ctypes.c_void_p()
+        rc = self.L.hge_batch_create(n_participants, device, ctypes.byref(h))
+        if rc != 0:
+            raise HgeError(rc, "hge_batch_create failed")
+        self.h = h
+        self.n = n_participants
+        self.status = []
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.hge_batch_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != 0:
+            raise HgeError(rc, self.L.hge_batch_last_error(self.h).decode())
+
+    def add(self, dag_or_events, call_points):
+        ev = dag_or_events if isinstance(dag_or_events, np.ndarray) else events_array(dag_or_events)
+        ev = np.ascontiguousarray(ev, EVENT_DTYPE)
+        cp = np.ascontiguousarray(call_points, np.int64)
+        st = np.zeros(max(len(ev), 1), np.int32)
+        g = ctypes.c_int32()
+        self._check(self.L.hge_batch_add(self.h, ev.ctypes.data, len(ev), _p64(cp), len(cp), _p32(st),
+                                         ctypes.byref(g)))
+        self.status.append(st[:len(ev)])
+        return g.value
+
+    def stage(self):
+        self._check(self.L.hge_batch_stage(self.h))
+
+    def run(self):
+        m = ctypes.c_int64()
+        self._check(self.L.hge_batch_run(self.h, ctypes.byref(m)))
+        return m.value
+
+    def graphs(self):
+        return self.L.hge_batch_graphs(self.h)
+
+    def info(self, g):
+        a = np.zeros(8, np.int64)
+        self._check(self.L.hge_batch_info(self.h, g, _p64(a)))
+        keys = ("events", "calls", "rounds", "lcr", "lcre", "transactions", "ordered", "undetermined")
+        return dict(zip(keys, a.tolist()))
+
+    def kernel_ms(self):
+        a = (ctypes.c_float * 4)()
+        self._check(self.L.hge_batch_kernel_ms(self.h, a))
+        return dict(zip(("kb_coords", "kb_fd", "kb_rounds", "kb_consensus"), [float(v) for v in a]))
+
+    def state(self, g):
+        """Graph g's state: the fields of tests/golden/digest.py (status, order, counts,
+        rounds, witness, fame, rr, cts, undetermined, scalars)."""
+        inf = self.info(g)
+        E, K, R = inf["events"], inf["calls"], inf["rounds"]
+        order = np.zeros(max(inf["ordered"], 1), np.int32)
+        counts = np.zeros(max(K, 1), np.int64)
+        rounds = np.zeros(max(E, 1), np.int32)
+        wit = np.zeros(max(E, 1), np.uint8)
+        rr = np.zeros(max(E, 1), np.int32)
+        cts = np.zeros(max(E, 1), np.int64)
+        fame = np.zeros((max(R, 1), self.n), np.int8)
+        und = np.zeros(max(inf["undetermined"], 1), np.int32)
+        self._check(self.L.hge_batch_results(self.h, g, _p32(order), _p64(counts), _p32(rounds),
+                                             wit.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), _p32(rr),
+                                             _p64(cts), fame.ctypes.data_as(ctypes.POINTER(ctypes.c_int8)),
+                                             _p32(und)))
+        return dict(status=self.status[g], order=order[:inf["ordered"]], counts=counts[:K], rounds=rounds[:E],
+                    witness=wit[:E].astype(bool), fame=fame[:R], rr=rr[:E], cts=cts[:E],
+                    undetermined=und[:inf["undetermined"]],
+                    scalars=np.array([R, inf["lcr"], inf["lcre"], inf["transactions"]], np.int64))

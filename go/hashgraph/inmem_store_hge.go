@@ -40,6 +40,7 @@ type InmemStore struct {
 	st           *C.hge_store         // the standalone containers
 	eng          *C.hge_engine        // the bound Hashgraph's engine, or nil
 	participants map[string]int
+	extra        map[string]int // participants SetEvent met that were not registered
 }
 
 // NewInmemStore (inmem_store.go:27-36): usable on its own at once; NewHashgraph
@@ -51,6 +52,7 @@ func NewInmemStore(participants map[string]int, cacheSize int) *InmemStore {
 		ids:          make(map[string]C.int32_t),
 		keys:         make(map[string]int64),
 		participants: participants,
+		extra:        make(map[string]int),
 	}
 	if rc := C.hge_store_create(C.int32_t(len(participants)), C.int64_t(cacheSize), &s.st); rc != C.HGE_OK {
 		panic(fmt.Sprintf("hge_store_create: status %d", int(rc)))
@@ -132,25 +134,36 @@ func (s *InmemStore) GetEvent(key string) (Event, error) {
 // SetEvent (inmem_store.go:51-64) keeps the full Event.  Bound, the engine already
 // holds its coordinates and its place in the creator's list (hge_insert_events);
 // on its own, the first SetEvent of a hash appends it to its creator's list.
+// A creator that is not a registered participant gets its own list, as
+// ParticipantEventsCache.Add creates one (caches.go:99-106).  The event is kept
+// only once the store accepted it.
 func (s *InmemStore) SetEvent(event Event) error {
 	key := event.Hex()
-	s.events[key] = event
 	if s.bound() {
+		s.events[key] = event
 		return nil
 	}
 	c, err := s.creatorID(event.Creator())
 	if err != nil {
+		c = C.int32_t(len(s.participants) + len(s.extra))
+		s.extra[event.Creator()] = int(c)
+	}
+	if err := storeErr(C.hge_store_set_event(s.st, s.key(key), c)); err != nil {
 		return err
 	}
-	return storeErr(C.hge_store_set_event(s.st, s.key(key), c))
+	s.events[key] = event
+	return nil
 }
 
+// a registered participant's id, or the list id SetEvent gave an unregistered one
 func (s *InmemStore) creatorID(participant string) (C.int32_t, error) {
-	id, ok := s.participants[participant]
-	if !ok {
-		return -1, ErrKeyNotFound
+	if id, ok := s.participants[participant]; ok {
+		return C.int32_t(id), nil
 	}
-	return C.int32_t(id), nil
+	if id, ok := s.extra[participant]; ok && !s.bound() {
+		return C.int32_t(id), nil
+	}
+	return -1, ErrKeyNotFound
 }
 
 // ParticipantEvents (caches.go:45-76): hashes from position skip on.
@@ -316,16 +329,34 @@ func (s *InmemStore) setRound(r int) (RoundInfo, bool) {
 	return *ri, true
 }
 
-// GetRound (inmem_store.go:107-113): the RoundInfo set with SetRound, as set; bound,
-// a round nobody set is the engine's: every event of the round, the witnesses with
-// their fame.
+// GetRound (inmem_store.go:107-113).  On its own: the RoundInfo set with SetRound,
+// as set.  Bound: the engine's live round -- every event of the round, the
+// witnesses with their current fame -- with the SetRound copy's entries added
+// only for hashes the engine does not know (non-inserted events); for an event
+// the engine knows, the engine wins, so fame decided and events divided after a
+// SetRound show up as they do in the reference, whose Hashgraph calls SetRound on
+// every update (hashgraph.go:573-588, 654-661).
 func (s *InmemStore) GetRound(r int) (RoundInfo, error) {
-	if ri, ok := s.setRound(r); ok {
-		return ri, nil
-	}
+	set, have := s.setRound(r)
 	if !s.bound() || r < 0 || r >= s.Rounds() {
+		if have {
+			return set, nil
+		}
 		return *NewRoundInfo(), ErrKeyNotFound
 	}
+	ri := s.engineRound(r)
+	if have {
+		for hash, re := range set.Events {
+			if _, known := s.ids[hash]; !known {
+				ri.Events[hash] = re
+			}
+		}
+	}
+	return *ri, nil
+}
+
+// the engine's round r: its events, the witnesses with their fame
+func (s *InmemStore) engineRound(r int) *RoundInfo {
 	ri := NewRoundInfo()
 	var n C.int64_t
 	C.hge_round_event_ids(s.eng, C.int32_t(r), nil, nil, 0, &n)
@@ -344,7 +375,7 @@ func (s *InmemStore) GetRound(r int) (RoundInfo, error) {
 			ri.Events[s.hash(id)] = re
 		}
 	}
-	return *ri, nil
+	return ri
 }
 
 // SetRound (inmem_store.go:115-118): any RoundInfo -- non-witness entries and hashes
@@ -404,14 +435,19 @@ func (s *InmemStore) RoundWitnesses(r int) []string {
 	return round.Witnesses()
 }
 
+// RoundEvents (inmem_store.go:132-138): len(GetRound(r).Events)
 func (s *InmemStore) RoundEvents(r int) int {
-	if ri, ok := s.setRound(r); ok {
-		return len(ri.Events)
+	if _, have := s.setRound(r); !have && s.bound() {
+		if r < 0 || r >= s.Rounds() {
+			return 0
+		}
+		return int(C.hge_round_events(s.eng, C.int32_t(r)))
 	}
-	if !s.bound() {
+	ri, err := s.GetRound(r)
+	if err != nil {
 		return 0
 	}
-	return int(C.hge_round_events(s.eng, C.int32_t(r)))
+	return len(ri.Events)
 }
 
 func (s *InmemStore) Close() error {

@@ -158,6 +158,38 @@ int hge_replay_prepare(hge_engine* h, const hge_event* ev, int64_t n_sub,
 int hge_replay_run(hge_engine* h, int64_t* n_ordered);
 int hge_replay_fetch(hge_engine* h, int32_t* order_out, int64_t cap, int64_t* call_counts_out);
 
+/* ---- a batch of independent hashgraphs (BASELINE config 5, Monte Carlo) -------- */
+/* Many small hashgraphs (N <= 64 participants each) replayed together: every stage
+ * is one launch over the whole batch (one wavefront per graph) and each graph's
+ * whole call schedule runs on the device, so a batch costs a handful of launches
+ * however many graphs it holds (hge_batch.hip).  Per graph the semantics are
+ * hge_replay's: parents are submission indices, admission (FromParentsLatest,
+ * hashgraph.go:366-396, and the index rule of HGE_ERR_INDEX) happens in
+ * hge_batch_add on the host, RunConsensus runs after every call point, and the
+ * results are identical to hge_replay on the same stream. */
+typedef struct hge_batch hge_batch;
+int hge_batch_create(int32_t n_participants, int32_t device, hge_batch** out);
+void hge_batch_destroy(hge_batch* b);
+const char* hge_batch_last_error(hge_batch* b);
+/* Admit one graph's stream (status_out[i]: the event's id in its graph, or a negative
+ * hge_status) and stage it on the host; *graph_out = its index in the batch. */
+int hge_batch_add(hge_batch* b, const hge_event* ev, int64_t n_sub, const int64_t* call_points, int64_t n_calls,
+                  int32_t* status_out, int32_t* graph_out);
+int hge_batch_stage(hge_batch* b); /* upload the added graphs to HBM (hge_batch_run does it if needed) */
+int hge_batch_run(hge_batch* b, int64_t* n_ordered); /* replay every graph; *n_ordered = events ordered in all */
+int32_t hge_batch_graphs(hge_batch* b);
+/* After a run: info[8] = {accepted events, calls, Rounds(), LastConsensusRound (-1 nil),
+ * LastCommitedRoundEvents, ConsensusTransactions, ordered events, undetermined events}. */
+int hge_batch_info(hge_batch* b, int32_t g, int64_t* info);
+/* Graph g's state (any pointer may be NULL; sizes from hge_batch_info): the consensus
+ * order, per-call batch sizes, every event's round / witness flag / round received
+ * (-1 none) / consensus timestamp (0 none), fame[Rounds()][N] (-1 no witness, 0
+ * undecided, 1 famous, 2 not famous) and the undetermined list. */
+int hge_batch_results(hge_batch* b, int32_t g, int32_t* order, int64_t* counts, int32_t* round, uint8_t* witness,
+                      int32_t* rr, int64_t* cts, int8_t* fame, int32_t* undetermined);
+/* device ms of the last run's stages: coordinates, firstDescendants, rounds, consensus */
+int hge_batch_kernel_ms(hge_batch* b, float* ms4);
+
 /* ---- one hashgraph split across GPUs (babble_amd/dist.py) ------ */
 /* Sharded replay.  Every rank stages the whole stream (hge_replay_prepare) and
  * makes the same plan: part p owns the events [ev_bounds[p], ev_bounds[p+1]) and
@@ -292,9 +324,13 @@ int hge_read_wire_parents(hge_engine* h, int32_t creator_id, int32_t self_parent
  * caches_test.go:22-131).  Same containers: per-participant RollingLists and a
  * consensus RollingList of cache_size (ErrTooLate / ErrKeyNotFound as the
  * reference's, caches.go:45-115, common/rolling_list.go:25-67) and an LRU of
- * cache_size RoundInfos (Rounds() = its length, common/lru.go); cache_size <= 0 =
- * unbounded.  Events are the caller's int64 keys (the shim's hash <-> key map);
- * event bodies stay with the caller, kept without eviction.  The engine-bound Store
+ * cache_size RoundInfos (Rounds() = its length, common/lru.go), and the eventCache as
+ * an LRU of cache_size keys (SetEvent appends a key GetEvent does not find to its
+ * creator's list, inmem_store.go:51-64).  cache_size 0 is the reference's NewLRU(0) /
+ * NewRollingList(0): the LRUs keep nothing and the lists never roll; a negative size
+ * is HGE_ERR_ARG.  A creator id >= n_participants gets its list on first use
+ * (caches.go:99-106) and is left out of Known.  Events are the caller's int64 keys
+ * (the shim's hash <-> key map); event bodies stay with the caller.  The engine-bound Store
  * (the hge_* views above) serves a Hashgraph; this one serves NewInmemStore until a
  * Hashgraph binds it (go/hashgraph/inmem_store_hge.go). */
 typedef struct hge_store hge_store;

@@ -1,0 +1,45 @@
+#!/bin/bash
+# Round-4 GPU runs (gpurun): `scripts/gpu_r04.sh STEP...`, each step under its own limit,
+# stopping at the first failure.
+#   full     tests/test_gpu_fullsize.py (whole-stream digests at 64/1M and 256/10M)
+#   gpu      the whole pytest -m gpu suite
+#   bench    the default bench line (256/10M) -> gpurun_out/r04/bench.json
+#   mc       bench.py --workload mc -> gpurun_out/r04/bench_mc.json
+#   prof     rocprofv3 kernel stats of the default bench -> gpurun_out/r04/prof
+#   profmc   rocprofv3 kernel stats of the mc bench -> gpurun_out/r04/profmc
+#   smoke    __graft_entry__.smoke()
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 9
+mkdir -p gpurun_out/r04
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+for s in "$@"; do
+  echo "== $s $(date +%T)"
+  case "$s" in
+    full) timeout -k 10 400 $PYT -m gpu tests/test_gpu_fullsize.py > gpurun_out/r04/full.log 2>&1 || { tail -30 gpurun_out/r04/full.log; exit 1; }
+          tail -3 gpurun_out/r04/full.log ;;
+    gpu) timeout -k 10 900 $PYT -m gpu tests > gpurun_out/r04/gpu.log 2>&1 || { tail -40 gpurun_out/r04/gpu.log; exit 1; }
+         tail -3 gpurun_out/r04/gpu.log ;;
+    batch) timeout -k 10 600 $PYT -m gpu tests/test_gpu_batch.py > gpurun_out/r04/batch.log 2>&1 || { tail -60 gpurun_out/r04/batch.log; exit 1; }
+         tail -3 gpurun_out/r04/batch.log ;;
+    mcgpu) timeout -k 10 600 $PYT -m gpu tests/test_gpu_mc.py tests/test_gpu_batch.py > gpurun_out/r04/mcgpu.log 2>&1 || { tail -40 gpurun_out/r04/mcgpu.log; exit 1; }
+         tail -3 gpurun_out/r04/mcgpu.log ;;
+    bench) timeout -k 10 600 python -u bench.py > gpurun_out/r04/bench.json 2> gpurun_out/r04/bench.err || { tail -20 gpurun_out/r04/bench.err; exit 2; }
+           python -c "
+import json
+d=json.loads(open('gpurun_out/r04/bench.json').read().strip().splitlines()[-1])
+print(round(d['value']/1e6,2), d['ms_per_step'], d['roofline']['frac']); print(d['parity'])
+print(d['kernels_ms_per_replay'])" ;;
+    mc) timeout -k 10 600 python -u bench.py --workload mc > gpurun_out/r04/bench_mc.json 2> gpurun_out/r04/bench_mc.err || { tail -20 gpurun_out/r04/bench_mc.err; exit 2; }
+        python -c "
+import json
+d=json.loads(open('gpurun_out/r04/bench_mc.json').read().strip().splitlines()[-1])
+print(round(d['value']/1e6,2), d['ms_per_step'], d['roofline']['frac']); print(d['parity']); print(d['cpu_baseline'])
+print(d['kernels_ms_per_replay'])" ;;
+    prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r04/prof -o run -- python -u bench.py --no-secondary --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/r04/prof.log 2>&1 || { tail -20 gpurun_out/r04/prof.log; exit 3; } ;;
+    profmc) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r04/profmc -o run -- python -u bench.py --workload mc --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/r04/profmc.log 2>&1 || { tail -20 gpurun_out/r04/profmc.log; exit 3; } ;;
+    smoke) timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r04/smoke.log 2>&1 || { tail -20 gpurun_out/r04/smoke.log; exit 4; }
+           tail -1 gpurun_out/r04/smoke.log ;;
+    *) echo "unknown step $s"; exit 8 ;;
+  esac
+done
+echo "== done $(date +%T)"

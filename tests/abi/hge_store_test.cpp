@@ -70,10 +70,17 @@ static void inmem_events() {
   CHECK(hge_store_last_from(s, 2, &k, &found) == HGE_OK && found == 1 && k == key(2, testSize - 1));
   CHECK(hge_store_participant_event(s, 1, 4, &k) == HGE_OK && k == key(1, 4));
   CHECK(hge_store_participant_event(s, 1, testSize, &k) == HGE_ERR_NOT_FOUND);
-  CHECK(hge_store_set_event(s, 99999, 7) == HGE_ERR_NOT_FOUND);
+  // a participant the store was not created with: ParticipantEventsCache.Add creates
+  // its list (caches.go:99-106); Known reports the registered ones only
   int rc;
+  pevents(s, 7, 0, &rc);
+  CHECK(rc == HGE_ERR_NOT_FOUND);
+  CHECK(hge_store_set_event(s, 99999, 7) == HGE_OK);
+  std::vector<int64_t> p7 = pevents(s, 7, 0, &rc);
+  CHECK(rc == HGE_OK && p7.size() == 1 && p7[0] == 99999);
   pevents(s, 9, 0, &rc);
   CHECK(rc == HGE_ERR_NOT_FOUND);
+  CHECK(hge_store_set_event(s, 5, -1) == HGE_ERR_ARG);
   hge_store_destroy(s);
 }
 
@@ -171,7 +178,39 @@ static void round_lru() {
   hge_store_destroy(s);
 }
 
+// cache size 0 (NewLRU(0), NewRollingList(0)) and the eventCache LRU
+static void lru_edges() {
+  hge_store* s = nullptr;
+  CHECK(hge_store_create(2, -1, &s) == HGE_ERR_ARG);
+  CHECK(hge_store_create(2, 0, &s) == HGE_OK);
+  int64_t k = 7;
+  uint8_t w = 1, f = 0;
+  CHECK(hge_store_set_round(s, 0, &k, &w, &f, 1) == HGE_OK);  // Add evicts it at once
+  CHECK(hge_store_rounds(s) == 0);
+  int32_t m;
+  CHECK(hge_store_get_round(s, 0, nullptr, nullptr, nullptr, 0, &m) == HGE_ERR_NOT_FOUND);
+  // the eventCache keeps nothing: every SetEvent appends the key again
+  CHECK(hge_store_set_event(s, 11, 1) == HGE_OK && hge_store_set_event(s, 11, 1) == HGE_OK);
+  CHECK(hge_store_has_event(s, 11) == 0);
+  int rc;
+  std::vector<int64_t> v = pevents(s, 1, 0, &rc);
+  CHECK(rc == HGE_OK && v.size() == 2);
+  for (int i = 0; i < 50; i++) CHECK(hge_store_add_consensus_event(s, i) == HGE_OK);  // never rolls
+  CHECK(hge_store_consensus_events(s, nullptr, 0) == 50);
+  hge_store_destroy(s);
+  // size 2: a key evicted from the eventCache is appended again by its next SetEvent
+  CHECK(hge_store_create(1, 2, &s) == HGE_OK);
+  for (int64_t key_ : {1, 2, 3}) CHECK(hge_store_set_event(s, key_, 0) == HGE_OK);  // evicts 1
+  CHECK(hge_store_has_event(s, 1) == 0 && hge_store_has_event(s, 2) == 1);
+  CHECK(hge_store_set_event(s, 2, 0) == HGE_OK);  // still cached: nothing appended
+  CHECK(hge_store_set_event(s, 1, 0) == HGE_OK);  // evicted: appended again
+  int32_t known = 0;
+  CHECK(hge_store_known(s, &known) == HGE_OK && known == 4);
+  hge_store_destroy(s);
+}
+
 int main() {
+  lru_edges();
   inmem_events();
   inmem_rounds();
   participant_events_cache(25);
