@@ -47,8 +47,6 @@ namespace hgb {
 
 constexpr int32_t INF = 0x7fffffff;
 constexpr int64_t TS_MAX = INT64_MAX;
-constexpr int64_t ZERO_TIME = INT64_MIN;  // Go's zero time.Time (hashgraph.go:765: a missing event)
-constexpr int LB = 512;                   // call batch sorted in LDS (larger: global scratch)
 
 struct GDesc {
   int64_t eo;    // first event of the graph in the per-event pools
@@ -64,7 +62,7 @@ struct GDesc {
 struct BT {
   int N, SM, ccap;
   const GDesc* gd;
-  const int32_t *cr, *ix, *sp, *op, *ntx, *clen;
+  const int32_t *cr, *ix, *sp, *op, *oc, *ntx, *clen;  // oc: the other-parent's creator
   const int64_t* ts;
   const uint64_t* S;  // 4 limbs per event, most significant first
   const uint8_t* coin;
@@ -73,20 +71,22 @@ struct BT {
   const int64_t* calls;  // accepted-event count at each call point
   int32_t* LA;           // [eo + x][N] lastAncestors (positions; -1 none)
   int32_t* FDT;          // [g][j][c][ccap] firstDescendants in run layout (INF none)
+  int32_t* FD;           // [eo + x][N] firstDescendants rows (positions; INF none)
   int32_t* round;
   uint8_t* wit;
   int32_t* rr;
   int64_t* cts;
   int32_t *W, *WIX, *WFD;      // [ro + r][N] witness id / its index, [ro + r][N][N] its FD row
+  uint8_t* WCOIN;              // [ro + r][N] the witness's coin (middleBit)
   uint64_t *ssb, *seeb;        // [ro + r][N] bitsets over round r-1's witness creators
   int8_t* fame;                // [ro + r][N] 0 undefined, 1 true, 2 false (persisted)
   int32_t *rcnt, *ver, *thv;   // [ro + r] events in the round so far, fame/witness version, theta's version
   int32_t* th;                 // [ro + r][N] receive thresholds
-  int32_t* U;                  // [eo + k] undetermined list
+  int32_t *U, *Ur, *Ucp;       // [eo + k] undetermined list past LDS: id, round, creator << 24 | index
   int32_t* order;              // [eo + k] consensus order
   int64_t* counts;             // [co + c] batch size of call c
   int64_t* scal;               // [g][8] R, LCR, LCRE, transactions, ordered, undetermined, error
-  int32_t* krr;                // [eo + k] sort scratch for batches past LB keys
+  int32_t* krr;                // [2 eo + k] sort scratch for call batches past the LDS keys
   int64_t* kct;
   uint64_t* ks0;
   int32_t* kid;
@@ -125,6 +125,11 @@ __device__ __forceinline__ void st(T* p, V v) {
 __device__ __forceinline__ void wsync() { __builtin_amdgcn_wave_barrier(); }
 
 // ---------------------------------------------------------------------------
+// Each graph is one wavefront, so nothing hides its memory latency but its own
+// prefetching: every kernel below loads the next chunk of events while it works on
+// the current one, and the consensus kernel keeps the state of the last RW rounds
+// (witnesses, their vote bitsets, fame, thresholds) and the undetermined list in LDS.
+
 // lastAncestors (InitEventCoordinates, hashgraph.go:399-463): in insertion order,
 // LA[x] = max(LA[sp], LA[op]) with LA[x][creator] = index.  The self-parent is the
 // creator's head (admission: "Self-parent not last known", hashgraph.go:390-393),
@@ -141,16 +146,21 @@ __global__ __launch_bounds__(64) void kb_coords(BT t) {
   }
   __syncthreads();
   int32_t* LA = t.LA + d.eo * N;
-  for (int base = 0; base < d.E; base += 64) {
-    const int i = base + k;
-    int mcr = 0, mix = 0, msp = -1, mop = -1, moc = 0;
+  auto meta = [&](int i, int& cr, int& ix, int& sp, int& op, int& oc) {
+    cr = 0, ix = 0, sp = -1, op = -1, oc = 0;
     if (i < d.E) {
-      mcr = t.cr[d.eo + i];
-      mix = t.ix[d.eo + i];
-      msp = t.sp[d.eo + i];
-      mop = t.op[d.eo + i];
-      moc = mop >= 0 ? t.cr[d.eo + mop] : 0;
+      cr = t.cr[d.eo + i];
+      ix = t.ix[d.eo + i];
+      sp = t.sp[d.eo + i];
+      op = t.op[d.eo + i];
+      oc = t.oc[d.eo + i];
     }
+  };
+  int mcr, mix, msp, mop, moc;
+  meta(k, mcr, mix, msp, mop, moc);
+  for (int base = 0; base < d.E; base += 64) {
+    int ncr, nix, nsp, nop, noc;
+    meta(base + 64 + k, ncr, nix, nsp, nop, noc);  // the next chunk, in flight meanwhile
     const int cnt = min(64, d.E - base);
     for (int u = 0; u < cnt; u++) {
       const int cr = rl(mcr, u), ix = rl(mix, u), sp = rl(msp, u), op = rl(mop, u), oc = rl(moc, u);
@@ -166,40 +176,94 @@ __global__ __launch_bounds__(64) void kb_coords(BT t) {
       if (k == 0) headid[cr] = base + u;
       wsync();
     }
+    mcr = ncr, mix = nix, msp = nsp, mop = nop, moc = noc;
   }
 }
 
 // ---------------------------------------------------------------------------
 // firstDescendants in run layout (UpdateAncestorFirstDescendant, hashgraph.go:466-494):
-// lane c walks chain j and hands positions (LA[(j,k-1)][c], LA[(j,k)][c]] of chain c
-// the first descendant k; positions no chain-j event sees keep INF (MaxInt64).
+// chain-j event k is the first chain-j descendant of the chain-c positions
+// (LA[(j,k-1)][c], LA[(j,k)][c]]; positions no chain-j event sees keep INF
+// (MaxInt64).  Lane c walks chain j (N <= 32: lanes 32-63 walk chain j + 1), 64
+// rows at a time with the next 64 rows' loads in flight.
 template <int NM>
 __global__ __launch_bounds__(64) void kb_fd(BT t) {
+  constexpr int HALVES = NM == 32 ? 2 : 1;
   const int g = blockIdx.x;
   const GDesc d = t.gd[g];
-  const int N = t.N, c = threadIdx.x, cc = t.ccap;
+  const int N = t.N, cc = t.ccap, lane = threadIdx.x;
+  const int c = NM == 32 ? (lane & 31) : lane, h = NM == 32 ? (lane >> 5) : 0;
   const int32_t* LA = t.LA + d.eo * N;
   const int lenc = c < N ? t.clen[g * N + c] : 0;
-  for (int j = 0; j < N; j++) {
-    const int lenj = t.clen[g * N + j];
-    const int32_t* ch = t.chain + ((int64_t)g * N + j) * cc;
-    int32_t* out = t.FDT + (((int64_t)g * N + j) * N + c) * cc;
+  for (int j0 = 0; j0 < N; j0 += HALVES) {
+    const int j = j0 + h;
+    const bool jon = j < N;           // the half has a chain (its lanes load the chain's ids)
+    const bool on = c < N && jon;     // the lane has a column too
+    const int lenj = jon ? t.clen[g * N + j] : 0;
+    const int lmax = max(rl(lenj, 0), HALVES == 2 ? rl(lenj, 32) : 0);
+    const int32_t* ch = t.chain + ((int64_t)g * N + (jon ? j : 0)) * cc;
+    int32_t* out = t.FDT + (((int64_t)g * N + (on ? j : 0)) * N + c) * cc;
     int prev = -1;
-    for (int base = 0; base < lenj; base += 64) {
-      const int mx = base + c < lenj ? ch[base + c] : 0;
-      const int cnt = min(64, lenj - base);
-      int nxt = c < N && cnt > 0 ? LA[(int64_t)rl(mx, 0) * N + c] : -1;
-      for (int u = 0; u < cnt; u++) {
-        const int cur = nxt;
-        if (u + 1 < cnt && c < N) nxt = LA[(int64_t)rl(mx, u + 1) * N + c];
-        if (c < N) {
-          for (int p = prev + 1; p <= cur; p++) out[p] = base + u;
-          prev = max(prev, cur);
+    constexpr int CH = 64 / HALVES;  // rows per chunk and half
+    // lane (h, i) holds the id of row base + i of its half's chain; the LA values of
+    // the CH rows are loaded one chunk ahead
+    const int sub = NM == 32 ? (lane & 31) : lane;
+    int idc = jon && sub < lenj ? ch[sub] : 0;
+    int cur[CH], nxt[CH];
+#pragma unroll
+    for (int u = 0; u < CH; u++) {
+      const int x = HALVES == 2 ? (h ? rl(idc, 32 + u) : rl(idc, u)) : rl(idc, u);
+      cur[u] = on && u < lenj ? LA[(int64_t)x * N + c] : -1;
+    }
+    for (int base = 0; base < lmax; base += CH) {
+      const bool more = base + CH < lmax;
+      if (more) {
+        const int idn = jon && base + CH + sub < lenj ? ch[base + CH + sub] : 0;
+#pragma unroll
+        for (int u = 0; u < CH; u++) {
+          const int x = HALVES == 2 ? (h ? rl(idn, 32 + u) : rl(idn, u)) : rl(idn, u);
+          nxt[u] = on && base + CH + u < lenj ? LA[(int64_t)x * N + c] : -1;
         }
       }
+#pragma unroll
+      for (int u = 0; u < CH; u++) {
+        if (on && base + u < lenj) {
+          const int v = cur[u];
+          for (int p = prev + 1; p <= v; p++) out[p] = base + u;
+          prev = max(prev, v);
+        }
+      }
+      if (more) {
+#pragma unroll
+        for (int u = 0; u < CH; u++) cur[u] = nxt[u];
+      }
     }
-    if (c < N)
+    if (on)
       for (int p = prev + 1; p < lenc; p++) out[p] = INF;
+  }
+}
+
+// firstDescendants as event rows: FD[eo + (c, p)][j] = FDT[j][c][p], through an LDS
+// tile of 64 positions x N chains per step.  One workgroup per (graph, chain c).
+template <int NM>
+__global__ __launch_bounds__(256) void kb_fdrows(BT t) {
+  const int g = blockIdx.x / t.N, c = blockIdx.x % t.N;
+  const GDesc d = t.gd[g];
+  const int N = t.N, cc = t.ccap, tid = threadIdx.x;
+  __shared__ int32_t tile[NM][65];
+  const int len = t.clen[g * N + c];
+  const int32_t* ch = t.chain + ((int64_t)g * N + c) * cc;
+  for (int p0 = 0; p0 < len; p0 += 64) {
+    for (int e = tid; e < N * 64; e += 256) {  // read along positions
+      const int j = e >> 6, p = e & 63;
+      tile[j][p] = p0 + p < len ? t.FDT[(((int64_t)g * N + j) * N + c) * cc + p0 + p] : INF;
+    }
+    __syncthreads();
+    for (int e = tid; e < N * 64; e += 256) {  // write event rows
+      const int p = e / N, j = e % N;
+      if (p0 + p < len) t.FD[(d.eo + ch[p0 + p]) * N + j] = tile[j][p];
+    }
+    __syncthreads();
   }
 }
 
@@ -209,71 +273,98 @@ __global__ __launch_bounds__(64) void kb_fd(BT t) {
 // events before it: Rounds() = 1 + their highest round, and RoundWitnesses(pr) are
 // the witnesses of round pr among them.  StronglySee(x, w) counts the columns with
 // LA[x][k] >= FD[w][k] (hashgraph.go:189-208); FD here is final, which gives the same
-// count (a descendant of w that x sees precedes x).
+// count (a descendant of w that x sees precedes x).  The LA and FD rows of 32 events
+// at a time are staged in LDS, the next 32 in flight in registers.
 template <int NM, int RING>
-__global__ __launch_bounds__(64) void kb_rounds(BT t) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void kb_rounds(BT t) {
+  constexpr int CH = 32;                 // events per chunk
+  constexpr int PER = CH * NM / 64;      // row elements per lane and chunk
   const int g = blockIdx.x;
   const GDesc d = t.gd[g];
-  const int N = t.N, SM = t.SM, k = threadIdx.x, cc = t.ccap;
-  __shared__ int32_t rhead[NM], headid[NM];
+  const int N = t.N, SM = t.SM, k = threadIdx.x;
   __shared__ int32_t wid[RING][NM], wixr[RING][NM];
-  __shared__ int32_t wfd[RING][NM][NM];  // [slot][column k][witness creator]
-  if (k < N) {
-    rhead[k] = -1;
-    headid[k] = -1;
-    for (int s = 0; s < RING; s++) wid[s][k] = -1;
-  }
+  __shared__ int32_t wfd[RING][NM][NM];  // [slot][witness creator][column k]: the witness's FD row
+  __shared__ uint64_t wpres[RING];        // the slot's witnesses so far (bit = creator)
+  __shared__ int32_t bla[CH][NM], bfd[CH][NM];
+  int rh = -1, hid = -1;  // lane c: the round and the id of chain c's head
+  if (k < NM)
+    for (int s = 0; s < RING; s++) {
+      wid[s][k] = -1;
+      for (int q = 0; q < NM; q++) wfd[s][q][k] = INF;
+    }
+  if (k < RING) wpres[k] = 0;
   __syncthreads();
   const int32_t* LA = t.LA + d.eo * N;
-  const int32_t* FDTg = t.FDT + (int64_t)g * N * N * cc;
+  const int32_t* FD = t.FD + d.eo * N;
   int top = -1;   // highest round with a ring slot
   int maxr = -1;  // highest round so far (Rounds() - 1)
   int err = 0;
-  // count of lanes d whose witness of round r is strongly seen by the LA row `la`
+  // the witnesses (slot d) of round r that the LA row `la` strongly sees
+  // the witnesses (bit d = creator) of round r that the LA row `la` (lane k holds
+  // column k) strongly sees: per witness, one compare of the row against the
+  // witness's FD row across the lanes and a popcount of the ballot
+  // (hashgraph.go:189-208); columns past N hold la = -1 < INF, never counted
   auto ss_mask = [&](int r, int la, bool ring) -> uint64_t {
-    bool ss = false;
-    if (k < N) {
-      if (ring) {
-        const int s = r % RING;
-        if (wid[s][k] >= 0) {
-          int cnt = 0;
-          for (int q = 0; q < N; q++) cnt += rl(la, q) >= wfd[s][q][k];
-          ss = cnt >= SM;
-        }
-      } else {
-        const int w = ld(&t.W[(int64_t)(d.ro + r) * N + k]);
-        if (w >= 0) {
-          const int32_t* f = t.WFD + ((int64_t)(d.ro + r) * N + k) * N;
-          int cnt = 0;
-          for (int q = 0; q < N; q++) cnt += rl(la, q) >= ld(&f[q]);
-          ss = cnt >= SM;
-        }
-      }
+    uint64_t m = 0;
+    if (ring) {
+      const int s = r % RING;
+      const uint64_t pres = wpres[s];
+      int wv[NM];
+#pragma unroll
+      for (int dd = 0; dd < NM; dd++) wv[dd] = wfd[s][dd][k];
+#pragma unroll
+      for (int dd = 0; dd < NM; dd++)
+        if (__popcll(ballot(la >= wv[dd])) >= SM) m |= 1ull << dd;
+      return m & pres;
     }
-    return ballot(ss);
+    for (int dd = 0; dd < N; dd++) {
+      const int w = ld(&t.W[(int64_t)(d.ro + r) * N + dd]);
+      if (w < 0) continue;
+      const int f = k < N ? ld(&t.WFD[((int64_t)(d.ro + r) * N + dd) * N + k]) : INF;
+      if (__popcll(ballot(la >= f)) >= SM) m |= 1ull << dd;
+    }
+    return m;
   };
-  for (int base = 0; base < d.E && !err; base += 64) {
-    const int i = base + k;
-    int mcr = 0, mix = 0, msp = -1, mop = -1, moc = 0;
-    if (i < d.E) {
-      mcr = t.cr[d.eo + i];
-      mix = t.ix[d.eo + i];
-      msp = t.sp[d.eo + i];
-      mop = t.op[d.eo + i];
-      moc = mop >= 0 ? t.cr[d.eo + mop] : 0;
+  // chunk loads: element e = k + 64 v of the chunk's CH x N row block
+  int rla[PER], rfd[PER], mcr, mix, msp, mop, moc, mco;
+  auto load = [&](int base) {
+#pragma unroll
+    for (int v = 0; v < PER; v++) {
+      const int e = k + 64 * v, row = e / NM, col = e % NM;
+      const bool on = col < N && base + row < d.E;
+      rla[v] = on ? LA[(int64_t)(base + row) * N + col] : -1;
+      rfd[v] = on ? FD[(int64_t)(base + row) * N + col] : INF;
     }
-    const int cnt = min(64, d.E - base);
-    int la = k < N && cnt > 0 ? LA[(int64_t)base * N + k] : -1;
+    const int i = base + k;
+    const bool on = k < CH && i < d.E;
+    mcr = on ? t.cr[d.eo + i] : 0;
+    mix = on ? t.ix[d.eo + i] : 0;
+    msp = on ? t.sp[d.eo + i] : -1;
+    mop = on ? t.op[d.eo + i] : -1;
+    moc = on ? t.oc[d.eo + i] : 0;
+    mco = on ? t.coin[d.eo + i] : 0;
+  };
+  load(0);
+  for (int base = 0; base < d.E && !err; base += CH) {
+#pragma unroll
+    for (int v = 0; v < PER; v++) {
+      const int e = k + 64 * v;
+      bla[e / NM][e % NM] = rla[v];
+      bfd[e / NM][e % NM] = rfd[v];
+    }
+    const int ccr = mcr, cix = mix, csp = msp, cop = mop, coc = moc, cco = mco;
+    wsync();
+    if (base + CH < d.E) load(base + CH);  // the next chunk, in flight meanwhile
+    const int cnt = min(CH, d.E - base);
     for (int u = 0; u < cnt; u++) {
       const int x = base + u;
-      const int cr = rl(mcr, u), ix = rl(mix, u), sp = rl(msp, u), op = rl(mop, u), oc = rl(moc, u);
-      const int lax = la;
-      if (u + 1 < cnt) la = k < N ? LA[(int64_t)(x + 1) * N + k] : -1;
+      const int cr = rl(ccr, u), ix = rl(cix, u), sp = rl(csp, u), op = rl(cop, u), oc = rl(coc, u);
+      const int lax = k < N ? bla[u][k] : -1;
       // ParentRound (hashgraph.go:220-244): 0 without both parents
-      const int rsp = sp >= 0 ? rhead[cr] : -1;
+      const int rsp = sp >= 0 ? rl(rh, cr) : -1;
       int pr = 0;
       if (sp >= 0 && op >= 0) {
-        const int rop = headid[oc] == op ? rhead[oc] : ld(&t.round[d.eo + op]);
+        const int rop = rl(hid, oc) == op ? rl(rh, oc) : ld(&t.round[d.eo + op]);
         pr = max(rsp, rop);
       }
       // RoundInc (hashgraph.go:263-285): Rounds() < pr + 1 -> false
@@ -288,10 +379,9 @@ __global__ __launch_bounds__(64) void kb_rounds(BT t) {
         st(&t.round[d.eo + x], r);
         t.wit[d.eo + x] = w;
       }
-      wsync();
-      if (k == 0) {
-        rhead[cr] = r;
-        headid[cr] = x;
+      if (k == cr) {
+        rh = r;
+        hid = x;
       }
       maxr = max(maxr, r);
       if (w) {
@@ -302,19 +392,22 @@ __global__ __launch_bounds__(64) void kb_rounds(BT t) {
         while (top < r) {  // a new round takes the oldest ring slot
           top++;
           if (k < N) wid[top % RING][k] = -1;
+          if (k == 0) wpres[top % RING] = 0;
         }
         const bool inring = r > top - RING;
-        const int fdk = k < N ? FDTg[((int64_t)k * N + cr) * cc + ix] : INF;
+        const int fdk = k < N ? bfd[u][k] : INF;
         if (k < N) st(&t.WFD[((int64_t)(d.ro + r) * N + cr) * N + k], fdk);
         if (k == 0) {
           st(&t.W[(int64_t)(d.ro + r) * N + cr], x);
           st(&t.WIX[(int64_t)(d.ro + r) * N + cr], ix);
+          t.WCOIN[(int64_t)(d.ro + r) * N + cr] = (uint8_t)rl(cco, u);
         }
-        if (inring && k < N) wfd[r % RING][k][cr] = fdk;
+        if (inring && k < N) wfd[r % RING][cr][k] = fdk;
         wsync();
         if (inring && k == 0) {
           wid[r % RING][cr] = x;
           wixr[r % RING][cr] = ix;
+          wpres[r % RING] |= 1ull << cr;
         }
         wsync();
         if (r >= 1) {
@@ -337,6 +430,7 @@ __global__ __launch_bounds__(64) void kb_rounds(BT t) {
       }
       wsync();
     }
+    wsync();
   }
   if (k == 0 && err) t.scal[(int64_t)blockIdx.x * 8 + 6] = 1;
 }
@@ -420,66 +514,175 @@ __device__ void sort_keys(const BT& t, int64_t eo, int n, int32_t* kr, int64_t* 
   }
 }
 
+// ascending bitonic sorting network over M register values (M a power of two)
+template <int M>
+__device__ __forceinline__ void sort_regs(int64_t (&v)[M]) {
+#pragma unroll
+  for (int size = 2; size <= M; size <<= 1)
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1)
+#pragma unroll
+      for (int i = 0; i < M; i++) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool up = (i & size) == 0;
+          const int64_t a = v[i], b = v[j];
+          const bool sw = up ? a > b : a < b;
+          v[i] = sw ? b : a;
+          v[j] = sw ? a : b;
+        }
+      }
+}
+
+// ---------------------------------------------------------------------------
+// The graph's call schedule in order.  LDS holds the state of the rounds
+// [R - RW, R) (witnesses and their indexes, vote bitsets, coins, fame, event
+// counts, versions, receive thresholds and famous masks) and the undetermined list
+// with each event's round, creator and index; rounds below the window and lists
+// past UL entries live in global memory, where every mutation is also written.
 template <int NM>
 __global__ __launch_bounds__(64) void kb_consensus(BT t) {
+  constexpr int RW = 16, UL = 768, KB = 256;
   const int g = blockIdx.x;
   const GDesc d = t.gd[g];
   const int N = t.N, SM = t.SM, lane = threadIdx.x, cc = t.ccap;
   const int64_t eo = d.eo;
   const int32_t* LA = t.LA + eo * N;
-  const int32_t* FDTg = t.FDT + (int64_t)g * N * N * cc;
+  const int32_t* FD = t.FD + eo * N;
   const int64_t* tschg = t.tsch + (int64_t)g * N * cc;
-  __shared__ int32_t kr[LB], ki[LB];
-  __shared__ int64_t kc[LB];
-  __shared__ uint64_t ks[LB];
+  __shared__ int32_t wid[RW][NM], wix[RW][NM], thL[RW][NM];
+  __shared__ uint64_t ssbL[RW][NM], seebL[RW][NM];
+  __shared__ uint64_t coinL[RW], fmL[RW];
+  __shared__ int8_t fameL[RW][NM];
+  __shared__ int32_t rcntL[RW], verL[RW], thvL[RW];
+  __shared__ int32_t Uid_s[UL], Ur_s[UL], Ucp_s[UL];
+  __shared__ int32_t kr[KB], ki[KB];
+  __shared__ int64_t kc[KB];
+  __shared__ uint64_t ks[KB];
   if (t.scal[(int64_t)g * 8 + 6]) return;  // the rounds pass failed: nothing to decide
   int R = 0, lcr = -1, lcre = 0, nord = 0, nU = 0, n_prev = 0;
   int64_t ctx = 0;
+  bool ug = false;  // the undetermined list lives in global memory
+  int32_t *Ug = t.U + eo, *Urg = t.Ur + eo, *Ucpg = t.Ucp + eo;
+  auto uget = [&](const int32_t* ls, const int32_t* gs, int i) -> int { return ug ? ld(&gs[i]) : ls[i]; };
+  auto uput = [&](int32_t* ls, int32_t* gs, int i, int v) {
+    if (ug) st(&gs[i], v);
+    else ls[i] = v;
+  };
+  // ---- round accessors: LDS for [R - RW, R), global below ----
+  auto res = [&](int r) { return r >= 0 && r < R && r >= R - RW; };
+  auto row = [&](int r) { return (int64_t)(d.ro + r) * N; };
+  auto W_ = [&](int r, int c) -> int { return res(r) ? wid[r & (RW - 1)][c] : t.W[row(r) + c]; };
+  auto WIX_ = [&](int r, int c) -> int { return res(r) ? wix[r & (RW - 1)][c] : t.WIX[row(r) + c]; };
+  auto fame_ = [&](int r, int c) -> int { return res(r) ? fameL[r & (RW - 1)][c] : ld(&t.fame[row(r) + c]); };
+  auto rcnt_ = [&](int r) -> int { return res(r) ? rcntL[r & (RW - 1)] : ld(&t.rcnt[d.ro + r]); };
+  auto ver_ = [&](int r) -> int { return res(r) ? verL[r & (RW - 1)] : ld(&t.ver[d.ro + r]); };
+  auto thv_ = [&](int r) -> int { return res(r) ? thvL[r & (RW - 1)] : ld(&t.thv[d.ro + r]); };
+  // single-writer updates (lane 0 or the lane of column c), written through
+  auto set_rcnt = [&](int r, int v) {
+    if (res(r)) rcntL[r & (RW - 1)] = v;
+    st(&t.rcnt[d.ro + r], v);
+  };
+  auto set_ver = [&](int r, int v) {
+    if (res(r)) verL[r & (RW - 1)] = v;
+    st(&t.ver[d.ro + r], v);
+  };
   for (int c = 0; c < d.K; c++) {
     const int n_c = (int)t.calls[d.co + c];
     // ---- DivideRounds (hashgraph.go:573-588): the new events join the store ----
     {
-      int rmax = -1;
-      for (int b0 = n_prev; b0 < n_c; b0 += 64) {
-        const int i = b0 + lane;
-        const bool on = i < n_c;
-        const int r = on ? t.round[eo + i] : -1;
-        const bool w = on && t.wit[eo + i];
-        if (on) st(&t.U[eo + nU + (i - n_prev)], i);
-        rmax = max(rmax, r);
-        // per-round event counts (RoundEvents) and witness versions, one writer per round
-        uint64_t rem = ballot(on);
-        while (rem) {
-          const int r0 = rl(r, __ffsll((unsigned long long)rem) - 1);
-          const uint64_t same = ballot(on && r == r0);
-          const int nw = __popcll(ballot(on && r == r0 && w));
-          if (lane == 0) {
-            st(&t.rcnt[d.ro + r0], ld(&t.rcnt[d.ro + r0]) + __popcll(same));
-            if (nw) st(&t.ver[d.ro + r0], ld(&t.ver[d.ro + r0]) + 1);
-          }
-          rem &= ~same;
+      const int nn = n_c - n_prev;
+      // the first 64 new events stay in registers (K <= 64: every call's)
+      const bool on0 = lane < nn;
+      const int x0 = n_prev + lane;
+      int r0 = on0 ? t.round[eo + x0] : -1;
+      const int w0 = on0 ? t.wit[eo + x0] : 0;
+      const int cp0 = on0 ? (t.cr[eo + x0] << 24 | t.ix[eo + x0]) : 0;
+      int rmax = r0;
+      for (int b0 = n_prev + 64; b0 < n_c; b0 += 64)
+        if (b0 + lane < n_c) rmax = max(rmax, t.round[eo + b0 + lane]);
+      rmax = wave_max(rmax);
+      const int Rnew = nn > 0 ? max(R, rmax + 1) : R;
+      // rounds entering the window: their immutable rows, fresh mutable state
+      for (int r = max(R, Rnew - RW); r < Rnew; r++) {
+        const int s = r & (RW - 1);
+        const bool cl = lane < N;
+        const int64_t rw_ = (int64_t)(d.ro + r) * N;
+        const int w = cl ? t.W[rw_ + lane] : -1;
+        if (cl) {
+          wid[s][lane] = w;
+          wix[s][lane] = t.WIX[rw_ + lane];
+          ssbL[s][lane] = t.ssb[rw_ + lane];
+          seebL[s][lane] = t.seeb[rw_ + lane];
+          fameL[s][lane] = 0;
+        }
+        const uint64_t cm = ballot(cl && w >= 0 && t.WCOIN[rw_ + lane]);
+        if (lane == 0) {
+          coinL[s] = cm;
+          fmL[s] = 0;
+          rcntL[s] = 0;
+          verL[s] = 0;
+          thvL[s] = -1;
         }
       }
-      rmax = wave_max(rmax);
-      if (n_c > n_prev) R = max(R, rmax + 1);
-      nU += n_c - n_prev;
+      R = Rnew;
+      wsync();
+      // RoundEvents counts and witness versions, one writer per round; the
+      // undetermined list grows by the new events in insertion order
+      if (!ug && nU + nn > UL) {  // past the LDS list: move it to global memory for good
+        for (int i = lane; i < nU; i += 64) {
+          st(&Ug[i], Uid_s[i]);
+          st(&Urg[i], Ur_s[i]);
+          st(&Ucpg[i], Ucp_s[i]);
+        }
+        ug = true;
+      }
+      for (int b0 = n_prev; b0 < n_c; b0 += 64) {
+        const int x = b0 + lane;
+        const bool on = x < n_c;
+        const int r = b0 == n_prev ? r0 : (on ? t.round[eo + x] : -1);
+        const int w = b0 == n_prev ? w0 : (on ? t.wit[eo + x] : 0);
+        const int cp = b0 == n_prev ? cp0 : (on ? (t.cr[eo + x] << 24 | t.ix[eo + x]) : 0);
+        if (on) {
+          uput(Uid_s, Ug, nU + (x - n_prev), x);
+          uput(Ur_s, Urg, nU + (x - n_prev), r);
+          uput(Ucp_s, Ucpg, nU + (x - n_prev), cp);
+        }
+        uint64_t rem = ballot(on);
+        while (rem) {
+          const int rr0 = rl(r, __ffsll((unsigned long long)rem) - 1);
+          const uint64_t same = ballot(on && r == rr0);
+          const bool nw = ballot(on && r == rr0 && w) != 0;
+          if (lane == 0) {
+            set_rcnt(rr0, rcnt_(rr0) + __popcll(same));
+            if (nw) set_ver(rr0, ver_(rr0) + 1);
+          }
+          rem &= ~same;
+          wsync();
+        }
+      }
+      nU += nn;
       n_prev = n_c;
     }
     wsync();
     // ---- DecideFame (hashgraph.go:598-664) ----
     for (int i = lcr + 1; i < R - 1; i++) {
-      const int xid = lane < N ? t.W[(int64_t)(d.ro + i) * N + lane] : -1;
+      const int xid = lane < N ? W_(i, lane) : -1;
       const bool px = xid >= 0 && xid < n_c;
-      const int fv0 = px ? ld(&t.fame[(int64_t)(d.ro + i) * N + lane]) : 0;
+      const int fv0 = px ? fame_(i, lane) : 0;
       int fv = fv0;
       uint64_t prev = 0;
       for (int j = i + 1; j < R; j++) {
         const int diff = j - i;
-        const int64_t row = (int64_t)(d.ro + j) * N;
-        const int yid = lane < N ? t.W[row + lane] : -1;
+        const bool rj = res(j);
+        const int sj = j & (RW - 1);
+        const int yid = lane < N ? W_(j, lane) : -1;
         const bool py = yid >= 0 && yid < n_c;
-        const uint64_t ybits = lane < N ? (diff == 1 ? t.seeb[row + lane] : t.ssb[row + lane]) : 0;
-        const int ycoin = py ? t.coin[eo + yid] : 0;
+        uint64_t ybits = 0;
+        if (lane < N)
+          ybits = diff == 1 ? (rj ? seebL[sj][lane] : t.seeb[row(j) + lane])
+                            : (rj ? ssbL[sj][lane] : t.ssb[row(j) + lane]);
+        const uint64_t ycoin = rj ? coinL[sj] : ballot(py && t.WCOIN[row(j) + lane]);
         uint64_t mm = ballot(py);
         uint64_t cur = 0;
         bool on = px;
@@ -500,8 +703,8 @@ __global__ __launch_bounds__(64) void kb_consensus(BT t) {
               } else if (v) {
                 cur |= 1ull << dd;
               }
-            } else {  // coin round
-              if (tt < SM) v = rl(ycoin, dd) != 0;
+            } else {  // coin round: the middle bit of y's hash when no supermajority
+              if (tt < SM) v = (ycoin >> dd) & 1;
               if (v) cur |= 1ull << dd;
             }
           }
@@ -509,118 +712,132 @@ __global__ __launch_bounds__(64) void kb_consensus(BT t) {
         prev = cur;
       }
       const bool chg = px && fv != fv0;
-      if (chg) st(&t.fame[(int64_t)(d.ro + i) * N + lane], (int8_t)fv);
-      if (ballot(chg) && lane == 0) st(&t.ver[d.ro + i], ld(&t.ver[d.ro + i]) + 1);
+      if (chg) {
+        if (res(i)) fameL[i & (RW - 1)][lane] = (int8_t)fv;
+        st(&t.fame[row(i) + lane], (int8_t)fv);
+      }
+      wsync();
+      if (ballot(chg) && lane == 0) set_ver(i, ver_(i) + 1);
       const bool decided = ballot(px && fv == 0) == 0;  // WitnessesDecided (roundInfo.go:78-85)
       if (decided && (lcr < 0 || i > lcr)) {           // setLastConsensusRound (hashgraph.go:666-673)
         lcr = i;
-        lcre = i >= 1 ? ld(&t.rcnt[d.ro + i - 1]) : 0;
+        lcre = i >= 1 ? rcnt_(i - 1) : 0;
       }
+      wsync();
     }
-    wsync();
     // ---- DecideRoundReceived (hashgraph.go:676-721) ----
-    // the rounds the undetermined events can be received in: (min round, R)
     int rmin = INF;
-    for (int b0 = 0; b0 < nU; b0 += 64) {
-      const int x = b0 + lane < nU ? ld(&t.U[eo + b0 + lane]) : -1;
-      rmin = min(rmin, x >= 0 ? t.round[eo + x] : INF);
-    }
+    for (int b0 = 0; b0 < nU; b0 += 64)
+      if (b0 + lane < nU) rmin = min(rmin, uget(Ur_s, Urg, b0 + lane));
     rmin = wave_min(rmin);
-    if (rmin == INF) rmin = R;  // nothing undetermined
-    // per round: decided, the famous witnesses, the thresholds (kept across calls
-    // while the round's fame and witnesses are unchanged)
+    if (rmin == INF) rmin = R;
+    // decided rounds past the lowest undetermined round: the famous mask and the
+    // thresholds theta (kept while the round's version holds)
     for (int i = rmin + 1; i < R; i++) {
-      const int64_t row = (int64_t)(d.ro + i) * N;
-      const int w = lane < N ? t.W[row + lane] : -1;
+      const int w = lane < N ? W_(i, lane) : -1;
       const bool pw = w >= 0 && w < n_c;
-      const int f = pw ? ld(&t.fame[row + lane]) : 0;
-      if (ballot(pw && f == 0)) continue;  // not decided: thresholds unused
-      const int v = ld(&t.ver[d.ro + i]);
-      if (ld(&t.thv[d.ro + i]) == v) continue;
+      const int f = pw ? fame_(i, lane) : 0;
+      if (ballot(pw && f == 0)) continue;  // not decided
+      const int v = ver_(i);
+      if (thv_(i) == v) continue;
       const uint64_t fm = ballot(pw && f == 1);
       const int m = __popcll(fm);
-      int th = -1;
+      int th = -2;  // no famous witness: nothing is received in the round
       if (lane < N && m > 0) {
+        int vals[NM];
+#pragma unroll
+        for (int dd = 0; dd < NM; dd++) vals[dd] = (fm >> dd) & 1 ? LA[(int64_t)rl(w, dd) * N + lane] : -1;
         const int need = m / 2 + 1;  // len(s) > len(fws)/2
-        int lo = -1, hi = t.clen[g * N + lane] - 1;  // count_ge(lo) = m >= need
+        int lo = -1, hi = t.clen[g * N + lane] - 1;
         while (lo < hi) {
           const int mid = (lo + hi + 1) >> 1;
           int cnt = 0;
-          uint64_t q = fm;
-          while (q) {
-            const int dd = __ffsll((unsigned long long)q) - 1;
-            q &= q - 1;
-            cnt += LA[(int64_t)rl(w, dd) * N + lane] >= mid;
-          }
+#pragma unroll
+          for (int dd = 0; dd < NM; dd++) cnt += ((fm >> dd) & 1) && vals[dd] >= mid;
           if (cnt >= need) lo = mid;
           else hi = mid - 1;
         }
         th = lo;
       }
-      if (lane < N) st(&t.th[row + lane], m > 0 ? th : -2);
+      if (lane < N) {
+        if (res(i)) thL[i & (RW - 1)][lane] = th;
+        st(&t.th[row(i) + lane], th);
+      }
       wsync();
-      if (lane == 0) st(&t.thv[d.ro + i], v);
+      if (lane == 0) {
+        if (res(i)) {
+          thvL[i & (RW - 1)] = v;
+          fmL[i & (RW - 1)] = fm;
+        }
+        st(&t.thv[d.ro + i], v);
+      }
+      wsync();
     }
-    wsync();
-    __threadfence_block();
     // the undetermined events in order: received ones become the call's batch (keys
-    // to LDS, and to global scratch past LB), the rest stay undetermined (compacted)
+    // to LDS, and to global scratch past KB), the rest stay (compacted in place)
     int nb = 0, nk = 0;
+    int64_t tx = 0;
     for (int b0 = 0; b0 < nU; b0 += 64) {
       const bool on = b0 + lane < nU;
-      const int x = on ? ld(&t.U[eo + b0 + lane]) : -1;
+      const int x = on ? uget(Uid_s, Ug, b0 + lane) : -1;
+      const int r = on ? uget(Ur_s, Urg, b0 + lane) : 0;
+      const int cp = on ? uget(Ucp_s, Ucpg, b0 + lane) : 0;
+      const int cx = cp >> 24, px = cp & 0xFFFFFF;
       int found = -1;
-      int cx = 0, px = 0;
       if (on) {
-        const int r = t.round[eo + x];
-        cx = t.cr[eo + x];
-        px = t.ix[eo + x];
         for (int i = r + 1; i < R; i++) {
-          const int64_t row = (int64_t)(d.ro + i) * N;
-          // decided rounds have thresholds of the current version; -2: no famous witness
-          if (ld(&t.thv[d.ro + i]) != ld(&t.ver[d.ro + i])) continue;
-          const int th = ld(&t.th[row + cx]);
-          if (th == -2) continue;
-          if (px <= th) {
+          int th;
+          if (res(i)) {
+            const int s = i & (RW - 1);
+            if (thvL[s] != verL[s]) continue;  // not decided (or thresholds stale: never here)
+            th = thL[s][cx];
+          } else {
+            if (ld(&t.thv[d.ro + i]) != ld(&t.ver[d.ro + i])) continue;
+            th = ld(&t.th[row(i) + cx]);
+          }
+          if (th != -2 && px <= th) {
             found = i;
             break;
           }
         }
       }
       int64_t med = 0;
+      uint64_t s0 = 0;
       if (found >= 0) {
-        // MedianTimestamp over OldestSelfAncestorToSee(w, x) of the famous witnesses
-        // w that see x (hashgraph.go:704-709, 762-770): the upper median
-        const int64_t row = (int64_t)(d.ro + found) * N;
+        // MedianTimestamp over OldestSelfAncestorToSee(w, x) of the famous witnesses w
+        // that see x (hashgraph.go:704-709, 762-770), the upper median.  w = (d, i_w)
+        // sees x iff FD[x][d] <= i_w, and FD[x][d] is then OldestSelfAncestorToSee
+        s0 = t.S[(eo + x) * 4];
+        tx += t.ntx[eo + x];
+        uint64_t fm;
+        if (res(found)) {
+          fm = fmL[found & (RW - 1)];
+        } else {
+          fm = 0;
+          for (int dd = 0; dd < N; dd++) {
+            const int w = t.W[row(found) + dd];
+            if (w >= 0 && w < n_c && ld(&t.fame[row(found) + dd]) == 1) fm |= 1ull << dd;
+          }
+        }
         int64_t vals[NM];
+        int q[NM];
+#pragma unroll
+        for (int dd = 0; dd < NM; dd++) q[dd] = dd < N && ((fm >> dd) & 1) ? FD[(int64_t)x * N + dd] : INF;
         int m = 0;
 #pragma unroll
         for (int dd = 0; dd < NM; dd++) {
           vals[dd] = TS_MAX;
-          if (dd < N) {
-            const int w = t.W[row + dd];
-            if (w >= 0 && w < n_c && ld(&t.fame[row + dd]) == 1 && LA[(int64_t)w * N + cx] >= px) {
-              const int q = FDTg[((int64_t)dd * N + cx) * cc + px];
-              vals[dd] = q <= t.WIX[row + dd] ? tschg[(int64_t)dd * cc + q] : ZERO_TIME;
-              m++;
-            }
+          if (q[dd] != INF && q[dd] <= WIX_(found, dd)) {
+            vals[dd] = tschg[(int64_t)dd * cc + q[dd]];
+            m++;
           }
         }
+        // the upper median: the m real values sort before the TS_MAX fillers
+        sort_regs<NM>(vals);
         const int want = m / 2;
-        bool got = false;
 #pragma unroll
-        for (int a = 0; a < NM; a++) {
-          if (a < N && vals[a] != TS_MAX && !got) {
-            int rank = 0;
-#pragma unroll
-            for (int b = 0; b < NM; b++)
-              rank += (b < N) && vals[b] != TS_MAX && (vals[b] < vals[a] || (vals[b] == vals[a] && b < a));
-            if (rank == want) {
-              med = vals[a];
-              got = true;
-            }
-          }
-        }
+        for (int a = 0; a < NM; a++)
+          if (a == want) med = vals[a];
         t.rr[eo + x] = found;
         t.cts[eo + x] = med;
       }
@@ -629,47 +846,50 @@ __global__ __launch_bounds__(64) void kb_consensus(BT t) {
       const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
       if (found >= 0) {
         const int p = nb + __popcll(rec & below);
-        const uint64_t s0 = t.S[(eo + x) * 4];
-        if (p < LB) {
+        if (p < KB) {
           kr[p] = found;
           kc[p] = med;
           ks[p] = s0;
           ki[p] = x;
         }
-        st(&t.krr[2 * eo + nord + p], found);
-        st(&t.kct[2 * eo + nord + p], med);
-        st(&t.ks0[2 * eo + nord + p], s0);
-        st(&t.kid[2 * eo + nord + p], x);
+        const int64_t so = 2 * eo + nord + p;
+        st(&t.krr[so], found);
+        st(&t.kct[so], med);
+        st(&t.ks0[so], s0);
+        st(&t.kid[so], x);
       }
-      if (on && found < 0) st(&t.U[eo + nk + __popcll(keep & below)], x);
+      if (on && found < 0) {
+        const int p = nk + __popcll(keep & below);
+        uput(Uid_s, Ug, p, x);
+        uput(Ur_s, Urg, p, r);
+        uput(Ucp_s, Ucpg, p, cp);
+      }
       nb += __popcll(rec);
       nk += __popcll(keep);
       wsync();
     }
     nU = nk;
     wsync();
-    __threadfence_block();
     // ---- FindOrder (hashgraph.go:723-760): sort the batch, append it ----
     if (nb > 0) {
-      if (nb <= LB) {
+      if (nb <= KB) {
         sort_keys<false>(t, eo, nb, kr, kc, ks, ki);
         for (int p = lane; p < nb; p += 64) t.order[eo + nord + p] = ki[p];
       } else {
-        // past LB keys: the same network on the graph's global scratch (2E entries from
-        // 2 eo: nord + the padded size stays below 2E)
+        // past KB keys: the same network on the graph's global scratch (2E entries
+        // from 2 eo: nord + the padded size stays below 2E)
         const int64_t so = 2 * eo + nord;
         sort_keys<true>(t, eo, nb, t.krr + so, t.kct + so, t.ks0 + so, t.kid + so);
         for (int p = lane; p < nb; p += 64) t.order[eo + nord + p] = ld(&t.kid[so + p]);
       }
-      int64_t tx = 0;
-      for (int p = lane; p < nb; p += 64) tx += t.ntx[eo + (nb <= LB ? ki[p] : ld(&t.kid[2 * eo + nord + p]))];
       ctx += wave_sum64(tx);
     }
     if (lane == 0) t.counts[d.co + c] = nb;
     nord += nb;
     wsync();
-    __threadfence_block();
   }
+  // the undetermined list for the host
+  for (int i = lane; i < nU; i += 64) t.U[eo + i] = uget(Uid_s, Ug, i);
   if (lane == 0) {
     int64_t* s = t.scal + (int64_t)g * 8;
     s[0] = R;
@@ -723,10 +943,10 @@ struct Buf {
 struct hge_batch {
   int N = 0, SM = 1, device = 0;
   hipStream_t st = nullptr;
-  hipEvent_t ev[5] = {};
+  hipEvent_t ev[6] = {};
   std::string err;
   struct Graph {
-    std::vector<int32_t> cr, ix, sp, op, ntx;
+    std::vector<int32_t> cr, ix, sp, op, oc, ntx;
     std::vector<int64_t> ts;
     std::vector<uint64_t> S;
     std::vector<uint8_t> coin;
@@ -740,25 +960,29 @@ struct hge_batch {
   int64_t Ktot = 0, Rtot = 0;
   int ccap = 0;
   std::vector<int64_t> h_scal;
-  float kms[4] = {};
+  static constexpr int NK = 5;
+  float kms[NK] = {};
   // device tables
   Buf<GDesc> d_gd;
-  Buf<int32_t> d_cr, d_ix, d_sp, d_op, d_ntx, d_clen, d_chain, d_LA, d_FDT, d_round, d_rr, d_W, d_WIX, d_WFD;
-  Buf<int32_t> d_rcnt, d_ver, d_thv, d_th, d_U, d_order, d_krr, d_kid;
+  Buf<int32_t> d_cr, d_ix, d_sp, d_op, d_oc, d_ntx, d_clen, d_chain, d_LA, d_FDT, d_FD, d_round, d_rr, d_W, d_WIX,
+      d_WFD;
+  Buf<int32_t> d_rcnt, d_ver, d_thv, d_th, d_U, d_Ur, d_Ucp, d_order, d_krr, d_kid;
   Buf<int64_t> d_ts, d_tsch, d_calls, d_cts, d_counts, d_scal, d_kct;
   Buf<uint64_t> d_S, d_ssb, d_seeb, d_ks0;
-  Buf<uint8_t> d_coin, d_wit;
+  Buf<uint8_t> d_coin, d_wit, d_WCOIN;
   Buf<int8_t> d_fame;
 
   void free_all() {
     d_gd.free_();
-    for (auto* b : {&d_cr, &d_ix, &d_sp, &d_op, &d_ntx, &d_clen, &d_chain, &d_LA, &d_FDT, &d_round, &d_rr, &d_W,
-                    &d_WIX, &d_WFD, &d_rcnt, &d_ver, &d_thv, &d_th, &d_U, &d_order, &d_krr, &d_kid})
+    for (auto* b : {&d_cr, &d_ix, &d_sp, &d_op, &d_oc, &d_ntx, &d_clen, &d_chain, &d_LA, &d_FDT, &d_FD, &d_round,
+                    &d_rr, &d_W, &d_WIX, &d_WFD, &d_rcnt, &d_ver, &d_thv, &d_th, &d_U, &d_Ur, &d_Ucp, &d_order,
+                    &d_krr, &d_kid})
       b->free_();
     for (auto* b : {&d_ts, &d_tsch, &d_calls, &d_cts, &d_counts, &d_scal, &d_kct}) b->free_();
     for (auto* b : {&d_S, &d_ssb, &d_seeb, &d_ks0}) b->free_();
     d_coin.free_();
     d_wit.free_();
+    d_WCOIN.free_();
     d_fame.free_();
   }
 
@@ -800,6 +1024,7 @@ struct hge_batch {
         G.ix.push_back(ev[i].index);
         G.sp.push_back(sp);
         G.op.push_back(op);
+        G.oc.push_back(op >= 0 ? G.cr[op] : 0);
         G.ntx.push_back(ev[i].n_tx);
         G.ts.push_back(ev[i].timestamp_ns);
         for (int k = 0; k < 4; k++) {
@@ -851,7 +1076,8 @@ struct hge_batch {
       for (int c = 0; c < N; c++) ccap = std::max(ccap, (int)gr.chain[c].size());
     }
     if (Rtot >= INT32_MAX || Ktot >= INT32_MAX) throw BatchError{HGE_ERR_CAPACITY, "batch too large"};
-    std::vector<int32_t> cr, ix, sp, op, ntx, clen((size_t)G * N), chain((size_t)G * N * ccap, -1);
+    if (ccap >= (1 << 24)) throw BatchError{HGE_ERR_CAPACITY, "batch graph with a chain of 2^24 events or more"};
+    std::vector<int32_t> cr, ix, sp, op, oc, ntx, clen((size_t)G * N), chain((size_t)G * N * ccap, -1);
     std::vector<int64_t> ts, tsch((size_t)G * N * ccap, 0), calls;
     std::vector<uint64_t> S;
     std::vector<uint8_t> coin;
@@ -862,6 +1088,7 @@ struct hge_batch {
       ix.insert(ix.end(), gr.ix.begin(), gr.ix.end());
       sp.insert(sp.end(), gr.sp.begin(), gr.sp.end());
       op.insert(op.end(), gr.op.begin(), gr.op.end());
+      oc.insert(oc.end(), gr.oc.begin(), gr.oc.end());
       ntx.insert(ntx.end(), gr.ntx.begin(), gr.ntx.end());
       ts.insert(ts.end(), gr.ts.begin(), gr.ts.end());
       S.insert(S.end(), gr.S.begin(), gr.S.end());
@@ -879,6 +1106,7 @@ struct hge_batch {
     up(d_ix, ix);
     up(d_sp, sp);
     up(d_op, op);
+    up(d_oc, oc);
     up(d_ntx, ntx);
     up(d_ts, ts);
     up(d_S, S);
@@ -892,11 +1120,14 @@ struct hge_batch {
     const size_t E1 = (size_t)std::max<int64_t>(Etot, 1);
     d_LA.need(E1 * N);
     d_FDT.need((size_t)G * N * N * ccap);
+    d_FD.need(E1 * N);
     d_round.need(E1);
     d_wit.need(E1);
     d_rr.need(E1);
     d_cts.need(E1);
     d_U.need(E1);
+    d_Ur.need(E1);
+    d_Ucp.need(E1);
     d_order.need(E1);
     d_krr.need(2 * E1 + 64);
     d_kct.need(2 * E1 + 64);
@@ -906,6 +1137,7 @@ struct hge_batch {
     d_W.need(RN);
     d_WIX.need(RN);
     d_WFD.need(RN * N);
+    d_WCOIN.need(RN);
     d_ssb.need(RN);
     d_seeb.need(RN);
     d_fame.need(RN);
@@ -929,6 +1161,7 @@ struct hge_batch {
     t.ix = d_ix.p;
     t.sp = d_sp.p;
     t.op = d_op.p;
+    t.oc = d_oc.p;
     t.ntx = d_ntx.p;
     t.clen = d_clen.p;
     t.ts = d_ts.p;
@@ -939,6 +1172,7 @@ struct hge_batch {
     t.calls = d_calls.p;
     t.LA = d_LA.p;
     t.FDT = d_FDT.p;
+    t.FD = d_FD.p;
     t.round = d_round.p;
     t.wit = d_wit.p;
     t.rr = d_rr.p;
@@ -946,6 +1180,7 @@ struct hge_batch {
     t.W = d_W.p;
     t.WIX = d_WIX.p;
     t.WFD = d_WFD.p;
+    t.WCOIN = d_WCOIN.p;
     t.ssb = d_ssb.p;
     t.seeb = d_seeb.p;
     t.fame = d_fame.p;
@@ -954,6 +1189,8 @@ struct hge_batch {
     t.thv = d_thv.p;
     t.th = d_th.p;
     t.U = d_U.p;
+    t.Ur = d_Ur.p;
+    t.Ucp = d_Ucp.p;
     t.order = d_order.p;
     t.counts = d_counts.p;
     t.scal = d_scal.p;
@@ -965,8 +1202,8 @@ struct hge_batch {
   }
 
   template <typename K>
-  void launch(K kern, int G, const BT& t) {
-    hipLaunchKernelGGL(kern, dim3(G), dim3(64), 0, st, t);
+  void launch(K kern, int G, const BT& t, int block = 64) {
+    hipLaunchKernelGGL(kern, dim3(G), dim3(block), 0, st, t);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) throw BatchError{HGE_ERR_DEVICE, std::string("batch launch: ") + hipGetErrorString(e)};
   }
@@ -995,23 +1232,27 @@ struct hge_batch {
       BCHK(hipEventRecord(ev[1], st));
       launch(kb_fd<32>, G, t);
       BCHK(hipEventRecord(ev[2], st));
-      launch(kb_rounds<32, 4>, G, t);
+      launch(kb_fdrows<32>, G * N, t, 256);
       BCHK(hipEventRecord(ev[3], st));
+      launch(kb_rounds<32, 4>, G, t);
+      BCHK(hipEventRecord(ev[4], st));
       launch(kb_consensus<32>, G, t);
     } else {
       launch(kb_coords<64>, G, t);
       BCHK(hipEventRecord(ev[1], st));
       launch(kb_fd<64>, G, t);
       BCHK(hipEventRecord(ev[2], st));
-      launch(kb_rounds<64, 2>, G, t);
+      launch(kb_fdrows<64>, G * N, t, 256);
       BCHK(hipEventRecord(ev[3], st));
+      launch(kb_rounds<64, 2>, G, t);
+      BCHK(hipEventRecord(ev[4], st));
       launch(kb_consensus<64>, G, t);
     }
-    BCHK(hipEventRecord(ev[4], st));
+    BCHK(hipEventRecord(ev[5], st));
     h_scal.resize((size_t)G * 8);
     BCHK(hipMemcpyAsync(h_scal.data(), d_scal.p, (size_t)G * 64, hipMemcpyDeviceToHost, st));
     BCHK(hipStreamSynchronize(st));
-    for (int k = 0; k < 4; k++) BCHK(hipEventElapsedTime(&kms[k], ev[k], ev[k + 1]));
+    for (int k = 0; k < NK; k++) BCHK(hipEventElapsedTime(&kms[k], ev[k], ev[k + 1]));
     int64_t tot = 0;
     for (int g = 0; g < G; g++) {
       if (h_scal[(size_t)g * 8 + 6])
@@ -1143,10 +1384,24 @@ int hge_batch_results(hge_batch* b, int32_t g, int32_t* order, int64_t* counts, 
   BGUARD_END(b)
 }
 
-int hge_batch_kernel_ms(hge_batch* b, float* ms4) {
-  if (!b || !ms4) return HGE_ERR_ARG;
-  for (int k = 0; k < 4; k++) ms4[k] = b->kms[k];
-  return HGE_OK;
+int hge_batch_kernel_ms(hge_batch* b, float* ms, int32_t cap) {
+  if (!b || (!ms && cap > 0)) return HGE_ERR_ARG;
+  for (int k = 0; k < hge_batch::NK && k < cap; k++) ms[k] = b->kms[k];
+  return hge_batch::NK;
 }
 
 }  // extern "C"
+
+// diagnostics (not part of the C ABI): graph g's lastAncestors (which 0) or
+// firstDescendants (which 1) rows after a run, E x N int32 into out
+extern "C" int hgb_debug_rows(hge_batch* b, int32_t g, int32_t which, int32_t* out) {
+  if (!b || !out || g < 0 || g >= (int)b->gs.size() || !b->ran) return HGE_ERR_ARG;
+  BGUARD_BEGIN
+  const GDesc& d = b->hd[g];
+  if (which == 2)  // the run layout FDT[j][c][p], N x N x ccap
+    b->down(out, b->d_FDT.p + (size_t)g * b->N * b->N * b->ccap, (size_t)b->N * b->N * b->ccap);
+  else
+    b->down(out, (which ? b->d_FD.p : b->d_LA.p) + d.eo * b->N, (size_t)d.E * b->N);
+  return HGE_OK;
+  BGUARD_END(b)
+}

@@ -119,7 +119,8 @@ __global__ void __launch_bounds__(256) k_la_sweep(Tables t, const int2* segs, in
 }
 
 // ---------------------------------------------------------------------------
-// Packed 16-bit sweeps (N > 32, where chains are capped at 65,534 events):
+// Packed 16-bit sweeps (N > 32 while every chain holds at most 65,534 events; past
+// that the engine switches to the int32 tables for good, hge_wide32.hip):
 // the fixed-point sweeps run on LA16, a table of (LA + 1) as uint16 pairs
 // (NW2 = ceil(N / 2) words per row, -1 -> 0), so every sweep streams half the
 // bytes of the int32 sweep; k_la16_rows_runs then writes the int32 LA rows and

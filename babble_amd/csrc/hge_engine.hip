@@ -594,6 +594,15 @@ struct hge_engine {
     }
     if (known >= chain_limit) {
       if (N > 32 && N <= 256 && !wide32) {  // past the uint16 positions: int32 from here on
+        // the int32 LA and LAT tables must fit beside what is allocated: else refuse
+        // the event here (the stream stops, as at any rejection) rather than lift
+        // the cap and fail at the next coordinate step
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+            free_b < 2 * sizeof(int32_t) * (size_t)N * N * (size_t)std::max(ccap, known + 2) + (64u << 20)) {
+          err = "Chain capacity exceeded: the int32 position tables past 65,534 events per creator do not fit";
+          return HGE_ERR_CAPACITY;
+        }
         wide32_pending = true;
         chain_limit = INT32_MAX;
       } else {
@@ -1159,8 +1168,10 @@ struct hge_engine {
     }
     int maxlen = 0;
     for (int c = 0; c < N; c++) maxlen = std::max(maxlen, chain_len[c]);
+    // admission switches the engine to int32 positions (to_wide32) before a chain
+    // passes 65,534 events, so this packed walk never sees one; the check guards it
     if (maxlen >= 0xFFFF)
-      throw EngineError(HGE_ERR_CAPACITY, "wide rounds: chain longer than 65534 events");
+      throw EngineError(HGE_ERR_INTERNAL, "packed rounds walk reached a chain past 65,534 events");
     s_bar.need(2);
     s_gran.need(2 * (size_t)N);
     HIPCHK(hipMemsetAsync(s_bar.p, 0, 8, st));
@@ -1282,13 +1293,17 @@ struct hge_engine {
   // the switch to int32 positions (hge_wide32.hip): the int32 LA rows of every event
   // with coordinates, unpacked from LA16; from here on the N <= 32 sweeps and
   // transposes, k_round_step32 and k_seg_theta32 take the wide path's place
+  // Runs at the next coordinate step after admission lifted the cap.  The pending
+  // flag is cleared only once the int32 tables exist: a failed allocation leaves the
+  // engine refusing every later step (the packed tables can no longer hold the
+  // positions) instead of packing positions past 65,534 into uint16.
   void to_wide32() {
-    wide32_pending = false;
     grow_chain_table(d_LA, ccap, false);
     grow_chain_table(d_LAT, ccap, false, false);
     s_w32.need(N);
     h2d(s_w32.p, coords_len.data(), 4 * (size_t)N);
     wide32 = true;
+    wide32_pending = false;
     Tables t = tables();
     int64_t most = 1;
     for (int c = 0; c < N; c++) most = std::max<int64_t>(most, (int64_t)coords_len[c] * N);

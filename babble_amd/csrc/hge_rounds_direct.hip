@@ -27,7 +27,9 @@
 // hge_rounds_coop.hip (8-byte {epoch, value} granules, relaxed agent-scope
 // stores and loads, double-buffered by round parity; cdna_hip_programming.md
 // Guideline 16, R2).  Chain positions must fit uint16 with room for the +2
-// encoding: chains are capped at 65,534 events at admission.
+// encoding: the engine runs this kernel only while every chain holds at most
+// 65,534 events; a longer chain switches it to int32 positions for good
+// (hge_wide32.hip, k_round_step32).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

@@ -230,7 +230,7 @@ def lib():
     L.hge_batch_info.argtypes = [vp, i32, P(i64)]
     L.hge_batch_results.argtypes = [vp, i32, P(i32), P(i64), P(i32), P(ctypes.c_uint8), P(i32), P(i64),
                                     P(ctypes.c_int8), P(i32)]
-    L.hge_batch_kernel_ms.argtypes = [vp, P(ctypes.c_float)]
+    L.hge_batch_kernel_ms.argtypes = [vp, P(ctypes.c_float), i32]
     _lib = L
     return L
 
@@ -914,10 +914,15 @@ class Batch:
         keys = ("events", "calls", "rounds", "lcr", "lcre", "transactions", "ordered", "undetermined")
         return dict(zip(keys, a.tolist()))
 
+    KERNELS = ("kb_coords", "kb_fd", "kb_fdrows", "kb_rounds", "kb_consensus")
+
     def kernel_ms(self):
-        a = (ctypes.c_float * 4)()
-        self._check(self.L.hge_batch_kernel_ms(self.h, a))
-        return dict(zip(("kb_coords", "kb_fd", "kb_rounds", "kb_consensus"), [float(v) for v in a]))
+        """Device ms of the last run's stages (HIP events between the launches)."""
+        a = (ctypes.c_float * 8)()
+        n = self.L.hge_batch_kernel_ms(self.h, a, 8)
+        if n < 0:
+            self._check(n)
+        return dict(zip(self.KERNELS, [float(a[k]) for k in range(n)]))
 
     def state(self, g):
         """Graph g's state: the fields of tests/golden/digest.py (status, order, counts,

@@ -13,9 +13,9 @@ Workloads (BASELINE.json configs):
       hashgraphs with simulated Byzantine forkers (10 of 32 creators fork with
       p=0.05; half of the fork twins get events built on them, which are
       rejected in cascade), 10k submissions each, K=32; the batch is split
-      across ranks.
-      Every graph has its own engine (HIP stream); host threads drive them
-      concurrently.
+      across ranks.  One step = one replay of every graph of the rank's share
+      on the batch engine (hge_batch_*: four launches for the whole batch, the
+      graphs' call schedules inside the consensus kernel).
 
 Multi-GPU (torch.distributed over RCCL, one process per GPU):
   gossip (default): ONE hashgraph sharded by time across the ranks
@@ -48,7 +48,6 @@ import os
 import platform
 import sys
 import time
-from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -267,6 +266,152 @@ def small_replay(n, E, K, seed, device, steps=20):
                        else "MISMATCH vs CPU oracle")}
 
 
+MC_KERNEL_BYTES = {  # algorithmic bytes per event (kb_consensus: per ordered event), SURVEY 8(d)
+    "kb_coords": lambda n: 4 * n + 16,  # the LA row written, the parents' creator / index / ids read
+    "kb_fd": lambda n: 8 * n,           # the LA row read, its firstDescendant runs written
+    "kb_fdrows": lambda n: 8 * n,       # the runs read, the firstDescendant row written
+    "kb_rounds": lambda n: 8 * n,       # the LA and FD rows read once (strongly-see counts, witness rows)
+    "kb_consensus": lambda n: 4 * n + 48,  # the median's rows and the sort key
+}
+
+
+def mc_main(args, n, E, K, rank, world, local_rank, dist):
+    """Config 5 on the batch engine: this rank's share of the Monte Carlo batch,
+    one replay of all of it per step (four launches), every graph checked
+    against the oracle's committed full-state digest."""
+    from babble_amd.dist import reduce_step, shard_range
+    from babble_amd.engine import Batch
+    from babble_amd.gossip import random_gossip, schedule
+    first, per = shard_range(args.graphs, world, rank)
+    t0 = time.perf_counter()
+    dags = [random_gossip(n, E, seed=args.seed + first + g, forkers=10, fork_p=0.05, cascade_p=0.5)
+            for g in range(per)]
+    batch = Batch(n, device=local_rank)
+    t_adm = time.perf_counter()
+    for d in dags:
+        batch.add(d, schedule(len(d["creator"]), K))
+    batch.stage()
+    admission_s = time.perf_counter() - t_adm
+    ingest_s = time.perf_counter() - t0
+    events = sum(len(d["creator"]) for d in dags)
+
+    def sync_all():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    t_ramp = time.perf_counter()
+    while time.perf_counter() - t_ramp < args.ramp_s:
+        batch.run()
+    for _ in range(args.warmup):
+        batch.run()
+    sync_all()
+    kacc = {}
+    t0 = time.perf_counter()
+    ordered = 0
+    for _ in range(args.steps):
+        ordered = batch.run()
+        for k_, v_ in batch.kernel_ms().items():  # HIP events between the launches, on the batch stream
+            kacc[k_] = kacc.get(k_, 0.0) + v_
+    t1 = time.perf_counter()
+    sync_all()
+    step_s = (t1 - t0) / args.steps
+    kms = {k_: v_ / args.steps for k_, v_ in kacc.items()}
+    tot_ordered, max_step = ordered, step_s
+    if dist is not None:
+        max_step, tot_ordered = reduce_step(dist, step_s, ordered, f"cuda:{local_rank}")
+
+    # every graph of this rank against the oracle's full-state digest
+    checks = []
+    dg = mc_digests(n, E, K, args.seed)
+    bad, nchk = 0, 0
+    if dg is not None:
+        sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+        from digest import digest
+        for g in range(per):
+            gi = first + g
+            if gi >= len(dg):
+                continue
+            nchk += 1
+            bad += digest(batch.state(g)) != dg[gi]
+    if dist is not None:
+        import torch
+        t_ = torch.tensor([nchk, bad], dtype=torch.int64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t_)
+        nchk, bad = int(t_[0].item()), int(t_[1].item())
+    if nchk:
+        checks.append(f"{'bit-exact' if bad == 0 else f'MISMATCH on {bad} graphs'} vs the oracle's "
+                      f"full-state digests on {nchk} of {args.graphs} graphs (status, order, batches, rounds, "
+                      f"witnesses, fame, round received, timestamps, undetermined, scalars; "
+                      f"tests/golden/mc_*_digests.json)")
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        # the Go-faithful oracle on whole graphs of the batch, one core, ~10 s of work
+        from oracle.oracle import replay as oracle_replay
+        tc = time.perf_counter()
+        tot, ng = 0, 0
+        for d in dags:
+            _, _, corder, _ = oracle_replay(d, schedule(len(d["creator"]), K))
+            tot += len(corder)
+            ng += 1
+            if time.perf_counter() - tc > 10.0:
+                break
+        cs = time.perf_counter() - tc
+        cpu = {"value": round(tot / cs, 1), "unit": "events/s", "cores": 1, "kind": "port",
+               "sample": f"Go-faithful C++ oracle (oracle/hg_oracle.cpp, faithful mode), the first {ng} graphs "
+                         f"of the batch (whole graphs, K={K}), {tot} ordered in {cs:.2f} s on "
+                         f"{platform.processor() or platform.machine()} (host nproc {os.cpu_count()})"}
+    if rank != 0:
+        batch.close()
+        return
+    value = tot_ordered / max_step
+    dom = max(kms, key=kms.get)
+    per_unit = MC_KERNEL_BYTES[dom](n)
+    units = ordered if dom == "kb_consensus" else events
+    alg = per_unit * units
+    achieved = alg / (kms[dom] * 1e-3) / 1e9
+    hbm = {k_: {"ms": round(v_, 4), "alg_bytes": MC_KERNEL_BYTES[k_](n) * (ordered if k_ == "kb_consensus"
+                                                                         else events),
+                "achieved_gbs": round(MC_KERNEL_BYTES[k_](n) * (ordered if k_ == "kb_consensus" else events)
+                                      / (v_ * 1e-3) / 1e9, 2)} for k_, v_ in kms.items()}
+    line = {
+        "metric": "consensus-ordered events/sec at N participants",
+        "value": round(value, 1),
+        "unit": "events/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(max_step * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic",
+        "config": {"workload": (f"Monte Carlo batch: {args.graphs} independent random-gossip hashgraphs, "
+                                f"{n} participants, {E} submissions each, 10 forkers p=0.05 with cascades, "
+                                f"RunConsensus every K={K}"),
+                   "participants": n, "events_per_graph": E, "k": K, "graphs_per_gpu": per,
+                   "ordered_per_step": tot_ordered,
+                   "parallelism": f"replicas{world}: the batch split across {world} GPUs, no collective"},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "algorithmic_bytes_per_launch": int(alg), "launch_ms": round(kms[dom], 4),
+                     "hbm_kernels": hbm,
+                     "path": {"bytes_per_event": 24 * n + 48,
+                              "achieved_gbs": round(value / world * (24 * n + 48) / 1e9, 2),
+                              "frac": round(value / world * (24 * n + 48) / 1e9 / HBM_PEAK_GBS, 5)}},
+        "cpu_baseline": cpu,
+        "parity": "; ".join(checks) if checks else None,
+        "ingest_host_ms": round(ingest_s * 1e3, 2),
+        "admission_ms": round(admission_s * 1e3, 2),
+        "kernels_ms_per_replay": {k_: round(v_, 4) for k_, v_ in sorted(kms.items(), key=lambda kv: -kv[1])},
+        "kernel_launches_per_replay": {k_: 1 for k_ in kms},
+    }
+    print(json.dumps(line), flush=True)
+    batch.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -279,8 +424,6 @@ def main():
     ap.add_argument("--events", type=int, default=None)
     ap.add_argument("--k", type=int, default=None, help="RunConsensus every k submissions")
     ap.add_argument("--graphs", type=int, default=1024, help="mc: hashgraphs in the whole batch")
-    ap.add_argument("--threads", type=int, default=16,
-                    help="mc: host threads driving engines (the box's CPU share per GPU; 4 / 8 / 16 threads: 44.3 / 53.1 / 58.3M ev/s, profiles/r03/configs/mc_threads)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
@@ -314,34 +457,29 @@ def main():
         dist_.init_process_group(args.dist_backend)
         dist = dist_
 
-    from babble_amd.dist import reduce_step, shard_range
+    if mc:
+        mc_main(args, n, E, K, rank, world, local_rank, dist)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    from babble_amd.dist import reduce_step
     from babble_amd.engine import Engine, events_array
     from babble_amd.gossip import random_gossip, schedule
 
     # ---- stage the workload in HBM (host admission + upload; not timed) ----
     t0 = time.perf_counter()
-    admission_s = None
-    if mc:
-        first, per = shard_range(args.graphs, world, rank)
-        dags = [random_gossip(n, E, seed=args.seed + first + g, forkers=10, fork_p=0.05, cascade_p=0.5)
-                for g in range(per)]
-        engines = [Engine(n, len(d["creator"]) + 64, device=local_rank) for d in dags]
-        for eng, d in zip(engines, dags):
-            eng.prepare(events_array(d), schedule(len(d["creator"]), K))
-    else:
-        split = not args.replicas and world > 1
-        # split: every rank stages the same stream (seed, not seed + rank)
-        dags = [random_gossip(n, E, seed=args.seed + (0 if split else rank))]
-        engines = [Engine(n, E, device=local_rank)]
-        ev0 = events_array(dags[0])
-        t_adm = time.perf_counter()
-        engines[0].prepare(ev0, schedule(E, K))
-        admission_s = time.perf_counter() - t_adm
-        del ev0
+    split = not args.replicas and world > 1
+    # split: every rank stages the same stream (seed, not seed + rank)
+    dags = [random_gossip(n, E, seed=args.seed + (0 if split else rank))]
+    engines = [Engine(n, E, device=local_rank)]
+    ev0 = events_array(dags[0])
+    t_adm = time.perf_counter()
+    engines[0].prepare(ev0, schedule(E, K))
+    admission_s = time.perf_counter() - t_adm
+    del ev0
     ingest_s = time.perf_counter() - t0
-    pool = ThreadPoolExecutor(max_workers=max(1, min(args.threads, len(engines))))
 
-    split = (not mc) and not args.replicas and world > 1
     gather, exchange, split_stats = None, None, {}
     if split:
         from babble_amd.dist import TorchExchange, split_run, torch_gather, walk_split_run
@@ -353,9 +491,7 @@ def main():
             return walk_split_run(engines[0], rank, world, gather)
         if split:
             return split_run(engines[0], rank, world, exchange, stats=split_stats)
-        if len(engines) == 1:
-            return engines[0].run()
-        return sum(pool.map(lambda e: e.run(), engines))
+        return engines[0].run()
 
     def sync_all():
         if dist is not None:
@@ -440,31 +576,7 @@ def main():
                                  "launches_per_replay": lpr}
 
     cpu, parity, checks = None, None, []
-    if mc:
-        # every graph of this rank against the oracle's full-state digest
-        # (tests/golden/make_mc_digests.py): order, batches, rounds, witnesses,
-        # fame, round received, timestamps, undetermined list, scalars
-        dg = mc_digests(n, E, K, args.seed)
-        bad, nchk = 0, 0
-        if dg is not None:
-            from digest import digest, engine_state
-            for g, eng in enumerate(engines):
-                gi = first + g
-                if gi >= len(dg):
-                    continue
-                st_, ord_, cnt_ = eng.fetch()
-                nchk += 1
-                bad += digest(engine_state(eng, st_, ord_, cnt_)) != dg[gi]
-        if dist is not None:
-            import torch
-            t_ = torch.tensor([nchk, bad], dtype=torch.int64, device=f"cuda:{local_rank}")
-            dist.all_reduce(t_)
-            nchk, bad = int(t_[0].item()), int(t_[1].item())
-        if nchk:
-            checks.append(f"{'bit-exact' if bad == 0 else f'MISMATCH on {bad} graphs'} vs the oracle's "
-                          f"full-state digests on {nchk} of {args.graphs} graphs (order, batches, rounds, "
-                          f"witnesses, fame, round received, timestamps; tests/golden/mc_*_digests.json)")
-    if rank == 0 and not mc:
+    if rank == 0:
         gp = golden_prefix(n, E, K, args.seed)
         if gp is not None:
             sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -494,23 +606,7 @@ def main():
             checks.append(f"{'bit-exact' if not bad else 'MISMATCH in ' + ','.join(bad)} vs the oracle's "
                           f"whole-stream digests ({what}; all {gf['n_calls']} calls, {gf['ordered']} ordered, "
                           f"{gf['scalars'][0]} rounds, LCR {gf['scalars'][1]})")
-    if rank == 0 and not args.no_cpu_baseline and mc:
-        # the oracle on whole graphs of the batch, one core, until ~10 s of work
-        from oracle.oracle import replay as oracle_replay
-        t0 = time.perf_counter()
-        tot, ng = 0, 0
-        for d in dags:
-            _, _, corder, _ = oracle_replay(d, schedule(len(d["creator"]), K))
-            tot += len(corder)
-            ng += 1
-            if time.perf_counter() - t0 > 10.0:
-                break
-        cs = time.perf_counter() - t0
-        cpu = {"value": round(tot / cs, 1), "unit": "events/s", "cores": 1, "kind": "port",
-               "sample": f"Go-faithful C++ oracle (oracle/hg_oracle.cpp), the first {ng} graphs of the batch "
-                         f"(whole graphs, K={K}), {tot} ordered in {cs:.2f} s on "
-                         f"{platform.processor() or platform.machine()} (host nproc {os.cpu_count()})"}
-    elif rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         from oracle.oracle import replay as oracle_replay
         d = dags[0]
         ns = args.cpu_sample_events or (20480 if n >= 128 else 100_000)
@@ -548,7 +644,7 @@ def main():
             "workload": f"{world} independent replays of the same stream, one per GPU (no collective)",
             "value": round(rep_tot / rep_step, 1), "unit": "events/s", "ms_per_step": round(rep_step * 1e3, 4),
             "scaling": "weak"}}
-    if (rank == 0 and not mc and not args.no_secondary and (n, E) == DEFAULT and world == 1):
+    if rank == 0 and not args.no_secondary and (n, E) == DEFAULT and world == 1:
         secondary = {"replay_16_100k": small_replay(16, 100_000, 16, args.seed, local_rank),
                      "online_16_100k": online_path(16, 100_000, 16, args.seed, local_rank),
                      "online_64_1m": online_path(64, 1_000_000, 64, args.seed, local_rank),
@@ -561,14 +657,9 @@ def main():
 
     if rank == 0:
         value = tot_ordered / max_step
-        if mc:
-            workload = (f"Monte Carlo batch: {args.graphs} independent random-gossip hashgraphs, "
-                        f"{n} participants, {E} submissions each, 10 forkers p=0.05 with cascades, "
-                        f"RunConsensus every K={K}")
-        else:
-            workload = (f"random-gossip DAG, {n} participants, {E} events "
-                        f"{'in one hashgraph' if split else 'per GPU'}, "
-                        f"RunConsensus every K={K} events ({len(schedule(E, K))} calls)")
+        workload = (f"random-gossip DAG, {n} participants, {E} events "
+                    f"{'in one hashgraph' if split else 'per GPU'}, "
+                    f"RunConsensus every K={K} events ({len(schedule(E, K))} calls)")
         cfg_key = f"{args.workload}_n{n}_e{E}_k{K}"
         line = {
             "metric": "consensus-ordered events/sec at N participants",
@@ -584,7 +675,7 @@ def main():
             "dtype": "int32",
             "data": "synthetic",
             "config": {"workload": workload, "participants": n, "events_per_graph": E, "k": K,
-                       "graphs_per_gpu": len(engines), "ordered_per_step": tot_ordered,
+                       "graphs_per_gpu": 1, "ordered_per_step": tot_ordered,
                        "parallelism": ((f"split{world}: one hashgraph, rounds walk split across {world} GPUs"
                                         if args.walk_only else
                                         f"shard{world}: one hashgraph sharded by time across {world} GPUs "
@@ -621,7 +712,6 @@ def main():
         if secondary is not None:
             line["secondary"] = secondary
         print(json.dumps(line), flush=True)
-    pool.shutdown()
     for e in engines:
         e.close()
     if os.environ.get("HGE_DUMP_MAPS"):

@@ -187,8 +187,9 @@ int hge_batch_info(hge_batch* b, int32_t g, int64_t* info);
  * undecided, 1 famous, 2 not famous) and the undetermined list. */
 int hge_batch_results(hge_batch* b, int32_t g, int32_t* order, int64_t* counts, int32_t* round, uint8_t* witness,
                       int32_t* rr, int64_t* cts, int8_t* fame, int32_t* undetermined);
-/* device ms of the last run's stages: coordinates, firstDescendants, rounds, consensus */
-int hge_batch_kernel_ms(hge_batch* b, float* ms4);
+/* device ms of the last run's stages (HIP events between the launches): coordinates,
+ * firstDescendant runs, firstDescendant rows, rounds, consensus; returns the count */
+int hge_batch_kernel_ms(hge_batch* b, float* ms, int32_t cap);
 
 /* ---- one hashgraph split across GPUs (babble_amd/dist.py) ------ */
 /* Sharded replay.  Every rank stages the whole stream (hge_replay_prepare) and

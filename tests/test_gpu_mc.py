@@ -1,7 +1,8 @@
 """Config 5 on the GPU: many independent 32-participant hashgraphs with
-Byzantine forkers (and fork cascades), one engine (HIP stream) each, driven
-concurrently by host threads on one device -- the shape bench.py --workload mc
-times.  Every graph is compared bit-exact with the oracle."""
+Byzantine forkers (and fork cascades).  The batch engine (hge_batch_*, what
+bench.py --workload mc times) replays all 1,024 graphs of the bench's batch and
+every graph's full state must equal the oracle's committed digest; the
+single-graph engines, driven by host threads, are checked on a smaller batch."""
 import json
 import os
 import sys
@@ -48,9 +49,43 @@ def test_monte_carlo_batch_threads():
             e.close()
 
 
+def test_monte_carlo_config5_batch_all_digests():
+    """Config 5 at its stated size on the batch engine: all 1,024 graphs x 10k
+    submissions of bench.py --workload mc in one batch, each graph's FULL state
+    (status, order, batches, rounds, witnesses, fame, round received, timestamps,
+    undetermined list, scalars) against the oracle digests committed in
+    tests/golden/mc_n32_e10000_k32_digests.json, and 8 graphs against the oracle
+    run live, field by field."""
+    from babble_amd.engine import Batch
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    sys.path.insert(0, here)
+    from digest import digest, first_difference
+    from make_mc_digests import OUT, graph_stream, oracle_state
+    ref = json.load(open(OUT))
+    graphs = ref["graphs"]
+    assert graphs == 1024
+    streams = [graph_stream(g) for g in range(graphs)]
+    b = Batch(32)
+    try:
+        for d, calls in streams:
+            b.add(d, calls)
+        tot = b.run()
+        got = [b.state(g) for g in range(graphs)]
+        bad = [g for g in range(graphs) if digest(got[g]) != ref["digests"][g]]
+        assert not bad, f"graphs differing from the oracle digests: {bad[:16]}"
+        assert tot == sum(ref["ordered"])
+        assert sum(int((s["status"] < 0).sum()) for s in got) == sum(ref["rejected"])
+        with ThreadPoolExecutor(8) as pool:
+            live = list(pool.map(lambda g: oracle_state(*streams[g]), range(0, graphs, graphs // 8)))
+        for j, g in enumerate(range(0, graphs, graphs // 8)):
+            assert first_difference(got[g], live[j]) is None, f"graph {g}: {first_difference(got[g], live[j])}"
+    finally:
+        b.close()
+
+
 def test_monte_carlo_config5_size():
-    """Config 5 at its stated size: 256 of the batch's 1024 graphs x 10k
-    submissions (graphs 0-255 of bench.py --workload mc), 8 host threads, each
+    """Config 5's graphs on the single-graph engines: 256 of the batch's 1024 graphs
+    x 10k submissions (graphs 0-255 of bench.py --workload mc), 8 host threads, each
     graph's FULL state (order, batches, rounds, witnesses, fame, round received,
     timestamps, undetermined list, scalars) against the oracle digests committed
     in tests/golden/mc_n32_e10000_k32_digests.json, and 8 graphs also against the
