@@ -37,6 +37,8 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -71,7 +73,9 @@ struct BT {
   const int64_t* calls;  // accepted-event count at each call point
   int32_t* LA;           // [eo + x][N] lastAncestors (positions; -1 none)
   int32_t* FDT;          // [g][j][c][ccap] firstDescendants in run layout (INF none)
-  int32_t* FD;           // [eo + x][N] firstDescendants rows (positions; INF none)
+  int32_t* FD;           // [g][c][p][N] firstDescendants rows of chain positions (INF none)
+  const uint64_t* Sch;   // [g][c][p] limb 0 of S in chain layout (the sort key)
+  const int32_t* ntxch;  // [g][c][p] transaction counts in chain layout
   int32_t* round;
   uint8_t* wit;
   int32_t* rr;
@@ -90,6 +94,7 @@ struct BT {
   int64_t* kct;
   uint64_t* ks0;
   int32_t* kid;
+  uint64_t* dbg;               // diagnostics: per-graph section cycles (null: off)
 };
 
 __device__ __forceinline__ int rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -184,67 +189,67 @@ __global__ __launch_bounds__(64) void kb_coords(BT t) {
 // firstDescendants in run layout (UpdateAncestorFirstDescendant, hashgraph.go:466-494):
 // chain-j event k is the first chain-j descendant of the chain-c positions
 // (LA[(j,k-1)][c], LA[(j,k)][c]]; positions no chain-j event sees keep INF
-// (MaxInt64).  Lane c walks chain j (N <= 32: lanes 32-63 walk chain j + 1), 64
-// rows at a time with the next 64 rows' loads in flight.
+// (MaxInt64).  Lane r holds row k0 + r of chain j (all N columns, registers); for
+// each column c the 64 rows' runs tile one contiguous range of chain c's positions,
+// so the stores of a column are contiguous across the lanes.  The next 64 rows'
+// loads are in flight meanwhile.
 template <int NM>
-__global__ __launch_bounds__(64) void kb_fd(BT t) {
-  constexpr int HALVES = NM == 32 ? 2 : 1;
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void kb_fd(BT t) {
   const int g = blockIdx.x;
   const GDesc d = t.gd[g];
   const int N = t.N, cc = t.ccap, lane = threadIdx.x;
-  const int c = NM == 32 ? (lane & 31) : lane, h = NM == 32 ? (lane >> 5) : 0;
   const int32_t* LA = t.LA + d.eo * N;
-  const int lenc = c < N ? t.clen[g * N + c] : 0;
-  for (int j0 = 0; j0 < N; j0 += HALVES) {
-    const int j = j0 + h;
-    const bool jon = j < N;           // the half has a chain (its lanes load the chain's ids)
-    const bool on = c < N && jon;     // the lane has a column too
-    const int lenj = jon ? t.clen[g * N + j] : 0;
-    const int lmax = max(rl(lenj, 0), HALVES == 2 ? rl(lenj, 32) : 0);
-    const int32_t* ch = t.chain + ((int64_t)g * N + (jon ? j : 0)) * cc;
-    int32_t* out = t.FDT + (((int64_t)g * N + (on ? j : 0)) * N + c) * cc;
-    int prev = -1;
-    constexpr int CH = 64 / HALVES;  // rows per chunk and half
-    // lane (h, i) holds the id of row base + i of its half's chain; the LA values of
-    // the CH rows are loaded one chunk ahead
-    const int sub = NM == 32 ? (lane & 31) : lane;
-    int idc = jon && sub < lenj ? ch[sub] : 0;
-    int cur[CH], nxt[CH];
+  const int lenc = lane < N ? t.clen[g * N + lane] : 0;  // lane c's chain length (the INF tails)
+  for (int j = 0; j < N; j++) {
+    const int lenj = t.clen[g * N + j];
+    const int32_t* ch = t.chain + ((int64_t)g * N + j) * cc;
+    int32_t* outj = t.FDT + ((int64_t)g * N + j) * N * cc;  // + c * cc + p
+    int row[NM], nrow[NM];
+    int carry[NM];  // the last row's value of column c before the chunk (uniform)
 #pragma unroll
-    for (int u = 0; u < CH; u++) {
-      const int x = HALVES == 2 ? (h ? rl(idc, 32 + u) : rl(idc, u)) : rl(idc, u);
-      cur[u] = on && u < lenj ? LA[(int64_t)x * N + c] : -1;
-    }
-    for (int base = 0; base < lmax; base += CH) {
-      const bool more = base + CH < lmax;
-      if (more) {
-        const int idn = jon && base + CH + sub < lenj ? ch[base + CH + sub] : 0;
+    for (int c = 0; c < NM; c++) carry[c] = -1;
+    auto load = [&](int k0, int (&v)[NM]) {
+      const bool ok = k0 + lane < lenj;
+      const int x = ok ? ch[k0 + lane] : 0;
 #pragma unroll
-        for (int u = 0; u < CH; u++) {
-          const int x = HALVES == 2 ? (h ? rl(idn, 32 + u) : rl(idn, u)) : rl(idn, u);
-          nxt[u] = on && base + CH + u < lenj ? LA[(int64_t)x * N + c] : -1;
-        }
-      }
+      for (int c = 0; c < NM; c++) v[c] = ok && c < N ? LA[(int64_t)x * N + c] : -1;
+    };
+    if (lenj > 0) load(0, row);
+    for (int k0 = 0; k0 < lenj; k0 += 64) {
+      const bool more = k0 + 64 < lenj;
+      if (more) load(k0 + 64, nrow);
+      const bool ok = k0 + lane < lenj;
+      const int last = min(64, lenj - k0) - 1;  // the chunk's last valid lane
 #pragma unroll
-      for (int u = 0; u < CH; u++) {
-        if (on && base + u < lenj) {
-          const int v = cur[u];
-          for (int p = prev + 1; p <= v; p++) out[p] = base + u;
-          prev = max(prev, v);
+      for (int c = 0; c < NM; c++) {
+        if (c < N) {
+          const int up = __shfl_up(row[c], 1);
+          const int a = lane == 0 ? carry[c] : up;  // positions (a, b] take k0 + lane
+          const int b = ok ? row[c] : a;
+          int32_t* out = outj + (int64_t)c * cc;
+          for (int p = a + 1; p <= b; p++) out[p] = k0 + lane;
+          carry[c] = rl(row[c], last);
         }
       }
       if (more) {
 #pragma unroll
-        for (int u = 0; u < CH; u++) cur[u] = nxt[u];
+        for (int c = 0; c < NM; c++) row[c] = nrow[c];
       }
     }
-    if (on)
-      for (int p = prev + 1; p < lenc; p++) out[p] = INF;
+    // chain c's positions no chain-j event sees: one coalesced sweep per column
+#pragma unroll
+    for (int c = 0; c < NM; c++) {
+      if (c < N) {
+        const int lc = rl(lenc, c);
+        int32_t* out = outj + (int64_t)c * cc;
+        for (int p = carry[c] + 1 + lane; p < lc; p += 64) out[p] = INF;
+      }
+    }
   }
 }
 
-// firstDescendants as event rows: FD[eo + (c, p)][j] = FDT[j][c][p], through an LDS
-// tile of 64 positions x N chains per step.  One workgroup per (graph, chain c).
+// firstDescendants as rows in chain layout: FD[g][c][p][j] = FDT[j][c][p], through an
+// LDS tile of 64 positions x N chains per step.  One workgroup per (graph, chain c).
 template <int NM>
 __global__ __launch_bounds__(256) void kb_fdrows(BT t) {
   const int g = blockIdx.x / t.N, c = blockIdx.x % t.N;
@@ -261,7 +266,7 @@ __global__ __launch_bounds__(256) void kb_fdrows(BT t) {
     __syncthreads();
     for (int e = tid; e < N * 64; e += 256) {  // write event rows
       const int p = e / N, j = e % N;
-      if (p0 + p < len) t.FD[(d.eo + ch[p0 + p]) * N + j] = tile[j][p];
+      if (p0 + p < len) t.FD[(((int64_t)g * N + c) * cc + p0 + p) * N + j] = tile[j][p];
     }
     __syncthreads();
   }
@@ -295,7 +300,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   if (k < RING) wpres[k] = 0;
   __syncthreads();
   const int32_t* LA = t.LA + d.eo * N;
-  const int32_t* FD = t.FD + d.eo * N;
+  const int32_t* FDg = t.FD + (int64_t)g * N * t.ccap * N;  // [c][p][N]
   int top = -1;   // highest round with a ring slot
   int maxr = -1;  // highest round so far (Rounds() - 1)
   int err = 0;
@@ -328,13 +333,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
   // chunk loads: element e = k + 64 v of the chunk's CH x N row block
   int rla[PER], rfd[PER], mcr, mix, msp, mop, moc, mco;
   auto load = [&](int base) {
-#pragma unroll
-    for (int v = 0; v < PER; v++) {
-      const int e = k + 64 * v, row = e / NM, col = e % NM;
-      const bool on = col < N && base + row < d.E;
-      rla[v] = on ? LA[(int64_t)(base + row) * N + col] : -1;
-      rfd[v] = on ? FD[(int64_t)(base + row) * N + col] : INF;
-    }
     const int i = base + k;
     const bool on = k < CH && i < d.E;
     mcr = on ? t.cr[d.eo + i] : 0;
@@ -343,6 +341,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     mop = on ? t.op[d.eo + i] : -1;
     moc = on ? t.oc[d.eo + i] : 0;
     mco = on ? t.coin[d.eo + i] : 0;
+#pragma unroll
+    for (int v = 0; v < PER; v++) {
+      const int e = k + 64 * v, row = e / NM, col = e % NM;
+      const bool ok = col < N && base + row < d.E;
+      const int rcr = __shfl(mcr, row), rix = __shfl(mix, row);  // the row's chain position
+      rla[v] = ok ? LA[(int64_t)(base + row) * N + col] : -1;
+      rfd[v] = ok ? FDg[((int64_t)rcr * t.ccap + rix) * N + col] : INF;
+    }
   };
   load(0);
   for (int base = 0; base < d.E && !err; base += CH) {
@@ -542,28 +548,38 @@ __device__ __forceinline__ void sort_regs(int64_t (&v)[M]) {
 // past UL entries live in global memory, where every mutation is also written.
 template <int NM>
 __global__ __launch_bounds__(64) void kb_consensus(BT t) {
-  constexpr int RW = 16, UL = 768, KB = 256;
+  constexpr int RW = 8, UL = 1536, KB = 768;
   const int g = blockIdx.x;
   const GDesc d = t.gd[g];
   const int N = t.N, SM = t.SM, lane = threadIdx.x, cc = t.ccap;
   const int64_t eo = d.eo;
   const int32_t* LA = t.LA + eo * N;
-  const int32_t* FD = t.FD + eo * N;
+  const int32_t* FDg = t.FD + (int64_t)g * N * cc * N;  // [c][p][N]
   const int64_t* tschg = t.tsch + (int64_t)g * N * cc;
   __shared__ int32_t wid[RW][NM], wix[RW][NM], thL[RW][NM];
   __shared__ uint64_t ssbL[RW][NM], seebL[RW][NM];
   __shared__ uint64_t coinL[RW], fmL[RW];
   __shared__ int8_t fameL[RW][NM];
   __shared__ int32_t rcntL[RW], verL[RW], thvL[RW];
-  __shared__ int32_t Uid_s[UL], Ur_s[UL], Ucp_s[UL];
+  // the undetermined list: creator << 24 | index, and round (the id is chain[c][index])
+  __shared__ int32_t Ur_s[UL], Ucp_s[UL];
   __shared__ int32_t kr[KB], ki[KB];
   __shared__ int64_t kc[KB];
   __shared__ uint64_t ks[KB];
   if (t.scal[(int64_t)g * 8 + 6]) return;  // the rounds pass failed: nothing to decide
   int R = 0, lcr = -1, lcre = 0, nord = 0, nU = 0, n_prev = 0;
   int64_t ctx = 0;
+  uint64_t cyc[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t t0_ = t.dbg ? __builtin_amdgcn_s_memtime() : 0;
+#define HGB_STAMP(i)                                      \
+  if (t.dbg) {                                            \
+    const uint64_t t1_ = __builtin_amdgcn_s_memtime();    \
+    cyc[i] += t1_ - t0_;                                  \
+    t0_ = t1_;                                            \
+  }
   bool ug = false;  // the undetermined list lives in global memory
-  int32_t *Ug = t.U + eo, *Urg = t.Ur + eo, *Ucpg = t.Ucp + eo;
+  int32_t *Urg = t.Ur + eo, *Ucpg = t.Ucp + eo;
+  const int32_t* chg = t.chain + (int64_t)g * N * cc;  // [c][p] -> id
   auto uget = [&](const int32_t* ls, const int32_t* gs, int i) -> int { return ug ? ld(&gs[i]) : ls[i]; };
   auto uput = [&](int32_t* ls, int32_t* gs, int i, int v) {
     if (ug) st(&gs[i], v);
@@ -631,7 +647,6 @@ __global__ __launch_bounds__(64) void kb_consensus(BT t) {
       // undetermined list grows by the new events in insertion order
       if (!ug && nU + nn > UL) {  // past the LDS list: move it to global memory for good
         for (int i = lane; i < nU; i += 64) {
-          st(&Ug[i], Uid_s[i]);
           st(&Urg[i], Ur_s[i]);
           st(&Ucpg[i], Ucp_s[i]);
         }
@@ -644,7 +659,6 @@ __global__ __launch_bounds__(64) void kb_consensus(BT t) {
         const int w = b0 == n_prev ? w0 : (on ? t.wit[eo + x] : 0);
         const int cp = b0 == n_prev ? cp0 : (on ? (t.cr[eo + x] << 24 | t.ix[eo + x]) : 0);
         if (on) {
-          uput(Uid_s, Ug, nU + (x - n_prev), x);
           uput(Ur_s, Urg, nU + (x - n_prev), r);
           uput(Ucp_s, Ucpg, nU + (x - n_prev), cp);
         }
@@ -665,6 +679,7 @@ __global__ __launch_bounds__(64) void kb_consensus(BT t) {
       n_prev = n_c;
     }
     wsync();
+    HGB_STAMP(0)
     // ---- DecideFame (hashgraph.go:598-664) ----
     for (int i = lcr + 1; i < R - 1; i++) {
       const int xid = lane < N ? W_(i, lane) : -1;
@@ -725,6 +740,7 @@ __global__ __launch_bounds__(64) void kb_consensus(BT t) {
       }
       wsync();
     }
+    HGB_STAMP(1)
     // ---- DecideRoundReceived (hashgraph.go:676-721) ----
     int rmin = INF;
     for (int b0 = 0; b0 < nU; b0 += 64)
@@ -773,16 +789,17 @@ __global__ __launch_bounds__(64) void kb_consensus(BT t) {
       }
       wsync();
     }
+    HGB_STAMP(2)
     // the undetermined events in order: received ones become the call's batch (keys
     // to LDS, and to global scratch past KB), the rest stay (compacted in place)
     int nb = 0, nk = 0;
     int64_t tx = 0;
     for (int b0 = 0; b0 < nU; b0 += 64) {
       const bool on = b0 + lane < nU;
-      const int x = on ? uget(Uid_s, Ug, b0 + lane) : -1;
       const int r = on ? uget(Ur_s, Urg, b0 + lane) : 0;
       const int cp = on ? uget(Ucp_s, Ucpg, b0 + lane) : 0;
       const int cx = cp >> 24, px = cp & 0xFFFFFF;
+      int x = -1;
       int found = -1;
       if (on) {
         for (int i = r + 1; i < R; i++) {
@@ -807,8 +824,10 @@ __global__ __launch_bounds__(64) void kb_consensus(BT t) {
         // MedianTimestamp over OldestSelfAncestorToSee(w, x) of the famous witnesses w
         // that see x (hashgraph.go:704-709, 762-770), the upper median.  w = (d, i_w)
         // sees x iff FD[x][d] <= i_w, and FD[x][d] is then OldestSelfAncestorToSee
-        s0 = t.S[(eo + x) * 4];
-        tx += t.ntx[eo + x];
+        const int64_t cpos = (int64_t)cx * cc + px;
+        x = chg[cpos];
+        s0 = t.Sch[(int64_t)g * N * cc + cpos];
+        tx += t.ntxch[(int64_t)g * N * cc + cpos];
         uint64_t fm;
         if (res(found)) {
           fm = fmL[found & (RW - 1)];
@@ -822,7 +841,8 @@ __global__ __launch_bounds__(64) void kb_consensus(BT t) {
         int64_t vals[NM];
         int q[NM];
 #pragma unroll
-        for (int dd = 0; dd < NM; dd++) q[dd] = dd < N && ((fm >> dd) & 1) ? FD[(int64_t)x * N + dd] : INF;
+        for (int dd = 0; dd < NM; dd++)
+          q[dd] = dd < N && ((fm >> dd) & 1) ? FDg[((int64_t)cx * cc + px) * N + dd] : INF;
         int m = 0;
 #pragma unroll
         for (int dd = 0; dd < NM; dd++) {
@@ -860,7 +880,6 @@ __global__ __launch_bounds__(64) void kb_consensus(BT t) {
       }
       if (on && found < 0) {
         const int p = nk + __popcll(keep & below);
-        uput(Uid_s, Ug, p, x);
         uput(Ur_s, Urg, p, r);
         uput(Ucp_s, Ucpg, p, cp);
       }
@@ -870,6 +889,7 @@ __global__ __launch_bounds__(64) void kb_consensus(BT t) {
     }
     nU = nk;
     wsync();
+    HGB_STAMP(3)
     // ---- FindOrder (hashgraph.go:723-760): sort the batch, append it ----
     if (nb > 0) {
       if (nb <= KB) {
@@ -887,9 +907,16 @@ __global__ __launch_bounds__(64) void kb_consensus(BT t) {
     if (lane == 0) t.counts[d.co + c] = nb;
     nord += nb;
     wsync();
+    HGB_STAMP(4)
   }
+#undef HGB_STAMP
+  if (t.dbg && lane == 0)
+    for (int i = 0; i < 5; i++) t.dbg[(int64_t)g * 8 + i] = cyc[i];
   // the undetermined list for the host
-  for (int i = lane; i < nU; i += 64) t.U[eo + i] = uget(Uid_s, Ug, i);
+  for (int i = lane; i < nU; i += 64) {
+    const int cp = uget(Ucp_s, Ucpg, i);
+    t.U[eo + i] = chg[(int64_t)(cp >> 24) * cc + (cp & 0xFFFFFF)];
+  }
   if (lane == 0) {
     int64_t* s = t.scal + (int64_t)g * 8;
     s[0] = R;
@@ -968,9 +995,13 @@ struct hge_batch {
       d_WFD;
   Buf<int32_t> d_rcnt, d_ver, d_thv, d_th, d_U, d_Ur, d_Ucp, d_order, d_krr, d_kid;
   Buf<int64_t> d_ts, d_tsch, d_calls, d_cts, d_counts, d_scal, d_kct;
+  Buf<uint64_t> d_Sch;
+  Buf<int32_t> d_ntxch;
   Buf<uint64_t> d_S, d_ssb, d_seeb, d_ks0;
   Buf<uint8_t> d_coin, d_wit, d_WCOIN;
   Buf<int8_t> d_fame;
+  Buf<uint64_t> d_dbg;
+  bool dbg_on = getenv("HGB_STAMPS") != nullptr;
 
   void free_all() {
     d_gd.free_();
@@ -979,7 +1010,8 @@ struct hge_batch {
                     &d_krr, &d_kid})
       b->free_();
     for (auto* b : {&d_ts, &d_tsch, &d_calls, &d_cts, &d_counts, &d_scal, &d_kct}) b->free_();
-    for (auto* b : {&d_S, &d_ssb, &d_seeb, &d_ks0}) b->free_();
+    for (auto* b : {&d_S, &d_ssb, &d_seeb, &d_ks0, &d_Sch}) b->free_();
+    d_ntxch.free_();
     d_coin.free_();
     d_wit.free_();
     d_WCOIN.free_();
@@ -1079,6 +1111,8 @@ struct hge_batch {
     if (ccap >= (1 << 24)) throw BatchError{HGE_ERR_CAPACITY, "batch graph with a chain of 2^24 events or more"};
     std::vector<int32_t> cr, ix, sp, op, oc, ntx, clen((size_t)G * N), chain((size_t)G * N * ccap, -1);
     std::vector<int64_t> ts, tsch((size_t)G * N * ccap, 0), calls;
+    std::vector<uint64_t> Sch((size_t)G * N * ccap, 0);
+    std::vector<int32_t> ntxch((size_t)G * N * ccap, 0);
     std::vector<uint64_t> S;
     std::vector<uint8_t> coin;
     cr.reserve(Etot);
@@ -1099,6 +1133,8 @@ struct hge_batch {
         for (size_t p = 0; p < gr.chain[c].size(); p++) {
           chain[((size_t)g * N + c) * ccap + p] = gr.chain[c][p];
           tsch[((size_t)g * N + c) * ccap + p] = gr.ts[gr.chain[c][p]];
+          Sch[((size_t)g * N + c) * ccap + p] = gr.S[4 * (size_t)gr.chain[c][p]];
+          ntxch[((size_t)g * N + c) * ccap + p] = gr.ntx[gr.chain[c][p]];
         }
       }
     }
@@ -1115,12 +1151,14 @@ struct hge_batch {
     up(d_clen, clen);
     up(d_chain, chain);
     up(d_tsch, tsch);
+    up(d_Sch, Sch);
+    up(d_ntxch, ntxch);
     d_gd.need(G);
     BCHK(hipMemcpyAsync(d_gd.p, hd.data(), sizeof(GDesc) * G, hipMemcpyHostToDevice, st));
     const size_t E1 = (size_t)std::max<int64_t>(Etot, 1);
     d_LA.need(E1 * N);
     d_FDT.need((size_t)G * N * N * ccap);
-    d_FD.need(E1 * N);
+    d_FD.need((size_t)G * N * ccap * N);
     d_round.need(E1);
     d_wit.need(E1);
     d_rr.need(E1);
@@ -1147,6 +1185,7 @@ struct hge_batch {
     d_thv.need(RN / N);
     d_counts.need(std::max<int64_t>(Ktot, 1));
     d_scal.need((size_t)G * 8);
+    if (dbg_on) d_dbg.need((size_t)G * 8);
     BCHK(hipStreamSynchronize(st));
     staged = true;
   }
@@ -1173,6 +1212,8 @@ struct hge_batch {
     t.LA = d_LA.p;
     t.FDT = d_FDT.p;
     t.FD = d_FD.p;
+    t.Sch = d_Sch.p;
+    t.ntxch = d_ntxch.p;
     t.round = d_round.p;
     t.wit = d_wit.p;
     t.rr = d_rr.p;
@@ -1198,6 +1239,7 @@ struct hge_batch {
     t.kct = d_kct.p;
     t.ks0 = d_ks0.p;
     t.kid = d_kid.p;
+    t.dbg = dbg_on ? d_dbg.p : nullptr;
     return t;
   }
 
@@ -1253,6 +1295,15 @@ struct hge_batch {
     BCHK(hipMemcpyAsync(h_scal.data(), d_scal.p, (size_t)G * 64, hipMemcpyDeviceToHost, st));
     BCHK(hipStreamSynchronize(st));
     for (int k = 0; k < NK; k++) BCHK(hipEventElapsedTime(&kms[k], ev[k], ev[k + 1]));
+    if (dbg_on) {  // section cycles of kb_consensus, summed over the graphs
+      std::vector<uint64_t> hd_((size_t)G * 8);
+      BCHK(hipMemcpy(hd_.data(), d_dbg.p, (size_t)G * 64, hipMemcpyDeviceToHost));
+      double sum[5] = {};
+      for (int g = 0; g < G; g++)
+        for (int i = 0; i < 5; i++) sum[i] += (double)hd_[(size_t)g * 8 + i];
+      fprintf(stderr, "[hgb stamps] per graph cycles: divide %.0f fame %.0f thresholds %.0f receive %.0f order %.0f\n",
+              sum[0] / G, sum[1] / G, sum[2] / G, sum[3] / G, sum[4] / G);
+    }
     int64_t tot = 0;
     for (int g = 0; g < G; g++) {
       if (h_scal[(size_t)g * 8 + 6])
@@ -1401,7 +1452,7 @@ extern "C" int hgb_debug_rows(hge_batch* b, int32_t g, int32_t which, int32_t* o
   if (which == 2)  // the run layout FDT[j][c][p], N x N x ccap
     b->down(out, b->d_FDT.p + (size_t)g * b->N * b->N * b->ccap, (size_t)b->N * b->N * b->ccap);
   else
-    b->down(out, (which ? b->d_FD.p : b->d_LA.p) + d.eo * b->N, (size_t)d.E * b->N);
+    b->down(out, b->d_LA.p + d.eo * b->N, (size_t)d.E * b->N);
   return HGE_OK;
   BGUARD_END(b)
 }

@@ -900,7 +900,7 @@ struct hge_engine {
       if (retry) h2d(k_rs, rs, 12);
       t = tables();
       const int NP = (N + 15) & ~15;
-      if (N > 32 && wide32) {
+      if (N > 32 && (wide32 || frontier_fallback)) {
         rounds_step32();
       } else if (N > 32) {
         rounds_coop(fresh);
@@ -1020,7 +1020,18 @@ struct hge_engine {
       mnr_key[2] = n1;
       if (coop_err_check) {
         coop_err_check = false;
-        if (coop_err) throw EngineError(HGE_ERR_DEVICE, "rounds frontier hand-off timed out");
+        if (coop_err) {
+          // a wide walk's frontier hand-off timed out (its workgroups were not all
+          // resident: another grid on the device, e.g. one engine per rank on a
+          // shared GPU).  The kernels after it stood down; the engine walks again
+          // with k_round_step32, one launch per round, which needs no co-residency,
+          // and keeps that walk from here on.  Rows at and past the rounds this
+          // batch started from are recomputed from scratch.
+          frontier_fallback = true;
+          n_frontier_fallbacks++;
+          HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(d_C.p + (size_t)R * N), INF32, (size_t)(Rcap - R) * N, st));
+          continue;
+        }
       }
       if (h_minw[Rcap + 1]) {
         ensure_rcap((int64_t)Rcap * 2);
@@ -1138,6 +1149,8 @@ struct hge_engine {
   // (the caller holds frontier_lock() until the stream has drained)
   int32_t coop_err = 0;
   bool coop_err_check = false;
+  bool frontier_fallback = false;  // k_round_step32 for good after a hand-off timeout
+  int64_t n_frontier_fallbacks = 0;
   void rounds_coop(bool fresh) {
     Tables t = tables();
     s_fst.need(N + 1);
@@ -1160,8 +1173,11 @@ struct hge_engine {
       HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_rounds_coop, COOP_BS, 0));
       HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
       HIPCHK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device));
-      if (!coop || (int64_t)nb * ncu < N)
-        throw EngineError(HGE_ERR_DEVICE, "cooperative rounds kernel cannot be co-resident");
+      if (!coop || (int64_t)nb * ncu < N) {  // a device too small for the walk's grid
+        frontier_fallback = true;
+        rounds_step32();
+        return;
+      }
       coop_nb = nb;
       coop_ncu = ncu;
       coop_checked = true;
@@ -1238,7 +1254,13 @@ struct hge_engine {
       KLAUNCH(k_coop_join, dim3(64), dim3(256), 0, st, t, cs, d_ssc.p, rstate, resume);
       int32_t hres[2] = {0, 0};
       readback(&hres[0], err, 1);
-      if (hres[0]) throw EngineError(HGE_ERR_DEVICE, "rounds frontier hand-off timed out");
+      if (hres[0]) {  // co-residency failure: coords_b falls back to k_round_step32
+        const int32_t down[2] = {Rprev, 4};
+        h2d(rstate, down, 8);
+        coop_err = 1;
+        coop_err_check = true;
+        return;
+      }
       readback(&hres[1], resume, 1);
       if (getenv("HGE_WALK_DEBUG")) {
         std::vector<int32_t> hn(2 * nw);
@@ -1279,6 +1301,11 @@ struct hge_engine {
       prof_begin("k_rounds_coop");
       HIPCHK(launch_resident((const void*)k_rounds_coop, dim3(N), dim3(COOP_BS), args));
       prof_end();
+    }
+    if (getenv("HGE_TEST_HANDOFF_FAIL")) {  // tests: the walk reports a hand-off timeout
+      const int32_t one = 1, down = 4;
+      h2d(err, &one, 4);
+      h2d(rstate + 1, &down, 4);
     }
     // the hand-off error flag comes back with the round count (coords_b)
     d2h(&coop_err, s_bar.p + 1, 4);
@@ -3009,6 +3036,11 @@ int hge_stage_times(hge_engine* h, float* ms_out, int cap) {
   int n = std::min(cap, 7);
   for (int i = 0; i < n; i++) ms_out[i] = h->stage_ms[i];
   return n;
+}
+
+int64_t hge_frontier_fallbacks(hge_engine* h) {
+  if (!h) return HGE_ERR_ARG;
+  return h->n_frontier_fallbacks;
 }
 
 }  // extern "C"

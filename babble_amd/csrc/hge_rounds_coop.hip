@@ -390,7 +390,7 @@ __global__ void __launch_bounds__(COOP_BS) k_rounds_coop(Tables t, const int32_t
           any |= (P != INF32);
         }
         if (__all(ok)) break;
-        if (++spins > (1u << 24)) {  // never a normal wait: co-residency failure
+        if (++spins > (1u << 21)) {  // never a normal wait (~2 s): co-residency failure
           fail = true;
           break;
         }
@@ -400,7 +400,10 @@ __global__ void __launch_bounds__(COOP_BS) k_rounds_coop(Tables t, const int32_t
       any = __ballot(any) != 0;
       if (tid == 0) {
         L.s_stop = fail ? 2 : (any ? 0 : 1);
-        if (fail) atomicOr(err, 1);
+        if (fail) {  // the host falls back to k_round_step32
+          atomicOr(err, 1);
+          atomicOr(rstate + 1, 4);  // the downstream kernels stand down, as on overflow
+        }
       }
     }
     __syncthreads();
@@ -538,7 +541,7 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4, 4)))
           h += coop_mix(((uint64_t)dd << 32) | (uint32_t)P);
         }
         if (__all(ok)) break;
-        if (++spins > (1u << 24)) {  // never a normal wait: co-residency failure
+        if (++spins > (1u << 21)) {  // never a normal wait (~2 s): co-residency failure
           fail = true;
           break;
         }

@@ -618,7 +618,7 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
           P = (int)(uint32_t)x;
         }
         if (__all(ok)) break;
-        if (++spins > (1u << 24)) {  // never a normal wait: co-residency failure
+        if (++spins > (1u << 21)) {  // never a normal wait (~2 s): co-residency failure
           fail = true;
           break;
         }
@@ -630,7 +630,10 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
       const bool notpast = stopcut && __ballot(part == 0 && d < N && P < stopcut[d]) != 0;  // INF32 passes
       if ((threadIdx.x & 63) == 0 && (any || notpast || fail))
         atomicOr(&L.sFlag[(r + 1) & 1], (any ? 1 : 0) | (notpast ? 2 : 0) | (fail ? 4 : 0));
-      if (fail && (threadIdx.x & 63) == 0) atomicOr(err, 1);
+      if (fail && (threadIdx.x & 63) == 0) {  // the host falls back to k_round_step32
+        atomicOr(err, 1);
+        atomicOr(rstate + 1, 4);  // the downstream kernels stand down, as on overflow
+      }
       if (!fail) dir_members_mb<BS, NPOW>(mbp[(r + 1) & 1], mw);
     }
     __syncthreads();  // every wave has polled (and stored its window rows)

@@ -72,7 +72,8 @@ EXPORTS = [
     "hge_undetermined", "hge_known", "hge_round_of", "hge_is_witness", "hge_round_witness",
     "hge_fame", "hge_round_events", "hge_round_received", "hge_consensus_timestamp",
     "hge_ancestor", "hge_self_ancestor", "hge_see", "hge_strongly_see",
-    "hge_oldest_self_ancestor_to_see", "hge_coordinates", "hge_coordinate_sweeps", "hge_host_syncs", "hge_stage_times",
+    "hge_oldest_self_ancestor_to_see", "hge_coordinates", "hge_coordinate_sweeps", "hge_host_syncs", "hge_frontier_fallbacks",
+    "hge_stage_times",
     "hge_set_profiling", "hge_reset_kernel_stats", "hge_kernel_stats",
     "hge_consensus_log", "hge_event_rounds", "hge_event_received", "hge_set_cache_size",
     "hge_cache_size", "hge_participant_events", "hge_participant_event", "hge_last_from",
@@ -172,6 +173,8 @@ def lib():
     if hasattr(L, "hge_host_syncs"):
         L.hge_host_syncs.restype = i64
         L.hge_host_syncs.argtypes = [vp]
+    L.hge_frontier_fallbacks.restype = i64
+    L.hge_frontier_fallbacks.argtypes = [vp]
     L.hge_consensus_log.argtypes = [vp, i64, P(i32), i64]
     L.hge_consensus_log.restype = i64
     L.hge_event_rounds.argtypes = [vp, P(i32), P(ctypes.c_uint8), i64]
@@ -651,6 +654,11 @@ class Engine:
     def host_syncs(self):
         """Host round trips so far (waits on the engine stream)."""
         return int(self.L.hge_host_syncs(self.h))
+
+    def frontier_fallbacks(self):
+        """Times the wide rounds walk timed out on its frontier hand-off and walked
+        again launch per round (hge_frontier_fallbacks)."""
+        return int(self.L.hge_frontier_fallbacks(self.h))
 
     def stage_times(self):
         out = (ctypes.c_float * 7)()

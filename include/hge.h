@@ -437,6 +437,11 @@ int32_t hge_coordinate_sweeps(hge_engine* h);
 /* Host round trips so far: the number of times the host has waited on the
  * engine's stream (each readback of a control value or result is one). */
 int64_t hge_host_syncs(hge_engine* h);
+/* Times the wide rounds walk (N > 32) found its frontier hand-off timed out (its
+ * workgroups were not all resident, e.g. several engines sharing one GPU) and
+ * walked again with the launch-per-round kernel, which the engine then keeps;
+ * results are unchanged.  Replaces returning HGE_ERR_DEVICE from the replay. */
+int64_t hge_frontier_fallbacks(hge_engine* h);
 /* Per-kernel timing: HIP events around every launch on the engine stream. */
 int hge_set_profiling(hge_engine* h, int on);
 int hge_reset_kernel_stats(hge_engine* h);

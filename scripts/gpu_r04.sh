@@ -8,6 +8,8 @@
 #   prof     rocprofv3 kernel stats of the default bench -> gpurun_out/r04/prof
 #   profmc   rocprofv3 kernel stats of the mc bench -> gpurun_out/r04/profmc
 #   smoke    __graft_entry__.smoke()
+#   fallback the hand-off fallback and RCCL world-1 exchange tests
+#   stamps   the batch engine's per-section cycle stamps (HGB_STAMPS)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 9
 mkdir -p gpurun_out/r04
@@ -21,6 +23,10 @@ for s in "$@"; do
          tail -3 gpurun_out/r04/gpu.log ;;
     batch) timeout -k 10 600 $PYT -m gpu tests/test_gpu_batch.py > gpurun_out/r04/batch.log 2>&1 || { tail -60 gpurun_out/r04/batch.log; exit 1; }
          tail -3 gpurun_out/r04/batch.log ;;
+    fallback) timeout -k 10 400 $PYT -m gpu tests/test_gpu_wide.py tests/test_gpu_split.py -k "handoff or nccl_world" > gpurun_out/r04/fallback.log 2>&1 || { tail -40 gpurun_out/r04/fallback.log; exit 1; }
+         tail -3 gpurun_out/r04/fallback.log ;;
+    stamps) HGB_STAMPS=1 timeout -k 10 300 python -u bench.py --workload mc --no-cpu-baseline --steps 2 --warmup 1 --ramp-s 0 > gpurun_out/r04/stamps.json 2> gpurun_out/r04/stamps.err || { tail -20 gpurun_out/r04/stamps.err; exit 2; }
+         grep "hgb stamps" gpurun_out/r04/stamps.err | tail -1 ;;
     mcgpu) timeout -k 10 600 $PYT -m gpu tests/test_gpu_mc.py tests/test_gpu_batch.py > gpurun_out/r04/mcgpu.log 2>&1 || { tail -40 gpurun_out/r04/mcgpu.log; exit 1; }
          tail -3 gpurun_out/r04/mcgpu.log ;;
     bench) timeout -k 10 600 python -u bench.py > gpurun_out/r04/bench.json 2> gpurun_out/r04/bench.err || { tail -20 gpurun_out/r04/bench.err; exit 2; }

@@ -257,3 +257,69 @@ def test_sharded_split_emulated_parts(n, E, G):
     finally:
         ref.close()
         eng.close()
+
+
+def _nccl_world1(port, q):
+    import torch
+    import torch.distributed as dist
+    from babble_amd.dist import TorchExchange, split_run
+    from babble_amd.engine import Engine, events_array
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda:0"))
+    out = {"slots": []}
+    try:
+        x = TorchExchange(dist, "cuda:0")
+        out["nccl"] = x.nccl
+        # op 0 / op 1 as the engine calls them (hge_split_exchange): the slot comes back
+        # unchanged through all_gather_into_tensor; a larger exchange regrows the buffer
+        for nbytes, seed in ((4096, 1), (1 << 20, 2), (4096, 3)):
+            p = x(0, nbytes)
+            g = torch.Generator(device="cuda:0").manual_seed(seed)
+            want = torch.randint(0, 256, (nbytes,), generator=g, device="cuda:0").to(torch.uint8)
+            torch.cuda.synchronize()
+            x.buf[:nbytes].copy_(want)
+            torch.cuda.synchronize()
+            assert x(1, nbytes) is None
+            out["slots"].append(p == x.buf.data_ptr() and bool(torch.equal(x.buf[:nbytes], want)))
+        # a world of one: split_run replays unsplit with the exchange installed
+        n, E = 64, 12_000
+        dag = random_gossip(n, E, seed=93)
+        ev = events_array(dag)
+        calls = schedule(E, n)
+        eng = Engine(n, E + 64, device=0)
+        ref = Engine(n, E + 64, device=0)
+        try:
+            eng.prepare(ev, calls)
+            stats = {}
+            split_run(eng, 0, 1, x, 8, stats)
+            _, order, counts = eng.fetch()
+            _, rorder, rcounts = ref.replay(ev, calls)
+            out["equal"] = bool(np.array_equal(order, rorder) and np.array_equal(counts, rcounts))
+            out["stats"] = stats
+        finally:
+            eng.close()
+            ref.close()
+    except Exception as e:  # reported to the parent
+        out["error"] = repr(e)
+    finally:
+        dist.destroy_process_group()
+    q.put(out)
+
+
+def test_torch_exchange_nccl_world_one():
+    """TorchExchange on a world-size-1 "nccl" (RCCL) group: op 0 hands out the slot
+    buffer and op 1 runs all_gather_into_tensor -- the branch the multi-GPU bench's
+    split replay takes -- at two sizes (the buffer regrows), then split_run with the
+    exchange installed equals the one-GPU replay."""
+    import torch.multiprocessing as mp
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_world1, args=(port, q))
+    p.start()
+    out = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert "error" not in out, out
+    assert out["nccl"] and out["slots"] == [True, True, True], out
+    assert out["equal"] and not out["stats"], out

@@ -209,3 +209,47 @@ def test_two_wide_engines_concurrently():
     finally:
         for e in engines:
             e.close()
+
+
+@pytest.mark.parametrize("n,events,k", [(64, 4000, 16), (128, 6000, 1)])
+def test_handoff_timeout_falls_back_per_round(n, events, k, monkeypatch):
+    """A wide walk whose frontier hand-off times out (forced: HGE_TEST_HANDOFF_FAIL
+    makes the walk report the timeout after it ran) walks again one launch per round
+    (k_round_step32) and keeps that walk; the results equal the oracle's."""
+    from babble_amd.engine import Engine
+    monkeypatch.setenv("HGE_TEST_HANDOFF_FAIL", "1")
+    eng = Engine(n, 1 << 14)
+    try:
+        run_case(eng, random_gossip(n, events, seed=900 + n), k)
+        assert eng.frontier_fallbacks() == 1
+    finally:
+        eng.close()
+
+
+def test_handoff_timeout_online_path(monkeypatch):
+    """The fallback in the middle of an online run (one RunConsensus per batch): the
+    rows of the batch are recomputed from the rounds it started with."""
+    from babble_amd.engine import Engine, events_array
+    from babble_amd.gossip import schedule
+    n, E, k = 64, 3000, 12
+    dag = random_gossip(n, E, seed=31)
+    calls = schedule(E, k)
+    a = Engine(n, 1 << 13)
+    b = Engine(n, 1 << 13)
+    try:
+        _, order, _ = a.replay(dag, calls)
+        ev = events_array(dag)
+        nxt = 0
+        for q, c in enumerate(calls):
+            if q == 5:
+                monkeypatch.setenv("HGE_TEST_HANDOFF_FAIL", "1")
+            b.insert_events(ev[nxt:c].copy())
+            b.run_consensus()
+            nxt = c
+        assert b.frontier_fallbacks() == 1
+        np.testing.assert_array_equal(b.consensus_events(), order)
+        assert b.rounds() == a.rounds()
+        assert a.frontier_fallbacks() == 0
+    finally:
+        a.close()
+        b.close()
