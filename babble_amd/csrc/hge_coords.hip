@@ -118,6 +118,56 @@ __global__ void __launch_bounds__(256) k_la_sweep(Tables t, const int2* segs, in
   if (__ballot(ch) && (threadIdx.x & 63) == __builtin_ctzll(__ballot(ch))) *changed = 1;
 }
 
+// lastAncestors of a small batch of new events [n0, n1) (an online call at N <= 32)
+// in ONE exact pass: no fixed-point sweeps, so no host round trip for their
+// convergence flags.  The same recurrence as k_la_sweep, in insertion order (a
+// parent is inserted before its child):
+//   phase 1 (all lanes, NP per event): the max of the rows of the event's chain
+//     predecessor and other-parent that existed before the batch, with its own
+//     column; the batch indices of the parents inserted in it;
+//   phase 2 (the first NP lanes of wave 0, lane = column): the events in order,
+//     folding their in-batch parents' rows from LDS (two LDS reads per event);
+//   phase 3: the rows to LA, coalesced.
+// m * NP <= LASEQ_MAX (the host checks; larger batches take the sweeps).
+constexpr int LASEQ_MAX = 8192;
+template <int NP>
+__global__ void __launch_bounds__(256) k_la_seq(Tables t, int n0, int n1) {
+  __shared__ int rows[LASEQ_MAX];
+  __shared__ int2 par[LASEQ_MAX / NP];
+  constexpr int G = 256 / NP;
+  const int N = t.N, m = n1 - n0;
+  const int tid = threadIdx.x, i = tid % NP;
+  for (int e = tid / NP; e < m; e += G) {
+    const int x = n0 + e;
+    const int cx = t.creator[x], px = t.index[x];
+    const int s = px > 0 ? t.chain[(size_t)cx * t.ccap + px - 1] : -1;
+    const int2 oc = t.opcp[(size_t)cx * t.ccap + px];
+    const int o = oc.x >= 0 ? t.chain[(size_t)oc.x * t.ccap + oc.y] : -1;
+    int v = -1;
+    if (i < N) {
+      if (s >= 0 && s < n0) v = t.LA[rowoff(t, cx, px - 1) + i];
+      if (o >= 0 && o < n0) v = max(v, t.LA[rowoff(t, oc.x, oc.y) + i]);
+      if (i == cx) v = max(v, px);
+    }
+    rows[e * NP + i] = v;
+    if (i == 0) par[e] = make_int2(s >= n0 ? s - n0 : -1, o >= n0 ? o - n0 : -1);
+  }
+  __syncthreads();
+  if (tid < NP) {
+    for (int e = 0; e < m; e++) {
+      const int2 pp = par[e];
+      const int a = pp.x >= 0 ? rows[pp.x * NP + i] : -1;
+      const int b = pp.y >= 0 ? rows[pp.y * NP + i] : -1;
+      rows[e * NP + i] = max(rows[e * NP + i], max(a, b));
+    }
+  }
+  __syncthreads();
+  for (int e = tid / NP; e < m; e += G) {
+    const int x = n0 + e;
+    if (i < N) t.LA[rowoff(t, t.creator[x], t.index[x]) + i] = rows[e * NP + i];
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Packed 16-bit sweeps (N > 32 while every chain holds at most 65,534 events; past
 // that the engine switches to the int32 tables for good, hge_wide32.hip):

@@ -177,7 +177,7 @@ struct hge_engine {
   DBuf<uint8_t> d_FDTW;  // N > 16: per (row, 64-column tile) out-of-range flags of d_FDTD
   DBuf<int32_t> d_WLA;   // N > 16: round frontier rows transposed (k_witness_la)
   DBuf<uint64_t> d_ssc, s_gran;
-  DBuf<int32_t> s_bseg;
+  DBuf<int32_t> s_bseg, s_choff;
   DBuf<uint64_t> s_H;                // speculative walk: epoch-tagged histories
   DBuf<int32_t> s_hn, s_hres;        // rows written + progress hints, merge results
   uint32_t walk_epoch = 0;
@@ -907,14 +907,35 @@ struct hge_engine {
       } else {
         // first-strong-seer rows for every event that can still be a frontier member
         // (from a fresh state the frontier starts at round 0, position 0: no round trip)
+        int maxlen = 0;
+        for (int c = 0; c < N; c++) maxlen = std::max(maxlen, chain_len[c]);
+        const int Rprev = R;  // C rows >= Rprev are empty before this batch
+        if (!fresh && maxlen < 0xFFFF) {
+          // an online call: the walk's first round, its k_fss rows and their count
+          // stay on the device (k_frontier_start writes them; k_fss loops over the
+          // count, k_rounds_walk stands down at INF32): no host round trip
+          s_fst.need(N + 1);
+          KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p, k_lo);
+          const int64_t guess = m + 16 * (int64_t)N;  // the grid loops past it
+#define FSSD(NPC, LPC, B)                                                                              \
+  KLAUNCH(k_fss<NPC>, dim3((unsigned)std::min<int64_t>(1024, div_up(guess * NPC, 256))), dim3(256), 0, st, t, \
+          k_lo, k_lo + N, 0, (int32_t*)nullptr, (uint16_t*)d_FSS.p, (const int32_t*)(k_lo + 2 * N));          \
+  KLAUNCH((k_rounds_walk<NPC, LPC, B>), dim3(1), dim3(1024), 0, st, t, (const uint16_t*)d_FSS.p, k_len,       \
+          k_len + N, k_rs, 0, Rprev, dbg_p(), (const int32_t*)s_fst.p);
+          if (NP == 16) {
+            FSSD(16, 4, 256)
+          } else {
+            FSSD(32, 2, 64)
+          }
+#undef FSSD
+        } else {
         std::vector<int32_t> fst(N + 1, 0);
         if (!fresh) {
           s_fst.need(N + 1);
-          KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p);
+          KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p, (int32_t*)nullptr);
           readback(fst.data(), s_fst.p, N + 1);
         }
         const int rlo = fst[0];
-        const int Rprev = R;  // C rows >= Rprev are empty before this batch
         if (rlo != INF32) {
           int tot = fresh ? tot0 : 0;
           if (!fresh) {
@@ -927,15 +948,13 @@ struct hge_engine {
             lo_off[2 * N] = tot;
             h2d(k_lo, lo_off.data(), 4 * (2 * N + 1));
           }
-          int maxlen = 0;
-          for (int c = 0; c < N; c++) maxlen = std::max(maxlen, chain_len[c]);
           if (tot > 0) {
             // the LDS walk keeps chain positions as uint16; longer chains take the
             // register walk over the global fss rows
 #define FSSL(NPC, LPC, B)                                                                          \
   if (maxlen < 0xFFFF) {                                                                           \
     KLAUNCH(k_fss<NPC>, dim3(div_up((int64_t)tot * NPC, 256)), dim3(256), 0, st, t, k_lo, k_lo + N, \
-            tot, (int32_t*)nullptr, (uint16_t*)d_FSS.p);                                           \
+            tot, (int32_t*)nullptr, (uint16_t*)d_FSS.p, (const int32_t*)nullptr);                  \
     const int nw = fresh ? spec_walkers(maxlen) : 0;                                               \
     if (nw > 1) {                                                                                  \
       const char* hc = getenv("HGE_WALK_HCAP"); /* tests: force the capacity fallback */          \
@@ -964,7 +983,7 @@ struct hge_engine {
     }                                                                                              \
   } else {                                                                                         \
     KLAUNCH(k_fss<NPC>, dim3(div_up((int64_t)tot * NPC, 256)), dim3(256), 0, st, t, k_lo, k_lo + N, \
-            tot, d_FSS.p, (uint16_t*)nullptr);                                                     \
+            tot, d_FSS.p, (uint16_t*)nullptr, (const int32_t*)nullptr);                            \
     KLAUNCH(k_rounds_fss<NPC>, dim3(1), dim3(64), 0, st, t, d_FSS.p, k_len, k_len + N, k_rs, rlo);  \
   }
             if (NP == 16) {
@@ -974,6 +993,7 @@ struct hge_engine {
             }
 #undef FSSL
           }
+        }
         }
       }
       // rounds, witnesses and the first witness of every round, then ONE round
@@ -1154,7 +1174,7 @@ struct hge_engine {
   void rounds_coop(bool fresh) {
     Tables t = tables();
     s_fst.need(N + 1);
-    KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p);
+    KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p, (int32_t*)nullptr);
     // the lowest round to recompute: read back for a fresh state (the walkers and the
     // joined rows need it on the host), else read by the frontier kernel itself,
     // which stands down at INF32 (no round trip)
@@ -1343,7 +1363,7 @@ struct hge_engine {
   void rounds_step32() {
     Tables t = tables();
     s_fst.need(N + 1);
-    KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p);
+    KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p, (int32_t*)nullptr);
     int32_t rlo = INF32;
     readback(&rlo, s_fst.p, 1);
     if (rlo == INF32) return;
@@ -1442,8 +1462,17 @@ struct hge_engine {
     const bool p16 = sweep16();
     // skip segments whose inputs did not change in the previous sweep
     const bool SKIP = true;
+    const int NPs = N <= 16 ? 16 : 32;
+    const int64_t mnew = n_events - n_coords;
     if (p16 && la_windows()) {
       la_windows_run(t);
+    } else if (!p16 && N <= 32 && mnew * NPs <= LASEQ_MAX && !getenv("HGE_NO_LASEQ")) {
+      // a small batch (an online call): one exact pass in insertion order
+      if (NPs == 16)
+        KLAUNCH(k_la_seq<16>, dim3(1), dim3(256), 0, st, t, (int)n_coords, (int)n_events);
+      else
+        KLAUNCH(k_la_seq<32>, dim3(1), dim3(256), 0, st, t, (int)n_coords, (int)n_events);
+      n_sweeps = 1;
     } else {
     int32_t* dirty = nullptr;
     if (p16 && SKIP) {
@@ -2091,9 +2120,17 @@ struct hge_engine {
     const bool wmed = N > 16;
     const bool ident = fresh && cand == d_und.p && (int64_t)ncand == n_events;
     int32_t* bseg = nullptr;
+    const int32_t* choff = nullptr;
     if (wmed) {
       s_bseg.need(ncand);
       bseg = s_bseg.p;
+      if (ident && !getenv("HGE_MED_EVORDER")) {  // chain-major waves (k_median_wave)
+        std::vector<int32_t> off(N + 1, 0);
+        for (int c = 0; c < N; c++) off[c + 1] = off[c] + chain_len[c];
+        s_choff.need(N + 1);
+        h2d(s_choff.p, off.data(), 4 * (size_t)(N + 1));
+        choff = s_choff.p;
+      }
       if (R_last > rr_lo) {
         d_WLA.need((size_t)Rcap * N * N);
         Tables tw = tables();
@@ -2112,7 +2149,7 @@ struct hge_engine {
     if (wmed)                                                                                    \
       KLAUNCH(k_median_wave<B>, dim3(div_up(ncand, 4 * HGE_MW_E)), dim3(256), 0, st, tables(),              \
               ident ? (const int32_t*)nullptr : cand, ncand, s_recv.p, s_rr.p, bseg, s_segfws.p,  \
-              s_cts.p);                                                                          \
+              s_cts.p, choff);                                                                   \
     break;
       RCASE(1)
       RCASE(2)

@@ -236,55 +236,63 @@ __device__ __forceinline__ int select_kth(int (&v)[NPC], int k) {
 // pw + 1 (an event never strongly sees itself); otherwise int32 rows of N.
 template <int NPC>
 __global__ void __launch_bounds__(256) k_fss(Tables t, const int32_t* lo, const int32_t* off,
-                                             int total, int32_t* FSS, uint16_t* FSS16) {
-  constexpr int EPB = 256 / NPC;  // events per block
+                                             int total_arg, int32_t* FSS, uint16_t* FSS16,
+                                             const int32_t* total_dev) {
+  constexpr int EPB = 256 / NPC;  // events per block and pass
   __shared__ int s_off[NPC + 1], s_lo[NPC];
   __shared__ int tr[EPB][NPC][NPC + 1];
   const int N = t.N;
   const int tid = threadIdx.x;
+  // total_dev (non-null): the count written by k_frontier_start on the device (an
+  // online call's walk; the grid loops over it, sized by the host without a readback)
+  const int total = total_dev ? *total_dev : total_arg;
   if (tid <= N) s_off[tid] = off[tid];
   if (tid < N) s_lo[tid] = lo[tid];
   __syncthreads();
   const int e = tid / NPC, c = tid - (tid / NPC) * NPC;
-  const int ev = blockIdx.x * EPB + e;
-  const bool valid = ev < total;
-  int cw = 0;
-  if (valid)
-    while (s_off[cw + 1] <= ev) cw++;
-  const int pw = valid ? s_lo[cw] + (ev - s_off[cw]) : 0;
-  // row of (c, z_c): FD[(c, z_c)][0..N)
-  const int z = (valid && c < N) ? t.FD[rowoff(t, cw, pw) + c] : INF32;
-  int* row = tr[e][c];
-  if (z == INF32) {
+  for (int b = blockIdx.x; b * EPB < total; b += gridDim.x) {
+    const int ev = b * EPB + e;
+    const bool valid = ev < total;
+    int cw = 0;
+    if (valid)
+      while (s_off[cw + 1] <= ev) cw++;
+    const int pw = valid ? s_lo[cw] + (ev - s_off[cw]) : 0;
+    // row of (c, z_c): FD[(c, z_c)][0..N)
+    const int z = (valid && c < N) ? t.FD[rowoff(t, cw, pw) + c] : INF32;
+    int* row = tr[e][c];
+    if (z == INF32) {
 #pragma unroll
-    for (int j = 0; j < NPC; j++) row[j] = INF32;
-  } else {
-    const int32_t* src = t.FD + rowoff(t, c, z);
-    if (N == NPC) {
-#pragma unroll
-      for (int j = 0; j < NPC; j += 4) {
-        const int4 q4 = *(const int4*)(src + j);
-        row[j] = q4.x;
-        row[j + 1] = q4.y;
-        row[j + 2] = q4.z;
-        row[j + 3] = q4.w;
-      }
+      for (int j = 0; j < NPC; j++) row[j] = INF32;
     } else {
+      const int32_t* src = t.FD + rowoff(t, c, z);
+      if (N == NPC) {
 #pragma unroll
-      for (int j = 0; j < NPC; j++) row[j] = j < N ? src[j] : INF32;
+        for (int j = 0; j < NPC; j += 4) {
+          const int4 q4 = *(const int4*)(src + j);
+          row[j] = q4.x;
+          row[j + 1] = q4.y;
+          row[j + 2] = q4.z;
+          row[j + 3] = q4.w;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < NPC; j++) row[j] = j < N ? src[j] : INF32;
+      }
     }
-  }
-  __syncthreads();
-  if (!valid) return;
-  int v[NPC];
+    __syncthreads();
+    if (valid) {
+      int v[NPC];
 #pragma unroll
-  for (int i = 0; i < NPC; i++) v[i] = tr[e][i][c];
-  int f = (c < N) ? select_kth<NPC>(v, t.SM) : INF32;
-  if (FSS16) {
-    if (c == cw && f != INF32) f = max(f, pw + 1);
-    FSS16[((size_t)cw * t.ccap + pw) * NPC + c] = (f == INF32) ? 0xFFFF : (uint16_t)f;
-  } else if (c < N) {
-    FSS[rowoff(t, cw, pw) + c] = f;
+      for (int i = 0; i < NPC; i++) v[i] = tr[e][i][c];
+      int f = (c < N) ? select_kth<NPC>(v, t.SM) : INF32;
+      if (FSS16) {
+        if (c == cw && f != INF32) f = max(f, pw + 1);
+        FSS16[((size_t)cw * t.ccap + pw) * NPC + c] = (f == INF32) ? 0xFFFF : (uint16_t)f;
+      } else if (c < N) {
+        FSS[rowoff(t, cw, pw) + c] = f;
+      }
+    }
+    __syncthreads();  // tr is reused by the next pass
   }
 }
 
@@ -444,8 +452,10 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* 
                                                       uint64_t* dbg, const int32_t* rlo_dev) {
   // rlo_dev (non-null): the round to resume from, written by k_walk_join (-1: the
   // speculative walk completed and there is nothing left to walk)
+  // (k_frontier_start's INF32: no new event needs a round; an online call reads
+  // its first round this way, without a host round trip)
   const int rlo = rlo_dev ? *rlo_dev : rlo_arg;
-  if (rlo < 0) return;
+  if (rlo < 0 || rlo == INF32) return;
   constexpr int VPL = NPC / LPC;
   constexpr int RB = 64;       // C rows buffered per restage
   constexpr int Q8 = NPC / 8;  // int4 loads per fss row
@@ -683,8 +693,12 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* 
 }
 
 // frontier start: r_lo and the first position per chain that can be a member
+// lo_off (non-null): the k_fss rows of the walk from r_lo, [0, N) the start
+// positions, [N, 2N] their prefix offsets (the candidates' count last), written here
+// so that an online call at N <= 32 needs no host round trip for them
 __global__ void k_frontier_start(Tables t, const int32_t* olen, const int32_t* len,
-                                 int32_t* out /* [0] rlo, [1..N] start positions */) {
+                                 int32_t* out /* [0] rlo, [1..N] start positions */,
+                                 int32_t* lo_off = nullptr) {
   __shared__ int s_rlo;
   const int N = t.N;
   if (threadIdx.x == 0) s_rlo = INF32;
@@ -703,6 +717,19 @@ __global__ void k_frontier_start(Tables t, const int32_t* olen, const int32_t* l
       if (rlo == 0 && olen[c] == 0 && len[c] > 0) p = 0;
     }
     out[1 + c] = p == INF32 ? len[c] : p;
+    if (lo_off) lo_off[c] = p == INF32 ? len[c] : p;
+  }
+  if (lo_off && threadIdx.x == 0) {
+    int tot = 0;
+    for (int c = 0; c < N; c++) {
+      lo_off[N + c] = tot;
+      if (rlo != INF32) {
+        const int p = t.C[(size_t)rlo * N + c];
+        const int s0 = (rlo == 0 && olen[c] == 0 && len[c] > 0) ? 0 : (p == INF32 ? len[c] : p);
+        tot += max(0, len[c] - s0);
+      }
+    }
+    lo_off[2 * N] = tot;
   }
 }
 
@@ -1845,7 +1872,7 @@ template <int VPL>
 __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* cand, int ncand,
                                                      const int32_t* recv_call, const int32_t* rr_in,
                                                      const int32_t* bseg, const uint64_t* seg_fws,
-                                                     int64_t* cts_out) {
+                                                     int64_t* cts_out, const int32_t* choff) {
   // MW_E events per wave (candidates q0 + e * nw, nw = the grid's wave count; 1 measured
   // fastest once the select became cheap: 6.36 vs 6.62 ms at 2, 8.19 at 3): all
   // their loads are in flight together before the first select
@@ -1855,8 +1882,14 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
   constexpr int MW_E = HGE_MW_E;
   __shared__ __attribute__((aligned(16))) int s_mhist[4][256];  // each wave's select bins
   const int nw = gridDim.x * 4;
-  // (the XCD-aware order of k_fame_decide measured 0.2 ms slower here)
-  const int q0 = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // choff (non-null: a fresh replay, candidate = event id): the waves take the events
+  // in chain-major order (choff = the chains' prefix offsets, N + 1), each XCD a
+  // contiguous range of it.  The events of one chain and round share their threshold
+  // row WLA[rr][cx] (~14 consecutive positions at 256/10M) and their FDTD rows are
+  // consecutive, so a row is fetched into one XCD's L2 once instead of into every
+  // L2 (insertion order interleaves the chains, and neighbouring blocks go to
+  // different XCDs).
+  const int q0 = (choff ? (int)xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int N = t.N, NW = t.NW;
   int qe[MW_E], ixe[MW_E];
@@ -1869,7 +1902,16 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
   int wde[MW_E];
 #pragma unroll
   for (int e = 0; e < MW_E; e++) {
-    const int q = q0 + e * nw;
+    int q = q0 + e * nw;
+    if (choff && q < ncand) {  // chain-major position -> event id
+      int lo = 0, hi = N - 1;  // the chain c with choff[c] <= q < choff[c + 1]
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (choff[mid] <= q) lo = mid;
+        else hi = mid - 1;
+      }
+      q = t.chain[(size_t)lo * t.ccap + (q - choff[lo])];
+    }
     const int qq = q < ncand ? q : ncand - 1;  // valid indices; the result is not stored
     const int x = cand ? cand[qq] : qq;
     const int rc = recv_call[qq], rr0 = rr_in[qq], sg0 = bseg[qq];

@@ -310,7 +310,7 @@ __device__ __forceinline__ int coop_select(const Tables& t, const int32_t* FDT, 
 // 1024 threads: four waves per SIMD (the gather loop is issue/latency-bound at
 // one); gather batches of 8 columns keep it within 128 VGPRs
 constexpr int COOP_BS = 1024;
-constexpr int COOP_SPEC_BS = 512;  // walkers: 512 threads, 2 per CU (1024 = 1 per CU, HGE_COOP_SPEC_BS)
+constexpr int COOP_SPEC_BS = 512;  // walkers: 512 threads, 2 per CU
 __global__ void __launch_bounds__(COOP_BS) k_rounds_coop(Tables t, const int32_t* FDT, const int32_t* olen,
                                                      const int32_t* len, int32_t* rstate, int rlo,
                                                      const int32_t* rlo_dev, int Rprev, uint64_t* gran,

@@ -16,8 +16,10 @@ Two ways to use N GPUs:
     Every rank ends with the whole replay's state, identical to the one-GPU
     replay; a stream the candidate halo does not cover (HGE_ERR_SPLIT, every rank
     at the same point) is replayed unsplit.
-  * walk_split_run keeps round 2's walk-only split (walkers + one all-gather of
-    their rows), measured and documented, not the default.
+  * walk_split_run is DIAGNOSTIC only: round 2's walk-only split (walkers + one
+    all-gather of their rows), kept for the convergence measurements of
+    scripts/analysis/split_converge.py; bench.py no longer offers it (its walkers
+    do not meet at N = 256, profiles/r03/split).
 torch.distributed is plumbing here: "nccl" (RCCL over xGMI) on the GPU box,
 "gloo" in the CPU tests.
 """
@@ -144,7 +146,7 @@ def walk_rows(eng, rank, world, extra):
 
 
 def walk_split_run(eng, rank, world, gather, extra=256):
-    """Round 2's walk-only split: every rank computes everything but the rounds
+    """DIAGNOSTIC (not a production path).  Round 2's walk-only split: every rank computes everything but the rounds
     walk, which is walked by one walker per rank from its time cut; the rows are
     all-gathered (gather(obj) -> [obj of every rank]) and joined.  Exact; the
     sequential walk resumes where the walkers did not meet, which at N = 256 is

@@ -435,9 +435,6 @@ def main():
                          "ONE hashgraph sharded across the ranks (babble_amd.dist.split_run)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="torch.distributed backend (nccl = RCCL; gloo: rehearsing N ranks on one GPU)")
-    ap.add_argument("--walk-only", action="store_true",
-                    help="gossip, N > 1: round 2's walk-only split (walkers from time cuts joined by row "
-                         "equality; every rank computes the rest) instead of the sharded replay")
     args = ap.parse_args()
     mc = args.workload == "mc"
     n = args.participants or (32 if mc else DEFAULT[0])
@@ -480,15 +477,12 @@ def main():
     del ev0
     ingest_s = time.perf_counter() - t0
 
-    gather, exchange, split_stats = None, None, {}
+    exchange, split_stats = None, {}
     if split:
-        from babble_amd.dist import TorchExchange, split_run, torch_gather, walk_split_run
-        gather = torch_gather(dist, f"cuda:{local_rank}")
+        from babble_amd.dist import TorchExchange, split_run
         exchange = TorchExchange(dist, f"cuda:{local_rank}")
 
     def step():
-        if split and args.walk_only:
-            return walk_split_run(engines[0], rank, world, gather)
         if split:
             return split_run(engines[0], rank, world, exchange, stats=split_stats)
         return engines[0].run()
@@ -630,7 +624,7 @@ def main():
         parity = "; ".join(checks) if checks else None
 
     secondary = None
-    if split and not args.walk_only:
+    if split:
         # the same job as independent replicas (every rank replays the whole stream on
         # its own GPU, no collective): the weak-scaling line next to the strong one
         sync_all()
@@ -676,9 +670,7 @@ def main():
             "data": "synthetic",
             "config": {"workload": workload, "participants": n, "events_per_graph": E, "k": K,
                        "graphs_per_gpu": 1, "ordered_per_step": tot_ordered,
-                       "parallelism": ((f"split{world}: one hashgraph, rounds walk split across {world} GPUs"
-                                        if args.walk_only else
-                                        f"shard{world}: one hashgraph sharded by time across {world} GPUs "
+                       "parallelism": ((f"shard{world}: one hashgraph sharded by time across {world} GPUs "
                                         f"(fame by round, round received / median / order by call; RCCL "
                                         f"all-gathers; coordinates and the sequential rounds walk on every "
                                         f"rank)") if split else f"replicas{world}")},

@@ -9,6 +9,10 @@
 #   profmc   rocprofv3 kernel stats of the mc bench -> gpurun_out/r04/profmc
 #   smoke    __graft_entry__.smoke()
 #   fallback the hand-off fallback and RCCL world-1 exchange tests
+#   emulate  the one-hashgraph split emulated part by part (256/10M, 2/4/8 parts)
+#   configs  16/100k, 32/1M, 64/1M, 128/1M bench lines
+#   core     parity, wide, golden and replay-path GPU tests
+#   online   per-call profile of the online path (16/100k, 256 prefix)
 #   stamps   the batch engine's per-section cycle stamps (HGB_STAMPS)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 9
@@ -27,6 +31,21 @@ for s in "$@"; do
          tail -3 gpurun_out/r04/fallback.log ;;
     stamps) HGB_STAMPS=1 timeout -k 10 300 python -u bench.py --workload mc --no-cpu-baseline --steps 2 --warmup 1 --ramp-s 0 > gpurun_out/r04/stamps.json 2> gpurun_out/r04/stamps.err || { tail -20 gpurun_out/r04/stamps.err; exit 2; }
          grep "hgb stamps" gpurun_out/r04/stamps.err | tail -1 ;;
+    online) timeout -k 10 300 python -u scripts/analysis/online_profile.py 16 100000 16 2000 > gpurun_out/r04/online16.json 2> gpurun_out/r04/online16.err || { tail -20 gpurun_out/r04/online16.err; exit 2; }
+         timeout -k 10 300 python -u scripts/analysis/online_profile.py 256 600000 256 800 > gpurun_out/r04/online256.json 2> gpurun_out/r04/online256.err || { tail -20 gpurun_out/r04/online256.err; exit 2; }
+         head -12 gpurun_out/r04/online16.json ;;
+    core) timeout -k 10 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_wide.py tests/test_gpu_golden.py tests/test_gpu_replay_paths.py > gpurun_out/r04/core.log 2>&1 || { tail -40 gpurun_out/r04/core.log; exit 1; }
+         tail -3 gpurun_out/r04/core.log ;;
+    emulate) timeout -k 10 600 python -u scripts/analysis/split_emulate.py 256 10000000 2 4 8 > gpurun_out/r04/emulate.log 2>&1 || { tail -20 gpurun_out/r04/emulate.log; exit 3; }
+         grep -E "unsplit|max part" gpurun_out/r04/emulate.log ;;
+    configs) for NE in "16 100000" "32 1000000" "64 1000000" "128 1000000"; do
+           set -- $NE
+           timeout -k 10 300 python -u bench.py --participants $1 --events $2 --no-secondary --no-cpu-baseline --steps 5 --warmup 2 > gpurun_out/r04/n$1_e$2.json 2> gpurun_out/r04/n$1_e$2.err || { tail -20 gpurun_out/r04/n$1_e$2.err; exit 1; }
+           python -c "
+import json
+d=json.loads(open('gpurun_out/r04/n$1_e$2.json').read().strip().splitlines()[-1])
+print('$1/$2', round(d['value']/1e6,2), d['ms_per_step'], d['parity'][:120])"
+         done ;;
     mcgpu) timeout -k 10 600 $PYT -m gpu tests/test_gpu_mc.py tests/test_gpu_batch.py > gpurun_out/r04/mcgpu.log 2>&1 || { tail -40 gpurun_out/r04/mcgpu.log; exit 1; }
          tail -3 gpurun_out/r04/mcgpu.log ;;
     bench) timeout -k 10 600 python -u bench.py > gpurun_out/r04/bench.json 2> gpurun_out/r04/bench.err || { tail -20 gpurun_out/r04/bench.err; exit 2; }
