@@ -34,7 +34,7 @@ for s in "$@"; do
     online) timeout -k 10 300 python -u scripts/analysis/online_profile.py 16 100000 16 2000 > gpurun_out/r04/online16.json 2> gpurun_out/r04/online16.err || { tail -20 gpurun_out/r04/online16.err; exit 2; }
          timeout -k 10 300 python -u scripts/analysis/online_profile.py 256 600000 256 800 > gpurun_out/r04/online256.json 2> gpurun_out/r04/online256.err || { tail -20 gpurun_out/r04/online256.err; exit 2; }
          head -12 gpurun_out/r04/online16.json ;;
-    core) timeout -k 10 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_wide.py tests/test_gpu_golden.py tests/test_gpu_replay_paths.py > gpurun_out/r04/core.log 2>&1 || { tail -40 gpurun_out/r04/core.log; exit 1; }
+    core) timeout -k 10 600 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_wide.py tests/test_gpu_golden.py tests/test_gpu_replay_paths.py tests/test_gpu_reference.py > gpurun_out/r04/core.log 2>&1 || { tail -40 gpurun_out/r04/core.log; exit 1; }
          tail -3 gpurun_out/r04/core.log ;;
     emulate) timeout -k 10 600 python -u scripts/analysis/split_emulate.py 256 10000000 2 4 8 > gpurun_out/r04/emulate.log 2>&1 || { tail -20 gpurun_out/r04/emulate.log; exit 3; }
          grep -E "unsplit|max part" gpurun_out/r04/emulate.log ;;

@@ -225,3 +225,17 @@ def test_cpp_abi_binary_on_gpu():
     out = subprocess.run([os.path.join(root, "build", "hge_abi_test"), "--gpu"], capture_output=True,
                          text=True, timeout=120)
     assert out.returncode == 0, out.stderr + out.stdout
+
+
+def test_go_shim_logic_replayed_on_gpu():
+    """tests/abi/shim_replay_test.cpp --gpu: the Go shim's Hashgraph + bound InmemStore
+    restated in C++ (hash <-> id map, tsByNano, FindOrder's batch mapping) through
+    TestFindOrder, and a SetRound before consensus that GetRound must not let hide the
+    fame the engine decides afterwards."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([os.path.join(root, "build", "shim_replay_test"), "--gpu"], capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode == 0, out.stderr + out.stdout
+    assert "0 failures" in out.stdout
