@@ -253,11 +253,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 template <int NM>
 __global__ __launch_bounds__(256) void kb_fdrows(BT t) {
   const int g = blockIdx.x / t.N, c = blockIdx.x % t.N;
-  const GDesc d = t.gd[g];
   const int N = t.N, cc = t.ccap, tid = threadIdx.x;
   __shared__ int32_t tile[NM][65];
   const int len = t.clen[g * N + c];
-  const int32_t* ch = t.chain + ((int64_t)g * N + c) * cc;
   for (int p0 = 0; p0 < len; p0 += 64) {
     for (int e = tid; e < N * 64; e += 256) {  // read along positions
       const int j = e >> 6, p = e & 63;
@@ -520,6 +518,43 @@ __device__ void sort_keys(const BT& t, int64_t eo, int n, int32_t* kr, int64_t* 
   }
 }
 
+// the same network in LDS over packed keys: kri = roundReceived << 16 | id (both
+// below 65,535: the host checks, sentinel 0xFFFFFFFF), n padded to a power of two
+// P <= the arrays' size
+__device__ void sort_keys_lds(const BT& t, int64_t eo, int n, uint32_t* kri, int64_t* kc, uint64_t* ks) {
+  const int lane = threadIdx.x;
+  int P = 1;
+  while (P < n) P <<= 1;
+  for (int p = n + lane; p < P; p += 64) kri[p] = 0xFFFFFFFFu;
+  wsync();
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int q = lane; q < P / 2; q += 64) {
+        const int a = 2 * q - (q & (stride - 1));
+        const int b = a + stride;
+        const bool up = (a & size) == 0;
+        const uint32_t pa = kri[a], pb = kri[b];
+        const bool na = pa == 0xFFFFFFFFu, nb_ = pb == 0xFFFFFFFFu;
+        if (na && nb_) continue;
+        const int ra = (int)(pa >> 16), ia = (int)(pa & 0xFFFFu), rb = (int)(pb >> 16), ib = (int)(pb & 0xFFFFu);
+        const int64_t ca = na ? 0 : kc[a], cb = nb_ ? 0 : kc[b];
+        const uint64_t sa = na ? 0 : ks[a], sb = nb_ ? 0 : ks[b];
+        const bool b_lt_a = nb_ ? false : (na ? true : key_less(t, eo, rb, cb, sb, ib, ra, ca, sa, ia));
+        const bool a_lt_b = na ? false : (nb_ ? true : key_less(t, eo, ra, ca, sa, ia, rb, cb, sb, ib));
+        if (up ? b_lt_a : a_lt_b) {
+          kri[a] = pb;
+          kri[b] = pa;
+          kc[a] = cb;
+          kc[b] = ca;
+          ks[a] = sb;
+          ks[b] = sa;
+        }
+      }
+      wsync();
+    }
+  }
+}
+
 // ascending bitonic sorting network over M register values (M a power of two)
 template <int M>
 __device__ __forceinline__ void sort_regs(int64_t (&v)[M]) {
@@ -548,7 +583,8 @@ __device__ __forceinline__ void sort_regs(int64_t (&v)[M]) {
 // past UL entries live in global memory, where every mutation is also written.
 template <int NM>
 __global__ __launch_bounds__(64) void kb_consensus(BT t) {
-  constexpr int RW = 8, UL = 1536, KB = 768;
+  // KB: the LDS sort's capacity, a power of two (the network pads to one)
+  constexpr int RW = 8, UL = 1536, KB = 1024;
   const int g = blockIdx.x;
   const GDesc d = t.gd[g];
   const int N = t.N, SM = t.SM, lane = threadIdx.x, cc = t.ccap;
@@ -563,10 +599,12 @@ __global__ __launch_bounds__(64) void kb_consensus(BT t) {
   __shared__ int32_t rcntL[RW], verL[RW], thvL[RW];
   // the undetermined list: creator << 24 | index, and round (the id is chain[c][index])
   __shared__ int32_t Ur_s[UL], Ucp_s[UL];
-  __shared__ int32_t kr[KB], ki[KB];
+  __shared__ uint32_t kri[KB];  // roundReceived << 16 | id
   __shared__ int64_t kc[KB];
   __shared__ uint64_t ks[KB];
   if (t.scal[(int64_t)g * 8 + 6]) return;  // the rounds pass failed: nothing to decide
+  // packed LDS keys need ids and rounds below 65,535 (else the global-scratch sort)
+  const bool lds_keys = d.E < 0xFFFF && d.Rcap < 0xFFFF;
   int R = 0, lcr = -1, lcre = 0, nord = 0, nU = 0, n_prev = 0;
   int64_t ctx = 0;
   uint64_t cyc[6] = {0, 0, 0, 0, 0, 0};
@@ -866,11 +904,10 @@ __global__ __launch_bounds__(64) void kb_consensus(BT t) {
       const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
       if (found >= 0) {
         const int p = nb + __popcll(rec & below);
-        if (p < KB) {
-          kr[p] = found;
+        if (p < KB && lds_keys) {
+          kri[p] = (uint32_t)found << 16 | (uint32_t)x;
           kc[p] = med;
           ks[p] = s0;
-          ki[p] = x;
         }
         const int64_t so = 2 * eo + nord + p;
         st(&t.krr[so], found);
@@ -892,9 +929,9 @@ __global__ __launch_bounds__(64) void kb_consensus(BT t) {
     HGB_STAMP(3)
     // ---- FindOrder (hashgraph.go:723-760): sort the batch, append it ----
     if (nb > 0) {
-      if (nb <= KB) {
-        sort_keys<false>(t, eo, nb, kr, kc, ks, ki);
-        for (int p = lane; p < nb; p += 64) t.order[eo + nord + p] = ki[p];
+      if (nb <= KB && lds_keys) {
+        sort_keys_lds(t, eo, nb, kri, kc, ks);
+        for (int p = lane; p < nb; p += 64) t.order[eo + nord + p] = (int32_t)(kri[p] & 0xFFFFu);
       } else {
         // past KB keys: the same network on the graph's global scratch (2E entries
         // from 2 eo: nord + the padded size stays below 2E)

@@ -532,17 +532,21 @@ __global__ void __launch_bounds__(256) k_fdt_runs(Tables t, const int32_t* LAT, 
 
 // lowest chain-c position whose FD row a new event can change:
 // min over chains j with old events of LA[(j, olen_j - 1)][c] + 1
-__global__ void k_fd_qlo(Tables t, const int32_t* olen, const int32_t* len, int32_t* qlo) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= t.N) return;
-  int m = olen[c];  // the new positions themselves
-  for (int j = 0; j < t.N; j++) {
-    if (len[j] == olen[j]) continue;  // chain j got no new event
+// grid N blocks (chain c), thread j = chain j: one load per thread and a block
+// min (a thread looping over the N chains was a chain of 256 dependent-latency
+// loads: ~40 us per online call at N = 256)
+__global__ void __launch_bounds__(256) k_fd_qlo(Tables t, const int32_t* olen, const int32_t* len, int32_t* qlo) {
+  __shared__ int s_m;
+  const int c = blockIdx.x, j = threadIdx.x;
+  if (j == 0) s_m = olen[c];  // the new positions themselves
+  __syncthreads();
+  if (j < t.N && len[j] != olen[j]) {  // chain j got a new event
     const int ol = olen[j];
     const int v = ol > 0 ? la_at(t, j, ol - 1, c) + 1 : 0;
-    m = min(m, v);
+    atomicMin(&s_m, v);
   }
-  qlo[c] = max(0, m);
+  __syncthreads();
+  if (j == 0) qlo[c] = max(0, s_m);
 }
 
 }  // namespace hge

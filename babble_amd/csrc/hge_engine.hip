@@ -1016,7 +1016,7 @@ struct hge_engine {
         KLAUNCH(k_witness_bits, dim3(std::min(div_up(wmax * NW * G, 256), 8192)), dim3(256), 0,
                 st, t, s_newwit.p, k_rs + 2, N > 32 ? (const uint64_t*)d_ssc.p : nullptr, G);
       }
-      KLAUNCH(k_round_minw, dim3(div_up(Rcap, 256)), dim3(256), 0, st, t, 0,
+      KLAUNCH(k_round_minw, dim3(div_up(Rcap, 4)), dim3(256), 0, st, t, 0,
               (const int32_t*)k_rs, d_minw.p);
       h_minw.resize(Rcap + 2);
       d2h(h_minw.data(), d_minw.p, 4 * ((size_t)Rcap + 2));
@@ -1547,7 +1547,7 @@ struct hge_engine {
     // tiles past their grid, sized here for the new positions plus a tile)
     int span = 1;
     if (!fresh) {
-      KLAUNCH(k_fd_qlo, dim3(div_up(N, 256)), dim3(256), 0, st, t, olen, len, k_qlo);
+      KLAUNCH(k_fd_qlo, dim3(N), dim3(256), 0, st, t, olen, len, k_qlo);
       span = maxnew + 64;
     } else {
       for (int c = 0; c < N; c++) span = std::max(span, chain_len[c]);

@@ -831,8 +831,11 @@ __global__ void k_round_ranges(Tables t, const int32_t* len, const int32_t* rsta
 }
 
 // first witness id per round (monotone increasing in r); rounds [r0, R)
-__global__ void k_round_minw(Tables t, int r0, const int32_t* rstate, int32_t* minw) {
-  const int r = r0 + blockIdx.x * blockDim.x + threadIdx.x;
+// minw[r] = the lowest witness id of round r: one wave per round, lanes over the
+// creators (a thread per round looping over N creators was latency-bound: ~27 us
+// per online call at N = 256)
+__global__ void __launch_bounds__(256) k_round_minw(Tables t, int r0, const int32_t* rstate, int32_t* minw) {
+  const int r = r0 + blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   // the round count and overflow flag ride along at minw[Rcap..Rcap+1] (one readback)
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     minw[t.Rcap] = rstate[0];
@@ -840,11 +843,13 @@ __global__ void k_round_minw(Tables t, int r0, const int32_t* rstate, int32_t* m
   }
   if (rstate[1] || r >= rstate[0]) return;
   int m = INF32;
-  for (int c = 0; c < t.N; c++) {
+  for (int c = lane; c < t.N; c += 64) {
     const int w = t.W[(size_t)r * t.N + c];
     if (w >= 0) m = min(m, w);
   }
-  minw[r] = m;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = min(m, __shfl_xor(m, o));
+  if (lane == 0) minw[r] = m;
 }
 
 // strongly-see / see bitsets of each new witness y (round j >= 1) over the
@@ -1467,19 +1472,31 @@ __global__ void __launch_bounds__(256) k_seg_theta_wide(Tables t, const int32_t*
         // round see chain cx up to about the same point): bisect [min, max], not [0, 65535].
         // Values are LA + 1 (0: no ancestor on chain cx); the padding past nf is 0,
         // which no probe value mid >= 1 counts.
+        // every row's value is loaded before the first is used: the loads are
+        // branch-free, so they stay in
+        // flight together instead of one dependent latency per group of 8 rows
+        // (an online call's few segments were ~90 us of latency at N = 256);
+        // rows past nf read row 0 (allocated, any value) and are masked
         int vmin = 65535, vmax = 0;
-        for (int k0 = 0; k0 < nf; k0 += 8) {
-          uint32_t w[4];
+        constexpr int MAXG = NWT * 8;  // nf <= 64 NWT rows, 8 per group
+        uint32_t wv[MAXG][4];
+#pragma unroll
+        for (int gI = 0; gI < MAXG; gI++) {
 #pragma unroll
           for (int u = 0; u < 8; u += 2) {
-            const int a = k0 + u < nf ? la_row(t, (size_t)s_row[k0 + u], cx) + 1 : -1;
-            const int b = k0 + u + 1 < nf ? la_row(t, (size_t)s_row[k0 + u + 1], cx) + 1 : -1;
+            const int k = gI * 8 + u;
+            const int ra = k < nf ? s_row[k] : 0, rb = k + 1 < nf ? s_row[k + 1] : 0;  // row 0: allocated
+            const int la_a = la_row(t, (size_t)ra, cx), la_b = la_row(t, (size_t)rb, cx);
+            const int a = k < nf ? la_a + 1 : -1;
+            const int b = k + 1 < nf ? la_b + 1 : -1;
+            wv[gI][u >> 1] = (uint32_t)max(a, 0) | ((uint32_t)max(b, 0) << 16);
             if (a >= 0) { vmin = min(vmin, a); vmax = max(vmax, a); }
             if (b >= 0) { vmin = min(vmin, b); vmax = max(vmax, b); }
-            w[u >> 1] = (uint32_t)max(a, 0) | ((uint32_t)max(b, 0) << 16);
           }
-          sv[k0 >> 3][cx] = make_uint4(w[0], w[1], w[2], w[3]);
         }
+#pragma unroll
+        for (int gI = 0; gI < MAXG; gI++)
+          if (gI * 8 < nf) sv[gI][cx] = make_uint4(wv[gI][0], wv[gI][1], wv[gI][2], wv[gI][3]);
         if (((nf + 7) >> 3) & 1) sv[(nf + 7) >> 3][cx] = make_uint4(0, 0, 0, 0);  // even group count
         int th = (int)0x80000000;
         if (nf > 0) {

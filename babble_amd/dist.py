@@ -119,6 +119,8 @@ def split_run(eng, rank, world, exchange, halo_rounds=8, stats=None):
     (TorchExchange / ThreadExchange).  Returns the number of events ordered
     (identical to eng.run()); stats["fallback"] counts unsplit replays."""
     from .engine import HGE_ERR_SPLIT, HgeError
+    if world <= 1:  # nothing to shard: the one-GPU replay
+        return eng.run()
     plan = split_plan(eng.call_events(), eng.event_count(), world,
                       halo_rounds * ROUND_EVENTS_PER_PARTICIPANT * eng.n)
     eng.split_plan(rank, world, plan)

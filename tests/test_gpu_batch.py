@@ -35,6 +35,8 @@ CASES = [
     (32, 3000, 32, 4, 10, 0.05, 0.5, 0),     # config 5's graph shape with cascades
     (32, 4000, 32, 16, 10, 0.05, 0.0, 0),
     (32, 2500, 2500, 22, 0, 0.0, 0.0, 0),    # one call at N = 32
+    (32, 5000, 700, 25, 0, 0.0, 0.0, 0),     # 513-1,024-key batches: the LDS sort pads to 1,024
+    (16, 4000, 900, 26, 2, 0.05, 0.5, 0),
     (33, 3000, 50, 17, 0, 0.0, 0.0, 3),
     (48, 5000, 48, 23, 5, 0.05, 0.5, 0),
     (64, 6000, 64, 18, 0, 0.0, 0.0, 0),
