@@ -130,13 +130,18 @@ __global__ void __launch_bounds__(256) k_la_sweep(Tables t, const int2* segs, in
 //   phase 3: the rows to LA, coalesced.
 // m * NP <= LASEQ_MAX (the host checks; larger batches take the sweeps).
 constexpr int LASEQ_MAX = 8192;
+// It also fills the chain table for the batch first (k_chain_fill's work: one
+// launch less per online call); the barrier makes those global writes visible to
+// the block.
 template <int NP>
-__global__ void __launch_bounds__(256) k_la_seq(Tables t, int n0, int n1) {
+__global__ void __launch_bounds__(256) k_la_seq(Tables t, int n0, int n1, const UpEv* up, UpDst dst) {
   __shared__ int rows[LASEQ_MAX];
   __shared__ int2 par[LASEQ_MAX / NP];
   constexpr int G = 256 / NP;
   const int N = t.N, m = n1 - n0;
   const int tid = threadIdx.x, i = tid % NP;
+  for (int x = n0 + tid; x < n1; x += 256) chain_fill_one(t, x, n0, up, dst);
+  __syncthreads();
   for (int e = tid / NP; e < m; e += G) {
     const int x = n0 + e;
     const int cx = t.creator[x], px = t.index[x];

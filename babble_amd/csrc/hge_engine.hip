@@ -177,7 +177,7 @@ struct hge_engine {
   DBuf<uint8_t> d_FDTW;  // N > 16: per (row, 64-column tile) out-of-range flags of d_FDTD
   DBuf<int32_t> d_WLA;   // N > 16: round frontier rows transposed (k_witness_la)
   DBuf<uint64_t> d_ssc, s_gran;
-  DBuf<int32_t> s_bseg, s_choff;
+  DBuf<int32_t> s_bseg;
   DBuf<uint64_t> s_H;                // speculative walk: epoch-tagged histories
   DBuf<int32_t> s_hn, s_hres;        // rows written + progress hints, merge results
   uint32_t walk_epoch = 0;
@@ -512,7 +512,7 @@ struct hge_engine {
     if (N > 32) d_ssc.grow_keep(nr * N * NW, oldn * NW, st, 0);
     d_fame.grow_keep(nr * N, oldn, st, 0);
     d_rcnt.grow_keep(nr, Rcap, st, 0);
-    d_minw.need(nr + 2);  // + the round count and overflow flag (k_round_minw)
+    d_minw.need(nr + 4);  // + round count, overflow flag, lowest candidate round, hand-off error (k_round_minw)
     // C must be INF32 beyond the old rows
     fill_i32(d_C.p + oldn, (int64_t)(nr - Rcap) * N, INF32);
     sync();
@@ -534,6 +534,7 @@ struct hge_engine {
     h_chain.assign(N, {});
     coords_len.assign(N, 0);
     n_events = n_dev = n_coords = n_divided = 0;
+    up_n0 = up_n1 = -1;
     R = 0;
     R_set = 0;
     h_minw.clear();
@@ -632,6 +633,9 @@ struct hge_engine {
     chain_last[e.creator] = (int32_t)id;
   }
 
+  // a packed upload of the events [up_n0, up_n1) waiting for k_chain_fill (upload())
+  DBuf<UpEv> s_up;
+  int64_t up_n0 = -1, up_n1 = -1;
   void upload() {
     if (n_dev == n_events) return;
     ensure_events(n_events);
@@ -639,6 +643,30 @@ struct hge_engine {
     for (int c = 0; c < N; c++) maxlen = std::max(maxlen, chain_len[c]);
     ensure_ccap(maxlen + 1);
     const int64_t a = n_dev, m = n_events - n_dev;
+    if (m <= 16384 && a == n_coords) {
+      // a small batch (an online call): one packed record per event through the
+      // pinned arena, unpacked by the coordinate step's k_chain_fill (eight copies
+      // from pageable memory were ~25 us of an online call)
+      std::vector<UpEv> up((size_t)m);
+      for (int64_t i = 0; i < m; i++) {
+        UpEv& r = up[(size_t)i];
+        const size_t x = (size_t)(a + i);
+        r.creator = h_creator[x];
+        r.index = h_index[x];
+        r.sp = h_sp[x];
+        r.op = h_op[x];
+        r.ntx = h_ntx[x];
+        r.coin = h_coin[x];
+        r.ts = h_ts[x];
+        for (int k = 0; k < 4; k++) r.S[k] = h_S[4 * x + k];
+      }
+      s_up.need((size_t)m);
+      h2d(s_up.p, up.data(), sizeof(UpEv) * (size_t)m);
+      up_n0 = a;
+      up_n1 = n_events;
+      n_dev = n_events;
+      return;
+    }
     HIPCHK(hipMemcpyAsync(d_creator.p + a, h_creator.data() + a, 4 * m, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_index.p + a, h_index.data() + a, 4 * m, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_sp.p + a, h_sp.data() + a, 4 * m, hipMemcpyHostToDevice, st));
@@ -874,7 +902,15 @@ struct hge_engine {
     k_segs = (int2*)(s_kctl.p + o_seg);
     k_segbase = s_kctl.p + o_sb;
     k_fd = split_on() ? s_kctl.p + o_fd : nullptr;
-    KLAUNCH(k_chain_fill, dim3(div_up((int)(n1 - n0), 256)), dim3(256), 0, st, t, (int)n0, (int)n1);
+    {
+      const bool packed = up_n0 == n0 && up_n1 == n1;
+      fill_up = packed ? (const UpEv*)s_up.p : (const UpEv*)nullptr;
+      fill_dst = UpDst{d_creator.p, d_index.p, d_sp.p, d_op.p, d_ntx.p, d_ts.p, d_S.p, d_coin.p};
+      up_n0 = up_n1 = -1;
+      if (!la_seq_ok(n1 - n0))  // (k_la_seq fills the chain table itself)
+        KLAUNCH(k_chain_fill, dim3(div_up((int)(n1 - n0), 256)), dim3(256), 0, st, t, (int)n0, (int)n1, fill_up,
+                fill_dst);
+    }
     coords_sweep(t, (int)segs.size(), SEG, maxnew, fresh);
     cs_pending = true;
     cs_fresh = fresh;
@@ -915,7 +951,8 @@ struct hge_engine {
           // stay on the device (k_frontier_start writes them; k_fss loops over the
           // count, k_rounds_walk stands down at INF32): no host round trip
           s_fst.need(N + 1);
-          KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p, k_lo);
+          KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p, k_lo,
+                  (int32_t*)nullptr, (uint64_t*)nullptr, 0);
           const int64_t guess = m + 16 * (int64_t)N;  // the grid loops past it
 #define FSSD(NPC, LPC, B)                                                                              \
   KLAUNCH(k_fss<NPC>, dim3((unsigned)std::min<int64_t>(1024, div_up(guess * NPC, 256))), dim3(256), 0, st, t, \
@@ -932,7 +969,8 @@ struct hge_engine {
         std::vector<int32_t> fst(N + 1, 0);
         if (!fresh) {
           s_fst.need(N + 1);
-          KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p, (int32_t*)nullptr);
+          KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p, (int32_t*)nullptr,
+                  (int32_t*)nullptr, (uint64_t*)nullptr, 0);
           readback(fst.data(), s_fst.p, N + 1);
         }
         const int rlo = fst[0];
@@ -1017,24 +1055,24 @@ struct hge_engine {
                 st, t, s_newwit.p, k_rs + 2, N > 32 ? (const uint64_t*)d_ssc.p : nullptr, G);
       }
       KLAUNCH(k_round_minw, dim3(div_up(Rcap, 4)), dim3(256), 0, st, t, 0,
-              (const int32_t*)k_rs, d_minw.p);
-      h_minw.resize(Rcap + 2);
-      d2h(h_minw.data(), d_minw.p, 4 * ((size_t)Rcap + 2));
+              (const int32_t*)k_rs, d_minw.p, (const int32_t*)coop_err_src);
       // the lowest round of the next batch's candidates (the undetermined list and the
       // events the next divide appends), read with the round count
       // (a fresh replay's candidates start at event 0, round 0: nothing to read)
       if (!fresh) {
-        s_small.need(16);
-        h2d(s_small.p + 9, &kInf, 4);
         if (n_und > 0)
           KLAUNCH(k_min_round, dim3(div_up(n_und, 256)), dim3(256), 0, st, d_round.p, d_und.p, (int)n_und,
-                  s_small.p + 9);
+                  d_minw.p + Rcap + 2);
         if (n1 > n_divided)
           KLAUNCH(k_min_round_range, dim3(div_up(n1 - n_divided, 256)), dim3(256), 0, st, d_round.p,
-                  (int)n_divided, (int)n1, s_small.p + 9);
-        d2h(&mnr_pre, s_small.p + 9, 4);
+                  (int)n_divided, (int)n1, d_minw.p + Rcap + 2);
       }
+      h_minw.resize(Rcap + 4);
+      d2h(h_minw.data(), d_minw.p, 4 * ((size_t)Rcap + 4));
       sync();
+      if (!fresh) mnr_pre = h_minw[Rcap + 2];
+      if (coop_err_check && coop_err_src) coop_err = h_minw[Rcap + 3];
+      coop_err_src = nullptr;
       mnr_key[0] = fresh ? -1 : n_und;
       mnr_key[1] = n_divided;
       mnr_key[2] = n1;
@@ -1169,12 +1207,17 @@ struct hge_engine {
   // (the caller holds frontier_lock() until the stream has drained)
   int32_t coop_err = 0;
   bool coop_err_check = false;
+  const int32_t* coop_err_src = nullptr;  // the walk's error flag on the device (read with minw)
   bool frontier_fallback = false;  // k_round_step32 for good after a hand-off timeout
   int64_t n_frontier_fallbacks = 0;
   void rounds_coop(bool fresh) {
     Tables t = tables();
     s_fst.need(N + 1);
-    KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p, (int32_t*)nullptr);
+    // (the hand-off flags and granules are zeroed by k_frontier_start)
+    s_bar.need(2);
+    s_gran.need(2 * (size_t)N);
+    KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p, (int32_t*)nullptr,
+            s_bar.p, (uint64_t*)s_gran.p, 2 * N);
     // the lowest round to recompute: read back for a fresh state (the walkers and the
     // joined rows need it on the host), else read by the frontier kernel itself,
     // which stands down at INF32 (no round trip)
@@ -1208,10 +1251,6 @@ struct hge_engine {
     // passes 65,534 events, so this packed walk never sees one; the check guards it
     if (maxlen >= 0xFFFF)
       throw EngineError(HGE_ERR_INTERNAL, "packed rounds walk reached a chain past 65,534 events");
-    s_bar.need(2);
-    s_gran.need(2 * (size_t)N);
-    HIPCHK(hipMemsetAsync(s_bar.p, 0, 8, st));
-    HIPCHK(hipMemsetAsync(s_gran.p, 0, 16 * (size_t)N, st));
     const int32_t* FDT = d_FDT.p;
     const int32_t* olen = k_len;
     const int32_t* len = k_len + N;
@@ -1279,6 +1318,7 @@ struct hge_engine {
         h2d(rstate, down, 8);
         coop_err = 1;
         coop_err_check = true;
+        coop_err_src = nullptr;
         return;
       }
       readback(&hres[1], resume, 1);
@@ -1327,8 +1367,8 @@ struct hge_engine {
       h2d(err, &one, 4);
       h2d(rstate + 1, &down, 4);
     }
-    // the hand-off error flag comes back with the round count (coords_b)
-    d2h(&coop_err, s_bar.p + 1, 4);
+    // the hand-off error flag comes back with the round count (coords_b, k_round_minw)
+    coop_err_src = s_bar.p + 1;
     coop_err_check = true;
     dbg_dump();
   }
@@ -1363,7 +1403,8 @@ struct hge_engine {
   void rounds_step32() {
     Tables t = tables();
     s_fst.need(N + 1);
-    KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p, (int32_t*)nullptr);
+    KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p, (int32_t*)nullptr,
+            (int32_t*)nullptr, (uint64_t*)nullptr, 0);
     int32_t rlo = INF32;
     readback(&rlo, s_fst.p, 1);
     if (rlo == INF32) return;
@@ -1451,6 +1492,12 @@ struct hge_engine {
   }
 
   // coordinates: chain-prefix sweeps + transposes (hge_coords.hip)
+  // the one-pass lastAncestors kernel (k_la_seq) takes batches of m new events at N <= 32
+  bool la_seq_ok(int64_t m) const {
+    return !sweep16() && N <= 32 && m > 0 && m * (N <= 16 ? 16 : 32) <= LASEQ_MAX && !getenv("HGE_NO_LASEQ");
+  }
+  const UpEv* fill_up = nullptr;  // coords_a -> the chain-table fill (packed upload or the tables)
+  UpDst fill_dst{};
   void coords_sweep(Tables t, int nseg, int SEG, int maxnew, bool fresh) {
     const int32_t* olen = k_len;
     const int32_t* len = k_len + N;
@@ -1462,16 +1509,16 @@ struct hge_engine {
     const bool p16 = sweep16();
     // skip segments whose inputs did not change in the previous sweep
     const bool SKIP = true;
-    const int NPs = N <= 16 ? 16 : 32;
     const int64_t mnew = n_events - n_coords;
     if (p16 && la_windows()) {
       la_windows_run(t);
-    } else if (!p16 && N <= 32 && mnew * NPs <= LASEQ_MAX && !getenv("HGE_NO_LASEQ")) {
-      // a small batch (an online call): one exact pass in insertion order
-      if (NPs == 16)
-        KLAUNCH(k_la_seq<16>, dim3(1), dim3(256), 0, st, t, (int)n_coords, (int)n_events);
+    } else if (la_seq_ok(mnew)) {
+      // a small batch (an online call): one exact pass in insertion order, the chain
+      // table filled by the same kernel
+      if (N <= 16)
+        KLAUNCH(k_la_seq<16>, dim3(1), dim3(256), 0, st, t, (int)n_coords, (int)n_events, fill_up, fill_dst);
       else
-        KLAUNCH(k_la_seq<32>, dim3(1), dim3(256), 0, st, t, (int)n_coords, (int)n_events);
+        KLAUNCH(k_la_seq<32>, dim3(1), dim3(256), 0, st, t, (int)n_coords, (int)n_events, fill_up, fill_dst);
       n_sweeps = 1;
     } else {
     int32_t* dirty = nullptr;
@@ -1725,9 +1772,10 @@ struct hge_engine {
     int32_t* o_cc = s_out.p + 8;
     int32_t* o_ids = s_out.p + 8 + ncalls;
     unsigned long long* o_ntx = (unsigned long long*)(s_out.p + 4);
-    HIPCHK(hipMemsetAsync(s_out.p, 0, 4 * (8 + (size_t)ncalls), st));
-    if (lcr_dev)  // the new LastConsensusRound into the results block (o_cnt[3])
-      HIPCHK(hipMemcpyAsync(s_out.p + 3, c_flags + 1, 4, hipMemcpyDeviceToDevice, st));
+    // the results header zeroed, with the new LastConsensusRound (o_cnt[3]) when the
+    // device holds it (one launch in place of a memset and a copy)
+    KLAUNCH(k_out_init, dim3(div_up(8 + ncalls, 256)), dim3(256), 0, st, s_out.p, 8 + ncalls,
+            lcr_dev ? (const int32_t*)(c_flags + 1) : (const int32_t*)nullptr);
     if (ord) {
       if (nr > 0) {
         SegInfo si;
@@ -1767,9 +1815,19 @@ struct hge_engine {
             (const int32_t*)s_seground.p, (const int32_t*)c_sgo, (const int32_t*)s_segcnt.p, nr,   \
             (const uint64_t*)s_segfws.p, s_theta.p);                                               \
   else                                                                                             \
-    KLAUNCH(k_seg_theta_wide<B>, dim3(std::min(nr, 4096)), dim3(256), 0, st, t,                    \
+    KLAUNCH(k_seg_theta_wide<B>, dim3(std::min(nr, 4096), nr < 64 ? 8 : 2), dim3(256), 0, st, t,   \
             (const int32_t*)s_seground.p, (const int32_t*)c_sgo, (const int32_t*)s_segcnt.p, nr,   \
-            (const uint64_t*)s_segfws.p, s_theta.p);
+            (const uint64_t*)s_segfws.p, s_theta.p, dbg_p());
+        // the frontier rows transposed (WLA) for the batch's rounds: theta (N > 64) and
+        // the median (N > 16) read them
+        const bool wla = N > 16 && R_last > rr_lo;
+        if (wla) {
+          d_WLA.need((size_t)Rcap * N * N);
+          Tables tw = tables();
+          KLAUNCH(k_witness_la, dim3(div_up(N, 64), div_up(N, 64), R_last - rr_lo), dim3(256), 0, st, tw,
+                  rr_lo);
+          t = tables();
+        }
         if (G == 16) {
           SEG1(16, 1)
         } else if (G == 32) {
@@ -1788,11 +1846,28 @@ struct hge_engine {
         }
 #undef SEG1
 #undef THW
+        if (getenv("HGE_SEG_DEBUG")) {  // diagnostics: the segments theta walks this batch
+          std::vector<int32_t> sc(nr);
+          readback(sc.data(), s_segcnt.p, nr);
+          int tot = 0, mx = 0;
+          for (int v : sc) {
+            tot += v;
+            mx = std::max(mx, v);
+          }
+          fprintf(stderr, "[hge seg] calls %d rounds %d segments %d max per round %d\n", ncalls, nr, tot, mx);
+          if (dbg_on && s_dbg.p) {
+            uint64_t v[16];
+            readback(v, s_dbg.p, 16);
+            fprintf(stderr, "[hge theta] segments %llu cycles: rows %llu staging %llu bisection %llu\n",
+                    (unsigned long long)v[15], (unsigned long long)v[12], (unsigned long long)v[13],
+                    (unsigned long long)v[14]);
+          }
+        }
         // round-received per candidate
         s_recv.need(ncand);
         s_rr.need(ncand);
         s_cts.need(ncand);
-        recv_dispatch(t, cand, ncand, ncalls, rr_lo, R_last, fresh_und);
+        recv_dispatch(t, cand, ncand, ncalls, rr_lo, R_last, fresh_und, wla);
       } else {
         s_recv.need(ncand);
         HIPCHK(hipMemsetAsync(s_recv.p, 0xFF, 4 * ncand, st));
@@ -2035,6 +2110,10 @@ struct hge_engine {
   }
 
   void scan_large(const int32_t* in, int32_t* out, int n, int32_t* total) {
+    if (n <= 16384) {  // one block (an online call's candidates): one launch, not three
+      KLAUNCH(k_scan_small, dim3(1), dim3(1024), 0, st, in, out, n, total);
+      return;
+    }
     const int nb = div_up(n, 1024);
     s_part.need(2 * (size_t)nb + 2);
     KLAUNCH(k_scan_blocks, dim3(nb), dim3(256), 0, st, in, out, n, s_part.p);
@@ -2112,7 +2191,7 @@ struct hge_engine {
   }
 
   void recv_dispatch(const Tables& t, const int32_t* cand, int ncand, int ncalls, int rr_lo,
-                     int R_last, bool fresh) {
+                     int R_last, bool fresh, bool wla_done) {
     // N > 16: the median is a wave-wide radix select (k_median_wave) over coalesced
     // rows: the round frontier rows transposed (WLA, k_witness_la, for every round a
     // candidate can receive) and the FD timestamp offsets (FDTD).  A fresh replay's
@@ -2120,18 +2199,10 @@ struct hge_engine {
     const bool wmed = N > 16;
     const bool ident = fresh && cand == d_und.p && (int64_t)ncand == n_events;
     int32_t* bseg = nullptr;
-    const int32_t* choff = nullptr;
     if (wmed) {
       s_bseg.need(ncand);
       bseg = s_bseg.p;
-      if (ident && !getenv("HGE_MED_EVORDER")) {  // chain-major waves (k_median_wave)
-        std::vector<int32_t> off(N + 1, 0);
-        for (int c = 0; c < N; c++) off[c + 1] = off[c] + chain_len[c];
-        s_choff.need(N + 1);
-        h2d(s_choff.p, off.data(), 4 * (size_t)(N + 1));
-        choff = s_choff.p;
-      }
-      if (R_last > rr_lo) {
+      if (R_last > rr_lo && !wla_done) {
         d_WLA.need((size_t)Rcap * N * N);
         Tables tw = tables();
         KLAUNCH(k_witness_la, dim3(div_up(N, 64), div_up(N, 64), R_last - rr_lo), dim3(256), 0, st, tw,
@@ -2149,7 +2220,7 @@ struct hge_engine {
     if (wmed)                                                                                    \
       KLAUNCH(k_median_wave<B>, dim3(div_up(ncand, 4 * HGE_MW_E)), dim3(256), 0, st, tables(),              \
               ident ? (const int32_t*)nullptr : cand, ncand, s_recv.p, s_rr.p, bseg, s_segfws.p,  \
-              s_cts.p, choff);                                                                   \
+              s_cts.p);                                                                          \
     break;
       RCASE(1)
       RCASE(2)

@@ -172,15 +172,68 @@ __global__ void k_scan_add(int32_t* out, int n, const int32_t* partial_scanned) 
   if (i < n) out[i] += partial_scanned[i / 1024];
 }
 
-// chain table: chain[c][index] = id for the new events
-__global__ void k_chain_fill(Tables t, int n0, int n1) {
-  const int x = n0 + blockIdx.x * blockDim.x + threadIdx.x;
-  if (x >= n1) return;
-  const size_t at = (size_t)t.creator[x] * t.ccap + t.index[x];
+// A small batch's event fields uploaded as one packed record per event (one copy
+// instead of eight; hge_engine.hip upload()), unpacked by k_chain_fill.
+struct UpEv {
+  int32_t creator, index, sp, op, ntx, coin;
+  int64_t ts;
+  uint64_t S[4];
+};
+struct UpDst {
+  int32_t *creator, *index, *sp, *op, *ntx;
+  int64_t* ts;
+  uint64_t* S;
+  uint8_t* coin;
+};
+
+// a batch's results header: out[0, n) = 0, out[3] = *lcr when given
+__global__ void k_out_init(int32_t* out, int n, const int32_t* lcr) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (i == 3 && lcr) ? *lcr : 0;
+}
+
+// chain table: chain[c][index] = id for the new events.  up (non-null): the new
+// events' fields arrive packed (record x - n0) and are unpacked into their tables
+// here; an other-parent inside the batch is read from its record (its table entry
+// is being written by another thread)
+__device__ __forceinline__ void chain_fill_one(const Tables& t, int x, int n0, const UpEv* up, const UpDst& dst) {
+  int cx, ix, o;
+  int64_t ts;
+  if (up) {
+    const UpEv r = up[x - n0];
+    cx = r.creator;
+    ix = r.index;
+    o = r.op;
+    ts = r.ts;
+    dst.creator[x] = cx;
+    dst.index[x] = ix;
+    dst.sp[x] = r.sp;
+    dst.op[x] = o;
+    dst.ntx[x] = r.ntx;
+    dst.ts[x] = ts;
+    dst.coin[x] = (uint8_t)r.coin;
+#pragma unroll
+    for (int k = 0; k < 4; k++) dst.S[4 * (size_t)x + k] = r.S[k];
+  } else {
+    cx = t.creator[x];
+    ix = t.index[x];
+    o = t.op[x];
+    ts = t.ts[x];
+  }
+  const size_t at = (size_t)cx * t.ccap + ix;
   t.chain[at] = x;
-  t.tsch[at] = t.ts[x];
-  const int o = t.op[x];
-  t.opcp[at] = o >= 0 ? make_int2(t.creator[o], t.index[o]) : make_int2(-1, -1);
+  t.tsch[at] = ts;
+  int2 oc = make_int2(-1, -1);
+  if (o >= 0) {
+    if (up && o >= n0) oc = make_int2(up[o - n0].creator, up[o - n0].index);
+    else oc = make_int2(t.creator[o], t.index[o]);
+  }
+  t.opcp[at] = oc;
+}
+
+__global__ void k_chain_fill(Tables t, int n0, int n1, const UpEv* up, UpDst dst) {
+  const int x = n0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (x < n1) chain_fill_one(t, x, n0, up, dst);
 }
 
 // HGE_STAMPS diagnostics: shader-clock stamp, ordered with the code around it
@@ -696,9 +749,14 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* 
 // lo_off (non-null): the k_fss rows of the walk from r_lo, [0, N) the start
 // positions, [N, 2N] their prefix offsets (the candidates' count last), written here
 // so that an online call at N <= 32 needs no host round trip for them
+// zbar / zgran (non-null): the wide rounds walk's hand-off flags and its 2 ngran
+// granules, zeroed here in place of two memsets
 __global__ void k_frontier_start(Tables t, const int32_t* olen, const int32_t* len,
                                  int32_t* out /* [0] rlo, [1..N] start positions */,
-                                 int32_t* lo_off = nullptr) {
+                                 int32_t* lo_off, int32_t* zbar, uint64_t* zgran, int ngran) {
+  if (zbar && threadIdx.x < 2) zbar[threadIdx.x] = 0;
+  if (zgran)
+    for (int i = threadIdx.x; i < ngran; i += blockDim.x) zgran[i] = 0;
   __shared__ int s_rlo;
   const int N = t.N;
   if (threadIdx.x == 0) s_rlo = INF32;
@@ -834,12 +892,18 @@ __global__ void k_round_ranges(Tables t, const int32_t* len, const int32_t* rsta
 // minw[r] = the lowest witness id of round r: one wave per round, lanes over the
 // creators (a thread per round looping over N creators was latency-bound: ~27 us
 // per online call at N = 256)
-__global__ void __launch_bounds__(256) k_round_minw(Tables t, int r0, const int32_t* rstate, int32_t* minw) {
+__global__ void __launch_bounds__(256) k_round_minw(Tables t, int r0, const int32_t* rstate, int32_t* minw,
+                                                    const int32_t* err_in) {
   const int r = r0 + blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  // the round count and overflow flag ride along at minw[Rcap..Rcap+1] (one readback)
+  // the round count and overflow flag ride along at minw[Rcap..Rcap+1], the next
+  // batch's lowest candidate round at [Rcap+2] (INF32 here, lowered by k_min_round*
+  // after this kernel) and the rounds walk's hand-off error flag at [Rcap+3]: one
+  // readback for all of them
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     minw[t.Rcap] = rstate[0];
     minw[t.Rcap + 1] = rstate[1];
+    minw[t.Rcap + 2] = INF32;
+    minw[t.Rcap + 3] = err_in ? *err_in : 0;
   }
   if (rstate[1] || r >= rstate[0]) return;
   int m = INF32;
@@ -1422,26 +1486,34 @@ __global__ void __launch_bounds__(256) k_segments_1p(Tables t, int rr_lo, int nr
   if (valid && d == 0) segcnt[qi] = nseg;
 }
 
-// theta for N > 64: one 256-thread block per round, its segments in turn
-// (thread = creator cx).
-// The famous witnesses' lastAncestors rows are staged in LDS as uint16
-// (position + 1; chains are < 65535 long on the wide path), then each thread
-// bisects the value domain of its column for the (|fws|/2 + 1)-th largest.
+// theta for N > 64: one 256-thread block per (round, segment stride), thread =
+// creator cx.  The famous witnesses' lastAncestors values of column cx (from WLA,
+// which k_witness_la has written for the batch's rounds before this kernel) are
+// staged in LDS as uint16 (position + 1; chains are < 65535 long on the wide path),
+// then each thread bisects the value domain of its column for the (|fws|/2 + 1)-th
+// largest.
 template <int NWT>
 __global__ void __launch_bounds__(256) k_seg_theta_wide(Tables t, const int32_t* seg_round,
                                                         const int32_t* segoff, const int32_t* segcnt,
                                                         int nr, const uint64_t* seg_fws,
-                                                        int32_t* theta) {
+                                                        int32_t* theta, uint64_t* dbg) {
   // [famous k / 8][cx]: 8 values of a column per 16 bytes, as uint16 pairs
   __shared__ uint4 sv[32][256];
   __shared__ int s_row[256];
   __shared__ int s_nf;
   const int N = t.N;
   const int tid = threadIdx.x;
-  // one block per round (grid-stride), its segments [segoff[q], segoff[q] + segcnt[q]) in turn
+  // blocks (x, y): rounds x, x + gridDim.x, ... (grid-stride) and, of each round's
+  // segments [segoff[q], segoff[q] + segcnt[q]), those l = y, y + gridDim.y, ...
+  // (an online call decides a few rounds of a few segments each: one block per
+  // round left them serial, ~90 us per call at N = 256)
   for (int q = blockIdx.x; q < nr; q += gridDim.x) {
     const int cnt = segcnt[q];
-    for (int l = 0; l < cnt; l++) {
+    for (int l = blockIdx.y; l < cnt; l += gridDim.y) {
+      // HGE_STAMPS diagnostics (block (0, 0), thread 0): cycles of the row list,
+      // the staging and the bisection into dbg[12..14], segments into dbg[15]
+      const bool stmp = dbg && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0;
+      uint64_t ts0 = stmp ? __builtin_amdgcn_s_memtime() : 0, ts1 = 0, ts2 = 0;
       const int sg = segoff[q] + l;
       const int i = seg_round[sg];
       // the famous witnesses' rows, in ascending creator order: thread d places
@@ -1459,12 +1531,12 @@ __global__ void __launch_bounds__(256) k_seg_theta_wide(Tables t, const int32_t*
           int rank = __popcll(fw[d >> 6] & ((1ull << (d & 63)) - 1));
 #pragma unroll
           for (int w = 0; w < NWT; w++) rank += w < (d >> 6) ? __popcll(fw[w]) : 0;
-          const int x = t.W[(size_t)i * N + d];
-          s_row[rank] = d * t.ccap + t.index[x];
+          s_row[rank] = d;  // the famous witness of chain d: its LA row is WLA[i][.][d]
         }
         if (tid == 0) s_nf = nfw;
       }
       __syncthreads();
+      if (stmp) ts1 = __builtin_amdgcn_s_memtime();
       const int nf = s_nf;
       const int cx = tid;
       if (cx < N) {
@@ -1472,32 +1544,30 @@ __global__ void __launch_bounds__(256) k_seg_theta_wide(Tables t, const int32_t*
         // round see chain cx up to about the same point): bisect [min, max], not [0, 65535].
         // Values are LA + 1 (0: no ancestor on chain cx); the padding past nf is 0,
         // which no probe value mid >= 1 counts.
-        // every row's value is loaded before the first is used: the loads are
-        // branch-free, so they stay in
-        // flight together instead of one dependent latency per group of 8 rows
-        // (an online call's few segments were ~90 us of latency at N = 256);
-        // rows past nf read row 0 (allocated, any value) and are masked
+        // the famous witnesses' LA values of column cx from the frontier rows transposed
+        // (k_witness_la: WLA[i][cx][d] = LA[(d, C[i][d])][cx], the witness of round i on
+        // chain d sits at C[i][d]): one contiguous row per thread.  Gathering the
+        // witnesses' own LA16 rows (one page each) cost ~160k cycles per segment in
+        // dependent latencies at N = 256 (HGE_STAMPS, profiles/r04), 80 us per online call.
+        const int32_t* wrow = t.WLA + ((size_t)i * N + cx) * N;
         int vmin = 65535, vmax = 0;
-        constexpr int MAXG = NWT * 8;  // nf <= 64 NWT rows, 8 per group
-        uint32_t wv[MAXG][4];
-#pragma unroll
-        for (int gI = 0; gI < MAXG; gI++) {
+        for (int k0 = 0; k0 < nf; k0 += 8) {
+          uint32_t w[4];
 #pragma unroll
           for (int u = 0; u < 8; u += 2) {
-            const int k = gI * 8 + u;
-            const int ra = k < nf ? s_row[k] : 0, rb = k + 1 < nf ? s_row[k + 1] : 0;  // row 0: allocated
-            const int la_a = la_row(t, (size_t)ra, cx), la_b = la_row(t, (size_t)rb, cx);
-            const int a = k < nf ? la_a + 1 : -1;
-            const int b = k + 1 < nf ? la_b + 1 : -1;
-            wv[gI][u >> 1] = (uint32_t)max(a, 0) | ((uint32_t)max(b, 0) << 16);
+            const int a = k0 + u < nf ? wrow[s_row[k0 + u]] + 1 : -1;
+            const int b = k0 + u + 1 < nf ? wrow[s_row[k0 + u + 1]] + 1 : -1;
             if (a >= 0) { vmin = min(vmin, a); vmax = max(vmax, a); }
             if (b >= 0) { vmin = min(vmin, b); vmax = max(vmax, b); }
+            w[u >> 1] = (uint32_t)max(a, 0) | ((uint32_t)max(b, 0) << 16);
           }
+          sv[k0 >> 3][cx] = make_uint4(w[0], w[1], w[2], w[3]);
         }
-#pragma unroll
-        for (int gI = 0; gI < MAXG; gI++)
-          if (gI * 8 < nf) sv[gI][cx] = make_uint4(wv[gI][0], wv[gI][1], wv[gI][2], wv[gI][3]);
         if (((nf + 7) >> 3) & 1) sv[(nf + 7) >> 3][cx] = make_uint4(0, 0, 0, 0);  // even group count
+        if (stmp) {
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          ts2 = __builtin_amdgcn_s_memtime();
+        }
         int th = (int)0x80000000;
         if (nf > 0) {
           const int kk = nf / 2 + 1;  // k-th largest = largest v with count(>= v) >= kk
@@ -1537,6 +1607,13 @@ __global__ void __launch_bounds__(256) k_seg_theta_wide(Tables t, const int32_t*
           th = lo - 1;
         }
         theta[(size_t)sg * N + cx] = th;
+        if (stmp) {
+          const uint64_t ts3 = __builtin_amdgcn_s_memtime();
+          dbg[12] += ts1 - ts0;
+          dbg[13] += ts2 - ts1;
+          dbg[14] += ts3 - ts2;
+          dbg[15] += 1;
+        }
       }
       __syncthreads();
     }
@@ -1859,14 +1936,21 @@ __global__ void __launch_bounds__(256) k_witness_la(Tables t, int rr_lo) {
   const int rr = rr_lo + blockIdx.z;
   const int d0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  for (int r = ty; r < 64; r += 4) {
-    const int d = d0 + r, cx = c0 + tx;
-    int v = -1;
-    if (d < N && cx < N) {
-      const int pw = t.C[(size_t)rr * N + d];
-      if (pw != INF32) v = la_at(t, d, pw, cx);
-    }
-    tile[r][tx] = v;
+  // all 16 frontier positions, then all 16 row values, each batch in flight
+  // together (a loop with one dependent pair of loads per row was ~12 us per online
+  // call at N = 256: the rows sit in different pages)
+  int pw[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int d = d0 + ty + 4 * k;
+    pw[k] = d < N ? t.C[(size_t)rr * N + d] : INF32;
+  }
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int d = d0 + ty + 4 * k, cx = c0 + tx;
+    const bool on = d < N && cx < N && pw[k] != INF32;
+    const int v = la_at(t, on ? d : 0, on ? pw[k] : 0, on ? cx : 0);
+    tile[ty + 4 * k][tx] = on ? v : -1;
   }
   __syncthreads();
   for (int r = ty; r < 64; r += 4) {
@@ -1889,7 +1973,7 @@ template <int VPL>
 __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* cand, int ncand,
                                                      const int32_t* recv_call, const int32_t* rr_in,
                                                      const int32_t* bseg, const uint64_t* seg_fws,
-                                                     int64_t* cts_out, const int32_t* choff) {
+                                                     int64_t* cts_out) {
   // MW_E events per wave (candidates q0 + e * nw, nw = the grid's wave count; 1 measured
   // fastest once the select became cheap: 6.36 vs 6.62 ms at 2, 8.19 at 3): all
   // their loads are in flight together before the first select
@@ -1899,14 +1983,9 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
   constexpr int MW_E = HGE_MW_E;
   __shared__ __attribute__((aligned(16))) int s_mhist[4][256];  // each wave's select bins
   const int nw = gridDim.x * 4;
-  // choff (non-null: a fresh replay, candidate = event id): the waves take the events
-  // in chain-major order (choff = the chains' prefix offsets, N + 1), each XCD a
-  // contiguous range of it.  The events of one chain and round share their threshold
-  // row WLA[rr][cx] (~14 consecutive positions at 256/10M) and their FDTD rows are
-  // consecutive, so a row is fetched into one XCD's L2 once instead of into every
-  // L2 (insertion order interleaves the chains, and neighbouring blocks go to
-  // different XCDs).
-  const int q0 = (choff ? (int)xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x) * 4 + (threadIdx.x >> 6);
+  // (the XCD-aware order of k_fame_decide measured 0.2 ms slower here, and a
+  // chain-major order -- a threshold row shared by consecutive waves -- 10.4 vs 6.0 ms)
+  const int q0 = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int N = t.N, NW = t.NW;
   int qe[MW_E], ixe[MW_E];
@@ -1919,16 +1998,7 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
   int wde[MW_E];
 #pragma unroll
   for (int e = 0; e < MW_E; e++) {
-    int q = q0 + e * nw;
-    if (choff && q < ncand) {  // chain-major position -> event id
-      int lo = 0, hi = N - 1;  // the chain c with choff[c] <= q < choff[c + 1]
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (choff[mid] <= q) lo = mid;
-        else hi = mid - 1;
-      }
-      q = t.chain[(size_t)lo * t.ccap + (q - choff[lo])];
-    }
+    const int q = q0 + e * nw;
     const int qq = q < ncand ? q : ncand - 1;  // valid indices; the result is not stored
     const int x = cand ? cand[qq] : qq;
     const int rc = recv_call[qq], rr0 = rr_in[qq], sg0 = bseg[qq];

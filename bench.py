@@ -107,11 +107,11 @@ def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
 
 def pmc_traffic(config_key, kernel, launches_per_replay):
     """HBM bytes per launch of `kernel` in this configuration from the committed
-    rocprofv3 PMC passes (profiles/r03/pmc_traffic.json, else r02's, made by
+    rocprofv3 PMC passes (profiles/r04/pmc_traffic.json, else an earlier round's, made by
     scripts/pmc_traffic.py on the GPU box): the kernel's bytes per replay over
     the launches that did work (k_la_sweep: the sweeps up to the quiet one), or None."""
     pm = None
-    for rnd in ("r03", "r02"):  # the latest round's passes
+    for rnd in ("r04", "r03", "r02"):  # the latest round's passes
         try:
             pm = json.load(open(os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")))
             break

@@ -11,8 +11,12 @@
 #   fallback the hand-off fallback and RCCL world-1 exchange tests
 #   emulate  the one-hashgraph split emulated part by part (256/10M, 2/4/8 parts)
 #   configs  16/100k, 32/1M, 64/1M, 128/1M bench lines
+#   pmc      FETCH_SIZE / WRITE_SIZE passes -> profiles/r04/pmc_traffic.json (the bench's roofline traffic)
+#   diag     SQ / TCC / LDS counter passes at 256/2M
+#   gap      microbenchmarks: launch_gap (stream launches vs a HIP graph), granule_hop (hand-off floor)
 #   core     parity, wide, golden and replay-path GPU tests
 #   online   per-call profile of the online path (16/100k, 256 prefix)
+#   onprof   rocprofv3 kernel stats and SQ counters of 400 online calls at 256 participants
 #   stamps   the batch engine's per-section cycle stamps (HGB_STAMPS)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 9
@@ -46,6 +50,17 @@ import json
 d=json.loads(open('gpurun_out/r04/n$1_e$2.json').read().strip().splitlines()[-1])
 print('$1/$2', round(d['value']/1e6,2), d['ms_per_step'], d['parity'][:120])"
          done ;;
+    gap) timeout -k 10 120 ./build/launch_gap 32 2000 > gpurun_out/r04/launch_gap.json && timeout -k 10 120 ./build/launch_gap 16 2000 >> gpurun_out/r04/launch_gap.json || exit 5
+         timeout -k 10 120 ./build/granule_hop 256 4000 > gpurun_out/r04/granule_hop.json || exit 5
+         cat gpurun_out/r04/launch_gap.json gpurun_out/r04/granule_hop.json ;;
+    pmc) bash scripts/gpu_pmc.sh r04/pmc || exit 6 ;;
+    diag) bash scripts/gpu_pmc_diag.sh r04/diag && bash scripts/gpu_pmc_lds.sh r04/lds || exit 6 ;;
+    onprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r04/onprof -o run -- python3 -u scripts/analysis/online_profile.py 256 600000 256 400 > gpurun_out/r04/onprof.log 2>&1 || { tail -20 gpurun_out/r04/onprof.log; exit 7; }
+         timeout -s KILL 200 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU --output-format csv -d gpurun_out/r04/onpmc -o pmc -- python3 -u scripts/analysis/online_profile.py 256 600000 256 400 > gpurun_out/r04/onpmc.log 2>&1 || { tail -20 gpurun_out/r04/onpmc.log; exit 7; }
+         find gpurun_out/r04 -name "*.db" -delete; find gpurun_out/r04/onpmc gpurun_out/r04/onprof -name "*kernel_trace.csv" -delete
+         find gpurun_out/r04/onprof -name "*kernel_stats.csv" | head -1 | xargs head -20 ;;
+    segdbg) HGE_STAMPS=1 HGE_SEG_DEBUG=1 timeout -k 10 300 python3 -u scripts/analysis/online_profile.py 256 600000 256 300 > gpurun_out/r04/segdbg.json 2> gpurun_out/r04/segdbg.err || { tail -5 gpurun_out/r04/segdbg.err; exit 7; }
+         grep "hge seg" gpurun_out/r04/segdbg.err | sort | uniq -c | sort -rn | head -8; grep "hge theta" gpurun_out/r04/segdbg.err | tail -3 ;;
     mcgpu) timeout -k 10 600 $PYT -m gpu tests/test_gpu_mc.py tests/test_gpu_batch.py > gpurun_out/r04/mcgpu.log 2>&1 || { tail -40 gpurun_out/r04/mcgpu.log; exit 1; }
          tail -3 gpurun_out/r04/mcgpu.log ;;
     bench) timeout -k 10 600 python -u bench.py > gpurun_out/r04/bench.json 2> gpurun_out/r04/bench.err || { tail -20 gpurun_out/r04/bench.err; exit 2; }
@@ -60,8 +75,10 @@ import json
 d=json.loads(open('gpurun_out/r04/bench_mc.json').read().strip().splitlines()[-1])
 print(round(d['value']/1e6,2), d['ms_per_step'], d['roofline']['frac']); print(d['parity']); print(d['cpu_baseline'])
 print(d['kernels_ms_per_replay'])" ;;
-    prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r04/prof -o run -- python -u bench.py --no-secondary --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/r04/prof.log 2>&1 || { tail -20 gpurun_out/r04/prof.log; exit 3; } ;;
-    profmc) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r04/profmc -o run -- python -u bench.py --workload mc --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/r04/profmc.log 2>&1 || { tail -20 gpurun_out/r04/profmc.log; exit 3; } ;;
+    prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r04/prof -o run -- python -u bench.py --no-secondary --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/r04/prof.log 2>&1 || { tail -20 gpurun_out/r04/prof.log; exit 3; }
+          find gpurun_out/r04/prof -name "*kernel_trace.csv" -delete; find gpurun_out/r04/prof -name "*kernel_stats.csv" | head -1 | xargs head -12 ;;
+    profmc) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r04/profmc -o run -- python -u bench.py --workload mc --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/r04/profmc.log 2>&1 || { tail -20 gpurun_out/r04/profmc.log; exit 3; }
+            find gpurun_out/r04/profmc -name "*kernel_trace.csv" -delete; find gpurun_out/r04/profmc -name "*kernel_stats.csv" | head -1 | xargs head -8 ;;
     smoke) timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r04/smoke.log 2>&1 || { tail -20 gpurun_out/r04/smoke.log; exit 4; }
            tail -1 gpurun_out/r04/smoke.log ;;
     *) echo "unknown step $s"; exit 8 ;;

@@ -5,7 +5,7 @@ Runs two counter passes over `python3 bench.py <bench args>` (FETCH_SIZE, then
 WRITE_SIZE: they cannot share one pass on gfx950), each in its own rocprofv3
 run with --kernel-trace only, parses counter_collection.csv and merges
 {config-key: {kernel: {fetch_bytes, write_bytes, bytes_per_launch, launches}}}
-into profiles/r03/pmc_traffic.json.  FETCH_SIZE is reported in KiB and, on gfx950,
+into profiles/<round>/pmc_traffic.json (ROUND below).  FETCH_SIZE is reported in KiB and, on gfx950,
 counts half of the bytes of wide coalesced reads (MI355X_MICROARCH.md §HBM),
 so it is doubled; WRITE_SIZE (KiB) is taken as is.
 """
@@ -18,6 +18,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
+
+ROUND = "r04"  # the profiles/ directory this round's passes go to
 
 def run_pass(out_dir, counter, bench_args, parse_only=False):
     d = os.path.join(out_dir, counter.lower())
@@ -64,12 +66,15 @@ def main():
         res[name] = {"fetch_bytes": round(fetch_b), "write_bytes": round(write_b),
                      "bytes_per_launch": round(fetch_b + write_b), "launches": launches,
                      "bytes_per_replay": round(per_replay), "replays": replays}
-    path = os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json")
+    path = os.path.join(ROOT, "profiles", ROUND, "pmc_traffic.json")
     os.makedirs(os.path.dirname(path), exist_ok=True)
     try:
         allres = json.load(open(path))
     except (OSError, ValueError):
         allres = {}
+    if "configs" in allres and "round" not in allres:
+        allres = {}  # an older round's file: start this round's afresh
+    allres["round"] = ROUND
     allres.setdefault("note", "HBM bytes per launch from rocprofv3 FETCH_SIZE (x2, gfx950) + "
                               "WRITE_SIZE, separate passes (scripts/pmc_traffic.py)")
     allres.setdefault("configs", {})[key] = res

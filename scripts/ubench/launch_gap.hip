@@ -1,0 +1,145 @@
+// Microbenchmark: what a chain of small dependent kernels costs per launch on one
+// stream, launched one by one vs replayed as an instantiated HIP graph, and with
+// host syncs in the middle (the online per-call path: ~32 launches and 2 host
+// round trips per RunConsensus).  Each kernel is one 64-thread
+// block that bumps a counter (no work: the cost is dispatch and completion).
+//   launch_gap [launches per call] [calls]
+// prints microseconds per call for: stream launches + 1 sync, the same as a graph,
+// stream launches with 2 syncs (half and half), the graph split at the sync, and
+// a graph re-captured per call (new arguments) and updated in place before its launch.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                  \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+__global__ void k_tiny(int* p) {
+  if (threadIdx.x == 0) p[0] += 1;
+}
+
+// the engine's kernels take a ~300-byte Tables struct by value
+struct Big {
+  int* p;
+  int v[72];
+};
+__global__ void k_big(Big b) {
+  if (threadIdx.x == 0) b.p[0] += b.v[threadIdx.x & 63];
+}
+
+static double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int main(int argc, char** argv) {
+  const int L = argc > 1 ? atoi(argv[1]) : 32, C = argc > 2 ? atoi(argv[2]) : 2000;
+  int* d;
+  CK(hipMalloc(&d, 64));
+  CK(hipMemset(d, 0, 64));
+  hipStream_t st;
+  CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  auto launches = [&](int n) {
+    for (int i = 0; i < n; i++) hipLaunchKernelGGL(k_tiny, dim3(1), dim3(64), 0, st, d);
+  };
+  // graphs: all L launches, and the two halves
+  hipGraph_t g[3];
+  hipGraphExec_t ge[3];
+  const int parts[3] = {L, L / 2, L - L / 2};
+  for (int k = 0; k < 3; k++) {
+    CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
+    launches(parts[k]);
+    CK(hipStreamEndCapture(st, &g[k]));
+    CK(hipGraphInstantiate(&ge[k], g[k], nullptr, nullptr, 0));
+  }
+  for (int w = 0; w < 200; w++) {  // warm up (clocks, code objects)
+    launches(L);
+    CK(hipStreamSynchronize(st));
+    CK(hipGraphLaunch(ge[0], st));
+    CK(hipStreamSynchronize(st));
+  }
+  double t0 = now_us();
+  for (int c = 0; c < C; c++) {
+    launches(L);
+    CK(hipStreamSynchronize(st));
+  }
+  const double a = (now_us() - t0) / C;
+  t0 = now_us();
+  for (int c = 0; c < C; c++) {
+    CK(hipGraphLaunch(ge[0], st));
+    CK(hipStreamSynchronize(st));
+  }
+  const double b = (now_us() - t0) / C;
+  t0 = now_us();
+  for (int c = 0; c < C; c++) {
+    launches(L / 2);
+    CK(hipStreamSynchronize(st));
+    launches(L - L / 2);
+    CK(hipStreamSynchronize(st));
+  }
+  const double a2 = (now_us() - t0) / C;
+  t0 = now_us();
+  for (int c = 0; c < C; c++) {
+    CK(hipGraphLaunch(ge[1], st));
+    CK(hipStreamSynchronize(st));
+    CK(hipGraphLaunch(ge[2], st));
+    CK(hipStreamSynchronize(st));
+  }
+  const double b2 = (now_us() - t0) / C;
+  // per call: capture the launches (arguments differ per call, as the engine's do),
+  // update the instantiated graph in place, launch it (what a per-call graph costs)
+  hipGraphExec_t gu;
+  {
+    hipGraph_t g0;
+    CK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+    launches(L);
+    CK(hipStreamEndCapture(st, &g0));
+    CK(hipGraphInstantiate(&gu, g0, nullptr, nullptr, 0));
+    CK(hipGraphDestroy(g0));
+  }
+  int upd_fail = 0;
+  double cap_us = 0, upd_us = 0;
+  t0 = now_us();
+  for (int c = 0; c < C; c++) {
+    const double a0 = now_us();
+    hipGraph_t gc;
+    CK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+    for (int i = 0; i < L; i++) hipLaunchKernelGGL(k_tiny, dim3(1), dim3(64), 0, st, d + ((c + i) & 7));
+    CK(hipStreamEndCapture(st, &gc));
+    const double a1 = now_us();
+    hipGraphExecUpdateResult r;
+    hipGraphNode_t en;
+    if (hipGraphExecUpdate(gu, gc, &en, &r) != hipSuccess) upd_fail++;
+    const double a2 = now_us();
+    CK(hipGraphLaunch(gu, st));
+    CK(hipStreamSynchronize(st));
+    CK(hipGraphDestroy(gc));
+    cap_us += a1 - a0;
+    upd_us += a2 - a1;
+  }
+  const double cu = (now_us() - t0) / C;
+  Big bg;
+  bg.p = d;
+  for (int i = 0; i < 72; i++) bg.v[i] = i;
+  t0 = now_us();
+  for (int c = 0; c < C; c++) {
+    for (int i = 0; i < L; i++) hipLaunchKernelGGL(k_big, dim3(1), dim3(64), 0, st, bg);
+    CK(hipStreamSynchronize(st));
+  }
+  const double ab = (now_us() - t0) / C;
+  t0 = now_us();
+  for (int c = 0; c < C; c++) CK(hipStreamSynchronize(st));
+  const double s = (now_us() - t0) / C;
+  printf("{\"launches_per_call\": %d, \"calls\": %d, \"stream_1sync_us\": %.1f, \"graph_1sync_us\": %.1f, "
+         "\"stream_2sync_us\": %.1f, \"graph_2sync_us\": %.1f, \"empty_sync_us\": %.2f, "
+         "\"capture_update_launch_us\": %.1f, \"capture_us\": %.1f, \"update_us\": %.1f, \"update_failures\": %d, \"stream_1sync_300B_args_us\": %.1f}\n",
+         L, C, a, b, a2, b2, s, cu, cap_us / C, upd_us / C, upd_fail, ab);
+  return 0;
+}
