@@ -176,6 +176,7 @@ struct hge_engine {
   DBuf<int32_t> d_FDTD;  // N > 16: timestamp offsets at the FD positions (the wide median)
   DBuf<uint8_t> d_FDTW;  // N > 16: per (row, 64-column tile) out-of-range flags of d_FDTD
   DBuf<int32_t> d_WLA;   // N > 16: round frontier rows transposed (k_witness_la)
+  DBuf<uint16_t> d_WLR;  // N > 64, packed path: the same rows row-major as LA + 1 (theta)
   DBuf<uint64_t> d_ssc, s_gran;
   DBuf<int32_t> s_bseg;
   DBuf<uint64_t> s_H;                // speculative walk: epoch-tagged histories
@@ -245,6 +246,7 @@ struct hge_engine {
     t.FDTD = d_FDTD.p;
     t.FDTW = d_FDTW.p;
     t.WLA = d_WLA.p;
+    t.WLR = (N > 64 && !wide32) ? d_WLR.p : nullptr;
     t.round = d_round.p;
     t.wit = d_wit.p;
     t.C = d_C.p;
@@ -355,6 +357,7 @@ struct hge_engine {
                              &s_lwrisky};
     for (auto* b : i32s) b->free_();
     s_lwplan.free_();
+    d_WLR.free_();
     s_xbuf.free_();
     s_sord.free_();
     s_soff.free_();
@@ -1823,6 +1826,7 @@ struct hge_engine {
         const bool wla = N > 16 && R_last > rr_lo;
         if (wla) {
           d_WLA.need((size_t)Rcap * N * N);
+          if (N > 64 && !wide32) d_WLR.need((size_t)Rcap * N * N);
           Tables tw = tables();
           KLAUNCH(k_witness_la, dim3(div_up(N, 64), div_up(N, 64), R_last - rr_lo), dim3(256), 0, st, tw,
                   rr_lo);
@@ -2204,6 +2208,7 @@ struct hge_engine {
       bseg = s_bseg.p;
       if (R_last > rr_lo && !wla_done) {
         d_WLA.need((size_t)Rcap * N * N);
+        if (N > 64 && !wide32) d_WLR.need((size_t)Rcap * N * N);
         Tables tw = tables();
         KLAUNCH(k_witness_la, dim3(div_up(N, 64), div_up(N, 64), R_last - rr_lo), dim3(256), 0, st, tw,
                 rr_lo);

@@ -44,6 +44,7 @@ struct Tables {
   int32_t* FDTD;
   uint8_t* FDTW;  // N > 16: [N][ccap][ceil(N / 64)]: 1 = the tile holds an out-of-range delta
   int32_t* WLA;   // N > 16: [Rcap][N][N] LA[(d, C[r][d])][cx] at [r][cx][d]
+  uint16_t* WLR;  // N > 64, packed path: [Rcap][N][N] LA + 1 of the same rows, row-major [r][d][cx] (theta)
   int32_t* LA;
   int32_t* FD;
   int32_t* round;
@@ -1544,24 +1545,36 @@ __global__ void __launch_bounds__(256) k_seg_theta_wide(Tables t, const int32_t*
         // round see chain cx up to about the same point): bisect [min, max], not [0, 65535].
         // Values are LA + 1 (0: no ancestor on chain cx); the padding past nf is 0,
         // which no probe value mid >= 1 counts.
-        // the famous witnesses' LA values of column cx from the frontier rows transposed
-        // (k_witness_la: WLA[i][cx][d] = LA[(d, C[i][d])][cx], the witness of round i on
-        // chain d sits at C[i][d]): one contiguous row per thread.  Gathering the
-        // witnesses' own LA16 rows (one page each) cost ~160k cycles per segment in
-        // dependent latencies at N = 256 (HGE_STAMPS, profiles/r04), 80 us per online call.
-        const int32_t* wrow = t.WLA + ((size_t)i * N + cx) * N;
+        // the famous witnesses' LA values of column cx from the frontier rows copied by
+        // k_witness_la (the witness of round i on chain d sits at C[i][d]).  Gathering
+        // the witnesses' own LA16 rows (one page each) cost ~160k cycles per segment in
+        // dependent latencies at N = 256 (HGE_STAMPS, profiles/r04), 80 us per online
+        // call; the transposed WLA rows (one per thread) still ~85k.
+        // WLR[i][d][cx] = LA + 1 of the round's frontier row on chain d: a famous
+        // witness's values are one coalesced row per wave instruction, loaded 64 rows
+        // at a time (all in flight) and packed 8 per 16 bytes
+        const uint16_t* wr = t.WLR + (size_t)i * N * N + cx;
         int vmin = 65535, vmax = 0;
-        for (int k0 = 0; k0 < nf; k0 += 8) {
-          uint32_t w[4];
+        for (int b0 = 0; b0 < nf; b0 += 64) {
+          uint32_t v[64];
 #pragma unroll
-          for (int u = 0; u < 8; u += 2) {
-            const int a = k0 + u < nf ? wrow[s_row[k0 + u]] + 1 : -1;
-            const int b = k0 + u + 1 < nf ? wrow[s_row[k0 + u + 1]] + 1 : -1;
-            if (a >= 0) { vmin = min(vmin, a); vmax = max(vmax, a); }
-            if (b >= 0) { vmin = min(vmin, b); vmax = max(vmax, b); }
-            w[u >> 1] = (uint32_t)max(a, 0) | ((uint32_t)max(b, 0) << 16);
+          for (int u = 0; u < 64; u++) v[u] = wr[(size_t)s_row[b0 + u < nf ? b0 + u : 0] * N];
+#pragma unroll
+          for (int g8 = 0; g8 < 8; g8++) {
+            const int k0 = b0 + 8 * g8;
+            if (k0 < nf) {
+              uint32_t w[4];
+#pragma unroll
+              for (int u = 0; u < 8; u += 2) {
+                const int a = k0 + u < nf ? (int)v[8 * g8 + u] : -1;
+                const int b = k0 + u + 1 < nf ? (int)v[8 * g8 + u + 1] : -1;
+                if (a >= 0) { vmin = min(vmin, a); vmax = max(vmax, a); }
+                if (b >= 0) { vmin = min(vmin, b); vmax = max(vmax, b); }
+                w[u >> 1] = (uint32_t)max(a, 0) | ((uint32_t)max(b, 0) << 16);
+              }
+              sv[k0 >> 3][cx] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
           }
-          sv[k0 >> 3][cx] = make_uint4(w[0], w[1], w[2], w[3]);
         }
         if (((nf + 7) >> 3) & 1) sv[(nf + 7) >> 3][cx] = make_uint4(0, 0, 0, 0);  // even group count
         if (stmp) {
@@ -1951,6 +1964,8 @@ __global__ void __launch_bounds__(256) k_witness_la(Tables t, int rr_lo) {
     const bool on = d < N && cx < N && pw[k] != INF32;
     const int v = la_at(t, on ? d : 0, on ? pw[k] : 0, on ? cx : 0);
     tile[ty + 4 * k][tx] = on ? v : -1;
+    // the row-major copy (theta's staging reads a famous witness's row coalesced)
+    if (t.WLR && d < N && cx < N) t.WLR[((size_t)rr * N + d) * N + cx] = (uint16_t)((on ? v : -1) + 1);
   }
   __syncthreads();
   for (int r = ty; r < 64; r += 4) {
