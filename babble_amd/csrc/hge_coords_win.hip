@@ -182,23 +182,39 @@ __global__ void __launch_bounds__(1024) k_la_win(Tables t, const int4* plan, int
   // starting rows: the heads before s0 as stored (pass 1: a new row of another
   // window is not written yet, take its own column only)
   uint32_t* ib = initbuf + (size_t)w * N * W;
-  for (int i = tid; i < NPOW * RWW; i += 1024) {
+  // the head positions first, then every thread's row words with all their loads in
+  // flight (a loop with a dependent pair of loads per word was ~45 us per online call
+  // at N = 256, where one window holds the whole batch)
+  for (int c = tid; c < NPOW; c += 1024) {
+    s_hp[c] = c < N ? wpos[(size_t)w * N + c] - 1 : -1;
+    s_ol[c] = c < N ? olen[c] : 0;
+  }
+  __syncthreads();
+  constexpr int PERT = NPOW * RWW / 1024;
+  uint32_t sv0[PERT];
+#pragma unroll
+  for (int k = 0; k < PERT; k++) {
+    const int i = tid + k * 1024;
     const int c = i / RWW, q = i - (i / RWW) * RWW;
     uint32_t val = 0;
     if (c < N && q < W) {
-      const int hp = wpos[(size_t)w * N + c] - 1;
+      const int hp = s_hp[c];
       if (hp >= 0) {
-        if (hp < olen[c] || pass > 1) val = t.LA16[((size_t)c * t.ccap + hp) * W + q];
+        if (hp < s_ol[c] || pass > 1) val = t.LA16[((size_t)c * t.ccap + hp) * W + q];
         else val = (q == (c >> 1)) ? (uint32_t)(hp + 1) << ((c & 1) * 16) : 0u;
       }
-      if (pass > 1 && ib[(size_t)c * W + q] != val) atomicOr(&s_dirty[c >> 5], 1u << (c & 31));
-      ib[(size_t)c * W + q] = val;
     }
-    s_st[i] = val;
-    if (q == 0) {
-      s_hp[c] = c < N ? wpos[(size_t)w * N + c] - 1 : -1;
-      s_ol[c] = c < N ? olen[c] : 0;
+    sv0[k] = val;
+  }
+#pragma unroll
+  for (int k = 0; k < PERT; k++) {
+    const int i = tid + k * 1024;
+    const int c = i / RWW, q = i - (i / RWW) * RWW;
+    if (c < N && q < W) {
+      if (pass > 1 && ib[(size_t)c * W + q] != sv0[k]) atomicOr(&s_dirty[c >> 5], 1u << (c & 31));
+      ib[(size_t)c * W + q] = sv0[k];
     }
+    s_st[i] = sv0[k];
   }
   const int rl = risky[w];  // last risky id of the window (-1: none)
   __syncthreads();

@@ -218,6 +218,7 @@ struct hge_engine {
   int2* k_segs = nullptr;
   int32_t* k_segbase = nullptr;
   int32_t* k_fd = nullptr;  // split: the candidates' chain positions [lo N, hi N)
+  int32_t* k_risky1 = nullptr;  // la_windows_run's one-window risky id (-1 as uploaded)
   bool und_fresh = false;  // the candidate list is every event of a fresh replay
   float stage_ms[7] = {};
 
@@ -870,7 +871,8 @@ struct hge_engine {
     const size_t o_sb = o_seg + 2 * segs.size();  // chain-major segment bases (sweep skipping)
     const size_t o_fd = o_sb + N;  // split: the chain positions of the part's candidates
     std::vector<int32_t>& kc = h_kctl;
-    kc.assign(o_fd + 2 * N, 0);
+    kc.assign(o_fd + 2 * N + 1, 0);
+    kc[o_fd + 2 * N] = -1;  // the one-window lastAncestors pass's risky id (la_windows_run)
     if (split_on()) {
       // FD timestamp rows (the median's input) of the ids [cand_lo, the part's end)
       const int64_t A = sp.clo[sp.part], B = sp.a[sp.part + 1];
@@ -905,6 +907,7 @@ struct hge_engine {
     k_segs = (int2*)(s_kctl.p + o_seg);
     k_segbase = s_kctl.p + o_sb;
     k_fd = split_on() ? s_kctl.p + o_fd : nullptr;
+    k_risky1 = s_kctl.p + o_fd + 2 * N;
     {
       const bool packed = up_n0 == n0 && up_n1 == n1;
       fill_up = packed ? (const UpEv*)s_up.p : (const UpEv*)nullptr;
@@ -1463,10 +1466,16 @@ struct hge_engine {
     s_lwrisky.need(G);
     const int MAXP = 64;
     s_chg.need(MAXP);
-    KLAUNCH(k_lw_pos, dim3(div_up(std::max<int64_t>(G * N, MAXP), 256)), dim3(256), 0, st, t, n0, (int)WN, (int)G,
-            len, s_lwpos.p, s_lwrisky.p, s_chg.p, MAXP);
+    // one window (an online call): its chain start positions are the chains' old
+    // lengths and its risky id starts at -1 in the control block, so k_lw_pos is not
+    // needed (one launch less per call)
+    const int32_t* wpos = G == 1 ? olen : s_lwpos.p;
+    int32_t* risky = G == 1 ? k_risky1 : s_lwrisky.p;
+    if (G > 1)
+      KLAUNCH(k_lw_pos, dim3(div_up(std::max<int64_t>(G * N, MAXP), 256)), dim3(256), 0, st, t, n0, (int)WN, (int)G,
+              len, s_lwpos.p, s_lwrisky.p, s_chg.p, MAXP);
     KLAUNCH(k_lw_plan, dim3(div_up(div_up(ne, LW_K), 4)), dim3(256), 0, st, t, n0, n1, (int)WN, len, s_lwplan.p,
-            s_lwrisky.p);
+            risky);
     int p = 0;
     for (int group = G == 1 ? 1 : 3;; group = 2) {
       for (int g = 0; g < group; g++, p++) {
@@ -1474,8 +1483,8 @@ struct hge_engine {
         const int32_t* prev = p > 0 ? s_chg.p + p - 1 : nullptr;
         const int pass = p + 1;
 #define LWIN(NP)                                                                                         \
-  KLAUNCH(k_la_win<NP>, dim3(G), dim3(1024), 0, st, t, s_lwplan.p, n0, n1, (int)WN, s_lwpos.p, olen,     \
-          s_lwinit.p, s_lwrisky.p, s_lwsum.p, pass, prev, s_chg.p + p)
+  KLAUNCH(k_la_win<NP>, dim3(G), dim3(1024), 0, st, t, s_lwplan.p, n0, n1, (int)WN, wpos, olen,          \
+          s_lwinit.p, (const int32_t*)risky, s_lwsum.p, pass, prev, s_chg.p + p)
         if (npow == 64) LWIN(64);
         else if (npow == 128) LWIN(128);
         else LWIN(256);

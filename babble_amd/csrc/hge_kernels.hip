@@ -115,30 +115,42 @@ __global__ void k_min_round_range(const int32_t* round, int lo, int hi, int32_t*
   if ((threadIdx.x & 63) == 0 && v != INF32) atomicMin(out, v);
 }
 
-// exclusive scan of a small int array by one block (n <= ~64k)
+// exclusive scan of a small int array by one block (n <= ~64k): per-thread
+// contiguous runs, a wave scan by shuffles and one scan of the 16 wave totals
+// (two barriers; a Hillis-Steele over 1024 partials took 20)
 __global__ void __launch_bounds__(1024) k_scan_small(const int32_t* in, int32_t* out, int n,
                                                      int32_t* total) {
-  __shared__ int tmp[1024];
-  const int T = blockDim.x, tid = threadIdx.x;
+  __shared__ int wsum[16];
+  const int T = blockDim.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int per = (n + T - 1) / T;
   const int lo = min(n, tid * per), hi = min(n, lo + per);
   int s = 0;
   for (int i = lo; i < hi; i++) s += in[i];
-  tmp[tid] = s;
-  __syncthreads();
-  for (int off = 1; off < T; off <<= 1) {
-    const int add = (tid >= off) ? tmp[tid - off] : 0;
-    __syncthreads();
-    tmp[tid] += add;
-    __syncthreads();
+  int inc = s;  // inclusive scan over the wave
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
   }
-  int run = tmp[tid] - s;
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  if (wv == 0) {
+    int v = lane < T / 64 ? wsum[lane] : 0;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const int y = __shfl_up(v, o, 64);
+      if (lane >= o) v += y;
+    }
+    if (lane < T / 64) wsum[lane] = v;  // inclusive totals of the waves
+  }
+  __syncthreads();
+  int run = (wv > 0 ? wsum[wv - 1] : 0) + inc - s;
   for (int i = lo; i < hi; i++) {
-    int v = in[i];
+    const int v = in[i];
     out[i] = run;
     run += v;
   }
-  if (tid == T - 1 && total) *total = tmp[T - 1];
+  if (tid == T - 1 && total) *total = wsum[T / 64 - 1];
 }
 
 // multi-block exclusive scan: 1024 elements per 256-thread block
