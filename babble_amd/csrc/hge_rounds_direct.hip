@@ -66,7 +66,6 @@ template <int BS, int NPOW>
 struct DirLDS {
   int sP[256];
   uint32_t sLA[DirGeo<BS, NPOW>::W * DirGeo<BS, NPOW>::RS] __attribute__((aligned(16)));
-  int32_t sFD[DirGeo<BS, NPOW>::W * NPOW] __attribute__((aligned(16)));  // the window's FD rows (int32, by LDS DMA)
   int sCnt[DIR_MAXP];
   int sCntW[DIR_MAXP][BS / 64] __attribute__((aligned(16)));  // per-wave passing members of a probe
   int sHist[DirGeo<BS, NPOW>::W / 2];  // members by first passing offset (dir_select_pm)
@@ -140,38 +139,15 @@ __device__ __forceinline__ void dir_store(const Tables& t, DirLDS<BS, NPOW>& L, 
   }
 }
 
-// FD rows [p0, p0 + nr) of chain c (rows < lenc) into their ring slots of sFD by
-// LDS DMA (global_load_lds_dwordx4: one wave instruction per row, rows dealt
-// round-robin to the waves, no registers).  The staging of the chosen row then
-// reads LDS instead of waiting on HBM on the hand-off path.  Complete after
-// every wave's vmcnt(0) and a barrier.
-template <int BS, int NPOW>
-__device__ __forceinline__ void dir_fetch_fd(const Tables& t, DirLDS<BS, NPOW>& L, int c, int p0, int nr,
-                                             int lenc) {
-  if (p0 == INF32 || nr <= 0) return;
-  const int N = t.N;
-  const int have = min(nr, lenc - p0);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int r = wave; r < have; r += BS / 64) {
-    const int p = p0 + r;
-    if (4 * lane < N)
-      __builtin_amdgcn_global_load_lds((const void*)(t.FD + rowoff(t, c, p) + 4 * lane),
-                                       (__attribute__((address_space(3))) void*)&L.sFD[(p & (DirGeo<BS, NPOW>::W - 1)) * NPOW],
-                                       16, 0, 0);
-  }
-}
-
 // rows [p0, p0 + nr) into their ring slots, chunk by chunk (caller syncs before a probe)
 template <int BS, int NPOW>
 __device__ __forceinline__ void dir_load(const Tables& t, DirLDS<BS, NPOW>& L, int c, int p0, int nr, int lenc,
                                          uint2 (&v)[DirGeo<BS, NPOW>::PREF]) {
   if (p0 == INF32) return;
-  dir_fetch_fd<BS, NPOW>(t, L, c, p0, nr, lenc);
   for (int q = 0; q < nr; q += DIR_CH) {
     dir_fetch<BS, NPOW>(t, c, p0 + q, nr - q, lenc, v);
     dir_store<BS, NPOW>(t, L, p0 + q, nr - q, lenc, v);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the FD rows have landed (caller syncs)
 }
 
 // member slice of thread (d, part) for the first round: FD[(d, Pd)][part * CPT, +CPT)
@@ -231,20 +207,20 @@ __device__ __forceinline__ void dir_members_mb(const uint32_t* mb, uint32_t (&mw
 }
 
 // wave 0 of chain c's workgroup: stage FD[(c, p)] (p = INF32: no member) into MB,
-// from the window's FD rows in LDS when p is in the ring (else from HBM).
+// read from HBM after the pick.  (Round 3 staged every window row's FD row in LDS
+// ahead of the pick so the stage read LDS: ~10 GB of the kernel's traffic per
+// 256/10M replay for no measured time, 24.57-24.68 vs 24.62-24.69 ms in a
+// same-box A/B, profiles/r04/abfd_*.)
 // Lane l packs columns 4l .. 4l + 3 into row words 2l, 2l + 1 (one part, one chunk).
 template <int BS, int NPOW>
-__device__ __forceinline__ void dir_stage_member(const Tables& t, const DirLDS<BS, NPOW>& L, uint32_t* mb,
-                                                 int c, int p, bool in_ring) {
+__device__ __forceinline__ void dir_stage_member(const Tables& t, uint32_t* mb, int c, int p) {
   using G = DirGeo<BS, NPOW>;
   constexpr int MVW = G::MVW;
   const int lane = threadIdx.x;  // < 64
   const int N = t.N;
   if (4 * lane < NPOW) {
     int4 a = make_int4(INF32, INF32, INF32, INF32);
-    if (p != INF32 && 4 * lane < N)
-      a = in_ring ? *(const int4*)&L.sFD[(p & (DirGeo<BS, NPOW>::W - 1)) * NPOW + 4 * lane]
-                  : *(const int4*)(t.FD + rowoff(t, c, p) + 4 * lane);
+    if (p != INF32 && 4 * lane < N) a = *(const int4*)(t.FD + rowoff(t, c, p) + 4 * lane);
     const unsigned long long x =
         (unsigned long long)dir_pack_fd(a.x, a.y) | ((unsigned long long)dir_pack_fd(a.z, a.w) << 32);
     const int w = 2 * lane, part = w / G::CW, wp = w - part * G::CW;
@@ -548,7 +524,7 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
     // publish C_{r+1}[c]: wave 0 stages the next member row, drains its stores,
     // then lane 0 stores the granule
     if (tid < 64) {
-      dir_stage_member<BS, NPOW>(t, L, mbp[(r + 1) & 1], c, nxt, nxt >= lo && nxt - lo < DirGeo<BS, NPOW>::W);
+      dir_stage_member<BS, NPOW>(t, mbp[(r + 1) & 1], c, nxt);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (tid == 0) {
         if (hist) hist[(size_t)(r + 1) * N + c] = nxt;
@@ -588,7 +564,6 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
     }
     lo = nxt;
     dir_fetch<BS, NPOW>(t, c, f0, fn, lenc, pv);
-    dir_fetch_fd<BS, NPOW>(t, L, c, f0, fn, lenc);
     dir_store<BS, NPOW>(t, L, f0, fn, lenc, pv);
     if (fn > DIR_CH) {  // rare: the LA rows past the first chunk (the FD rows are in flight)
       for (int q = DIR_CH; q < fn; q += DIR_CH) {

@@ -14,6 +14,7 @@
 #   pmc      FETCH_SIZE / WRITE_SIZE passes -> profiles/r04/pmc_traffic.json (the bench's roofline traffic)
 #   diag     SQ / TCC / LDS counter passes at 256/2M
 #   gap      microbenchmarks: launch_gap (stream launches vs a HIP graph), granule_hop (hand-off floor)
+#   abfd     A/B of the rounds kernel without the window's FD rows in LDS (HGE_DIR_NOFD)
 #   core     parity, wide, golden and replay-path GPU tests
 #   online   per-call profile of the online path (16/100k, 256 prefix)
 #   onprof   rocprofv3 kernel stats and SQ counters of 400 online calls at 256 participants
@@ -61,6 +62,14 @@ print('$1/$2', round(d['value']/1e6,2), d['ms_per_step'], d['parity'][:120])"
          find gpurun_out/r04/onprof -name "*kernel_stats.csv" | head -1 | xargs head -20 ;;
     segdbg) HGE_STAMPS=1 HGE_SEG_DEBUG=1 timeout -k 10 300 python3 -u scripts/analysis/online_profile.py 256 600000 256 300 > gpurun_out/r04/segdbg.json 2> gpurun_out/r04/segdbg.err || { tail -5 gpurun_out/r04/segdbg.err; exit 7; }
          grep "hge seg" gpurun_out/r04/segdbg.err | sort | uniq -c | sort -rn | head -8; grep "hge theta" gpurun_out/r04/segdbg.err | tail -3 ;;
+    abfd) for v in 0 1 0 1; do
+           if [ $v = 1 ]; then export HGE_DIR_NOFD=1; else unset HGE_DIR_NOFD; fi
+           timeout -k 10 300 python -u bench.py --no-secondary --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/r04/abfd_$v.json 2> gpurun_out/r04/abfd_$v.err || { tail -5 gpurun_out/r04/abfd_$v.err; exit 2; }
+           python -c "
+import json
+d=json.loads(open('gpurun_out/r04/abfd_$v.json').read().strip().splitlines()[-1])
+print('nofd=$v', round(d['value']/1e6,2), d['ms_per_step'], d['kernels_ms_per_replay']['k_rounds_direct'], d['parity'][:40])"
+         done; unset HGE_DIR_NOFD ;;
     mcgpu) timeout -k 10 600 $PYT -m gpu tests/test_gpu_mc.py tests/test_gpu_batch.py > gpurun_out/r04/mcgpu.log 2>&1 || { tail -40 gpurun_out/r04/mcgpu.log; exit 1; }
          tail -3 gpurun_out/r04/mcgpu.log ;;
     bench) timeout -k 10 600 python -u bench.py > gpurun_out/r04/bench.json 2> gpurun_out/r04/bench.err || { tail -20 gpurun_out/r04/bench.err; exit 2; }
