@@ -341,18 +341,24 @@ __global__ void __launch_bounds__(256) k_la16_rows_runs(Tables t, FT* FDT, const
   }
   if (p0 >= lj) return;
   // rows p0 - 1 .. p0 + 63: 32 packed words = 64 columns; lanes 0..31 take one word of
-  // row r, lanes 32..63 the same word of row r + 1
-  for (int r = 2 * ty; r < 66; r += 8) {
-    const int rr = r + (tx >> 5), w = tx & 31;
+  // row r, lanes 32..63 the same word of row r + 1.  All of a thread's loads are
+  // issued before the first LDS store (the loop as written compiled to one load and a
+  // vmcnt(0) wait per row pair: nine serial memory latencies per tile)
+  constexpr int NIT = 9;  // r = 2 ty + 8 i < 66
+  uint32_t xv[NIT];
+#pragma unroll
+  for (int i = 0; i < NIT; i++) {
+    const int rr = 2 * ty + 8 * i + (tx >> 5), w = tx & 31;
     const int p = p0 - 1 + rr, c = c0 + 2 * w;
-    if (rr < 65 && p >= 0 && p < lj && c < N) {
-      const uint32_t x = t.LA16[rowoff16(t, j, p) + (c >> 1)];
-      const int lo = (int)(x & 0xFFFFu) - 1, hi = (int)(x >> 16) - 1;
-      tile[rr][2 * w] = lo;
-      tile[rr][2 * w + 1] = hi;
-    } else if (rr < 65) {
-      tile[rr][2 * w] = -1;
-      tile[rr][2 * w + 1] = -1;
+    const bool ok = rr < 65 && p >= 0 && p < lj && c < N;
+    xv[i] = ok ? t.LA16[rowoff16(t, j, ok ? p : 0) + (ok ? (c >> 1) : 0)] : 0u;  // 0: -1 after unpacking
+  }
+#pragma unroll
+  for (int i = 0; i < NIT; i++) {
+    const int rr = 2 * ty + 8 * i + (tx >> 5), w = tx & 31;
+    if (rr < 65) {
+      tile[rr][2 * w] = (int)(xv[i] & 0xFFFFu) - 1;
+      tile[rr][2 * w + 1] = (int)(xv[i] >> 16) - 1;
     }
   }
   __syncthreads();
