@@ -1050,8 +1050,11 @@ struct hge_engine {
         KLAUNCH(k_round_ranges, dim3(div_up((int64_t)Rcap * N, 256)), dim3(256), 0, st, t, k_len + N,
                 (const int32_t*)k_rs, s_newwit.p, k_rs + 2);
       } else {
+        // DivideRounds right after (divide()) with nothing coordinated but undivided:
+        // the new ids join the undetermined list here (no k_iota launch)
+        und_appended = dividing && n_divided == n0;
         KLAUNCH(k_round_assign, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0, (int)n1,
-                (const int32_t*)k_rs, s_newwit.p, k_rs + 2);
+                (const int32_t*)k_rs, s_newwit.p, k_rs + 2, und_appended ? d_und.p + n_und : (int32_t*)nullptr);
       }
       {
         int G = 1;
@@ -1060,12 +1063,15 @@ struct hge_engine {
         KLAUNCH(k_witness_bits, dim3(std::min(div_up(wmax * NW * G, 256), 8192)), dim3(256), 0,
                 st, t, s_newwit.p, k_rs + 2, N > 32 ? (const uint64_t*)d_ssc.p : nullptr, G);
       }
-      KLAUNCH(k_round_minw, dim3(div_up(Rcap, 4)), dim3(256), 0, st, t, 0,
-              (const int32_t*)k_rs, d_minw.p, (const int32_t*)coop_err_src);
       // the lowest round of the next batch's candidates (the undetermined list and the
-      // events the next divide appends), read with the round count
-      // (a fresh replay's candidates start at event 0, round 0: nothing to read)
-      if (!fresh) {
+      // events the next divide appends), read with the round count (a fresh replay's
+      // candidates start at event 0, round 0: nothing to read); an online call's few
+      // candidates are reduced by one extra block of k_round_minw
+      const bool mr = !fresh && n_und + (n1 - n_divided) <= 65536;
+      KLAUNCH(k_round_minw, dim3(div_up(Rcap, 4) + (mr ? 1 : 0)), dim3(256), 0, st, t, 0,
+              (const int32_t*)k_rs, d_minw.p, (const int32_t*)coop_err_src, mr ? 1 : 0, (const int32_t*)d_und.p,
+              (int)n_und, (int)n_divided, (int)n1);
+      if (!fresh && !mr) {
         if (n_und > 0)
           KLAUNCH(k_min_round, dim3(div_up(n_und, 256)), dim3(256), 0, st, d_round.p, d_und.p, (int)n_und,
                   d_minw.p + Rcap + 2);
@@ -2247,13 +2253,23 @@ struct hge_engine {
   }
 
   // DivideRounds: everything inserted becomes visible to the consensus calls
+  bool dividing = false, und_appended = false;
   void divide() {
-    coords();
+    dividing = true;
+    und_appended = false;
+    try {
+      coords();
+    } catch (...) {
+      dividing = false;
+      throw;
+    }
+    dividing = false;
     if (n_divided < n_coords) {
-      // append the newly divided events to the undetermined list (insertion order)
+      // append the newly divided events to the undetermined list (insertion order),
+      // unless k_round_assign already did
       const int64_t a = n_divided, m = n_coords - n_divided;
       ensure_events(n_coords);
-      KLAUNCH(k_iota, dim3(div_up(m, 256)), dim3(256), 0, st, d_und.p + n_und, m, (int32_t)a);
+      if (!und_appended) KLAUNCH(k_iota, dim3(div_up(m, 256)), dim3(256), 0, st, d_und.p + n_und, m, (int32_t)a);
       n_und += m;
       n_divided = n_coords;
     }

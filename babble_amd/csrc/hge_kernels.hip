@@ -807,12 +807,15 @@ __global__ void k_frontier_start(Tables t, const int32_t* olen, const int32_t* l
 // round(x) = max r with C[r][cx] <= px; witness iff C[round][cx] == px
 // (consecutive events share a round: the per-round counts and the new-witness
 // slots are aggregated per wave before touching global atomics)
+// und_app (non-null: DivideRounds of an online call): the new ids are appended to the
+// undetermined list there too (in place of a k_iota launch)
 __global__ void k_round_assign(Tables t, int n0, int n1, const int32_t* rstate, int32_t* newwit,
-                               int32_t* nnewwit) {
+                               int32_t* nnewwit, int32_t* und_app) {
   if (rstate[1]) return;  // the rounds table overflowed: the host grows it and walks again
   const int R = rstate[0];
   const int x = n0 + blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = x < n1;
+  if (und_app && valid) und_app[x - n0] = x;
   const int N = t.N;
   const int lane = threadIdx.x & 63;
   int lo = 0;
@@ -905,17 +908,35 @@ __global__ void k_round_ranges(Tables t, const int32_t* len, const int32_t* rsta
 // minw[r] = the lowest witness id of round r: one wave per round, lanes over the
 // creators (a thread per round looping over N creators was latency-bound: ~27 us
 // per online call at N = 256)
+// mr (an online call's candidates, few): the grid's last block also takes the
+// lowest round over und[0, n_und) and the ids [lo, hi) and stores it at
+// minw[Rcap+2] itself (in place of k_min_round / k_min_round_range)
 __global__ void __launch_bounds__(256) k_round_minw(Tables t, int r0, const int32_t* rstate, int32_t* minw,
-                                                    const int32_t* err_in) {
+                                                    const int32_t* err_in, int mr, const int32_t* und, int n_und,
+                                                    int lo, int hi) {
+  if (mr && blockIdx.x == gridDim.x - 1) {
+    __shared__ int s_m;
+    if (threadIdx.x == 0) s_m = INF32;
+    __syncthreads();
+    int m = INF32;
+    for (int i = threadIdx.x; i < n_und; i += blockDim.x) m = min(m, t.round[und[i]]);
+    for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) m = min(m, t.round[i]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = min(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) atomicMin(&s_m, m);
+    __syncthreads();
+    if (threadIdx.x == 0) minw[t.Rcap + 2] = s_m;
+    return;
+  }
   const int r = r0 + blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   // the round count and overflow flag ride along at minw[Rcap..Rcap+1], the next
-  // batch's lowest candidate round at [Rcap+2] (INF32 here, lowered by k_min_round*
+  // batch's lowest candidate round at [Rcap+2] (INF32 here when k_min_round* lower it
   // after this kernel) and the rounds walk's hand-off error flag at [Rcap+3]: one
   // readback for all of them
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     minw[t.Rcap] = rstate[0];
     minw[t.Rcap + 1] = rstate[1];
-    minw[t.Rcap + 2] = INF32;
+    if (!mr) minw[t.Rcap + 2] = INF32;
     minw[t.Rcap + 3] = err_in ? *err_in : 0;
   }
   if (rstate[1] || r >= rstate[0]) return;
