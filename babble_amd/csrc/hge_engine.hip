@@ -1833,7 +1833,7 @@ struct hge_engine {
             (const int32_t*)s_seground.p, (const int32_t*)c_sgo, (const int32_t*)s_segcnt.p, nr,   \
             (const uint64_t*)s_segfws.p, s_theta.p);                                               \
   else                                                                                             \
-    KLAUNCH(k_seg_theta_wide<B>, dim3(std::min(nr, 4096), nr < 64 ? 8 : 2), dim3(256), 0, st, t,   \
+    KLAUNCH(k_seg_theta_wide<B>, dim3(std::min(nr, 4096), nr < 64 ? 8 : 2), dim3(1024), 0, st, t,  \
             (const int32_t*)s_seground.p, (const int32_t*)c_sgo, (const int32_t*)s_segcnt.p, nr,   \
             (const uint64_t*)s_segfws.p, s_theta.p, dbg_p());
         // the frontier rows transposed (WLA) for the batch's rounds: theta (N > 64) and

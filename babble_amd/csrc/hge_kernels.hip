@@ -1527,14 +1527,15 @@ __global__ void __launch_bounds__(256) k_segments_1p(Tables t, int rr_lo, int nr
 // then each thread bisects the value domain of its column for the (|fws|/2 + 1)-th
 // largest.
 template <int NWT>
-__global__ void __launch_bounds__(256) k_seg_theta_wide(Tables t, const int32_t* seg_round,
-                                                        const int32_t* segoff, const int32_t* segcnt,
-                                                        int nr, const uint64_t* seg_fws,
-                                                        int32_t* theta, uint64_t* dbg) {
+__global__ void __launch_bounds__(1024) k_seg_theta_wide(Tables t, const int32_t* seg_round,
+                                                         const int32_t* segoff, const int32_t* segcnt,
+                                                         int nr, const uint64_t* seg_fws,
+                                                         int32_t* theta, uint64_t* dbg) {
   // [famous k / 8][cx]: 8 values of a column per 16 bytes, as uint16 pairs
   __shared__ uint4 sv[32][256];
   __shared__ int s_row[256];
   __shared__ int s_nf;
+  __shared__ int s_vmin[256], s_vmax[256];
   const int N = t.N;
   const int tid = threadIdx.x;
   // blocks (x, y): rounds x, x + gridDim.x, ... (grid-stride) and, of each round's
@@ -1552,7 +1553,7 @@ __global__ void __launch_bounds__(256) k_seg_theta_wide(Tables t, const int32_t*
       const int i = seg_round[sg];
       // the famous witnesses' rows, in ascending creator order: thread d places
       // its own at its rank (a serial walk here was a chain of dependent loads)
-      {
+      if (tid < 256) {
         uint64_t fw[NWT];
         int nfw = 0;
 #pragma unroll
@@ -1565,101 +1566,114 @@ __global__ void __launch_bounds__(256) k_seg_theta_wide(Tables t, const int32_t*
           int rank = __popcll(fw[d >> 6] & ((1ull << (d & 63)) - 1));
 #pragma unroll
           for (int w = 0; w < NWT; w++) rank += w < (d >> 6) ? __popcll(fw[w]) : 0;
-          s_row[rank] = d;  // the famous witness of chain d: its LA row is WLA[i][.][d]
+          s_row[rank] = d;  // the famous witness of chain d: its row is WLR[i][d][.]
         }
         if (tid == 0) s_nf = nfw;
+        s_vmin[tid] = 65535;
+        s_vmax[tid] = 0;
       }
       __syncthreads();
       if (stmp) ts1 = __builtin_amdgcn_s_memtime();
-      const int nf = s_nf;
-      const int cx = tid;
-      if (cx < N) {
-        // the column's values span a few dozen positions (the famous witnesses of one
-        // round see chain cx up to about the same point): bisect [min, max], not [0, 65535].
-        // Values are LA + 1 (0: no ancestor on chain cx); the padding past nf is 0,
-        // which no probe value mid >= 1 counts.
-        // the famous witnesses' LA values of column cx from the frontier rows copied by
-        // k_witness_la (the witness of round i on chain d sits at C[i][d]).  Gathering
-        // the witnesses' own LA16 rows (one page each) cost ~160k cycles per segment in
-        // dependent latencies at N = 256 (HGE_STAMPS, profiles/r04), 80 us per online
-        // call; the transposed WLA rows (one per thread) still ~85k.
-        // WLR[i][d][cx] = LA + 1 of the round's frontier row on chain d: a famous
-        // witness's values are one coalesced row per wave instruction, loaded 64 rows
-        // at a time (all in flight) and packed 8 per 16 bytes
-        const uint16_t* wr = t.WLR + (size_t)i * N * N + cx;
-        int vmin = 65535, vmax = 0;
-        for (int b0 = 0; b0 < nf; b0 += 64) {
-          uint32_t v[64];
+      const int nf = s_nf, ng = (nf + 7) >> 3;
+      // staging (thread = column cx, quarter pa of the 8-row groups g = pa + 4 u): the
+      // famous witnesses' LA + 1 values of column cx from WLR[i][d][cx], the round's
+      // frontier rows written row-major by k_witness_la (the witness of round i on
+      // chain d sits at C[i][d]); a wave reads 64 consecutive columns of one row, and
+      // a thread's loads go out 32 at a time.  (Round 3 gathered the
+      // witnesses' own LA16 rows, one page each: ~160k cycles per segment of
+      // dependent latencies at N = 256, 80 us per online call.)
+      {
+        const int cx = tid & 255, pa = tid >> 8;
+        if (cx < N) {
+          const uint16_t* wr = t.WLR + (size_t)i * N * N + cx;
+          int vmin = 65535, vmax = 0;
+#pragma unroll 1
+          for (int hb = 0; hb < 2; hb++) {  // two batches of 32 loads in flight (registers)
+            if (8 * (pa + 16 * hb) >= nf) break;
+            uint32_t v[32];
 #pragma unroll
-          for (int u = 0; u < 64; u++) v[u] = wr[(size_t)s_row[b0 + u < nf ? b0 + u : 0] * N];
+            for (int u = 0; u < 4; u++)
 #pragma unroll
-          for (int g8 = 0; g8 < 8; g8++) {
-            const int k0 = b0 + 8 * g8;
-            if (k0 < nf) {
-              uint32_t w[4];
-#pragma unroll
-              for (int u = 0; u < 8; u += 2) {
-                const int a = k0 + u < nf ? (int)v[8 * g8 + u] : -1;
-                const int b = k0 + u + 1 < nf ? (int)v[8 * g8 + u + 1] : -1;
-                if (a >= 0) { vmin = min(vmin, a); vmax = max(vmax, a); }
-                if (b >= 0) { vmin = min(vmin, b); vmax = max(vmax, b); }
-                w[u >> 1] = (uint32_t)max(a, 0) | ((uint32_t)max(b, 0) << 16);
+              for (int e = 0; e < 8; e++) {
+                const int k = 8 * (pa + 4 * (u + 4 * hb)) + e;
+                v[8 * u + e] = wr[(size_t)s_row[k < nf ? k : 0] * N];
               }
-              sv[k0 >> 3][cx] = make_uint4(w[0], w[1], w[2], w[3]);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+              const int g = pa + 4 * (u + 4 * hb);
+              if (g < ng) {
+                uint32_t w[4];
+#pragma unroll
+                for (int e = 0; e < 8; e += 2) {
+                  const int k = 8 * g + e;
+                  const int a = k < nf ? (int)v[8 * u + e] : -1;
+                  const int b = k + 1 < nf ? (int)v[8 * u + e + 1] : -1;
+                  if (a >= 0) { vmin = min(vmin, a); vmax = max(vmax, a); }
+                  if (b >= 0) { vmin = min(vmin, b); vmax = max(vmax, b); }
+                  w[e >> 1] = (uint32_t)max(a, 0) | ((uint32_t)max(b, 0) << 16);
+                }
+                sv[g][cx] = make_uint4(w[0], w[1], w[2], w[3]);
+              }
             }
           }
+          if (nf > 0) {
+            atomicMin(&s_vmin[cx], vmin);
+            atomicMax(&s_vmax[cx], vmax);
+          }
         }
-        if (((nf + 7) >> 3) & 1) sv[(nf + 7) >> 3][cx] = make_uint4(0, 0, 0, 0);  // even group count
-        if (stmp) {
-          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-          ts2 = __builtin_amdgcn_s_memtime();
-        }
+      }
+      __syncthreads();
+      if (stmp) ts2 = __builtin_amdgcn_s_memtime();
+      // bisection (thread = column cx = tid / 4, quarter pb = tid % 4 of the groups,
+      // a quad per column: the counts are summed by two DPP quad permutes).  The
+      // column's values span a few dozen positions (the famous witnesses of one round
+      // see chain cx up to about the same point): bisect [min, max], not [0, 65535].
+      // Values are LA + 1 (0: no ancestor on chain cx), never counted for mid >= 1.
+      {
+        const int cx = tid >> 2, pb = tid & 3;
         int th = (int)0x80000000;
-        if (nf > 0) {
+        if (nf > 0 && cx < N) {
           const int kk = nf / 2 + 1;  // k-th largest = largest v with count(>= v) >= kk
-          const int ng = (nf + 7) >> 3;
-          int lo = vmin, hi = vmax;
-          while (lo < hi) {
+          int lo = s_vmin[cx], hi = s_vmax[cx];
+          while (lo < hi) {  // quad-uniform (one column)
             const int mid = (lo + hi + 1) >> 1;
             // v >= mid <=> v -sat (mid - 1) != 0: packed saturating subtract, min 1, add
-            // (the same three packed ops as the strongly-see probe, hge_rounds_direct.hip)
             const uint32_t m1 = (uint32_t)(mid - 1) * 0x00010001u, one = 0x00010001u;
             uint32_t acc0 = 0, acc1 = 0;
-            for (int g = 0; g < ng; g += 2) {  // two groups per step (ng padded to even)
-#pragma unroll
-              for (int h = 0; h < 2; h++) {
-                const uint4 x = sv[g + h][cx];
-                uint32_t d0, d1, d2, d3;
-                asm("v_pk_sub_u16 %0, %6, %10 clamp\n\t"
-                    "v_pk_sub_u16 %1, %7, %10 clamp\n\t"
-                    "v_pk_sub_u16 %2, %8, %10 clamp\n\t"
-                    "v_pk_sub_u16 %3, %9, %10 clamp\n\t"
-                    "v_pk_min_u16 %0, %0, %11\n\t"
-                    "v_pk_min_u16 %1, %1, %11\n\t"
-                    "v_pk_min_u16 %2, %2, %11\n\t"
-                    "v_pk_min_u16 %3, %3, %11\n\t"
-                    "v_pk_add_u16 %4, %4, %0\n\t"
-                    "v_pk_add_u16 %5, %5, %1\n\t"
-                    "v_pk_add_u16 %4, %4, %2\n\t"
-                    "v_pk_add_u16 %5, %5, %3"
-                    : "=&v"(d0), "=&v"(d1), "=&v"(d2), "=&v"(d3), "+v"(acc0), "+v"(acc1)
-                    : "v"(x.x), "v"(x.y), "v"(x.z), "v"(x.w), "v"(m1), "v"(one));
-              }
+            for (int g = pb; g < ng; g += 4) {
+              const uint4 x = sv[g][cx];
+              uint32_t d0, d1, d2, d3;
+              asm("v_pk_sub_u16 %0, %6, %10 clamp\n\t"
+                  "v_pk_sub_u16 %1, %7, %10 clamp\n\t"
+                  "v_pk_sub_u16 %2, %8, %10 clamp\n\t"
+                  "v_pk_sub_u16 %3, %9, %10 clamp\n\t"
+                  "v_pk_min_u16 %0, %0, %11\n\t"
+                  "v_pk_min_u16 %1, %1, %11\n\t"
+                  "v_pk_min_u16 %2, %2, %11\n\t"
+                  "v_pk_min_u16 %3, %3, %11\n\t"
+                  "v_pk_add_u16 %4, %4, %0\n\t"
+                  "v_pk_add_u16 %5, %5, %1\n\t"
+                  "v_pk_add_u16 %4, %4, %2\n\t"
+                  "v_pk_add_u16 %5, %5, %3"
+                  : "=&v"(d0), "=&v"(d1), "=&v"(d2), "=&v"(d3), "+v"(acc0), "+v"(acc1)
+                  : "v"(x.x), "v"(x.y), "v"(x.z), "v"(x.w), "v"(m1), "v"(one));
             }
-            const int c2 = (int)(acc0 & 0xFFFFu) + (int)(acc0 >> 16) + (int)(acc1 & 0xFFFFu) + (int)(acc1 >> 16);
+            int c2 = (int)(acc0 & 0xFFFFu) + (int)(acc0 >> 16) + (int)(acc1 & 0xFFFFu) + (int)(acc1 >> 16);
+            c2 += __builtin_amdgcn_mov_dpp(c2, 0xB1, 0xF, 0xF, false);  // quad_perm xor 1
+            c2 += __builtin_amdgcn_mov_dpp(c2, 0x4E, 0xF, 0xF, false);  // quad_perm xor 2
             if (c2 >= kk) lo = mid;
             else hi = mid - 1;
           }
           th = lo - 1;
         }
-        theta[(size_t)sg * N + cx] = th;
-        if (stmp) {
-          const uint64_t ts3 = __builtin_amdgcn_s_memtime();
-          dbg[12] += ts1 - ts0;
-          dbg[13] += ts2 - ts1;
-          dbg[14] += ts3 - ts2;
-          dbg[15] += 1;
-        }
+        if (cx < N && pb == 0) theta[(size_t)sg * N + cx] = th;
+      }
+      if (stmp) {
+        const uint64_t ts3 = __builtin_amdgcn_s_memtime();
+        dbg[12] += ts1 - ts0;
+        dbg[13] += ts2 - ts1;
+        dbg[14] += ts3 - ts2;
+        dbg[15] += 1;
       }
       __syncthreads();
     }
