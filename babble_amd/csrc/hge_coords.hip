@@ -546,9 +546,10 @@ __global__ void __launch_bounds__(256) k_fdt_runs(Tables t, const int32_t* LAT, 
 // grid N blocks (chain c), thread j = chain j: one load per thread and a block
 // min (a thread looping over the N chains was a chain of 256 dependent-latency
 // loads: ~40 us per online call at N = 256)
-__global__ void __launch_bounds__(256) k_fd_qlo(Tables t, const int32_t* olen, const int32_t* len, int32_t* qlo) {
+__device__ __forceinline__ void fd_qlo_body(const Tables& t, const int32_t* olen, const int32_t* len, int32_t* qlo,
+                                            int c) {
   __shared__ int s_m;
-  const int c = blockIdx.x, j = threadIdx.x;
+  const int j = threadIdx.x;
   if (j == 0) s_m = olen[c];  // the new positions themselves
   __syncthreads();
   if (j < t.N && len[j] != olen[j]) {  // chain j got a new event
@@ -558,6 +559,20 @@ __global__ void __launch_bounds__(256) k_fd_qlo(Tables t, const int32_t* olen, c
   }
   __syncthreads();
   if (j == 0) qlo[c] = max(0, s_m);
+}
+__global__ void __launch_bounds__(256) k_fd_qlo(Tables t, const int32_t* olen, const int32_t* len, int32_t* qlo) {
+  fd_qlo_body(t, olen, len, qlo, blockIdx.x);
+}
+// k_chain_fill (blocks [0, nfb)) and k_fd_qlo (the N blocks after) in one launch:
+// the row bounds read only the old events' LA rows, which the batch leaves alone
+__global__ void __launch_bounds__(256) k_chain_fill_qlo(Tables t, int n0, int n1, const UpEv* up, UpDst dst, int nfb,
+                                                        const int32_t* olen, const int32_t* len, int32_t* qlo) {
+  if ((int)blockIdx.x < nfb) {
+    const int x = n0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (x < n1) chain_fill_one(t, x, n0, up, dst);
+  } else {
+    fd_qlo_body(t, olen, len, qlo, blockIdx.x - nfb);
+  }
 }
 
 }  // namespace hge

@@ -214,6 +214,7 @@ struct hge_engine {
   DBuf<int32_t> s_kctl;
   std::vector<int32_t> h_kctl;
   std::vector<int2> h_segs;
+  bool qlo_fused = false;  // k_fd_qlo ran with k_chain_fill (coords_a)
   int32_t *k_rs = nullptr, *k_len = nullptr, *k_plo = nullptr, *k_qlo = nullptr, *k_lo = nullptr;
   int2* k_segs = nullptr;
   int32_t* k_segbase = nullptr;
@@ -516,7 +517,9 @@ struct hge_engine {
     if (N > 32) d_ssc.grow_keep(nr * N * NW, oldn * NW, st, 0);
     d_fame.grow_keep(nr * N, oldn, st, 0);
     d_rcnt.grow_keep(nr, Rcap, st, 0);
-    d_minw.need(nr + 4);  // + round count, overflow flag, lowest candidate round, hand-off error (k_round_minw)
+    // + round count, overflow flag, lowest candidate round, hand-off error and up to 16
+    // partial lowest rounds (k_round_minw)
+    d_minw.need(nr + 20);
     // C must be INF32 beyond the old rows
     fill_i32(d_C.p + oldn, (int64_t)(nr - Rcap) * N, INF32);
     sync();
@@ -913,9 +916,17 @@ struct hge_engine {
       fill_up = packed ? (const UpEv*)s_up.p : (const UpEv*)nullptr;
       fill_dst = UpDst{d_creator.p, d_index.p, d_sp.p, d_op.p, d_ntx.p, d_ts.p, d_S.p, d_coin.p};
       up_n0 = up_n1 = -1;
-      if (!la_seq_ok(n1 - n0))  // (k_la_seq fills the chain table itself)
-        KLAUNCH(k_chain_fill, dim3(div_up((int)(n1 - n0), 256)), dim3(256), 0, st, t, (int)n0, (int)n1, fill_up,
-                fill_dst);
+      qlo_fused = false;
+      if (!la_seq_ok(n1 - n0)) {  // (k_la_seq fills the chain table itself)
+        const int nfb = div_up((int)(n1 - n0), 256);
+        if (!fresh && N <= 256) {  // + k_fd_qlo's blocks (coords_b)
+          KLAUNCH(k_chain_fill_qlo, dim3(nfb + N), dim3(256), 0, st, t, (int)n0, (int)n1, fill_up, fill_dst, nfb,
+                  (const int32_t*)k_len, (const int32_t*)(k_len + N), k_qlo);
+          qlo_fused = true;
+        } else {
+          KLAUNCH(k_chain_fill, dim3(nfb), dim3(256), 0, st, t, (int)n0, (int)n1, fill_up, fill_dst);
+        }
+      }
     }
     coords_sweep(t, (int)segs.size(), SEG, maxnew, fresh);
     cs_pending = true;
@@ -1056,21 +1067,24 @@ struct hge_engine {
         KLAUNCH(k_round_assign, dim3(div_up(m, 256)), dim3(256), 0, st, t, (int)n0, (int)n1,
                 (const int32_t*)k_rs, s_newwit.p, k_rs + 2, und_appended ? d_und.p + n_und : (int32_t*)nullptr);
       }
-      {
-        int G = 1;
-        while (G < std::min(N, 64)) G <<= 1;
-        const int64_t wmax = std::min<int64_t>(m, (int64_t)Rcap * N);  // witnesses <= both
-        KLAUNCH(k_witness_bits, dim3(std::min(div_up(wmax * NW * G, 256), 8192)), dim3(256), 0,
-                st, t, s_newwit.p, k_rs + 2, N > 32 ? (const uint64_t*)d_ssc.p : nullptr, G);
-      }
+      // k_witness_bits (new witnesses' see / strongly-see bitsets) and k_round_minw
+      // (first witness per round, round count, the candidates' lowest round) in one
+      // launch (k_round_tail)
       // the lowest round of the next batch's candidates (the undetermined list and the
       // events the next divide appends), read with the round count (a fresh replay's
       // candidates start at event 0, round 0: nothing to read); an online call's few
       // candidates are reduced by one extra block of k_round_minw
-      const bool mr = !fresh && n_und + (n1 - n_divided) <= 65536;
-      KLAUNCH(k_round_minw, dim3(div_up(Rcap, 4) + (mr ? 1 : 0)), dim3(256), 0, st, t, 0,
-              (const int32_t*)k_rs, d_minw.p, (const int32_t*)coop_err_src, mr ? 1 : 0, (const int32_t*)d_und.p,
-              (int)n_und, (int)n_divided, (int)n1);
+      const int64_t n_mr = n_und + (n1 - n_divided);
+      const int mr = !fresh && n_mr <= 65536 ? (int)std::max<int64_t>(1, std::min<int64_t>(16, div_up(n_mr, 2048))) : 0;
+      {
+        int G = 1;
+        while (G < std::min(N, 64)) G <<= 1;
+        const int64_t wmax = std::min<int64_t>(m, (int64_t)Rcap * N);  // witnesses <= both
+        const int nb_wb = std::max(1, std::min(div_up(wmax * NW * G, 256), 8192));
+        KLAUNCH(k_round_tail, dim3(nb_wb + div_up(Rcap, 4) + mr), dim3(256), 0, st, t, s_newwit.p, k_rs + 2,
+                N > 32 ? (const uint64_t*)d_ssc.p : nullptr, G, nb_wb, (const int32_t*)k_rs, d_minw.p,
+                (const int32_t*)coop_err_src, mr, (const int32_t*)d_und.p, (int)n_und, (int)n_divided, (int)n1);
+      }
       if (!fresh && !mr) {
         if (n_und > 0)
           KLAUNCH(k_min_round, dim3(div_up(n_und, 256)), dim3(256), 0, st, d_round.p, d_und.p, (int)n_und,
@@ -1079,10 +1093,13 @@ struct hge_engine {
           KLAUNCH(k_min_round_range, dim3(div_up(n1 - n_divided, 256)), dim3(256), 0, st, d_round.p,
                   (int)n_divided, (int)n1, d_minw.p + Rcap + 2);
       }
-      h_minw.resize(Rcap + 4);
-      d2h(h_minw.data(), d_minw.p, 4 * ((size_t)Rcap + 4));
+      h_minw.resize(Rcap + 4 + mr);
+      d2h(h_minw.data(), d_minw.p, 4 * ((size_t)Rcap + 4 + mr));
       sync();
-      if (!fresh) mnr_pre = h_minw[Rcap + 2];
+      if (!fresh) {
+        mnr_pre = h_minw[Rcap + 2];
+        for (int b = 0; b < mr; b++) mnr_pre = std::min(mnr_pre, h_minw[Rcap + 4 + b]);
+      }
       if (coop_err_check && coop_err_src) coop_err = h_minw[Rcap + 3];
       coop_err_src = nullptr;
       mnr_key[0] = fresh ? -1 : n_und;
@@ -1612,7 +1629,8 @@ struct hge_engine {
     // tiles past their grid, sized here for the new positions plus a tile)
     int span = 1;
     if (!fresh) {
-      KLAUNCH(k_fd_qlo, dim3(N), dim3(256), 0, st, t, olen, len, k_qlo);
+      if (!qlo_fused) KLAUNCH(k_fd_qlo, dim3(N), dim3(256), 0, st, t, olen, len, k_qlo);
+      qlo_fused = false;
       span = maxnew + 64;
     } else {
       for (int c = 0; c < N; c++) span = std::max(span, chain_len[c]);
@@ -1792,8 +1810,10 @@ struct hge_engine {
     unsigned long long* o_ntx = (unsigned long long*)(s_out.p + 4);
     // the results header zeroed, with the new LastConsensusRound (o_cnt[3]) when the
     // device holds it (one launch in place of a memset and a copy)
-    KLAUNCH(k_out_init, dim3(div_up(8 + ncalls, 256)), dim3(256), 0, st, s_out.p, 8 + ncalls,
-            lcr_dev ? (const int32_t*)(c_flags + 1) : (const int32_t*)nullptr);
+    // (folded into k_visibility's launch when that runs)
+    const int32_t* lcr_src = lcr_dev ? (const int32_t*)(c_flags + 1) : (const int32_t*)nullptr;
+    if (!(ord && nr > 0))
+      KLAUNCH(k_out_init, dim3(div_up(8 + ncalls, 256)), dim3(256), 0, st, s_out.p, 8 + ncalls, lcr_src);
     if (ord) {
       if (nr > 0) {
         SegInfo si;
@@ -1811,8 +1831,8 @@ struct hge_engine {
         s_segcnt.need(nr);
         s_vis.need(std::max<int64_t>(n_coords, 1));
         // first call at which each event is visible (arrivals, round received)
-        KLAUNCH(k_visibility, dim3(div_up(n_coords, 256)), dim3(256), 0, st, (const int64_t*)c_nc,
-                ncalls, (int)n_coords, s_vis.p);
+        KLAUNCH(k_visibility, dim3(div_up(n_coords, 256) + div_up(8 + ncalls, 256)), dim3(256), 0, st,
+                (const int64_t*)c_nc, ncalls, (int)n_coords, s_vis.p, s_out.p, 8 + ncalls, lcr_src);
         // one pass into per-round capacity slots (no count round trip); theta inline
         // for N <= 64, by k_seg_theta_wide above
         const int G = group_lanes();
@@ -1926,9 +1946,10 @@ struct hge_engine {
         KLAUNCH(k_bucket_sort, dim3(std::min(ncalls, 2048)), dim3(256), 0, st,
                 (const int32_t*)s_bpos.p, (const int32_t*)o_cc, (const int32_t*)blist,
                 (const int32_t*)nblist, k1, k2, o_ids, 1);
-        KLAUNCH(k_bucket_sort_big, dim3(std::min(ncalls, n_cu())), dim3(1024), 0, st,
-                (const int32_t*)s_bpos.p, (const int32_t*)o_cc, (const int32_t*)blist,
-                (const int32_t*)nblist, (const OKey*)k1, k2, o_ids);
+        if (ncand > 512)  // (no bucket past 512 keys otherwise: an online call's sort is one launch)
+          KLAUNCH(k_bucket_sort_big, dim3(std::min(ncalls, n_cu())), dim3(1024), 0, st,
+                  (const int32_t*)s_bpos.p, (const int32_t*)o_cc, (const int32_t*)blist,
+                  (const int32_t*)nblist, (const OKey*)k1, k2, o_ids);
         // new undetermined list (in candidate order)
         scan_large(s_fund.p, s_upos.p, ncand, o_cnt + 1);
         // scatter into the spare list (same capacity) and swap: no device copy

@@ -124,8 +124,19 @@ __global__ void __launch_bounds__(1024) k_scan_small(const int32_t* in, int32_t*
   const int T = blockDim.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int per = (n + T - 1) / T;
   const int lo = min(n, tid * per), hi = min(n, lo + per);
+  // runs up to 16 (n <= 16k, scan_large's case) are loaded at once and kept in
+  // registers (a loop of dependent-issue loads, read twice, was ~10 us at n = 10k)
+  constexpr int RK = 16;
+  int rv[RK];
   int s = 0;
-  for (int i = lo; i < hi; i++) s += in[i];
+  if (per <= RK) {
+#pragma unroll
+    for (int k = 0; k < RK; k++) rv[k] = lo + k < hi ? in[lo + k] : 0;
+#pragma unroll
+    for (int k = 0; k < RK; k++) s += rv[k];
+  } else {
+    for (int i = lo; i < hi; i++) s += in[i];
+  }
   int inc = s;  // inclusive scan over the wave
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -145,10 +156,18 @@ __global__ void __launch_bounds__(1024) k_scan_small(const int32_t* in, int32_t*
   }
   __syncthreads();
   int run = (wv > 0 ? wsum[wv - 1] : 0) + inc - s;
-  for (int i = lo; i < hi; i++) {
-    const int v = in[i];
-    out[i] = run;
-    run += v;
+  if (per <= RK) {
+#pragma unroll
+    for (int k = 0; k < RK; k++) {
+      if (lo + k < hi) out[lo + k] = run;
+      run += rv[k];
+    }
+  } else {
+    for (int i = lo; i < hi; i++) {
+      const int v = in[i];
+      out[i] = run;
+      run += v;
+    }
   }
   if (tid == T - 1 && total) *total = wsum[T / 64 - 1];
 }
@@ -908,35 +927,50 @@ __global__ void k_round_ranges(Tables t, const int32_t* len, const int32_t* rsta
 // minw[r] = the lowest witness id of round r: one wave per round, lanes over the
 // creators (a thread per round looping over N creators was latency-bound: ~27 us
 // per online call at N = 256)
-// mr (an online call's candidates, few): the grid's last block also takes the
-// lowest round over und[0, n_und) and the ids [lo, hi) and stores it at
-// minw[Rcap+2] itself (in place of k_min_round / k_min_round_range)
-__global__ void __launch_bounds__(256) k_round_minw(Tables t, int r0, const int32_t* rstate, int32_t* minw,
-                                                    const int32_t* err_in, int mr, const int32_t* und, int n_und,
-                                                    int lo, int hi) {
-  if (mr && blockIdx.x == gridDim.x - 1) {
+// mr (an online call's candidates, few): the grid's last mr blocks also take the
+// lowest round over und[0, n_und) and the ids [lo, hi), each over its slice, and
+// store their partial minima at minw[Rcap+4+b] (the host folds them: in place of
+// k_min_round / k_min_round_range; one block looping over ~10k gathers was ~15 us)
+__device__ __forceinline__ void round_minw_body(const Tables& t, int r0, const int32_t* rstate, int32_t* minw,
+                                                const int32_t* err_in, int mr, const int32_t* und, int n_und,
+                                                int lo, int hi, int bid, int nblocks) {
+  if (mr && bid >= nblocks - mr) {
     __shared__ int s_m;
+    const int b = bid - (nblocks - mr);
     if (threadIdx.x == 0) s_m = INF32;
     __syncthreads();
     int m = INF32;
-    for (int i = threadIdx.x; i < n_und; i += blockDim.x) m = min(m, t.round[und[i]]);
-    for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) m = min(m, t.round[i]);
+    const int tot = n_und + (hi - lo);
+    constexpr int U = 8;
+    for (int i0 = b * 256 * U + threadIdx.x; i0 < tot; i0 += mr * 256 * U) {
+      int id[U];
+#pragma unroll
+      for (int k = 0; k < U; k++) {
+        const int i = i0 + k * 256;
+        id[k] = i < n_und ? und[min(i, n_und - 1)] : lo + (i - n_und);
+      }
+      int rv[U];
+#pragma unroll
+      for (int k = 0; k < U; k++) rv[k] = i0 + k * 256 < tot ? t.round[id[k]] : INF32;
+#pragma unroll
+      for (int k = 0; k < U; k++) m = min(m, rv[k]);
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = min(m, __shfl_xor(m, o));
     if ((threadIdx.x & 63) == 0) atomicMin(&s_m, m);
     __syncthreads();
-    if (threadIdx.x == 0) minw[t.Rcap + 2] = s_m;
+    if (threadIdx.x == 0) minw[t.Rcap + 4 + b] = s_m;
     return;
   }
-  const int r = r0 + blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int r = r0 + bid * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   // the round count and overflow flag ride along at minw[Rcap..Rcap+1], the next
   // batch's lowest candidate round at [Rcap+2] (INF32 here when k_min_round* lower it
   // after this kernel) and the rounds walk's hand-off error flag at [Rcap+3]: one
   // readback for all of them
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (bid == 0 && threadIdx.x == 0) {
     minw[t.Rcap] = rstate[0];
     minw[t.Rcap + 1] = rstate[1];
-    if (!mr) minw[t.Rcap + 2] = INF32;
+    minw[t.Rcap + 2] = INF32;
     minw[t.Rcap + 3] = err_in ? *err_in : 0;
   }
   if (rstate[1] || r >= rstate[0]) return;
@@ -956,8 +990,8 @@ __global__ void __launch_bounds__(256) k_round_minw(Tables t, int r0, const int3
 // One group of G lanes (G = N rounded up to a power of two, at most 64) per
 // (witness, 64-slot word): the group's ballots ARE the word, stored by its
 // first lane (no global atomics: same-address atomics serialise at memory).
-__global__ void k_witness_bits(Tables t, const int32_t* newwit, const int32_t* pnnew,
-                               const uint64_t* ssc, int G) {
+__device__ __forceinline__ void witness_bits_body(const Tables& t, const int32_t* newwit, const int32_t* pnnew,
+                                                  const uint64_t* ssc, int G, int bid, int nblocks) {
   const int N = t.N, NW = t.NW;
   const int lane = threadIdx.x & 63;
   const int gl = lane & (G - 1);
@@ -965,8 +999,8 @@ __global__ void k_witness_bits(Tables t, const int32_t* newwit, const int32_t* p
   const int gshift = G == 64 ? 0 : (lane & ~(G - 1));
   // grid-stride over whole groups (the count lives on the device)
   const int64_t total = (int64_t)(*pnnew) * NW * G;
-  for (int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; item < total;
-       item += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t item = (int64_t)bid * blockDim.x + threadIdx.x; item < total;
+       item += (int64_t)nblocks * blockDim.x) {
     const int64_t grp = item / G;
     const int y = newwit[grp / NW];
     const int wd = (int)(grp - (grp / NW) * NW);
@@ -997,6 +1031,16 @@ __global__ void k_witness_bits(Tables t, const int32_t* newwit, const int32_t* p
       t.ssb[off] = bss;
     }
   }
+}
+
+// the rounds step's tail in one launch: blocks [0, nb_wb) k_witness_bits' work,
+// the rest k_round_minw's (they are independent; one launch less per call)
+__global__ void __launch_bounds__(256) k_round_tail(Tables t, const int32_t* newwit, const int32_t* pnnew,
+                                                    const uint64_t* ssc, int G, int nb_wb, const int32_t* rstate,
+                                                    int32_t* minw, const int32_t* err_in, int mr, const int32_t* und,
+                                                    int n_und, int lo, int hi) {
+  if ((int)blockIdx.x < nb_wb) witness_bits_body(t, newwit, pnnew, ssc, G, blockIdx.x, nb_wb);
+  else round_minw_body(t, 0, rstate, minw, err_in, mr, und, n_und, lo, hi, blockIdx.x - nb_wb, gridDim.x - nb_wb);
 }
 
 // ---------------------------------------------------------------------------
@@ -1381,11 +1425,19 @@ struct SegInfo {
 // events [0, nev): a block takes 256 consecutive events and binary-searches
 // them in an LDS window of the calls from the first one that sees its first
 // event (the global search is the fallback past the window)
+// out (non-null): the blocks past the events' also zero the results header
+// out[0, nout) with out[3] = *lcr when given (k_out_init's work, one launch less)
 __global__ void __launch_bounds__(256) k_visibility(const int64_t* nc, int ncalls, int nev,
-                                                    int32_t* vis) {
+                                                    int32_t* vis, int32_t* out, int nout, const int32_t* lcr) {
   __shared__ int64_t s_nc[256];
   __shared__ int s_c0;
   const int tid = threadIdx.x;
+  const int nvb = (nev + 255) >> 8;
+  if ((int)blockIdx.x >= nvb) {
+    const int i = ((int)blockIdx.x - nvb) * 256 + tid;
+    if (i < nout) out[i] = (i == 3 && lcr) ? *lcr : 0;
+    return;
+  }
   const int x0 = blockIdx.x * 256;
   auto upper = [&](int64_t x, int lo, int hi) {
     while (lo < hi) {
@@ -2255,6 +2307,21 @@ __device__ int merge_corank(const OKey* A, int la, const OKey* B, int lb, int k)
   return lo;
 }
 
+// barrier after a bitonic stage of stride cur followed by one of stride nxt: with
+// i = pair index = thread (+ k * blockDim), a stride <= 64 keeps a wave's pairs
+// inside its own 128 slots [128w, 128w + 128), so two such stages in a row need
+// only the wave's own LDS order (no block barrier: 10 of 55 stages at 1,024 keys
+// keep one)
+__device__ __forceinline__ void bitonic_sync(int cur, int nxt) {
+  if (cur <= 64 && nxt <= 64) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  } else {
+    __syncthreads();
+  }
+}
+
 // LDS chunk of keys as structure-of-arrays (conflict-free per field) sorted
 // through a uint16 index permutation: a compare-exchange reads two indices and
 // the fields up to the first difference, and swaps only the indices.
@@ -2309,7 +2376,7 @@ struct SortChunk {
             ix[hi] = (uint16_t)x;
           }
         }
-        __syncthreads();
+        bitonic_sync(stride, stride > 1 ? stride >> 1 : size);
       }
     }
   }
@@ -2467,7 +2534,7 @@ __device__ void big_bitonic(const OKey* K, int n, uint64_t* sb, uint32_t* sr, ui
           ix[hi] = (uint16_t)x;
         }
       }
-      __syncthreads();
+      bitonic_sync(stride, stride > 1 ? stride >> 1 : size);
     }
   }
 }

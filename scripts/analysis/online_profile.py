@@ -22,6 +22,7 @@ def run(n, E, K, ncalls, profile):
     if profile:
         eng.set_profiling(True)
     lat = []
+    cpu = []
     prev = 0
     s0 = eng.host_syncs()
     warm = min(200, len(calls) // 4)
@@ -29,18 +30,22 @@ def run(n, E, K, ncalls, profile):
         if profile and i == warm:
             eng.set_profiling(True)  # (resets the stats)
         t = time.perf_counter()
+        tc = time.thread_time()
         eng.insert_events(ev[prev:c])
         eng.run_consensus()
         lat.append(time.perf_counter() - t)
+        cpu.append(time.thread_time() - tc)
         prev = c
     syncs = (eng.host_syncs() - s0) / len(calls)
     stats = eng.kernel_stats() if profile else {}
     eng.close()
     lat = np.array(lat[warm:])
+    cpu = np.array(cpu[warm:])
     per = len(calls) - warm
     ks = sorted(((k, v[0] * 1e3 / per, v[1] / per) for k, v in stats.items()), key=lambda x: -x[1])
     return {"p50_us": round(float(np.percentile(lat, 50)) * 1e6, 1),
             "mean_us": round(float(lat.mean()) * 1e6, 1),
+            "host_cpu_us_mean": round(float(cpu.mean()) * 1e6, 1),
             "round_trips_per_call": round(syncs, 2),
             "device_us_per_call": round(sum(k[1] for k in ks), 1),
             "launches_per_call": round(sum(k[2] for k in ks), 1),
