@@ -128,15 +128,41 @@ __global__ void __launch_bounds__(256) k_la_sweep(Tables t, const int2* segs, in
 //   phase 2 (the first NP lanes of wave 0, lane = column): the events in order,
 //     folding their in-batch parents' rows from LDS (two LDS reads per event);
 //   phase 3: the rows to LA, coalesced.
+// lowest chain-c position whose FD row a new event can change:
+// min over chains j with old events of LA[(j, olen_j - 1)][c] + 1
+// grid N blocks (chain c), thread j = chain j: one load per thread and a block
+// min (a thread looping over the N chains was a chain of 256 dependent-latency
+// loads: ~40 us per online call at N = 256)
+__device__ __forceinline__ void fd_qlo_body(const Tables& t, const int32_t* olen, const int32_t* len, int32_t* qlo,
+                                            int c) {
+  __shared__ int s_m;
+  const int j = threadIdx.x;
+  if (j == 0) s_m = olen[c];  // the new positions themselves
+  __syncthreads();
+  if (j < t.N && len[j] != olen[j]) {  // chain j got a new event
+    const int ol = olen[j];
+    const int v = ol > 0 ? la_at(t, j, ol - 1, c) + 1 : 0;
+    atomicMin(&s_m, v);
+  }
+  __syncthreads();
+  if (j == 0) qlo[c] = max(0, s_m);
+}
 // m * NP <= LASEQ_MAX (the host checks; larger batches take the sweeps).
 constexpr int LASEQ_MAX = 8192;
 // It also fills the chain table for the batch first (k_chain_fill's work: one
 // launch less per online call); the barrier makes those global writes visible to
 // the block.
+// qlo (non-null): blocks 1 .. N take k_fd_qlo's work for chain blockIdx.x - 1 (it
+// reads only the old events' LA rows; one launch less per online call)
 template <int NP>
-__global__ void __launch_bounds__(256) k_la_seq(Tables t, int n0, int n1, const UpEv* up, UpDst dst) {
+__global__ void __launch_bounds__(256) k_la_seq(Tables t, int n0, int n1, const UpEv* up, UpDst dst,
+                                                const int32_t* qolen, const int32_t* qlen, int32_t* qlo) {
   __shared__ int rows[LASEQ_MAX];
   __shared__ int2 par[LASEQ_MAX / NP];
+  if (blockIdx.x > 0) {
+    fd_qlo_body(t, qolen, qlen, qlo, blockIdx.x - 1);
+    return;
+  }
   constexpr int G = 256 / NP;
   const int N = t.N, m = n1 - n0;
   const int tid = threadIdx.x, i = tid % NP;
@@ -316,21 +342,29 @@ __global__ void __launch_bounds__(256) k_la_sweep16(Tables t, const int2* segs, 
 // every other new position lies in a new event's run.  Tile: positions
 // [p0, p0 + 64) of chain j (from plo_j = olen_j - 1: the row before the first
 // new event is the first run's lower bound) x columns [c0, c0 + 64).
-// FT = int32_t (INF32 = none) or uint16_t (0xFFFF = none; N > 128, FD transpose only)
-template <typename FT>
+// FT = int32_t (INF32 = none) or uint16_t (0xFFFF = none; N > 128, FD transpose only).
+// L32: the tile from the int32 LA rows (N <= 32, or a wide hashgraph past the uint16
+// positions), in place of round 3's transpose to a LAT table and a runs kernel over it.
+template <typename FT, bool L32 = false>
 __global__ void __launch_bounds__(256) k_la16_rows_runs(Tables t, FT* FDT, const int32_t* plo,
                                                         const int32_t* olen, const int32_t* len) {
   constexpr FT FINF = sizeof(FT) == 2 ? (FT)0xFFFF : (FT)INF32;
   __shared__ int32_t tile[65][65];  // row 0: position p0 - 1; row 1 + r: position p0 + r
   const int N = t.N;
   const size_t ccap = t.ccap;
-  const int j = blockIdx.z;
+  // XCD-aware tile order (xcd_block): neighbouring position tiles of a (chain, column
+  // tile) write neighbouring q ranges of the same 64 FDT rows, and now run on one XCD,
+  // whose L2 merges the cache lines they share instead of writing partial lines from two
+  const int64_t gxy = (int64_t)gridDim.x * gridDim.y;
+  const int64_t lb = xcd_block(blockIdx.x + (int64_t)gridDim.x * blockIdx.y + gxy * blockIdx.z, gxy * gridDim.z);
+  const int bz = (int)(lb / gxy), by = (int)((lb - bz * gxy) / gridDim.x), bx = (int)(lb - bz * gxy - (int64_t)by * gridDim.x);
+  const int j = bz;
   const int lj = len[j], oj = olen[j];
-  const int p0 = plo[j] + blockIdx.x * 64;
-  const int c0 = blockIdx.y * 64;
+  const int p0 = plo[j] + bx * 64;
+  const int c0 = by * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
   if (lj == 0) {  // empty chain: every new position of every chain c has no chain-j descendant
-    if (blockIdx.x == 0)
+    if (bx == 0)
       for (int cc = ty; cc < 64; cc += 4) {
         const int c = c0 + cc;
         if (c >= N) continue;
@@ -344,21 +378,39 @@ __global__ void __launch_bounds__(256) k_la16_rows_runs(Tables t, FT* FDT, const
   // row r, lanes 32..63 the same word of row r + 1.  All of a thread's loads are
   // issued before the first LDS store (the loop as written compiled to one load and a
   // vmcnt(0) wait per row pair: nine serial memory latencies per tile)
-  constexpr int NIT = 9;  // r = 2 ty + 8 i < 66
-  uint32_t xv[NIT];
+  if constexpr (L32) {
+    // 65 rows x 64 columns, lane = column: 17 loads per thread, all in flight
+    constexpr int NIT = 17;  // 256 * 17 >= 65 * 64
+    int xv[NIT];
 #pragma unroll
-  for (int i = 0; i < NIT; i++) {
-    const int rr = 2 * ty + 8 * i + (tx >> 5), w = tx & 31;
-    const int p = p0 - 1 + rr, c = c0 + 2 * w;
-    const bool ok = rr < 65 && p >= 0 && p < lj && c < N;
-    xv[i] = ok ? t.LA16[rowoff16(t, j, ok ? p : 0) + (ok ? (c >> 1) : 0)] : 0u;  // 0: -1 after unpacking
-  }
+    for (int i = 0; i < NIT; i++) {
+      const int idx = (int)threadIdx.x + 256 * i, rr = idx >> 6, c = c0 + (idx & 63);
+      const int p = p0 - 1 + rr;
+      const bool ok = rr < 65 && p >= 0 && p < lj && c < N;
+      xv[i] = ok ? t.LA[((size_t)j * ccap + p) * N + c] : -1;
+    }
 #pragma unroll
-  for (int i = 0; i < NIT; i++) {
-    const int rr = 2 * ty + 8 * i + (tx >> 5), w = tx & 31;
-    if (rr < 65) {
-      tile[rr][2 * w] = (int)(xv[i] & 0xFFFFu) - 1;
-      tile[rr][2 * w + 1] = (int)(xv[i] >> 16) - 1;
+    for (int i = 0; i < NIT; i++) {
+      const int idx = (int)threadIdx.x + 256 * i, rr = idx >> 6;
+      if (rr < 65) tile[rr][idx & 63] = xv[i];
+    }
+  } else {
+    constexpr int NIT = 9;  // r = 2 ty + 8 i < 66
+    uint32_t xv[NIT];
+#pragma unroll
+    for (int i = 0; i < NIT; i++) {
+      const int rr = 2 * ty + 8 * i + (tx >> 5), w = tx & 31;
+      const int p = p0 - 1 + rr, c = c0 + 2 * w;
+      const bool ok = rr < 65 && p >= 0 && p < lj && c < N;
+      xv[i] = ok ? t.LA16[rowoff16(t, j, ok ? p : 0) + (ok ? (c >> 1) : 0)] : 0u;  // 0: -1 after unpacking
+    }
+#pragma unroll
+    for (int i = 0; i < NIT; i++) {
+      const int rr = 2 * ty + 8 * i + (tx >> 5), w = tx & 31;
+      if (rr < 65) {
+        tile[rr][2 * w] = (int)(xv[i] & 0xFFFFu) - 1;
+        tile[rr][2 * w + 1] = (int)(xv[i] >> 16) - 1;
+      }
     }
   }
   __syncthreads();
@@ -517,49 +569,6 @@ __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const FT* FDT
   }
 }
 
-// runs: chain-j event k (new) is the first chain-j descendant of chain-c
-// positions (LAT[j][c][k-1], LAT[j][c][k]].  The new chain-c positions past the
-// last chain-j event's ancestor have no chain-j descendant yet (INF32); every
-// other new position lies in a new event's run (an old event cannot have a new
-// ancestor), so no separate clear pass is needed.  FDR_K events per workgroup.
-constexpr int FDR_K = 1024;
-__global__ void __launch_bounds__(256) k_fdt_runs(Tables t, const int32_t* LAT, int32_t* FDT,
-                                                  const int32_t* olen, const int32_t* len) {
-  const int c = blockIdx.y, j = blockIdx.z;
-  const size_t base = ((size_t)j * t.N + c) * t.ccap;
-  int32_t* row = FDT + base;
-  const int oj = olen[j], lj = len[j], oc = olen[c], lc = len[c];
-  const int tail0 = max(oc, lj > 0 ? LAT[base + lj - 1] + 1 : 0);
-  for (int q = tail0 + blockIdx.x * blockDim.x + threadIdx.x; q < lc; q += gridDim.x * blockDim.x)
-    row[q] = INF32;
-  const int k0 = oj + blockIdx.x * FDR_K;
-  const int k1 = min(lj, k0 + FDR_K);
-  for (int k = k0 + threadIdx.x; k < k1; k += blockDim.x) {
-    const int hi = LAT[base + k];
-    const int lo = k > 0 ? LAT[base + k - 1] : -1;
-    for (int q = lo + 1; q <= hi; q++) row[q] = k;
-  }
-}
-
-// lowest chain-c position whose FD row a new event can change:
-// min over chains j with old events of LA[(j, olen_j - 1)][c] + 1
-// grid N blocks (chain c), thread j = chain j: one load per thread and a block
-// min (a thread looping over the N chains was a chain of 256 dependent-latency
-// loads: ~40 us per online call at N = 256)
-__device__ __forceinline__ void fd_qlo_body(const Tables& t, const int32_t* olen, const int32_t* len, int32_t* qlo,
-                                            int c) {
-  __shared__ int s_m;
-  const int j = threadIdx.x;
-  if (j == 0) s_m = olen[c];  // the new positions themselves
-  __syncthreads();
-  if (j < t.N && len[j] != olen[j]) {  // chain j got a new event
-    const int ol = olen[j];
-    const int v = ol > 0 ? la_at(t, j, ol - 1, c) + 1 : 0;
-    atomicMin(&s_m, v);
-  }
-  __syncthreads();
-  if (j == 0) qlo[c] = max(0, s_m);
-}
 __global__ void __launch_bounds__(256) k_fd_qlo(Tables t, const int32_t* olen, const int32_t* len, int32_t* qlo) {
   fd_qlo_body(t, olen, len, qlo, blockIdx.x);
 }

@@ -163,7 +163,7 @@ struct hge_engine {
   DBuf<int32_t> s_part, s_fst;
   // coordinate sweeps: transposed tables and scratch
   int n_sweeps = 0;
-  DBuf<int32_t> d_LAT, d_FDT, s_chg, s_bar, s_dirty;
+  DBuf<int32_t> d_FDT, s_chg, s_bar, s_dirty;
   // windowed lastAncestors (hge_coords_win.hip): chunk plans, row sums, starting rows
   DBuf<int4> s_lwplan;
   DBuf<uint32_t> s_lwsum, s_lwinit;
@@ -353,7 +353,7 @@ struct hge_engine {
                              &d_W,       &d_rcnt,   &d_minw,  &s_small,  &s_newwit,  &s_LCR,
                              &s_clast,   &s_segcnt, &s_segcall, &s_seground, &s_theta,
                              &s_recv,    &s_rr,     &s_bpos,  &s_fund,   &s_upos,    &s_vis,
-                             &s_und2,    &s_part,   &s_fst,    &d_FSS,     &d_LAT,
+                             &s_und2,    &s_part,   &s_fst,    &d_FSS,
                              &d_FDT,     &s_chg,    &s_bar,   &s_bseg,   &s_kctl,    &s_cctl,
                              &s_out,     &s_hn,     &s_hres,  &s_dirty,  &d_WLA,     &s_lwpos,
                              &s_lwrisky};
@@ -501,7 +501,6 @@ struct hge_engine {
     // first-strong-seer rows (N <= 32): int32 rows of N, or uint16 rows padded to
     // 16/32 columns for the LDS walk; rebuilt from the frontier on, never kept
     if (N <= 32) d_FSS.need((size_t)N * nc * std::max(N, 16));
-    if (!sweep16()) grow_chain_table(d_LAT, nc, false, false);  // rebuilt per batch from LA
     grow_chain_table(d_FDT, nc, true, false);  // persistent: FD in run layout
     ccap = (int)nc;
   }
@@ -602,12 +601,12 @@ struct hge_engine {
     }
     if (known >= chain_limit) {
       if (N > 32 && N <= 256 && !wide32) {  // past the uint16 positions: int32 from here on
-        // the int32 LA and LAT tables must fit beside what is allocated: else refuse
+        // the int32 LA table must fit beside what is allocated: else refuse
         // the event here (the stream stops, as at any rejection) rather than lift
         // the cap and fail at the next coordinate step
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
-            free_b < 2 * sizeof(int32_t) * (size_t)N * N * (size_t)std::max(ccap, known + 2) + (64u << 20)) {
+            free_b < sizeof(int32_t) * (size_t)N * N * (size_t)std::max(ccap, known + 2) + (64u << 20)) {
           err = "Chain capacity exceeded: the int32 position tables past 65,534 events per creator do not fit";
           return HGE_ERR_CAPACITY;
         }
@@ -1415,7 +1414,6 @@ struct hge_engine {
   // positions) instead of packing positions past 65,534 into uint16.
   void to_wide32() {
     grow_chain_table(d_LA, ccap, false);
-    grow_chain_table(d_LAT, ccap, false, false);
     s_w32.need(N);
     h2d(s_w32.p, coords_len.data(), 4 * (size_t)N);
     wide32 = true;
@@ -1550,10 +1548,15 @@ struct hge_engine {
     } else if (la_seq_ok(mnew)) {
       // a small batch (an online call): one exact pass in insertion order, the chain
       // table filled by the same kernel
+      // (+ k_fd_qlo's N blocks past a fresh state: coords_b skips its launch)
+      const bool q = !fresh;
       if (N <= 16)
-        KLAUNCH(k_la_seq<16>, dim3(1), dim3(256), 0, st, t, (int)n_coords, (int)n_events, fill_up, fill_dst);
+        KLAUNCH(k_la_seq<16>, dim3(q ? 1 + N : 1), dim3(256), 0, st, t, (int)n_coords, (int)n_events, fill_up,
+                fill_dst, olen, len, q ? k_qlo : (int32_t*)nullptr);
       else
-        KLAUNCH(k_la_seq<32>, dim3(1), dim3(256), 0, st, t, (int)n_coords, (int)n_events, fill_up, fill_dst);
+        KLAUNCH(k_la_seq<32>, dim3(q ? 1 + N : 1), dim3(256), 0, st, t, (int)n_coords, (int)n_events, fill_up,
+                fill_dst, olen, len, q ? k_qlo : (int32_t*)nullptr);
+      qlo_fused = q;
       n_sweeps = 1;
     } else {
     int32_t* dirty = nullptr;
@@ -1616,12 +1619,11 @@ struct hge_engine {
       KLAUNCH((k_la16_rows_runs<int32_t>), dim3(div_up(maxnew + 1, 64), div_up(N, 64), N), dim3(256), 0, st, t,
               d_FDT.p, k_plo, olen, len);
     } else {
-      // LA -> LAT for positions [olen-1, len), then the runs of the new events (and
-      // the new positions with no descendant yet)
-      KLAUNCH(k_transpose, dim3(div_up(maxnew + 1, 64), div_up(N, 64), N), dim3(256), 0, st, t,
-              (const int32_t*)nullptr, d_LAT.p, k_plo, len, 0);
-      KLAUNCH(k_fdt_runs, dim3(div_up(maxnew, FDR_K), N, N), dim3(256), 0, st, t, d_LAT.p, d_FDT.p,
-              olen, len);
+      // the int32 LA rows -> the runs of the new events (and the new positions with no
+      // descendant yet) through 64 x 64 LDS tiles (one launch; round 3's LA -> LAT
+      // transpose + k_fdt_runs took two and the LAT table)
+      KLAUNCH((k_la16_rows_runs<int32_t, true>), dim3(div_up(maxnew + 1, 64), div_up(N, 64), N), dim3(256), 0,
+              st, t, d_FDT.p, k_plo, olen, len);
     }
     // FDT -> FD rows for every chain-c position a new event can have touched
     // (from a fresh state: every row, qlo = 0 as uploaded; no round trip)
@@ -1933,8 +1935,16 @@ struct hge_engine {
         s_bpos.need(2 * (size_t)ncalls + 2);
         int32_t* blist = s_bpos.p + ncalls;     // non-empty buckets
         int32_t* nblist = s_bpos.p + 2 * ncalls;  // their count
-        KLAUNCH(k_bucket_list, dim3(1), dim3(1024), 0, st, (const int32_t*)o_cc, ncalls, s_bpos.p,
-                o_cnt, blist, nblist);
+        // a small candidate set: the undetermined list's scan and scatter ride with the
+        // call buckets (k_list_und; the list swap below is the same)
+        const bool lu = ncand <= 16384;
+        s_und2.need(d_und.n);
+        if (lu)
+          KLAUNCH(k_list_und, dim3(2), dim3(1024), 0, st, (const int32_t*)o_cc, ncalls, s_bpos.p, o_cnt, blist,
+                  nblist, (const int32_t*)s_fund.p, s_upos.p, (int)ncand, o_cnt + 1, cand, s_und2.p);
+        else
+          KLAUNCH(k_bucket_list, dim3(1), dim3(1024), 0, st, (const int32_t*)o_cc, ncalls, s_bpos.p,
+                  o_cnt, blist, nblist);
         s_keys.need((size_t)ncand * sizeof(OKey));
         s_keys2.need((size_t)ncand * sizeof(OKey));
         OKey* k1 = (OKey*)s_keys.p;
@@ -1950,12 +1960,13 @@ struct hge_engine {
           KLAUNCH(k_bucket_sort_big, dim3(std::min(ncalls, n_cu())), dim3(1024), 0, st,
                   (const int32_t*)s_bpos.p, (const int32_t*)o_cc, (const int32_t*)blist,
                   (const int32_t*)nblist, (const OKey*)k1, k2, o_ids);
-        // new undetermined list (in candidate order)
-        scan_large(s_fund.p, s_upos.p, ncand, o_cnt + 1);
-        // scatter into the spare list (same capacity) and swap: no device copy
-        s_und2.need(d_und.n);
-        KLAUNCH(k_scatter_und, dim3(div_up(ncand, 256)), dim3(256), 0, st, cand, ncand,
-                           s_fund.p, s_upos.p, s_und2.p);
+        // new undetermined list (in candidate order), scattered into the spare list
+        // (same capacity) and swapped: no device copy
+        if (!lu) {
+          scan_large(s_fund.p, s_upos.p, ncand, o_cnt + 1);
+          KLAUNCH(k_scatter_und, dim3(div_up(ncand, 256)), dim3(256), 0, st, cand, ncand, s_fund.p, s_upos.p,
+                  s_und2.p);
+        }
         std::swap(d_und, s_und2);
         got_order = true;
       }

@@ -118,8 +118,10 @@ __global__ void k_min_round_range(const int32_t* round, int lo, int hi, int32_t*
 // exclusive scan of a small int array by one block (n <= ~64k): per-thread
 // contiguous runs, a wave scan by shuffles and one scan of the 16 wave totals
 // (two barriers; a Hillis-Steele over 1024 partials took 20)
-__global__ void __launch_bounds__(1024) k_scan_small(const int32_t* in, int32_t* out, int n,
-                                                     int32_t* total) {
+// scat (non-null): also und[out[i]] = scat[i] for every i with in[i] != 0 (the
+// undetermined list's compaction, k_scatter_und's work)
+__device__ __forceinline__ void scan_small_body(const int32_t* in, int32_t* out, int n, int32_t* total,
+                                                const int32_t* scat, int32_t* und) {
   __shared__ int wsum[16];
   const int T = blockDim.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int per = (n + T - 1) / T;
@@ -159,17 +161,24 @@ __global__ void __launch_bounds__(1024) k_scan_small(const int32_t* in, int32_t*
   if (per <= RK) {
 #pragma unroll
     for (int k = 0; k < RK; k++) {
-      if (lo + k < hi) out[lo + k] = run;
+      if (lo + k < hi) {
+        out[lo + k] = run;
+        if (scat && rv[k]) und[run] = scat[lo + k];
+      }
       run += rv[k];
     }
   } else {
     for (int i = lo; i < hi; i++) {
       const int v = in[i];
       out[i] = run;
+      if (scat && v) und[run] = scat[i];
       run += v;
     }
   }
   if (tid == T - 1 && total) *total = wsum[T / 64 - 1];
+}
+__global__ void __launch_bounds__(1024) k_scan_small(const int32_t* in, int32_t* out, int n, int32_t* total) {
+  scan_small_body(in, out, n, total, nullptr, nullptr);
 }
 
 // multi-block exclusive scan: 1024 elements per 256-thread block
@@ -2384,9 +2393,8 @@ struct SortChunk {
 
 // bucket offsets (exclusive scan of the per-call counts, total = events
 // received) and the list of non-empty buckets, by one block
-__global__ void __launch_bounds__(1024) k_bucket_list(const int32_t* cnt, int n, int32_t* off,
-                                                      int32_t* total, int32_t* list,
-                                                      int32_t* nlist) {
+__device__ __forceinline__ void bucket_list_body(const int32_t* cnt, int n, int32_t* off, int32_t* total,
+                                                 int32_t* list, int32_t* nlist) {
   __shared__ int ts[1024], tn[1024];
   const int T = blockDim.x, tid = threadIdx.x;
   const int per = (n + T - 1) / T;
@@ -2417,6 +2425,20 @@ __global__ void __launch_bounds__(1024) k_bucket_list(const int32_t* cnt, int n,
     *total = ts[T - 1];
     *nlist = tn[T - 1];
   }
+}
+__global__ void __launch_bounds__(1024) k_bucket_list(const int32_t* cnt, int n, int32_t* off, int32_t* total,
+                                                      int32_t* list, int32_t* nlist) {
+  bucket_list_body(cnt, n, off, total, list, nlist);
+}
+// an online call's two single-block steps after k_recv_flags in one launch: block 0
+// the call buckets (k_bucket_list), block 1 the new undetermined list's scan and
+// compaction (k_scan_small + k_scatter_und; fl.size <= 16k)
+__global__ void __launch_bounds__(1024) k_list_und(const int32_t* cnt, int n, int32_t* off, int32_t* total,
+                                                   int32_t* list, int32_t* nlist, const int32_t* f_und,
+                                                   int32_t* upos, int ncand, int32_t* nund, const int32_t* cand,
+                                                   int32_t* und) {
+  if (blockIdx.x == 0) bucket_list_body(cnt, n, off, total, list, nlist);
+  else scan_small_body(f_und, upos, ncand, nund, cand, und);
 }
 
 // keys per bucket that k_bucket_sort_big sorts whole in LDS (k_bucket_sort leaves them to it)

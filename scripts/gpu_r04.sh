@@ -14,6 +14,8 @@
 #   pmc      FETCH_SIZE / WRITE_SIZE passes -> profiles/r04/pmc_traffic.json (the bench's roofline traffic)
 #   diag     SQ / TCC / LDS counter passes at 256/2M
 #   gap      microbenchmarks: launch_gap (stream launches vs a HIP graph), granule_hop (hand-off floor)
+#   ab       same-box A/B: build/ab/libhge_head.so (the last commit's engine), build/ab/libhge_alt.so
+#            (a variant, when present) and this tree's
 #   abfd     A/B of the rounds kernel without the window's FD rows in LDS (HGE_DIR_NOFD)
 #   core     parity, wide, golden and replay-path GPU tests
 #   online   per-call profile of the online path (16/100k, 256 prefix)
@@ -70,6 +72,16 @@ import json
 d=json.loads(open('gpurun_out/r04/abfd_$v.json').read().strip().splitlines()[-1])
 print('nofd=$v', round(d['value']/1e6,2), d['ms_per_step'], d['kernels_ms_per_replay']['k_rounds_direct'], d['parity'][:40])"
          done; unset HGE_DIR_NOFD ;;
+    ab) vs="head new head new"; [ -f build/ab/libhge_alt.so ] && vs="head alt new head alt new"
+         for v in $vs; do
+           case $v in head) export HGE_LIB=build/ab/libhge_head.so ;; alt) export HGE_LIB=build/ab/libhge_alt.so ;; *) unset HGE_LIB ;; esac
+           timeout -k 10 300 python -u bench.py --no-secondary --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/r04/ab_$v.json 2> gpurun_out/r04/ab_$v.err || { tail -5 gpurun_out/r04/ab_$v.err; exit 2; }
+           python -c "
+import json
+d=json.loads(open('gpurun_out/r04/ab_$v.json').read().strip().splitlines()[-1])
+k=d['kernels_ms_per_replay']
+print('$v', round(d['value']/1e6,2), d['ms_per_step'], {n: k[n] for n in k if 'median' in n or 'rows_runs' in n or 'transpose' in n}, d['parity'][:40])"
+         done; unset HGE_LIB ;;
     mcgpu) timeout -k 10 600 $PYT -m gpu tests/test_gpu_mc.py tests/test_gpu_batch.py > gpurun_out/r04/mcgpu.log 2>&1 || { tail -40 gpurun_out/r04/mcgpu.log; exit 1; }
          tail -3 gpurun_out/r04/mcgpu.log ;;
     bench) timeout -k 10 600 python -u bench.py > gpurun_out/r04/bench.json 2> gpurun_out/r04/bench.err || { tail -20 gpurun_out/r04/bench.err; exit 2; }
