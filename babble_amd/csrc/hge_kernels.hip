@@ -120,22 +120,37 @@ __global__ void k_min_round_range(const int32_t* round, int lo, int hi, int32_t*
 // (two barriers; a Hillis-Steele over 1024 partials took 20)
 // scat (non-null): also und[out[i]] = scat[i] for every i with in[i] != 0 (the
 // undetermined list's compaction, k_scatter_und's work)
+// n <= 16,384 (scan_large's case): the input is loaded coalesced into LDS (padded one
+// word per 16: the per-thread runs read it without bank conflicts), each thread scans
+// its contiguous run there, and the positions go back out coalesced.  (Runs loaded
+// straight from HBM put 64 cache lines behind every load instruction: ~10 us at
+// 10k entries.)  scat: flags in[] are 0 / 1 (the compaction's case).
+constexpr int SCAN_LDS = 16384;
 __device__ __forceinline__ void scan_small_body(const int32_t* in, int32_t* out, int n, int32_t* total,
                                                 const int32_t* scat, int32_t* und) {
   __shared__ int wsum[16];
+  __shared__ int sv[SCAN_LDS + SCAN_LDS / 16];
   const int T = blockDim.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int per = (n + T - 1) / T;
   const int lo = min(n, tid * per), hi = min(n, lo + per);
-  // runs up to 16 (n <= 16k, scan_large's case) are loaded at once and kept in
-  // registers (a loop of dependent-issue loads, read twice, was ~10 us at n = 10k)
-  constexpr int RK = 16;
-  int rv[RK];
+  const bool lds = n <= SCAN_LDS && T == 1024;  // block-uniform
+  auto P = [](int i) { return i + (i >> 4); };
   int s = 0;
-  if (per <= RK) {
+  if (lds) {
+    constexpr int K = SCAN_LDS / 1024;
+    int rv[K];
 #pragma unroll
-    for (int k = 0; k < RK; k++) rv[k] = lo + k < hi ? in[lo + k] : 0;
+    for (int k = 0; k < K; k++) {
+      const int i = tid + 1024 * k;
+      rv[k] = i < n ? in[i] : 0;
+    }
 #pragma unroll
-    for (int k = 0; k < RK; k++) s += rv[k];
+    for (int k = 0; k < K; k++) {
+      const int i = tid + 1024 * k;
+      if (i < n) sv[P(i)] = rv[k];
+    }
+    __syncthreads();
+    for (int i = lo; i < hi; i++) s += sv[P(i)];
   } else {
     for (int i = lo; i < hi; i++) s += in[i];
   }
@@ -158,14 +173,26 @@ __device__ __forceinline__ void scan_small_body(const int32_t* in, int32_t* out,
   }
   __syncthreads();
   int run = (wv > 0 ? wsum[wv - 1] : 0) + inc - s;
-  if (per <= RK) {
+  const int tot = wsum[T / 64 - 1];
+  if (lds) {
+    for (int i = lo; i < hi; i++) {  // the run's exclusive positions, in place
+      const int v = sv[P(i)];
+      sv[P(i)] = run;
+      run += v;
+    }
+    __syncthreads();
+    constexpr int K = SCAN_LDS / 1024;
 #pragma unroll
-    for (int k = 0; k < RK; k++) {
-      if (lo + k < hi) {
-        out[lo + k] = run;
-        if (scat && rv[k]) und[run] = scat[lo + k];
+    for (int k = 0; k < K; k++) {
+      const int i = tid + 1024 * k;
+      if (i < n) {
+        const int o = sv[P(i)];
+        out[i] = o;
+        if (scat) {
+          const int nx = i + 1 < n ? sv[P(i + 1)] : tot;
+          if (nx != o) und[o] = scat[i];
+        }
       }
-      run += rv[k];
     }
   } else {
     for (int i = lo; i < hi; i++) {
@@ -175,7 +202,7 @@ __device__ __forceinline__ void scan_small_body(const int32_t* in, int32_t* out,
       run += v;
     }
   }
-  if (tid == T - 1 && total) *total = wsum[T / 64 - 1];
+  if (tid == T - 1 && total) *total = tot;
 }
 __global__ void __launch_bounds__(1024) k_scan_small(const int32_t* in, int32_t* out, int n, int32_t* total) {
   scan_small_body(in, out, n, total, nullptr, nullptr);
@@ -1259,22 +1286,34 @@ __global__ void __launch_bounds__(1024) k_lcr_scan(const int32_t* Lc, int ncalls
                                                    int32_t* LCR, const int32_t* pr_round,
                                                    const int32_t* pr_cf, const int32_t* pr_len,
                                                    int nrounds, int32_t* clast, int32_t* flags) {
-  __shared__ int tmp[1025];
-  const int T = blockDim.x, tid = threadIdx.x;
+  __shared__ int wm[16];
+  const int T = blockDim.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int per = (ncalls + T - 1) / T;
   const int lo = min(ncalls, tid * per), hi = min(ncalls, lo + per);
   int m = -1;
   for (int i = lo; i < hi; i++) m = max(m, Lc[i]);
-  tmp[tid] = m;
-  __syncthreads();
-  // inclusive max-scan over the threads' partial maxima (Hillis-Steele)
-  for (int off = 1; off < T; off <<= 1) {
-    const int o = (tid >= off) ? tmp[tid - off] : -1;
-    __syncthreads();
-    tmp[tid] = max(tmp[tid], o);
-    __syncthreads();
+  // exclusive max-scan over the threads' partial maxima: wave shuffles, then one
+  // scan of the 16 wave maxima (two barriers; a Hillis-Steele over 1024 took twenty)
+  int inc = m;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc = max(inc, y);
   }
-  int run = max(lcr_start, tid > 0 ? tmp[tid - 1] : -1);
+  if (lane == 63) wm[wv] = inc;
+  __syncthreads();
+  if (wv == 0) {
+    int v = lane < T / 64 ? wm[lane] : -1;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const int y = __shfl_up(v, o, 64);
+      if (lane >= o) v = max(v, y);
+    }
+    if (lane < T / 64) wm[lane] = v;
+  }
+  __syncthreads();
+  const int ex = __shfl_up(inc, 1, 64);  // the wave's prefix before this thread
+  int run = max(lcr_start, max(wv > 0 ? wm[wv - 1] : -1, lane > 0 ? ex : -1));
   for (int i = lo; i < hi; i++) {
     run = max(run, Lc[i]);
     LCR[i] = run;
@@ -2395,26 +2434,49 @@ struct SortChunk {
 // received) and the list of non-empty buckets, by one block
 __device__ __forceinline__ void bucket_list_body(const int32_t* cnt, int n, int32_t* off, int32_t* total,
                                                  int32_t* list, int32_t* nlist) {
-  __shared__ int ts[1024], tn[1024];
-  const int T = blockDim.x, tid = threadIdx.x;
+  // per-thread contiguous runs, wave scans by shuffles, one scan of the 16 wave
+  // totals: two barriers (a Hillis-Steele over the 1024 partials took twenty)
+  __shared__ int ws[16], wn[16];
+  const int T = blockDim.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int per = (n + T - 1) / T;
   const int lo = min(n, tid * per), hi = min(n, lo + per);
   int s = 0, ne = 0;
   for (int i = lo; i < hi; i++) {
-    s += cnt[i];
-    ne += cnt[i] > 0 ? 1 : 0;
+    const int v = cnt[i];
+    s += v;
+    ne += v > 0 ? 1 : 0;
   }
-  ts[tid] = s;
-  tn[tid] = ne;
+  int is = s, in = ne;  // inclusive over the wave
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int a = __shfl_up(is, o, 64), b = __shfl_up(in, o, 64);
+    if (lane >= o) {
+      is += a;
+      in += b;
+    }
+  }
+  if (lane == 63) {
+    ws[wv] = is;
+    wn[wv] = in;
+  }
   __syncthreads();
-  for (int o = 1; o < T; o <<= 1) {
-    const int a = tid >= o ? ts[tid - o] : 0, b = tid >= o ? tn[tid - o] : 0;
-    __syncthreads();
-    ts[tid] += a;
-    tn[tid] += b;
-    __syncthreads();
+  if (wv == 0) {
+    int a = lane < T / 64 ? ws[lane] : 0, b = lane < T / 64 ? wn[lane] : 0;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const int x = __shfl_up(a, o, 64), y = __shfl_up(b, o, 64);
+      if (lane >= o) {
+        a += x;
+        b += y;
+      }
+    }
+    if (lane < T / 64) {
+      ws[lane] = a;
+      wn[lane] = b;
+    }
   }
-  int run = ts[tid] - s, pos = tn[tid] - ne;
+  __syncthreads();
+  int run = (wv > 0 ? ws[wv - 1] : 0) + is - s, pos = (wv > 0 ? wn[wv - 1] : 0) + in - ne;
   for (int i = lo; i < hi; i++) {
     const int v = cnt[i];
     off[i] = run;
@@ -2422,8 +2484,8 @@ __device__ __forceinline__ void bucket_list_body(const int32_t* cnt, int n, int3
     if (v > 0) list[pos++] = i;
   }
   if (tid == T - 1) {
-    *total = ts[T - 1];
-    *nlist = tn[T - 1];
+    *total = ws[T / 64 - 1];
+    *nlist = wn[T / 64 - 1];
   }
 }
 __global__ void __launch_bounds__(1024) k_bucket_list(const int32_t* cnt, int n, int32_t* off, int32_t* total,
