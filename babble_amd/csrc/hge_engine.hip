@@ -1952,14 +1952,20 @@ struct hge_engine {
         KLAUNCH(k_bucket_keys, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand, s_recv.p,
                 s_rr.p, s_cts.p, s_bpos.p, k1, d_rr.p, d_cts.p,
                 (unsigned long long*)(s_out.p + o_tx));
-        // buckets of 513 .. 2 * BIG_SORT keys in LDS (k_bucket_sort_big), the rest here
-        KLAUNCH(k_bucket_sort, dim3(std::min(ncalls, 2048)), dim3(256), 0, st,
-                (const int32_t*)s_bpos.p, (const int32_t*)o_cc, (const int32_t*)blist,
-                (const int32_t*)nblist, k1, k2, o_ids, 1);
-        if (ncand > 512)  // (no bucket past 512 keys otherwise: an online call's sort is one launch)
-          KLAUNCH(k_bucket_sort_big, dim3(std::min(ncalls, n_cu())), dim3(1024), 0, st,
+        if (ncalls <= 8) {
+          // a few buckets (an online call): one launch, each bucket to the path its size takes
+          KLAUNCH(k_bucket_sort_all, dim3(ncalls), dim3(1024), 0, st, (const int32_t*)s_bpos.p,
+                  (const int32_t*)o_cc, (const int32_t*)blist, (const int32_t*)nblist, k1, k2, o_ids);
+        } else {
+          // buckets of 513 .. 2 * BIG_SORT keys in LDS (k_bucket_sort_big), the rest here
+          KLAUNCH(k_bucket_sort, dim3(std::min(ncalls, 2048)), dim3(256), 0, st,
                   (const int32_t*)s_bpos.p, (const int32_t*)o_cc, (const int32_t*)blist,
-                  (const int32_t*)nblist, (const OKey*)k1, k2, o_ids);
+                  (const int32_t*)nblist, k1, k2, o_ids, 1);
+          if (ncand > 512)  // (no bucket past 512 keys otherwise)
+            KLAUNCH(k_bucket_sort_big, dim3(std::min(ncalls, n_cu())), dim3(1024), 0, st,
+                    (const int32_t*)s_bpos.p, (const int32_t*)o_cc, (const int32_t*)blist,
+                    (const int32_t*)nblist, (const OKey*)k1, k2, o_ids);
+        }
         // new undetermined list (in candidate order), scattered into the spare list
         // (same capacity) and swapped: no device copy
         if (!lu) {

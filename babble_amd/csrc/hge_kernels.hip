@@ -2506,10 +2506,10 @@ __global__ void __launch_bounds__(1024) k_list_und(const int32_t* cnt, int n, in
 // keys per bucket that k_bucket_sort_big sorts whole in LDS (k_bucket_sort leaves them to it)
 constexpr int BIG_SORT = 8192;
 
+constexpr int SORT_CH = 512;  // keys per LDS chunk (k_bucket_sort)
 __device__ void bucket_sort_one(int b, const int32_t* bend, const int32_t* bcnt, OKey* keys,
-                                OKey* tmp, int32_t* ids_out, bool skip_big) {
-  constexpr int CH = 512;  // keys per LDS chunk
-  __shared__ SortChunk<CH> sc;
+                                OKey* tmp, int32_t* ids_out, bool skip_big, SortChunk<SORT_CH>& sc) {
+  constexpr int CH = SORT_CH;
   const int n = bcnt[b];
   if (n == 0 || (skip_big && n > CH && n <= 2 * BIG_SORT)) return;
   const int start = bend[b] - n;
@@ -2565,8 +2565,9 @@ __device__ void bucket_sort_one(int b, const int32_t* bend, const int32_t* bcnt,
 __global__ void __launch_bounds__(256) k_bucket_sort(const int32_t* bend, const int32_t* bcnt,
                                                      const int32_t* list, const int32_t* nlist,
                                                      OKey* keys, OKey* tmp, int32_t* ids_out, int skip_big) {
+  __shared__ SortChunk<SORT_CH> sc;
   for (int li = blockIdx.x; li < *nlist; li += gridDim.x) {
-    bucket_sort_one(list[li], bend, bcnt, keys, tmp, ids_out, skip_big != 0);
+    bucket_sort_one(list[li], bend, bcnt, keys, tmp, ids_out, skip_big != 0, sc);
     __syncthreads();
   }
 }
@@ -2627,24 +2628,18 @@ __device__ void big_bitonic(const OKey* K, int n, uint64_t* sb, uint32_t* sr, ui
 // round's worth: 33 calls of 8-16k keys at 256/10M) are two halves sorted in LDS
 // the same way, then one merge-path pass over their index lists (scratch: the
 // bucket's slice of tmp), each thread placing nb / 1024 outputs from its co-rank.
-__global__ void __launch_bounds__(1024) k_bucket_sort_big(const int32_t* bend, const int32_t* bcnt,
-                                                          const int32_t* list, const int32_t* nlist,
-                                                          const OKey* keys, OKey* tmp, int32_t* ids_out) {
-  __shared__ uint64_t sb[BIG_SORT];
-  __shared__ uint32_t sr[BIG_SORT], ss[BIG_SORT];
-  __shared__ uint16_t ix[BIG_SORT];
+// one bucket of 513 .. 2 * BIG_SORT keys (block-uniform)
+__device__ void bucket_sort_big_one(int b, int nb, const int32_t* bend, const OKey* keys, OKey* tmp,
+                                    int32_t* ids_out, uint64_t* sb, uint32_t* sr, uint32_t* ss, uint16_t* ix) {
   const int tid = threadIdx.x, T = blockDim.x;
-  for (int li = blockIdx.x; li < *nlist; li += gridDim.x) {
-    const int b = list[li];
-    const int nb = bcnt[b];
-    if (nb <= 512 || nb > 2 * BIG_SORT) continue;  // block-uniform
+  {
     const OKey* K = keys + (bend[b] - nb);
     int32_t* out = ids_out + (bend[b] - nb);
     if (nb <= BIG_SORT) {
       big_bitonic(K, nb, sb, sr, ss, ix);
       for (int i = tid; i < nb; i += T) out[i] = (int32_t)K[ix[i]].id;
       __syncthreads();
-      continue;
+      return;
     }
     int32_t* S = (int32_t*)(tmp + (bend[b] - nb));  // 4 of the 48 scratch bytes per key
     const int na = (nb + 1) >> 1, nbb = nb - na;
@@ -2668,6 +2663,43 @@ __global__ void __launch_bounds__(1024) k_bucket_sort_big(const int32_t* bend, c
       const bool takeA = j >= nbb || (i < na && okless(K[A[i]], K[B[j]]));
       out[k] = (int32_t)K[takeA ? A[i++] : B[j++]].id;
     }
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(1024) k_bucket_sort_big(const int32_t* bend, const int32_t* bcnt,
+                                                          const int32_t* list, const int32_t* nlist,
+                                                          const OKey* keys, OKey* tmp, int32_t* ids_out) {
+  __shared__ uint64_t sb[BIG_SORT];
+  __shared__ uint32_t sr[BIG_SORT], ss[BIG_SORT];
+  __shared__ uint16_t ix[BIG_SORT];
+  for (int li = blockIdx.x; li < *nlist; li += gridDim.x) {
+    const int b = list[li];
+    const int nb = bcnt[b];
+    if (nb <= 512 || nb > 2 * BIG_SORT) continue;  // block-uniform
+    bucket_sort_big_one(b, nb, bend, keys, tmp, ids_out, sb, sr, ss, ix);
+  }
+}
+
+// A few buckets (an online call's one): both sorts in one launch of 1024-thread
+// blocks, each bucket to the path its size takes, the two paths' LDS as one pool
+// (one launch in place of k_bucket_sort + k_bucket_sort_big)
+__global__ void __launch_bounds__(1024) k_bucket_sort_all(const int32_t* bend, const int32_t* bcnt,
+                                                          const int32_t* list, const int32_t* nlist,
+                                                          OKey* keys, OKey* tmp, int32_t* ids_out) {
+  constexpr size_t BIG_LDS = (size_t)BIG_SORT * (8 + 4 + 4 + 2);
+  constexpr size_t POOL = BIG_LDS > sizeof(SortChunk<SORT_CH>) ? BIG_LDS : sizeof(SortChunk<SORT_CH>);
+  __shared__ __attribute__((aligned(16))) unsigned char pool[POOL];
+  uint64_t* sb = (uint64_t*)pool;
+  uint32_t* sr = (uint32_t*)(pool + (size_t)BIG_SORT * 8);
+  uint32_t* ss = (uint32_t*)(pool + (size_t)BIG_SORT * 12);
+  uint16_t* ix = (uint16_t*)(pool + (size_t)BIG_SORT * 16);
+  SortChunk<SORT_CH>& sc = *(SortChunk<SORT_CH>*)pool;
+  for (int li = blockIdx.x; li < *nlist; li += gridDim.x) {
+    const int b = list[li];
+    const int nb = bcnt[b];
+    if (nb > 512 && nb <= 2 * BIG_SORT) bucket_sort_big_one(b, nb, bend, keys, tmp, ids_out, sb, sr, ss, ix);
+    else bucket_sort_one(b, bend, bcnt, keys, tmp, ids_out, false, sc);
     __syncthreads();
   }
 }
