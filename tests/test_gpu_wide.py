@@ -170,10 +170,11 @@ def test_median_select_extremes(n, events, kind):
 @pytest.mark.parametrize("n,events", [(128, 16000), (256, 12000), (64, 20000), (4, 20000)])
 def test_oversized_call_buckets(n, events):
     """One RunConsensus over the whole stream: a single FindOrder call bucket of more
-    than 8,192 keys.  128/16k and 256/12k (8,193 .. 16,384 keys): two halves sorted
-    in LDS and merged by k_bucket_sort_big; 64/20k and 4/20k (more than 16,384 keys):
-    the chunk sort + merges of k_bucket_sort.  Order and consensus state vs the
-    oracle (FindOrder, hashgraph.go:744-745)."""
+    than 8,192 keys, sorted by k_bucket_sort_all (one call: both sort paths in one
+    launch).  128/16k and 256/12k (8,193 .. 16,384 keys): two halves sorted in LDS
+    and merged; 64/20k and 4/20k (more than 16,384 keys): the chunk sort + merges,
+    here by a 1024-thread block.  Order and consensus state vs the oracle
+    (FindOrder, hashgraph.go:744-745)."""
     from babble_amd.engine import Engine
     eng = Engine(n, 1 << 15)
     try:
