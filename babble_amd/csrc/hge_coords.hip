@@ -559,8 +559,11 @@ __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const FT* FDT
         const size_t o = rowoff(t, a, q) + jj;
         const int32_t dv = toff[tx][r];
         esc = dv == INT32_MIN;  // a real offset lies in [-INT32_MAX, INT32_MAX]
-        t.FD[o] = tile[tx][r];
-        if (tsrow) t.FDTD[o] = dv;
+        // streaming stores: 20 GB per 256/10M replay, read back only by later kernels
+        // (7.24-7.28 vs 7.40-7.41 ms in a same-box A/B; the runs kernel's scattered short
+        // runs need the L2 to merge their lines: 18.9 vs 6.55 ms with streaming stores)
+        __builtin_nontemporal_store(tile[tx][r], t.FD + o);
+        if (tsrow) __builtin_nontemporal_store(dv, t.FDTD + o);
       }
       const bool any = __ballot(esc) != 0;
       if (tx == 0 && q < pend && tsrow) t.FDTW[((size_t)a * ccap + q) * NT + by] = any ? 1 : 0;
