@@ -68,19 +68,19 @@ def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
                     once per fixed-point sweep (the sweeps' re-reads are waste);
       k_la_clear     4N/event (the new rows' -1 fill);
       k_la_sweep16 / k_la_clear16  6N / 2N per event (N > 32: the same on packed u16);
-      k_transpose   16N/event at N <= 16 (LA -> LAT and FDT -> FD: each reads and
-                    writes 4N), 8N at 16 < N <= 32 (LA -> LAT only);
+      k_transpose    8N/event at N <= 16 (FDT -> FD: reads and writes 4N);
       k_fd_transpose_ts 12N/event (N > 16: FDT read, FD and the 4-byte FD
                     timestamp offsets written);
       k_witness_la   8N^2 per round (frontier rows read, transposed rows written);
-      k_la16_rows_runs 6N/event (N > 32: LA16 read, the FDT runs written);
+      k_la16_rows_runs 6N/event (N > 32: LA16 read, the FDT runs written); 8N/event
+                    over int32 LA tiles (<int32_t, true>: N <= 32 and wide hashgraphs);
       k_la_win      (2N + 20)/event (32 < N <= 256, windowed exact propagation: the
                     head rows live in LDS, so per event only the packed row is
                     written, the 16-byte plan entry read and the 4-byte row sum
                     written -- once per replay, however many passes);
       k_lw_plan     40/event (creator, index, other-parent and two chain gathers
                     read, the plan entry written);
-      k_fdt_clear    4N/event; k_fdt_runs 8N/event (LAT read, FDT written);
+      k_fdt_clear    4N/event;
       k_fss          8N/event (FD row read, fss row written, N <= 32);
       rounds        4N/event (the strongly-see round test reads each row once);
       k_round_received / k_median_wave (4N + 48) per ordered event (FD row for
@@ -91,9 +91,11 @@ def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
     name = kernel.strip("()").split("<")[0]
     if name == "k_witness_la":
         return 8 * n * n * rounds
-    per_event = {"k_la_sweep": 12 * n, "k_la_clear": 4 * n, "k_transpose": 16 * n if n <= 16 else 8 * n,
+    if name == "k_la16_rows_runs" and "true" in kernel:
+        return 8 * n * events
+    per_event = {"k_la_sweep": 12 * n, "k_la_clear": 4 * n, "k_transpose": 8 * n,
                  "k_fd_transpose_ts": 12 * n,
-                 "k_fdt_clear": 4 * n, "k_fdt_runs": 8 * n, "k_fss": 8 * n,
+                 "k_fdt_clear": 4 * n, "k_fss": 8 * n,
                  "k_rounds_walk": 4 * n, "k_rounds_coop": 4 * n, "k_rounds_coop_spec": 4 * n,
                  "k_walk_spec": 4 * n, "k_rounds_fss": 4 * n, "k_rounds_direct": 4 * n,
                  "k_la_clear16": 2 * n, "k_la_sweep16": 6 * n, "k_la16_rows_runs": 6 * n,
@@ -560,7 +562,7 @@ def main():
     hbm_kernels = {}
     for name in kstats:
         base = name.strip("()").split("<")[0]
-        if base in ("k_la_sweep", "k_la_clear", "k_transpose", "k_fss", "k_fdt_runs",
+        if base in ("k_la_sweep", "k_la_clear", "k_transpose", "k_fss",
                     "k_fdt_clear", "k_rounds_coop", "k_rounds_coop_spec", "k_median_wave",
                     "k_la_clear16", "k_la_sweep16", "k_la16_rows_runs", "k_rounds_direct",
                     "k_fd_transpose_ts", "k_witness_la", "k_la_win", "k_lw_plan"):
