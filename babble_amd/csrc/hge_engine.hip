@@ -1926,8 +1926,11 @@ struct hge_engine {
       s_upos.need(ncand);
       s_rr.need(ncand);
       s_cts.need(ncand);
-      KLAUNCH(k_recv_flags, dim3(div_up(ncand, 256)), dim3(256), 0, st, s_recv.p, ncand,
-              (int32_t*)nullptr, s_fund.p, commit ? 1 : 0, commit ? o_cc : (int32_t*)nullptr);
+      // an online call's flags, buckets and undetermined list: one launch (k_recv_list_und below)
+      const bool rlu = commit && ncand <= 16384 && ncalls <= 8;
+      if (!rlu)
+        KLAUNCH(k_recv_flags, dim3(div_up(ncand, 256)), dim3(256), 0, st, s_recv.p, ncand,
+                (int32_t*)nullptr, s_fund.p, commit ? 1 : 0, commit ? o_cc : (int32_t*)nullptr);
       if (!commit)
         KLAUNCH(k_set_rr, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand, s_recv.p,
                 s_rr.p, s_cts.p, d_rr.p, d_cts.p, o_ntx, 0);
@@ -1939,7 +1942,10 @@ struct hge_engine {
         // call buckets (k_list_und; the list swap below is the same)
         const bool lu = ncand <= 16384;
         s_und2.need(d_und.n);
-        if (lu)
+        if (rlu)
+          KLAUNCH(k_recv_list_und, dim3(2), dim3(1024), 0, st, (const int32_t*)s_recv.p, (int)ncand, o_cc, ncalls,
+                  s_bpos.p, o_cnt, blist, nblist, s_fund.p, s_upos.p, o_cnt + 1, cand, s_und2.p);
+        else if (lu)
           KLAUNCH(k_list_und, dim3(2), dim3(1024), 0, st, (const int32_t*)o_cc, ncalls, s_bpos.p, o_cnt, blist,
                   nblist, (const int32_t*)s_fund.p, s_upos.p, (int)ncand, o_cnt + 1, cand, s_und2.p);
         else

@@ -2492,6 +2492,35 @@ __global__ void __launch_bounds__(1024) k_bucket_list(const int32_t* cnt, int n,
                                                       int32_t* list, int32_t* nlist) {
   bucket_list_body(cnt, n, off, total, list, nlist);
 }
+// An online call (a few calls, <= 16k candidates): k_recv_flags' work folded in as
+// well.  Block 0 counts the received events per call in LDS, stores the counts and
+// builds the call buckets from them; block 1 writes the undetermined flags
+// (recv_call == -1), then scans and compacts them.  Each block reads back only
+// global data it wrote itself, after a barrier.
+__global__ void __launch_bounds__(1024) k_recv_list_und(const int32_t* recv_call, int ncand, int32_t* cnt,
+                                                        int ncalls, int32_t* off, int32_t* total, int32_t* list,
+                                                        int32_t* nlist, int32_t* f_und, int32_t* upos,
+                                                        int32_t* nund, const int32_t* cand, int32_t* und) {
+  constexpr int MAXC = 8;
+  if (blockIdx.x == 0) {
+    __shared__ int s_cnt[MAXC];
+    if (threadIdx.x < MAXC) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    for (int q = threadIdx.x; q < ncand; q += blockDim.x) {
+      const int rc = recv_call[q];
+      if (rc >= 0) atomicAdd(&s_cnt[rc], 1);
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < ncalls) cnt[threadIdx.x] = s_cnt[threadIdx.x];
+    __syncthreads();
+    bucket_list_body(cnt, ncalls, off, total, list, nlist);
+  } else {
+    for (int q = threadIdx.x; q < ncand; q += blockDim.x) f_und[q] = recv_call[q] == -1 ? 1 : 0;
+    __syncthreads();
+    scan_small_body(f_und, upos, ncand, nund, cand, und);
+  }
+}
+
 // an online call's two single-block steps after k_recv_flags in one launch: block 0
 // the call buckets (k_bucket_list), block 1 the new undetermined list's scan and
 // compaction (k_scan_small + k_scatter_und; fl.size <= 16k)
