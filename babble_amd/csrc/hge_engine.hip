@@ -1987,21 +1987,27 @@ struct hge_engine {
     // ---- persist fame / LCR ----
     bool lcr_up = false;
     if (do_fame && nrounds > 0) {
-      fame_dispatch(1, t, nrounds, npairs, ncalls);
       if (lcr_dev) {
-        // RoundEvents(LCR - 1) as below, the new LCR and its call read on the device
+        // the persisted fame and RoundEvents(LCR - 1) as below (the new LCR and its
+        // call read on the device) in one launch
         const int64_t nfrom = std::min<int64_t>(calls[0], n_coords);
-        KLAUNCH(k_lcre_dev, dim3(std::max(1, div_up(n_coords - nfrom, 256))), dim3(256), 0, st, t,
-                (const int64_t*)c_nc, (const int32_t*)c_flags, lcr, (int)nfrom, (int)n_coords, o_cnt + 2);
-      } else if (lcr_new > lcr) {
-        // RoundEvents(lcr_new - 1) at call c_set: events of that round minus the
-        // ones inserted after that call
-        lcr_up = true;
-        const int r = lcr_new - 1;
-        if (r >= 0) {
-          const int64_t nfrom = std::min<int64_t>(calls[c_set], n_coords);
-          KLAUNCH(k_lcre, dim3(std::max(1, div_up(n_coords - nfrom, 256))), dim3(256), 0, st, t,
-                  (int)nfrom, (int)n_coords, r, o_cnt + 2);
+        const int nb_fp = (int)div_up((int64_t)nrounds * N, 256);
+        KLAUNCH(k_fame_persist_lcre, dim3(nb_fp + std::max(1, div_up(n_coords - nfrom, 256))), dim3(256), 0, st, t,
+                (const int32_t*)c_pr, (const int32_t*)(c_pr + nrounds), (const int32_t*)(c_pr + 2 * nrounds),
+                (const int32_t*)(c_pr + 3 * nrounds), nrounds, (const int32_t*)s_clast.p, (const uint8_t*)s_dec.p,
+                nb_fp, (const int64_t*)c_nc, (const int32_t*)c_flags, lcr, (int)nfrom, (int)n_coords, o_cnt + 2);
+      } else {
+        fame_dispatch(1, t, nrounds, npairs, ncalls);
+        if (lcr_new > lcr) {
+          // RoundEvents(lcr_new - 1) at call c_set: events of that round minus the
+          // ones inserted after that call
+          lcr_up = true;
+          const int r = lcr_new - 1;
+          if (r >= 0) {
+            const int64_t nfrom = std::min<int64_t>(calls[c_set], n_coords);
+            KLAUNCH(k_lcre, dim3(std::max(1, div_up(n_coords - nfrom, 256))), dim3(256), 0, st, t,
+                    (int)nfrom, (int)n_coords, r, o_cnt + 2);
+          }
         }
       }
     }

@@ -1352,11 +1352,11 @@ __global__ void __launch_bounds__(1024) k_lcr_scan(const int32_t* Lc, int ncalls
 
 // persisted fame after the batch: decisions up to c_last(i); one lane per
 // (processed round, witness slot), coalesced over the slots
-__global__ void k_fame_persist(Tables t, const int32_t* pr_round, const int32_t* pr_off,
-                               const int32_t* pr_cf, const int32_t* pr_len, int nrounds,
-                               const int32_t* clast, const uint8_t* dec) {
+__device__ __forceinline__ void fame_persist_body(const Tables& t, const int32_t* pr_round, const int32_t* pr_off,
+                                                  const int32_t* pr_cf, const int32_t* pr_len, int nrounds,
+                                                  const int32_t* clast, const uint8_t* dec, int bid) {
   const int N = t.N;
-  const int64_t item = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t item = (int64_t)bid * blockDim.x + threadIdx.x;
   const int ri = (int)(item / N), d = (int)(item - (item / N) * N);
   if (ri >= nrounds) return;
   const int i = pr_round[ri];
@@ -1367,6 +1367,10 @@ __global__ void k_fame_persist(Tables t, const int32_t* pr_round, const int32_t*
     if (o) f = o;
   }
   t.fame[(size_t)i * N + d] = f;
+}
+__global__ void k_fame_persist(Tables t, const int32_t* pr_round, const int32_t* pr_off, const int32_t* pr_cf,
+                               const int32_t* pr_len, int nrounds, const int32_t* clast, const uint8_t* dec) {
+  fame_persist_body(t, pr_round, pr_off, pr_cf, pr_len, nrounds, clast, dec, blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -2863,15 +2867,24 @@ __global__ void k_lcre(Tables t, int n_from, int n1, int r, int32_t* out) {
 // k_lcre with the new LastConsensusRound L = flags[1] and its call flags[2] read
 // on the device: nothing unless L > lcr_old; the blocks before the call's event
 // count n_c stand down
-__global__ void k_lcre_dev(Tables t, const int64_t* nc, const int32_t* flags, int lcr_old, int n_lo, int n1,
-                           int32_t* out) {
+__device__ __forceinline__ void lcre_dev_body(const Tables& t, const int64_t* nc, const int32_t* flags, int lcr_old,
+                                              int n_lo, int n1, int32_t* out, int bid) {
   const int L = flags[1];
   if (L <= lcr_old || L < 1) return;
   const int r = L - 1;
   const int n_from = (int)min<int64_t>(nc[flags[2]], (int64_t)n1);
-  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(out, t.rcnt[r]);
-  const int x = n_lo + blockIdx.x * blockDim.x + threadIdx.x;
+  if (bid == 0 && threadIdx.x == 0) atomicAdd(out, t.rcnt[r]);
+  const int x = n_lo + bid * blockDim.x + threadIdx.x;
   if (x >= n_from && x < n1 && t.round[x] == r) atomicSub(out, 1);
+}
+// k_fame_persist (blocks [0, nb_fp)) and the LCR round count (lcre_dev_body, the rest) in one launch: the
+// persisted fame and the LCR round's event count read and write disjoint tables
+__global__ void k_fame_persist_lcre(Tables t, const int32_t* pr_round, const int32_t* pr_off, const int32_t* pr_cf,
+                                    const int32_t* pr_len, int nrounds, const int32_t* clast, const uint8_t* dec,
+                                    int nb_fp, const int64_t* nc, const int32_t* flags, int lcr_old, int n_lo,
+                                    int n1, int32_t* out) {
+  if ((int)blockIdx.x < nb_fp) fame_persist_body(t, pr_round, pr_off, pr_cf, pr_len, nrounds, clast, dec, blockIdx.x);
+  else lcre_dev_body(t, nc, flags, lcr_old, n_lo, n1, out, blockIdx.x - nb_fp);
 }
 
 // fresh consensus state: C = INF, W = -1, bitsets / fame / counts = 0, rr = -1
