@@ -1401,8 +1401,9 @@ struct hge_engine {
     dbg_dump();
   }
 
-  // N > 32: lastAncestors live only in the packed 16-bit table (chains are capped at
-  // 65,534 events there); the int32 LA rows exist for N <= 32
+  // N > 32: lastAncestors live in the packed 16-bit table while every chain holds at
+  // most 65,534 events; a longer chain switches the engine to int32 LA rows for good
+  // (to_wide32 below), which the N <= 32 path uses from the start
   bool sweep16() const { return N > 32 && !wide32; }
 
   // the switch to int32 positions (hge_wide32.hip): the int32 LA rows of every event

@@ -39,7 +39,7 @@
 //        round's fame changes; the median is taken over the same set;
 //      - optional release of the coordinates of events ordered long ago (any
 //        later read of them aborts the process, so a completed run used none).
-//    tests/test_oracle_fast.py checks both modes field by field, and every
+//    tests/test_oracle_scale.py checks both modes field by field, and every
 //    golden regenerated in scale mode is byte-identical to the faithful one.
 //
 // Coordinates (event.go:68-71, EventCoordinates{hash, index}) are stored as
