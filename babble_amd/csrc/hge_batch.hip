@@ -139,49 +139,50 @@ __device__ __forceinline__ void wsync() { __builtin_amdgcn_wave_barrier(); }
 // LA[x] = max(LA[sp], LA[op]) with LA[x][creator] = index.  The self-parent is the
 // creator's head (admission: "Self-parent not last known", hashgraph.go:390-393),
 // so its row is in LDS; so is the other-parent's when it is its chain's head.
+// Lane k keeps column k of every chain's head row in registers (hr[c], indexed by
+// the wave-uniform creator: v_movrels / v_movreld), and lane c the id of chain
+// c's head, so an event costs a handful of VALU instructions and one row store.
 template <int NM>
 __global__ __launch_bounds__(64) void kb_coords(BT t) {
   const GDesc d = t.gd[blockIdx.x];
   const int N = t.N, k = threadIdx.x;
-  __shared__ int32_t head[NM][NM];
-  __shared__ int32_t headid[NM];
-  if (k < N) {
-    for (int c = 0; c < N; c++) head[c][k] = -1;
-    headid[k] = -1;
-  }
-  __syncthreads();
+  int hr[NM];
+#pragma unroll
+  for (int c = 0; c < NM; c++) hr[c] = -1;
+  int hid = -1;
   int32_t* LA = t.LA + d.eo * N;
-  auto meta = [&](int i, int& cr, int& ix, int& sp, int& op, int& oc) {
-    cr = 0, ix = 0, sp = -1, op = -1, oc = 0;
+  // per event: creator | other-parent creator << 8 | has-self-parent << 16, index, other-parent
+  auto meta = [&](int i, int& pk, int& ix, int& op) {
+    pk = 0, ix = 0, op = -1;
     if (i < d.E) {
-      cr = t.cr[d.eo + i];
+      pk = t.cr[d.eo + i] | t.oc[d.eo + i] << 8 | (t.sp[d.eo + i] >= 0 ? 1 << 16 : 0);
       ix = t.ix[d.eo + i];
-      sp = t.sp[d.eo + i];
       op = t.op[d.eo + i];
-      oc = t.oc[d.eo + i];
     }
   };
-  int mcr, mix, msp, mop, moc;
-  meta(k, mcr, mix, msp, mop, moc);
+  // No load is left in flight across the event loop: a register-indexed read (hr[cr])
+  // makes the compiler wait for every outstanding load (vmcnt(0), which on CDNA also
+  // drains the row stores) before it, i.e. once per event.
   for (int base = 0; base < d.E; base += 64) {
-    int ncr, nix, nsp, nop, noc;
-    meta(base + 64 + k, ncr, nix, nsp, nop, noc);  // the next chunk, in flight meanwhile
+    int mpk, mix, mop;
+    meta(base + k, mpk, mix, mop);
+    asm volatile("" : "+v"(mpk), "+v"(mix), "+v"(mop));  // landed here, not waited for per event
     const int cnt = min(64, d.E - base);
     for (int u = 0; u < cnt; u++) {
-      const int cr = rl(mcr, u), ix = rl(mix, u), sp = rl(msp, u), op = rl(mop, u), oc = rl(moc, u);
-      const bool oph = op >= 0 && headid[oc] == op;
-      if (k < N) {
-        int v = sp >= 0 ? head[cr][k] : -1;
-        if (op >= 0) v = max(v, oph ? head[oc][k] : ld(&LA[(int64_t)op * N + k]));
-        if (k == cr) v = ix;
-        head[cr][k] = v;
-        LA[(int64_t)(base + u) * N + k] = v;
+      const int pk = rl(mpk, u), ix = rl(mix, u), op = rl(mop, u);
+      const int cr = pk & 0xFF, oc = (pk >> 8) & 0xFF;
+      int v = (pk >> 16) ? hr[cr] : -1;
+      if (op >= 0) {
+        if (rl(hid, oc) == op) v = max(v, hr[oc]);
+        else v = max(v, k < N ? ld(&LA[(int64_t)op * N + k]) : -1);  // not its chain's head
       }
-      wsync();
-      if (k == 0) headid[cr] = base + u;
-      wsync();
+      if (k == cr) {
+        v = ix;
+        hid = base + u;
+      }
+      hr[cr] = v;
+      if (k < N) LA[(int64_t)(base + u) * N + k] = v;
     }
-    mcr = ncr, mix = nix, msp = nsp, mop = nop, moc = noc;
   }
 }
 
@@ -195,12 +196,12 @@ __global__ __launch_bounds__(64) void kb_coords(BT t) {
 // loads are in flight meanwhile.
 template <int NM>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void kb_fd(BT t) {
-  const int g = blockIdx.x;
+  const int g = blockIdx.x / t.N, j = blockIdx.x - (blockIdx.x / t.N) * t.N;  // one wave per (graph, chain j)
   const GDesc d = t.gd[g];
   const int N = t.N, cc = t.ccap, lane = threadIdx.x;
   const int32_t* LA = t.LA + d.eo * N;
   const int lenc = lane < N ? t.clen[g * N + lane] : 0;  // lane c's chain length (the INF tails)
-  for (int j = 0; j < N; j++) {
+  {
     const int lenj = t.clen[g * N + j];
     const int32_t* ch = t.chain + ((int64_t)g * N + j) * cc;
     int32_t* outj = t.FDT + ((int64_t)g * N + j) * N * cc;  // + c * cc + p
@@ -314,7 +315,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
       const uint64_t pres = wpres[s];
       int wv[NM];
 #pragma unroll
-      for (int dd = 0; dd < NM; dd++) wv[dd] = wfd[s][dd][k];
+      for (int dd = 0; dd < NM; dd++) wv[dd] = k < NM ? wfd[s][dd][k] : INF;  // lanes past NM: no column
 #pragma unroll
       for (int dd = 0; dd < NM; dd++)
         if (__popcll(ballot(la >= wv[dd])) >= SM) m |= 1ull << dd;
@@ -440,6 +441,166 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 }
 
 // ---------------------------------------------------------------------------
+// Round / Witness by the round frontier, one 1024-thread workgroup per graph.
+// Round(x) is a function of x's ancestry alone: the witnesses x strongly sees are
+// its ancestors, so "the witnesses of the parent round inserted so far"
+// (hashgraph.go:263-285) are all it can count.  With C_r[c] the first position of
+// chain c whose round is >= r (rounds never decrease along a chain):
+//   round(x) >= r + 1  <=>  x strongly sees >= SM of the members (d, C_r[d]),
+//   fss_c(w) = the first position of chain c that strongly sees w
+//            = SM-th smallest over i of FD[(i, FD[w][i])][c]
+//     (x on chain c sees w's first descendant on chain i iff pos(x) >= that entry;
+//     StronglySee counts those i, hashgraph.go:189-208),
+//   C_{r+1}[c] = SM-th smallest over d of fss_c(C_r[d])  (the own-chain term at
+//     least C_r[c] + 1: an event never strongly sees itself; matters at N = 1).
+// The single-graph engine walks the same recurrence (k_fss / k_rounds_fss,
+// hge_kernels.hip).  Per round: thread (member d, chain c) gathers the N rows
+// FD[(i, FD[w_d][i])] at column c (one 128-byte row per half wave) and selects;
+// then chain c's thread selects over the members.  Chain c's round-r events are
+// the positions [C_r[c], C_{r+1}[c]), the first of them the witness; a witness's
+// strongly-see bits over round r-1's witnesses are fss_c(w) <= its position, its
+// see bits LA[x][d] >= index(w) (the vote adjacency of DecideFame).
+// k-th smallest (1-based) of M register values: bitonic network, then a select
+template <int M>
+__device__ __forceinline__ int kth_smallest(int (&v)[M], int k) {
+#pragma unroll
+  for (int size = 2; size <= M; size <<= 1)
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1)
+#pragma unroll
+      for (int i = 0; i < M; i++) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool up = (i & size) == 0;
+          const int a = v[i], b = v[j];
+          v[i] = up ? min(a, b) : max(a, b);
+          v[j] = up ? max(a, b) : min(a, b);
+        }
+      }
+  // v is ascending: v[k-1] is the maximum of v[0..k-1] (a select chain on i == k-1
+  // is turned into a dynamically indexed scratch array)
+  int r = INT32_MIN;
+#pragma unroll
+  for (int i = 0; i < M; i++) r = max(r, i < k ? v[i] : INT32_MIN);
+  return r;
+}
+
+template <int NM>
+__global__ __launch_bounds__(1024) void kb_front(BT t) {
+  constexpr int NT = 1024, NW = NT / 64;
+  const int g = blockIdx.x;
+  const GDesc d = t.gd[g];
+  const int N = t.N, SM = t.SM, cc = t.ccap, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  __shared__ int32_t zrow[NM][NM];     // [member d][i]: the FD row of (d, C_r[d])
+  __shared__ int32_t fssL[2][NM][NM];  // [r & 1][member d][chain c]: fss_c((d, C_r[d])), INF: no member
+  __shared__ int32_t Cl[3][NM];        // C_{r-1}, C_r, C_{r+1} by r mod 3 (INF: none)
+  __shared__ int32_t lenL[NM];
+  __shared__ int s_more;
+  const int32_t* FDg = t.FD + (int64_t)g * N * cc * N;  // [c][p][N]
+  const int32_t* chg = t.chain + (int64_t)g * N * cc;   // [c][p] -> id
+  const int32_t* LA = t.LA + d.eo * N;
+  if (tid < N) {
+    const int ln = t.clen[g * N + tid];
+    lenL[tid] = ln;
+    Cl[0][tid] = ln > 0 ? 0 : INF;  // the first event of a chain has no parents: round 0
+    Cl[2][tid] = INF;
+  }
+  __syncthreads();
+  // round r's outputs once C_{r+1} is known: the frontier ranges' rounds and witness
+  // flags, the witness rows, and (r >= 1) each witness's bits over round r-1's
+  auto outputs = [&](int r) {
+    const int* Cp = Cl[(r + 2) % 3];
+    const int* Cc = Cl[r % 3];
+    const int* Cn = Cl[(r + 1) % 3];
+    const int64_t row = (int64_t)(d.ro + r) * N;
+    const int per = NT / N;  // threads per chain
+    if (tid < per * N) {
+      const int c = tid % N, k = tid / N;
+      const int lo = Cc[c], hi = min(Cn[c], lenL[c]);
+      if (lo != INF)
+        for (int p = lo + k; p < hi; p += per) {
+          const int x = chg[(int64_t)c * cc + p];
+          t.round[d.eo + x] = r;
+          t.wit[d.eo + x] = p == lo;
+          if (p == lo) {
+            t.W[row + c] = x;
+            t.WIX[row + c] = lo;
+            t.WCOIN[row + c] = t.coin[d.eo + x];
+          }
+        }
+    }
+    if (r >= 1)
+      for (int c = wv; c < N; c += NW) {  // one wave per witness of round r, lane = d
+        const int lo = Cc[c], hi = min(Cn[c], lenL[c]);
+        if (lo == INF || lo >= hi) continue;
+        bool ss = false, see = false;
+        if (lane < N) {
+          const int pw = Cp[lane];
+          if (pw != INF && pw < min(Cc[lane], lenL[lane])) {  // (lane, pw) is a witness of round r-1
+            ss = fssL[(r - 1) & 1][lane][c] <= lo;
+            const int x = chg[(int64_t)c * cc + lo];
+            see = LA[(int64_t)x * N + lane] >= pw;
+          }
+        }
+        const uint64_t bss = ballot(ss), bsee = ballot(see);
+        if (lane == 0) {
+          t.ssb[row + c] = bss;
+          t.seeb[row + c] = bsee;
+        }
+      }
+  };
+  for (int r = 0;; r++) {
+    if (r >= d.Rcap) {  // never for a consistent graph (R <= E / SM + 1)
+      if (tid == 0) t.scal[(int64_t)g * 8 + 6] = 1;
+      return;
+    }
+    const int* Cc = Cl[r % 3];
+    int* Cn = Cl[(r + 1) % 3];
+    // the members' FD rows
+    for (int e = tid; e < N * N; e += NT) {
+      const int dd = e / N, i = e - (e / N) * N;
+      const int P = Cc[dd];
+      zrow[dd][i] = P != INF ? FDg[((int64_t)dd * cc + P) * N + i] : INF;
+    }
+    __syncthreads();
+    // fss_c of every member (c fastest: a half wave reads one 128-byte row)
+    for (int e = tid; e < N * N; e += NT) {
+      const int dd = e / N, c = e - (e / N) * N;
+      int f = INF;
+      if (Cc[dd] != INF) {
+        int v[NM];
+#pragma unroll
+        for (int i = 0; i < NM; i++) {
+          const int z = i < N ? zrow[dd][i] : INF;
+          v[i] = z != INF ? FDg[((int64_t)i * cc + z) * N + c] : INF;
+        }
+        f = kth_smallest<NM>(v, SM);
+        if (dd == c && f != INF) f = max(f, Cc[c] + 1);
+      }
+      fssL[r & 1][dd][c] = f;
+    }
+    __syncthreads();
+    // the next frontier
+    if (wv == 0) {
+      int nxt = INF;
+      if (lane < N && Cc[lane] != INF) {
+        int v[NM];
+#pragma unroll
+        for (int dd = 0; dd < NM; dd++) v[dd] = dd < N ? fssL[r & 1][dd][lane] : INF;
+        const int sel = kth_smallest<NM>(v, SM);
+        nxt = sel < lenL[lane] ? sel : INF;
+      }
+      if (lane < N) Cn[lane] = nxt;
+      const uint64_t any = ballot(lane < N && nxt != INF);
+      if (lane == 0) s_more = any != 0;
+    }
+    __syncthreads();
+    outputs(r);
+    if (!s_more) break;  // uniform: written before the barrier above
+  }
+}
+
+// ---------------------------------------------------------------------------
 // consensus sorter keys (consensus_sorter.go:36-59 with PRN = 0): roundReceived,
 // consensus timestamp, S (4 limbs), then the id (S never ties for real signatures)
 __device__ __forceinline__ bool key_less(const BT& t, int64_t eo, int ra, int64_t ca, uint64_t sa, int ia,
@@ -454,66 +615,63 @@ __device__ __forceinline__ bool key_less(const BT& t, int64_t eo, int ra, int64_
   return ia < ib;
 }
 
-// a key slot of the call's batch: LDS (plain accesses) or global scratch
-// (device-coherent accesses: lanes exchange keys between stages)
-template <bool G, typename T>
-__device__ __forceinline__ T kget(const T* p) {
-  if constexpr (G) return ld(p);
-  else return *p;
-}
-template <bool G, typename T>
-__device__ __forceinline__ void kput(T* p, T v) {
-  if constexpr (G) st(p, v);
-  else *p = v;
+// Bitonic networks over the whole workgroup.  Stage (size, stride): thread q of the
+// pair loop compares a = 2q - (q & (stride - 1)) and a + stride; for stride <= 64 a
+// wave's 64 pairs stay inside its own 128 slots (also on the next pass of the q
+// loop, 2 blockDim slots further), so two consecutive such stages need only the
+// wave's own sync; a block barrier brackets every wider stage.
+__device__ __forceinline__ void stage_sync(int size, int stride) {
+  const int next = stride > 1 ? stride >> 1 : size;  // the next stage's stride
+  if (stride > 64 || next > 64) __syncthreads();
+  else wsync();
 }
 
-// bitonic sort of n keys (padded to a power of two with sentinels, id INF, that
-// order after every key) by one wavefront
-template <bool G>
-__device__ void sort_keys(const BT& t, int64_t eo, int n, int32_t* kr, int64_t* kc, uint64_t* ks, int32_t* ki) {
-  const int lane = threadIdx.x;
+// n keys (padded to a power of two with sentinels, id INF, that order after every
+// key) in the graph's global scratch (device-coherent accesses: threads exchange
+// keys between stages)
+__device__ void sort_keys_g(const BT& t, int64_t eo, int n, int32_t* kr, int64_t* kc, uint64_t* ks, int32_t* ki) {
+  const int tid = threadIdx.x, NT = blockDim.x;
   int P = 1;
   while (P < n) P <<= 1;
-  for (int p = n + lane; p < P; p += 64) kput<G>(ki + p, INF);
-  wsync();
+  for (int p = n + tid; p < P; p += NT) st(ki + p, INF);
   __threadfence_block();
+  __syncthreads();
   for (int size = 2; size <= P; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int q = lane; q < P / 2; q += 64) {
+      for (int q = tid; q < P / 2; q += NT) {
         const int a = 2 * q - (q & (stride - 1));
         const int b = a + stride;
         const bool up = (a & size) == 0;
-        const int ia = kget<G>(ki + a), ib = kget<G>(ki + b);
+        const int ia = ld(ki + a), ib = ld(ki + b);
         if (ia == INF && ib == INF) continue;
         int ra = 0, rb = 0;
         int64_t ca = 0, cb = 0;
         uint64_t sa = 0, sb = 0;
         if (ia != INF) {
-          ra = kget<G>(kr + a);
-          ca = kget<G>(kc + a);
-          sa = kget<G>(ks + a);
+          ra = ld(kr + a);
+          ca = ld(kc + a);
+          sa = ld(ks + a);
         }
         if (ib != INF) {
-          rb = kget<G>(kr + b);
-          cb = kget<G>(kc + b);
-          sb = kget<G>(ks + b);
+          rb = ld(kr + b);
+          cb = ld(kc + b);
+          sb = ld(ks + b);
         }
-        // b < a ?
         const bool b_lt_a = ib == INF ? false : (ia == INF ? true : key_less(t, eo, rb, cb, sb, ib, ra, ca, sa, ia));
         const bool a_lt_b = ia == INF ? false : (ib == INF ? true : key_less(t, eo, ra, ca, sa, ia, rb, cb, sb, ib));
         if (up ? b_lt_a : a_lt_b) {
-          kput<G>(kr + a, rb);
-          kput<G>(kr + b, ra);
-          kput<G>(kc + a, cb);
-          kput<G>(kc + b, ca);
-          kput<G>(ks + a, sb);
-          kput<G>(ks + b, sa);
-          kput<G>(ki + a, ib);
-          kput<G>(ki + b, ia);
+          st(kr + a, rb);
+          st(kr + b, ra);
+          st(kc + a, cb);
+          st(kc + b, ca);
+          st(ks + a, sb);
+          st(ks + b, sa);
+          st(ki + a, ib);
+          st(ki + b, ia);
         }
       }
-      wsync();
       __threadfence_block();
+      stage_sync(size, stride);
     }
   }
 }
@@ -522,14 +680,14 @@ __device__ void sort_keys(const BT& t, int64_t eo, int n, int32_t* kr, int64_t* 
 // below 65,535: the host checks, sentinel 0xFFFFFFFF), n padded to a power of two
 // P <= the arrays' size
 __device__ void sort_keys_lds(const BT& t, int64_t eo, int n, uint32_t* kri, int64_t* kc, uint64_t* ks) {
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, NT = blockDim.x;
   int P = 1;
   while (P < n) P <<= 1;
-  for (int p = n + lane; p < P; p += 64) kri[p] = 0xFFFFFFFFu;
-  wsync();
+  for (int p = n + tid; p < P; p += NT) kri[p] = 0xFFFFFFFFu;
+  __syncthreads();
   for (int size = 2; size <= P; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int q = lane; q < P / 2; q += 64) {
+      for (int q = tid; q < P / 2; q += NT) {
         const int a = 2 * q - (q & (stride - 1));
         const int b = a + stride;
         const bool up = (a & size) == 0;
@@ -550,7 +708,7 @@ __device__ void sort_keys_lds(const BT& t, int64_t eo, int n, uint32_t* kri, int
           ks[b] = sa;
         }
       }
-      wsync();
+      stage_sync(size, stride);
     }
   }
 }
@@ -576,18 +734,33 @@ __device__ __forceinline__ void sort_regs(int64_t (&v)[M]) {
 }
 
 // ---------------------------------------------------------------------------
-// The graph's call schedule in order.  LDS holds the state of the rounds
-// [R - RW, R) (witnesses and their indexes, vote bitsets, coins, fame, event
-// counts, versions, receive thresholds and famous masks) and the undetermined list
-// with each event's round, creator and index; rounds below the window and lists
-// past UL entries live in global memory, where every mutation is also written.
+// The graph's call schedule in order, one workgroup of NWV waves per graph.  LDS
+// holds the state of the rounds [R - RW, R) (witnesses and their indexes, vote
+// bitsets, coins, fame, event counts, versions, receive thresholds and famous
+// masks) and the undetermined list with each event's round, creator and index;
+// rounds below the window and lists past UL entries live in global memory, where
+// every mutation is also written.  Per call:
+//   DivideRounds    wave 0 (the other waves compute the same scalars from the same
+//                   loads: R, the list length, its lowest round);
+//   DecideFame      rounds i split over the waves (each round's fame is decided from
+//                   the vote adjacency alone), LastConsensusRound = the highest
+//                   decided round, folded through LDS;
+//   thresholds      rounds split over the waves;
+//   round received  the list in spans of NWV x CPW chunks of 64: pass 1 loads a
+//                   span's entries into registers and finds each one's round
+//                   received, a prefix over the chunks' counts places the call's
+//                   batch and the remaining entries (compacted in place: a span's
+//                   entries move only below its own start), pass 2 takes the median
+//                   timestamps and writes both;
+//   FindOrder       the batch's bitonic sort over the whole workgroup.
 template <int NM>
-__global__ __launch_bounds__(64) void kb_consensus(BT t) {
+__global__ __launch_bounds__(256) void kb_consensus(BT t) {
   // KB: the LDS sort's capacity, a power of two (the network pads to one)
-  constexpr int RW = 8, UL = 1536, KB = 1024;
+  constexpr int NWV = 4, RW = 8, UL = 1536, KB = 1024, CPW = 2, NCH = NWV * CPW, SPAN = 64 * NCH;
   const int g = blockIdx.x;
   const GDesc d = t.gd[g];
-  const int N = t.N, SM = t.SM, lane = threadIdx.x, cc = t.ccap;
+  const int N = t.N, SM = t.SM, cc = t.ccap;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, NT = NWV * 64;
   const int64_t eo = d.eo;
   const int32_t* LA = t.LA + eo * N;
   const int32_t* FDg = t.FD + (int64_t)g * N * cc * N;  // [c][p][N]
@@ -602,15 +775,19 @@ __global__ __launch_bounds__(64) void kb_consensus(BT t) {
   __shared__ uint32_t kri[KB];  // roundReceived << 16 | id
   __shared__ int64_t kc[KB];
   __shared__ uint64_t ks[KB];
+  __shared__ int32_t cntR[NCH], cntK[NCH];  // a span's chunks: received / kept entries
+  __shared__ int32_t wred[3][NWV];          // per-wave partials: decided round, thresholds changed, kept minimum
+  __shared__ int64_t wtx[NWV];              // per-wave transaction counts of the call's batch
   if (t.scal[(int64_t)g * 8 + 6]) return;  // the rounds pass failed: nothing to decide
   // packed LDS keys need ids and rounds below 65,535 (else the global-scratch sort)
   const bool lds_keys = d.E < 0xFFFF && d.Rcap < 0xFFFF;
   int R = 0, lcr = -1, lcre = 0, nord = 0, nU = 0, n_prev = 0;
+  int umin = INF;  // the lowest round in the undetermined list
   int64_t ctx = 0;
   uint64_t cyc[6] = {0, 0, 0, 0, 0, 0};
   uint64_t t0_ = t.dbg ? __builtin_amdgcn_s_memtime() : 0;
 #define HGB_STAMP(i)                                      \
-  if (t.dbg) {                                            \
+  if (t.dbg && wv == 0) {                                 \
     const uint64_t t1_ = __builtin_amdgcn_s_memtime();    \
     cyc[i] += t1_ - t0_;                                  \
     t0_ = t1_;                                            \
@@ -632,7 +809,7 @@ __global__ __launch_bounds__(64) void kb_consensus(BT t) {
   auto rcnt_ = [&](int r) -> int { return res(r) ? rcntL[r & (RW - 1)] : ld(&t.rcnt[d.ro + r]); };
   auto ver_ = [&](int r) -> int { return res(r) ? verL[r & (RW - 1)] : ld(&t.ver[d.ro + r]); };
   auto thv_ = [&](int r) -> int { return res(r) ? thvL[r & (RW - 1)] : ld(&t.thv[d.ro + r]); };
-  // single-writer updates (lane 0 or the lane of column c), written through
+  // single-writer updates (lane 0 or the lane of column c of the owning wave), written through
   auto set_rcnt = [&](int r, int v) {
     if (res(r)) rcntL[r & (RW - 1)] = v;
     st(&t.rcnt[d.ro + r], v);
@@ -643,157 +820,211 @@ __global__ __launch_bounds__(64) void kb_consensus(BT t) {
   };
   for (int c = 0; c < d.K; c++) {
     const int n_c = (int)t.calls[d.co + c];
+    const int nU0 = nU, umin0 = umin;  // the list before this call's events
+    int rnmin;                         // the lowest round among the call's new events
     // ---- DivideRounds (hashgraph.go:573-588): the new events join the store ----
     {
       const int nn = n_c - n_prev;
       // the first 64 new events stay in registers (K <= 64: every call's)
       const bool on0 = lane < nn;
       const int x0 = n_prev + lane;
-      int r0 = on0 ? t.round[eo + x0] : -1;
-      const int w0 = on0 ? t.wit[eo + x0] : 0;
-      const int cp0 = on0 ? (t.cr[eo + x0] << 24 | t.ix[eo + x0]) : 0;
-      int rmax = r0;
+      const int r0 = on0 ? t.round[eo + x0] : -1;
+      int rmax = r0, rlo = on0 ? r0 : INF;
       for (int b0 = n_prev + 64; b0 < n_c; b0 += 64)
-        if (b0 + lane < n_c) rmax = max(rmax, t.round[eo + b0 + lane]);
+        if (b0 + lane < n_c) {
+          const int r = t.round[eo + b0 + lane];
+          rmax = max(rmax, r);
+          rlo = min(rlo, r);
+        }
       rmax = wave_max(rmax);
+      rnmin = wave_min(rlo);
+      umin = min(umin, rnmin);
       const int Rnew = nn > 0 ? max(R, rmax + 1) : R;
-      // rounds entering the window: their immutable rows, fresh mutable state
-      for (int r = max(R, Rnew - RW); r < Rnew; r++) {
-        const int s = r & (RW - 1);
-        const bool cl = lane < N;
-        const int64_t rw_ = (int64_t)(d.ro + r) * N;
-        const int w = cl ? t.W[rw_ + lane] : -1;
-        if (cl) {
-          wid[s][lane] = w;
-          wix[s][lane] = t.WIX[rw_ + lane];
-          ssbL[s][lane] = t.ssb[rw_ + lane];
-          seebL[s][lane] = t.seeb[rw_ + lane];
-          fameL[s][lane] = 0;
-        }
-        const uint64_t cm = ballot(cl && w >= 0 && t.WCOIN[rw_ + lane]);
-        if (lane == 0) {
-          coinL[s] = cm;
-          fmL[s] = 0;
-          rcntL[s] = 0;
-          verL[s] = 0;
-          thvL[s] = -1;
-        }
-      }
+      const int Rold = R;
       R = Rnew;
-      wsync();
-      // RoundEvents counts and witness versions, one writer per round; the
-      // undetermined list grows by the new events in insertion order
-      if (!ug && nU + nn > UL) {  // past the LDS list: move it to global memory for good
-        for (int i = lane; i < nU; i += 64) {
-          st(&Urg[i], Ur_s[i]);
-          st(&Ucpg[i], Ucp_s[i]);
-        }
-        ug = true;
-      }
-      for (int b0 = n_prev; b0 < n_c; b0 += 64) {
-        const int x = b0 + lane;
-        const bool on = x < n_c;
-        const int r = b0 == n_prev ? r0 : (on ? t.round[eo + x] : -1);
-        const int w = b0 == n_prev ? w0 : (on ? t.wit[eo + x] : 0);
-        const int cp = b0 == n_prev ? cp0 : (on ? (t.cr[eo + x] << 24 | t.ix[eo + x]) : 0);
-        if (on) {
-          uput(Ur_s, Urg, nU + (x - n_prev), r);
-          uput(Ucp_s, Ucpg, nU + (x - n_prev), cp);
-        }
-        uint64_t rem = ballot(on);
-        while (rem) {
-          const int rr0 = rl(r, __ffsll((unsigned long long)rem) - 1);
-          const uint64_t same = ballot(on && r == rr0);
-          const bool nw = ballot(on && r == rr0 && w) != 0;
-          if (lane == 0) {
-            set_rcnt(rr0, rcnt_(rr0) + __popcll(same));
-            if (nw) set_ver(rr0, ver_(rr0) + 1);
+      const bool ug_new = !ug && nU + nn > UL;  // past the LDS list: it moves to global memory for good
+      if (wv == 0) {
+        // rounds entering the window: their immutable rows, fresh mutable state
+        for (int r = max(Rold, Rnew - RW); r < Rnew; r++) {
+          const int s = r & (RW - 1);
+          const bool cl = lane < N;
+          const int64_t rw_ = (int64_t)(d.ro + r) * N;
+          const int w = cl ? t.W[rw_ + lane] : -1;
+          if (cl) {
+            wid[s][lane] = w;
+            wix[s][lane] = t.WIX[rw_ + lane];
+            ssbL[s][lane] = t.ssb[rw_ + lane];
+            seebL[s][lane] = t.seeb[rw_ + lane];
+            fameL[s][lane] = 0;
           }
-          rem &= ~same;
-          wsync();
+          const uint64_t cm = ballot(cl && w >= 0 && t.WCOIN[rw_ + lane]);
+          if (lane == 0) {
+            coinL[s] = cm;
+            fmL[s] = 0;
+            rcntL[s] = 0;
+            verL[s] = 0;
+            thvL[s] = -1;
+          }
         }
+        wsync();
+        // RoundEvents counts and witness versions, one writer per round; the
+        // undetermined list grows by the new events in insertion order
+        if (ug_new) {
+          for (int i = lane; i < nU; i += 64) {
+            st(&Urg[i], Ur_s[i]);
+            st(&Ucpg[i], Ucp_s[i]);
+          }
+          ug = true;
+        }
+        const int w0 = on0 ? t.wit[eo + x0] : 0;
+        const int cp0 = on0 ? (t.cr[eo + x0] << 24 | t.ix[eo + x0]) : 0;
+        for (int b0 = n_prev; b0 < n_c; b0 += 64) {
+          const int x = b0 + lane;
+          const bool on = x < n_c;
+          const int r = b0 == n_prev ? r0 : (on ? t.round[eo + x] : -1);
+          const int w = b0 == n_prev ? w0 : (on ? t.wit[eo + x] : 0);
+          const int cp = b0 == n_prev ? cp0 : (on ? (t.cr[eo + x] << 24 | t.ix[eo + x]) : 0);
+          if (on) {
+            uput(Ur_s, Urg, nU + (x - n_prev), r);
+            uput(Ucp_s, Ucpg, nU + (x - n_prev), cp);
+          }
+          uint64_t rem = ballot(on);
+          while (rem) {
+            const int rr0 = rl(r, __ffsll((unsigned long long)rem) - 1);
+            const uint64_t same = ballot(on && r == rr0);
+            const bool nw = ballot(on && r == rr0 && w) != 0;
+            if (lane == 0) {
+              set_rcnt(rr0, rcnt_(rr0) + __popcll(same));
+              if (nw) set_ver(rr0, ver_(rr0) + 1);
+            }
+            rem &= ~same;
+            wsync();
+          }
+        }
+        __threadfence_block();
       }
+      ug = ug || ug_new;
       nU += nn;
       n_prev = n_c;
     }
-    wsync();
+    __syncthreads();
     HGB_STAMP(0)
     // ---- DecideFame (hashgraph.go:598-664) ----
-    for (int i = lcr + 1; i < R - 1; i++) {
-      const int xid = lane < N ? W_(i, lane) : -1;
-      const bool px = xid >= 0 && xid < n_c;
-      const int fv0 = px ? fame_(i, lane) : 0;
-      int fv = fv0;
-      uint64_t prev = 0;
-      for (int j = i + 1; j < R; j++) {
-        const int diff = j - i;
-        const bool rj = res(j);
-        const int sj = j & (RW - 1);
-        const int yid = lane < N ? W_(j, lane) : -1;
-        const bool py = yid >= 0 && yid < n_c;
-        uint64_t ybits = 0;
-        if (lane < N)
-          ybits = diff == 1 ? (rj ? seebL[sj][lane] : t.seeb[row(j) + lane])
-                            : (rj ? ssbL[sj][lane] : t.ssb[row(j) + lane]);
-        const uint64_t ycoin = rj ? coinL[sj] : ballot(py && t.WCOIN[row(j) + lane]);
-        uint64_t mm = ballot(py);
-        uint64_t cur = 0;
-        bool on = px;
-        while (mm) {
-          const int dd = __ffsll((unsigned long long)mm) - 1;
-          mm &= mm - 1;
-          const uint64_t s = rl64(ybits, dd);
-          if (diff == 1) {
-            if (on && ((s >> lane) & 1)) cur |= 1ull << dd;  // setVote(y, x, See(y, x))
-          } else if (on) {
-            const int yays = __popcll(s & prev), tot = __popcll(s), nays = tot - yays;
-            bool v = yays >= nays;
-            const int tt = v ? yays : nays;
-            if (diff % N != 0) {  // normal round
-              if (tt >= SM) {
-                fv = v ? 1 : 2;  // SetFame(x, v); break out of the y loop
-                on = false;
-              } else if (v) {
-                cur |= 1ull << dd;
+    // Lane y is a voter of round j (y = lane, or lane & 31 with two half waves at
+    // N <= 32); the witnesses x of round i are spread over the waves and half
+    // waves, KX per lane group.  For one x and one j every present y's yays / nays
+    // come at once (popcounts of its strongly-see bits against x's votes from round
+    // j-1), the y loop's `break` is the first y whose tally reaches SM (a ballot's
+    // lowest bit): x's votes from round j are the v of the y before it, its fame the
+    // v of that y; later j decide again and the last decision stays.  Coin rounds
+    // (diff % N == 0) vote the middle bit where no supermajority.  Missing votes are
+    // nays.  Per round, the waves' "changed" / "undecided" flags meet in LDS.
+    int mydec = -1;
+    {
+      constexpr int HV = NM <= 32 ? 2 : 1, XS = NWV * HV, KX = (NM + XS - 1) / XS;
+      const int h = HV == 2 ? lane >> 5 : 0, y = HV == 2 ? lane & 31 : lane;
+      const int xb = wv * HV + h;
+      auto half = [&](uint64_t m) -> uint64_t { return HV == 2 ? (m >> (32 * h)) & 0xFFFFFFFFull : m; };
+      for (int i = lcr + 1; i < R - 1; i++) {
+        bool px[KX];
+        int fv[KX], fv0[KX];
+        uint64_t prev[KX];
+#pragma unroll
+        for (int k = 0; k < KX; k++) {
+          const int x = xb + XS * k;
+          const int xid = x < N ? W_(i, x) : -1;
+          px[k] = xid >= 0 && xid < n_c;
+          fv0[k] = px[k] ? fame_(i, x) : 0;
+          fv[k] = fv0[k];
+          prev[k] = 0;
+        }
+        for (int j = i + 1; j < R; j++) {
+          const int diff = j - i;
+          const bool rj = res(j);
+          const int sj = j & (RW - 1);
+          const int yid = y < N ? W_(j, y) : -1;
+          const bool py = yid >= 0 && yid < n_c;
+          uint64_t yb = 0;
+          bool ycoin = false;
+          if (py) {
+            yb = diff == 1 ? (rj ? seebL[sj][y] : t.seeb[row(j) + y]) : (rj ? ssbL[sj][y] : t.ssb[row(j) + y]);
+            ycoin = rj ? (coinL[sj] >> y) & 1 : t.WCOIN[row(j) + y] != 0;
+          }
+          const int tot = __popcll(yb);
+#pragma unroll
+          for (int k = 0; k < KX; k++) {
+            const int x = xb + XS * k;
+            uint64_t cur;
+            if (diff == 1) {
+              cur = half(ballot(py && ((yb >> x) & 1)));  // setVote(y, x, See(y, x))
+            } else {
+              const int yays = __popcll(yb & prev[k]), nays = tot - yays;
+              const bool v = yays >= nays;
+              const int tt = v ? yays : nays;
+              if (diff % N != 0) {  // normal round: SetFame(x, v) and break at the first tt >= SM
+                const uint64_t dm = half(ballot(py && tt >= SM));
+                const uint64_t vm = half(ballot(py && v));
+                if (dm) {
+                  const int ys = __ffsll((unsigned long long)dm) - 1;
+                  if (px[k]) fv[k] = (vm >> ys) & 1 ? 1 : 2;
+                  cur = vm & ((1ull << ys) - 1);
+                } else {
+                  cur = vm;
+                }
+              } else {  // coin round: the middle bit of y's hash when no supermajority
+                cur = half(ballot(py && (tt >= SM ? v : ycoin)));
               }
-            } else {  // coin round: the middle bit of y's hash when no supermajority
-              if (tt < SM) v = (ycoin >> dd) & 1;
-              if (v) cur |= 1ull << dd;
             }
+            prev[k] = cur;
           }
         }
-        prev = cur;
+        bool chg = false, und = false;
+#pragma unroll
+        for (int k = 0; k < KX; k++) {
+          const int x = xb + XS * k;
+          const bool ch = px[k] && fv[k] != fv0[k];
+          if (ch && y == 0) {
+            if (res(i)) fameL[i & (RW - 1)][x] = (int8_t)fv[k];
+            st(&t.fame[row(i) + x], (int8_t)fv[k]);
+          }
+          chg = chg || ch;
+          und = und || (px[k] && fv[k] == 0);
+        }
+        const uint64_t bc = ballot(chg), bu = ballot(und);
+        if (lane == 0) wred[0][wv] = (bc ? 1 : 0) | (bu ? 2 : 0);
+        __threadfence_block();
+        __syncthreads();
+        int fl = 0;
+        for (int w = 0; w < NWV; w++) fl |= wred[0][w];
+        if ((fl & 1) && tid == 0) set_ver(i, ver_(i) + 1);
+        if (!(fl & 2)) mydec = i;  // WitnessesDecided (roundInfo.go:78-85)
+        __syncthreads();           // wred[0] is the next round's
       }
-      const bool chg = px && fv != fv0;
-      if (chg) {
-        if (res(i)) fameL[i & (RW - 1)][lane] = (int8_t)fv;
-        st(&t.fame[row(i) + lane], (int8_t)fv);
-      }
-      wsync();
-      if (ballot(chg) && lane == 0) set_ver(i, ver_(i) + 1);
-      const bool decided = ballot(px && fv == 0) == 0;  // WitnessesDecided (roundInfo.go:78-85)
-      if (decided && (lcr < 0 || i > lcr)) {           // setLastConsensusRound (hashgraph.go:666-673)
-        lcr = i;
-        lcre = i >= 1 ? rcnt_(i - 1) : 0;
-      }
-      wsync();
     }
+    {
+      // setLastConsensusRound (hashgraph.go:666-673): i runs upwards from lcr + 1 and
+      // every decided i is past the last one set, so the highest decided round wins
+      if (mydec >= 0) {
+        lcr = mydec;
+        lcre = mydec >= 1 ? rcnt_(mydec - 1) : 0;
+      }
+    }
+    __syncthreads();  // the versions set above, for the thresholds
     HGB_STAMP(1)
     // ---- DecideRoundReceived (hashgraph.go:676-721) ----
-    int rmin = INF;
-    for (int b0 = 0; b0 < nU; b0 += 64)
-      if (b0 + lane < nU) rmin = min(rmin, uget(Ur_s, Urg, b0 + lane));
-    rmin = wave_min(rmin);
-    if (rmin == INF) rmin = R;
+    const int rmin = umin == INF ? R : umin;
     // decided rounds past the lowest undetermined round: the famous mask and the
-    // thresholds theta (kept while the round's version holds)
-    for (int i = rmin + 1; i < R; i++) {
+    // thresholds theta (kept while the round's version holds: every fame change and
+    // every new witness bumps the version, so thv == ver means decided and current)
+    bool thchg = false;
+    for (int i = rmin + 1 + wv; i < R; i += NWV) {
+      const int v = ver_(i);
+      if (thv_(i) == v) continue;
       const int w = lane < N ? W_(i, lane) : -1;
       const bool pw = w >= 0 && w < n_c;
       const int f = pw ? fame_(i, lane) : 0;
       if (ballot(pw && f == 0)) continue;  // not decided
-      const int v = ver_(i);
-      if (thv_(i) == v) continue;
+      thchg = true;
       const uint64_t fm = ballot(pw && f == 1);
       const int m = __popcll(fm);
       int th = -2;  // no famous witness: nothing is received in the round
@@ -827,134 +1058,204 @@ __global__ __launch_bounds__(64) void kb_consensus(BT t) {
       }
       wsync();
     }
+    if (lane == 0) wred[1][wv] = thchg;
+    __threadfence_block();
+    __syncthreads();
+    for (int w = 0; w < NWV; w++) thchg = thchg || wred[1][w];
     HGB_STAMP(2)
     // the undetermined events in order: received ones become the call's batch (keys
-    // to LDS, and to global scratch past KB), the rest stay (compacted in place)
-    int nb = 0, nk = 0;
+    // to LDS, and to global scratch past KB), the rest stay (compacted in place).
+    // With no thresholds (re)computed in this call no earlier entry can be received
+    // now (a round leaving the decided state only removes candidates), so only the
+    // call's new events are examined.
+    // Nor can a new event be, unless some round above it is decided: then the call
+    // receives nothing and the list only grew.
+    bool scan = thchg;
+    for (int i = rnmin == INF ? R : rnmin + 1; i < R && !scan; i++) scan = thv_(i) == ver_(i);
+    const int u0 = thchg ? 0 : nU0;
+    int nb = 0, nk = scan ? u0 : nU, kmin = INF;
     int64_t tx = 0;
-    for (int b0 = 0; b0 < nU; b0 += 64) {
-      const bool on = b0 + lane < nU;
-      const int r = on ? uget(Ur_s, Urg, b0 + lane) : 0;
-      const int cp = on ? uget(Ucp_s, Ucpg, b0 + lane) : 0;
-      const int cx = cp >> 24, px = cp & 0xFFFFFF;
-      int x = -1;
-      int found = -1;
-      if (on) {
-        for (int i = r + 1; i < R; i++) {
-          int th;
-          if (res(i)) {
-            const int s = i & (RW - 1);
-            if (thvL[s] != verL[s]) continue;  // not decided (or thresholds stale: never here)
-            th = thL[s][cx];
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (int sb = u0; scan && sb < nU; sb += SPAN) {
+      // pass 1: the span's entries (chunk k * NWV + wv of the span is this wave's k-th)
+      int er[CPW], ecp[CPW], ef[CPW];
+#pragma unroll
+      for (int k = 0; k < CPW; k++) {
+        const int e = sb + (k * NWV + wv) * 64 + lane;
+        const bool on = e < nU;
+        er[k] = on ? uget(Ur_s, Urg, e) : 0;
+        ecp[k] = on ? uget(Ucp_s, Ucpg, e) : 0;
+        int found = -1;
+        if (on) {
+          const int cx = ecp[k] >> 24, px = ecp[k] & 0xFFFFFF;
+          for (int i = er[k] + 1; i < R; i++) {
+            int th;
+            if (res(i)) {
+              const int s = i & (RW - 1);
+              if (thvL[s] != verL[s]) continue;  // not decided (or thresholds stale: never here)
+              th = thL[s][cx];
+            } else {
+              if (ld(&t.thv[d.ro + i]) != ld(&t.ver[d.ro + i])) continue;
+              th = ld(&t.th[row(i) + cx]);
+            }
+            if (th != -2 && px <= th) {
+              found = i;
+              break;
+            }
+          }
+        }
+        ef[k] = found;
+        const int nr = __popcll(ballot(found >= 0)), nkp = __popcll(ballot(on && found < 0));
+        if (lane == 0) {
+          cntR[k * NWV + wv] = nr;
+          cntK[k * NWV + wv] = nkp;
+        }
+      }
+      __syncthreads();
+      int preR[CPW], preK[CPW], totR = 0, totK = 0;
+#pragma unroll
+      for (int k = 0; k < CPW; k++) preR[k] = preK[k] = 0;
+      for (int q = 0; q < NCH; q++) {
+#pragma unroll
+        for (int k = 0; k < CPW; k++)
+          if (q == k * NWV + wv) {
+            preR[k] = totR;
+            preK[k] = totK;
+          }
+        totR += cntR[q];
+        totK += cntK[q];
+      }
+      // pass 2: medians and keys of the received entries, the kept ones compacted
+#pragma unroll
+      for (int k = 0; k < CPW; k++) {
+        const int e = sb + (k * NWV + wv) * 64 + lane;
+        const bool on = e < nU;
+        const int found = ef[k];
+        const int cx = ecp[k] >> 24, px = ecp[k] & 0xFFFFFF;
+        const uint64_t rec = ballot(found >= 0), keep = ballot(on && found < 0);
+        if (found >= 0) {
+          // MedianTimestamp over OldestSelfAncestorToSee(w, x) of the famous witnesses w
+          // that see x (hashgraph.go:704-709, 762-770), the upper median.  w = (d, i_w)
+          // sees x iff FD[x][d] <= i_w, and FD[x][d] is then OldestSelfAncestorToSee
+          const int64_t cpos = (int64_t)cx * cc + px;
+          const int x = chg[cpos];
+          const uint64_t s0 = t.Sch[(int64_t)g * N * cc + cpos];
+          tx += t.ntxch[(int64_t)g * N * cc + cpos];
+          uint64_t fm;
+          if (res(found)) {
+            fm = fmL[found & (RW - 1)];
           } else {
-            if (ld(&t.thv[d.ro + i]) != ld(&t.ver[d.ro + i])) continue;
-            th = ld(&t.th[row(i) + cx]);
+            fm = 0;
+            for (int dd = 0; dd < N; dd++) {
+              const int w = t.W[row(found) + dd];
+              if (w >= 0 && w < n_c && ld(&t.fame[row(found) + dd]) == 1) fm |= 1ull << dd;
+            }
           }
-          if (th != -2 && px <= th) {
-            found = i;
-            break;
-          }
-        }
-      }
-      int64_t med = 0;
-      uint64_t s0 = 0;
-      if (found >= 0) {
-        // MedianTimestamp over OldestSelfAncestorToSee(w, x) of the famous witnesses w
-        // that see x (hashgraph.go:704-709, 762-770), the upper median.  w = (d, i_w)
-        // sees x iff FD[x][d] <= i_w, and FD[x][d] is then OldestSelfAncestorToSee
-        const int64_t cpos = (int64_t)cx * cc + px;
-        x = chg[cpos];
-        s0 = t.Sch[(int64_t)g * N * cc + cpos];
-        tx += t.ntxch[(int64_t)g * N * cc + cpos];
-        uint64_t fm;
-        if (res(found)) {
-          fm = fmL[found & (RW - 1)];
-        } else {
-          fm = 0;
-          for (int dd = 0; dd < N; dd++) {
-            const int w = t.W[row(found) + dd];
-            if (w >= 0 && w < n_c && ld(&t.fame[row(found) + dd]) == 1) fm |= 1ull << dd;
-          }
-        }
-        int64_t vals[NM];
-        int q[NM];
+          int64_t vals[NM];
+          int q[NM];
 #pragma unroll
-        for (int dd = 0; dd < NM; dd++)
-          q[dd] = dd < N && ((fm >> dd) & 1) ? FDg[((int64_t)cx * cc + px) * N + dd] : INF;
-        int m = 0;
+          for (int dd = 0; dd < NM; dd++)
+            q[dd] = dd < N && ((fm >> dd) & 1) ? FDg[cpos * N + dd] : INF;
+          int m = 0;
 #pragma unroll
-        for (int dd = 0; dd < NM; dd++) {
-          vals[dd] = TS_MAX;
-          if (q[dd] != INF && q[dd] <= WIX_(found, dd)) {
-            vals[dd] = tschg[(int64_t)dd * cc + q[dd]];
-            m++;
+          for (int dd = 0; dd < NM; dd++) {
+            vals[dd] = TS_MAX;
+            if (q[dd] != INF && q[dd] <= WIX_(found, dd)) {
+              vals[dd] = tschg[(int64_t)dd * cc + q[dd]];
+              m++;
+            }
+          }
+          // the upper median: the m real values sort before the TS_MAX fillers
+          sort_regs<NM>(vals);
+          const int want = m / 2;
+          int64_t med = 0;
+#pragma unroll
+          for (int a = 0; a < NM; a++)
+            if (a == want) med = vals[a];
+          t.rr[eo + x] = found;
+          t.cts[eo + x] = med;
+          const int p = nb + preR[k] + __popcll(rec & below);
+          if (p < KB && lds_keys) {
+            kri[p] = (uint32_t)found << 16 | (uint32_t)x;
+            kc[p] = med;
+            ks[p] = s0;
+          } else {
+            const int64_t so = 2 * eo + nord + p;
+            st(&t.krr[so], found);
+            st(&t.kct[so], med);
+            st(&t.ks0[so], s0);
+            st(&t.kid[so], x);
           }
         }
-        // the upper median: the m real values sort before the TS_MAX fillers
-        sort_regs<NM>(vals);
-        const int want = m / 2;
-#pragma unroll
-        for (int a = 0; a < NM; a++)
-          if (a == want) med = vals[a];
-        t.rr[eo + x] = found;
-        t.cts[eo + x] = med;
-      }
-      const uint64_t rec = ballot(found >= 0);
-      const uint64_t keep = ballot(on && found < 0);
-      const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-      if (found >= 0) {
-        const int p = nb + __popcll(rec & below);
-        if (p < KB && lds_keys) {
-          kri[p] = (uint32_t)found << 16 | (uint32_t)x;
-          kc[p] = med;
-          ks[p] = s0;
+        if (on && found < 0) {
+          const int p = nk + preK[k] + __popcll(keep & below);
+          uput(Ur_s, Urg, p, er[k]);
+          uput(Ucp_s, Ucpg, p, ecp[k]);
+          kmin = min(kmin, er[k]);
         }
-        const int64_t so = 2 * eo + nord + p;
-        st(&t.krr[so], found);
-        st(&t.kct[so], med);
-        st(&t.ks0[so], s0);
-        st(&t.kid[so], x);
       }
-      if (on && found < 0) {
-        const int p = nk + __popcll(keep & below);
-        uput(Ur_s, Urg, p, r);
-        uput(Ucp_s, Ucpg, p, cp);
-      }
-      nb += __popcll(rec);
-      nk += __popcll(keep);
-      wsync();
+      nb += totR;
+      nk += totK;
+      __threadfence_block();
+      __syncthreads();  // cntR / cntK are the next span's; its entries lie past every write above
     }
     nU = nk;
-    wsync();
+    {
+      const int km = wave_min(kmin);
+      const int64_t tw = wave_sum64(tx);
+      if (lane == 0) {
+        wred[2][wv] = km;
+        wtx[wv] = tw;
+      }
+    }
+    __syncthreads();
+    {
+      int km = INF;
+      for (int w = 0; w < NWV; w++) {
+        km = min(km, wred[2][w]);
+        ctx += wtx[w];
+      }
+      if (scan) umin = min(thchg ? INF : umin0, km);
+    }
     HGB_STAMP(3)
     // ---- FindOrder (hashgraph.go:723-760): sort the batch, append it ----
     if (nb > 0) {
       if (nb <= KB && lds_keys) {
         sort_keys_lds(t, eo, nb, kri, kc, ks);
-        for (int p = lane; p < nb; p += 64) t.order[eo + nord + p] = (int32_t)(kri[p] & 0xFFFFu);
+        __syncthreads();
+        for (int p = tid; p < nb; p += NT) t.order[eo + nord + p] = (int32_t)(kri[p] & 0xFFFFu);
       } else {
         // past KB keys: the same network on the graph's global scratch (2E entries
-        // from 2 eo: nord + the padded size stays below 2E)
+        // from 2 eo: nord + the padded size stays below 2E); the first KB keys are in LDS
         const int64_t so = 2 * eo + nord;
-        sort_keys<true>(t, eo, nb, t.krr + so, t.kct + so, t.ks0 + so, t.kid + so);
-        for (int p = lane; p < nb; p += 64) t.order[eo + nord + p] = ld(&t.kid[so + p]);
+        if (lds_keys)
+          for (int p = tid; p < KB; p += NT) {
+            st(&t.krr[so + p], (int32_t)(kri[p] >> 16));
+            st(&t.kct[so + p], kc[p]);
+            st(&t.ks0[so + p], ks[p]);
+            st(&t.kid[so + p], (int32_t)(kri[p] & 0xFFFFu));
+          }
+        __threadfence_block();
+        __syncthreads();
+        sort_keys_g(t, eo, nb, t.krr + so, t.kct + so, t.ks0 + so, t.kid + so);
+        __syncthreads();
+        for (int p = tid; p < nb; p += NT) t.order[eo + nord + p] = ld(&t.kid[so + p]);
       }
-      ctx += wave_sum64(tx);
     }
-    if (lane == 0) t.counts[d.co + c] = nb;
+    if (tid == 0) t.counts[d.co + c] = nb;
     nord += nb;
-    wsync();
+    __syncthreads();  // kri and the window state are the next call's
     HGB_STAMP(4)
   }
 #undef HGB_STAMP
-  if (t.dbg && lane == 0)
+  if (t.dbg && tid == 0)
     for (int i = 0; i < 5; i++) t.dbg[(int64_t)g * 8 + i] = cyc[i];
   // the undetermined list for the host
-  for (int i = lane; i < nU; i += 64) {
+  for (int i = tid; i < nU; i += NT) {
     const int cp = uget(Ucp_s, Ucpg, i);
     t.U[eo + i] = chg[(int64_t)(cp >> 24) * cc + (cp & 0xFFFFFF)];
   }
-  if (lane == 0) {
+  if (tid == 0) {
     int64_t* s = t.scal + (int64_t)g * 8;
     s[0] = R;
     s[1] = lcr;
@@ -1309,23 +1610,23 @@ struct hge_batch {
     if (N <= 32) {
       launch(kb_coords<32>, G, t);
       BCHK(hipEventRecord(ev[1], st));
-      launch(kb_fd<32>, G, t);
+      launch(kb_fd<32>, G * N, t);
       BCHK(hipEventRecord(ev[2], st));
       launch(kb_fdrows<32>, G * N, t, 256);
       BCHK(hipEventRecord(ev[3], st));
-      launch(kb_rounds<32, 4>, G, t);
+      launch(kb_front<32>, G, t, 1024);
       BCHK(hipEventRecord(ev[4], st));
-      launch(kb_consensus<32>, G, t);
+      launch(kb_consensus<32>, G, t, 256);
     } else {
       launch(kb_coords<64>, G, t);
       BCHK(hipEventRecord(ev[1], st));
-      launch(kb_fd<64>, G, t);
+      launch(kb_fd<64>, G * N, t);
       BCHK(hipEventRecord(ev[2], st));
       launch(kb_fdrows<64>, G * N, t, 256);
       BCHK(hipEventRecord(ev[3], st));
-      launch(kb_rounds<64, 2>, G, t);
+      launch(kb_front<64>, G, t, 1024);
       BCHK(hipEventRecord(ev[4], st));
-      launch(kb_consensus<64>, G, t);
+      launch(kb_consensus<64>, G, t, 256);
     }
     BCHK(hipEventRecord(ev[5], st));
     h_scal.resize((size_t)G * 8);

@@ -922,7 +922,7 @@ class Batch:
         keys = ("events", "calls", "rounds", "lcr", "lcre", "transactions", "ordered", "undetermined")
         return dict(zip(keys, a.tolist()))
 
-    KERNELS = ("kb_coords", "kb_fd", "kb_fdrows", "kb_rounds", "kb_consensus")
+    KERNELS = ("kb_coords", "kb_fd", "kb_fdrows", "kb_front", "kb_consensus")
 
     def kernel_ms(self):
         """Device ms of the last run's stages (HIP events between the launches)."""

@@ -38,9 +38,12 @@ kernel's device time for the roofline.  Rank 0 also
   * times the CPU baseline: the Go-faithful oracle on one host core over a
     bounded prefix of the same stream, and compares its order too;
   * with the default configuration, adds a `secondary` object: the 16/100k
-    replay (bit-exact against the oracle over the whole stream) and the online
+    replay (bit-exact against the oracle over the whole stream), the online
     per-call path (hge_insert_events of K events + hge_run_consensus per call,
-    what node/core.go:179-202 does) at 16/100k.
+    what node/core.go:179-202 does) at 16/100k, 64/1M and on the bench's own
+    256-wide stream, the ingest pipeline, and config 5 (`mc_1024x32x10k`: the
+    1,024-graph Monte Carlo batch on the batch engine, every graph against the
+    oracle's digest, with its own CPU baseline).
 """
 import argparse
 import json
@@ -268,19 +271,34 @@ def small_replay(n, E, K, seed, device, steps=20):
                        else "MISMATCH vs CPU oracle")}
 
 
-MC_KERNEL_BYTES = {  # algorithmic bytes per event (kb_consensus: per ordered event), SURVEY 8(d)
-    "kb_coords": lambda n: 4 * n + 16,  # the LA row written, the parents' creator / index / ids read
-    "kb_fd": lambda n: 8 * n,           # the LA row read, its firstDescendant runs written
-    "kb_fdrows": lambda n: 8 * n,       # the runs read, the firstDescendant row written
-    "kb_rounds": lambda n: 8 * n,       # the LA and FD rows read once (strongly-see counts, witness rows)
-    "kb_consensus": lambda n: 4 * n + 48,  # the median's rows and the sort key
-}
+def mc_kernel_bytes(kernel, n, events, ordered, rounds):
+    """Algorithmic bytes of one batch-engine stage over the whole batch:
+    `events` accepted events, `ordered` ordered ones, `rounds` summed over the graphs."""
+    per_event = {
+        "kb_coords": 4 * n + 16,  # the LA row written, the parents' creator / index / ids read
+        "kb_fd": 8 * n,           # the LA row read, its firstDescendant runs written
+        "kb_fdrows": 8 * n,       # the runs read, the firstDescendant row written
+    }
+    if kernel in per_event:
+        return per_event[kernel] * events
+    if kernel == "kb_front":
+        # per round: N member rows and, per member, the N rows FD[(i, FD[w][i])]
+        # (4N bytes each); per event its chain slot read and round / witness written
+        return rounds * (4 * n * n + 4 * n * n * n) + 9 * events
+    return (4 * n + 48) * ordered  # kb_consensus: the median's rows and the sort key
 
 
 def mc_main(args, n, E, K, rank, world, local_rank, dist):
+    line = mc_line(args, n, E, K, rank, world, local_rank, dist)
+    if line is not None:
+        print(json.dumps(line), flush=True)
+
+
+def mc_line(args, n, E, K, rank, world, local_rank, dist, cpu_s=10.0):
     """Config 5 on the batch engine: this rank's share of the Monte Carlo batch,
-    one replay of all of it per step (four launches), every graph checked
-    against the oracle's committed full-state digest."""
+    one replay of all of it per step (five launches), every graph checked
+    against the oracle's committed full-state digest.  Returns rank 0's line
+    (None elsewhere); the CPU baseline takes about `cpu_s` seconds."""
     from babble_amd.dist import reduce_step, shard_range
     from babble_amd.engine import Batch
     from babble_amd.gossip import random_gossip, schedule
@@ -324,6 +342,7 @@ def mc_main(args, n, E, K, rank, world, local_rank, dist):
     if dist is not None:
         max_step, tot_ordered = reduce_step(dist, step_s, ordered, f"cuda:{local_rank}")
 
+    rounds_tot = sum(batch.info(g)["rounds"] for g in range(per))
     # every graph of this rank against the oracle's full-state digest
     checks = []
     dg = mc_digests(n, E, K, args.seed)
@@ -357,7 +376,7 @@ def mc_main(args, n, E, K, rank, world, local_rank, dist):
             _, _, corder, _ = oracle_replay(d, schedule(len(d["creator"]), K))
             tot += len(corder)
             ng += 1
-            if time.perf_counter() - tc > 10.0:
+            if time.perf_counter() - tc > cpu_s:
                 break
         cs = time.perf_counter() - tc
         cpu = {"value": round(tot / cs, 1), "unit": "events/s", "cores": 1, "kind": "port",
@@ -366,17 +385,14 @@ def mc_main(args, n, E, K, rank, world, local_rank, dist):
                          f"{platform.processor() or platform.machine()} (host nproc {os.cpu_count()})"}
     if rank != 0:
         batch.close()
-        return
+        return None
     value = tot_ordered / max_step
     dom = max(kms, key=kms.get)
-    per_unit = MC_KERNEL_BYTES[dom](n)
-    units = ordered if dom == "kb_consensus" else events
-    alg = per_unit * units
+    kb = {k_: mc_kernel_bytes(k_, n, events, ordered, rounds_tot) for k_ in kms}
+    alg = kb[dom]
     achieved = alg / (kms[dom] * 1e-3) / 1e9
-    hbm = {k_: {"ms": round(v_, 4), "alg_bytes": MC_KERNEL_BYTES[k_](n) * (ordered if k_ == "kb_consensus"
-                                                                         else events),
-                "achieved_gbs": round(MC_KERNEL_BYTES[k_](n) * (ordered if k_ == "kb_consensus" else events)
-                                      / (v_ * 1e-3) / 1e9, 2)} for k_, v_ in kms.items()}
+    hbm = {k_: {"ms": round(v_, 4), "alg_bytes": kb[k_], "achieved_gbs": round(kb[k_] / (v_ * 1e-3) / 1e9, 2)}
+           for k_, v_ in kms.items()}
     line = {
         "metric": "consensus-ordered events/sec at N participants",
         "value": round(value, 1),
@@ -410,8 +426,8 @@ def mc_main(args, n, E, K, rank, world, local_rank, dist):
         "kernels_ms_per_replay": {k_: round(v_, 4) for k_, v_ in sorted(kms.items(), key=lambda kv: -kv[1])},
         "kernel_launches_per_replay": {k_: 1 for k_ in kms},
     }
-    print(json.dumps(line), flush=True)
     batch.close()
+    return line
 
 
 def main():
@@ -650,6 +666,11 @@ def main():
                               f"{n}-participant stream, hge_insert_events(K={K}) + hge_run_consensus per call "
                               f"({len(schedule(ONLINE_PREFIX, K))} calls)"),
                      "ingest_16_100k": ingest_path(16, 100_000, 16, args.seed, local_rank)}
+        # config 5 (BASELINE configs[4]) on the batch engine, the same steps as this line
+        import copy
+        mca = copy.copy(args)
+        mca.graphs = 1024
+        secondary["mc_1024x32x10k"] = mc_line(mca, 32, 10_000, 32, 0, 1, local_rank, None, cpu_s=5.0)
 
     if rank == 0:
         value = tot_ordered / max_step

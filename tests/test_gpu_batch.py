@@ -86,7 +86,7 @@ def test_batch_many_graphs_one_launch_per_stage():
             b.add(dag, calls)
         b.run()
         ms = b.kernel_ms()
-        assert set(ms) == {"kb_coords", "kb_fd", "kb_fdrows", "kb_rounds", "kb_consensus"}
+        assert set(ms) == {"kb_coords", "kb_fd", "kb_fdrows", "kb_front", "kb_consensus"}
         for g in range(0, 256, 5):
             w = oracle_state(*streams[g])
             assert first_difference(b.state(g), w) is None, f"graph {g}"
