@@ -5,31 +5,33 @@
 // The single-graph engine (hge_engine.hip) sizes its grids from one graph and
 // makes a few host round trips per replay; driving 1,024 of them means ~50k
 // launches per batch from host threads (58M ev/s, the
-// host bound).  Here every stage is ONE launch over the whole batch, one
-// 64-lane wavefront per graph (N <= 64: lane = participant column / witness
-// slot), and the graph's whole call schedule runs inside the consensus kernel:
+// host bound).  Here every stage is ONE launch over the whole batch, and the
+// graph's whole call schedule runs inside the consensus kernel:
 //
-//   kb_coords     lastAncestors rows in insertion order (hashgraph.go:399-463);
-//                 the chain heads' rows live in LDS, a row is a max of the
-//                 self-parent head and the other-parent row.
-//   kb_fd         firstDescendants in run layout FDT[j][c][p]: chain-j event k is
-//                 the first chain-j descendant of chain-c positions
-//                 (LA[(j,k-1)][c], LA[(j,k)][c]] (hashgraph.go:466-494).
-//   kb_rounds     Round / Witness of every event in insertion order
-//                 (hashgraph.go:220-305): ParentRound from the parents' rounds,
-//                 RoundInc = strongly seeing >= SM witnesses of the parent round
-//                 present so far (the last rounds' witness FD rows in an LDS ring);
-//                 each new witness gets its strongly-see / see bitsets over the
-//                 previous round's witnesses (the vote adjacency of DecideFame).
-//   kb_consensus  for every call point in order: DivideRounds' bookkeeping,
-//                 DecideFame (hashgraph.go:598-664: lane = witness x of round i,
-//                 its votes over round j's witnesses a 64-bit mask, the `break`,
-//                 missing votes as nays, coin rounds), DecideRoundReceived
-//                 (hashgraph.go:676-721: x is seen by more than half of the famous
-//                 witnesses iff index(x) <= theta(round, creator(x)), the
-//                 (|F|/2+1)-th largest lastAncestor of the famous witnesses),
-//                 MedianTimestamp (:762-770) and the ConsensusSorter sort of the
-//                 call's batch (consensus_sorter.go:36-59, PRN = 0) in LDS.
+//   kb_coords     lastAncestors rows in insertion order (hashgraph.go:399-463), one
+//                 wave per graph (lane = column); the chain heads' rows live in
+//                 registers, a row is a max of the self-parent head and the
+//                 other-parent row.
+//   kb_fd         firstDescendants in run layout FDT[j][c][p], one wave per (graph,
+//                 chain j): chain-j event k is the first chain-j descendant of
+//                 chain-c positions (LA[(j,k-1)][c], LA[(j,k)][c]] (hashgraph.go:466-494);
+//   kb_fdrows     ... transposed to rows FD[c][p][j] through LDS tiles.
+//   kb_front      Round / Witness of every event (hashgraph.go:220-305) by the round
+//                 frontier: C_{r+1}[c] = the SM-th smallest over the round-r
+//                 members d of the first position of chain c that strongly sees d,
+//                 one 1024-thread workgroup per graph; each witness's strongly-see /
+//                 see bitsets over the previous round's witnesses (the vote adjacency
+//                 of DecideFame).
+//   kb_consensus  for every call point in order, one 4-wave workgroup per graph:
+//                 DivideRounds' bookkeeping, DecideFame (hashgraph.go:598-664: lane
+//                 = voter y, witnesses x over the waves, a vote set a 64-bit mask,
+//                 the `break` as the first y whose tally reaches SM, missing votes as
+//                 nays, coin rounds), DecideRoundReceived (hashgraph.go:676-721: x is
+//                 seen by more than half of the famous witnesses iff index(x) <=
+//                 theta(round, creator(x)), the (|F|/2+1)-th largest lastAncestor of
+//                 the famous witnesses), MedianTimestamp (:762-770) and the
+//                 ConsensusSorter sort of the call's batch (consensus_sorter.go:36-59,
+//                 PRN = 0) in LDS.
 //
 // Everything on the path is integer; results are bit-exact with the oracle
 // (tests/test_gpu_batch.py, tests/test_gpu_mc.py: every graph's full-state digest).
@@ -48,7 +50,6 @@
 namespace hgb {
 
 constexpr int32_t INF = 0x7fffffff;
-constexpr int64_t TS_MAX = INT64_MAX;
 
 struct GDesc {
   int64_t eo;    // first event of the graph in the per-event pools
@@ -269,175 +270,6 @@ __global__ __launch_bounds__(256) void kb_fdrows(BT t) {
     }
     __syncthreads();
   }
-}
-
-// ---------------------------------------------------------------------------
-// Round / Witness in insertion order (hashgraph.go:220-305).  DivideRounds computes
-// Round(x) in insertion order, so when x is computed the store holds exactly the
-// events before it: Rounds() = 1 + their highest round, and RoundWitnesses(pr) are
-// the witnesses of round pr among them.  StronglySee(x, w) counts the columns with
-// LA[x][k] >= FD[w][k] (hashgraph.go:189-208); FD here is final, which gives the same
-// count (a descendant of w that x sees precedes x).  The LA and FD rows of 32 events
-// at a time are staged in LDS, the next 32 in flight in registers.
-template <int NM, int RING>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void kb_rounds(BT t) {
-  constexpr int CH = 32;                 // events per chunk
-  constexpr int PER = CH * NM / 64;      // row elements per lane and chunk
-  const int g = blockIdx.x;
-  const GDesc d = t.gd[g];
-  const int N = t.N, SM = t.SM, k = threadIdx.x;
-  __shared__ int32_t wid[RING][NM], wixr[RING][NM];
-  __shared__ int32_t wfd[RING][NM][NM];  // [slot][witness creator][column k]: the witness's FD row
-  __shared__ uint64_t wpres[RING];        // the slot's witnesses so far (bit = creator)
-  __shared__ int32_t bla[CH][NM], bfd[CH][NM];
-  int rh = -1, hid = -1;  // lane c: the round and the id of chain c's head
-  if (k < NM)
-    for (int s = 0; s < RING; s++) {
-      wid[s][k] = -1;
-      for (int q = 0; q < NM; q++) wfd[s][q][k] = INF;
-    }
-  if (k < RING) wpres[k] = 0;
-  __syncthreads();
-  const int32_t* LA = t.LA + d.eo * N;
-  const int32_t* FDg = t.FD + (int64_t)g * N * t.ccap * N;  // [c][p][N]
-  int top = -1;   // highest round with a ring slot
-  int maxr = -1;  // highest round so far (Rounds() - 1)
-  int err = 0;
-  // the witnesses (slot d) of round r that the LA row `la` strongly sees
-  // the witnesses (bit d = creator) of round r that the LA row `la` (lane k holds
-  // column k) strongly sees: per witness, one compare of the row against the
-  // witness's FD row across the lanes and a popcount of the ballot
-  // (hashgraph.go:189-208); columns past N hold la = -1 < INF, never counted
-  auto ss_mask = [&](int r, int la, bool ring) -> uint64_t {
-    uint64_t m = 0;
-    if (ring) {
-      const int s = r % RING;
-      const uint64_t pres = wpres[s];
-      int wv[NM];
-#pragma unroll
-      for (int dd = 0; dd < NM; dd++) wv[dd] = k < NM ? wfd[s][dd][k] : INF;  // lanes past NM: no column
-#pragma unroll
-      for (int dd = 0; dd < NM; dd++)
-        if (__popcll(ballot(la >= wv[dd])) >= SM) m |= 1ull << dd;
-      return m & pres;
-    }
-    for (int dd = 0; dd < N; dd++) {
-      const int w = ld(&t.W[(int64_t)(d.ro + r) * N + dd]);
-      if (w < 0) continue;
-      const int f = k < N ? ld(&t.WFD[((int64_t)(d.ro + r) * N + dd) * N + k]) : INF;
-      if (__popcll(ballot(la >= f)) >= SM) m |= 1ull << dd;
-    }
-    return m;
-  };
-  // chunk loads: element e = k + 64 v of the chunk's CH x N row block
-  int rla[PER], rfd[PER], mcr, mix, msp, mop, moc, mco;
-  auto load = [&](int base) {
-    const int i = base + k;
-    const bool on = k < CH && i < d.E;
-    mcr = on ? t.cr[d.eo + i] : 0;
-    mix = on ? t.ix[d.eo + i] : 0;
-    msp = on ? t.sp[d.eo + i] : -1;
-    mop = on ? t.op[d.eo + i] : -1;
-    moc = on ? t.oc[d.eo + i] : 0;
-    mco = on ? t.coin[d.eo + i] : 0;
-#pragma unroll
-    for (int v = 0; v < PER; v++) {
-      const int e = k + 64 * v, row = e / NM, col = e % NM;
-      const bool ok = col < N && base + row < d.E;
-      const int rcr = __shfl(mcr, row), rix = __shfl(mix, row);  // the row's chain position
-      rla[v] = ok ? LA[(int64_t)(base + row) * N + col] : -1;
-      rfd[v] = ok ? FDg[((int64_t)rcr * t.ccap + rix) * N + col] : INF;
-    }
-  };
-  load(0);
-  for (int base = 0; base < d.E && !err; base += CH) {
-#pragma unroll
-    for (int v = 0; v < PER; v++) {
-      const int e = k + 64 * v;
-      bla[e / NM][e % NM] = rla[v];
-      bfd[e / NM][e % NM] = rfd[v];
-    }
-    const int ccr = mcr, cix = mix, csp = msp, cop = mop, coc = moc, cco = mco;
-    wsync();
-    if (base + CH < d.E) load(base + CH);  // the next chunk, in flight meanwhile
-    const int cnt = min(CH, d.E - base);
-    for (int u = 0; u < cnt; u++) {
-      const int x = base + u;
-      const int cr = rl(ccr, u), ix = rl(cix, u), sp = rl(csp, u), op = rl(cop, u), oc = rl(coc, u);
-      const int lax = k < N ? bla[u][k] : -1;
-      // ParentRound (hashgraph.go:220-244): 0 without both parents
-      const int rsp = sp >= 0 ? rl(rh, cr) : -1;
-      int pr = 0;
-      if (sp >= 0 && op >= 0) {
-        const int rop = rl(hid, oc) == op ? rl(rh, oc) : ld(&t.round[d.eo + op]);
-        pr = max(rsp, rop);
-      }
-      // RoundInc (hashgraph.go:263-285): Rounds() < pr + 1 -> false
-      bool inc = false;
-      if (maxr + 1 >= pr + 1) {
-        const bool ring = pr <= top && pr > top - RING;
-        inc = __popcll(ss_mask(pr, lax, ring)) >= SM;
-      }
-      const int r = pr + (inc ? 1 : 0);
-      const bool w = sp < 0 || r > rsp;  // Witness (hashgraph.go:247-260)
-      if (k == 0) {
-        st(&t.round[d.eo + x], r);
-        t.wit[d.eo + x] = w;
-      }
-      if (k == cr) {
-        rh = r;
-        hid = x;
-      }
-      maxr = max(maxr, r);
-      if (w) {
-        if (r >= d.Rcap) {
-          err = 1;
-          break;
-        }
-        while (top < r) {  // a new round takes the oldest ring slot
-          top++;
-          if (k < N) wid[top % RING][k] = -1;
-          if (k == 0) wpres[top % RING] = 0;
-        }
-        const bool inring = r > top - RING;
-        const int fdk = k < N ? bfd[u][k] : INF;
-        if (k < N) st(&t.WFD[((int64_t)(d.ro + r) * N + cr) * N + k], fdk);
-        if (k == 0) {
-          st(&t.W[(int64_t)(d.ro + r) * N + cr], x);
-          st(&t.WIX[(int64_t)(d.ro + r) * N + cr], ix);
-          t.WCOIN[(int64_t)(d.ro + r) * N + cr] = (uint8_t)rl(cco, u);
-        }
-        if (inring && k < N) wfd[r % RING][cr][k] = fdk;
-        wsync();
-        if (inring && k == 0) {
-          wid[r % RING][cr] = x;
-          wixr[r % RING][cr] = ix;
-          wpres[r % RING] |= 1ull << cr;
-        }
-        wsync();
-        if (r >= 1) {
-          // the vote adjacency: x's strongly-see / see bits over the witnesses of
-          // round r-1 inserted before it (later ones are not its ancestors: bits 0)
-          const bool ring1 = r - 1 <= top && r - 1 > top - RING;
-          const uint64_t ssm = ss_mask(r - 1, lax, ring1);
-          bool see = false;
-          if (k < N) {
-            const int wr = ring1 ? wid[(r - 1) % RING][k] : ld(&t.W[(int64_t)(d.ro + r - 1) * N + k]);
-            const int wix = ring1 ? wixr[(r - 1) % RING][k] : ld(&t.WIX[(int64_t)(d.ro + r - 1) * N + k]);
-            see = wr >= 0 && lax >= wix;
-          }
-          const uint64_t sem = ballot(see);
-          if (k == 0) {
-            t.ssb[(int64_t)(d.ro + r) * N + cr] = ssm;
-            t.seeb[(int64_t)(d.ro + r) * N + cr] = sem;
-          }
-        }
-      }
-      wsync();
-    }
-    wsync();
-  }
-  if (k == 0 && err) t.scal[(int64_t)blockIdx.x * 8 + 6] = 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -713,7 +545,24 @@ __device__ void sort_keys_lds(const BT& t, int64_t eo, int n, uint32_t* kri, int
   }
 }
 
-// ascending bitonic sorting network over M register values (M a power of two)
+// ascending bitonic sorting networks over M register values (M a power of two)
+template <int M>
+__device__ __forceinline__ void sort_regs32(int32_t (&v)[M]) {
+#pragma unroll
+  for (int size = 2; size <= M; size <<= 1)
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1)
+#pragma unroll
+      for (int i = 0; i < M; i++) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool up = (i & size) == 0;
+          const int32_t a = v[i], b = v[j];
+          v[i] = up ? min(a, b) : max(a, b);
+          v[j] = up ? max(a, b) : min(a, b);
+        }
+      }
+}
 template <int M>
 __device__ __forceinline__ void sort_regs(int64_t (&v)[M]) {
 #pragma unroll
@@ -753,8 +602,11 @@ __device__ __forceinline__ void sort_regs(int64_t (&v)[M]) {
 //                   entries move only below its own start), pass 2 takes the median
 //                   timestamps and writes both;
 //   FindOrder       the batch's bitonic sort over the whole workgroup.
-template <int NM>
-__global__ __launch_bounds__(256) void kb_consensus(BT t) {
+// OCC: workgroups per CU the register budget is sized for.  One graph per CU
+// leaves the compiler its 230 VGPRs; with more graphs than two per CU, 4 per CU
+// (128 VGPRs, a few spills) take the whole batch in one pass.
+template <int NM, int OCC>
+__global__ __launch_bounds__(256, OCC) void kb_consensus(BT t) {
   // KB: the LDS sort's capacity, a power of two (the network pads to one)
   constexpr int NWV = 4, RW = 8, UL = 1536, KB = 1024, CPW = 2, NCH = NWV * CPW, SPAN = 64 * NCH;
   const int g = blockIdx.x;
@@ -1151,27 +1003,55 @@ __global__ __launch_bounds__(256) void kb_consensus(BT t) {
               if (w >= 0 && w < n_c && ld(&t.fame[row(found) + dd]) == 1) fm |= 1ull << dd;
             }
           }
-          int64_t vals[NM];
-          int q[NM];
-#pragma unroll
-          for (int dd = 0; dd < NM; dd++)
-            q[dd] = dd < N && ((fm >> dd) & 1) ? FDg[cpos * N + dd] : INF;
+          // the timestamps as int32 offsets from x's own (a register sort of 32-bit
+          // values); an offset outside int32 takes the exact 64-bit count below
+          const int64_t tsx = tschg[cpos];
+          int32_t vals[NM];
           int m = 0;
+          bool ovf = false;
 #pragma unroll
           for (int dd = 0; dd < NM; dd++) {
-            vals[dd] = TS_MAX;
-            if (q[dd] != INF && q[dd] <= WIX_(found, dd)) {
-              vals[dd] = tschg[(int64_t)dd * cc + q[dd]];
+            const int q = dd < N && ((fm >> dd) & 1) ? FDg[cpos * N + dd] : INF;
+            vals[dd] = INT32_MAX;  // fillers sort last (a real INT32_MAX ties with them)
+            if (q != INF && q <= WIX_(found, dd)) {
+              const int64_t o = tschg[(int64_t)dd * cc + q] - tsx;
+              ovf = ovf || o < -(int64_t)INT32_MAX || o > (int64_t)INT32_MAX;
+              vals[dd] = (int32_t)o;
               m++;
             }
           }
-          // the upper median: the m real values sort before the TS_MAX fillers
-          sort_regs<NM>(vals);
-          const int want = m / 2;
+          const int want = m / 2;  // the upper median
           int64_t med = 0;
+          if (!ovf) {
+            sort_regs32<NM>(vals);
 #pragma unroll
-          for (int a = 0; a < NM; a++)
-            if (a == want) med = vals[a];
+            for (int a = 0; a < NM; a++)
+              if (a == want) med = tsx + vals[a];
+          } else {
+            // the value whose rank among the m timestamps covers `want`
+            auto tv = [&](int dd, int64_t& v) -> bool {
+              if (!((fm >> dd) & 1)) return false;
+              const int q = FDg[cpos * N + dd];
+              if (q == INF || q > WIX_(found, dd)) return false;
+              v = tschg[(int64_t)dd * cc + q];
+              return true;
+            };
+            for (int a = 0; a < N; a++) {
+              int64_t va;
+              if (!tv(a, va)) continue;
+              int lt = 0, eq = 0;
+              for (int b = 0; b < N; b++) {
+                int64_t vb;
+                if (!tv(b, vb)) continue;
+                lt += vb < va;
+                eq += vb == va;
+              }
+              if (lt <= want && want < lt + eq) {
+                med = va;
+                break;
+              }
+            }
+          }
           t.rr[eo + x] = found;
           t.cts[eo + x] = med;
           const int p = nb + preR[k] + __popcll(rec & below);
@@ -1306,7 +1186,7 @@ struct Buf {
 }  // namespace
 
 struct hge_batch {
-  int N = 0, SM = 1, device = 0;
+  int N = 0, SM = 1, device = 0, ncu = 256;
   hipStream_t st = nullptr;
   hipEvent_t ev[6] = {};
   std::string err;
@@ -1616,7 +1496,8 @@ struct hge_batch {
       BCHK(hipEventRecord(ev[3], st));
       launch(kb_front<32>, G, t, 1024);
       BCHK(hipEventRecord(ev[4], st));
-      launch(kb_consensus<32>, G, t, 256);
+      if (G > 2 * ncu) launch(kb_consensus<32, 4>, G, t, 256);
+      else launch(kb_consensus<32, 1>, G, t, 256);
     } else {
       launch(kb_coords<64>, G, t);
       BCHK(hipEventRecord(ev[1], st));
@@ -1626,7 +1507,8 @@ struct hge_batch {
       BCHK(hipEventRecord(ev[3], st));
       launch(kb_front<64>, G, t, 1024);
       BCHK(hipEventRecord(ev[4], st));
-      launch(kb_consensus<64>, G, t, 256);
+      if (G > 2 * ncu) launch(kb_consensus<64, 4>, G, t, 256);
+      else launch(kb_consensus<64, 1>, G, t, 256);
     }
     BCHK(hipEventRecord(ev[5], st));
     h_scal.resize((size_t)G * 8);
@@ -1680,6 +1562,7 @@ int hge_batch_create(int32_t n_participants, int32_t device, hge_batch** out) {
   b->device = device;
   try {
     BCHK(hipSetDevice(device));
+    BCHK(hipDeviceGetAttribute(&b->ncu, hipDeviceAttributeMultiprocessorCount, device));
     BCHK(hipStreamCreateWithFlags(&b->st, hipStreamNonBlocking));
     for (auto& e : b->ev) BCHK(hipEventCreate(&e));
   } catch (BatchError& e) {
