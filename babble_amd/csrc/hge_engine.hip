@@ -1376,8 +1376,11 @@ struct hge_engine {
       const int32_t* nostart = nullptr;
       int32_t* nohist = nullptr;
       int hmax = 0, extra = 0;
+      // tests: the walk stalls at this hand-off epoch (chain 0 never publishes it)
+      const char* hs = getenv("HGE_TEST_HANDOFF_STALL");
+      int stall_ep = hs ? atoi(hs) : 0;
       void* dargs[] = {&t, &olen, &len, &rstate, &rlo, &rlo_dev, &Rprev, &gran, &err, &ssc, &mb, &dbg,
-                       &nostart, &nohist, &hmax, &nostart, &extra};
+                       &nostart, &nohist, &hmax, &nostart, &extra, &stall_ep};
       const void* fn = N <= 64 ? (const void*)k_rounds_direct<1024, 64>
                      : N <= 128 ? (const void*)k_rounds_direct<1024, 128>
                                 : (const void*)k_rounds_direct<1024, 256>;
@@ -2720,9 +2723,9 @@ int hge_frontier_walk(hge_engine* h, const int32_t* start, const int32_t* stopcu
   uint64_t* dbg = nullptr;
   const int32_t* st0 = h->s_hstate.p;
   int32_t* hist = h->s_hist.p;
-  int hm = hmax, ex = std::max(0, (int)extra);
+  int hm = hmax, ex = std::max(0, (int)extra), nostall = 0;
   void* args[] = {&t, &olen, &len, &rstate, &rlo, &rlo_dev, &Rprev, &gran, &err, &ssc, &mb, &dbg,
-                  &st0, &hist, &hm, &cut, &ex};
+                  &st0, &hist, &hm, &cut, &ex, &nostall};
   const void* fn = N <= 64 ? (const void*)k_rounds_direct<1024, 64>
                  : N <= 128 ? (const void*)k_rounds_direct<1024, 128>
                             : (const void*)k_rounds_direct<1024, 256>;

@@ -427,13 +427,16 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
                                                       int Rprev, uint64_t* gran,
                                                       int32_t* err, uint64_t* ssc, uint32_t* mbuf,
                                                       uint64_t* dbg, const int32_t* start, int32_t* hist,
-                                                      int hmax, const int32_t* stopcut, int extra) {
+                                                      int hmax, const int32_t* stopcut, int extra, int stall_ep) {
   // History mode (hist != nullptr; a walker of the cross-GPU split, babble_amd/dist.py):
   // the walk starts at the frontier `start` (rlo = 0, Rprev = 0), writes frontier
   // row j to hist[j * N + c] instead of C, the ssc bits of row j to ssc row j, and
   // stops after row hmax - 1 (rstate[1] = 1), `extra` rows after its frontier
   // first reached stopcut on every chain (the next walker's start; rstate[1] = 2),
   // or at the empty frontier; rstate[0] = rows written.
+  // stall_ep > 0 (tests, HGE_TEST_HANDOFF_STALL): at hand-off epoch stall_ep chain 0
+  // does not publish and every workgroup gives up at once, as on a timed-out poll, so
+  // the other chains' rows of that round are written and chain 0's is not.
   using G = DirGeo<BS, NPOW>;
   // rlo_dev: the first round to recompute, read here (INF32: nothing to do)
   if (rlo_dev) {
@@ -523,7 +526,8 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
     if (stamping) st_acc[6] += slot;
     // publish C_{r+1}[c]: wave 0 stages the next member row, drains its stores,
     // then lane 0 stores the granule
-    if (tid < 64) {
+    const bool stall = stall_ep > 0 && r - rlo + 1 == stall_ep;
+    if (tid < 64 && !(stall && c == 0)) {
       dir_stage_member<BS, NPOW>(t, mbp[(r + 1) & 1], c, nxt);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (tid == 0) {
@@ -593,7 +597,7 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
           P = (int)(uint32_t)x;
         }
         if (__all(ok)) break;
-        if (++spins > (1u << 21)) {  // never a normal wait (~2 s): co-residency failure
+        if (stall || ++spins > (1u << 21)) {  // never a normal wait (~2 s): co-residency failure
           fail = true;
           break;
         }
@@ -640,10 +644,10 @@ __global__ void __launch_bounds__(BS, 4) k_rounds_direct(Tables t, const int32_t
 }
 
 template __global__ void k_rounds_direct<1024, 64>(Tables, const int32_t*, const int32_t*, int32_t*, int, const int32_t*, int,
-    uint64_t*, int32_t*, uint64_t*, uint32_t*, uint64_t*, const int32_t*, int32_t*, int, const int32_t*, int);
+    uint64_t*, int32_t*, uint64_t*, uint32_t*, uint64_t*, const int32_t*, int32_t*, int, const int32_t*, int, int);
 template __global__ void k_rounds_direct<1024, 128>(Tables, const int32_t*, const int32_t*, int32_t*, int, const int32_t*, int,
-    uint64_t*, int32_t*, uint64_t*, uint32_t*, uint64_t*, const int32_t*, int32_t*, int, const int32_t*, int);
+    uint64_t*, int32_t*, uint64_t*, uint32_t*, uint64_t*, const int32_t*, int32_t*, int, const int32_t*, int, int);
 template __global__ void k_rounds_direct<1024, 256>(Tables, const int32_t*, const int32_t*, int32_t*, int, const int32_t*, int,
-    uint64_t*, int32_t*, uint64_t*, uint32_t*, uint64_t*, const int32_t*, int32_t*, int, const int32_t*, int);
+    uint64_t*, int32_t*, uint64_t*, uint32_t*, uint64_t*, const int32_t*, int32_t*, int, const int32_t*, int, int);
 
 }  // namespace hge

@@ -123,10 +123,21 @@ func (s *InmemStore) CacheSize() int {
 	return s.cacheSize
 }
 
+// GetEvent (inmem_store.go:42-49).  On its own the store answers as the
+// reference's eventCache does, an LRU of cacheSize events: a key evicted from it
+// (every key at size 0) is not found, and a lookup refreshes it (common/lru.go
+// Get), so the SetEvent that follows appends it to its creator's list again.
+// Bound, every event the engine holds is found.
 func (s *InmemStore) GetEvent(key string) (Event, error) {
 	ev, ok := s.events[key]
 	if !ok {
 		return Event{}, ErrKeyNotFound
+	}
+	if !s.bound() {
+		k, known := s.keys[key]
+		if !known || C.hge_store_has_event(s.st, C.int64_t(k)) == 0 {
+			return Event{}, ErrKeyNotFound
+		}
 	}
 	return ev, nil
 }

@@ -34,7 +34,7 @@ for s in "$@"; do
          tail -3 gpurun_out/r05/gpu.log ;;
     batch) timeout -k 10 600 $PYT -m gpu tests/test_gpu_batch.py > gpurun_out/r05/batch.log 2>&1 || { tail -60 gpurun_out/r05/batch.log; exit 1; }
          tail -3 gpurun_out/r05/batch.log ;;
-    fallback) timeout -k 10 400 $PYT -m gpu tests/test_gpu_wide.py tests/test_gpu_split.py -k "handoff or nccl_world" > gpurun_out/r05/fallback.log 2>&1 || { tail -40 gpurun_out/r05/fallback.log; exit 1; }
+    fallback) timeout -k 10 400 $PYT -m gpu tests/test_gpu_wide.py tests/test_gpu_split.py -k "handoff or nccl_world or stall" > gpurun_out/r05/fallback.log 2>&1 || { tail -40 gpurun_out/r05/fallback.log; exit 1; }
          tail -3 gpurun_out/r05/fallback.log ;;
     stamps) HGB_STAMPS=1 timeout -k 10 300 python -u bench.py --workload mc --no-cpu-baseline --steps 2 --warmup 1 --ramp-s 0 > gpurun_out/r05/stamps.json 2> gpurun_out/r05/stamps.err || { tail -20 gpurun_out/r05/stamps.err; exit 2; }
          grep "hgb stamps" gpurun_out/r05/stamps.err | tail -1 ;;

@@ -107,6 +107,10 @@ struct InmemStore {
   Err GetEvent(const std::string& k, Event& out) const {
     auto it = events.find(k);
     if (it == events.end()) return ErrKeyNotFound;
+    if (!bound()) {  // the eventCache LRU answers (evicted: not found; a hit refreshes)
+      auto kt = keys.find(k);
+      if (kt == keys.end() || !hge_store_has_event(st, kt->second)) return ErrKeyNotFound;
+    }
     out = it->second;
     return OK;
   }
@@ -554,9 +558,53 @@ static int gpu_checks() {
   return failures;
 }
 
+// GetEvent / SetEvent of a standalone store against the reference's eventCache
+// (inmem_store.go:42-64, common/lru.go): with cacheSize 2 the oldest of three events
+// is evicted, so GetEvent misses it and its next SetEvent appends it to the
+// creator's list again, while a GetEvent hit refreshes its key; with cacheSize 0
+// nothing is kept and every SetEvent appends.
+static void lru_checks() {
+  std::map<std::string, int> parts;
+  parts[pub(0)] = 0;
+  {
+    InmemStore store(parts, 2);
+    Event ev[3];
+    for (int i = 0; i < 3; i++) {
+      ev[i].creator = pub(0);
+      ev[i].hex = hexOf("lru:" + std::to_string(i));
+      CHECK(store.SetEvent(ev[i]) == OK);
+    }
+    Event got;
+    CHECK(store.GetEvent(ev[0].hex, got) == ErrKeyNotFound);  // evicted by ev[2]
+    CHECK(store.GetEvent(ev[2].hex, got) == OK && got.hex == ev[2].hex);
+    CHECK(store.GetEvent(ev[1].hex, got) == OK);  // refreshes ev[1]: ev[2] is now the oldest
+    CHECK(store.SetEvent(ev[0]) == OK);           // a miss: appended again, evicts ev[2]
+    CHECK(store.GetEvent(ev[2].hex, got) == ErrKeyNotFound);
+    CHECK(store.GetEvent(ev[1].hex, got) == OK);
+    CHECK(store.SetEvent(ev[1]) == OK);  // a hit: not appended
+    std::vector<std::string> pe;
+    CHECK(store.ParticipantEvents(pub(0), 0, pe) == OK);
+    CHECK(pe.size() == 4);
+    if (pe.size() == 4) CHECK(pe[0] == ev[0].hex && pe[1] == ev[1].hex && pe[2] == ev[2].hex && pe[3] == ev[0].hex);
+  }
+  {
+    InmemStore store(parts, 0);
+    Event e;
+    e.creator = pub(0);
+    e.hex = hexOf("lru0");
+    CHECK(store.SetEvent(e) == OK);
+    Event got;
+    CHECK(store.GetEvent(e.hex, got) == ErrKeyNotFound);
+    CHECK(store.SetEvent(e) == OK);
+    std::map<int, int> known = store.Known();
+    CHECK(known[0] == 2);
+  }
+}
+
 int main(int argc, char** argv) {
   const bool gpu = argc > 1 && !strcmp(argv[1], "--gpu");
   store_checks();
+  lru_checks();
   if (gpu) gpu_checks();
   printf("%s: %d failures\n", gpu ? "shim replay (store + engine)" : "shim replay (store)", failures);
   return failures ? 1 : 0;

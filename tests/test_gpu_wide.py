@@ -254,3 +254,20 @@ def test_handoff_timeout_online_path(monkeypatch):
     finally:
         a.close()
         b.close()
+
+
+@pytest.mark.parametrize("n,events,k,epoch", [(64, 4000, 16, 3), (128, 6000, 1, 2)])
+def test_handoff_stall_mid_walk(n, events, k, epoch, monkeypatch):
+    """A walk that gives up part-way (HGE_TEST_HANDOFF_STALL: at hand-off `epoch`
+    chain 0 never publishes and every workgroup stops as on a timed-out poll), so
+    that round's row is written for every chain but chain 0: the launch-per-round
+    walk takes over from the rows as left (kept rows stand, missing ones are
+    computed) and the results equal the oracle's."""
+    from babble_amd.engine import Engine
+    monkeypatch.setenv("HGE_TEST_HANDOFF_STALL", str(epoch))
+    eng = Engine(n, 1 << 14)
+    try:
+        run_case(eng, random_gossip(n, events, seed=950 + n), k)
+        assert eng.frontier_fallbacks() == 1
+    finally:
+        eng.close()
