@@ -513,7 +513,57 @@ __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const FT* FDT
   const int ts0 = tlo ? tlo[a] : 0, ts1 = thi ? thi[a] : pend;
   const int c0 = by * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
-  for (int p0 = plo[a] + bz * 64; p0 < pend; p0 += gridDim.z * 64) {
+  // uint16 runs: tiles start at a multiple of 4 positions, so a lane reads 4 of them
+  // with one 8-byte load (the rows below plo it re-writes hold their final values)
+  const int pb = sizeof(FT) == 2 ? (plo[a] & ~3) : plo[a];
+  for (int p0 = pb + bz * 64; p0 < pend; p0 += gridDim.z * 64) {
+    if constexpr (sizeof(FT) == 2) {
+      // read phase: thread i takes row jj = c0 + (i >> 4) + 16 h, positions
+      // p0 + 4 (i & 15) .. + 3 (16 lanes per 128-byte row segment, 4 rows per wave)
+      __shared__ int64_t s_own[64];
+      if (threadIdx.x < 64) s_own[threadIdx.x] = t.tsch[(size_t)a * ccap + min(p0 + (int)threadIdx.x, pend - 1)];
+      const int qd = threadIdx.x & 15, r0 = threadIdx.x >> 4;
+      uint2 w[4];
+#pragma unroll
+      for (int h = 0; h < 4; h++) {
+        const int jj = c0 + r0 + 16 * h, q = p0 + 4 * qd;
+        w[h] = (jj < N && q < pend) ? *(const uint2*)(FDT + ((size_t)jj * N + a) * ccap + q) : make_uint2(~0u, ~0u);
+      }
+      int kv[16];
+#pragma unroll
+      for (int h = 0; h < 4; h++) {
+        const uint32_t lo = w[h].x, hi = w[h].y;
+        const uint32_t u[4] = {lo & 0xFFFFu, lo >> 16, hi & 0xFFFFu, hi >> 16};
+#pragma unroll
+        for (int e = 0; e < 4; e++) kv[4 * h + e] = (u[e] == 0xFFFFu || p0 + 4 * qd + e >= pend) ? INF32 : (int)u[e];
+      }
+      int64_t tv[16];
+#pragma unroll
+      for (int h = 0; h < 4; h++) {
+        const int jj = c0 + r0 + 16 * h;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          const int qq = p0 + 4 * qd + e;
+          const bool tson = qq >= ts0 && qq < ts1;
+          tv[4 * h + e] = tson && kv[4 * h + e] != INF32 ? t.tsch[(size_t)(jj < N ? jj : 0) * ccap + kv[4 * h + e]] : 0;
+        }
+      }
+      __syncthreads();  // s_own
+#pragma unroll
+      for (int h = 0; h < 4; h++) {
+        const int r = r0 + 16 * h;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          const int col = 4 * qd + e;
+          const int k = kv[4 * h + e];
+          const int qq = p0 + col;
+          tile[r][col] = k;
+          const int64_t dlt = tv[4 * h + e] - s_own[col];
+          const bool esc = dlt < -(int64_t)INT32_MAX || dlt > (int64_t)INT32_MAX;
+          toff[r][col] = (k == INF32 || qq < ts0 || qq >= ts1) ? 0 : (esc ? INT32_MIN : (int32_t)dlt);
+        }
+      }
+    } else {
     // read phase: lane tx walks row q = p0 + tx (its own timestamp is one load), all
     // 16 FDT loads of a thread in flight, then all 16 timestamp gathers
     const int64_t own = t.tsch[(size_t)a * ccap + min(p0 + tx, pend - 1)];
@@ -549,6 +599,7 @@ __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const FT* FDT
         toff[ty + 4 * (h + i)][tx] = kv[i] == INF32 ? 0 : (esc ? INT32_MIN : (int32_t)d);
       }
     }
+    }
     __syncthreads();
     const int NT = (N + 63) >> 6;
     for (int r = ty; r < 64; r += 4) {  // wave ty writes rows r: the 64 columns of one row each time
@@ -570,6 +621,12 @@ __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const FT* FDT
     }
     __syncthreads();
   }
+}
+
+// the uint16 run table widened to int32 (0xFFFF -> INF32) at the switch to int32 positions
+__global__ void k_fdt16_to32(const uint16_t* src, int32_t* dst, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = src[i] == 0xFFFFu ? INF32 : (int32_t)src[i];
 }
 
 __global__ void __launch_bounds__(256) k_fd_qlo(Tables t, const int32_t* olen, const int32_t* len, int32_t* qlo) {

@@ -164,6 +164,7 @@ struct hge_engine {
   // coordinate sweeps: transposed tables and scratch
   int n_sweeps = 0;
   DBuf<int32_t> d_FDT, s_chg, s_bar, s_dirty;
+  DBuf<int32_t> s_src;  // hge_consensus_timestamp_sources: ids, then their sources
   // windowed lastAncestors (hge_coords_win.hip): chunk plans, row sums, starting rows
   DBuf<int4> s_lwplan;
   DBuf<uint32_t> s_lwsum, s_lwinit;
@@ -356,7 +357,7 @@ struct hge_engine {
                              &s_und2,    &s_part,   &s_fst,    &d_FSS,
                              &d_FDT,     &s_chg,    &s_bar,   &s_bseg,   &s_kctl,    &s_cctl,
                              &s_out,     &s_hn,     &s_hres,  &s_dirty,  &d_WLA,     &s_lwpos,
-                             &s_lwrisky};
+                             &s_lwrisky, &s_src};
     for (auto* b : i32s) b->free_();
     s_lwplan.free_();
     d_WLR.free_();
@@ -442,7 +443,8 @@ struct hge_engine {
 
   void ensure_ccap(int64_t m) {
     if (m <= ccap) return;
-    int64_t nc = std::max<int64_t>(m, (int64_t)ccap + ccap / 2);
+    // a multiple of 64 positions: the uint16 run table's rows stay 8-byte aligned
+    int64_t nc = (std::max<int64_t>(m, (int64_t)ccap + ccap / 2) + 63) & ~(int64_t)63;
     int32_t* chain = nullptr;
     HIPCHK(hipMalloc(&chain, sizeof(int32_t) * N * nc));
     HIPCHK(hipMemsetAsync(chain, 0xFF, sizeof(int32_t) * N * nc, st));
@@ -501,7 +503,19 @@ struct hge_engine {
     // first-strong-seer rows (N <= 32): int32 rows of N, or uint16 rows padded to
     // 16/32 columns for the LDS walk; rebuilt from the frontier on, never kept
     if (N <= 32) d_FSS.need((size_t)N * nc * std::max(N, 16));
-    grow_chain_table(d_FDT, nc, true, false);  // persistent: FD in run layout
+    if (fdt16()) {  // uint16 runs: rows of ccap halves (the buffer keeps int32 capacity)
+      int32_t* q = nullptr;
+      HIPCHK(hipMalloc(&q, sizeof(int32_t) * (size_t)N * nc * N));
+      if (ccap > 0 && d_FDT.p)
+        HIPCHK(hipMemcpy2DAsync(q, 2 * (size_t)nc, d_FDT.p, 2 * (size_t)ccap, 2 * (size_t)ccap, (size_t)N * N,
+                                hipMemcpyDeviceToDevice, st));
+      sync();
+      d_FDT.free_();
+      d_FDT.p = q;
+      d_FDT.n = (size_t)N * nc * N;
+    } else {
+      grow_chain_table(d_FDT, nc, true, false);  // persistent: FD in run layout
+    }
     ccap = (int)nc;
   }
 
@@ -1417,6 +1431,17 @@ struct hge_engine {
   // engine refusing every later step (the packed tables can no longer hold the
   // positions) instead of packing positions past 65,534 into uint16.
   void to_wide32() {
+    if (fdt16()) {  // the runs continue in int32 from here: widen the kept uint16 ones
+      int32_t* q = nullptr;
+      const size_t n = (size_t)N * N * ccap;
+      HIPCHK(hipMalloc(&q, sizeof(int32_t) * n));
+      KLAUNCH(k_fdt16_to32, dim3((unsigned)std::min<size_t>(div_up(n, 256), 65536)), dim3(256), 0, st,
+              (const uint16_t*)d_FDT.p, q, n);
+      sync();
+      d_FDT.free_();
+      d_FDT.p = q;
+      d_FDT.n = n;
+    }
     grow_chain_table(d_LA, ccap, false);
     s_w32.need(N);
     h2d(s_w32.p, coords_len.data(), 4 * (size_t)N);
@@ -1463,6 +1488,16 @@ struct hge_engine {
       }
     }
   }
+
+  // N > 128, N % 4 == 0, uint16 positions: the FDT runs as uint16 (k_la16_rows_runs<uint16_t>,
+  // k_fd_transpose_ts<uint16_t>: half the run table's bytes written and read).  Neither the
+  // direct walk nor theta reads FDT; the speculative walkers (N <= 128) and the
+  // FDT-gather walk (N % 4 != 0) read int32 runs.
+#ifdef HGE_AB_NO_FDT16  // A/B builds: int32 runs throughout
+  bool fdt16() const { return false; }
+#else
+  bool fdt16() const { return N > 128 && (N & 3) == 0 && !wide32; }
+#endif
 
   // 32 < N <= 256: lastAncestors by windowed exact propagation (hge_coords_win.hip)
   // instead of the sweeps
@@ -1618,7 +1653,10 @@ struct hge_engine {
       }
     }
     }
-    if (p16) {
+    if (fdt16()) {
+      KLAUNCH((k_la16_rows_runs<uint16_t>), dim3(div_up(maxnew + 1, 64), div_up(N, 64), N), dim3(256), 0, st, t,
+              (uint16_t*)d_FDT.p, k_plo, olen, len);
+    } else if (p16) {
       // LA16 -> the int32 LA rows and the FDT runs from the same tiles (no LAT)
       KLAUNCH((k_la16_rows_runs<int32_t>), dim3(div_up(maxnew + 1, 64), div_up(N, 64), N), dim3(256), 0, st, t,
               d_FDT.p, k_plo, olen, len);
@@ -1642,7 +1680,11 @@ struct hge_engine {
       for (int c = 0; c < N; c++) span = std::max(span, chain_len[c]);
     }
     // (a split part writes the timestamp rows of its own candidates only)
-    if (N > 16)
+    if (fdt16())
+      KLAUNCH((k_fd_transpose_ts<uint16_t>), dim3(N, div_up(N, 64), std::min(div_up(span, 64), 65535)), dim3(256),
+              0, st, t, (const uint16_t*)d_FDT.p, k_qlo, len, (const int32_t*)k_fd,
+              (const int32_t*)(k_fd ? k_fd + N : nullptr));
+    else if (N > 16)
       KLAUNCH((k_fd_transpose_ts<int32_t>), dim3(N, div_up(N, 64), std::min(div_up(span, 64), 65535)), dim3(256),
               0, st, t, (const int32_t*)d_FDT.p, k_qlo, len, (const int32_t*)k_fd,
               (const int32_t*)(k_fd ? k_fd + N : nullptr));
@@ -3117,6 +3159,24 @@ int hge_event_received(hge_engine* h, int32_t* rr_out, int64_t* cts_out, int64_t
   if (m > 0 && rr_out) h->d2h(rr_out, h->d_rr.p, 4 * (size_t)m);
   if (m > 0 && cts_out) h->d2h(cts_out, h->d_cts.p, 8 * (size_t)m);
   h->sync();
+  return HGE_OK;
+  GUARD_END(h)
+}
+
+int hge_consensus_timestamp_sources(hge_engine* h, const int32_t* ids, int64_t n, int32_t* src_out) {
+  if (!h || n < 0 || (n > 0 && (!ids || !src_out))) return HGE_ERR_ARG;
+  GUARD_BEGIN
+  if (n == 0) return HGE_OK;
+  for (int64_t i = 0; i < n; i++)
+    if (ids[i] < 0 || ids[i] >= h->n_events) throw EngineError(HGE_ERR_ARG, "hge_consensus_timestamp_sources: unknown id");
+  h->s_src.need((size_t)n * 2);
+  h->h2d(h->s_src.p, ids, 4 * (size_t)n);
+  hipLaunchKernelGGL(k_cts_source, dim3((unsigned)div_up(n, 4)), dim3(256), 0, h->st, h->tables(),
+                     (const int32_t*)h->s_src.p, (int)n, (const int32_t*)h->d_rr.p, (const int64_t*)h->d_cts.p,
+                     h->s_src.p + n);
+  const hipError_t le = hipGetLastError();
+  if (le != hipSuccess) throw EngineError(HGE_ERR_DEVICE, std::string("launch k_cts_source: ") + hipGetErrorString(le));
+  h->readback(src_out, h->s_src.p + n, (size_t)n);
   return HGE_OK;
   GUARD_END(h)
 }

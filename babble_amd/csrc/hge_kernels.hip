@@ -2905,4 +2905,46 @@ __global__ void k_reset_rounds(Tables t, int64_t nrow, int64_t nbits, int64_t ne
     t.rcnt[i] = 0;
 }
 
+// ---------------------------------------------------------------------------
+// MedianTimestamp's source (hashgraph.go:762-770): the event whose Body.Timestamp
+// becomes x's consensus timestamp.  The candidates are OldestSelfAncestorToSee(w, x)
+// = (d, FD[x][d]) for the famous witnesses w = W[rr][d] of x's round received that
+// see x (hashgraph.go:704-709); the source is one whose timestamp is the median.
+// Several may share that instant in different zones: Go's sort.Sort over a list
+// built in map order leaves which one lands at len/2 unspecified, and the lowest
+// creator d is returned here.  Fame of a round at or below LastConsensusRound is
+// final, so the persisted fame table gives the set the median used.  One wave per
+// event, lane = d; -1 for an event with no round received.
+__global__ void __launch_bounds__(256) k_cts_source(Tables t, const int32_t* ids, int n, const int32_t* rr,
+                                                    const int64_t* cts, int32_t* out) {
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (q >= n) return;  // wave-uniform
+  const int x = ids[q];
+  const int r = rr[x];
+  int src = -1;
+  if (r >= 0) {
+    const int cx = t.creator[x], ix = t.index[x];
+    const int64_t c = cts[x];
+    for (int d0 = 0; d0 < t.N; d0 += 64) {
+      const int d = d0 + lane;
+      bool hit = false;
+      int p = 0;
+      if (d < t.N) {
+        const int w = t.W[(size_t)r * t.N + d];
+        if (w >= 0 && t.fame[(size_t)r * t.N + d] == 1 && la_at(t, d, t.index[w], cx) >= ix) {
+          p = t.FD[rowoff(t, cx, ix) + d];
+          hit = p != INF32 && t.tsch[(size_t)d * t.ccap + p] == c;
+        }
+      }
+      const uint64_t b = __ballot(hit);
+      if (b) {
+        const int l = __ffsll((unsigned long long)b) - 1;
+        src = t.chain[(size_t)(d0 + l) * t.ccap + __shfl(p, l)];
+        break;
+      }
+    }
+  }
+  if (lane == 0) out[q] = src;
+}
+
 }  // namespace hge

@@ -71,6 +71,7 @@ EXPORTS = [
     "hge_consensus_transactions", "hge_consensus_count", "hge_consensus_events",
     "hge_undetermined", "hge_known", "hge_round_of", "hge_is_witness", "hge_round_witness",
     "hge_fame", "hge_round_events", "hge_round_received", "hge_consensus_timestamp",
+    "hge_consensus_timestamp_sources",
     "hge_ancestor", "hge_self_ancestor", "hge_see", "hge_strongly_see",
     "hge_oldest_self_ancestor_to_see", "hge_coordinates", "hge_coordinate_sweeps", "hge_host_syncs", "hge_frontier_fallbacks",
     "hge_stage_times",
@@ -179,6 +180,7 @@ def lib():
     L.hge_consensus_log.restype = i64
     L.hge_event_rounds.argtypes = [vp, P(i32), P(ctypes.c_uint8), i64]
     L.hge_event_received.argtypes = [vp, P(i32), P(i64), i64]
+    L.hge_consensus_timestamp_sources.argtypes = [vp, P(i32), i64, P(i32)]
     L.hge_fame_table.argtypes = [vp, i32, P(ctypes.c_int8)]
     L.hge_fame_table.restype = i32
     L.hge_set_cache_size.argtypes = [vp, i64]
@@ -759,6 +761,15 @@ class Engine:
         cts = np.zeros(max(m, 1), np.int64)
         self._check(self.L.hge_event_received(self.h, _p32(rr), _p64(cts), m))
         return rr[:m], cts[:m]
+
+    def consensus_timestamp_sources(self, ids):
+        """For each id, the event whose timestamp is its consensus timestamp
+        (MedianTimestamp's source, hge_consensus_timestamp_sources; -1: not received)."""
+        ids = np.ascontiguousarray(ids, np.int32)
+        out = np.zeros(max(len(ids), 1), np.int32)
+        if len(ids):
+            self._check(self.L.hge_consensus_timestamp_sources(self.h, _p32(ids), len(ids), _p32(out)))
+        return out[:len(ids)]
 
     def round_event_ids(self, r):
         """Every event of round r (insertion order) and its witness flag (hge_round_event_ids)."""

@@ -48,10 +48,6 @@ type Hashgraph struct {
 
 	eng   *C.hge_engine
 	store *InmemStore // the engine-backed store (owns the hash <-> id maps)
-	// the Body.Timestamp of an inserted event per instant (UnixNano): a consensus
-	// timestamp is one of them (MedianTimestamp returns a source event's Time,
-	// hashgraph.go:762-770), so FindOrder hands back that Time value, zone included
-	tsByNano map[int64]time.Time
 
 	logger *logrus.Logger
 }
@@ -79,7 +75,6 @@ func NewHashgraph(participants map[string]int, store Store, commitCh chan []Even
 		commitCh:            commitCh,
 		store:               s,
 		logger:              logger,
-		tsByNano:            make(map[int64]time.Time),
 	}
 	capacity := C.int64_t(s.cacheSize)
 	if capacity < 1<<16 {
@@ -252,9 +247,6 @@ func (h *Hashgraph) insert(event *Event) error {
 	}
 	hex := event.Hex()
 	h.store.remember(hex, status)
-	if _, seen := h.tsByNano[int64(ev.timestamp_ns)]; !seen {
-		h.tsByNano[int64(ev.timestamp_ns)] = event.Body.Timestamp
-	}
 	if err := h.SetWireInfo(event); err != nil {
 		return err
 	}
@@ -420,20 +412,25 @@ func (h *Hashgraph) FindOrder() error {
 	batch := make([]Event, 0, int(n))
 	if n > 0 {
 		ids := make([]C.int32_t, int(n))
+		srcs := make([]C.int32_t, int(n))
 		C.hge_consensus_log(h.eng, C.int64_t(from), &ids[0], n)
-		for _, id := range ids {
+		// MedianTimestamp returns the source event's own Body.Timestamp
+		// (hashgraph.go:762-770): its location too, not only the instant
+		if C.hge_consensus_timestamp_sources(h.eng, &ids[0], n, &srcs[0]) != C.HGE_OK {
+			return h.engineErr()
+		}
+		for q, id := range ids {
 			hex := h.store.hash(id)
 			ev, err := h.Store.GetEvent(hex)
 			if err != nil {
 				return err
 			}
-			ev.SetRoundReceived(int(C.hge_round_received(h.eng, id)))
-			cts := int64(C.hge_consensus_timestamp(h.eng, id))
-			if t, ok := h.tsByNano[cts]; ok {
-				ev.consensusTimestamp = t // the source event's Time (location included)
-			} else {
-				ev.consensusTimestamp = time.Unix(0, cts)
+			src, err := h.Store.GetEvent(h.store.hash(srcs[q]))
+			if err != nil {
+				return err
 			}
+			ev.SetRoundReceived(int(C.hge_round_received(h.eng, id)))
+			ev.consensusTimestamp = src.Body.Timestamp
 			h.store.events[hex] = ev
 			batch = append(batch, ev)
 		}

@@ -280,6 +280,14 @@ int hge_round_event_ids(hge_engine* h, int32_t round, int32_t* ids_out, uint8_t*
                         int64_t* n_out);
 int32_t hge_round_received(hge_engine* h, int32_t id);           /* -1 = nil */
 int64_t hge_consensus_timestamp(hge_engine* h, int32_t id);
+/* MedianTimestamp's source (hashgraph.go:762-770: events[len(events)/2].Body.Timestamp):
+ * for each id, the id of the event whose Body.Timestamp is its consensus timestamp --
+ * OldestSelfAncestorToSee(w, x) for a famous witness w of x's round received that
+ * sees x, at the median instant -- so a caller returns that event's own time.Time
+ * (its zone included).  Among candidates sharing the instant the lowest creator is
+ * chosen (the reference's sort.Sort over a map-ordered list leaves it unspecified).
+ * -1 for an id with no round received. */
+int hge_consensus_timestamp_sources(hge_engine* h, const int32_t* ids, int64_t n, int32_t* src_out);
 
 /* Bulk reads for ids [0, min(cap, hge_event_count)): Round/Witness of every
  * event (DivideRounds state), and RoundReceived (-1 = nil) / consensus timestamp. */

@@ -103,6 +103,18 @@ d=json.loads(open('gpurun_out/r05/bench_mc128.json').read().strip().splitlines()
 print('mc128', round(d['value']/1e6,2), d['ms_per_step'], d['parity']); print(d['kernels_ms_per_replay'])" ;;
     stamps128) HGB_STAMPS=1 timeout -k 10 300 python -u bench.py --workload mc --graphs 128 --no-cpu-baseline --steps 2 --warmup 1 --ramp-s 0 > gpurun_out/r05/stamps128.json 2> gpurun_out/r05/stamps128.err || { tail -20 gpurun_out/r05/stamps128.err; exit 2; }
          grep "hgb stamps" gpurun_out/r05/stamps128.err | tail -1 ;;
+    trace) timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/r05/trace -o run -- python -u bench.py --no-secondary --no-cpu-baseline --steps 1 --warmup 0 --ramp-s 0 --profile-steps 1 > gpurun_out/r05/trace.log 2>&1 || { tail -20 gpurun_out/r05/trace.log; exit 3; }
+          python scripts/analysis/gaps.py gpurun_out/r05/trace > gpurun_out/r05/gaps.txt && head -40 gpurun_out/r05/gaps.txt
+          find gpurun_out/r05/trace -name "*.db" -delete ;;
+    abenv) for v in 0 1 0 1; do
+           if [ $v = 1 ]; then export $ABVAR=1; else unset $ABVAR; fi
+           timeout -k 10 300 python -u bench.py --no-secondary --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/r05/ab_${ABVAR}_$v.json 2> gpurun_out/r05/ab_${ABVAR}_$v.err || { tail -5 gpurun_out/r05/ab_${ABVAR}_$v.err; exit 2; }
+           python -c "
+import json
+d=json.loads(open('gpurun_out/r05/ab_${ABVAR}_$v.json').read().strip().splitlines()[-1])
+k=d['kernels_ms_per_replay']
+print('$ABVAR=$v', round(d['value']/1e6,2), d['ms_per_step'], {n: k[n] for n in k if 'median' in n or 'rows_runs' in n or 'transpose' in n or 'rounds_direct' in n}, d['parity'][:60])"
+         done; unset $ABVAR ;;
     prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r05/prof -o run -- python -u bench.py --no-secondary --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/r05/prof.log 2>&1 || { tail -20 gpurun_out/r05/prof.log; exit 3; }
           find gpurun_out/r05/prof -name "*kernel_trace.csv" -delete; find gpurun_out/r05/prof -name "*kernel_stats.csv" | head -1 | xargs head -12 ;;
     profmc) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r05/profmc -o run -- python -u bench.py --workload mc --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/r05/profmc.log 2>&1 || { tail -20 gpurun_out/r05/profmc.log; exit 3; }

@@ -9,9 +9,10 @@
 //     SetRound copy's entries added only for hashes the engine does not know
 //     (a copy must not hide fame decided after the SetRound);
 //   * FindOrder: the batch as the tail of the consensus log, round received, and
-//     the consensus timestamp handed back as the source event's Time found by
-//     its instant (tsByNano: UnixNano -> the first Body.Timestamp seen, zone
-//     included).
+//     the consensus timestamp handed back as the median's source event's own Time
+//     (hge_consensus_timestamp_sources: MedianTimestamp returns
+//     events[len/2].Body.Timestamp, hashgraph.go:762-770), zone included -- also
+//     when several events share the instant in different zones.
 // Each class mirrors one Go type method by method (names kept); a Time is
 // (UnixNano, zone tag) since only those two fields matter to the lookup.
 //
@@ -293,7 +294,6 @@ struct Hashgraph {
   InmemStore* store;
   std::vector<std::string> UndeterminedEvents;
   int LastConsensusRound = -1;
-  std::map<int64_t, Time> tsByNano;
   std::vector<std::vector<Event>> commits;  // what commitCh received
   hge_engine* eng = nullptr;
 
@@ -325,7 +325,6 @@ struct Hashgraph {
     int64_t accepted = 0;
     if (hge_insert_events(eng, &ev, 1, &status, &accepted) != HGE_OK) return ErrOther;
     store->remember(event.hex, status);
-    if (!tsByNano.count(ev.timestamp_ns)) tsByNano[ev.timestamp_ns] = event.ts;
     if (Err e = store->SetEvent(event)) return e;
     UndeterminedEvents.push_back(event.hex);
     return OK;
@@ -343,16 +342,16 @@ struct Hashgraph {
     const int64_t total = hge_consensus_count(eng), from = total - n;
     std::vector<Event> batch;
     if (n > 0) {
-      std::vector<int32_t> is(n);
+      std::vector<int32_t> is(n), src(n);
       hge_consensus_log(eng, from, is.data(), n);
-      for (int32_t id : is) {
-        const std::string hex = store->hash(id);
-        Event ev;
+      if (hge_consensus_timestamp_sources(eng, is.data(), n, src.data()) != HGE_OK) return ErrOther;
+      for (int64_t q = 0; q < n; q++) {
+        const std::string hex = store->hash(is[q]);
+        Event ev, sev;
         if (Err e = store->GetEvent(hex, ev)) return e;
-        ev.round_received = hge_round_received(eng, id);
-        const int64_t cts = hge_consensus_timestamp(eng, id);
-        auto t = tsByNano.find(cts);
-        ev.consensus_ts = t != tsByNano.end() ? t->second : Time{cts, -1};
+        if (Err e = store->GetEvent(store->hash(src[q]), sev)) return e;
+        ev.round_received = hge_round_received(eng, is[q]);
+        ev.consensus_ts = sev.ts;  // the source event's Body.Timestamp, zone included
         store->events[hex] = ev;
         batch.push_back(ev);
       }
@@ -601,11 +600,62 @@ static void lru_checks() {
   }
 }
 
+// The same DAG with every event at ONE instant in its own zone: every consensus
+// timestamp is that instant, and its zone must be the median source's -- the
+// OldestSelfAncestorToSee(w, x) of the lowest-creator famous witness w of x's round
+// received that sees x (ties at the median instant resolve to the lowest creator) --
+// not the zone of whichever event showed that instant first (round 4's tsByNano).
+static void shared_instant_checks() {
+  std::map<std::string, int> parts;
+  for (int i = 0; i < 3; i++) parts[pub(i)] = i;
+  InmemStore store(parts, 1000);
+  Hashgraph h(parts, &store);
+  const int64_t T = 1500000000000000000LL;
+  std::map<int32_t, int> zone_of;  // engine id -> zone
+  int seq[3] = {0, 0, 0};
+  for (int i = 0; i < kE; i++) {
+    Event ev;
+    ev.creator = pub(kDag[i].creator);
+    ev.index = seq[kDag[i].creator]++;
+    ev.hex = hexOf(std::string("z") + kDag[i].name);
+    ev.self_parent = kDag[i].sp[0] ? hexOf(std::string("z") + kDag[i].sp) : "";
+    ev.other_parent = kDag[i].op[0] ? hexOf(std::string("z") + kDag[i].op) : "";
+    ev.ts = Time{T, 100 + i};
+    ev.s[0] = (uint8_t)(10 + i);
+    for (int b = 0; b < 32; b++) ev.hash[b] = (uint8_t)(i * 7 + b + 1);
+    CHECK(h.insert(ev) == OK);
+    zone_of[i] = 100 + i;
+  }
+  CHECK(h.DivideRounds() == OK);
+  CHECK(h.DecideFame() == OK);
+  CHECK(h.FindOrder() == OK);
+  CHECK(h.commits.size() == 1);
+  int not_first = 0;
+  for (auto& ev : h.commits.empty() ? std::vector<Event>() : h.commits[0]) {
+    const int32_t x = store.ids[ev.hex];
+    const int r = ev.round_received;
+    int want = -1;
+    for (int d = 0; d < 3 && want < 0; d++) {
+      const int32_t w = hge_round_witness(h.eng, r, d);
+      if (w >= 0 && hge_fame(h.eng, r, d) == 1 && hge_see(h.eng, w, x)) {
+        const int32_t osa = hge_oldest_self_ancestor_to_see(h.eng, w, x);
+        if (osa >= 0) want = zone_of[osa];
+      }
+    }
+    CHECK(ev.consensus_ts.nano == T && ev.consensus_ts.zone == want);
+    not_first += want != 100;
+  }
+  CHECK(not_first > 0);  // some source is not the first event seen at that instant
+}
+
 int main(int argc, char** argv) {
   const bool gpu = argc > 1 && !strcmp(argv[1], "--gpu");
   store_checks();
   lru_checks();
-  if (gpu) gpu_checks();
+  if (gpu) {
+    gpu_checks();
+    shared_instant_checks();
+  }
   printf("%s: %d failures\n", gpu ? "shim replay (store + engine)" : "shim replay (store)", failures);
   return failures ? 1 : 0;
 }

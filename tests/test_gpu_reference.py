@@ -239,3 +239,41 @@ def test_go_shim_logic_replayed_on_gpu():
                          text=True, timeout=120)
     assert out.returncode == 0, out.stderr + out.stdout
     assert "0 failures" in out.stdout
+
+
+@pytest.mark.parametrize("n,events,k", [(4, 800, 4), (16, 3000, 16), (64, 4000, 64)])
+def test_consensus_timestamp_sources(n, events, k):
+    """hge_consensus_timestamp_sources (MedianTimestamp's source, hashgraph.go:762-770):
+    every ordered event's source has the consensus timestamp as its own timestamp and is
+    OldestSelfAncestorToSee(w, x) of a famous witness w of x's round received that sees
+    x (the oracle's predicates); unordered events have none."""
+    from babble_amd.engine import Engine
+    from babble_amd.gossip import random_gossip, schedule
+    from oracle.oracle import replay as oracle_replay
+    # timestamps with repeats: several candidates share an instant
+    dag = random_gossip(n, events, seed=61)
+    dag["ts"] = dag["ts"] // 7000 * 7000
+    calls = schedule(events, k)
+    eng = Engine(n, events + 64)
+    try:
+        st, order, _ = eng.replay(dag, calls)
+        o, ost, oorder, _ = oracle_replay(dag, calls)
+        assert np.array_equal(order, oorder)
+        ids = np.arange(len(st), dtype=np.int32)
+        src = eng.consensus_timestamp_sources(ids)
+        rr, cts = eng.event_received()
+        assert (st == np.arange(len(st))).all()  # no forks: engine id = submission index
+        ts = dag["ts"]
+        assert (src[rr < 0] == -1).all()
+        ordered = set(order.tolist())
+        assert ordered == set(np.nonzero(rr >= 0)[0].tolist())
+        for x in list(ordered)[:400]:
+            s = int(src[x])
+            assert s >= 0 and ts[s] == cts[x]
+            cands = set()
+            for w in o.round_witnesses(int(rr[x])):
+                if o.round_fame(int(rr[x]), w) == 1 and o.see(w, x):
+                    cands.add(o.oldest_self_ancestor_to_see(w, x))
+            assert s in cands
+    finally:
+        eng.close()

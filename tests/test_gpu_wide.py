@@ -271,3 +271,18 @@ def test_handoff_stall_mid_walk(n, events, k, epoch, monkeypatch):
         assert eng.frontier_fallbacks() == 1
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("n,events", [(16, 3000), (32, 11000)])
+def test_coin_rounds_wide_one_shot(n, events):
+    """One RunConsensus over a whole stream long enough that DecideFame's j loop
+    reaches diff = N (hashgraph.go:645-649, the coin branch) at N = 16 and N = 32:
+    the engine equals the live oracle field by field, and the oracle's statistics
+    show the coin branch taken."""
+    from babble_amd.engine import Engine
+    eng = Engine(n, events + 64)
+    try:
+        o, _ = run_case(eng, random_gossip(n, events, seed=78 if n == 32 else 77), events)
+        assert o.stats()["coin_evals"] > 0
+    finally:
+        eng.close()
