@@ -613,7 +613,12 @@ __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const FT* FDT
         // streaming stores: 20 GB per 256/10M replay, read back only by later kernels
         // (7.24-7.28 vs 7.40-7.41 ms in a same-box A/B; the runs kernel's scattered short
         // runs need the L2 to merge their lines: 18.9 vs 6.55 ms with streaming stores)
-        __builtin_nontemporal_store(tile[tx][r], t.FD + o);
+        if constexpr (sizeof(FT) == 2) {  // uint16 runs: the FD rows packed (FD + 1, 0xFFFF = none)
+          const int f = tile[tx][r];
+          __builtin_nontemporal_store((uint16_t)(f == INF32 ? 0xFFFFu : (uint32_t)f + 1), t.FD16 + o);
+        } else {
+          __builtin_nontemporal_store(tile[tx][r], t.FD + o);
+        }
         if (tsrow) __builtin_nontemporal_store(dv, t.FDTD + o);
       }
       const bool any = __ballot(esc) != 0;
@@ -623,10 +628,11 @@ __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const FT* FDT
   }
 }
 
-// the uint16 run table widened to int32 (0xFFFF -> INF32) at the switch to int32 positions
-__global__ void k_fdt16_to32(const uint16_t* src, int32_t* dst, size_t n) {
+// the uint16 tables widened to int32 at the switch to int32 positions: runs
+// (0xFFFF -> INF32, else the value) and FD rows (0xFFFF -> INF32, else value - 1)
+__global__ void k_fdt16_to32(const uint16_t* src, int32_t* dst, size_t n, int bias) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-    dst[i] = src[i] == 0xFFFFu ? INF32 : (int32_t)src[i];
+    dst[i] = src[i] == 0xFFFFu ? INF32 : (int32_t)src[i] - bias;
 }
 
 __global__ void __launch_bounds__(256) k_fd_qlo(Tables t, const int32_t* olen, const int32_t* len, int32_t* qlo) {

@@ -245,7 +245,8 @@ struct hge_engine {
     t.LA = d_LA.p;
     t.NW2 = (N + 1) / 2;
     t.LA16 = sweep16() ? d_LA16.p : nullptr;  // null: int32 rows (la_row)
-    t.FD = d_FD.p;
+    t.FD = fdt16() ? nullptr : d_FD.p;
+    t.FD16 = fdt16() ? (uint16_t*)d_FD.p : nullptr;
     t.FDTD = d_FDTD.p;
     t.FDTW = d_FDTW.p;
     t.WLA = d_WLA.p;
@@ -486,7 +487,19 @@ struct hge_engine {
       d_LA16.p = q;
       d_LA16.n = (size_t)N * nc * w;
     }
-    grow_chain_table(d_FD, nc, true);
+    if (fdt16()) {  // uint16 FD rows: a chain's block is ccap * N halves
+      int32_t* q = nullptr;
+      HIPCHK(hipMalloc(&q, sizeof(uint16_t) * (size_t)N * nc * N));
+      if (ccap > 0 && d_FD.p)
+        HIPCHK(hipMemcpy2DAsync(q, 2 * (size_t)nc * N, d_FD.p, 2 * (size_t)ccap * N, 2 * (size_t)ccap * N, N,
+                                hipMemcpyDeviceToDevice, st));
+      sync();
+      d_FD.free_();
+      d_FD.p = q;
+      d_FD.n = (size_t)N * nc * N / 2;
+    } else {
+      grow_chain_table(d_FD, nc, true);
+    }
     if (N > 16) {  // FD timestamp rows below a batch's qlo are kept
       grow_chain_table(d_FDTD, nc, true);
       const size_t NT = (size_t)(N + 63) / 64;
@@ -1431,16 +1444,19 @@ struct hge_engine {
   // engine refusing every later step (the packed tables can no longer hold the
   // positions) instead of packing positions past 65,534 into uint16.
   void to_wide32() {
-    if (fdt16()) {  // the runs continue in int32 from here: widen the kept uint16 ones
-      int32_t* q = nullptr;
+    if (fdt16()) {  // the runs and FD rows continue in int32 from here: widen the kept ones
       const size_t n = (size_t)N * N * ccap;
-      HIPCHK(hipMalloc(&q, sizeof(int32_t) * n));
-      KLAUNCH(k_fdt16_to32, dim3((unsigned)std::min<size_t>(div_up(n, 256), 65536)), dim3(256), 0, st,
-              (const uint16_t*)d_FDT.p, q, n);
-      sync();
-      d_FDT.free_();
-      d_FDT.p = q;
-      d_FDT.n = n;
+      for (int which = 0; which < 2; which++) {
+        DBuf<int32_t>& b = which ? d_FD : d_FDT;
+        int32_t* q = nullptr;
+        HIPCHK(hipMalloc(&q, sizeof(int32_t) * n));
+        KLAUNCH(k_fdt16_to32, dim3((unsigned)std::min<size_t>(div_up(n, 256), 65536)), dim3(256), 0, st,
+                (const uint16_t*)b.p, q, n, which);
+        sync();
+        b.free_();
+        b.p = q;
+        b.n = n;
+      }
     }
     grow_chain_table(d_LA, ccap, false);
     s_w32.need(N);
@@ -3002,6 +3018,12 @@ int hge_coordinates(hge_engine* h, int32_t id, int32_t* la_out, int32_t* fd_out)
     } else {
       h->readback(la_out, h->d_LA.p + off, h->N);
     }
+  }
+  if (fd_out && h->fdt16()) {  // packed rows: FD + 1, 0xFFFF = none
+    std::vector<uint16_t> row(h->N);
+    h->readback(row.data(), (const uint16_t*)h->d_FD.p + off, h->N);
+    for (int c = 0; c < h->N; c++) fd_out[c] = row[c] == 0xFFFFu ? INF32 : (int32_t)row[c] - 1;
+    return HGE_OK;
   }
   if (fd_out) h->readback(fd_out, h->d_FD.p + off, h->N);
   return HGE_OK;

@@ -47,6 +47,10 @@ struct Tables {
   uint16_t* WLR;  // N > 64, packed path: [Rcap][N][N] LA + 1 of the same rows, row-major [r][d][cx] (theta)
   int32_t* LA;
   int32_t* FD;
+  // N > 128, N % 4 == 0, uint16 positions (hge_engine.hip fdt16): the firstDescendants
+  // rows as uint16 FD + 1 (0xFFFF = none; the rounds walk's packed member format),
+  // [N][ccap][N]; FD is then null and every reader goes through fd_at
+  uint16_t* FD16;
   int32_t* round;
   uint8_t* wit;
   int32_t* C;
@@ -82,6 +86,14 @@ __device__ __forceinline__ int la_row(const Tables& t, size_t row, int col) {
     return (int)((w >> ((col & 1) << 4)) & 0xFFFFu) - 1;
   }
   return t.LA[row * (size_t)t.N + col];
+}
+// firstDescendants[row][col] (row = chain * ccap + position; INF32 = none)
+__device__ __forceinline__ int fd_at(const Tables& t, size_t row, int col) {
+  if (t.FD16) {
+    const uint32_t v = t.FD16[row * (size_t)t.N + col];
+    return v == 0xFFFFu ? INF32 : (int)v - 1;
+  }
+  return t.FD[row * (size_t)t.N + col];
 }
 __device__ __forceinline__ int la_at(const Tables& t, int c, int p, int col) {
   return la_row(t, (size_t)c * t.ccap + p, col);
@@ -1052,9 +1064,9 @@ __device__ __forceinline__ void witness_bits_body(const Tables& t, const int32_t
         if (ssc) {
           ss = (ssc[((size_t)j * N + cy) * NW + wd] >> (d & 63)) & 1ull;
         } else {
-          const int32_t* fd = t.FD + rowoff(t, d, t.index[w]);
+          const size_t frow = (size_t)d * t.ccap + t.index[w];
           int c = 0;
-          for (int i = 0; i < N; i++) c += (la_row(t, lrow, i) >= fd[i]) ? 1 : 0;
+          for (int i = 0; i < N; i++) c += (la_row(t, lrow, i) >= fd_at(t, frow, i)) ? 1 : 0;
           ss = c >= t.SM;
         }
       }
@@ -2200,7 +2212,7 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
 #pragma unroll
       for (int k = 0; k < VPL; k++) {
         const int dd = min(lane + 64 * k, N - 1);
-        const int f = t.FD[rw * N + dd];
+        const int f = fd_at(t, rw, dd);
         ts[e][k] = f != INF32 ? t.tsch[(size_t)dd * t.ccap + f] : 0;
       }
     }
@@ -2932,7 +2944,7 @@ __global__ void __launch_bounds__(256) k_cts_source(Tables t, const int32_t* ids
       if (d < t.N) {
         const int w = t.W[(size_t)r * t.N + d];
         if (w >= 0 && t.fame[(size_t)r * t.N + d] == 1 && la_at(t, d, t.index[w], cx) >= ix) {
-          p = t.FD[rowoff(t, cx, ix) + d];
+          p = fd_at(t, (size_t)cx * t.ccap + ix, d);
           hit = p != INF32 && t.tsch[(size_t)d * t.ccap + p] == c;
         }
       }

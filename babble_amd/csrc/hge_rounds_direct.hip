@@ -159,6 +159,17 @@ __device__ __forceinline__ void dir_members_fd(const Tables& t, int d, int part,
   const int N = t.N;
   const int c0 = part * G::CPT;
   const bool act = d < N && Pd != INF32;
+  if (t.FD16) {  // the rows are stored packed already (FD + 1, 0xFFFF = none)
+    const uint16_t* row = t.FD16 + rowoff(t, act ? d : 0, act ? Pd : 0);
+#pragma unroll
+    for (int k = 0; k < G::CW / 2; k++) {
+      uint2 a = *(const uint2*)(row + min(c0 + 4 * k, N - 4));
+      if (!act || c0 + 4 * k >= N) a = make_uint2(~0u, ~0u);
+      mw[2 * k] = a.x;
+      mw[2 * k + 1] = a.y;
+    }
+    return;
+  }
   const int32_t* row = t.FD + rowoff(t, act ? d : 0, act ? Pd : 0);
 #pragma unroll
   for (int k = 0; k < G::CW / 2; k++) {
@@ -219,10 +230,16 @@ __device__ __forceinline__ void dir_stage_member(const Tables& t, uint32_t* mb, 
   const int lane = threadIdx.x;  // < 64
   const int N = t.N;
   if (4 * lane < NPOW) {
-    int4 a = make_int4(INF32, INF32, INF32, INF32);
-    if (p != INF32 && 4 * lane < N) a = *(const int4*)(t.FD + rowoff(t, c, p) + 4 * lane);
-    const unsigned long long x =
-        (unsigned long long)dir_pack_fd(a.x, a.y) | ((unsigned long long)dir_pack_fd(a.z, a.w) << 32);
+    unsigned long long x;
+    if (t.FD16) {  // stored packed already
+      uint2 a = make_uint2(~0u, ~0u);
+      if (p != INF32 && 4 * lane < N) a = *(const uint2*)(t.FD16 + rowoff(t, c, p) + 4 * lane);
+      x = (unsigned long long)a.x | ((unsigned long long)a.y << 32);
+    } else {
+      int4 a = make_int4(INF32, INF32, INF32, INF32);
+      if (p != INF32 && 4 * lane < N) a = *(const int4*)(t.FD + rowoff(t, c, p) + 4 * lane);
+      x = (unsigned long long)dir_pack_fd(a.x, a.y) | ((unsigned long long)dir_pack_fd(a.z, a.w) << 32);
+    }
     const int w = 2 * lane, part = w / G::CW, wp = w - part * G::CW;
     const int k = wp / MVW, sub = wp - k * MVW;
     const size_t word = ((size_t)k * BS + (size_t)c * G::TPM + part) * MVW + sub;

@@ -40,9 +40,9 @@ __device__ __forceinline__ int w32_member(const Tables& t, const int32_t* olen, 
 // #{i : LA[(c,p)][i] >= FD[m][i]} >= SM, the LA row staged in LDS by the caller
 __device__ __forceinline__ bool w32_ss(const Tables& t, const int* sla, int d, int md) {
   if (md == INF32) return false;
-  const int32_t* fd = t.FD + ((size_t)d * t.ccap + md) * (size_t)t.N;
+  const size_t frow = (size_t)d * t.ccap + md;
   int n = 0;
-  for (int i = 0; i < t.N; i++) n += sla[i] >= fd[i] ? 1 : 0;
+  for (int i = 0; i < t.N; i++) n += sla[i] >= fd_at(t, frow, i) ? 1 : 0;
   return n >= t.SM;
 }
 

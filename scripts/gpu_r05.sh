@@ -115,6 +115,13 @@ d=json.loads(open('gpurun_out/r05/ab_${ABVAR}_$v.json').read().strip().splitline
 k=d['kernels_ms_per_replay']
 print('$ABVAR=$v', round(d['value']/1e6,2), d['ms_per_step'], {n: k[n] for n in k if 'median' in n or 'rows_runs' in n or 'transpose' in n or 'rounds_direct' in n}, d['parity'][:60])"
          done; unset $ABVAR ;;
+    mcg) for G in $GRAPHS; do
+           timeout -k 10 300 python -u bench.py --workload mc --graphs $G --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/r05/bench_mc$G.json 2> gpurun_out/r05/bench_mc$G.err || { tail -20 gpurun_out/r05/bench_mc$G.err; exit 2; }
+           python -c "
+import json
+d=json.loads(open('gpurun_out/r05/bench_mc$G.json').read().strip().splitlines()[-1])
+print('mc$G', round(d['value']/1e6,2), d['ms_per_step'], d['config']['ordered_per_step'], d['parity'][:50]); print(d['kernels_ms_per_replay'])"
+         done ;;
     prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r05/prof -o run -- python -u bench.py --no-secondary --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/r05/prof.log 2>&1 || { tail -20 gpurun_out/r05/prof.log; exit 3; }
           find gpurun_out/r05/prof -name "*kernel_trace.csv" -delete; find gpurun_out/r05/prof -name "*kernel_stats.csv" | head -1 | xargs head -12 ;;
     profmc) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r05/profmc -o run -- python -u bench.py --workload mc --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/r05/profmc.log 2>&1 || { tail -20 gpurun_out/r05/profmc.log; exit 3; }
