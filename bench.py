@@ -73,10 +73,15 @@ def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
       k_la_sweep16 / k_la_clear16  6N / 2N per event (N > 32: the same on packed u16);
       k_transpose    8N/event at N <= 16 (FDT -> FD: reads and writes 4N);
       k_fd_transpose_ts 12N/event (N > 16: FDT read, FD and the 4-byte FD
-                    timestamp offsets written);
+                    timestamp offsets written); 8N with uint16 runs and FD rows
+                    (N > 128: 2N FDT read, 2N FD and 4N offsets written).  These
+                    figures include the FDT intermediate and the offsets; SURVEY
+                    8(d)'s FD write alone (4N, 2N as uint16) is reported beside
+                    them as `fd_write_frac`;
       k_witness_la   8N^2 per round (frontier rows read, transposed rows written);
       k_la16_rows_runs 6N/event (N > 32: LA16 read, the FDT runs written); 8N/event
                     over int32 LA tiles (<int32_t, true>: N <= 32 and wide hashgraphs);
+                    4N with uint16 runs (<uint16_t>, N > 128);
       k_la_win      (2N + 20)/event (32 < N <= 256, windowed exact propagation: the
                     head rows live in LDS, so per event only the packed row is
                     written, the 16-byte plan entry read and the 4-byte row sum
@@ -96,6 +101,10 @@ def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
         return 8 * n * n * rounds
     if name == "k_la16_rows_runs" and "true" in kernel:
         return 8 * n * events
+    if name == "k_la16_rows_runs" and "uint16_t" in kernel:
+        return 4 * n * events
+    if name == "k_fd_transpose_ts" and "uint16_t" in kernel:
+        return 8 * n * events
     per_event = {"k_la_sweep": 12 * n, "k_la_clear": 4 * n, "k_transpose": 8 * n,
                  "k_fd_transpose_ts": 12 * n,
                  "k_fdt_clear": 4 * n, "k_fss": 8 * n,
@@ -112,11 +121,11 @@ def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
 
 def pmc_traffic(config_key, kernel, launches_per_replay):
     """HBM bytes per launch of `kernel` in this configuration from the committed
-    rocprofv3 PMC passes (profiles/r04/pmc_traffic.json, else an earlier round's, made by
+    rocprofv3 PMC passes (profiles/r05/pmc_traffic.json, else an earlier round's, made by
     scripts/pmc_traffic.py on the GPU box): the kernel's bytes per replay over
     the launches that did work (k_la_sweep: the sweeps up to the quiet one), or None."""
     pm = None
-    for rnd in ("r04", "r03", "r02"):  # the latest round's passes
+    for rnd in ("r05", "r04", "r03", "r02"):  # the latest round's passes
         try:
             pm = json.load(open(os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")))
             break
@@ -586,6 +595,10 @@ def main():
             hbm_kernels[name] = {"achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
                                  "alg_bytes_per_launch": int(b), "launch_ms": round(pl, 4),
                                  "launches_per_replay": lpr}
+            if base == "k_fd_transpose_ts":
+                # SURVEY 8(d)'s FD write alone (the FDT read and the offsets excluded)
+                fdw = (2 if "uint16_t" in name else 4) * n * ev0 / max(lpr, 1)
+                hbm_kernels[name]["fd_write_frac"] = round(fdw / (pl * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
 
     cpu, parity, checks = None, None, []
     if rank == 0:

@@ -19,7 +19,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-ROUND = "r04"  # the profiles/ directory this round's passes go to
+ROUND = "r05"  # the profiles/ directory this round's passes go to
 
 def run_pass(out_dir, counter, bench_args, parse_only=False):
     d = os.path.join(out_dir, counter.lower())
