@@ -129,6 +129,12 @@ __device__ __forceinline__ void st(T* p, V v) {
   __hip_atomic_store(p, (T)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void wsync() { __builtin_amdgcn_wave_barrier(); }
+// a workgroup barrier ordering LDS accesses only: no wait for outstanding global stores
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 
 // ---------------------------------------------------------------------------
 // Each graph is one wavefront, so nothing hides its memory latency but its own
@@ -137,53 +143,99 @@ __device__ __forceinline__ void wsync() { __builtin_amdgcn_wave_barrier(); }
 // (witnesses, their vote bitsets, fame, thresholds) and the undetermined list in LDS.
 
 // lastAncestors (InitEventCoordinates, hashgraph.go:399-463): in insertion order,
-// LA[x] = max(LA[sp], LA[op]) with LA[x][creator] = index.  The self-parent is the
-// creator's head (admission: "Self-parent not last known", hashgraph.go:390-393),
-// so its row is in LDS; so is the other-parent's when it is its chain's head.
-// Lane k keeps column k of every chain's head row in registers (hr[c], indexed by
-// the wave-uniform creator: v_movrels / v_movreld), and lane c the id of chain
-// c's head, so an event costs a handful of VALU instructions and one row store.
+// LA[x] = max(LA[sp], LA[op]) with LA[x][creator] = index.  One 256-thread
+// workgroup per graph, SL = 256 / NM event slots of NM columns.  The events go in
+// chunks of 64; a step takes the longest run of consecutive events none of which
+// has a parent inside the run (an event's parents precede it, so the run's rows
+// depend only on rows already final) and computes their rows together.  At N = 32
+// runs average ~4.5 events (a parent lands among the last j events with
+// probability ~j/32 per parent).  A parent's row comes from the chunk's LDS ring
+// (written once per slot, so a step needs one barrier, LDS-scoped: the row stores
+// to HBM are never waited for inside a chunk), from the snapshot of the chain heads
+// taken at the chunk's start (the self-parent is its creator's head, admission
+// "Self-parent not last known", hashgraph.go:390-393; the other-parent nearly
+// always is), or from HBM behind the chunk boundary's full barrier.
 template <int NM>
-__global__ __launch_bounds__(64) void kb_coords(BT t) {
+__global__ __launch_bounds__(256) void kb_coords(BT t) {
+  constexpr int SL = 256 / NM;
   const GDesc d = t.gd[blockIdx.x];
-  const int N = t.N, k = threadIdx.x;
-  int hr[NM];
-#pragma unroll
-  for (int c = 0; c < NM; c++) hr[c] = -1;
-  int hid = -1;
+  const int N = t.N, tid = threadIdx.x, s = tid / NM, k = tid - (tid / NM) * NM;
+  // rows 0..63: the chunk's ring; 64 + c: chain c's head row as of the chunk's start
+  __shared__ int32_t rows[64 + NM][NM];
+  __shared__ int32_t headid[NM];
+  // per event of the chunk: its parents' row sources (a row of `rows`, -1 none,
+  // -2 HBM), creator, index; the parents' ids for the HBM case
+  __shared__ int4 einfo[64];
+  __shared__ int32_t msp[64], mop[64];
+  __shared__ int32_t gst[65];   // the chunk's runs: [gst[i], gst[i + 1])
+  __shared__ int32_t clast[NM];  // the chunk's last event per chain (-1)
+  __shared__ int s_ng;
+  for (int i = tid; i < NM * NM; i += 256) rows[64 + i / NM][i - (i / NM) * NM] = -1;
+  if (tid < NM) headid[tid] = -1;
+  __syncthreads();
   int32_t* LA = t.LA + d.eo * N;
-  // per event: creator | other-parent creator << 8 | has-self-parent << 16, index, other-parent
-  auto meta = [&](int i, int& pk, int& ix, int& op) {
-    pk = 0, ix = 0, op = -1;
-    if (i < d.E) {
-      pk = t.cr[d.eo + i] | t.oc[d.eo + i] << 8 | (t.sp[d.eo + i] >= 0 ? 1 << 16 : 0);
-      ix = t.ix[d.eo + i];
-      op = t.op[d.eo + i];
-    }
-  };
-  // No load is left in flight across the event loop: a register-indexed read (hr[cr])
-  // makes the compiler wait for every outstanding load (vmcnt(0), which on CDNA also
-  // drains the row stores) before it, i.e. once per event.
   for (int base = 0; base < d.E; base += 64) {
-    int mpk, mix, mop;
-    meta(base + k, mpk, mix, mop);
-    asm volatile("" : "+v"(mpk), "+v"(mix), "+v"(mop));  // landed here, not waited for per event
     const int cnt = min(64, d.E - base);
-    for (int u = 0; u < cnt; u++) {
-      const int pk = rl(mpk, u), ix = rl(mix, u), op = rl(mop, u);
-      const int cr = pk & 0xFF, oc = (pk >> 8) & 0xFF;
-      int v = (pk >> 16) ? hr[cr] : -1;
-      if (op >= 0) {
-        if (rl(hid, oc) == op) v = max(v, hr[oc]);
-        else v = max(v, k < N ? ld(&LA[(int64_t)op * N + k]) : -1);  // not its chain's head
+    if (tid < 64) {
+      const int i = base + tid;
+      const bool on = i < d.E;
+      const int sp = on ? t.sp[d.eo + i] : -1, op = on ? t.op[d.eo + i] : -1;
+      const int cr = on ? t.cr[d.eo + i] : 0, oc = on ? t.oc[d.eo + i] : 0;
+      auto src = [&](int p, int c) -> int {
+        return p < 0 ? -1 : p >= base ? p - base : headid[c] == p ? 64 + c : -2;
+      };
+      einfo[tid] = make_int4(src(sp, cr), src(op, oc), cr, on ? t.ix[d.eo + i] : 0);
+      msp[tid] = sp;
+      mop[tid] = op;
+      if (tid < NM) clast[tid] = -1;
+      wsync();
+      if (on) atomicMax(&clast[cr], tid);
+      // the runs, greedily from the chunk's start: a run from u takes the events
+      // after u up to the first with a parent at or past base + u (at most SL)
+      const int pm = max(sp, op);
+      int u = 0, ng = 0;
+      while (u < cnt) {
+        const uint64_t bad = ballot(tid > u && (tid >= cnt || pm >= base + u));
+        const int lim = bad ? __ffsll((unsigned long long)bad) - 1 : 64;
+        if (tid == 0) gst[ng] = u;
+        ng++;
+        u += min(lim - u, SL);
       }
-      if (k == cr) {
-        v = ix;
-        hid = base + u;
+      if (tid == 0) {
+        gst[ng] = cnt;
+        s_ng = ng;
       }
-      hr[cr] = v;
-      if (k < N) LA[(int64_t)(base + u) * N + k] = v;
     }
+    __syncthreads();
+    const int ng = s_ng;
+    int u = gst[0], un = gst[1];
+    int4 ei = einfo[min(u + s, 63)];
+    for (int gi = 0; gi < ng; gi++) {
+      const int e = u + s;
+      const bool on = e < un && k < N;
+      // the next step's run and record, read ahead (nothing this step writes)
+      const int u2 = un, un2 = gi + 2 <= ng ? gst[min(gi + 2, ng)] : un;
+      const int4 ei2 = einfo[min(u2 + s, 63)];
+      if (on) {
+        const int a = ei.x >= 0 ? rows[ei.x][k] : ei.x == -1 ? -1 : ld(&LA[(int64_t)msp[e] * N + k]);
+        const int b = ei.y >= 0 ? rows[ei.y][k] : ei.y == -1 ? -1 : ld(&LA[(int64_t)mop[e] * N + k]);
+        const int val = k == ei.z ? ei.w : max(a, b);
+        rows[e][k] = val;
+        LA[(int64_t)(base + e) * N + k] = val;
+      }
+      lds_barrier();
+      u = u2;
+      un = un2;
+      ei = ei2;
+    }
+    // the heads after the chunk
+    if (k < N)
+      for (int c = s; c < N; c += SL) {
+        const int l = clast[c];
+        if (l >= 0) rows[64 + c][k] = rows[l][k];
+      }
+    if (tid < N && clast[tid] >= 0) headid[tid] = base + clast[tid];
+    __syncthreads();  // also: the chunk's row stores are complete before the next one reads HBM
   }
 }
 
@@ -1488,7 +1540,7 @@ struct hge_batch {
     const BT t = tables();
     BCHK(hipEventRecord(ev[0], st));
     if (N <= 32) {
-      launch(kb_coords<32>, G, t);
+      launch(kb_coords<32>, G, t, 256);
       BCHK(hipEventRecord(ev[1], st));
       launch(kb_fd<32>, G * N, t);
       BCHK(hipEventRecord(ev[2], st));
@@ -1499,7 +1551,7 @@ struct hge_batch {
       if (G > 2 * ncu) launch(kb_consensus<32, 4>, G, t, 256);
       else launch(kb_consensus<32, 1>, G, t, 256);
     } else {
-      launch(kb_coords<64>, G, t);
+      launch(kb_coords<64>, G, t, 256);
       BCHK(hipEventRecord(ev[1], st));
       launch(kb_fd<64>, G * N, t);
       BCHK(hipEventRecord(ev[2], st));
