@@ -9,9 +9,9 @@
 // graph's whole call schedule runs inside the consensus kernel:
 //
 //   kb_coords     lastAncestors rows in insertion order (hashgraph.go:399-463), one
-//                 wave per graph (lane = column); the chain heads' rows live in
-//                 registers, a row is a max of the self-parent head and the
-//                 other-parent row.
+//                 256-thread workgroup per graph: runs of mutually independent
+//                 events computed together, a row the max of its parents' rows
+//                 (from an LDS ring of the chunk or a snapshot of the chain heads).
 //   kb_fd         firstDescendants in run layout FDT[j][c][p], one wave per (graph,
 //                 chain j): chain-j event k is the first chain-j descendant of
 //                 chain-c positions (LA[(j,k-1)][c], LA[(j,k)][c]] (hashgraph.go:466-494);
@@ -137,10 +137,12 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 // ---------------------------------------------------------------------------
-// Each graph is one wavefront, so nothing hides its memory latency but its own
-// prefetching: every kernel below loads the next chunk of events while it works on
-// the current one, and the consensus kernel keeps the state of the last RW rounds
-// (witnesses, their vote bitsets, fame, thresholds) and the undetermined list in LDS.
+// A graph's work is a dependent chain (insertion order, rounds, the call schedule),
+// so each kernel below gives one graph one workgroup and hides its latency inside
+// it: the chain's independent steps spread over the waves, the next chunk's loads
+// issued before the current one is consumed, and the consensus kernel's state of
+// the last RW rounds (witnesses, vote bitsets, fame, thresholds) and the
+// undetermined list kept in LDS.
 
 // lastAncestors (InitEventCoordinates, hashgraph.go:399-463): in insertion order,
 // LA[x] = max(LA[sp], LA[op]) with LA[x][creator] = index.  One 256-thread

@@ -56,6 +56,8 @@ print('$1/$2', round(d['value']/1e6,2), d['ms_per_step'], d['parity'][:120])"
     gap) timeout -k 10 120 ./build/launch_gap 32 2000 > gpurun_out/r05/launch_gap.json && timeout -k 10 120 ./build/launch_gap 16 2000 >> gpurun_out/r05/launch_gap.json || exit 5
          timeout -k 10 120 ./build/granule_hop 256 4000 > gpurun_out/r05/granule_hop.json || exit 5
          cat gpurun_out/r05/launch_gap.json gpurun_out/r05/granule_hop.json ;;
+    gapargs) timeout -k 10 120 ./build/launch_gap args 20 2000 > gpurun_out/r05/launch_args.json && timeout -k 10 120 ./build/launch_gap args 8 2000 >> gpurun_out/r05/launch_args.json || exit 5
+         cat gpurun_out/r05/launch_args.json ;;
     pmc) bash scripts/gpu_pmc.sh r05/pmc || exit 6 ;;
     diag) bash scripts/gpu_pmc_diag.sh r05/diag && bash scripts/gpu_pmc_lds.sh r05/lds || exit 6 ;;
     onprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r05/onprof -o run -- python3 -u scripts/analysis/online_profile.py 256 600000 256 400 > gpurun_out/r05/onprof.log 2>&1 || { tail -20 gpurun_out/r05/onprof.log; exit 7; }

@@ -39,7 +39,53 @@ static double now_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// the same struct read through a device pointer (8 bytes of arguments)
+__global__ void k_bigp(const Big* __restrict__ b) {
+  if (threadIdx.x == 0) b->p[0] += b->v[threadIdx.x & 63];
+}
+
+// `launch_gap args L C`: argument size alone, interleaved A/B (8-byte pointer to a
+// device copy of the struct vs the 292-byte struct by value), 6 alternations
+static int args_ab(int L, int C) {
+  int* d;
+  CK(hipMalloc(&d, 64));
+  CK(hipMemset(d, 0, 64));
+  hipStream_t st;
+  CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  Big bg;
+  bg.p = d;
+  for (int i = 0; i < 72; i++) bg.v[i] = i;
+  Big* db;
+  CK(hipMalloc(&db, sizeof(Big)));
+  CK(hipMemcpy(db, &bg, sizeof(Big), hipMemcpyHostToDevice));
+  auto run = [&](int kind) {
+    const double t0 = now_us();
+    for (int c = 0; c < C; c++) {
+      for (int i = 0; i < L; i++) {
+        if (kind) hipLaunchKernelGGL(k_big, dim3(1), dim3(64), 0, st, bg);
+        else hipLaunchKernelGGL(k_bigp, dim3(1), dim3(64), 0, st, (const Big*)db);
+      }
+      CK(hipStreamSynchronize(st));
+    }
+    return (now_us() - t0) / C;
+  };
+  run(0);
+  run(1);
+  printf("{\"launches_per_call\": %d, \"calls\": %d, \"arg_bytes\": [8, %zu], \"ptr_us\": [", L, C, sizeof(Big));
+  double v[2][6];
+  for (int r = 0; r < 6; r++) {
+    v[0][r] = run(0);
+    v[1][r] = run(1);
+  }
+  for (int r = 0; r < 6; r++) printf("%s%.1f", r ? ", " : "", v[0][r]);
+  printf("], \"byvalue_us\": [");
+  for (int r = 0; r < 6; r++) printf("%s%.1f", r ? ", " : "", v[1][r]);
+  printf("]}\n");
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && argv[1][0] == 'a') return args_ab(argc > 2 ? atoi(argv[2]) : 20, argc > 3 ? atoi(argv[3]) : 2000);
   const int L = argc > 1 ? atoi(argv[1]) : 32, C = argc > 2 ? atoi(argv[2]) : 2000;
   int* d;
   CK(hipMalloc(&d, 64));
