@@ -44,6 +44,7 @@ using namespace hge;
 // must fail the call, never leave a table silently unwritten
 #define KLAUNCH(kern, ...)                                                             \
   do {                                                                                 \
+    hp.launches++;                                                                     \
     prof_begin(#kern);                                                                 \
     hipLaunchKernelGGL(kern, __VA_ARGS__);                                             \
     const hipError_t le_ = hipGetLastError();                                          \
@@ -346,6 +347,14 @@ struct hge_engine {
 
   void destroy() {
     if (st) (void)hipStreamSynchronize(st);
+    if (getenv("HGE_HOST_PHASES") && hp.calls) {
+      const double c = (double)hp.calls;
+      fprintf(stderr,
+              "{\"hge_host_phases\": {\"calls\": %lld, \"launches_per_call\": %.2f, \"copies_per_call\": %.2f, "
+              "\"insert_us\": %.2f, \"consensus_us\": %.2f, \"sync_wait_us\": %.2f}}\n",
+              (long long)hp.calls, hp.launches / c, hp.copies / c, hp.insert_ns / c / 1e3, hp.call_ns / c / 1e3,
+              hp.wait_ns / c / 1e3);
+    }
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
     for (auto& e : prof_pool) (void)hipEventDestroy(e);
@@ -752,11 +761,13 @@ struct hge_engine {
     if (!bytes) return;
     char* q = pin_take(bytes);
     memcpy(q, host, bytes);
+    hp.copies++;
     HIPCHK(hipMemcpyAsync(dev, q, bytes, hipMemcpyHostToDevice, st));
   }
   void d2h(void* host, const void* dev, size_t bytes) {
     if (!bytes) return;
     char* q = pin_take(bytes);
+    hp.copies++;
     HIPCHK(hipMemcpyAsync(q, dev, bytes, hipMemcpyDeviceToHost, st));
     pending.push_back({host, (size_t)(q - pin), bytes});
   }
@@ -764,13 +775,25 @@ struct hge_engine {
   // next sync() until the arena is used again (no second host copy)
   size_t d2h_pinned(const void* dev, size_t bytes) {
     char* q = pin_take(bytes);
+    if (bytes) hp.copies++;
     if (bytes) HIPCHK(hipMemcpyAsync(q, dev, bytes, hipMemcpyDeviceToHost, st));
     return (size_t)(q - pin);
   }
   int64_t n_syncs = 0;  // host waits on the stream (hge_host_syncs)
+  // where an online call's host time goes (HGE_HOST_PHASES=1: printed at destroy):
+  // calls, launches, copies, ns spent inside hipStreamSynchronize, ns in the calls
+  struct HostPhases {
+    int64_t calls = 0, launches = 0, copies = 0, wait_ns = 0, call_ns = 0, insert_ns = 0;
+  } hp;
+  static int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
   void sync() {
     n_syncs++;
+    const int64_t w0 = now_ns();
     HIPCHK(hipStreamSynchronize(st));
+    hp.wait_ns += now_ns() - w0;
     for (const Pending& pd : pending) memcpy(pd.dst, pin + pd.off, pd.bytes);
     pending.clear();
     pin_used = 0;
@@ -2455,6 +2478,7 @@ int hge_reset(hge_engine* h) {
 int hge_insert_events(hge_engine* h, const hge_event* ev, int64_t n, int32_t* status_out,
                       int64_t* n_accepted) {
   GUARD_BEGIN
+  const int64_t c0 = hge_engine::now_ns();
   int64_t acc = 0;
   int rc = HGE_OK;
   for (int64_t i = 0; i < n; i++) {
@@ -2470,6 +2494,7 @@ int hge_insert_events(hge_engine* h, const hge_event* ev, int64_t n, int32_t* st
     acc++;
   }
   if (n_accepted) *n_accepted = acc;
+  h->hp.insert_ns += hge_engine::now_ns() - c0;
   return rc;
   GUARD_END(h)
 }
@@ -2507,11 +2532,14 @@ int hge_find_order(hge_engine* h, int32_t* ids_out, int64_t cap, int64_t* n_out)
 
 int hge_run_consensus(hge_engine* h, int32_t* ids_out, int64_t cap, int64_t* n_out) {
   GUARD_BEGIN
+  const int64_t c0 = hge_engine::now_ns();
   h->divide();
   std::vector<int32_t> order;
   h->consensus_batch({h->n_divided}, true, true, true, &order, nullptr);
   for (int64_t i = 0; i < (int64_t)order.size() && i < cap && ids_out; i++) ids_out[i] = order[i];
   if (n_out) *n_out = (int64_t)order.size();
+  h->hp.calls++;
+  h->hp.call_ns += hge_engine::now_ns() - c0;
   return HGE_OK;
   GUARD_END(h)
 }

@@ -431,6 +431,7 @@ class Engine:
             raise HgeError(rc, "hge_create failed")
         self.h = h
         self.n = n_participants
+        self._obuf = None
 
     def close(self):
         if getattr(self, "h", None):
@@ -506,11 +507,16 @@ class Engine:
         self._check(self.L.hge_decide_round_received(self.h))
 
     def _order_call(self, fn):
+        # one output buffer for the engine's life, grown geometrically: a fresh
+        # zeroed array of every event's size per call cost more than the call at
+        # 1M events (~200 us)
         cap = max(1, int(self.L.hge_event_count(self.h)))
-        out = np.zeros(cap, np.int32)
+        if self._obuf is None or len(self._obuf) < cap:
+            self._obuf = np.empty(max(cap, 2 * (0 if self._obuf is None else len(self._obuf))), np.int32)
+        out = self._obuf
         n = ctypes.c_int64()
-        self._check(fn(self.h, _p32(out), cap, ctypes.byref(n)))
-        return out[:n.value]
+        self._check(fn(self.h, _p32(out), len(out), ctypes.byref(n)))
+        return out[:n.value].copy()
 
     def find_order(self):
         return self._order_call(self.L.hge_find_order)

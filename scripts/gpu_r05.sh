@@ -58,6 +58,13 @@ print('$1/$2', round(d['value']/1e6,2), d['ms_per_step'], d['parity'][:120])"
          cat gpurun_out/r05/launch_gap.json gpurun_out/r05/granule_hop.json ;;
     gapargs) timeout -k 10 120 ./build/launch_gap args 20 2000 > gpurun_out/r05/launch_args.json && timeout -k 10 120 ./build/launch_gap args 8 2000 >> gpurun_out/r05/launch_args.json || exit 5
          cat gpurun_out/r05/launch_args.json ;;
+    gapcopies) timeout -k 10 120 ./build/launch_gap copies 16 2000 > gpurun_out/r05/launch_copies.json && timeout -k 10 120 ./build/launch_gap copies 8 2000 >> gpurun_out/r05/launch_copies.json || exit 5
+         cat gpurun_out/r05/launch_copies.json ;;
+    onphase) for NE in "16 100000 16 3000" "64 1000000 64 2000" "256 600000 256 600"; do
+           HGE_HOST_PHASES=1 timeout -k 10 300 python -u scripts/analysis/online_profile.py $NE > gpurun_out/r05/onphase.json 2> gpurun_out/r05/onphase.err || { tail -20 gpurun_out/r05/onphase.err; exit 2; }
+           python -c "import json; d=json.load(open('gpurun_out/r05/onphase.json')); print('$NE', d['plain']['p50_us'], d['plain']['mean_us'], d['profiled']['launches_per_call'])"
+           grep hge_host_phases gpurun_out/r05/onphase.err | head -1
+         done ;;
     pmc) bash scripts/gpu_pmc.sh r05/pmc || exit 6 ;;
     diag) bash scripts/gpu_pmc_diag.sh r05/diag && bash scripts/gpu_pmc_lds.sh r05/lds || exit 6 ;;
     onprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r05/onprof -o run -- python3 -u scripts/analysis/online_profile.py 256 600000 256 400 > gpurun_out/r05/onprof.log 2>&1 || { tail -20 gpurun_out/r05/onprof.log; exit 7; }

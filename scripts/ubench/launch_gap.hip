@@ -84,7 +84,68 @@ static int args_ab(int L, int C) {
   return 0;
 }
 
+// `launch_gap copies L C`: what small stream-ordered copies cost inside a chain of
+// L launches (the online call's control uploads and result downloads): per call,
+// L launches + 1 sync with 0, 2 or 4 small copies (1 KB H2D from pinned memory,
+// then 1 KB D2H into pinned memory), vs the same data read and written by the
+// kernels themselves straight from / to pinned host memory (no copy operations)
+__global__ void k_zc(const int* __restrict__ hin, int* __restrict__ hout, int* d) {
+  if (threadIdx.x < 64) {
+    const int v = hin[threadIdx.x];
+    if (threadIdx.x == 0) d[0] += v;
+    hout[threadIdx.x] = v + 1;
+  }
+}
+static int copies_ab(int L, int C) {
+  int *d, *dbuf, *hp, *hq;
+  CK(hipMalloc(&d, 64));
+  CK(hipMemset(d, 0, 64));
+  CK(hipMalloc(&dbuf, 4096));
+  CK(hipHostMalloc((void**)&hp, 4096, hipHostMallocDefault));
+  CK(hipHostMalloc((void**)&hq, 4096, hipHostMallocDefault));
+  for (int i = 0; i < 1024; i++) hp[i] = i;
+  hipStream_t st;
+  CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  auto run = [&](int ncopy, bool zc) {
+    const double t0 = now_us();
+    for (int c = 0; c < C; c++) {
+      for (int i = 0; i < L; i++) {
+        if (ncopy && i == 0) CK(hipMemcpyAsync(dbuf, hp, 1024, hipMemcpyHostToDevice, st));
+        if (ncopy > 2 && i == L / 2) {
+          CK(hipMemcpyAsync(hq, dbuf, 1024, hipMemcpyDeviceToHost, st));
+          CK(hipMemcpyAsync(dbuf, hp, 1024, hipMemcpyHostToDevice, st));
+        }
+        if (zc && (i == 0 || i == L / 2 || i == L - 1)) hipLaunchKernelGGL(k_zc, dim3(1), dim3(64), 0, st, hp, hq, d);
+        else hipLaunchKernelGGL(k_tiny, dim3(1), dim3(64), 0, st, d);
+      }
+      if (ncopy) CK(hipMemcpyAsync(hq, dbuf, 1024, hipMemcpyDeviceToHost, st));
+      CK(hipStreamSynchronize(st));
+    }
+    return (now_us() - t0) / C;
+  };
+  run(0, false);
+  run(4, false);
+  run(0, true);
+  double v[4][5];
+  for (int r = 0; r < 5; r++) {
+    v[0][r] = run(0, false);
+    v[1][r] = run(2, false);
+    v[2][r] = run(4, false);
+    v[3][r] = run(0, true);
+  }
+  const char* nm[4] = {"no_copies_us", "copies2_us", "copies4_us", "zero_copy_us"};
+  printf("{\"launches_per_call\": %d, \"calls\": %d", L, C);
+  for (int k = 0; k < 4; k++) {
+    printf(", \"%s\": [", nm[k]);
+    for (int r = 0; r < 5; r++) printf("%s%.1f", r ? ", " : "", v[k][r]);
+    printf("]");
+  }
+  printf("}\n");
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && argv[1][0] == 'c') return copies_ab(argc > 2 ? atoi(argv[2]) : 16, argc > 3 ? atoi(argv[3]) : 2000);
   if (argc > 1 && argv[1][0] == 'a') return args_ab(argc > 2 ? atoi(argv[2]) : 20, argc > 3 ? atoi(argv[3]) : 2000);
   const int L = argc > 1 ? atoi(argv[1]) : 32, C = argc > 2 ? atoi(argv[2]) : 2000;
   int* d;
