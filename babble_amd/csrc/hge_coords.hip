@@ -154,11 +154,19 @@ constexpr int LASEQ_MAX = 8192;
 // the block.
 // qlo (non-null): blocks 1 .. N take k_fd_qlo's work for chain blockIdx.x - 1 (it
 // reads only the old events' LA rows; one launch less per online call)
+// fst (non-null): the grid's last block takes k_frontier_start's work (the rounds
+// walk's first round and k_fss rows, written to fst / fst_lo; it reads only the old
+// events' rounds and the C rows: one launch less per online call)
 template <int NP>
 __global__ void __launch_bounds__(256) k_la_seq(Tables t, int n0, int n1, const UpEv* up, UpDst dst,
-                                                const int32_t* qolen, const int32_t* qlen, int32_t* qlo) {
+                                                const int32_t* qolen, const int32_t* qlen, int32_t* qlo,
+                                                int32_t* fst, int32_t* fst_lo) {
   __shared__ int rows[LASEQ_MAX];
   __shared__ int2 par[LASEQ_MAX / NP];
+  if (fst && blockIdx.x == gridDim.x - 1) {
+    frontier_start_body(t, qolen, qlen, fst, fst_lo, nullptr, nullptr, 0);
+    return;
+  }
   if (blockIdx.x > 0) {
     fd_qlo_body(t, qolen, qlen, qlo, blockIdx.x - 1);
     return;

@@ -159,9 +159,12 @@ struct hge_engine {
   DBuf<uint8_t> s_segdec;
   DBuf<uint64_t> s_segfws;
   DBuf<int32_t> s_recv, s_rr, s_fund, s_upos, s_und2, s_bpos, s_vis;
+  bool vis_all = false;  // this batch: one call seeing every event (no visibility table)
   DBuf<int64_t> s_cts;
   DBuf<unsigned char> s_keys, s_keys2;
   DBuf<int32_t> s_part, s_fst;
+  bool fst_fused = false;  // this batch's k_la_seq ran k_frontier_start's block
+  bool asg_fused = false;  // this attempt's rounds walk assigned the new events' rounds
   // coordinate sweeps: transposed tables and scratch
   int n_sweeps = 0;
   DBuf<int32_t> d_FDT, s_chg, s_bar, s_dirty;
@@ -894,6 +897,7 @@ struct hge_engine {
     coords_b();
   }
   bool coords_a() {
+    fst_fused = false;
     upload();
     if (wide32_pending) to_wide32();
     const int64_t n0 = n_coords, n1 = n_events;
@@ -1000,6 +1004,7 @@ struct hge_engine {
       if (N > 32) flk = frontier_lock();
       int32_t rs[3] = {R, 0, 0};
       if (retry) h2d(k_rs, rs, 12);
+      asg_fused = false;
       t = tables();
       const int NP = (N + 15) & ~15;
       if (N > 32 && (wide32 || frontier_fallback)) {
@@ -1017,14 +1022,21 @@ struct hge_engine {
           // stay on the device (k_frontier_start writes them; k_fss loops over the
           // count, k_rounds_walk stands down at INF32): no host round trip
           s_fst.need(N + 1);
-          KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p, k_lo,
-                  (int32_t*)nullptr, (uint64_t*)nullptr, 0);
+          if (!fst_fused || retry)  // (else k_la_seq's last block wrote them)
+            KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p, k_lo,
+                    (int32_t*)nullptr, (uint64_t*)nullptr, 0);
           const int64_t guess = m + 16 * (int64_t)N;  // the grid loops past it
+          // the walk's block also assigns the new events' rounds (k_round_assign's work)
+          und_appended = dividing && n_divided == n0;
+          s_newwit.need(m);
+          const RoundAssign ra{(int)n0, (int)n1, s_newwit.p, k_rs + 2,
+                               und_appended ? d_und.p + n_und : (int32_t*)nullptr};
+          asg_fused = true;
 #define FSSD(NPC, LPC, B)                                                                              \
   KLAUNCH(k_fss<NPC>, dim3((unsigned)std::min<int64_t>(1024, div_up(guess * NPC, 256))), dim3(256), 0, st, t, \
           k_lo, k_lo + N, 0, (int32_t*)nullptr, (uint16_t*)d_FSS.p, (const int32_t*)(k_lo + 2 * N));          \
   KLAUNCH((k_rounds_walk<NPC, LPC, B>), dim3(1), dim3(1024), 0, st, t, (const uint16_t*)d_FSS.p, k_len,       \
-          k_len + N, k_rs, 0, Rprev, dbg_p(), (const int32_t*)s_fst.p);
+          k_len + N, k_rs, 0, Rprev, dbg_p(), (const int32_t*)s_fst.p, ra);
           if (NP == 16) {
             FSSD(16, 4, 256)
           } else {
@@ -1078,12 +1090,12 @@ struct hge_engine {
               (const int32_t*)s_hn.p, (const int4*)s_hres.p, nw, Hcap, k_rs, resume);              \
       KLAUNCH((k_rounds_walk<NPC, LPC, B>), dim3(1), dim3(1024), 0, st, t,                         \
               (const uint16_t*)d_FSS.p, k_len, k_len + N, k_rs, 0, 0, dbg_p(),                     \
-              (const int32_t*)resume);                                                             \
+              (const int32_t*)resume, RoundAssign{0, 0, nullptr, nullptr, nullptr});               \
       if (getenv("HGE_WALK_DEBUG")) walk_debug(nw);                                               \
     } else {                                                                                       \
       KLAUNCH((k_rounds_walk<NPC, LPC, B>), dim3(1), dim3(1024), 0, st, t,                         \
               (const uint16_t*)d_FSS.p, k_len, k_len + N, k_rs, rlo, Rprev, dbg_p(),               \
-              (const int32_t*)nullptr);                                                            \
+              (const int32_t*)nullptr, RoundAssign{0, 0, nullptr, nullptr, nullptr});              \
     }                                                                                              \
   } else {                                                                                         \
     KLAUNCH(k_fss<NPC>, dim3(div_up((int64_t)tot * NPC, 256)), dim3(256), 0, st, t, k_lo, k_lo + N, \
@@ -1109,7 +1121,7 @@ struct hge_engine {
         s_newwit.need((size_t)Rcap * N);
         KLAUNCH(k_round_ranges, dim3(div_up((int64_t)Rcap * N, 256)), dim3(256), 0, st, t, k_len + N,
                 (const int32_t*)k_rs, s_newwit.p, k_rs + 2);
-      } else {
+      } else if (!asg_fused) {
         // DivideRounds right after (divide()) with nothing coordinated but undivided:
         // the new ids join the undetermined list here (no k_iota launch)
         und_appended = dividing && n_divided == n0;
@@ -1179,6 +1191,7 @@ struct hge_engine {
     }
     n_coords = n1;
     coords_len = chain_len;
+    fst_fused = false;
     prof_collect();
   }
 
@@ -1628,12 +1641,20 @@ struct hge_engine {
       // table filled by the same kernel
       // (+ k_fd_qlo's N blocks past a fresh state: coords_b skips its launch)
       const bool q = !fresh;
+      // (+ k_frontier_start's block when coords_b walks as an online call)
+      int maxlen = 0;
+      for (int c = 0; c < N; c++) maxlen = std::max(maxlen, chain_len[c]);
+      fst_fused = q && maxlen < 0xFFFF;
+      if (fst_fused) s_fst.need(N + 1);
+      int32_t* fp = fst_fused ? s_fst.p : (int32_t*)nullptr;
+      int32_t* fl = fst_fused ? k_lo : (int32_t*)nullptr;
+      const int nb = (q ? 1 + N : 1) + (fst_fused ? 1 : 0);
       if (N <= 16)
-        KLAUNCH(k_la_seq<16>, dim3(q ? 1 + N : 1), dim3(256), 0, st, t, (int)n_coords, (int)n_events, fill_up,
-                fill_dst, olen, len, q ? k_qlo : (int32_t*)nullptr);
+        KLAUNCH(k_la_seq<16>, dim3(nb), dim3(256), 0, st, t, (int)n_coords, (int)n_events, fill_up,
+                fill_dst, olen, len, q ? k_qlo : (int32_t*)nullptr, fp, fl);
       else
-        KLAUNCH(k_la_seq<32>, dim3(q ? 1 + N : 1), dim3(256), 0, st, t, (int)n_coords, (int)n_events, fill_up,
-                fill_dst, olen, len, q ? k_qlo : (int32_t*)nullptr);
+        KLAUNCH(k_la_seq<32>, dim3(nb), dim3(256), 0, st, t, (int)n_coords, (int)n_events, fill_up,
+                fill_dst, olen, len, q ? k_qlo : (int32_t*)nullptr, fp, fl);
       qlo_fused = q;
       n_sweeps = 1;
     } else {
@@ -1780,6 +1801,11 @@ struct hge_engine {
     const int R_last = spl ? Rc[sp.cb[sp.part + 1] - 1] : Rc[ncalls - 1];
     const int nr = ord ? std::max(0, R_last - rr_lo) : 0;
 
+    // the results block's size (counters | per-call counts | order | per-block transaction
+    // sums), known before DecideFame: the single-call fame kernel writes its header
+    const size_t o_tx0 = (8 + (size_t)ncalls + (ord ? ncand : 0) + 1) & ~(size_t)1;
+    const int ntxb0 = ord ? div_up(ncand, 256) : 0;
+    bool hdr_done = false;
     // ---- DecideFame windows (host enumeration of (round, call) pairs) + control block ----
     std::vector<int32_t> pr_round, pr_off, pr_cf, pr_len;
     int npairs = 0, nrounds = 0;
@@ -1863,6 +1889,32 @@ struct hge_engine {
       s_decbit.need(npairs);
       s_LCR.need(ncalls);
       s_clast.need(nrounds);
+      bool full = true;
+      for (int k = 0; k < nrounds && full; k++) full = pr_cf[k] + pr_len[k] == ncalls;
+      // one call at N < 64 (an online call): decide, timeline, LCR and the results
+      // header in one single-block launch (their grids were a block or two each)
+      const int Gf = group_lanes();
+      if (ncalls == 1 && full && N < 64 && !split_on() && !rec_on && (int64_t)npairs * N <= 8192 &&
+          (int64_t)nrounds * Gf <= 8192) {
+        s_out.need(o_tx0 + 2 * (size_t)ntxb0);
+        int32_t* hdr = s_out.p;
+#define FCALL(GG)                                                                                     \
+  KLAUNCH(k_fame_call<GG>, dim3(1), dim3(1024), 0, st, t, c_pr, c_pr + nrounds, c_pr + 2 * nrounds,    \
+          c_pr + 3 * nrounds, nrounds, npairs, c_nc, c_Rc, s_dec.p, s_decbit.p, c_Lc, ncalls, lcr,       \
+          s_LCR.p, s_clast.p, c_flags, hdr, 8 + ncalls);
+        if (Gf == 16) {
+          FCALL(16)
+        } else if (Gf == 32) {
+          FCALL(32)
+        } else {
+          FCALL(64)
+        }
+#undef FCALL
+        hdr_done = true;
+        x_iter++;
+        lcr_dev = true;
+        break;
+      }
       fame_dispatch(0, t, nrounds, npairs, ncalls, &pr_round, &pr_off);
       if (rec_on && !split_on()) {
         rec_dec.emplace_back((size_t)npairs * N);
@@ -1871,8 +1923,6 @@ struct hge_engine {
       x_iter++;
       KLAUNCH(k_lcr_scan, dim3(1), dim3(1024), 0, st, c_Lc, ncalls, lcr, s_LCR.p, c_pr,
               c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds, s_clast.p, c_flags);
-      bool full = true;
-      for (int k = 0; k < nrounds && full; k++) full = pr_cf[k] + pr_len[k] == ncalls;
       if (full) {
         lcr_dev = true;
         break;
@@ -1888,8 +1938,8 @@ struct hge_engine {
     // ---- DecideRoundReceived / FindOrder ----
     bool got_order = false;
     // results block: counters | per-call counts | order | per-block transaction sums
-    const size_t o_tx = (8 + (size_t)ncalls + (ord ? ncand : 0) + 1) & ~(size_t)1;
-    const int ntxb = ord ? div_up(ncand, 256) : 0;
+    const size_t o_tx = o_tx0;
+    const int ntxb = ntxb0;
     s_out.need(o_tx + 2 * (size_t)ntxb);
     int32_t* o_cnt = s_out.p;  // [0] received [1] undetermined [2] LCR events [4..5] tx
     int32_t* o_cc = s_out.p + 8;
@@ -1899,7 +1949,7 @@ struct hge_engine {
     // device holds it (one launch in place of a memset and a copy)
     // (folded into k_visibility's launch when that runs)
     const int32_t* lcr_src = lcr_dev ? (const int32_t*)(c_flags + 1) : (const int32_t*)nullptr;
-    if (!(ord && nr > 0))
+    if (!(ord && nr > 0) && !hdr_done)
       KLAUNCH(k_out_init, dim3(div_up(8 + ncalls, 256)), dim3(256), 0, st, s_out.p, 8 + ncalls, lcr_src);
     if (ord) {
       if (nr > 0) {
@@ -1916,10 +1966,19 @@ struct hge_engine {
           si.dec = nullptr;
         }
         s_segcnt.need(nr);
-        s_vis.need(std::max<int64_t>(n_coords, 1));
-        // first call at which each event is visible (arrivals, round received)
-        KLAUNCH(k_visibility, dim3(div_up(n_coords, 256) + div_up(8 + ncalls, 256)), dim3(256), 0, st,
-                (const int64_t*)c_nc, ncalls, (int)n_coords, s_vis.p, s_out.p, 8 + ncalls, lcr_src);
+        // first call at which each event is visible (arrivals, round received); one call
+        // that sees every event (an online call) needs no table: 0 for all, and the
+        // header is zeroed alone (a table of every event per call grew with the stream)
+        vis_all = ncalls == 1 && calls[0] >= n_coords;
+        if (vis_all) {
+          if (!hdr_done)
+            KLAUNCH(k_out_init, dim3(div_up(8 + ncalls, 256)), dim3(256), 0, st, s_out.p, 8 + ncalls, lcr_src);
+        } else {
+          s_vis.need(std::max<int64_t>(n_coords, 1));
+          KLAUNCH(k_visibility, dim3(div_up(n_coords, 256) + div_up(8 + ncalls, 256)), dim3(256), 0, st,
+                  (const int64_t*)c_nc, ncalls, (int)n_coords, s_vis.p, s_out.p, 8 + ncalls, lcr_src);
+        }
+        const int32_t* visp = vis_all ? (const int32_t*)nullptr : (const int32_t*)s_vis.p;
         // one pass into per-round capacity slots (no count round trip); theta inline
         // for N <= 64, by k_seg_theta_wide above
         const int G = group_lanes();
@@ -1932,7 +1991,7 @@ struct hge_engine {
         segoff_p = c_sgo;
 #define SEG1(GG, SPL)                                                                              \
   KLAUNCH((k_segments_1p<GG, SPL>), dim3(div_up((int64_t)nr * GG, 256)), dim3(256), 0, st, t,      \
-          rr_lo, nr, ncalls, (const int32_t*)s_vis.p, si, (const int32_t*)c_sgo, s_segcnt.p,       \
+          rr_lo, nr, ncalls, visp, si, (const int32_t*)c_sgo, s_segcnt.p,                          \
           s_segcall.p, s_seground.p, s_segdec.p, s_segfws.p, s_theta.p);
 #define THW(B)                                                                                     \
   if (wide32)                                                                                      \
@@ -2368,7 +2427,7 @@ struct hge_engine {
 #define RCASE(B)                                                                                 \
   case B:                                                                                        \
     KLAUNCH(k_round_received<B>, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, \
-                       ncand, (const int32_t*)s_vis.p, ncalls, 0, rr_lo, R_last, segoff_p,     \
+                       ncand, vis_all ? (const int32_t*)nullptr : (const int32_t*)s_vis.p, ncalls, 0, rr_lo, R_last, segoff_p, \
                        s_segcnt.p,                                                               \
                        s_segcall.p, s_segdec.p, s_segfws.p, s_theta.p, s_recv.p, s_rr.p,         \
                        s_cts.p, bseg);                                                           \

@@ -579,10 +579,10 @@ __device__ __forceinline__ int net16_packed(uint32_t R0, uint32_t R1, int q, int
 }
 
 template <int NPC, int LPC, int B>
-__global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* FSS,
-                                                      const int32_t* olen, const int32_t* len,
-                                                      int32_t* rstate, int rlo_arg, int Rprev,
-                                                      uint64_t* dbg, const int32_t* rlo_dev) {
+__device__ __forceinline__ void rounds_walk_body(const Tables& t, const uint16_t* FSS,
+                                                 const int32_t* olen, const int32_t* len,
+                                                 int32_t* rstate, int rlo_arg, int Rprev,
+                                                 uint64_t* dbg, const int32_t* rlo_dev) {
   // rlo_dev (non-null): the round to resume from, written by k_walk_join (-1: the
   // speculative walk completed and there is nothing left to walk)
   // (k_frontier_start's INF32: no new event needs a round; an online call reads
@@ -831,9 +831,9 @@ __global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* 
 // so that an online call at N <= 32 needs no host round trip for them
 // zbar / zgran (non-null): the wide rounds walk's hand-off flags and its 2 ngran
 // granules, zeroed here in place of two memsets
-__global__ void k_frontier_start(Tables t, const int32_t* olen, const int32_t* len,
-                                 int32_t* out /* [0] rlo, [1..N] start positions */,
-                                 int32_t* lo_off, int32_t* zbar, uint64_t* zgran, int ngran) {
+__device__ __forceinline__ void frontier_start_body(const Tables& t, const int32_t* olen, const int32_t* len,
+                                                    int32_t* out, int32_t* lo_off, int32_t* zbar,
+                                                    uint64_t* zgran, int ngran) {
   if (zbar && threadIdx.x < 2) zbar[threadIdx.x] = 0;
   if (zgran)
     for (int i = threadIdx.x; i < ngran; i += blockDim.x) zgran[i] = 0;
@@ -870,17 +870,21 @@ __global__ void k_frontier_start(Tables t, const int32_t* olen, const int32_t* l
     lo_off[2 * N] = tot;
   }
 }
+__global__ void k_frontier_start(Tables t, const int32_t* olen, const int32_t* len,
+                                 int32_t* out /* [0] rlo, [1..N] start positions */,
+                                 int32_t* lo_off, int32_t* zbar, uint64_t* zgran, int ngran) {
+  frontier_start_body(t, olen, len, out, lo_off, zbar, zgran, ngran);
+}
 
 // round(x) = max r with C[r][cx] <= px; witness iff C[round][cx] == px
 // (consecutive events share a round: the per-round counts and the new-witness
 // slots are aggregated per wave before touching global atomics)
 // und_app (non-null: DivideRounds of an online call): the new ids are appended to the
 // undetermined list there too (in place of a k_iota launch)
-__global__ void k_round_assign(Tables t, int n0, int n1, const int32_t* rstate, int32_t* newwit,
-                               int32_t* nnewwit, int32_t* und_app) {
+__device__ __forceinline__ void round_assign_item(const Tables& t, int x, int n0, int n1, const int32_t* rstate,
+                                                  int32_t* newwit, int32_t* nnewwit, int32_t* und_app) {
   if (rstate[1]) return;  // the rounds table overflowed: the host grows it and walks again
   const int R = rstate[0];
-  const int x = n0 + blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = x < n1;
   if (und_app && valid) und_app[x - n0] = x;
   const int N = t.N;
@@ -915,6 +919,30 @@ __global__ void k_round_assign(Tables t, int n0, int n1, const int32_t* rstate, 
     if (lane == leader) base = atomicAdd(nnewwit, __popcll(wm));
     base = __shfl(base, leader);
     if (w) newwit[base + __popcll(wm & ((1ull << lane) - 1))] = x;
+  }
+}
+__global__ void k_round_assign(Tables t, int n0, int n1, const int32_t* rstate, int32_t* newwit,
+                               int32_t* nnewwit, int32_t* und_app) {
+  round_assign_item(t, n0 + blockIdx.x * blockDim.x + threadIdx.x, n0, n1, rstate, newwit, nnewwit, und_app);
+}
+// k_round_assign's work appended to a single-block rounds walk (an online call at
+// N <= 32: one launch less); n1 <= n0: none
+struct RoundAssign {
+  int n0, n1;
+  int32_t* newwit;
+  int32_t* nnewwit;
+  int32_t* und_app;
+};
+template <int NPC, int LPC, int B>
+__global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* FSS,
+                                                      const int32_t* olen, const int32_t* len,
+                                                      int32_t* rstate, int rlo_arg, int Rprev,
+                                                      uint64_t* dbg, const int32_t* rlo_dev, RoundAssign ra) {
+  rounds_walk_body<NPC, LPC, B>(t, FSS, olen, len, rstate, rlo_arg, Rprev, dbg, rlo_dev);
+  if (ra.n1 > ra.n0) {
+    __syncthreads();  // the walk's C rows and round count (global) are visible to the block
+    for (int b = ra.n0; b < ra.n1; b += blockDim.x)
+      round_assign_item(t, b + (int)threadIdx.x, ra.n0, ra.n1, rstate, ra.newwit, ra.nnewwit, ra.und_app);
   }
 }
 
@@ -1101,13 +1129,10 @@ __global__ void __launch_bounds__(256) k_round_tail(Tables t, const int32_t* new
 // ---------------------------------------------------------------------------
 // (N % 64 == 0 takes k_fame_decide_blk below: one pair per block, rows in LDS.)
 template <int NWT>
-__global__ void k_fame_decide(Tables t, const int32_t* pr_round, const int32_t* pr_off,
-                              const int32_t* pr_cf, int nrounds, int p0, int npairs,
-                              const int64_t* nc, const int32_t* Rc, uint8_t* dec) {
-  // pairs [p0, npairs): a part of a split replay decides the pairs of its rounds only
-  // (pr_* then start at its first round; pair indices stay absolute)
-  // (XCD-aware order: neighbouring pairs read the same rounds' witness rows)
-  const int item = (int)xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void fame_decide_item(const Tables& t, int item, const int32_t* pr_round,
+                                                 const int32_t* pr_off, const int32_t* pr_cf, int nrounds,
+                                                 int p0, int npairs, const int64_t* nc, const int32_t* Rc,
+                                                 uint8_t* dec) {
   const int N = t.N, SM = t.SM;
   if (item >= (npairs - p0) * N) return;
   int p = item / N;
@@ -1199,6 +1224,16 @@ __global__ void k_fame_decide(Tables t, const int32_t* pr_round, const int32_t* 
     }
   }
   dec[(size_t)p * N + xd] = out;
+}
+template <int NWT>
+__global__ void k_fame_decide(Tables t, const int32_t* pr_round, const int32_t* pr_off,
+                              const int32_t* pr_cf, int nrounds, int p0, int npairs,
+                              const int64_t* nc, const int32_t* Rc, uint8_t* dec) {
+  // pairs [p0, npairs): a part of a split replay decides the pairs of its rounds only
+  // (pr_* then start at its first round; pair indices stay absolute)
+  // (XCD-aware order: neighbouring pairs read the same rounds' witness rows)
+  const int item = (int)xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  fame_decide_item<NWT>(t, item, pr_round, pr_off, pr_cf, nrounds, p0, npairs, nc, Rc, dec);
 }
 
 // k_fame_decide for N = 64 * NWT, one (round i, call c) pair per block of N
@@ -1294,10 +1329,10 @@ __global__ void __launch_bounds__(256) k_fame_decide_blk(Tables t, const int32_t
 
 // LCR_c = max(LCR_start, prefix max of Lc); c_last(i) = first call with LCR >= i;
 // coverage check of each round's speculative window.
-__global__ void __launch_bounds__(1024) k_lcr_scan(const int32_t* Lc, int ncalls, int lcr_start,
-                                                   int32_t* LCR, const int32_t* pr_round,
-                                                   const int32_t* pr_cf, const int32_t* pr_len,
-                                                   int nrounds, int32_t* clast, int32_t* flags) {
+__device__ __forceinline__ void lcr_scan_body(const int32_t* Lc, int ncalls, int lcr_start, int32_t* LCR,
+                                              const int32_t* pr_round, const int32_t* pr_cf,
+                                              const int32_t* pr_len, int nrounds, int32_t* clast,
+                                              int32_t* flags) {
   __shared__ int wm[16];
   const int T = blockDim.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int per = (ncalls + T - 1) / T;
@@ -1361,6 +1396,12 @@ __global__ void __launch_bounds__(1024) k_lcr_scan(const int32_t* Lc, int ncalls
     }
   }
 }
+__global__ void __launch_bounds__(1024) k_lcr_scan(const int32_t* Lc, int ncalls, int lcr_start,
+                                                   int32_t* LCR, const int32_t* pr_round,
+                                                   const int32_t* pr_cf, const int32_t* pr_len,
+                                                   int nrounds, int32_t* clast, int32_t* flags) {
+  lcr_scan_body(Lc, ncalls, lcr_start, LCR, pr_round, pr_cf, pr_len, nrounds, clast, flags);
+}
 
 // persisted fame after the batch: decisions up to c_last(i); one lane per
 // (processed round, witness slot), coalesced over the slots
@@ -1405,15 +1446,14 @@ __device__ __forceinline__ int group_min(int v) {
 // k_fame_timeline with one group per processed round (G lanes; a lane holds
 // SPL witness slots d + 64k when N > 64)
 template <int G, int SPL>
-__global__ void __launch_bounds__(256) k_fame_timeline_g(Tables t, const int32_t* pr_round,
-                                                         const int32_t* pr_off, const int32_t* pr_cf,
-                                                         const int32_t* pr_len, int nrounds,
-                                                         const int64_t* nc, const uint8_t* dec,
-                                                         uint8_t* decbit, int32_t* Lc) {
+__device__ __forceinline__ void fame_timeline_group(const Tables& t, int64_t gthread, const int32_t* pr_round,
+                                                    const int32_t* pr_off, const int32_t* pr_cf,
+                                                    const int32_t* pr_len, int nrounds, const int64_t* nc,
+                                                    const uint8_t* dec, uint8_t* decbit, int32_t* Lc) {
   static_assert(SPL == 1 || G == 64, "several slots per lane need full-wave groups");
   const int N = t.N;
   const int lane = threadIdx.x & 63, d = lane & (G - 1);
-  const int ri = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G);
+  const int ri = (int)(gthread / G);
   const uint64_t gm = group_mask<G>(lane);
   const bool valid = ri < nrounds;  // uniform per group
   const int i = valid ? pr_round[ri] : 0;
@@ -1468,6 +1508,41 @@ __global__ void __launch_bounds__(256) k_fame_timeline_g(Tables t, const int32_t
     }
   }
 }
+template <int G, int SPL>
+__global__ void __launch_bounds__(256) k_fame_timeline_g(Tables t, const int32_t* pr_round,
+                                                         const int32_t* pr_off, const int32_t* pr_cf,
+                                                         const int32_t* pr_len, int nrounds,
+                                                         const int64_t* nc, const uint8_t* dec,
+                                                         uint8_t* decbit, int32_t* Lc) {
+  fame_timeline_group<G, SPL>(t, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, pr_round, pr_off, pr_cf, pr_len,
+                              nrounds, nc, dec, decbit, Lc);
+}
+
+// An online call's DecideFame at N < 64 in ONE launch (in place of k_fame_decide,
+// k_fame_timeline_g and k_lcr_scan, plus k_out_init's results header): one block of
+// 1024 threads, the three stages behind block barriers (their grids were one or two
+// blocks each for a single call).  out (non-null): the header zeroed with the new
+// LastConsensusRound at out[3].
+template <int G>
+__global__ void __launch_bounds__(1024) k_fame_call(Tables t, const int32_t* pr_round, const int32_t* pr_off,
+                                                    const int32_t* pr_cf, const int32_t* pr_len, int nrounds,
+                                                    int npairs, const int64_t* nc, const int32_t* Rc,
+                                                    uint8_t* dec, uint8_t* decbit, int32_t* Lc, int ncalls,
+                                                    int lcr_start, int32_t* LCR, int32_t* clast, int32_t* flags,
+                                                    int32_t* out, int nout) {
+  const int tid = threadIdx.x;
+  for (int it = tid; it < npairs * t.N; it += blockDim.x)
+    fame_decide_item<1>(t, it, pr_round, pr_off, pr_cf, nrounds, 0, npairs, nc, Rc, dec);
+  __syncthreads();  // the decisions (global) are visible to the block
+  for (int64_t b = 0; b < (int64_t)nrounds * G; b += blockDim.x)
+    fame_timeline_group<G, 1>(t, b + tid, pr_round, pr_off, pr_cf, pr_len, nrounds, nc, dec, decbit, Lc);
+  __syncthreads();
+  lcr_scan_body(Lc, ncalls, lcr_start, LCR, pr_round, pr_cf, pr_len, nrounds, clast, flags);
+  if (out) {
+    __syncthreads();
+    for (int i = tid; i < nout; i += blockDim.x) out[i] = i == 3 ? flags[1] : 0;
+  }
+}
 
 // ---------------------------------------------------------------------------
 // Round-state segments for DecideRoundReceived (hashgraph.go:676-721): for each
@@ -1485,7 +1560,8 @@ struct SegInfo {
 };
 
 // first call of the batch at which witness W[r][d] is visible (INF32: none / later)
-// vis[x] = first call whose event count exceeds x (ncalls: none), for the
+// vis[x] = first call whose event count exceeds x (ncalls: none; the readers take
+// a null table as 0 everywhere: one call that sees every event), for the
 // events [0, nev): a block takes 256 consecutive events and binary-searches
 // them in an LDS window of the calls from the first one that sees its first
 // event (the global search is the fallback past the window)
@@ -1559,7 +1635,10 @@ __global__ void __launch_bounds__(256) k_segments_1p(Tables t, int rr_lo, int nr
     known[k] = val[k] = false;
     if (slot[k]) {
       const int x = t.W[(size_t)i * N + sl];
-      if (x >= 0 && vis[x] < ncalls) a[k] = vis[x];
+      if (x >= 0) {
+        const int vx = vis ? vis[x] : 0;  // null: one call that sees every event
+        if (vx < ncalls) a[k] = vx;
+      }
       if (SPL == 1 && x >= 0) row = sl * t.ccap + t.index[x];
       const uint8_t f = t.fame[(size_t)i * N + sl];  // persisted BEFORE this batch's update
       known[k] = f != 0;
@@ -1817,7 +1896,7 @@ __global__ void k_round_received(Tables t, const int32_t* cand, int ncand, const
   const int cx = t.creator[x], ix = t.index[x];
   const int rx = t.round[x];
   // first call at which x is visible
-  const int c0 = max(call_lo, vis[x]);
+  const int c0 = max(call_lo, vis ? vis[x] : 0);  // null: one call that sees every event
   int best = INF32, rr = -1, bseg = -1;
   for (int i = rx + 1; i < R_last; i++) {
     const int qi = i - rr_lo;
