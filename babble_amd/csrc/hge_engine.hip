@@ -1806,6 +1806,7 @@ struct hge_engine {
     const size_t o_tx0 = (8 + (size_t)ncalls + (ord ? ncand : 0) + 1) & ~(size_t)1;
     const int ntxb0 = ord ? div_up(ncand, 256) : 0;
     bool hdr_done = false;
+    bool ocall = false;  // the order's stages ran as one launch (k_order_call)
     // ---- DecideFame windows (host enumeration of (round, call) pairs) + control block ----
     std::vector<int32_t> pr_round, pr_off, pr_cf, pr_len;
     int npairs = 0, nrounds = 0;
@@ -1989,6 +1990,68 @@ struct hge_engine {
         s_segfws.need(ns * NW);
         s_theta.need(ns * N);
         segoff_p = c_sgo;
+        // an online call at N <= 16: the order's stages in one single-block launch
+        // (k_order_call: segments, round received with its median, the call's bucket,
+        // the undetermined list, keys, the sort, the persisted fame)
+        ocall = vis_all && commit && N <= 16 && !spl && ncand <= SCAN_LDS && (int64_t)nr * G <= 65536 &&
+                (nrounds == 0 || lcr_dev) && !getenv("HGE_NO_ORDER_CALL");
+        if (ocall) {
+          s_recv.need(ncand);
+          s_rr.need(ncand);
+          s_cts.need(ncand);
+          s_fund.need(ncand);
+          s_upos.need(ncand);
+          s_bpos.need(2 * (size_t)ncalls + 2);
+          s_und2.need(d_und.n);
+          s_keys.need((size_t)ncand * sizeof(OKey));
+          s_keys2.need((size_t)ncand * sizeof(OKey));
+          OrderCall oc{};
+          oc.si = si;
+          oc.rr_lo = rr_lo;
+          oc.nr = nr;
+          oc.segoff = c_sgo;
+          oc.segcnt = s_segcnt.p;
+          oc.seg_call = s_segcall.p;
+          oc.seg_round = s_seground.p;
+          oc.seg_dec = s_segdec.p;
+          oc.seg_fws = s_segfws.p;
+          oc.theta = s_theta.p;
+          oc.cand = cand;
+          oc.ncand = ncand;
+          oc.R_last = R_last;
+          oc.recv = s_recv.p;
+          oc.rr = s_rr.p;
+          oc.cts = s_cts.p;
+          oc.cnt = o_cc;
+          oc.bpos = s_bpos.p;
+          oc.total = o_cnt;
+          oc.blist = s_bpos.p + ncalls;
+          oc.nblist = s_bpos.p + 2 * ncalls;
+          oc.f_und = s_fund.p;
+          oc.upos = s_upos.p;
+          oc.nund = o_cnt + 1;
+          oc.und_out = s_und2.p;
+          oc.k1 = (OKey*)s_keys.p;
+          oc.k2 = (OKey*)s_keys2.p;
+          oc.ev_rr = d_rr.p;
+          oc.ev_cts = d_cts.p;
+          oc.ntx = (unsigned long long*)(s_out.p + o_tx);
+          oc.ntxb = ntxb;
+          oc.ids = o_ids;
+          oc.pr = c_pr;
+          oc.nrounds = do_fame ? nrounds : 0;
+          oc.clast = s_clast.p;
+          oc.dec = s_dec.p;
+          oc.nc = c_nc;
+          oc.flags = c_flags;
+          oc.lcr_old = lcr;
+          oc.n_lo = (int)std::min<int64_t>(calls[0], n_coords);
+          oc.n1 = (int)n_coords;
+          oc.lcre_out = o_cnt + 2;
+          KLAUNCH(k_order_call<16>, dim3(1), dim3(1024), 0, st, t, oc);
+          std::swap(d_und, s_und2);
+          got_order = true;
+        }
 #define SEG1(GG, SPL)                                                                              \
   KLAUNCH((k_segments_1p<GG, SPL>), dim3(div_up((int64_t)nr * GG, 256)), dim3(256), 0, st, t,      \
           rr_lo, nr, ncalls, visp, si, (const int32_t*)c_sgo, s_segcnt.p,                          \
@@ -2004,7 +2067,7 @@ struct hge_engine {
             (const uint64_t*)s_segfws.p, s_theta.p, dbg_p());
         // the frontier rows transposed (WLA) for the batch's rounds: theta (N > 64) and
         // the median (N > 16) read them
-        const bool wla = N > 16 && R_last > rr_lo;
+        const bool wla = N > 16 && R_last > rr_lo && !ocall;
         if (wla) {
           d_WLA.need((size_t)Rcap * N * N);
           if (N > 64 && !wide32) d_WLR.need((size_t)Rcap * N * N);
@@ -2013,7 +2076,9 @@ struct hge_engine {
                   rr_lo);
           t = tables();
         }
-        if (G == 16) {
+        if (ocall) {
+          // (k_order_call above)
+        } else if (G == 16) {
           SEG1(16, 1)
         } else if (G == 32) {
           SEG1(32, 1)
@@ -2049,10 +2114,12 @@ struct hge_engine {
           }
         }
         // round-received per candidate
-        s_recv.need(ncand);
-        s_rr.need(ncand);
-        s_cts.need(ncand);
-        recv_dispatch(t, cand, ncand, ncalls, rr_lo, R_last, fresh_und, wla);
+        if (!ocall) {
+          s_recv.need(ncand);
+          s_rr.need(ncand);
+          s_cts.need(ncand);
+          recv_dispatch(t, cand, ncand, ncalls, rr_lo, R_last, fresh_und, wla);
+        }
       } else {
         s_recv.need(ncand);
         HIPCHK(hipMemsetAsync(s_recv.p, 0xFF, 4 * ncand, st));
@@ -2066,71 +2133,73 @@ struct hge_engine {
       }
       // compaction + the order as call buckets (the received count stays on the
       // device: o_cnt[0])
-      s_fund.need(ncand);
-      s_upos.need(ncand);
-      s_rr.need(ncand);
-      s_cts.need(ncand);
-      // an online call's flags, buckets and undetermined list: one launch (k_recv_list_und below)
-      const bool rlu = commit && ncand <= 16384 && ncalls <= 8;
-      if (!rlu)
-        KLAUNCH(k_recv_flags, dim3(div_up(ncand, 256)), dim3(256), 0, st, s_recv.p, ncand,
-                (int32_t*)nullptr, s_fund.p, commit ? 1 : 0, commit ? o_cc : (int32_t*)nullptr);
-      if (!commit)
-        KLAUNCH(k_set_rr, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand, s_recv.p,
-                s_rr.p, s_cts.p, d_rr.p, d_cts.p, o_ntx, 0);
-      if (commit) {
-        s_bpos.need(2 * (size_t)ncalls + 2);
-        int32_t* blist = s_bpos.p + ncalls;     // non-empty buckets
-        int32_t* nblist = s_bpos.p + 2 * ncalls;  // their count
-        // a small candidate set: the undetermined list's scan and scatter ride with the
-        // call buckets (k_list_und; the list swap below is the same)
-        const bool lu = ncand <= 16384;
-        s_und2.need(d_und.n);
-        if (rlu)
-          KLAUNCH(k_recv_list_und, dim3(2), dim3(1024), 0, st, (const int32_t*)s_recv.p, (int)ncand, o_cc, ncalls,
-                  s_bpos.p, o_cnt, blist, nblist, s_fund.p, s_upos.p, o_cnt + 1, cand, s_und2.p);
-        else if (lu)
-          KLAUNCH(k_list_und, dim3(2), dim3(1024), 0, st, (const int32_t*)o_cc, ncalls, s_bpos.p, o_cnt, blist,
-                  nblist, (const int32_t*)s_fund.p, s_upos.p, (int)ncand, o_cnt + 1, cand, s_und2.p);
-        else
-          KLAUNCH(k_bucket_list, dim3(1), dim3(1024), 0, st, (const int32_t*)o_cc, ncalls, s_bpos.p,
-                  o_cnt, blist, nblist);
-        s_keys.need((size_t)ncand * sizeof(OKey));
-        s_keys2.need((size_t)ncand * sizeof(OKey));
-        OKey* k1 = (OKey*)s_keys.p;
-        OKey* k2 = (OKey*)s_keys2.p;
-        KLAUNCH(k_bucket_keys, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand, s_recv.p,
-                s_rr.p, s_cts.p, s_bpos.p, k1, d_rr.p, d_cts.p,
-                (unsigned long long*)(s_out.p + o_tx));
-        if (ncalls <= 8) {
-          // a few buckets (an online call): one launch, each bucket to the path its size takes
-          KLAUNCH(k_bucket_sort_all, dim3(ncalls), dim3(1024), 0, st, (const int32_t*)s_bpos.p,
-                  (const int32_t*)o_cc, (const int32_t*)blist, (const int32_t*)nblist, k1, k2, o_ids);
-        } else {
-          // buckets of 513 .. 2 * BIG_SORT keys in LDS (k_bucket_sort_big), the rest here
-          KLAUNCH(k_bucket_sort, dim3(std::min(ncalls, 2048)), dim3(256), 0, st,
-                  (const int32_t*)s_bpos.p, (const int32_t*)o_cc, (const int32_t*)blist,
-                  (const int32_t*)nblist, k1, k2, o_ids, 1);
-          if (ncand > 512)  // (no bucket past 512 keys otherwise)
-            KLAUNCH(k_bucket_sort_big, dim3(std::min(ncalls, n_cu())), dim3(1024), 0, st,
+      if (!ocall) {
+        s_fund.need(ncand);
+        s_upos.need(ncand);
+        s_rr.need(ncand);
+        s_cts.need(ncand);
+        // an online call's flags, buckets and undetermined list: one launch (k_recv_list_und below)
+        const bool rlu = commit && ncand <= 16384 && ncalls <= 8;
+        if (!rlu)
+          KLAUNCH(k_recv_flags, dim3(div_up(ncand, 256)), dim3(256), 0, st, s_recv.p, ncand,
+                  (int32_t*)nullptr, s_fund.p, commit ? 1 : 0, commit ? o_cc : (int32_t*)nullptr);
+        if (!commit)
+          KLAUNCH(k_set_rr, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand, s_recv.p,
+                  s_rr.p, s_cts.p, d_rr.p, d_cts.p, o_ntx, 0);
+        if (commit) {
+          s_bpos.need(2 * (size_t)ncalls + 2);
+          int32_t* blist = s_bpos.p + ncalls;     // non-empty buckets
+          int32_t* nblist = s_bpos.p + 2 * ncalls;  // their count
+          // a small candidate set: the undetermined list's scan and scatter ride with the
+          // call buckets (k_list_und; the list swap below is the same)
+          const bool lu = ncand <= 16384;
+          s_und2.need(d_und.n);
+          if (rlu)
+            KLAUNCH(k_recv_list_und, dim3(2), dim3(1024), 0, st, (const int32_t*)s_recv.p, (int)ncand, o_cc, ncalls,
+                    s_bpos.p, o_cnt, blist, nblist, s_fund.p, s_upos.p, o_cnt + 1, cand, s_und2.p);
+          else if (lu)
+            KLAUNCH(k_list_und, dim3(2), dim3(1024), 0, st, (const int32_t*)o_cc, ncalls, s_bpos.p, o_cnt, blist,
+                    nblist, (const int32_t*)s_fund.p, s_upos.p, (int)ncand, o_cnt + 1, cand, s_und2.p);
+          else
+            KLAUNCH(k_bucket_list, dim3(1), dim3(1024), 0, st, (const int32_t*)o_cc, ncalls, s_bpos.p,
+                    o_cnt, blist, nblist);
+          s_keys.need((size_t)ncand * sizeof(OKey));
+          s_keys2.need((size_t)ncand * sizeof(OKey));
+          OKey* k1 = (OKey*)s_keys.p;
+          OKey* k2 = (OKey*)s_keys2.p;
+          KLAUNCH(k_bucket_keys, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand, s_recv.p,
+                  s_rr.p, s_cts.p, s_bpos.p, k1, d_rr.p, d_cts.p,
+                  (unsigned long long*)(s_out.p + o_tx));
+          if (ncalls <= 8) {
+            // a few buckets (an online call): one launch, each bucket to the path its size takes
+            KLAUNCH(k_bucket_sort_all, dim3(ncalls), dim3(1024), 0, st, (const int32_t*)s_bpos.p,
+                    (const int32_t*)o_cc, (const int32_t*)blist, (const int32_t*)nblist, k1, k2, o_ids);
+          } else {
+            // buckets of 513 .. 2 * BIG_SORT keys in LDS (k_bucket_sort_big), the rest here
+            KLAUNCH(k_bucket_sort, dim3(std::min(ncalls, 2048)), dim3(256), 0, st,
                     (const int32_t*)s_bpos.p, (const int32_t*)o_cc, (const int32_t*)blist,
-                    (const int32_t*)nblist, (const OKey*)k1, k2, o_ids);
+                    (const int32_t*)nblist, k1, k2, o_ids, 1);
+            if (ncand > 512)  // (no bucket past 512 keys otherwise)
+              KLAUNCH(k_bucket_sort_big, dim3(std::min(ncalls, n_cu())), dim3(1024), 0, st,
+                      (const int32_t*)s_bpos.p, (const int32_t*)o_cc, (const int32_t*)blist,
+                      (const int32_t*)nblist, (const OKey*)k1, k2, o_ids);
+          }
+          // new undetermined list (in candidate order), scattered into the spare list
+          // (same capacity) and swapped: no device copy
+          if (!lu) {
+            scan_large(s_fund.p, s_upos.p, ncand, o_cnt + 1);
+            KLAUNCH(k_scatter_und, dim3(div_up(ncand, 256)), dim3(256), 0, st, cand, ncand, s_fund.p, s_upos.p,
+                    s_und2.p);
+          }
+          std::swap(d_und, s_und2);
+          got_order = true;
         }
-        // new undetermined list (in candidate order), scattered into the spare list
-        // (same capacity) and swapped: no device copy
-        if (!lu) {
-          scan_large(s_fund.p, s_upos.p, ncand, o_cnt + 1);
-          KLAUNCH(k_scatter_und, dim3(div_up(ncand, 256)), dim3(256), 0, st, cand, ncand, s_fund.p, s_upos.p,
-                  s_und2.p);
-        }
-        std::swap(d_und, s_und2);
-        got_order = true;
       }
     }
 
     // ---- persist fame / LCR ----
     bool lcr_up = false;
-    if (do_fame && nrounds > 0) {
+    if (do_fame && nrounds > 0 && !ocall) {
       if (lcr_dev) {
         // the persisted fame and RoundEvents(LCR - 1) as below (the new LCR and its
         // call read on the device) in one launch

@@ -138,10 +138,10 @@ __global__ void k_min_round_range(const int32_t* round, int lo, int hi, int32_t*
 // straight from HBM put 64 cache lines behind every load instruction: ~10 us at
 // 10k entries.)  scat: flags in[] are 0 / 1 (the compaction's case).
 constexpr int SCAN_LDS = 16384;
-__device__ __forceinline__ void scan_small_body(const int32_t* in, int32_t* out, int n, int32_t* total,
-                                                const int32_t* scat, int32_t* und) {
+// sv: SCAN_LDS + SCAN_LDS / 16 ints of LDS (the caller's: k_order_call lends its sort pool)
+__device__ __forceinline__ void scan_small_core(const int32_t* in, int32_t* out, int n, int32_t* total,
+                                                const int32_t* scat, int32_t* und, int* sv) {
   __shared__ int wsum[16];
-  __shared__ int sv[SCAN_LDS + SCAN_LDS / 16];
   const int T = blockDim.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int per = (n + T - 1) / T;
   const int lo = min(n, tid * per), hi = min(n, lo + per);
@@ -215,6 +215,11 @@ __device__ __forceinline__ void scan_small_body(const int32_t* in, int32_t* out,
     }
   }
   if (tid == T - 1 && total) *total = tot;
+}
+__device__ __forceinline__ void scan_small_body(const int32_t* in, int32_t* out, int n, int32_t* total,
+                                                const int32_t* scat, int32_t* und) {
+  __shared__ int sv[SCAN_LDS + SCAN_LDS / 16];
+  scan_small_core(in, out, n, total, scat, und, sv);
 }
 __global__ void __launch_bounds__(1024) k_scan_small(const int32_t* in, int32_t* out, int n, int32_t* total) {
   scan_small_body(in, out, n, total, nullptr, nullptr);
@@ -1610,16 +1615,14 @@ __global__ void __launch_bounds__(256) k_visibility(const int64_t* nc, int ncall
 // segment's theta row is computed by the same group as it is found (lane =
 // witness slot, then = creator); wider hashgraphs take k_seg_theta_wide.
 template <int G, int SPL>
-__global__ void __launch_bounds__(256) k_segments_1p(Tables t, int rr_lo, int nr, int ncalls,
-                                                     const int32_t* vis, SegInfo si,
-                                                     const int32_t* segoff, int32_t* segcnt,
-                                                     int32_t* seg_call, int32_t* seg_round,
-                                                     uint8_t* seg_dec, uint64_t* seg_fws,
-                                                     int32_t* theta) {
+__device__ __forceinline__ void segments_group(const Tables& t, int64_t gthread, int rr_lo, int nr, int ncalls,
+                                               const int32_t* vis, const SegInfo& si, const int32_t* segoff,
+                                               int32_t* segcnt, int32_t* seg_call, int32_t* seg_round,
+                                               uint8_t* seg_dec, uint64_t* seg_fws, int32_t* theta) {
   static_assert(SPL == 1 || G == 64, "several slots per lane need full-wave groups");
   const int N = t.N;
   const int lane = threadIdx.x & 63, d = lane & (G - 1);
-  const int qi = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G);
+  const int qi = (int)(gthread / G);
   const uint64_t gm = group_mask<G>(lane);
   const int gshift = (G == 64) ? 0 : (lane & ~(G - 1));
   const bool valid = qi < nr;  // uniform per group
@@ -1713,6 +1716,16 @@ __global__ void __launch_bounds__(256) k_segments_1p(Tables t, int rr_lo, int nr
     c = nxt;
   }
   if (valid && d == 0) segcnt[qi] = nseg;
+}
+template <int G, int SPL>
+__global__ void __launch_bounds__(256) k_segments_1p(Tables t, int rr_lo, int nr, int ncalls,
+                                                     const int32_t* vis, SegInfo si,
+                                                     const int32_t* segoff, int32_t* segcnt,
+                                                     int32_t* seg_call, int32_t* seg_round,
+                                                     uint8_t* seg_dec, uint64_t* seg_fws,
+                                                     int32_t* theta) {
+  segments_group<G, SPL>(t, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, rr_lo, nr, ncalls, vis, si, segoff,
+                         segcnt, seg_call, seg_round, seg_dec, seg_fws, theta);
 }
 
 // theta for N > 64: one 256-thread block per (round, segment stride), thread =
@@ -1882,14 +1895,13 @@ __global__ void __launch_bounds__(1024) k_seg_theta_wide(Tables t, const int32_t
 // at c and whose famous witnesses see x by strict majority.
 // ---------------------------------------------------------------------------
 template <int NWT>
-__global__ void k_round_received(Tables t, const int32_t* cand, int ncand, const int32_t* vis,
-                                 int ncalls, int call_lo, int rr_lo, int R_last,
-                                 const int32_t* segoff, const int32_t* segcnt,
-                                 const int32_t* seg_call, const uint8_t* seg_dec,
-                                 const uint64_t* seg_fws, const int32_t* theta,
-                                 int32_t* recv_call, int32_t* rr_out, int64_t* cts_out,
-                                 int32_t* bseg_out) {
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void round_received_item(const Tables& t, int q, const int32_t* cand, int ncand,
+                                                    const int32_t* vis, int ncalls, int call_lo, int rr_lo,
+                                                    int R_last, const int32_t* segoff, const int32_t* segcnt,
+                                                    const int32_t* seg_call, const uint8_t* seg_dec,
+                                                    const uint64_t* seg_fws, const int32_t* theta,
+                                                    int32_t* recv_call, int32_t* rr_out, int64_t* cts_out,
+                                                    int32_t* bseg_out) {
   if (q >= ncand) return;
   const int N = t.N;
   const int x = cand[q];
@@ -1981,6 +1993,18 @@ __global__ void k_round_received(Tables t, const int32_t* cand, int ncand, const
   recv_call[q] = best;
   rr_out[q] = rr;
   cts_out[q] = med;
+}
+template <int NWT>
+__global__ void k_round_received(Tables t, const int32_t* cand, int ncand, const int32_t* vis,
+                                 int ncalls, int call_lo, int rr_lo, int R_last,
+                                 const int32_t* segoff, const int32_t* segcnt,
+                                 const int32_t* seg_call, const uint8_t* seg_dec,
+                                 const uint64_t* seg_fws, const int32_t* theta,
+                                 int32_t* recv_call, int32_t* rr_out, int64_t* cts_out,
+                                 int32_t* bseg_out) {
+  round_received_item<NWT>(t, blockIdx.x * blockDim.x + threadIdx.x, cand, ncand, vis, ncalls, call_lo, rr_lo,
+                           R_last, segoff, segcnt, seg_call, seg_dec, seg_fws, theta, recv_call, rr_out, cts_out,
+                           bseg_out);
 }
 
 // The upper median over 32-bit order-preserving images (int32 timestamp offsets ^
@@ -2382,21 +2406,18 @@ __global__ void k_recv_flags(const int32_t* recv_call, int ncand, int32_t* f_rec
 // ---------------------------------------------------------------------------
 // (also records roundReceived / consensusTimestamp and sums the transactions,
 // as k_set_rr does outside a committing batch)
-__global__ void k_bucket_keys(Tables t, const int32_t* cand, int ncand, const int32_t* recv_call,
-                              const int32_t* rr, const int64_t* cts, int32_t* bpos, OKey* keys,
-                              int32_t* ev_rr, int64_t* ev_cts, unsigned long long* ntx_sum) {
-  // ntx_sum: one partial per block (launched with 256 threads)
-  __shared__ unsigned long long s_tx[4];
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+// candidate q's key into its call's bucket (a slot per wave and call by one atomic);
+// returns the wave's transaction count (every lane)
+__device__ __forceinline__ unsigned long long bucket_key_item(const Tables& t, int q, const int32_t* cand, int ncand,
+                                                              const int32_t* recv_call, const int32_t* rr,
+                                                              const int64_t* cts, int32_t* bpos, OKey* keys,
+                                                              int32_t* ev_rr, int64_t* ev_cts) {
   const int lane = threadIdx.x & 63;
   const int rc = q < ncand ? recv_call[q] : -1;
   const bool rec = rc >= 0;
   const int x = rec ? cand[q] : 0;
-  // transactions: a per-block partial (summed by the host), no global atomics
   unsigned long long tx = rec ? (unsigned long long)t.ntx[x] : 0;
   for (int o = 32; o > 0; o >>= 1) tx += __shfl_xor(tx, o);
-  if (lane == 0) s_tx[threadIdx.x >> 6] = tx;
-  // bucket slots: one atomic per distinct call in the wave
   int slot = 0;
   uint64_t pending = __ballot(rec);
   while (pending) {
@@ -2409,25 +2430,38 @@ __global__ void k_bucket_keys(Tables t, const int32_t* cand, int ncand, const in
     if (rec && rc == c) slot = base + __popcll(same & ((1ull << lane) - 1));
     pending &= ~same;
   }
+  if (rec) {
+    ev_rr[x] = rr[q];
+    ev_cts[x] = cts[q];
+    OKey k;
+    k.a = ((uint64_t)(uint32_t)rc << 32) | (uint32_t)rr[q];
+    k.b = (uint64_t)cts[q] ^ 0x8000000000000000ull;
+    k.s0 = t.S[4 * (size_t)x];
+    k.s1 = t.S[4 * (size_t)x + 1];
+    k.s2 = t.S[4 * (size_t)x + 2];
+    k.s3 = t.S[4 * (size_t)x + 3];
+    k.id = (uint32_t)x;
+    k.pad = 0;
+    keys[slot] = k;
+  }
+  return tx;
+}
+
+__global__ void k_bucket_keys(Tables t, const int32_t* cand, int ncand, const int32_t* recv_call,
+                              const int32_t* rr, const int64_t* cts, int32_t* bpos, OKey* keys,
+                              int32_t* ev_rr, int64_t* ev_cts, unsigned long long* ntx_sum) {
+  // ntx_sum: one partial per block (launched with 256 threads; summed by the host, no
+  // global atomics)
+  __shared__ unsigned long long s_tx[4];
+  const unsigned long long tx = bucket_key_item(t, blockIdx.x * blockDim.x + threadIdx.x, cand, ncand, recv_call,
+                                                rr, cts, bpos, keys, ev_rr, ev_cts);
+  if ((threadIdx.x & 63) == 0) s_tx[threadIdx.x >> 6] = tx;
   __syncthreads();
   if (threadIdx.x == 0) {
     unsigned long long bt = 0;
     for (int w = 0; w < (int)(blockDim.x >> 6); w++) bt += s_tx[w];
     ntx_sum[blockIdx.x] = bt;
   }
-  if (!rec) return;
-  ev_rr[x] = rr[q];
-  ev_cts[x] = cts[q];
-  OKey k;
-  k.a = ((uint64_t)(uint32_t)recv_call[q] << 32) | (uint32_t)rr[q];
-  k.b = (uint64_t)cts[q] ^ 0x8000000000000000ull;
-  k.s0 = t.S[4 * (size_t)x];
-  k.s1 = t.S[4 * (size_t)x + 1];
-  k.s2 = t.S[4 * (size_t)x + 2];
-  k.s3 = t.S[4 * (size_t)x + 3];
-  k.id = (uint32_t)x;
-  k.pad = 0;
-  keys[slot] = k;
 }
 
 __device__ __forceinline__ OKey okey_inf() {
@@ -2976,6 +3010,114 @@ __global__ void k_fame_persist_lcre(Tables t, const int32_t* pr_round, const int
                                     int n1, int32_t* out) {
   if ((int)blockIdx.x < nb_fp) fame_persist_body(t, pr_round, pr_off, pr_cf, pr_len, nrounds, clast, dec, blockIdx.x);
   else lcre_dev_body(t, nc, flags, lcr_old, n_lo, n1, out, blockIdx.x - nb_fp);
+}
+
+// An online call's DecideRoundReceived / FindOrder at N <= 16 in ONE launch (in place
+// of k_segments_1p, k_round_received, k_recv_list_und, k_bucket_keys,
+// k_bucket_sort_all and k_fame_persist_lcre): one block of 1024 threads, the stages
+// behind block barriers, the same bodies as those kernels (one call that sees every
+// event; the host checks the candidate count against the LDS scan and sort).
+struct OrderCall {
+  SegInfo si;  // segments
+  int rr_lo, nr;
+  const int32_t* segoff;
+  int32_t *segcnt, *seg_call, *seg_round;
+  uint8_t* seg_dec;
+  uint64_t* seg_fws;
+  int32_t* theta;
+  const int32_t* cand;  // round received and the median
+  int ncand, R_last;
+  int32_t *recv, *rr;
+  int64_t* cts;
+  int32_t *cnt, *bpos, *total, *blist, *nblist;  // the call's bucket
+  int32_t *f_und, *upos, *nund, *und_out;        // the new undetermined list
+  OKey *k1, *k2;                                 // keys and the sort
+  int32_t* ev_rr;
+  int64_t* ev_cts;
+  unsigned long long* ntx;
+  int ntxb;
+  int32_t* ids;
+  const int32_t* pr;  // persisted fame (nrounds > 0) and the LCR round's count
+  int nrounds;
+  const int32_t* clast;
+  const uint8_t* dec;
+  const int64_t* nc;
+  const int32_t* flags;
+  int lcr_old, n_lo, n1;
+  int32_t* lcre_out;
+};
+template <int G>
+__global__ void __launch_bounds__(1024) k_order_call(Tables t, OrderCall o) {
+  constexpr size_t BIG_LDS = (size_t)BIG_SORT * (8 + 4 + 4 + 2);
+  constexpr size_t POOL = BIG_LDS > sizeof(SortChunk<SORT_CH>) ? BIG_LDS : sizeof(SortChunk<SORT_CH>);
+  static_assert(POOL >= sizeof(int) * (SCAN_LDS + SCAN_LDS / 16), "the scan borrows the sort pool");
+  __shared__ __attribute__((aligned(16))) unsigned char pool[POOL];
+  __shared__ int s_cnt;
+  __shared__ unsigned long long s_tx[16];
+  const int tid = threadIdx.x, T = blockDim.x;
+  // the round-state segments of the batch's rounds (theta inline)
+  for (int64_t b = 0; b < (int64_t)o.nr * G; b += T)
+    segments_group<G, 1>(t, b + tid, o.rr_lo, o.nr, 1, nullptr, o.si, o.segoff, o.segcnt, o.seg_call, o.seg_round,
+                         o.seg_dec, o.seg_fws, o.theta);
+  __syncthreads();
+  // round received and the median timestamp (inline at N <= 16)
+  for (int q = tid; q < o.ncand; q += T)
+    round_received_item<1>(t, q, o.cand, o.ncand, nullptr, 1, 0, o.rr_lo, o.R_last, o.segoff, o.segcnt,
+                           o.seg_call, o.seg_dec, o.seg_fws, o.theta, o.recv, o.rr, o.cts, nullptr);
+  if (tid == 0) s_cnt = 0;
+  __syncthreads();
+  // the call's received count and its bucket (k_recv_list_und's block 0)
+  int c = 0;
+  for (int q = tid; q < o.ncand; q += T) c += o.recv[q] >= 0 ? 1 : 0;
+  for (int s2 = 32; s2 > 0; s2 >>= 1) c += __shfl_xor(c, s2);
+  if ((tid & 63) == 0 && c) atomicAdd(&s_cnt, c);
+  for (int q = tid; q < o.ncand; q += T) o.f_und[q] = o.recv[q] == -1 ? 1 : 0;
+  __syncthreads();
+  if (tid == 0) o.cnt[0] = s_cnt;
+  __syncthreads();
+  bucket_list_body(o.cnt, 1, o.bpos, o.total, o.blist, o.nblist);
+  __syncthreads();
+  // the new undetermined list in candidate order (its block 1)
+  scan_small_core(o.f_und, o.upos, o.ncand, o.nund, o.cand, o.und_out, (int*)pool);
+  __syncthreads();
+  // keys into the bucket, the transactions summed
+  unsigned long long tx = 0;
+  for (int b = 0; b < o.ncand; b += T)
+    tx += bucket_key_item(t, b + tid, o.cand, o.ncand, o.recv, o.rr, o.cts, o.bpos, o.k1, o.ev_rr, o.ev_cts);
+  if ((tid & 63) == 0) s_tx[tid >> 6] = tx;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long bt = 0;
+    for (int w = 0; w < T / 64; w++) bt += s_tx[w];
+    o.ntx[0] = bt;
+  }
+  for (int i = 1 + tid; i < o.ntxb; i += T) o.ntx[i] = 0;
+  __syncthreads();
+  // the sort (k_bucket_sort_all's path for the bucket's size)
+  {
+    uint64_t* sb = (uint64_t*)pool;
+    uint32_t* sr = (uint32_t*)(pool + (size_t)BIG_SORT * 8);
+    uint32_t* ss = (uint32_t*)(pool + (size_t)BIG_SORT * 12);
+    uint16_t* ix = (uint16_t*)(pool + (size_t)BIG_SORT * 16);
+    SortChunk<SORT_CH>& sc = *(SortChunk<SORT_CH>*)pool;
+    const int nl = *o.nblist;
+    for (int li = 0; li < nl; li++) {
+      const int b = o.blist[li];
+      const int nb = o.cnt[b];
+      if (nb > 512 && nb <= 2 * BIG_SORT) bucket_sort_big_one(b, nb, o.bpos, o.k1, o.k2, o.ids, sb, sr, ss, ix);
+      else bucket_sort_one(b, o.bpos, o.cnt, o.k1, o.k2, o.ids, false, sc);
+      __syncthreads();
+    }
+  }
+  // the persisted fame, read above by the segments as it was before this call, and
+  // RoundEvents(LCR - 1) (k_fame_persist_lcre)
+  if (o.nrounds > 0) {
+    const int np = o.nrounds;
+    for (int b = 0; (int64_t)b * T < (int64_t)np * t.N; b++)
+      fame_persist_body(t, o.pr, o.pr + np, o.pr + 2 * np, o.pr + 3 * np, np, o.clast, o.dec, b);
+    for (int b = 0; b == 0 || b * T < o.n1 - o.n_lo; b++)
+      lcre_dev_body(t, o.nc, o.flags, o.lcr_old, o.n_lo, o.n1, o.lcre_out, b);
+  }
 }
 
 // fresh consensus state: C = INF, W = -1, bitsets / fame / counts = 0, rr = -1

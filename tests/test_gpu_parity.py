@@ -90,6 +90,29 @@ def test_online_matches_replay(engines):
     eng.close()
 
 
+@pytest.mark.parametrize("n,E,k", [(16, 6000, 16), (16, 3000, 3), (32, 6000, 32), (12, 2000, 1)])
+def test_online_matches_oracle_single_block_paths(engines, n, E, k):
+    """Online calls at N <= 32 take the single-block stages (k_fame_call; k_order_call at
+    N <= 16; the frontier start in k_la_seq, the rounds assignment in the walk): the
+    order, every call's batch and the whole state equal the oracle's."""
+    from babble_amd.engine import Engine, events_array
+    dag = random_gossip(n, E, seed=41 + n + k)
+    calls = schedule(E, k)
+    o, ost, oorder, ocounts = oracle_run(dag, calls)
+    eng = Engine(n, 1 << 14)
+    ev = events_array(dag)
+    nxt, counts = 0, []
+    for c in calls:
+        eng.insert_events(ev[nxt:c].copy())  # submission index == id (no rejections)
+        counts.append(len(eng.run_consensus()))
+        nxt = c
+    np.testing.assert_array_equal(eng.consensus_events(), oorder)
+    np.testing.assert_array_equal(np.asarray(counts), np.asarray(ocounts))
+    with_creators(eng, dag, ost)
+    compare_state(eng, o)
+    eng.close()
+
+
 def test_split_calls_match_run_consensus(engines):
     """DivideRounds / DecideFame / FindOrder as separate calls (node/core.go:179-202)."""
     from babble_amd.engine import Engine, events_array
