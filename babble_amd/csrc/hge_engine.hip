@@ -1807,6 +1807,7 @@ struct hge_engine {
     const int ntxb0 = ord ? div_up(ncand, 256) : 0;
     bool hdr_done = false;
     bool ocall = false;  // the order's stages ran as one launch (k_order_call)
+    bool otail = false;  // the order's stages from the call's bucket on ran as one launch
     // ---- DecideFame windows (host enumeration of (round, call) pairs) + control block ----
     std::vector<int32_t> pr_round, pr_off, pr_cf, pr_len;
     int npairs = 0, nrounds = 0;
@@ -1895,14 +1896,40 @@ struct hge_engine {
       // one call at N < 64 (an online call): decide, timeline, LCR and the results
       // header in one single-block launch (their grids were a block or two each)
       const int Gf = group_lanes();
-      if (ncalls == 1 && full && N < 64 && !split_on() && !rec_on && (int64_t)npairs * N <= 8192 &&
-          (int64_t)nrounds * Gf <= 8192) {
+      const bool one = ncalls == 1 && full && !split_on() && !rec_on && (int64_t)nrounds * Gf <= 8192;
+      if (one && N >= 64) {
+        // the pairs by k_fame_decide_blk, then the timeline, LCR and the results header
+        // in one single-block launch (in place of k_fame_timeline_g, k_lcr_scan, k_out_init)
+        s_out.need(o_tx0 + 2 * (size_t)ntxb0);
+        int32_t* hdr = s_out.p;
+        fame_dispatch(0, t, nrounds, npairs, ncalls, &pr_round, &pr_off, true);
+        switch (NW) {
+#define FTAIL(B)                                                                                      \
+  case B:                                                                                             \
+    KLAUNCH((k_fame_call<64, B, false>), dim3(1), dim3(1024), 0, st, t, c_pr, c_pr + nrounds,          \
+            c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds, npairs, c_nc, c_Rc, s_dec.p, s_decbit.p,   \
+            c_Lc, ncalls, lcr, s_LCR.p, s_clast.p, c_flags, hdr, 8 + ncalls);                           \
+    break;
+          FTAIL(1)
+          FTAIL(2)
+          FTAIL(3)
+          FTAIL(4)
+#undef FTAIL
+          default:
+            throw EngineError(HGE_ERR_INTERNAL, "unsupported N");
+        }
+        hdr_done = true;
+        x_iter++;
+        lcr_dev = true;
+        break;
+      }
+      if (one && N < 64 && (int64_t)npairs * N <= 8192) {
         s_out.need(o_tx0 + 2 * (size_t)ntxb0);
         int32_t* hdr = s_out.p;
 #define FCALL(GG)                                                                                     \
-  KLAUNCH(k_fame_call<GG>, dim3(1), dim3(1024), 0, st, t, c_pr, c_pr + nrounds, c_pr + 2 * nrounds,    \
-          c_pr + 3 * nrounds, nrounds, npairs, c_nc, c_Rc, s_dec.p, s_decbit.p, c_Lc, ncalls, lcr,       \
-          s_LCR.p, s_clast.p, c_flags, hdr, 8 + ncalls);
+  KLAUNCH((k_fame_call<GG, 1, true>), dim3(1), dim3(1024), 0, st, t, c_pr, c_pr + nrounds,             \
+          c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds, npairs, c_nc, c_Rc, s_dec.p, s_decbit.p,     \
+          c_Lc, ncalls, lcr, s_LCR.p, s_clast.p, c_flags, hdr, 8 + ncalls);
         if (Gf == 16) {
           FCALL(16)
         } else if (Gf == 32) {
@@ -1952,6 +1979,68 @@ struct hge_engine {
     const int32_t* lcr_src = lcr_dev ? (const int32_t*)(c_flags + 1) : (const int32_t*)nullptr;
     if (!(ord && nr > 0) && !hdr_done)
       KLAUNCH(k_out_init, dim3(div_up(8 + ncalls, 256)), dim3(256), 0, st, s_out.p, 8 + ncalls, lcr_src);
+    // the single-block order kernel's arguments (k_order_call; front: the caller sets it)
+    auto order_call_args = [&](const SegInfo& si) {
+      s_recv.need(ncand);
+      s_rr.need(ncand);
+      s_cts.need(ncand);
+      s_fund.need(ncand);
+      s_upos.need(ncand);
+      s_bpos.need(2 * (size_t)ncalls + 2);
+      s_und2.need(d_und.n);
+      s_keys.need((size_t)ncand * sizeof(OKey));
+      s_keys2.need((size_t)ncand * sizeof(OKey));
+      OrderCall oc{};
+      oc.si = si;
+      oc.rr_lo = rr_lo;
+      oc.nr = nr;
+      oc.segoff = c_sgo;
+      oc.segcnt = s_segcnt.p;
+      oc.seg_call = s_segcall.p;
+      oc.seg_round = s_seground.p;
+      oc.seg_dec = s_segdec.p;
+      oc.seg_fws = s_segfws.p;
+      oc.theta = s_theta.p;
+      oc.cand = cand;
+      oc.ncand = ncand;
+      oc.R_last = R_last;
+      oc.recv = s_recv.p;
+      oc.rr = s_rr.p;
+      oc.cts = s_cts.p;
+      oc.cnt = o_cc;
+      oc.bpos = s_bpos.p;
+      oc.total = o_cnt;
+      oc.blist = s_bpos.p + ncalls;
+      oc.nblist = s_bpos.p + 2 * ncalls;
+      oc.f_und = s_fund.p;
+      oc.upos = s_upos.p;
+      oc.nund = o_cnt + 1;
+      oc.und_out = s_und2.p;
+      oc.k1 = (OKey*)s_keys.p;
+      oc.k2 = (OKey*)s_keys2.p;
+      oc.ev_rr = d_rr.p;
+      oc.ev_cts = d_cts.p;
+      oc.ntx = (unsigned long long*)(s_out.p + o_tx);
+      oc.ntxb = ntxb;
+      oc.ids = o_ids;
+      oc.pr = c_pr;
+      oc.nrounds = do_fame ? nrounds : 0;
+      oc.clast = s_clast.p;
+      oc.dec = s_dec.p;
+      oc.nc = c_nc;
+      oc.flags = c_flags;
+      oc.lcr_old = lcr;
+      oc.n_lo = (int)std::min<int64_t>(calls[0], n_coords);
+      oc.n1 = (int)n_coords;
+      oc.lcre_out = o_cnt + 2;
+      return oc;
+    };
+    // one call's bucket, undetermined list, keys, sort and persisted fame as one
+    // single-block launch at any N (k_order_call, front = 0) when the order's first
+    // stages ran as their own grids
+    const bool otail_ok = ord && commit && ncalls == 1 && !spl && ncand <= SCAN_LDS &&
+                          (!do_fame || nrounds == 0 || lcr_dev) && !getenv("HGE_NO_ORDER_CALL");
+    SegInfo si_tail{};
     if (ord) {
       if (nr > 0) {
         SegInfo si;
@@ -1966,6 +2055,7 @@ struct hge_engine {
           si.pr_off = si.pr_cf = si.pr_len = si.clast = nullptr;
           si.dec = nullptr;
         }
+        si_tail = si;
         s_segcnt.need(nr);
         // first call at which each event is visible (arrivals, round received); one call
         // that sees every event (an online call) needs no table: 0 for all, and the
@@ -1996,58 +2086,8 @@ struct hge_engine {
         ocall = vis_all && commit && N <= 16 && !spl && ncand <= SCAN_LDS && (int64_t)nr * G <= 65536 &&
                 (nrounds == 0 || lcr_dev) && !getenv("HGE_NO_ORDER_CALL");
         if (ocall) {
-          s_recv.need(ncand);
-          s_rr.need(ncand);
-          s_cts.need(ncand);
-          s_fund.need(ncand);
-          s_upos.need(ncand);
-          s_bpos.need(2 * (size_t)ncalls + 2);
-          s_und2.need(d_und.n);
-          s_keys.need((size_t)ncand * sizeof(OKey));
-          s_keys2.need((size_t)ncand * sizeof(OKey));
-          OrderCall oc{};
-          oc.si = si;
-          oc.rr_lo = rr_lo;
-          oc.nr = nr;
-          oc.segoff = c_sgo;
-          oc.segcnt = s_segcnt.p;
-          oc.seg_call = s_segcall.p;
-          oc.seg_round = s_seground.p;
-          oc.seg_dec = s_segdec.p;
-          oc.seg_fws = s_segfws.p;
-          oc.theta = s_theta.p;
-          oc.cand = cand;
-          oc.ncand = ncand;
-          oc.R_last = R_last;
-          oc.recv = s_recv.p;
-          oc.rr = s_rr.p;
-          oc.cts = s_cts.p;
-          oc.cnt = o_cc;
-          oc.bpos = s_bpos.p;
-          oc.total = o_cnt;
-          oc.blist = s_bpos.p + ncalls;
-          oc.nblist = s_bpos.p + 2 * ncalls;
-          oc.f_und = s_fund.p;
-          oc.upos = s_upos.p;
-          oc.nund = o_cnt + 1;
-          oc.und_out = s_und2.p;
-          oc.k1 = (OKey*)s_keys.p;
-          oc.k2 = (OKey*)s_keys2.p;
-          oc.ev_rr = d_rr.p;
-          oc.ev_cts = d_cts.p;
-          oc.ntx = (unsigned long long*)(s_out.p + o_tx);
-          oc.ntxb = ntxb;
-          oc.ids = o_ids;
-          oc.pr = c_pr;
-          oc.nrounds = do_fame ? nrounds : 0;
-          oc.clast = s_clast.p;
-          oc.dec = s_dec.p;
-          oc.nc = c_nc;
-          oc.flags = c_flags;
-          oc.lcr_old = lcr;
-          oc.n_lo = (int)std::min<int64_t>(calls[0], n_coords);
-          oc.n1 = (int)n_coords;
-          oc.lcre_out = o_cnt + 2;
+          OrderCall oc = order_call_args(si);
+          oc.front = 1;
           KLAUNCH(k_order_call<16>, dim3(1), dim3(1024), 0, st, t, oc);
           std::swap(d_und, s_und2);
           got_order = true;
@@ -2133,7 +2173,14 @@ struct hge_engine {
       }
       // compaction + the order as call buckets (the received count stays on the
       // device: o_cnt[0])
-      if (!ocall) {
+      if (!ocall && otail_ok) {
+        OrderCall oc = order_call_args(si_tail);
+        oc.front = 0;
+        KLAUNCH(k_order_call<16>, dim3(1), dim3(1024), 0, st, t, oc);
+        std::swap(d_und, s_und2);
+        got_order = true;
+        otail = true;
+      } else if (!ocall) {
         s_fund.need(ncand);
         s_upos.need(ncand);
         s_rr.need(ncand);
@@ -2199,7 +2246,7 @@ struct hge_engine {
 
     // ---- persist fame / LCR ----
     bool lcr_up = false;
-    if (do_fame && nrounds > 0 && !ocall) {
+    if (do_fame && nrounds > 0 && !ocall && !otail) {
       if (lcr_dev) {
         // the persisted fame and RoundEvents(LCR - 1) as below (the new LCR and its
         // call read on the device) in one launch
@@ -2408,8 +2455,10 @@ struct hge_engine {
 
   // which 0: k_fame_decide (a split part: the pairs of its rounds, then the parts'
   // decisions all-gathered) and the per-round timeline; which 1: persist
+  // decide_only: the pairs' decisions only (k_fame_call<.., false> takes the timeline)
   void fame_dispatch(int which, const Tables& t, int nrounds, int npairs, int ncalls,
-                     const std::vector<int32_t>* pr_round = nullptr, const std::vector<int32_t>* pr_off = nullptr) {
+                     const std::vector<int32_t>* pr_round = nullptr, const std::vector<int32_t>* pr_off = nullptr,
+                     bool decide_only = false) {
     if (which == 1) {
       KLAUNCH(k_fame_persist, dim3(div_up((int64_t)nrounds * N, 256)), dim3(256), 0, st, t, c_pr,
               c_pr + nrounds, c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds, s_clast.p,
@@ -2445,6 +2494,7 @@ struct hge_engine {
       }
     }
     if (split_on() && pr_round) split_exchange_dec(*pr_round, *pr_off, npairs);
+    if (decide_only) return;
     switch (NW) {
 #define FCASE(B)                                                                                 \
   case B:                                                                                        \

@@ -1528,7 +1528,9 @@ __global__ void __launch_bounds__(256) k_fame_timeline_g(Tables t, const int32_t
 // 1024 threads, the three stages behind block barriers (their grids were one or two
 // blocks each for a single call).  out (non-null): the header zeroed with the new
 // LastConsensusRound at out[3].
-template <int G>
+// DECIDE false (N >= 64, where k_fame_decide_blk decides the pairs with a block per
+// pair): the timeline, LCR and header only.
+template <int G, int SPL, bool DECIDE>
 __global__ void __launch_bounds__(1024) k_fame_call(Tables t, const int32_t* pr_round, const int32_t* pr_off,
                                                     const int32_t* pr_cf, const int32_t* pr_len, int nrounds,
                                                     int npairs, const int64_t* nc, const int32_t* Rc,
@@ -1536,11 +1538,13 @@ __global__ void __launch_bounds__(1024) k_fame_call(Tables t, const int32_t* pr_
                                                     int lcr_start, int32_t* LCR, int32_t* clast, int32_t* flags,
                                                     int32_t* out, int nout) {
   const int tid = threadIdx.x;
-  for (int it = tid; it < npairs * t.N; it += blockDim.x)
-    fame_decide_item<1>(t, it, pr_round, pr_off, pr_cf, nrounds, 0, npairs, nc, Rc, dec);
-  __syncthreads();  // the decisions (global) are visible to the block
+  if (DECIDE) {
+    for (int it = tid; it < npairs * t.N; it += blockDim.x)
+      fame_decide_item<1>(t, it, pr_round, pr_off, pr_cf, nrounds, 0, npairs, nc, Rc, dec);
+    __syncthreads();  // the decisions (global) are visible to the block
+  }
   for (int64_t b = 0; b < (int64_t)nrounds * G; b += blockDim.x)
-    fame_timeline_group<G, 1>(t, b + tid, pr_round, pr_off, pr_cf, pr_len, nrounds, nc, dec, decbit, Lc);
+    fame_timeline_group<G, SPL>(t, b + tid, pr_round, pr_off, pr_cf, pr_len, nrounds, nc, dec, decbit, Lc);
   __syncthreads();
   lcr_scan_body(Lc, ncalls, lcr_start, LCR, pr_round, pr_cf, pr_len, nrounds, clast, flags);
   if (out) {
@@ -3016,7 +3020,9 @@ __global__ void k_fame_persist_lcre(Tables t, const int32_t* pr_round, const int
 // of k_segments_1p, k_round_received, k_recv_list_und, k_bucket_keys,
 // k_bucket_sort_all and k_fame_persist_lcre): one block of 1024 threads, the stages
 // behind block barriers, the same bodies as those kernels (one call that sees every
-// event; the host checks the candidate count against the LDS scan and sort).
+// event; the host checks the candidate count against the LDS scan and sort).  Wider
+// hashgraphs (front = 0) run the segments, theta, round received and the median as
+// their own grids and this kernel from the call's bucket on.
 struct OrderCall {
   SegInfo si;  // segments
   int rr_lo, nr;
@@ -3045,6 +3051,7 @@ struct OrderCall {
   const int32_t* flags;
   int lcr_old, n_lo, n1;
   int32_t* lcre_out;
+  int front;  // 1: the segments and round received here too (N <= 16); 0: from the stage kernels
 };
 template <int G>
 __global__ void __launch_bounds__(1024) k_order_call(Tables t, OrderCall o) {
@@ -3055,15 +3062,17 @@ __global__ void __launch_bounds__(1024) k_order_call(Tables t, OrderCall o) {
   __shared__ int s_cnt;
   __shared__ unsigned long long s_tx[16];
   const int tid = threadIdx.x, T = blockDim.x;
-  // the round-state segments of the batch's rounds (theta inline)
-  for (int64_t b = 0; b < (int64_t)o.nr * G; b += T)
-    segments_group<G, 1>(t, b + tid, o.rr_lo, o.nr, 1, nullptr, o.si, o.segoff, o.segcnt, o.seg_call, o.seg_round,
-                         o.seg_dec, o.seg_fws, o.theta);
-  __syncthreads();
-  // round received and the median timestamp (inline at N <= 16)
-  for (int q = tid; q < o.ncand; q += T)
-    round_received_item<1>(t, q, o.cand, o.ncand, nullptr, 1, 0, o.rr_lo, o.R_last, o.segoff, o.segcnt,
-                           o.seg_call, o.seg_dec, o.seg_fws, o.theta, o.recv, o.rr, o.cts, nullptr);
+  if (o.front) {
+    // the round-state segments of the batch's rounds (theta inline)
+    for (int64_t b = 0; b < (int64_t)o.nr * G; b += T)
+      segments_group<G, 1>(t, b + tid, o.rr_lo, o.nr, 1, nullptr, o.si, o.segoff, o.segcnt, o.seg_call,
+                           o.seg_round, o.seg_dec, o.seg_fws, o.theta);
+    __syncthreads();
+    // round received and the median timestamp (inline at N <= 16)
+    for (int q = tid; q < o.ncand; q += T)
+      round_received_item<1>(t, q, o.cand, o.ncand, nullptr, 1, 0, o.rr_lo, o.R_last, o.segoff, o.segcnt,
+                             o.seg_call, o.seg_dec, o.seg_fws, o.theta, o.recv, o.rr, o.cts, nullptr);
+  }
   if (tid == 0) s_cnt = 0;
   __syncthreads();
   // the call's received count and its bucket (k_recv_list_und's block 0)

@@ -90,9 +90,9 @@ def test_online_matches_replay(engines):
     eng.close()
 
 
-@pytest.mark.parametrize("n,E,k", [(16, 6000, 16), (16, 3000, 3), (32, 6000, 32), (12, 2000, 1)])
+@pytest.mark.parametrize("n,E,k", [(16, 6000, 16), (16, 3000, 3), (32, 6000, 32), (12, 2000, 1), (48, 5000, 48), (64, 6000, 64), (128, 6000, 128)])
 def test_online_matches_oracle_single_block_paths(engines, n, E, k):
-    """Online calls at N <= 32 take the single-block stages (k_fame_call; k_order_call at
+    """Online calls take the single-block stages (k_fame_call; k_order_call at
     N <= 16; the frontier start in k_la_seq, the rounds assignment in the walk): the
     order, every call's batch and the whole state equal the oracle's."""
     from babble_amd.engine import Engine, events_array
