@@ -157,10 +157,16 @@ constexpr int LASEQ_MAX = 8192;
 // fst (non-null): the grid's last block takes k_frontier_start's work (the rounds
 // walk's first round and k_fss rows, written to fst / fst_lo; it reads only the old
 // events' rounds and the C rows: one launch less per online call)
+// fdt (non-null, N <= 16): the firstDescendants of the batch written here too, in
+// place of k_la16_rows_runs + k_transpose (two launches less per online call): the new
+// positions' FD rows and FDT entries start as none, then chain-j event k is the first
+// chain-j descendant of chain-c positions (LA[(j, k-1)][c], LA[(j, k)][c]] -- the same
+// runs, stored straight into both layouts (FDT stays the runs table later batches
+// transpose from)
 template <int NP>
 __global__ void __launch_bounds__(256) k_la_seq(Tables t, int n0, int n1, const UpEv* up, UpDst dst,
                                                 const int32_t* qolen, const int32_t* qlen, int32_t* qlo,
-                                                int32_t* fst, int32_t* fst_lo) {
+                                                int32_t* fst, int32_t* fst_lo, int32_t* fdt) {
   __shared__ int rows[LASEQ_MAX];
   __shared__ int2 par[LASEQ_MAX / NP];
   if (fst && blockIdx.x == gridDim.x - 1) {
@@ -204,6 +210,29 @@ __global__ void __launch_bounds__(256) k_la_seq(Tables t, int n0, int n1, const 
   for (int e = tid / NP; e < m; e += G) {
     const int x = n0 + e;
     if (i < N) t.LA[rowoff(t, t.creator[x], t.index[x]) + i] = rows[e * NP + i];
+  }
+  if (!fdt) return;
+  const size_t ccap = t.ccap;
+  for (int e = tid / NP; e < m; e += G) {  // thread i: chain j = i of the new position
+    const int x = n0 + e, cx = t.creator[x], px = t.index[x];
+    if (i < N) {
+      t.FD[rowoff(t, cx, px) + i] = INF32;
+      fdt[((size_t)i * N + cx) * ccap + px] = INF32;
+    }
+  }
+  __syncthreads();  // (global, block scope) the runs below overwrite some of them
+  for (int e = tid / NP; e < m; e += G) {  // thread i: column c = i
+    const int x = n0 + e, j = t.creator[x], k = t.index[x];
+    if (i < N) {
+      const int2 pp = par[e];
+      int lo = -1;
+      if (k > 0) lo = pp.x >= 0 ? rows[pp.x * NP + i] : t.LA[rowoff(t, j, k - 1) + i];
+      const int hi = rows[e * NP + i];
+      for (int q = lo + 1; q <= hi; q++) {
+        t.FD[rowoff(t, i, q) + j] = k;
+        fdt[((size_t)j * N + i) * ccap + q] = k;
+      }
+    }
   }
 }
 

@@ -164,6 +164,7 @@ struct hge_engine {
   DBuf<unsigned char> s_keys, s_keys2;
   DBuf<int32_t> s_part, s_fst;
   bool fst_fused = false;  // this batch's k_la_seq ran k_frontier_start's block
+  bool fd_direct = false;  // this batch's k_la_seq wrote the FD rows (N <= 16)
   bool asg_fused = false;  // this attempt's rounds walk assigned the new events' rounds
   // coordinate sweeps: transposed tables and scratch
   int n_sweeps = 0;
@@ -580,6 +581,7 @@ struct hge_engine {
     coords_len.assign(N, 0);
     n_events = n_dev = n_coords = n_divided = 0;
     up_n0 = up_n1 = -1;
+    h_up.clear();
     R = 0;
     R_set = 0;
     h_minw.clear();
@@ -679,7 +681,7 @@ struct hge_engine {
   }
 
   // a packed upload of the events [up_n0, up_n1) waiting for k_chain_fill (upload())
-  DBuf<UpEv> s_up;
+  std::vector<UpEv> h_up;  // the packed records, uploaded with coords_a's control block
   int64_t up_n0 = -1, up_n1 = -1;
   void upload() {
     if (n_dev == n_events) return;
@@ -693,6 +695,7 @@ struct hge_engine {
       // pinned arena, unpacked by the coordinate step's k_chain_fill (eight copies
       // from pageable memory were ~25 us of an online call)
       std::vector<UpEv> up((size_t)m);
+      if (up_n0 >= 0) throw EngineError(HGE_ERR_INTERNAL, "packed upload pending twice");
       for (int64_t i = 0; i < m; i++) {
         UpEv& r = up[(size_t)i];
         const size_t x = (size_t)(a + i);
@@ -705,8 +708,8 @@ struct hge_engine {
         r.ts = h_ts[x];
         for (int k = 0; k < 4; k++) r.S[k] = h_S[4 * x + k];
       }
-      s_up.need((size_t)m);
-      h2d(s_up.p, up.data(), sizeof(UpEv) * (size_t)m);
+      // (they travel with the coordinate step's control block: one copy for both)
+      h_up.swap(up);
       up_n0 = a;
       up_n1 = n_events;
       n_dev = n_events;
@@ -953,6 +956,15 @@ struct hge_engine {
     }
     kc[o_lo + 2 * N] = tot0;
     if (!segs.empty()) memcpy(&kc[o_seg], segs.data(), sizeof(int2) * segs.size());
+    // the packed event records (an online call's upload) ride in the same copy
+    const bool packed = up_n0 == n0 && up_n1 == n1;
+    const size_t o_up = (kc.size() + 3) & ~(size_t)3;  // 16-byte aligned
+    const size_t up_words = packed ? (sizeof(UpEv) * h_up.size() + 3) / 4 : 0;
+    if (packed) {
+      static_assert(sizeof(UpEv) % 4 == 0, "records are whole words");
+      kc.resize(o_up + up_words, 0);
+      memcpy(&kc[o_up], h_up.data(), sizeof(UpEv) * h_up.size());
+    }
     s_kctl.need(kc.size());
     h2d(s_kctl.p, kc.data(), 4 * kc.size());
     k_rs = s_kctl.p;
@@ -965,10 +977,10 @@ struct hge_engine {
     k_fd = split_on() ? s_kctl.p + o_fd : nullptr;
     k_risky1 = s_kctl.p + o_fd + 2 * N;
     {
-      const bool packed = up_n0 == n0 && up_n1 == n1;
-      fill_up = packed ? (const UpEv*)s_up.p : (const UpEv*)nullptr;
+      fill_up = packed ? (const UpEv*)(s_kctl.p + o_up) : (const UpEv*)nullptr;
       fill_dst = UpDst{d_creator.p, d_index.p, d_sp.p, d_op.p, d_ntx.p, d_ts.p, d_S.p, d_coin.p};
       up_n0 = up_n1 = -1;
+      h_up.clear();
       qlo_fused = false;
       if (!la_seq_ok(n1 - n0)) {  // (k_la_seq fills the chain table itself)
         const int nfb = div_up((int)(n1 - n0), 256);
@@ -1648,13 +1660,18 @@ struct hge_engine {
       if (fst_fused) s_fst.need(N + 1);
       int32_t* fp = fst_fused ? s_fst.p : (int32_t*)nullptr;
       int32_t* fl = fst_fused ? k_lo : (int32_t*)nullptr;
-      const int nb = (q ? 1 + N : 1) + (fst_fused ? 1 : 0);
+      // N <= 16 past a fresh state: the batch's firstDescendants in the same launch (no
+      // runs, transpose or k_fd_qlo blocks)
+      fd_direct = q && N <= 16 && !getenv("HGE_NO_FD_DIRECT");
+      const int nq = q && !fd_direct ? N : 0;
+      const int nb = 1 + nq + (fst_fused ? 1 : 0);
       if (N <= 16)
         KLAUNCH(k_la_seq<16>, dim3(nb), dim3(256), 0, st, t, (int)n_coords, (int)n_events, fill_up,
-                fill_dst, olen, len, q ? k_qlo : (int32_t*)nullptr, fp, fl);
+                fill_dst, olen, len, nq ? k_qlo : (int32_t*)nullptr, fp, fl,
+                fd_direct ? d_FDT.p : (int32_t*)nullptr);
       else
         KLAUNCH(k_la_seq<32>, dim3(nb), dim3(256), 0, st, t, (int)n_coords, (int)n_events, fill_up,
-                fill_dst, olen, len, q ? k_qlo : (int32_t*)nullptr, fp, fl);
+                fill_dst, olen, len, nq ? k_qlo : (int32_t*)nullptr, fp, fl, (int32_t*)nullptr);
       qlo_fused = q;
       n_sweeps = 1;
     } else {
@@ -1712,6 +1729,11 @@ struct hge_engine {
         break;
       }
     }
+    }
+    if (fd_direct) {
+      fd_direct = false;  // (k_la_seq wrote the FD rows and FDT runs)
+      qlo_fused = false;
+      return;
     }
     if (fdt16()) {
       KLAUNCH((k_la16_rows_runs<uint16_t>), dim3(div_up(maxnew + 1, 64), div_up(N, 64), N), dim3(256), 0, st, t,
