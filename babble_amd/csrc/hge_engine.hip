@@ -166,6 +166,8 @@ struct hge_engine {
   bool fst_fused = false;  // this batch's k_la_seq ran k_frontier_start's block
   bool fd_direct = false;  // this batch's k_la_seq wrote the FD rows (N <= 16)
   bool asg_fused = false;  // this attempt's rounds walk assigned the new events' rounds
+  bool tail_fused = false;  // ... and did k_round_tail's work
+  bool minw_full = true;    // d_minw's rows are stale: the next rounds tail recomputes all
   // coordinate sweeps: transposed tables and scratch
   int n_sweeps = 0;
   DBuf<int32_t> d_FDT, s_chg, s_bar, s_dirty;
@@ -559,6 +561,7 @@ struct hge_engine {
     // + round count, overflow flag, lowest candidate round, hand-off error and up to 16
     // partial lowest rounds (k_round_minw)
     d_minw.need(nr + 20);
+    minw_full = true;  // (need() does not keep the rows' first witnesses)
     // C must be INF32 beyond the old rows
     fill_i32(d_C.p + oldn, (int64_t)(nr - Rcap) * N, INF32);
     sync();
@@ -567,6 +570,7 @@ struct hge_engine {
 
   void reset_state() {
     sync();
+    minw_full = true;
     h_creator.clear();
     h_index.clear();
     h_sp.clear();
@@ -1017,6 +1021,7 @@ struct hge_engine {
       int32_t rs[3] = {R, 0, 0};
       if (retry) h2d(k_rs, rs, 12);
       asg_fused = false;
+      tail_fused = false;
       t = tables();
       const int NP = (N + 15) & ~15;
       if (N > 32 && (wide32 || frontier_fallback)) {
@@ -1041,9 +1046,24 @@ struct hge_engine {
           // the walk's block also assigns the new events' rounds (k_round_assign's work)
           und_appended = dividing && n_divided == n0;
           s_newwit.need(m);
-          const RoundAssign ra{(int)n0, (int)n1, s_newwit.p, k_rs + 2,
-                               und_appended ? d_und.p + n_und : (int32_t*)nullptr};
+          RoundAssign ra{(int)n0, (int)n1, s_newwit.p, k_rs + 2,
+                         und_appended ? d_und.p + n_und : (int32_t*)nullptr};
           asg_fused = true;
+          // ... and k_round_tail's work (the new witnesses' bitsets, the first witness
+          // of the rounds from the walk's first one, the candidates' lowest round)
+          if (n_und + (n1 - n_divided) <= 65536) {
+            int Gw = 1;
+            while (Gw < std::min(N, 64)) Gw <<= 1;
+            ra.minw = d_minw.p;
+            ra.G = Gw;
+            ra.und = d_und.p;
+            ra.n_und = (int)n_und;
+            ra.lo = (int)n_divided;
+            ra.hi = (int)n1;
+            ra.r_from = minw_full ? 0 : -1;
+            ra.rlo_dev = s_fst.p;
+            tail_fused = true;
+          }
 #define FSSD(NPC, LPC, B)                                                                              \
   KLAUNCH(k_fss<NPC>, dim3((unsigned)std::min<int64_t>(1024, div_up(guess * NPC, 256))), dim3(256), 0, st, t, \
           k_lo, k_lo + N, 0, (int32_t*)nullptr, (uint16_t*)d_FSS.p, (const int32_t*)(k_lo + 2 * N));          \
@@ -1102,12 +1122,12 @@ struct hge_engine {
               (const int32_t*)s_hn.p, (const int4*)s_hres.p, nw, Hcap, k_rs, resume);              \
       KLAUNCH((k_rounds_walk<NPC, LPC, B>), dim3(1), dim3(1024), 0, st, t,                         \
               (const uint16_t*)d_FSS.p, k_len, k_len + N, k_rs, 0, 0, dbg_p(),                     \
-              (const int32_t*)resume, RoundAssign{0, 0, nullptr, nullptr, nullptr});               \
+              (const int32_t*)resume, RoundAssign{});                                              \
       if (getenv("HGE_WALK_DEBUG")) walk_debug(nw);                                               \
     } else {                                                                                       \
       KLAUNCH((k_rounds_walk<NPC, LPC, B>), dim3(1), dim3(1024), 0, st, t,                         \
               (const uint16_t*)d_FSS.p, k_len, k_len + N, k_rs, rlo, Rprev, dbg_p(),               \
-              (const int32_t*)nullptr, RoundAssign{0, 0, nullptr, nullptr, nullptr});              \
+              (const int32_t*)nullptr, RoundAssign{});                                             \
     }                                                                                              \
   } else {                                                                                         \
     KLAUNCH(k_fss<NPC>, dim3(div_up((int64_t)tot * NPC, 256)), dim3(256), 0, st, t, k_lo, k_lo + N, \
@@ -1148,8 +1168,10 @@ struct hge_engine {
       // candidates start at event 0, round 0: nothing to read); an online call's few
       // candidates are reduced by one extra block of k_round_minw
       const int64_t n_mr = n_und + (n1 - n_divided);
-      const int mr = !fresh && n_mr <= 65536 ? (int)std::max<int64_t>(1, std::min<int64_t>(16, div_up(n_mr, 2048))) : 0;
-      {
+      const int mr = tail_fused ? 0
+                     : !fresh && n_mr <= 65536 ? (int)std::max<int64_t>(1, std::min<int64_t>(16, div_up(n_mr, 2048)))
+                                               : 0;
+      if (!tail_fused) {
         int G = 1;
         while (G < std::min(N, 64)) G <<= 1;
         const int64_t wmax = std::min<int64_t>(m, (int64_t)Rcap * N);  // witnesses <= both
@@ -1158,7 +1180,7 @@ struct hge_engine {
                 N > 32 ? (const uint64_t*)d_ssc.p : nullptr, G, nb_wb, (const int32_t*)k_rs, d_minw.p,
                 (const int32_t*)coop_err_src, mr, (const int32_t*)d_und.p, (int)n_und, (int)n_divided, (int)n1);
       }
-      if (!fresh && !mr) {
+      if (!fresh && !mr && !tail_fused) {
         if (n_und > 0)
           KLAUNCH(k_min_round, dim3(div_up(n_und, 256)), dim3(256), 0, st, d_round.p, d_und.p, (int)n_und,
                   d_minw.p + Rcap + 2);
@@ -1169,6 +1191,7 @@ struct hge_engine {
       h_minw.resize(Rcap + 4 + mr);
       d2h(h_minw.data(), d_minw.p, 4 * ((size_t)Rcap + 4 + mr));
       sync();
+      minw_full = false;  // every round's first witness is in d_minw now
       if (!fresh) {
         mnr_pre = h_minw[Rcap + 2];
         for (int b = 0; b < mr; b++) mnr_pre = std::min(mnr_pre, h_minw[Rcap + 4 + b]);
@@ -1829,6 +1852,30 @@ struct hge_engine {
     const int ntxb0 = ord ? div_up(ncand, 256) : 0;
     bool hdr_done = false;
     bool ocall = false;  // the order's stages ran as one launch (k_order_call)
+    bool fame_deferred = false;  // N <= 16: k_fame_call waits to run with the order (k_consensus_call)
+    FameCall fc_pend{};
+    auto fame_call_args = [&](int nrounds_, int npairs_, int ncalls_, int32_t* hdr) {
+      FameCall f{};
+      f.pr_round = c_pr;
+      f.pr_off = c_pr + nrounds_;
+      f.pr_cf = c_pr + 2 * nrounds_;
+      f.pr_len = c_pr + 3 * nrounds_;
+      f.nrounds = nrounds_;
+      f.npairs = npairs_;
+      f.nc = c_nc;
+      f.Rc = c_Rc;
+      f.dec = s_dec.p;
+      f.decbit = s_decbit.p;
+      f.Lc = c_Lc;
+      f.ncalls = ncalls_;
+      f.lcr_start = lcr;
+      f.LCR = s_LCR.p;
+      f.clast = s_clast.p;
+      f.flags = c_flags;
+      f.out = hdr;
+      f.nout = 8 + ncalls_;
+      return f;
+    };
     bool otail = false;  // the order's stages from the call's bucket on ran as one launch
     // ---- DecideFame windows (host enumeration of (round, call) pairs) + control block ----
     std::vector<int32_t> pr_round, pr_off, pr_cf, pr_len;
@@ -1925,12 +1972,11 @@ struct hge_engine {
         s_out.need(o_tx0 + 2 * (size_t)ntxb0);
         int32_t* hdr = s_out.p;
         fame_dispatch(0, t, nrounds, npairs, ncalls, &pr_round, &pr_off, true);
+        const FameCall fc = fame_call_args(nrounds, npairs, ncalls, hdr);
         switch (NW) {
 #define FTAIL(B)                                                                                      \
   case B:                                                                                             \
-    KLAUNCH((k_fame_call<64, B, false>), dim3(1), dim3(1024), 0, st, t, c_pr, c_pr + nrounds,          \
-            c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds, npairs, c_nc, c_Rc, s_dec.p, s_decbit.p,   \
-            c_Lc, ncalls, lcr, s_LCR.p, s_clast.p, c_flags, hdr, 8 + ncalls);                           \
+    KLAUNCH((k_fame_call<64, B, false>), dim3(1), dim3(1024), 0, st, t, fc);                           \
     break;
           FTAIL(1)
           FTAIL(2)
@@ -1948,12 +1994,11 @@ struct hge_engine {
       if (one && N < 64 && (int64_t)npairs * N <= 8192) {
         s_out.need(o_tx0 + 2 * (size_t)ntxb0);
         int32_t* hdr = s_out.p;
-#define FCALL(GG)                                                                                     \
-  KLAUNCH((k_fame_call<GG, 1, true>), dim3(1), dim3(1024), 0, st, t, c_pr, c_pr + nrounds,             \
-          c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds, npairs, c_nc, c_Rc, s_dec.p, s_decbit.p,     \
-          c_Lc, ncalls, lcr, s_LCR.p, s_clast.p, c_flags, hdr, 8 + ncalls);
+        fc_pend = fame_call_args(nrounds, npairs, ncalls, hdr);
+#define FCALL(GG) KLAUNCH((k_fame_call<GG, 1, true>), dim3(1), dim3(1024), 0, st, t, fc_pend);
         if (Gf == 16) {
-          FCALL(16)
+          // launched with the order's stages when they run as one block (k_consensus_call)
+          fame_deferred = true;
         } else if (Gf == 32) {
           FCALL(32)
         } else {
@@ -1999,6 +2044,17 @@ struct hge_engine {
     // device holds it (one launch in place of a memset and a copy)
     // (folded into k_visibility's launch when that runs)
     const int32_t* lcr_src = lcr_dev ? (const int32_t*)(c_flags + 1) : (const int32_t*)nullptr;
+    // an online call at N <= 16: the order's stages in one single-block launch
+    // (k_order_call: segments, round received with its median, the call's bucket, the
+    // undetermined list, keys, the sort, the persisted fame), with DecideFame's block
+    // in front when it waited (k_consensus_call)
+    const bool ocall_pre = ord && nr > 0 && ncalls == 1 && calls[0] >= n_coords && commit && N <= 16 && !spl &&
+                           ncand <= SCAN_LDS && (int64_t)nr * group_lanes() <= 65536 &&
+                           (nrounds == 0 || lcr_dev) && !getenv("HGE_NO_ORDER_CALL");
+    if (fame_deferred && !ocall_pre) {
+      KLAUNCH((k_fame_call<16, 1, true>), dim3(1), dim3(1024), 0, st, t, fc_pend);
+      fame_deferred = false;
+    }
     if (!(ord && nr > 0) && !hdr_done)
       KLAUNCH(k_out_init, dim3(div_up(8 + ncalls, 256)), dim3(256), 0, st, s_out.p, 8 + ncalls, lcr_src);
     // the single-block order kernel's arguments (k_order_call; front: the caller sets it)
@@ -2102,15 +2158,16 @@ struct hge_engine {
         s_segfws.need(ns * NW);
         s_theta.need(ns * N);
         segoff_p = c_sgo;
-        // an online call at N <= 16: the order's stages in one single-block launch
-        // (k_order_call: segments, round received with its median, the call's bucket,
-        // the undetermined list, keys, the sort, the persisted fame)
-        ocall = vis_all && commit && N <= 16 && !spl && ncand <= SCAN_LDS && (int64_t)nr * G <= 65536 &&
-                (nrounds == 0 || lcr_dev) && !getenv("HGE_NO_ORDER_CALL");
+        ocall = ocall_pre;
         if (ocall) {
           OrderCall oc = order_call_args(si);
           oc.front = 1;
-          KLAUNCH(k_order_call<16>, dim3(1), dim3(1024), 0, st, t, oc);
+          if (fame_deferred) {
+            KLAUNCH(k_consensus_call<16>, dim3(1), dim3(1024), 0, st, t, fc_pend, oc);
+            fame_deferred = false;
+          } else {
+            KLAUNCH(k_order_call<16>, dim3(1), dim3(1024), 0, st, t, oc);
+          }
           std::swap(d_und, s_und2);
           got_order = true;
         }
@@ -2266,6 +2323,7 @@ struct hge_engine {
       }
     }
 
+    if (fame_deferred) throw EngineError(HGE_ERR_INTERNAL, "DecideFame's launch left pending");
     // ---- persist fame / LCR ----
     bool lcr_up = false;
     if (do_fame && nrounds > 0 && !ocall && !otail) {

@@ -937,19 +937,17 @@ struct RoundAssign {
   int32_t* newwit;
   int32_t* nnewwit;
   int32_t* und_app;
+  // minw (non-null): k_round_tail's work too -- the new witnesses' bitsets (groups of
+  // G lanes), the first witness of rounds [r_from, R) (r_from < 0: the walk's first
+  // round, rlo_dev[0]; the rows below it are unchanged since the last batch), the
+  // round count, overflow flag and hand-off error (0), and the lowest round over
+  // und[0, n_und) and the ids [lo, hi), final at minw[Rcap + 2]
+  int32_t* minw;
+  int G;
+  const int32_t* und;
+  int n_und, lo, hi, r_from;
+  const int32_t* rlo_dev;
 };
-template <int NPC, int LPC, int B>
-__global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* FSS,
-                                                      const int32_t* olen, const int32_t* len,
-                                                      int32_t* rstate, int rlo_arg, int Rprev,
-                                                      uint64_t* dbg, const int32_t* rlo_dev, RoundAssign ra) {
-  rounds_walk_body<NPC, LPC, B>(t, FSS, olen, len, rstate, rlo_arg, Rprev, dbg, rlo_dev);
-  if (ra.n1 > ra.n0) {
-    __syncthreads();  // the walk's C rows and round count (global) are visible to the block
-    for (int b = ra.n0; b < ra.n1; b += blockDim.x)
-      round_assign_item(t, b + (int)threadIdx.x, ra.n0, ra.n1, rstate, ra.newwit, ra.nnewwit, ra.und_app);
-  }
-}
 
 // The same from a fresh state, by frontier ranges: chain c's positions
 // [C[r][c], C[r+1][c]) are exactly its round-r events (rounds never decrease
@@ -1122,6 +1120,54 @@ __global__ void __launch_bounds__(256) k_round_tail(Tables t, const int32_t* new
                                                     int n_und, int lo, int hi) {
   if ((int)blockIdx.x < nb_wb) witness_bits_body(t, newwit, pnnew, ssc, G, blockIdx.x, nb_wb);
   else round_minw_body(t, 0, rstate, minw, err_in, mr, und, n_und, lo, hi, blockIdx.x - nb_wb, gridDim.x - nb_wb);
+}
+
+template <int NPC, int LPC, int B>
+__global__ void __launch_bounds__(1024) k_rounds_walk(Tables t, const uint16_t* FSS,
+                                                      const int32_t* olen, const int32_t* len,
+                                                      int32_t* rstate, int rlo_arg, int Rprev,
+                                                      uint64_t* dbg, const int32_t* rlo_dev, RoundAssign ra) {
+  rounds_walk_body<NPC, LPC, B>(t, FSS, olen, len, rstate, rlo_arg, Rprev, dbg, rlo_dev);
+  if (ra.n1 > ra.n0) {
+    __syncthreads();  // the walk's C rows and round count (global) are visible to the block
+    for (int b = ra.n0; b < ra.n1; b += blockDim.x)
+      round_assign_item(t, b + (int)threadIdx.x, ra.n0, ra.n1, rstate, ra.newwit, ra.nnewwit, ra.und_app);
+  }
+  if (!ra.minw) return;
+  __shared__ int s_mr;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nwv = blockDim.x >> 6;
+  if (tid == 0) s_mr = INF32;
+  __syncthreads();  // the new witnesses, their count and rounds
+  witness_bits_body(t, ra.newwit, ra.nnewwit, nullptr, ra.G, 0, 1);
+  const int R = rstate[0], ov = rstate[1];
+  int32_t* minw = ra.minw;
+  if (tid == 0) {
+    minw[t.Rcap] = R;
+    minw[t.Rcap + 1] = ov;
+    minw[t.Rcap + 3] = 0;
+  }
+  if (!ov) {
+    int r0 = ra.r_from >= 0 ? ra.r_from : *ra.rlo_dev;
+    r0 = max(0, r0);
+    for (int r = r0 + wv; r < R; r += nwv) {
+      int m = INF32;
+      for (int c = lane; c < t.N; c += 64) {
+        const int w = t.W[(size_t)r * t.N + c];
+        if (w >= 0) m = min(m, w);
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) m = min(m, __shfl_xor(m, o));
+      if (lane == 0) minw[r] = m;
+    }
+  }
+  int m = INF32;
+  const int tot = ra.n_und + (ra.hi - ra.lo);
+  for (int i = tid; i < tot; i += blockDim.x) m = min(m, t.round[i < ra.n_und ? ra.und[i] : ra.lo + (i - ra.n_und)]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = min(m, __shfl_xor(m, o));
+  if (lane == 0 && m != INF32) atomicMin(&s_mr, m);
+  __syncthreads();
+  if (tid == 0) minw[t.Rcap + 2] = s_mr;
 }
 
 // ---------------------------------------------------------------------------
@@ -1530,13 +1576,25 @@ __global__ void __launch_bounds__(256) k_fame_timeline_g(Tables t, const int32_t
 // LastConsensusRound at out[3].
 // DECIDE false (N >= 64, where k_fame_decide_blk decides the pairs with a block per
 // pair): the timeline, LCR and header only.
+struct FameCall {
+  const int32_t *pr_round, *pr_off, *pr_cf, *pr_len;
+  int nrounds, npairs;
+  const int64_t* nc;
+  const int32_t* Rc;
+  uint8_t *dec, *decbit;
+  int32_t* Lc;
+  int ncalls, lcr_start;
+  int32_t *LCR, *clast, *flags, *out;
+  int nout;
+};
 template <int G, int SPL, bool DECIDE>
-__global__ void __launch_bounds__(1024) k_fame_call(Tables t, const int32_t* pr_round, const int32_t* pr_off,
-                                                    const int32_t* pr_cf, const int32_t* pr_len, int nrounds,
-                                                    int npairs, const int64_t* nc, const int32_t* Rc,
-                                                    uint8_t* dec, uint8_t* decbit, int32_t* Lc, int ncalls,
-                                                    int lcr_start, int32_t* LCR, int32_t* clast, int32_t* flags,
-                                                    int32_t* out, int nout) {
+__device__ __forceinline__ void fame_call_body(const Tables& t, const FameCall& f) {
+  const int32_t *pr_round = f.pr_round, *pr_off = f.pr_off, *pr_cf = f.pr_cf, *pr_len = f.pr_len;
+  const int nrounds = f.nrounds, npairs = f.npairs, ncalls = f.ncalls, lcr_start = f.lcr_start, nout = f.nout;
+  const int64_t* nc = f.nc;
+  const int32_t* Rc = f.Rc;
+  uint8_t *dec = f.dec, *decbit = f.decbit;
+  int32_t *Lc = f.Lc, *LCR = f.LCR, *clast = f.clast, *flags = f.flags, *out = f.out;
   const int tid = threadIdx.x;
   if (DECIDE) {
     for (int it = tid; it < npairs * t.N; it += blockDim.x)
@@ -1551,6 +1609,10 @@ __global__ void __launch_bounds__(1024) k_fame_call(Tables t, const int32_t* pr_
     __syncthreads();
     for (int i = tid; i < nout; i += blockDim.x) out[i] = i == 3 ? flags[1] : 0;
   }
+}
+template <int G, int SPL, bool DECIDE>
+__global__ void __launch_bounds__(1024) k_fame_call(Tables t, FameCall f) {
+  fame_call_body<G, SPL, DECIDE>(t, f);
 }
 
 // ---------------------------------------------------------------------------
@@ -3053,12 +3115,11 @@ struct OrderCall {
   int32_t* lcre_out;
   int front;  // 1: the segments and round received here too (N <= 16); 0: from the stage kernels
 };
+constexpr size_t OC_BIG_LDS = (size_t)BIG_SORT * (8 + 4 + 4 + 2);
+constexpr size_t OC_POOL = OC_BIG_LDS > sizeof(SortChunk<SORT_CH>) ? OC_BIG_LDS : sizeof(SortChunk<SORT_CH>);
+static_assert(OC_POOL >= sizeof(int) * (SCAN_LDS + SCAN_LDS / 16), "the scan borrows the sort pool");
 template <int G>
-__global__ void __launch_bounds__(1024) k_order_call(Tables t, OrderCall o) {
-  constexpr size_t BIG_LDS = (size_t)BIG_SORT * (8 + 4 + 4 + 2);
-  constexpr size_t POOL = BIG_LDS > sizeof(SortChunk<SORT_CH>) ? BIG_LDS : sizeof(SortChunk<SORT_CH>);
-  static_assert(POOL >= sizeof(int) * (SCAN_LDS + SCAN_LDS / 16), "the scan borrows the sort pool");
-  __shared__ __attribute__((aligned(16))) unsigned char pool[POOL];
+__device__ __forceinline__ void order_call_body(const Tables& t, const OrderCall& o, unsigned char* pool) {
   __shared__ int s_cnt;
   __shared__ unsigned long long s_tx[16];
   const int tid = threadIdx.x, T = blockDim.x;
@@ -3127,6 +3188,20 @@ __global__ void __launch_bounds__(1024) k_order_call(Tables t, OrderCall o) {
     for (int b = 0; b == 0 || b * T < o.n1 - o.n_lo; b++)
       lcre_dev_body(t, o.nc, o.flags, o.lcr_old, o.n_lo, o.n1, o.lcre_out, b);
   }
+}
+template <int G>
+__global__ void __launch_bounds__(1024) k_order_call(Tables t, OrderCall o) {
+  __shared__ __attribute__((aligned(16))) unsigned char pool[OC_POOL];
+  order_call_body<G>(t, o, pool);
+}
+// the whole consensus part of an online call at N <= 16 in one launch: DecideFame,
+// LCR and the header (fame_call_body), then the order (order_call_body, front = 1)
+template <int G>
+__global__ void __launch_bounds__(1024) k_consensus_call(Tables t, FameCall f, OrderCall o) {
+  __shared__ __attribute__((aligned(16))) unsigned char pool[OC_POOL];
+  fame_call_body<G, 1, true>(t, f);
+  __syncthreads();  // decisions, LCR and the header (global) are visible to the block
+  order_call_body<G>(t, o, pool);
 }
 
 // fresh consensus state: C = INF, W = -1, bitsets / fame / counts = 0, rr = -1
