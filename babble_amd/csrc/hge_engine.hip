@@ -130,6 +130,24 @@ struct hge_engine {
   int lcre = 0;             // LastCommitedRoundEvents
   int64_t ctx = 0;          // ConsensusTransactions
   std::vector<int32_t> consensus;  // the consensus log (unbounded)
+  // a replay leaves its batch's order in HBM (the results block, s_out): the log's
+  // last cons_dev_n ids are downloaded on first use (consensus_sync), not inside the
+  // replay (40 MB at 256/10M)
+  const int32_t* cons_dev = nullptr;
+  int64_t cons_dev_n = 0;
+  bool lazy_order = false;
+  int64_t consensus_size() const { return (int64_t)consensus.size() + cons_dev_n; }
+  void consensus_sync() {
+    if (!cons_dev_n) return;
+    const size_t old = consensus.size();
+    consensus.resize(old + (size_t)cons_dev_n);
+    // through the pinned arena (a pageable destination made the runtime stage it: 13 ms
+    // for the 40 MB of 256/10M)
+    d2h(consensus.data() + old, cons_dev, 4 * (size_t)cons_dev_n);
+    sync();
+    cons_dev = nullptr;
+    cons_dev_n = 0;
+  }
   int64_t n_und = 0;
 
   // replay staging
@@ -571,6 +589,8 @@ struct hge_engine {
   void reset_state() {
     sync();
     minw_full = true;
+    cons_dev = nullptr;
+    cons_dev_n = 0;
     h_creator.clear();
     h_index.clear();
     h_sp.clear();
@@ -917,16 +937,21 @@ struct hge_engine {
     const int SEG = N <= 32 ? 16 : 64;
     std::vector<int2>& segs = h_segs;
     segs.clear();
+    // only the fixed-point sweeps read the segment list (the windowed pass and the
+    // one-pass batch kernel do not): 156k segments and their sort were ~3 ms of host
+    // time at the start of a 256/10M replay
+    const bool sweeps = !(sweep16() && la_windows()) && !la_seq_ok(n1 - n0);
     int maxnew = 0;
     for (int c = 0; c < N; c++) {
       maxnew = std::max(maxnew, chain_len[c] - coords_len[c] + 1);
-      for (int k = coords_len[c]; k < chain_len[c]; k += SEG) segs.push_back(make_int2(c, k));
+      if (sweeps)
+        for (int k = coords_len[c]; k < chain_len[c]; k += SEG) segs.push_back(make_int2(c, k));
     }
     // position-major order: workgroups are dispatched roughly in index order, so
     // early positions of every chain are swept first and later segments read
     // rows already updated in this sweep (Gauss-Seidel in time order)
-    std::stable_sort(segs.begin(), segs.end(),
-                       [](const int2& a, const int2& b) { return a.y < b.y; });
+    if (sweeps)
+      std::stable_sort(segs.begin(), segs.end(), [](const int2& a, const int2& b) { return a.y < b.y; });
     bool fresh = R == 0;
     for (int c = 0; c < N; c++) fresh = fresh && coords_len[c] == 0;
     const size_t o_len = 4, o_plo = o_len + 2 * N, o_qlo = o_plo + N, o_lo = o_qlo + N;
@@ -997,7 +1022,7 @@ struct hge_engine {
         }
       }
     }
-    coords_sweep(t, (int)segs.size(), SEG, maxnew, fresh);
+    coords_sweep(t, sweeps ? (int)segs.size() : 1, SEG, maxnew, fresh);
     cs_pending = true;
     cs_fresh = fresh;
     cs_n0 = n0;
@@ -1809,6 +1834,7 @@ struct hge_engine {
                        std::vector<int64_t>* counts_out) {
     const int ncalls = (int)calls.size();
     if (ncalls == 0) return;
+    consensus_sync();  // (the results block is reused below)
     Tables t = tables();
     x_iter = 0;
     // R_c = Rounds() after the DivideRounds of call c = #{r : minw[r] < n_c}
@@ -2357,20 +2383,29 @@ struct hge_engine {
       got_order = false;
       split_done = true;
     }
-    // the batch's one closing round trip (read in place from the pinned arena)
-    const size_t off = d2h_pinned(s_out.p, 4 * (got_order ? o_tx + 2 * (size_t)ntxb : 8 + (size_t)ncalls));
+    // the batch's one closing round trip (read in place from the pinned arena); a
+    // replay's order stays in HBM (lazy: counters, per-call counts and transaction sums only)
+    const bool lazy = got_order && lazy_order && !order_out;
+    const size_t off = d2h_pinned(s_out.p, 4 * (got_order && !lazy ? o_tx + 2 * (size_t)ntxb : 8 + (size_t)ncalls));
+    const size_t off_tx = lazy ? d2h_pinned(s_out.p + o_tx, 4 * 2 * (size_t)ntxb) : 0;
     sync();
     const int32_t* ho = (const int32_t*)(pin + off);
+    const int32_t* htx = lazy ? (const int32_t*)(pin + off_tx) : ho + o_tx;
     const int32_t nrecv = ho[0];
     if (got_order) {
       const int32_t* ids = ho + 8 + ncalls;
       unsigned long long ntx = 0;
       for (int b2 = 0; b2 < ntxb; b2++) {
         unsigned long long v = 0;
-        memcpy(&v, ho + o_tx + 2 * (size_t)b2, 8);
+        memcpy(&v, htx + 2 * (size_t)b2, 8);
         ntx += v;
       }
-      consensus.insert(consensus.end(), ids, ids + nrecv);
+      if (lazy) {
+        cons_dev = o_ids;
+        cons_dev_n = nrecv;
+      } else {
+        consensus.insert(consensus.end(), ids, ids + nrecv);
+      }
       ctx += (int64_t)ntx;
       if (order_out) order_out->insert(order_out->end(), ids, ids + nrecv);
       if (counts_out)
@@ -2856,6 +2891,8 @@ static void replay_begin(hge_engine* h) {
   h->lcre = 0;
   h->ctx = 0;
   h->consensus.clear();
+  h->cons_dev = nullptr;
+  h->cons_dev_n = 0;
   h->n_und = 0;
   h->ext_on = false;
   h->w_start = std::chrono::steady_clock::now();
@@ -2875,8 +2912,15 @@ static void replay_end(hge_engine* h, int64_t* n_ordered) {
   h->n_und = keep;
   h->und_fresh = keep > 0;
   h->replay_counts.clear();
-  // the consensus log (cleared above) is the replay's order
-  h->consensus_batch(h->replay_calls, true, true, true, nullptr, &h->replay_counts);
+  // the consensus log (cleared above) is the replay's order, left in HBM until read
+  h->lazy_order = true;
+  try {
+    h->consensus_batch(h->replay_calls, true, true, true, nullptr, &h->replay_counts);
+  } catch (...) {
+    h->lazy_order = false;
+    throw;
+  }
+  h->lazy_order = false;
   HIPCHK(hipEventRecord(h->ev[2], h->st));
   HIPCHK(hipEventSynchronize(h->ev[2]));
   const auto w2 = std::chrono::steady_clock::now();
@@ -2894,7 +2938,7 @@ static void replay_end(hge_engine* h, int64_t* n_ordered) {
   h->stage_ms[3] = b;
   h->stage_ms[4] = ms(h->w_start, w2);
   h->stage_ms[6] = a + b;
-  if (n_ordered) *n_ordered = (int64_t)h->consensus.size();
+  if (n_ordered) *n_ordered = h->consensus_size();
   h->dbg_dump();
 }
 
@@ -2906,6 +2950,7 @@ int hge_replay_run(hge_engine* h, int64_t* n_ordered) {
   replay_end(h, n_ordered);
   if (h->rec_on) {  // hge_split_emulate: the rest of the record
     const int64_t E = h->n_events;
+    h->consensus_sync();
     h->rec_order = h->consensus;
     h->rec_counts = h->replay_counts;
     h->rec_rr.resize(E);
@@ -3119,6 +3164,7 @@ int hge_split_finish(hge_engine* h, const int32_t* rows, const uint64_t* ssc, in
 
 int hge_replay_fetch(hge_engine* h, int32_t* order_out, int64_t cap, int64_t* call_counts_out) {
   GUARD_BEGIN
+  h->consensus_sync();
   for (int64_t i = 0; i < (int64_t)h->consensus.size() && i < cap && order_out; i++)
     order_out[i] = h->consensus[i];
   if (call_counts_out)
@@ -3143,7 +3189,7 @@ int32_t hge_rounds(hge_engine* h) { return std::max(h->R_div, h->R_set); }
 int32_t hge_last_consensus_round(hge_engine* h) { return h->lcr; }
 int32_t hge_last_committed_round_events(hge_engine* h) { return h->lcre; }
 int64_t hge_consensus_transactions(hge_engine* h) { return h->ctx; }
-int64_t hge_consensus_count(hge_engine* h) { return (int64_t)h->consensus.size(); }
+int64_t hge_consensus_count(hge_engine* h) { return h->consensus_size(); }
 // RollingList window (common/rolling_list.go:55-67): Add rolls the list back to
 // its last `size` items once it holds 2*size, so after `tot` adds it holds
 static int64_t window_len(int64_t tot, int64_t size) {
@@ -3151,11 +3197,23 @@ static int64_t window_len(int64_t tot, int64_t size) {
   return size + (tot - 2 * size - 1) % size + 1;
 }
 int64_t hge_consensus_events(hge_engine* h, int32_t* ids_out, int64_t cap) {
+  try {
+    h->consensus_sync();
+  } catch (const EngineError& e) {
+    h->err = e.msg;
+    return -1;
+  }
   const int64_t tot = (int64_t)h->consensus.size(), w = window_len(tot, h->cache_size);
   for (int64_t i = 0; i < w && i < cap && ids_out; i++) ids_out[i] = h->consensus[tot - w + i];
   return w;
 }
 int64_t hge_consensus_log(hge_engine* h, int64_t from, int32_t* ids_out, int64_t cap) {
+  try {
+    h->consensus_sync();
+  } catch (const EngineError& e) {
+    h->err = e.msg;
+    return -1;
+  }
   const int64_t tot = (int64_t)h->consensus.size();
   if (from < 0) from = 0;
   for (int64_t i = from; i < tot && i - from < cap && ids_out; i++) ids_out[i - from] = h->consensus[i];

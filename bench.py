@@ -549,7 +549,10 @@ def main():
     replay_ms = {"coords_gpu": st_ms[0], "coords_wall": st_ms[1], "consensus_gpu": st_ms[3],
                  "consensus_wall": st_ms[2], "gpu": st_ms[6], "wall": st_ms[4]}
     replay_ms = {k: round(v, 4) for k, v in replay_ms.items()}
+    # the replay leaves the order in HBM; its download (PCIe) is timed apart, outside the step
+    t_f = time.perf_counter()
     gstatus, gorder, gcounts = eng0.fetch()
+    order_download_ms = (time.perf_counter() - t_f) * 1e3
 
     # ---- profiled pass: per-kernel device time (HIP events on the engine stream) ----
     nprof = max(1, args.profile_steps)
@@ -727,6 +730,7 @@ def main():
             "ingest_host_ms": round(ingest_s * 1e3, 2),
             "admission_ms": None if admission_s is None else round(admission_s * 1e3, 2),
             "replay_ms": replay_ms,
+            "order_download_ms": round(order_download_ms, 3),
             "coordinate_sweeps": sweeps,
             "rounds": eng0.rounds(),
             "kernels_ms_per_replay": {k: round(v[0] / nprof, 4) for k, v in
