@@ -677,9 +677,14 @@ __global__ void __launch_bounds__(256) k_fd_qlo(Tables t, const int32_t* olen, c
 }
 // k_chain_fill (blocks [0, nfb)) and k_fd_qlo (the N blocks after) in one launch:
 // the row bounds read only the old events' LA rows, which the batch leaves alone
+// fst (non-null): the last block takes k_frontier_start's work for the wide rounds
+// walk (its first round, zeroed hand-off flags and granules; old rows only)
 __global__ void __launch_bounds__(256) k_chain_fill_qlo(Tables t, int n0, int n1, const UpEv* up, UpDst dst, int nfb,
-                                                        const int32_t* olen, const int32_t* len, int32_t* qlo) {
-  if ((int)blockIdx.x < nfb) {
+                                                        const int32_t* olen, const int32_t* len, int32_t* qlo,
+                                                        int32_t* fst, int32_t* zbar, uint64_t* zgran, int ngran) {
+  if (fst && blockIdx.x == gridDim.x - 1) {
+    frontier_start_body(t, olen, len, fst, nullptr, zbar, zgran, ngran);
+  } else if ((int)blockIdx.x < nfb) {
     const int x = n0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (x < n1) chain_fill_one(t, x, n0, up, dst);
   } else {

@@ -68,10 +68,9 @@ __global__ void k_lw_pos(Tables t, int64_t n0, int WN, int G, const int32_t* len
 // One wave per chunk of 64 ids.  plan[id - n0] for the chunk's ids, sorted by
 // level: {creator | level << 16 | flags << 24, index, opc, opp} (opc = -1: no
 // other-parent).  risky[w] = the last risky id of window w.
-__global__ void __launch_bounds__(256) k_lw_plan(Tables t, int64_t n0, int64_t n1, int WN,
-                                                 const int32_t* len, int4* plan, int32_t* risky) {
+__device__ __forceinline__ void lw_plan_chunk(const Tables& t, int64_t n0, int64_t n1, int WN, const int32_t* len,
+                                              int4* plan, int32_t* risky, int64_t cs) {
   const int lane = threadIdx.x & 63;
-  const int64_t cs = n0 + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * LW_K;
   if (cs >= n1) return;  // wave-uniform
   const int64_t e = cs + lane;
   const bool v = e < n1;
@@ -121,6 +120,10 @@ __global__ void __launch_bounds__(256) k_lw_plan(Tables t, int64_t n0, int64_t n
   const uint64_t rm = __ballot(v && (flags & LW_RISKY));
   if (rm && lane == 63 - __builtin_clzll(rm)) atomicMax(&risky[(cs - n0) / WN], (int32_t)e);
 }
+__global__ void __launch_bounds__(256) k_lw_plan(Tables t, int64_t n0, int64_t n1, int WN,
+                                                 const int32_t* len, int4* plan, int32_t* risky) {
+  lw_plan_chunk(t, n0, n1, WN, len, plan, risky, n0 + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * LW_K);
+}
 
 // WPT consecutive packed words of an LDS row / to HBM (16-, 8- or 4-byte accesses)
 template <int WPT>
@@ -151,11 +154,14 @@ __device__ __forceinline__ void lw_global_write(uint32_t* p, const uint32_t (&v)
 // head rows equal the previous pass's.  rsum[plan slot] = sum of the row's 16-bit
 // values (LA + 1); initbuf[w] = the starting rows a pass used; prev / changed:
 // the previous pass's changed flag (0: converged, return at once) and this pass's.
+// plan_here (one window, an online call): the window's 16 waves plan its chunks
+// first (k_lw_plan's work; the plan and the risky id are block-visible after the
+// barrier), one launch less
 template <int NPOW>
-__global__ void __launch_bounds__(1024) k_la_win(Tables t, const int4* plan, int64_t n0, int64_t n1, int WN,
+__global__ void __launch_bounds__(1024) k_la_win(Tables t, int4* plan, int64_t n0, int64_t n1, int WN,
                                                  const int32_t* wpos, const int32_t* olen, uint32_t* initbuf,
-                                                 const int32_t* risky, uint32_t* rsum, int pass,
-                                                 const int32_t* prev, int32_t* changed) {
+                                                 int32_t* risky, uint32_t* rsum, int pass,
+                                                 const int32_t* prev, int32_t* changed, const int32_t* plan_len) {
   constexpr int RWW = NPOW / 2;         // packed words per (padded) row
   constexpr int WPT = NPOW / 64;         // words per thread: 32 threads per event
   constexpr int TPE = RWW / WPT;         // = 32
@@ -170,6 +176,11 @@ __global__ void __launch_bounds__(1024) k_la_win(Tables t, const int4* plan, int
   __shared__ uint32_t s_dirty[NPOW / 32];
   __shared__ int s_nlv, s_wait;
   if (prev && *prev == 0) return;  // converged: the flag stays 0
+  if (plan_len) {
+    for (int64_t cs = n0 + (int64_t)(threadIdx.x >> 6) * LW_K; cs < n1; cs += (int64_t)(blockDim.x >> 6) * LW_K)
+      lw_plan_chunk(t, n0, n1, WN, plan_len, plan, risky, cs);
+    __syncthreads();
+  }
   const int N = t.N, W = t.NW2;
   const int w = blockIdx.x;
   const int64_t s0 = n0 + (int64_t)w * WN;

@@ -1014,8 +1014,17 @@ struct hge_engine {
       if (!la_seq_ok(n1 - n0)) {  // (k_la_seq fills the chain table itself)
         const int nfb = div_up((int)(n1 - n0), 256);
         if (!fresh && N <= 256) {  // + k_fd_qlo's blocks (coords_b)
-          KLAUNCH(k_chain_fill_qlo, dim3(nfb + N), dim3(256), 0, st, t, (int)n0, (int)n1, fill_up, fill_dst, nfb,
-                  (const int32_t*)k_len, (const int32_t*)(k_len + N), k_qlo);
+          // + k_frontier_start's block for the wide rounds walk (rounds_coop)
+          fst_fused = N > 32 && !wide32 && !frontier_fallback && !split_on() && !ext_on;
+          if (fst_fused) {
+            s_fst.need(N + 1);
+            s_bar.need(2);
+            s_gran.need(2 * (size_t)N);
+          }
+          KLAUNCH(k_chain_fill_qlo, dim3(nfb + N + (fst_fused ? 1 : 0)), dim3(256), 0, st, t, (int)n0, (int)n1,
+                  fill_up, fill_dst, nfb, (const int32_t*)k_len, (const int32_t*)(k_len + N), k_qlo,
+                  fst_fused ? s_fst.p : (int32_t*)nullptr, fst_fused ? s_bar.p : (int32_t*)nullptr,
+                  fst_fused ? (uint64_t*)s_gran.p : (uint64_t*)nullptr, 2 * N);
           qlo_fused = true;
         } else {
           KLAUNCH(k_chain_fill, dim3(nfb), dim3(256), 0, st, t, (int)n0, (int)n1, fill_up, fill_dst);
@@ -1367,8 +1376,10 @@ struct hge_engine {
     // (the hand-off flags and granules are zeroed by k_frontier_start)
     s_bar.need(2);
     s_gran.need(2 * (size_t)N);
-    KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p, (int32_t*)nullptr,
-            s_bar.p, (uint64_t*)s_gran.p, 2 * N);
+    if (!fst_fused || fresh)  // (else the chain fill's last block ran it)
+      KLAUNCH(k_frontier_start, dim3(1), dim3(256), 0, st, t, k_len, k_len + N, s_fst.p, (int32_t*)nullptr,
+              s_bar.p, (uint64_t*)s_gran.p, 2 * N);
+    fst_fused = false;
     // the lowest round to recompute: read back for a fresh state (the walkers and the
     // joined rows need it on the host), else read by the frontier kernel itself,
     // which stands down at INF32 (no round trip)
@@ -1646,8 +1657,10 @@ struct hge_engine {
     if (G > 1)
       KLAUNCH(k_lw_pos, dim3(div_up(std::max<int64_t>(G * N, MAXP), 256)), dim3(256), 0, st, t, n0, (int)WN, (int)G,
               len, s_lwpos.p, s_lwrisky.p, s_chg.p, MAXP);
-    KLAUNCH(k_lw_plan, dim3(div_up(div_up(ne, LW_K), 4)), dim3(256), 0, st, t, n0, n1, (int)WN, len, s_lwplan.p,
-            risky);
+    // one window: its workgroup plans its own chunks (k_la_win's plan_len)
+    if (G > 1)
+      KLAUNCH(k_lw_plan, dim3(div_up(div_up(ne, LW_K), 4)), dim3(256), 0, st, t, n0, n1, (int)WN, len, s_lwplan.p,
+              risky);
     int p = 0;
     for (int group = G == 1 ? 1 : 3;; group = 2) {
       for (int g = 0; g < group; g++, p++) {
@@ -1656,7 +1669,8 @@ struct hge_engine {
         const int pass = p + 1;
 #define LWIN(NP)                                                                                         \
   KLAUNCH(k_la_win<NP>, dim3(G), dim3(1024), 0, st, t, s_lwplan.p, n0, n1, (int)WN, wpos, olen,          \
-          s_lwinit.p, (const int32_t*)risky, s_lwsum.p, pass, prev, s_chg.p + p)
+          s_lwinit.p, risky, s_lwsum.p, pass, prev, s_chg.p + p,                                        \
+          G == 1 && p == 0 ? len : (const int32_t*)nullptr)
         if (npow == 64) LWIN(64);
         else if (npow == 128) LWIN(128);
         else LWIN(256);
