@@ -274,7 +274,8 @@ struct hge_engine {
     t.FD16 = fdt16() ? (uint16_t*)d_FD.p : nullptr;
     t.FDTD = d_FDTD.p;
     t.FDTW = d_FDTW.p;
-    t.WLA = d_WLA.p;
+    t.WLA = wla16() ? nullptr : d_WLA.p;
+    t.WLA16 = wla16() ? (uint16_t*)d_WLA.p : nullptr;
     t.WLR = (N > 64 && !wide32) ? d_WLR.p : nullptr;
     t.round = d_round.p;
     t.wit = d_wit.p;
@@ -1542,6 +1543,8 @@ struct hge_engine {
   // most 65,534 events; a longer chain switches the engine to int32 LA rows for good
   // (to_wide32 below), which the N <= 32 path uses from the start
   bool sweep16() const { return N > 32 && !wide32; }
+  // the median's threshold rows as uint16 (k_witness_la, k_median_wave's 4-witness lanes)
+  bool wla16() const { return N > 192 && (N & 3) == 0 && !wide32; }
 
   // the switch to int32 positions (hge_wide32.hip): the int32 LA rows of every event
   // with coordinates, unpacked from LA16; from here on the N <= 32 sweeps and

@@ -44,6 +44,9 @@ struct Tables {
   int32_t* FDTD;
   uint8_t* FDTW;  // N > 16: [N][ccap][ceil(N / 64)]: 1 = the tile holds an out-of-range delta
   int32_t* WLA;   // N > 16: [Rcap][N][N] LA[(d, C[r][d])][cx] at [r][cx][d]
+  // N > 192, N % 4 == 0, uint16 positions: the same rows as LA + 1 (0: none) in place of
+  // WLA (the median reads a lane's 4 thresholds with one 8-byte load)
+  uint16_t* WLA16;
   uint16_t* WLR;  // N > 64, packed path: [Rcap][N][N] LA + 1 of the same rows, row-major [r][d][cx] (theta)
   int32_t* LA;
   int32_t* FD;
@@ -2302,7 +2305,10 @@ __global__ void __launch_bounds__(256) k_witness_la(Tables t, int rr_lo) {
   __syncthreads();
   for (int r = ty; r < 64; r += 4) {
     const int cx = c0 + r, d = d0 + tx;
-    if (cx < N && d < N) t.WLA[((size_t)rr * N + cx) * N + d] = tile[tx][r];
+    if (cx < N && d < N) {
+      if (t.WLA16) t.WLA16[((size_t)rr * N + cx) * N + d] = (uint16_t)(tile[tx][r] + 1);
+      else t.WLA[((size_t)rr * N + cx) * N + d] = tile[tx][r];
+    }
   }
 }
 
@@ -2356,7 +2362,6 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
     const int rr = live[e] ? rr0 : 0, sg = live[e] ? sg0 : 0;
     qe[e] = q;
     ixe[e] = ix;
-    const int32_t* thr = t.WLA + ((size_t)rr * N + cx) * N;
     const size_t rw = (size_t)cx * t.ccap + ix;
     const int32_t* tdr = t.FDTD + rw * N;
     // the FD timestamps as int32 offsets from x's own timestamp; a row with an offset
@@ -2370,17 +2375,34 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
     }
     bse[e] = t.ts[x];
     wde[e] = __builtin_amdgcn_readfirstlane(wide);
+    if (VPL == 4 && t.WLA16) {
+      // lane l takes witnesses d = 4l .. 4l + 3: its thresholds in one 8-byte load
+      // (LA + 1 as uint16), its offsets in one 16-byte load, one fame word
+      const uint2 tw = *(const uint2*)(t.WLA16 + ((size_t)rr * N + cx) * N + 4 * lane);
+      const int4 ow = *(const int4*)(tdr + 4 * lane);
+      const uint64_t f = seg_fws[(size_t)sg * NW + (lane >> 4)];
+      const uint32_t u[4] = {tw.x & 0xFFFFu, tw.x >> 16, tw.y & 0xFFFFu, tw.y >> 16};
+      const int32_t o4[4] = {ow.x, ow.y, ow.z, ow.w};
 #pragma unroll
-    for (int k = 0; k < VPL; k++) {
-      const int dd = min(lane + 64 * k, N - 1);
-      fw[e][k] = seg_fws[(size_t)sg * NW + (k < NW ? k : 0)];
-      th[e][k] = thr[dd];
-      off[e][k] = tdr[dd];
+      for (int k = 0; k < VPL; k++) {
+        fw[e][k] = f;
+        th[e][k] = (int)u[k & 3] - 1;
+        off[e][k] = o4[k & 3];
+      }
+    } else {
+      const int32_t* thr = t.WLA + ((size_t)rr * N + cx) * N;
+#pragma unroll
+      for (int k = 0; k < VPL; k++) {
+        const int dd = min(lane + 64 * k, N - 1);
+        fw[e][k] = seg_fws[(size_t)sg * NW + (k < NW ? k : 0)];
+        th[e][k] = thr[dd];
+        off[e][k] = tdr[dd];
+      }
     }
     if (wde[e]) {
 #pragma unroll
       for (int k = 0; k < VPL; k++) {
-        const int dd = min(lane + 64 * k, N - 1);
+        const int dd = VPL == 4 && t.WLA16 ? 4 * lane + k : min(lane + 64 * k, N - 1);
         const int f = fd_at(t, rw, dd);
         ts[e][k] = f != INF32 ? t.tsch[(size_t)dd * t.ccap + f] : 0;
       }
@@ -2391,7 +2413,7 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
     bool in[VPL];
 #pragma unroll
     for (int k = 0; k < VPL; k++) {
-      const int d = lane + 64 * k;
+      const int d = VPL == 4 && t.WLA16 ? 4 * lane + k : lane + 64 * k;
       in[k] = d < N && ((fw[e][k] >> (d & 63)) & 1ull) && th[e][k] >= ixe[e];
     }
     int64_t med;
