@@ -2721,6 +2721,182 @@ struct hge_engine {
     update_rdiv();
   }
 
+  // An online RunConsensus at N <= 16 with ONE host round trip: the coordinate and
+  // rounds launches of divide() (k_la_seq with the frontier start and the batch's FD,
+  // k_fss, the rounds walk with the assignment and tail), then k_consensus_dyn, whose
+  // control block the device builds from the walk's round count and the candidates'
+  // lowest round; the results and the rounds' first witnesses come back together.
+  // The rounds table is grown first so that the walk cannot overflow it (R grows by
+  // at most one per new event).  Returns false (nothing done) when the call does not
+  // fit this path.
+  bool online_fast(std::vector<int32_t>& order) {
+    const int64_t n0 = n_coords, n1 = n_events, m = n1 - n0;
+    if (N > 16 || m <= 0 || R == 0 || cs_pending || split_on() || rec_on || ext_on || sp_active) return false;
+    if (n_divided != n0 || !la_seq_ok(m) || n_und + m > 65536 || n_und + m > SCAN_LDS) return false;
+    if (getenv("HGE_NO_ONLINE_FAST")) return false;
+    int maxlen = 0;
+    for (int c = 0; c < N; c++) maxlen = std::max(maxlen, chain_len[c]);
+    if (maxlen + 1 >= 0xFFFF) return false;
+    consensus_sync();
+    ensure_rcap((int64_t)R + m + 4);
+    // ---- divide(): coordinates and rounds, no readback
+    dividing = true;
+    und_appended = false;
+    if (!coords_a()) {
+      dividing = false;
+      throw EngineError(HGE_ERR_INTERNAL, "online call: no coordinates to compute");
+    }
+    if (!fst_fused || !cs_pending) throw EngineError(HGE_ERR_INTERNAL, "online call: frontier start not fused");
+    cs_pending = false;
+    Tables t = tables();
+    und_appended = true;  // (n_divided == n0: the walk's block appends the new ids)
+    s_newwit.need(m);
+    RoundAssign ra{(int)n0, (int)n1, s_newwit.p, k_rs + 2, d_und.p + n_und};
+    int Gw = 1;
+    while (Gw < std::min(N, 64)) Gw <<= 1;
+    ra.minw = d_minw.p;
+    ra.G = Gw;
+    ra.und = d_und.p;
+    ra.n_und = (int)n_und;
+    ra.lo = (int)n_divided;
+    ra.hi = (int)n1;
+    ra.r_from = minw_full ? 0 : -1;
+    ra.rlo_dev = s_fst.p;
+    const int64_t guess = m + 16 * (int64_t)N;
+    KLAUNCH(k_fss<16>, dim3((unsigned)std::min<int64_t>(1024, div_up(guess * 16, 256))), dim3(256), 0, st, t, k_lo,
+            k_lo + N, 0, (int32_t*)nullptr, (uint16_t*)d_FSS.p, (const int32_t*)(k_lo + 2 * N));
+    KLAUNCH((k_rounds_walk<16, 4, 256>), dim3(1), dim3(1024), 0, st, t, (const uint16_t*)d_FSS.p, k_len, k_len + N,
+            k_rs, 0, R, dbg_p(), (const int32_t*)s_fst.p, ra);
+    fst_fused = false;
+    dividing = false;
+    n_coords = n1;
+    coords_len = chain_len;
+    n_und += m;
+    n_divided = n_coords;
+    und_fresh = false;
+    // ---- consensus of the one call, control built on the device
+    const int Rmax = R + (int)m + 1;
+    const int nround_max = std::max(1, Rmax - 2 - lcr), nr_max = std::max(1, Rmax);
+    const int ncand = (int)n_und;
+    const size_t o_Rc = 2, o_Lc = 3, o_fl = 4, o_pr = 8, o_pidx = o_pr + 4 * (size_t)nround_max;
+    const size_t o_sgo = o_pidx + nr_max;
+    s_cctl.need(o_sgo + nr_max + 1);
+    c_nc = (int64_t*)s_cctl.p;
+    c_Rc = s_cctl.p + o_Rc;
+    c_Lc = s_cctl.p + o_Lc;
+    c_flags = s_cctl.p + o_fl;
+    c_pr = s_cctl.p + o_pr;
+    c_pidx = s_cctl.p + o_pidx;
+    c_sgo = s_cctl.p + o_sgo;
+    s_dec.need((size_t)nround_max * N);
+    s_decbit.need(nround_max);
+    s_LCR.need(1);
+    s_clast.need(nround_max);
+    const size_t nslot = (size_t)nr_max * (N + 3);
+    s_segcnt.need(nr_max);
+    s_segcall.need(nslot);
+    s_seground.need(nslot);
+    s_segdec.need(nslot);
+    s_segfws.need(nslot * NW);
+    s_theta.need(nslot * N);
+    const size_t o_tx = (8 + 1 + (size_t)ncand + 1) & ~(size_t)1;
+    const int ntxb = div_up(ncand, 256);
+    s_out.need(o_tx + 2 * (size_t)ntxb);
+    s_recv.need(ncand);
+    s_rr.need(ncand);
+    s_cts.need(ncand);
+    s_fund.need(ncand);
+    s_upos.need(ncand);
+    s_bpos.need(4);
+    s_und2.need(d_und.n);
+    s_keys.need((size_t)ncand * sizeof(OKey));
+    s_keys2.need((size_t)ncand * sizeof(OKey));
+    t = tables();
+    DynCall dc{};
+    dc.lcr = lcr;
+    dc.ncand = ncand;
+    dc.Rcap = Rcap;
+    dc.n_c = n_divided;
+    dc.rstate = k_rs;
+    dc.minw = d_minw.p;
+    dc.c_nc = c_nc;
+    dc.c_Rc = c_Rc;
+    dc.c_Lc = c_Lc;
+    dc.c_flags = c_flags;
+    dc.c_pr = c_pr;
+    dc.c_pidx = c_pidx;
+    dc.c_sgo = c_sgo;
+    dc.dec = s_dec.p;
+    dc.decbit = s_decbit.p;
+    dc.LCR = s_LCR.p;
+    dc.clast = s_clast.p;
+    dc.out = s_out.p;
+    OrderCall& o = dc.o;
+    o.segcnt = s_segcnt.p;
+    o.seg_call = s_segcall.p;
+    o.seg_round = s_seground.p;
+    o.seg_dec = s_segdec.p;
+    o.seg_fws = s_segfws.p;
+    o.theta = s_theta.p;
+    o.cand = d_und.p;
+    o.ncand = ncand;
+    o.recv = s_recv.p;
+    o.rr = s_rr.p;
+    o.cts = s_cts.p;
+    o.cnt = s_out.p + 8;
+    o.bpos = s_bpos.p;
+    o.total = s_out.p;
+    o.blist = s_bpos.p + 1;
+    o.nblist = s_bpos.p + 2;
+    o.f_und = s_fund.p;
+    o.upos = s_upos.p;
+    o.nund = s_out.p + 1;
+    o.und_out = s_und2.p;
+    o.k1 = (OKey*)s_keys.p;
+    o.k2 = (OKey*)s_keys2.p;
+    o.ev_rr = d_rr.p;
+    o.ev_cts = d_cts.p;
+    o.ntx = (unsigned long long*)(s_out.p + o_tx);
+    o.ntxb = ntxb;
+    o.ids = s_out.p + 9;
+    o.lcr_old = lcr;
+    o.n_lo = (int)n_divided;
+    o.n1 = (int)n_divided;
+    o.lcre_out = s_out.p + 2;
+    KLAUNCH(k_consensus_dyn<16>, dim3(1), dim3(1024), 0, st, t, dc);
+    std::swap(d_und, s_und2);
+    // ---- the one round trip: the results block and the rounds' first witnesses
+    const size_t off = d2h_pinned(s_out.p, 4 * (o_tx + 2 * (size_t)ntxb));
+    const size_t offw = d2h_pinned(d_minw.p, 4 * ((size_t)Rcap + 4));
+    sync();
+    const int32_t* hw = (const int32_t*)(pin + offw);
+    if (hw[Rcap + 1]) throw EngineError(HGE_ERR_INTERNAL, "online call: rounds table overflow past its bound");
+    R = hw[Rcap];
+    h_minw.assign(hw, hw + R);
+    minw_full = false;
+    mnr_key[0] = -1;
+    update_rdiv();
+    const int32_t* ho = (const int32_t*)(pin + off);
+    const int32_t nrecv = ho[0];
+    const int32_t* ids = ho + 9;
+    unsigned long long ntx = 0;
+    for (int b2 = 0; b2 < ntxb; b2++) {
+      unsigned long long v = 0;
+      memcpy(&v, ho + o_tx + 2 * (size_t)b2, 8);
+      ntx += v;
+    }
+    consensus.insert(consensus.end(), ids, ids + nrecv);
+    order.insert(order.end(), ids, ids + nrecv);
+    ctx += (int64_t)ntx;
+    n_und = ho[1];
+    if (ho[3] > lcr) {
+      lcr = ho[3];
+      lcre = lcr - 1 >= 0 ? ho[2] : 0;
+    }
+    prof_collect();
+    return true;
+  }
+
   // first witness id of every round (host copy: Rounds() as seen at any event count)
   void update_rdiv() {
     // h_minw was read back together with the round count (coords)
@@ -2843,9 +3019,11 @@ int hge_find_order(hge_engine* h, int32_t* ids_out, int64_t cap, int64_t* n_out)
 int hge_run_consensus(hge_engine* h, int32_t* ids_out, int64_t cap, int64_t* n_out) {
   GUARD_BEGIN
   const int64_t c0 = hge_engine::now_ns();
-  h->divide();
   std::vector<int32_t> order;
-  h->consensus_batch({h->n_divided}, true, true, true, &order, nullptr);
+  if (!h->online_fast(order)) {
+    h->divide();
+    h->consensus_batch({h->n_divided}, true, true, true, &order, nullptr);
+  }
   for (int64_t i = 0; i < (int64_t)order.size() && i < cap && ids_out; i++) ids_out[i] = order[i];
   if (n_out) *n_out = (int64_t)order.size();
   h->hp.calls++;

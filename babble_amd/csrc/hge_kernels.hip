@@ -3226,6 +3226,114 @@ __global__ void __launch_bounds__(1024) k_consensus_call(Tables t, FameCall f, O
   order_call_body<G>(t, o, pool);
 }
 
+// An online call's consensus at N <= 16 with its control built on the device
+// (k_consensus_call's stages after a prologue): the round count and the candidates'
+// lowest round are read where the rounds walk left them (rstate, minw[Rcap + 2]), so
+// the host enqueues the whole call without a round trip in the middle.  The single
+// call's DecideFame windows are one pair per round lcr+1 .. R-2 (consensus_batch's
+// enumeration for one call); the rounds DecideRoundReceived examines are
+// [mnr + 1, R), with their segment capacities.  Buffers are sized by the host from
+// R <= R_before + new events.
+struct DynCall {
+  int lcr, ncand, Rcap;
+  int64_t n_c;
+  const int32_t* rstate;
+  const int32_t* minw;
+  int64_t* c_nc;
+  int32_t *c_Rc, *c_Lc, *c_flags, *c_pr, *c_pidx, *c_sgo;
+  uint8_t *dec, *decbit;
+  int32_t *LCR, *clast, *out;
+  OrderCall o;  // buffers; its round scalars and control pointers are filled here
+};
+template <int G>
+__global__ void __launch_bounds__(1024) k_consensus_dyn(Tables t, DynCall dc) {
+  __shared__ __attribute__((aligned(16))) unsigned char pool[OC_POOL];
+  __shared__ int s_R, s_rrlo, s_nr, s_nround;
+  const int tid = threadIdx.x, T = blockDim.x, N = t.N;
+  if (tid == 0) {
+    const int R = dc.rstate[0];
+    const int mnr = dc.minw[dc.Rcap + 2];
+    const int rr_lo = mnr >= INF32 - 1 ? INF32 : mnr + 1;  // (INF32: no candidate)
+    s_R = R;
+    s_rrlo = rr_lo;
+    s_nr = max(0, R - rr_lo);
+    s_nround = max(0, R - 2 - dc.lcr);
+    dc.c_nc[0] = dc.n_c;
+    dc.c_Rc[0] = R;
+    dc.c_Lc[0] = -1;
+    for (int i = 0; i < 4; i++) dc.c_flags[i] = 0;
+  }
+  __syncthreads();
+  const int R = s_R, rr_lo = s_rrlo, nr = s_nr, nround = s_nround;
+  int32_t* pr = dc.c_pr;
+  for (int k = tid; k < nround; k += T) {
+    pr[k] = dc.lcr + 1 + k;
+    pr[nround + k] = k;
+    pr[2 * nround + k] = 0;
+    pr[3 * nround + k] = 1;
+  }
+  for (int q = tid; q < nr; q += T) {
+    const int k = rr_lo + q - (dc.lcr + 1);
+    dc.c_pidx[q] = k >= 0 && k < nround ? k : -1;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int slot = 0;
+    for (int q = 0; q < nr; q++) {
+      dc.c_sgo[q] = slot;
+      slot += N + 2 + (dc.c_pidx[q] >= 0 ? 1 : 0);
+    }
+    dc.c_sgo[nr] = slot;
+  }
+  __syncthreads();
+  FameCall f{};
+  f.pr_round = pr;
+  f.pr_off = pr + nround;
+  f.pr_cf = pr + 2 * nround;
+  f.pr_len = pr + 3 * nround;
+  f.nrounds = nround;
+  f.npairs = nround;
+  f.nc = dc.c_nc;
+  f.Rc = dc.c_Rc;
+  f.dec = dc.dec;
+  f.decbit = dc.decbit;
+  f.Lc = dc.c_Lc;
+  f.ncalls = 1;
+  f.lcr_start = dc.lcr;
+  f.LCR = dc.LCR;
+  f.clast = dc.clast;
+  f.flags = dc.c_flags;
+  f.out = dc.out;
+  f.nout = 9;
+  if (nround > 0) {
+    fame_call_body<G, 1, true>(t, f);
+  } else {
+    for (int i = tid; i < 9; i += T) dc.out[i] = i == 3 ? dc.lcr : 0;  // no new LastConsensusRound
+  }
+  __syncthreads();
+  OrderCall o = dc.o;
+  o.rr_lo = rr_lo;
+  o.nr = nr;
+  o.R_last = R;
+  o.segoff = dc.c_sgo;
+  o.si.pr_index = dc.c_pidx;
+  o.si.pr_off = nround ? pr + nround : nullptr;
+  o.si.pr_cf = nround ? pr + 2 * nround : nullptr;
+  o.si.pr_len = nround ? pr + 3 * nround : nullptr;
+  o.si.clast = nround ? dc.clast : nullptr;
+  o.si.dec = nround ? dc.dec : nullptr;
+  o.pr = pr;
+  o.nrounds = nround;
+  o.clast = dc.clast;
+  o.dec = dc.dec;
+  o.flags = dc.c_flags;
+  o.nc = dc.c_nc;
+  o.front = nr > 0 ? 1 : 0;
+  if (nr == 0)
+    for (int q = tid; q < o.ncand; q += T) o.recv[q] = -1;  // no round can receive
+  order_call_body<G>(t, o, pool);
+}
+
 // fresh consensus state: C = INF, W = -1, bitsets / fame / counts = 0, rr = -1
 __global__ void k_reset_rounds(Tables t, int64_t nrow, int64_t nbits, int64_t nev,
                                int32_t* rr) {
