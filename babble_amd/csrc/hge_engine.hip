@@ -180,7 +180,8 @@ struct hge_engine {
   bool vis_all = false;  // this batch: one call seeing every event (no visibility table)
   DBuf<int64_t> s_cts;
   DBuf<unsigned char> s_keys, s_keys2;
-  DBuf<int32_t> s_part, s_fst;
+  DBuf<int32_t> s_part, s_fst, s_relay, s_rfail;
+  DBuf<uint8_t> s_dec2;  // selective fame widening: the new layout's decisions
   bool fst_fused = false;  // this batch's k_la_seq ran k_frontier_start's block
   bool fd_direct = false;  // this batch's k_la_seq wrote the FD rows (N <= 16)
   bool asg_fused = false;  // this attempt's rounds walk assigned the new events' rounds
@@ -392,8 +393,9 @@ struct hge_engine {
                              &s_und2,    &s_part,   &s_fst,    &d_FSS,
                              &d_FDT,     &s_chg,    &s_bar,   &s_bseg,   &s_kctl,    &s_cctl,
                              &s_out,     &s_hn,     &s_hres,  &s_dirty,  &d_WLA,     &s_lwpos,
-                             &s_lwrisky, &s_src};
+                             &s_lwrisky, &s_src,    &s_relay, &s_rfail};
     for (auto* b : i32s) b->free_();
+    s_dec2.free_();
     s_lwplan.free_();
     d_WLR.free_();
     s_xbuf.free_();
@@ -1933,7 +1935,15 @@ struct hge_engine {
     const int i_hi = Rc[ncalls - 1] - 2;  // processed rounds: i <= R_c - 2
     // speculative fame window: calls up to R_c <= i + 2 + SPEC, widened when a round
     // stays undecided past it (narrower windows re-dispatch more often: slower)
-    for (int SPEC = 3;; SPEC *= 2) {
+    // Selective widening (N a multiple of 64, no split or record): every window starts
+    // at SPEC = 2 and only the rounds whose decision came past their window are
+    // widened and re-decided (their new pairs alone; the other rounds' decisions are
+    // moved to the new layout).  At 256/10M 6 of 2,836 rounds need it; a uniform
+    // SPEC = 3 decides a third more pairs, a uniform 2 re-decides every round.
+    const bool selective = do_fame && N % 64 == 0 && !split_on() && !rec_on && ncalls > 1;
+    std::vector<int> spec_r;
+    std::vector<int32_t> old_off, old_len;
+    for (int SPEC = selective ? 2 : 3, iter = 0;; SPEC *= 2, iter++) {
       pr_round.clear();
       pr_off.clear();
       pr_cf.clear();
@@ -1944,11 +1954,14 @@ struct hge_engine {
         for (int i = i_lo; i <= i_hi; i++) {
           while (cfp < ncalls && Rc[cfp] < i + 2) cfp++;
           if (cfp >= ncalls) break;
+          const int k = (int)pr_round.size();
+          if (selective && iter == 0) spec_r.push_back(SPEC);
+          const int sp = selective ? spec_r.at(k) : SPEC;
           // last call with R_c <= i + 2 + SPEC
           int a = cfp, b = ncalls - 1;
           while (a < b) {
             int mid = (a + b + 1) / 2;
-            if (Rc[mid] <= i + 2 + SPEC) a = mid;
+            if (Rc[mid] <= i + 2 + sp) a = mid;
             else b = mid - 1;
           }
           pr_round.push_back(i);
@@ -1999,7 +2012,7 @@ struct hge_engine {
       c_pidx = s_cctl.p + o_pidx;
       c_sgo = s_cctl.p + o_sgo;
       if (nrounds == 0) break;
-      s_dec.need((size_t)npairs * N);
+      if (!(selective && iter > 0)) s_dec.need((size_t)npairs * N);  // (a widening moves them first)
       s_decbit.need(npairs);
       s_LCR.need(ncalls);
       s_clast.need(nrounds);
@@ -2053,21 +2066,71 @@ struct hge_engine {
         lcr_dev = true;
         break;
       }
-      fame_dispatch(0, t, nrounds, npairs, ncalls, &pr_round, &pr_off);
+      if (selective && iter > 0) {
+        // the previous layout's decisions moved, then the widened rounds' new pairs
+        s_dec2.need((size_t)npairs * N);
+        std::vector<int32_t> rel(2 * (size_t)nrounds);
+        std::vector<int32_t> plist;
+        for (int k = 0; k < nrounds; k++) {
+          rel[k] = old_off[k];
+          rel[nrounds + k] = old_len[k];
+          for (int q = old_len[k]; q < pr_len[k]; q++) plist.push_back(pr_off[k] + q);
+        }
+        s_relay.need(rel.size() + plist.size() + 1);
+        h2d(s_relay.p, rel.data(), 4 * rel.size());
+        if (!plist.empty()) h2d(s_relay.p + rel.size(), plist.data(), 4 * plist.size());
+        KLAUNCH(k_dec_relayout, dim3(nrounds), dim3(256), 0, st, (const uint8_t*)s_dec.p, s_dec2.p,
+                (const int32_t*)s_relay.p, (const int32_t*)(s_relay.p + nrounds), (const int32_t*)(c_pr + nrounds),
+                N);
+        std::swap(s_dec, s_dec2);
+        if (!plist.empty()) {
+          switch (NW) {
+#define XCASE(B)                                                                                      \
+  case B:                                                                                             \
+    KLAUNCH((k_fame_decide_blk<B>), dim3((unsigned)plist.size()), dim3(N), 0, st, t, c_pr, c_pr + nrounds, \
+            c_pr + 2 * nrounds, nrounds, 0, npairs, c_nc, c_Rc, s_dec.p,                              \
+            (const int32_t*)(s_relay.p + rel.size()));                                                \
+    break;
+            XCASE(1)
+            XCASE(2)
+            XCASE(3)
+            XCASE(4)
+#undef XCASE
+            default:
+              throw EngineError(HGE_ERR_INTERNAL, "unsupported N");
+          }
+        }
+        // the timeline over the whole layout again
+        fame_dispatch(0, t, nrounds, 0, ncalls, &pr_round, &pr_off);
+      } else {
+        fame_dispatch(0, t, nrounds, npairs, ncalls, &pr_round, &pr_off);
+      }
       if (rec_on && !split_on()) {
         rec_dec.emplace_back((size_t)npairs * N);
         readback(rec_dec.back().data(), s_dec.p, (size_t)npairs * N);
       }
       x_iter++;
+      s_rfail.need(nrounds);
       KLAUNCH(k_lcr_scan, dim3(1), dim3(1024), 0, st, c_Lc, ncalls, lcr, s_LCR.p, c_pr,
-              c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds, s_clast.p, c_flags);
+              c_pr + 2 * nrounds, c_pr + 3 * nrounds, nrounds, s_clast.p, c_flags,
+              selective ? s_rfail.p : (int32_t*)nullptr);
       if (full) {
         lcr_dev = true;
         break;
       }
       int32_t fl[3];
+      std::vector<int32_t> rf(selective ? nrounds : 0);
+      if (selective) d2h(rf.data(), s_rfail.p, 4 * (size_t)nrounds);
       readback(fl, c_flags, 3);
-      if (fl[0]) continue;  // a round stayed undecided past its window: widen
+      if (fl[0]) {  // a round stayed undecided past its window: widen (those rounds only)
+        if (selective) {
+          old_off = pr_off;
+          old_len = pr_len;
+          for (int k = 0; k < nrounds; k++)
+            if (rf[k]) spec_r[k] *= 2;
+        }
+        continue;
+      }
       lcr_new = fl[1];
       if (lcr_new > lcr) c_set = fl[2];
       break;
@@ -2610,7 +2673,7 @@ struct hge_engine {
     if (N == 64 * B)                                                                                 \
       KLAUNCH((k_fame_decide_blk<B>), dim3(p1 - p0), dim3(N), 0, st, t, c_pr + k_lo,                  \
               c_pr + nrounds + k_lo, c_pr + 2 * nrounds + k_lo, k_hi - k_lo, p0, p1, c_nc, c_Rc,      \
-              s_dec.p);                                                                              \
+              s_dec.p, (const int32_t*)nullptr);                                                     \
     else                                                                                             \
       KLAUNCH((k_fame_decide<B>), dim3(div_up(items, 256)), dim3(256), 0, st, t, c_pr + k_lo,         \
               c_pr + nrounds + k_lo, c_pr + 2 * nrounds + k_lo, k_hi - k_lo, p0, p1, c_nc, c_Rc,      \

@@ -1297,15 +1297,17 @@ __global__ void k_fame_decide(Tables t, const int32_t* pr_round, const int32_t* 
 // the y loop reads them as LDS broadcasts (the per-lane k_fame_decide reads them
 // as chains of scalar loads, 8 slots at a time).  Same decisions, same output.
 template <int NWT>
+// plist (non-null): block b decides pair plist[b] (a widened window's new pairs only)
 __global__ void __launch_bounds__(256) k_fame_decide_blk(Tables t, const int32_t* pr_round, const int32_t* pr_off,
                                                          const int32_t* pr_cf, int nrounds, int p0, int npairs,
-                                                         const int64_t* nc, const int32_t* Rc, uint8_t* dec) {
+                                                         const int64_t* nc, const int32_t* Rc, uint8_t* dec,
+                                                         const int32_t* plist) {
   __shared__ int sY[64 * NWT];    // witness y of slot d, -1 if none or not yet inserted at call c
   __shared__ int sTot[64 * NWT];  // |ssb[y]|: the same for every lane
   __shared__ uint64_t sS[64 * NWT][NWT];
   __shared__ uint8_t sCoin[64 * NWT];
   const int N = t.N, SM = t.SM;
-  const int p = p0 + (int)xcd_block(blockIdx.x, gridDim.x);  // (XCD-aware: neighbouring pairs share rows)
+  const int p = plist ? plist[blockIdx.x] : p0 + (int)xcd_block(blockIdx.x, gridDim.x);  // (XCD-aware)
   if (p >= npairs) return;
   const int xd = threadIdx.x;
   int lo = 0, hi = nrounds - 1;  // last round with pr_off <= p
@@ -1383,10 +1385,11 @@ __global__ void __launch_bounds__(256) k_fame_decide_blk(Tables t, const int32_t
 
 // LCR_c = max(LCR_start, prefix max of Lc); c_last(i) = first call with LCR >= i;
 // coverage check of each round's speculative window.
+// rfail (non-null): rfail[ri] = 1 when round ri's window ended before its decision
 __device__ __forceinline__ void lcr_scan_body(const int32_t* Lc, int ncalls, int lcr_start, int32_t* LCR,
                                               const int32_t* pr_round, const int32_t* pr_cf,
                                               const int32_t* pr_len, int nrounds, int32_t* clast,
-                                              int32_t* flags) {
+                                              int32_t* flags, int32_t* rfail = nullptr) {
   __shared__ int wm[16];
   const int T = blockDim.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int per = (ncalls + T - 1) / T;
@@ -1441,20 +1444,30 @@ __device__ __forceinline__ void lcr_scan_body(const int32_t* Lc, int ncalls, int
     }
     clast[ri] = a;
     const int ce = pr_cf[ri] + pr_len[ri] - 1;
-    if (pr_len[ri] > 0) {
-      if (a < ncalls) {
-        if (a > ce) atomicOr(&flags[0], 1);
-      } else if (ce < ncalls - 1) {
-        atomicOr(&flags[0], 1);
-      }
-    }
+    bool bad = false;
+    if (pr_len[ri] > 0) bad = a < ncalls ? a > ce : ce < ncalls - 1;
+    if (bad) atomicOr(&flags[0], 1);
+    if (rfail) rfail[ri] = bad ? 1 : 0;
   }
 }
 __global__ void __launch_bounds__(1024) k_lcr_scan(const int32_t* Lc, int ncalls, int lcr_start,
                                                    int32_t* LCR, const int32_t* pr_round,
                                                    const int32_t* pr_cf, const int32_t* pr_len,
-                                                   int nrounds, int32_t* clast, int32_t* flags) {
-  lcr_scan_body(Lc, ncalls, lcr_start, LCR, pr_round, pr_cf, pr_len, nrounds, clast, flags);
+                                                   int nrounds, int32_t* clast, int32_t* flags,
+                                                   int32_t* rfail) {
+  lcr_scan_body(Lc, ncalls, lcr_start, LCR, pr_round, pr_cf, pr_len, nrounds, clast, flags, rfail);
+}
+
+// a widened DecideFame batch: every round's decisions of the previous layout
+// (old_off / old_len pairs of N slots) copied to the start of its new range (new_off);
+// the widened rounds' new pairs are then decided alone (k_fame_decide_blk's plist)
+__global__ void __launch_bounds__(256) k_dec_relayout(const uint8_t* old_dec, uint8_t* new_dec, const int32_t* old_off,
+                                                      const int32_t* old_len, const int32_t* new_off, int N) {
+  const int ri = blockIdx.x;
+  const size_t n = (size_t)old_len[ri] * N;
+  const uint8_t* src = old_dec + (size_t)old_off[ri] * N;
+  uint8_t* dst = new_dec + (size_t)new_off[ri] * N;
+  for (size_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
 }
 
 // persisted fame after the batch: decisions up to c_last(i); one lane per
