@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 GPU runs (gpurun): `scripts/gpu_r05.sh STEP...`, each step under its own limit,
+# Round-5 GPU runs (gpurun): `scripts/gpu_r05.sh STEP...`, each step under its own limit,
 # stopping at the first failure.
 #   full     tests/test_gpu_fullsize.py (whole-stream digests at 64/1M and 256/10M)
 #   gpu      the whole pytest -m gpu suite
@@ -21,6 +21,9 @@
 #   online   per-call profile of the online path (16/100k, 256 prefix)
 #   onprof   rocprofv3 kernel stats and SQ counters of 400 online calls at 256 participants
 #   stamps   the batch engine's per-section cycle stamps (HGB_STAMPS)
+#   onphase  online calls at 16, 64 and 256 participants with HGE_HOST_PHASES (host time split)
+#   gapargs / gapcopies  launch_gap modes: argument size, small stream copies vs zero-copy
+#   mcg      config 5 at GRAPHS="..." graphs per GPU
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 9
 mkdir -p gpurun_out/r05

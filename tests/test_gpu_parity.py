@@ -113,6 +113,40 @@ def test_online_matches_oracle_single_block_paths(engines, n, E, k):
     eng.close()
 
 
+@pytest.mark.parametrize("n,E,k", [(16, 4000, 16), (8, 2000, 2), (64, 4000, 64)])
+def test_online_single_block_paths_match_stage_kernels(engines, n, E, k, monkeypatch):
+    """The online call's fused paths (one round trip at N <= 16, the single-block order
+    and the batch's FD written by k_la_seq) against the per-stage kernels they replace
+    (HGE_NO_ONLINE_FAST / HGE_NO_ORDER_CALL / HGE_NO_FD_DIRECT): the same order, batches
+    and state."""
+    from babble_amd.engine import Engine, events_array
+    dag = random_gossip(n, E, seed=77 + n + k)
+    ev = events_array(dag)
+    calls = schedule(E, k)
+
+    def run():
+        eng = Engine(n, 1 << 13)
+        nxt, batches = 0, []
+        for c in calls:
+            eng.insert_events(ev[nxt:c].copy())
+            batches.append(eng.run_consensus())
+            nxt = c
+        state = (eng.consensus_events(), eng.undetermined(), eng.rounds(), eng.last_consensus_round(),
+                 eng.last_committed_round_events(), eng.consensus_transactions())
+        eng.close()
+        return batches, state
+
+    fused = run()
+    for v in ("HGE_NO_ONLINE_FAST", "HGE_NO_ORDER_CALL", "HGE_NO_FD_DIRECT"):
+        monkeypatch.setenv(v, "1")
+    staged = run()
+    assert len(fused[0]) == len(staged[0])
+    for a, b in zip(fused[0], staged[0]):
+        np.testing.assert_array_equal(a, b)
+    for a, b in zip(fused[1], staged[1]):
+        np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
+
+
 def test_split_calls_match_run_consensus(engines):
     """DivideRounds / DecideFame / FindOrder as separate calls (node/core.go:179-202)."""
     from babble_amd.engine import Engine, events_array
