@@ -1853,15 +1853,23 @@ struct hge_engine {
                        std::vector<int64_t>* counts_out) {
     const int ncalls = (int)calls.size();
     if (ncalls == 0) return;
+    const bool tph = ncalls > 1000 && getenv("HGE_HOST_PHASES");
+    int64_t tp[6] = {now_ns(), 0, 0, 0, 0, 0};
     consensus_sync();  // (the results block is reused below)
     Tables t = tables();
     x_iter = 0;
     // R_c = Rounds() after the DivideRounds of call c = #{r : minw[r] < n_c}
+    // (one merge pass over the ascending calls and first witnesses: 39k binary searches
+    // were ~0.5 ms of idle GPU at the start of a 256/10M replay's consensus)
     std::vector<int32_t> Rc(ncalls);
-    for (int c = 0; c < ncalls; c++)
-      Rc[c] = (int32_t)(std::lower_bound(h_minw.begin(), h_minw.end(), calls[c],
-                                         [](int32_t m, int64_t n) { return (int64_t)m < n; }) -
-                        h_minw.begin());
+    for (int c = 0, r = 0; c < ncalls; c++) {
+      if (c > 0 && calls[c] < calls[c - 1])  // (not ascending: search afresh)
+        r = (int)(std::lower_bound(h_minw.begin(), h_minw.end(), calls[c],
+                                   [](int32_t m, int64_t n) { return (int64_t)m < n; }) -
+                  h_minw.begin());
+      while (r < (int)h_minw.size() && (int64_t)h_minw[r] < calls[c]) r++;
+      Rc[c] = r;
+    }
     const bool fresh_und = und_fresh;
     und_fresh = false;
     const bool ord = do_order && n_und > 0;
@@ -1922,6 +1930,7 @@ struct hge_engine {
       return f;
     };
     bool otail = false;  // the order's stages from the call's bucket on ran as one launch
+    tp[1] = now_ns();
     // ---- DecideFame windows (host enumeration of (round, call) pairs) + control block ----
     std::vector<int32_t> pr_round, pr_off, pr_cf, pr_len;
     int npairs = 0, nrounds = 0;
@@ -2136,6 +2145,7 @@ struct hge_engine {
       break;
     }
 
+    tp[2] = now_ns();
     // ---- DecideRoundReceived / FindOrder ----
     bool got_order = false;
     // results block: counters | per-call counts | order | per-block transaction sums
@@ -2463,6 +2473,7 @@ struct hge_engine {
       got_order = false;
       split_done = true;
     }
+    tp[3] = now_ns();
     // the batch's one closing round trip (read in place from the pinned arena); a
     // replay's order stays in HBM (lazy: counters, per-call counts and transaction sums only)
     const bool lazy = got_order && lazy_order && !order_out;
@@ -2502,6 +2513,10 @@ struct hge_engine {
       lcr = lcr_new;
       lcre = lcr_new - 1 >= 0 ? ho[2] : 0;
     }
+    tp[4] = now_ns();
+    if (tph)
+      fprintf(stderr, "[hge consensus] prologue %.3f ms, fame %.3f ms (incl. syncs), order enqueue %.3f ms, closing %.3f ms\n",
+              (tp[1] - tp[0]) / 1e6, (tp[2] - tp[1]) / 1e6, (tp[3] - tp[2]) / 1e6, (tp[4] - tp[3]) / 1e6);
     prof_collect();
   }
 
