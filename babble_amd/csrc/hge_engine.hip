@@ -1987,10 +1987,16 @@ struct hge_engine {
       const size_t o_pr = o_fl + 4, o_pidx = o_pr + 4 * (size_t)nrounds;
       const size_t o_sgo = o_pidx + nr;  // N <= 64: per-round segment capacity offsets
       std::vector<int32_t>& cc = h_cctl;
-      cc.assign(o_sgo + nr + 1, 0);
-      memcpy(cc.data(), calls.data(), 8 * (size_t)ncalls);
-      memcpy(&cc[o_Rc], Rc.data(), 4 * (size_t)ncalls);
-      std::fill(cc.begin() + o_Lc, cc.begin() + o_fl, -1);
+      // a widening pass keeps the calls, R_c and their offsets (the round set is the
+      // same): only the window arrays are rewritten and uploaded, L_c and the flags are
+      // reset on the device (k_dec_relayout)
+      const bool part = selective && iter > 0;
+      if (!part) {
+        cc.assign(o_sgo + nr + 1, 0);
+        memcpy(cc.data(), calls.data(), 8 * (size_t)ncalls);
+        memcpy(&cc[o_Rc], Rc.data(), 4 * (size_t)ncalls);
+        std::fill(cc.begin() + o_Lc, cc.begin() + o_fl, -1);
+      }
       if (nrounds) {
         memcpy(&cc[o_pr], pr_round.data(), 4 * (size_t)nrounds);
         memcpy(&cc[o_pr + nrounds], pr_off.data(), 4 * (size_t)nrounds);
@@ -2011,8 +2017,12 @@ struct hge_engine {
         nslot += N + 2 + (k >= 0 ? pr_len[k] : 0);
       }
       cc[o_sgo + nr] = (int32_t)std::min<int64_t>(nslot, INF32);
-      s_cctl.need(cc.size());
-      h2d(s_cctl.p, cc.data(), 4 * cc.size());
+      if (part) {
+        h2d(s_cctl.p + o_pr, cc.data() + o_pr, 4 * (cc.size() - o_pr));
+      } else {
+        s_cctl.need(cc.size());
+        h2d(s_cctl.p, cc.data(), 4 * cc.size());
+      }
       c_nc = (int64_t*)s_cctl.p;
       c_Rc = s_cctl.p + o_Rc;
       c_Lc = s_cctl.p + o_Lc;
@@ -2090,7 +2100,7 @@ struct hge_engine {
         if (!plist.empty()) h2d(s_relay.p + rel.size(), plist.data(), 4 * plist.size());
         KLAUNCH(k_dec_relayout, dim3(nrounds), dim3(256), 0, st, (const uint8_t*)s_dec.p, s_dec2.p,
                 (const int32_t*)s_relay.p, (const int32_t*)(s_relay.p + nrounds), (const int32_t*)(c_pr + nrounds),
-                N);
+                N, c_Lc, ncalls, c_flags);
         std::swap(s_dec, s_dec2);
         if (!plist.empty()) {
           switch (NW) {

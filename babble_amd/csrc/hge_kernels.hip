@@ -1461,8 +1461,13 @@ __global__ void __launch_bounds__(1024) k_lcr_scan(const int32_t* Lc, int ncalls
 // a widened DecideFame batch: every round's decisions of the previous layout
 // (old_off / old_len pairs of N slots) copied to the start of its new range (new_off);
 // the widened rounds' new pairs are then decided alone (k_fame_decide_blk's plist)
+// (also L_c = -1 over the ncalls calls and the four flags zeroed: the pass's control
+// block keeps them otherwise)
 __global__ void __launch_bounds__(256) k_dec_relayout(const uint8_t* old_dec, uint8_t* new_dec, const int32_t* old_off,
-                                                      const int32_t* old_len, const int32_t* new_off, int N) {
+                                                      const int32_t* old_len, const int32_t* new_off, int N,
+                                                      int32_t* Lc, int ncalls, int32_t* flags) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ncalls; i += gridDim.x * blockDim.x) Lc[i] = -1;
+  if (blockIdx.x == 0 && threadIdx.x < 4) flags[threadIdx.x] = 0;
   const int ri = blockIdx.x;
   const size_t n = (size_t)old_len[ri] * N;
   const uint8_t* src = old_dec + (size_t)old_off[ri] * N;
