@@ -1944,12 +1944,13 @@ struct hge_engine {
     const int i_hi = Rc[ncalls - 1] - 2;  // processed rounds: i <= R_c - 2
     // speculative fame window: calls up to R_c <= i + 2 + SPEC, widened when a round
     // stays undecided past it (narrower windows re-dispatch more often: slower)
-    // Selective widening (N a multiple of 64, no split or record): every window starts
+    // Selective widening (N >= 192 a multiple of 64, no split or record; smaller N pay
+    // more for the passes' round trips than the fame work they save): every window starts
     // at SPEC = 1 and only the rounds whose decision came past their window are
     // widened and re-decided (their new pairs alone; the other rounds' decisions are
     // moved to the new layout).  At 256/10M 517 of 2,836 rounds go to SPEC = 2 and 6
     // of those to 4; a uniform SPEC = 3 decides twice the pairs.
-    const bool selective = do_fame && N % 64 == 0 && !split_on() && !rec_on && ncalls > 1;
+    const bool selective = do_fame && N % 64 == 0 && N >= 192 && !split_on() && !rec_on && ncalls > 1;
     std::vector<int> spec_r;
     std::vector<int32_t> old_off, old_len;
     for (int SPEC = selective ? 1 : 3, iter = 0;; SPEC *= 2, iter++) {

@@ -68,6 +68,18 @@ print('$1/$2', round(d['value']/1e6,2), d['ms_per_step'], d['parity'][:120])"
            python -c "import json; d=json.load(open('gpurun_out/r05/onphase.json')); print('$NE', d['plain']['p50_us'], d['plain']['mean_us'], d['profiled']['launches_per_call'])"
            grep hge_host_phases gpurun_out/r05/onphase.err | head -1
          done ;;
+    ab16) for v in head new head new; do
+           case $v in head) export HGE_LIB=build/ab/libhge_head.so ;; *) unset HGE_LIB ;; esac
+           for NE in ${AB_CONFIGS:-16:100000 32:1000000}; do
+             set -- ${NE/:/ }
+             timeout -k 10 300 python -u bench.py --participants $1 --events $2 --no-secondary --no-cpu-baseline --steps 10 --warmup 3 > gpurun_out/r05/ab16_$v_$1.json 2> gpurun_out/r05/ab16_$v_$1.err || { tail -5 gpurun_out/r05/ab16_$v_$1.err; exit 2; }
+             python -c "
+import json
+d=json.loads(open('gpurun_out/r05/ab16_$v_$1.json').read().strip().splitlines()[-1])
+k=d['kernels_ms_per_replay']
+print('$v', '$1/$2', round(d['value']/1e6,2), d['ms_per_step'], {n: round(k[n],3) for n in k if 'fame' in n}, d['parity'][:30])"
+           done
+         done; unset HGE_LIB ;;
     pmc) bash scripts/gpu_pmc.sh r05/pmc || exit 6 ;;
     diag) bash scripts/gpu_pmc_diag.sh r05/diag && bash scripts/gpu_pmc_lds.sh r05/lds || exit 6 ;;
     onprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r05/onprof -o run -- python3 -u scripts/analysis/online_profile.py 256 600000 256 400 > gpurun_out/r05/onprof.log 2>&1 || { tail -20 gpurun_out/r05/onprof.log; exit 7; }
