@@ -72,10 +72,10 @@ print('$1/$2', round(d['value']/1e6,2), d['ms_per_step'], d['parity'][:120])"
            case $v in head) export HGE_LIB=build/ab/libhge_head.so ;; *) unset HGE_LIB ;; esac
            for NE in ${AB_CONFIGS:-16:100000 32:1000000}; do
              set -- ${NE/:/ }
-             timeout -k 10 300 python -u bench.py --participants $1 --events $2 --no-secondary --no-cpu-baseline --steps 10 --warmup 3 > gpurun_out/r05/ab16_$v_$1.json 2> gpurun_out/r05/ab16_$v_$1.err || { tail -5 gpurun_out/r05/ab16_$v_$1.err; exit 2; }
+             timeout -k 10 300 python -u bench.py --participants $1 --events $2 --no-secondary --no-cpu-baseline --steps 10 --warmup 3 > gpurun_out/r05/ab16_${v}_$1.json 2> gpurun_out/r05/ab16_${v}_$1.err || { tail -5 gpurun_out/r05/ab16_${v}_$1.err; exit 2; }
              python -c "
 import json
-d=json.loads(open('gpurun_out/r05/ab16_$v_$1.json').read().strip().splitlines()[-1])
+d=json.loads(open('gpurun_out/r05/ab16_${v}_$1.json').read().strip().splitlines()[-1])
 k=d['kernels_ms_per_replay']
 print('$v', '$1/$2', round(d['value']/1e6,2), d['ms_per_step'], {n: round(k[n],3) for n in k if 'fame' in n}, d['parity'][:30])"
            done
