@@ -2101,6 +2101,23 @@ __global__ void k_round_received(Tables t, const int32_t* cand, int ncand, const
 // the select ends once one value is left.  A 20-24-bit span takes three digits; the
 // bit-at-a-time select it replaced took twenty-odd steps (6.27 -> 6.0 ms at 256/10M).
 // hist: the wave's 256 ints in LDS.  Returns the image.
+// Wave-wide inclusive scans by DPP row shifts and row broadcasts (VALU, no LDS
+// crossbar): row_shr 1/2/4/8 scan each 16-lane row, row_bcast15 / row_bcast31 carry
+// rows 0 -> 1, 2 -> 3 and rows 0-1 -> 2-3.  A lane whose source is outside its row
+// (or a row the mask leaves out) takes the identity.
+#define HGE_DPP_SCAN(x, op, id)                                                        \
+  do {                                                                                 \
+    x = op(x, __builtin_amdgcn_update_dpp((id), (x), 0x111, 0xf, 0xf, false));         \
+    x = op(x, __builtin_amdgcn_update_dpp((id), (x), 0x112, 0xf, 0xf, false));         \
+    x = op(x, __builtin_amdgcn_update_dpp((id), (x), 0x114, 0xf, 0xf, false));         \
+    x = op(x, __builtin_amdgcn_update_dpp((id), (x), 0x118, 0xf, 0xf, false));         \
+    x = op(x, __builtin_amdgcn_update_dpp((id), (x), 0x142, 0xa, 0xf, false));         \
+    x = op(x, __builtin_amdgcn_update_dpp((id), (x), 0x143, 0xc, 0xf, false));         \
+  } while (0)
+__device__ __forceinline__ int dpp_add(int a, int b) { return a + b; }
+__device__ __forceinline__ int dpp_umin(int a, int b) { return (int)min((uint32_t)a, (uint32_t)b); }
+__device__ __forceinline__ int dpp_umax(int a, int b) { return (int)max((uint32_t)a, (uint32_t)b); }
+
 template <int VPL>
 __device__ __forceinline__ uint32_t wave_upper_median32_r8(const uint32_t (&v)[VPL], const bool (&in)[VPL],
                                                            int* hist) {
@@ -2115,6 +2132,7 @@ __device__ __forceinline__ uint32_t wave_upper_median32_r8(const uint32_t (&v)[V
       mx = max(mx, v[k]);
     }
   }
+#ifdef HGE_MED_SHFL
   for (int o = 32; o > 0; o >>= 1) {
     mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
     mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
@@ -2122,6 +2140,14 @@ __device__ __forceinline__ uint32_t wave_upper_median32_r8(const uint32_t (&v)[V
   mn = __builtin_amdgcn_readfirstlane(mn);
   if (n == 0) return mn;  // no value (a candidate that is not stored)
   const uint32_t span = __builtin_amdgcn_readfirstlane(mx - mn);
+#else
+  int smn = (int)mn, smx = (int)mx;
+  HGE_DPP_SCAN(smn, dpp_umin, -1);
+  HGE_DPP_SCAN(smx, dpp_umax, 0);
+  mn = (uint32_t)__builtin_amdgcn_readlane(smn, 63);  // lane 63: the whole wave
+  if (n == 0) return mn;  // no value (a candidate that is not stored)
+  const uint32_t span = (uint32_t)__builtin_amdgcn_readlane(smx, 63) - mn;
+#endif
   int kk = n / 2;  // 0-based rank of the upper median
   uint32_t vr[VPL];
   bool live[VPL];
@@ -2146,10 +2172,14 @@ __device__ __forceinline__ uint32_t wave_upper_median32_r8(const uint32_t (&v)[V
     const int4 b = *(const int4*)&hist[4 * lane];
     const int tot = b.x + b.y + b.z + b.w;
     int inc = tot;  // inclusive scan of the lanes' totals
+#ifdef HGE_MED_SHFL
     for (int o = 1; o < 64; o <<= 1) {
       const int y = __shfl_up(inc, o, 64);
       if (lane >= o) inc += y;
     }
+#else
+    HGE_DPP_SCAN(inc, dpp_add, 0);
+#endif
     const int ex = inc - tot;
     const uint64_t hit = __ballot(ex <= kk && kk < inc);
     const int L = (int)__builtin_ctzll(hit);

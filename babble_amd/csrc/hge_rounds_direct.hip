@@ -421,14 +421,11 @@ __device__ int dir_select(const Tables& t, int c, int lenc, DirLDS<BS, NPOW>& L,
     L.sdbg[0] += t1 - t0;
     L.sdbg[1] += stamp() - t1;
   }
-  // every wave: inclusive prefix over the H bins, the first bin reaching SM
+  // every wave: inclusive prefix over the H bins (DPP, HGE_DPP_SCAN: no LDS
+  // permutes on the round's critical path), the first bin reaching SM
   const int lane = threadIdx.x & 63;
   int v = lane < H ? L.sHist[lane] : 0;
-#pragma unroll
-  for (int o = 1; o < H; o <<= 1) {
-    const int y = __shfl_up(v, o, 64);
-    if (lane >= o) v += y;
-  }
+  HGE_DPP_SCAN(v, dpp_add, 0);
   const uint64_t ge = __ballot(lane < H && v >= SM);
   const int ks = ge ? (int)__builtin_ctzll(ge) : H;
   if (ks < e) {
