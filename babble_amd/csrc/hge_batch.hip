@@ -96,6 +96,25 @@ struct BT {
   uint64_t* ks0;
   int32_t* kid;
   uint64_t* dbg;               // diagnostics: per-graph section cycles (null: off)
+  // the bulk call schedule (hge_batch_bulk.hip)
+  const int32_t* glist;  // kb_consensus: the graphs it replays (null: every graph)
+  const int32_t* cg;     // [co + c] the graph of each call
+  int32_t *Rc, *xcall;   // [co + c] Rounds() after call c's DivideRounds; [eo + x] x's insertion call
+  int32_t* rfirst;       // [ro + r] the first call with R_c >= r (r <= the last call's R)
+  uint64_t* arr;         // [eo + k] the witnesses in insertion order: call << 32 | round << 8 | creator
+  uint64_t* Dp;          // [((co + c) * BNS + s) * 2 + {0, 1}] DecideFame's decided / famous masks
+  int32_t* gx;           // [g][16] per-graph internals (GX_*)
+  int4* ivh;             // [(ro + r) * BVCAP + k] receive intervals: first call, end call, theta slot
+  uint64_t* ivF;         // ... and their famous witnesses
+  int32_t *nivl, *fsuf;  // [ro + r] intervals per round; the suffix minimum of their first starts
+  int32_t *thp, *thR;    // [g * BICAP + s][N] receive thresholds; [g * BICAP + s] their round
+  uint64_t* thF;         // [g * BICAP + s] their famous witnesses
+  int32_t* rcall;        // [eo + x] the call that receives x (-1 none)
+  int32_t* rrank;        // [eo + x] x's slot in that call's bucket (before the sort)
+  int32_t *bcnt, *boff;  // [co + c] call buckets: size, offset
+  int4* wl;              // the non-empty buckets (graph, size, offset in the graph's order)
+  int32_t* wlc;          // their count
+  int64_t* gctx;         // [g] ConsensusTransactions
 };
 
 __device__ __forceinline__ int rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -663,7 +682,7 @@ template <int NM, int OCC>
 __global__ __launch_bounds__(256, OCC) void kb_consensus(BT t) {
   // KB: the LDS sort's capacity, a power of two (the network pads to one)
   constexpr int NWV = 4, RW = 8, UL = 1536, KB = 1024, CPW = 2, NCH = NWV * CPW, SPAN = 64 * NCH;
-  const int g = blockIdx.x;
+  const int g = t.glist ? t.glist[blockIdx.x] : blockIdx.x;
   const GDesc d = t.gd[g];
   const int N = t.N, SM = t.SM, cc = t.ccap;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, NT = NWV * 64;
@@ -1200,6 +1219,8 @@ __global__ __launch_bounds__(256, OCC) void kb_consensus(BT t) {
   }
 }
 
+#include "hge_batch_bulk.hip"
+
 }  // namespace hgb
 
 // ===========================================================================
@@ -1242,7 +1263,7 @@ struct Buf {
 struct hge_batch {
   int N = 0, SM = 1, device = 0, ncu = 256;
   hipStream_t st = nullptr;
-  hipEvent_t ev[6] = {};
+  hipEvent_t ev[9] = {};
   std::string err;
   struct Graph {
     std::vector<int32_t> cr, ix, sp, op, oc, ntx;
@@ -1259,7 +1280,7 @@ struct hge_batch {
   int64_t Ktot = 0, Rtot = 0;
   int ccap = 0;
   std::vector<int64_t> h_scal;
-  static constexpr int NK = 5;
+  static constexpr int NK = 8;  // coords, fd, fdrows, front, fame (prep + pairs), fold (+ theta), receive, order
   float kms[NK] = {};
   // device tables
   Buf<GDesc> d_gd;
@@ -1274,6 +1295,15 @@ struct hge_batch {
   Buf<int8_t> d_fame;
   Buf<uint64_t> d_dbg;
   bool dbg_on = getenv("HGB_STAMPS") != nullptr;
+  // the bulk call schedule; HGB_SERIAL=1 (test hook): every graph through kb_consensus
+  bool serial = getenv("HGB_SERIAL") != nullptr;
+  Buf<int32_t> d_glist, d_cg, d_Rc, d_rfirst, d_rrank, d_xcall, d_gx, d_nivl, d_fsuf, d_thp, d_thR, d_rcall, d_bcnt, d_boff, d_wlc;
+  Buf<uint64_t> d_arr, d_Dp, d_ivF, d_thF;
+  Buf<int4> d_ivh;
+  Buf<int4> d_wl;
+  Buf<int64_t> d_gctx;
+  int Emax = 0;
+  int64_t n_fallback = 0;  // graphs the last run replayed through kb_consensus
 
   void free_all() {
     d_gd.free_();
@@ -1284,6 +1314,13 @@ struct hge_batch {
     for (auto* b : {&d_ts, &d_tsch, &d_calls, &d_cts, &d_counts, &d_scal, &d_kct}) b->free_();
     for (auto* b : {&d_S, &d_ssb, &d_seeb, &d_ks0, &d_Sch}) b->free_();
     d_ntxch.free_();
+    for (auto* b : {&d_glist, &d_cg, &d_Rc, &d_rfirst, &d_rrank, &d_xcall, &d_gx, &d_nivl, &d_fsuf, &d_thp, &d_thR, &d_rcall, &d_bcnt,
+                    &d_boff, &d_wlc})
+      b->free_();
+    for (auto* b : {&d_arr, &d_Dp, &d_ivF, &d_thF}) b->free_();
+    d_ivh.free_();
+    d_wl.free_();
+    d_gctx.free_();
     d_coin.free_();
     d_wit.free_();
     d_WCOIN.free_();
@@ -1381,7 +1418,12 @@ struct hge_batch {
     }
     if (Rtot >= INT32_MAX || Ktot >= INT32_MAX) throw BatchError{HGE_ERR_CAPACITY, "batch too large"};
     if (ccap >= (1 << 24)) throw BatchError{HGE_ERR_CAPACITY, "batch graph with a chain of 2^24 events or more"};
-    std::vector<int32_t> cr, ix, sp, op, oc, ntx, clen((size_t)G * N), chain((size_t)G * N * ccap, -1);
+    std::vector<int32_t> cr, ix, sp, op, oc, ntx, clen((size_t)G * N), chain((size_t)G * N * ccap, -1), cgv;
+    Emax = 0;
+    for (int g = 0; g < G; g++) {
+      cgv.insert(cgv.end(), (size_t)hd[g].K, g);
+      Emax = std::max(Emax, hd[g].E);
+    }
     std::vector<int64_t> ts, tsch((size_t)G * N * ccap, 0), calls;
     std::vector<uint64_t> Sch((size_t)G * N * ccap, 0);
     std::vector<int32_t> ntxch((size_t)G * N * ccap, 0);
@@ -1425,6 +1467,7 @@ struct hge_batch {
     up(d_tsch, tsch);
     up(d_Sch, Sch);
     up(d_ntxch, ntxch);
+    up(d_cg, cgv);
     d_gd.need(G);
     BCHK(hipMemcpyAsync(d_gd.p, hd.data(), sizeof(GDesc) * G, hipMemcpyHostToDevice, st));
     const size_t E1 = (size_t)std::max<int64_t>(Etot, 1);
@@ -1458,6 +1501,28 @@ struct hge_batch {
     d_counts.need(std::max<int64_t>(Ktot, 1));
     d_scal.need((size_t)G * 8);
     if (dbg_on) d_dbg.need((size_t)G * 8);
+    const size_t K1 = (size_t)std::max<int64_t>(Ktot, 1);
+    d_glist.need(G);
+    d_Rc.need(K1);
+    d_rfirst.need(RN / N);
+    d_xcall.need(E1);
+    d_arr.need(E1);
+    d_Dp.need(K1 * BNS * 2);
+    d_gx.need((size_t)G * 16);
+    d_ivh.need(RN / N * BVCAP);
+    d_ivF.need(RN / N * BVCAP);
+    d_nivl.need(RN / N);
+    d_fsuf.need(RN / N);
+    d_thp.need((size_t)G * BICAP * N);
+    d_thR.need((size_t)G * BICAP);
+    d_thF.need((size_t)G * BICAP);
+    d_rcall.need(E1);
+    d_rrank.need(E1);
+    d_bcnt.need(K1);
+    d_boff.need(K1);
+    d_wl.need(K1);
+    d_wlc.need(1);
+    d_gctx.need(G);
     BCHK(hipStreamSynchronize(st));
     staged = true;
   }
@@ -1512,6 +1577,28 @@ struct hge_batch {
     t.ks0 = d_ks0.p;
     t.kid = d_kid.p;
     t.dbg = dbg_on ? d_dbg.p : nullptr;
+    t.glist = nullptr;
+    t.cg = d_cg.p;
+    t.Rc = d_Rc.p;
+    t.rfirst = d_rfirst.p;
+    t.xcall = d_xcall.p;
+    t.arr = d_arr.p;
+    t.Dp = d_Dp.p;
+    t.gx = d_gx.p;
+    t.ivh = d_ivh.p;
+    t.ivF = d_ivF.p;
+    t.nivl = d_nivl.p;
+    t.fsuf = d_fsuf.p;
+    t.thp = d_thp.p;
+    t.thR = d_thR.p;
+    t.thF = d_thF.p;
+    t.rcall = d_rcall.p;
+    t.rrank = d_rrank.p;
+    t.bcnt = d_bcnt.p;
+    t.boff = d_boff.p;
+    t.wl = d_wl.p;
+    t.wlc = d_wlc.p;
+    t.gctx = d_gctx.p;
     return t;
   }
 
@@ -1520,6 +1607,37 @@ struct hge_batch {
     hipLaunchKernelGGL(kern, dim3(G), dim3(block), 0, st, t);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) throw BatchError{HGE_ERR_DEVICE, std::string("batch launch: ") + hipGetErrorString(e)};
+  }
+
+  template <int NM>
+  void run_stages(int G, const BT& t) {
+    launch(kb_coords<NM>, G, t, 256);
+    BCHK(hipEventRecord(ev[1], st));
+    launch(kb_fd<NM>, G * N, t);
+    BCHK(hipEventRecord(ev[2], st));
+    launch(kb_fdrows<NM>, G * N, t, 256);
+    BCHK(hipEventRecord(ev[3], st));
+    launch(kb_front<NM>, G, t, 1024);
+    BCHK(hipEventRecord(ev[4], st));
+    if (serial) {  // every graph through kb_consensus, after the run's readback
+      for (int k = 5; k < 9; k++) BCHK(hipEventRecord(ev[k], st));
+      return;
+    }
+    launch(kb_prep<NM>, G, t, 1024);
+    hipLaunchKernelGGL(kb_pairs<NM>, dim3(8, (unsigned)G), dim3(256), 0, st, t);
+    BCHK(hipGetLastError());
+    BCHK(hipEventRecord(ev[5], st));
+    launch(kb_fold<NM>, G, t, 64);
+    launch(kb_theta<NM>, G, t, 256);
+    BCHK(hipEventRecord(ev[6], st));
+    if (Emax > 0) {
+      hipLaunchKernelGGL(kb_receive<NM>, dim3((unsigned)(N * ((ccap + 255) / 256)), (unsigned)G), dim3(256), 0, st, t);
+      BCHK(hipGetLastError());
+    }
+    BCHK(hipEventRecord(ev[7], st));
+    launch(kb_order_prep<NM>, G, t, 1024);
+    launch(kb_sort, (int)std::min<int64_t>(std::max<int64_t>(Ktot, 1), (int64_t)ncu * 8), t, 256);
+    BCHK(hipEventRecord(ev[8], st));
   }
 
   int64_t run() {
@@ -1539,36 +1657,42 @@ struct hge_batch {
     BCHK(hipMemsetAsync(d_rr.p, 0xFF, E1 * 4, st));
     BCHK(hipMemsetAsync(d_cts.p, 0, E1 * 8, st));
     BCHK(hipMemsetAsync(d_scal.p, 0, (size_t)G * 64, st));
-    const BT t = tables();
+    const size_t K1 = (size_t)std::max<int64_t>(Ktot, 1);
+    BCHK(hipMemsetAsync(d_bcnt.p, 0, K1 * 4, st));
+    BCHK(hipMemsetAsync(d_wlc.p, 0, 4, st));
+    BCHK(hipMemsetAsync(d_gctx.p, 0, (size_t)G * 8, st));
+    BT t = tables();
     BCHK(hipEventRecord(ev[0], st));
-    if (N <= 32) {
-      launch(kb_coords<32>, G, t, 256);
-      BCHK(hipEventRecord(ev[1], st));
-      launch(kb_fd<32>, G * N, t);
-      BCHK(hipEventRecord(ev[2], st));
-      launch(kb_fdrows<32>, G * N, t, 256);
-      BCHK(hipEventRecord(ev[3], st));
-      launch(kb_front<32>, G, t, 1024);
-      BCHK(hipEventRecord(ev[4], st));
-      if (G > 2 * ncu) launch(kb_consensus<32, 4>, G, t, 256);
-      else launch(kb_consensus<32, 1>, G, t, 256);
-    } else {
-      launch(kb_coords<64>, G, t, 256);
-      BCHK(hipEventRecord(ev[1], st));
-      launch(kb_fd<64>, G * N, t);
-      BCHK(hipEventRecord(ev[2], st));
-      launch(kb_fdrows<64>, G * N, t, 256);
-      BCHK(hipEventRecord(ev[3], st));
-      launch(kb_front<64>, G, t, 1024);
-      BCHK(hipEventRecord(ev[4], st));
-      if (G > 2 * ncu) launch(kb_consensus<64, 4>, G, t, 256);
-      else launch(kb_consensus<64, 1>, G, t, 256);
-    }
-    BCHK(hipEventRecord(ev[5], st));
+    if (N <= 32) run_stages<32>(G, t);
+    else run_stages<64>(G, t);
     h_scal.resize((size_t)G * 8);
     BCHK(hipMemcpyAsync(h_scal.data(), d_scal.p, (size_t)G * 64, hipMemcpyDeviceToHost, st));
     BCHK(hipStreamSynchronize(st));
     for (int k = 0; k < NK; k++) BCHK(hipEventElapsedTime(&kms[k], ev[k], ev[k + 1]));
+    // graphs the bulk fold could not hold: replayed by kb_consensus (their outputs untouched so far)
+    std::vector<int32_t> fb;
+    for (int g = 0; g < G; g++)
+      if (serial || (h_scal[(size_t)g * 8 + 7] && !h_scal[(size_t)g * 8 + 6])) fb.push_back(g);
+    n_fallback = (int64_t)fb.size();
+    if (!fb.empty()) {
+      BCHK(hipMemcpyAsync(d_glist.p, fb.data(), fb.size() * 4, hipMemcpyHostToDevice, st));
+      t.glist = d_glist.p;
+      const int F = (int)fb.size();
+      float ms = 0;
+      BCHK(hipEventRecord(ev[7], st));
+      if (N <= 32) {
+        if (F > 2 * ncu) launch(kb_consensus<32, 4>, F, t, 256);
+        else launch(kb_consensus<32, 1>, F, t, 256);
+      } else {
+        if (F > 2 * ncu) launch(kb_consensus<64, 4>, F, t, 256);
+        else launch(kb_consensus<64, 1>, F, t, 256);
+      }
+      BCHK(hipEventRecord(ev[8], st));
+      BCHK(hipMemcpyAsync(h_scal.data(), d_scal.p, (size_t)G * 64, hipMemcpyDeviceToHost, st));
+      BCHK(hipStreamSynchronize(st));
+      BCHK(hipEventElapsedTime(&ms, ev[7], ev[8]));
+      kms[NK - 1] += ms;
+    }
     if (dbg_on) {  // section cycles of kb_consensus, summed over the graphs
       std::vector<uint64_t> hd_((size_t)G * 8);
       BCHK(hipMemcpy(hd_.data(), d_dbg.p, (size_t)G * 64, hipMemcpyDeviceToHost));
@@ -1709,6 +1833,8 @@ int hge_batch_results(hge_batch* b, int32_t g, int32_t* order, int64_t* counts, 
   return HGE_OK;
   BGUARD_END(b)
 }
+
+int64_t hge_batch_fallbacks(hge_batch* b) { return b ? b->n_fallback : -1; }
 
 int hge_batch_kernel_ms(hge_batch* b, float* ms, int32_t cap) {
   if (!b || (!ms && cap > 0)) return HGE_ERR_ARG;

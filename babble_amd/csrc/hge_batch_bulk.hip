@@ -1,0 +1,823 @@
+// hge_batch_bulk.hip — the batch engine's call schedule in bulk (included by
+// hge_batch.hip inside namespace hgb; the CPU model of these stages is
+// tests/bulk_model.py, checked against the oracle by tests/test_bulk_model.py).
+//
+// kb_consensus walks a graph's call points in order, one workgroup per graph, so
+// a GPU holding fewer graphs than CUs waits on each graph's ~11 us per call.  But
+// once kb_front has every event's round and witness flag (a function of the
+// event's ancestry alone), RunConsensus (node/core.go:179-202) at call c depends on
+// the earlier calls only through the persisted fame and LastConsensusRound:
+//   kb_prep     R_c, each event's insertion call, the witnesses in insertion order;
+//   kb_pairs    DecideFame's decisions for round i at call c (hashgraph.go:598-664;
+//               `votes` is rebuilt every call, so they depend on the witnesses
+//               present at c alone), one wave per (call, i = R_c - 2 - s), s < NS;
+//   kb_fold     per graph, one wave over the calls in order: arrivals set the
+//               present-witness masks, rounds LCR+1 .. R_c-2 take their pair's
+//               decisions (a pair outside the window is decided inline), then
+//               setLastConsensusRound (:666-673); each round's (decided, famous set)
+//               state over the calls as intervals;
+//   kb_theta    per interval, the receive threshold per creator (the (|F|/2+1)-th
+//               largest lastAncestor index over the famous witnesses F: x is seen by
+//               more than half of them iff index(x) <= theta, :696-712);
+//   kb_receive  per event, the first call at which a round above it has a decided
+//               interval that sees it, the lowest such round at that call
+//               (DecideRoundReceived, :676-721), and MedianTimestamp (:762-770);
+//   kb_order_prep / kb_sort   per call, the received events (FindOrder, :723-760)
+//               sorted by (roundReceived, timestamp, S, id) (consensus_sorter.go:36-59,
+//               PRN = 0), the undetermined list, the scalars.
+// A graph the fold cannot hold (more than 64 * FRS rounds, an interval table past
+// its capacity) is flagged in scal[7] and replayed by kb_consensus.
+
+constexpr int BNS = 3;      // DecideFame pairs per call: rounds R_c - 2 - s, s < BNS
+constexpr int BVCAP = 4;    // receive intervals per round
+constexpr int BICAP = 512;  // receive intervals per graph
+constexpr int FRS = 4;      // rounds per lane in kb_fold (64 * FRS rounds)
+constexpr int BLK = 1024;   // call buckets sorted in LDS up to this many keys
+
+// per-graph internals, t.gx[g * 16 + k]
+enum { GX_NARR = 0, GX_LCR = 2, GX_LCRC = 3, GX_NIV = 4, GX_MISS = 5, GX_RF = 6, GX_NLAST = 7 };
+
+// inclusive block scans over blockDim.x threads (a multiple of 64), s_w: blockDim.x / 64 ints
+__device__ __forceinline__ int block_scan_add(int v, int* s_w, int& total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_w[wv] = x;
+  __syncthreads();
+  int pre = 0, tot = 0;
+  for (int w = 0; w < nw; w++) {
+    const int s = s_w[w];
+    tot += s;
+    if (w < wv) pre += s;
+  }
+  __syncthreads();
+  total = tot;
+  return x + pre;
+}
+__device__ __forceinline__ int block_scan_max(int v, int* s_w, int& total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x = max(x, y);
+  }
+  if (lane == 63) s_w[wv] = x;
+  __syncthreads();
+  int pre = INT32_MIN, tot = INT32_MIN;
+  for (int w = 0; w < nw; w++) {
+    const int s = s_w[w];
+    tot = max(tot, s);
+    if (w < wv) pre = max(pre, s);
+  }
+  __syncthreads();
+  total = tot;
+  return max(x, pre);
+}
+
+// R_c, the insertion call of every event and the witnesses in insertion order
+// (arrival call << 32 | round << 8 | creator).  One 1024-thread workgroup per graph.
+template <int NM>
+__global__ __launch_bounds__(1024) void kb_prep(BT t) {
+  const int g = blockIdx.x;
+  const GDesc d = t.gd[g];
+  const int tid = threadIdx.x, NT = 1024;
+  __shared__ int s_w[16], s_pm[1024];
+  int32_t* gx = t.gx + (int64_t)g * 16;
+  if (t.scal[(int64_t)g * 8 + 6]) return;  // the rounds pass failed
+  const int K = d.K;
+  const int n_last = K > 0 ? (int)t.calls[d.co + K - 1] : 0;
+  int carry = -1;  // the highest round so far
+  for (int c0 = 0; c0 < K; c0 += NT) {
+    const int c = c0 + tid;
+    int mx = -1;
+    if (c < K) {
+      const int lo = c ? (int)t.calls[d.co + c - 1] : 0, hi = (int)t.calls[d.co + c];
+      for (int x = lo; x < hi; x++) {
+        t.xcall[d.eo + x] = c;
+        mx = max(mx, t.round[d.eo + x]);
+      }
+    }
+    int tot;
+    const int pm = max(block_scan_max(mx, s_w, tot), carry);
+    if (c < K) t.Rc[d.co + c] = pm + 1;
+    // rfirst[r] = the first call with R_c >= r, for r <= R of the last call
+    s_pm[tid] = pm;
+    __syncthreads();
+    const int prv = tid ? s_pm[tid - 1] : carry;
+    if (c < K)
+      for (int r = prv + 2; r <= pm + 1; r++) t.rfirst[d.ro + r] = c;
+    carry = max(carry, tot);
+    __syncthreads();
+  }
+  for (int x = n_last + tid; x < d.E; x += NT) t.xcall[d.eo + x] = K;
+  __threadfence_block();
+  __syncthreads();
+  int base = 0;
+  for (int x0 = 0; x0 < n_last; x0 += NT) {
+    const int x = x0 + tid;
+    const bool w = x < n_last && t.wit[d.eo + x];
+    int tot;
+    const int inc = block_scan_add(w ? 1 : 0, s_w, tot);
+    if (w) {
+      const uint32_t rc = (uint32_t)t.round[d.eo + x] << 8 | (uint32_t)t.cr[d.eo + x];
+      t.arr[d.eo + base + inc - 1] = (uint64_t)(uint32_t)ld(&t.xcall[d.eo + x]) << 32 | rc;
+    }
+    base += tot;
+  }
+  if (tid == 0) {
+    gx[GX_NARR] = base;
+    gx[GX_NLAST] = n_last;
+    gx[GX_RF] = K > 0 ? carry + 1 : 0;
+  }
+}
+
+// DecideFame for round i at a call that holds n_c events and R rounds
+// (hashgraph.go:598-664), one wave: lane y is a voter of round j (two half waves,
+// each its own witness x, at NM <= 32), the witnesses x of round i in chunks of
+// 16 per lane group.  For one x and one j every present y's yays / nays come from
+// popcounts at once; the y loop's `break` is the first y whose tally reaches SM
+// (a ballot's lowest bit): x's votes from round j are the v of the y before it and
+// its fame the v of that y; the last deciding j wins.  Coin rounds (diff % N == 0)
+// vote the middle bit where no supermajority; missing votes are nays.  dec: the
+// present witnesses decided at this call, val: their values (1 = famous).
+// src: the witness rows of rounds j >= i -- W(j, y) (id, -1 none), see(j, y) / ss(j, y)
+// (bits over round j-1's creators), coin(j, y).
+template <int NM, typename Src>
+__device__ void fame_pair(const BT& t, const Src& src, int i, int n_c, int R, uint64_t& dec_out,
+                          uint64_t& val_out) {
+  constexpr int HV = NM <= 32 ? 2 : 1, KX = 16, XPC = HV * KX;
+  const int lane = threadIdx.x & 63, N = t.N, SM = t.SM;
+  const int h = HV == 2 ? lane >> 5 : 0, y = HV == 2 ? (lane & 31) : lane;
+  auto half = [&](uint64_t m) -> uint64_t { return HV == 2 ? (m >> (32 * h)) & 0xFFFFFFFFull : m; };
+  const int wi = lane < N ? src.W(i, lane) : -1;
+  const uint64_t pm = ballot(lane < N && wi >= 0 && wi < n_c);
+  uint64_t dec = 0, val = 0;
+  for (int xc = 0; xc < N; xc += XPC) {
+    int fv[KX];
+    uint64_t prev[KX];
+#pragma unroll
+    for (int k = 0; k < KX; k++) {
+      fv[k] = 0;
+      prev[k] = 0;
+    }
+    for (int j = i + 1; j < R; j++) {
+      const int diff = j - i;
+      const int yid = y < N ? src.W(j, y) : -1;
+      const bool py = yid >= 0 && yid < n_c;
+      uint64_t yb = 0;
+      bool ycoin = false;
+      if (py) {
+        yb = diff == 1 ? src.see(j, y) : src.ss(j, y);
+        ycoin = src.coin(j, y);
+      }
+      const int tot = __popcll(yb);
+#pragma unroll
+      for (int k = 0; k < KX; k++) {
+        const int x = xc + h + HV * k;
+        uint64_t cur;
+        if (diff == 1) {
+          cur = half(ballot(py && x < 64 && ((yb >> (x & 63)) & 1)));  // setVote(y, x, See(y, x))
+        } else {
+          const int yays = __popcll(yb & prev[k]), nays = tot - yays;
+          const bool v = yays >= nays;
+          const int tt = v ? yays : nays;
+          if (diff % N != 0) {  // normal round: SetFame(x, v) and break at the first tt >= SM
+            const uint64_t dm = half(ballot(py && tt >= SM));
+            const uint64_t vm = half(ballot(py && v));
+            if (dm) {
+              const int ys = __ffsll((unsigned long long)dm) - 1;
+              fv[k] = (vm >> ys) & 1 ? 1 : 2;
+              cur = vm & ((1ull << ys) - 1);
+            } else {
+              cur = vm;
+            }
+          } else {  // coin round: the middle bit of y's hash when no supermajority
+            cur = half(ballot(py && (tt >= SM ? v : ycoin)));
+          }
+        }
+        prev[k] = cur;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KX; k++) {
+      const int x = xc + h + HV * k;
+      const bool on = y == 0 && x < N && ((pm >> x) & 1) && fv[k] != 0;
+      const uint64_t fb = ballot(on), vb = ballot(on && fv[k] == 1);
+      if (fb & 1) {
+        dec |= 1ull << (xc + HV * k);
+        if (vb & 1) val |= 1ull << (xc + HV * k);
+      }
+      if (HV == 2 && ((fb >> 32) & 1)) {
+        dec |= 1ull << (xc + 1 + HV * k);
+        if ((vb >> 32) & 1) val |= 1ull << (xc + 1 + HV * k);
+      }
+    }
+  }
+  dec_out = dec;
+  val_out = val;
+}
+
+// the witness rows in HBM
+struct GSrc {
+  const BT& t;
+  int64_t ro;
+  int N;
+  __device__ int W(int j, int y) const { return t.W[(ro + j) * N + y]; }
+  __device__ uint64_t see(int j, int y) const { return t.seeb[(ro + j) * N + y]; }
+  __device__ uint64_t ss(int j, int y) const { return t.ssb[(ro + j) * N + y]; }
+  __device__ bool coin(int j, int y) const { return t.WCOIN[(ro + j) * N + y] != 0; }
+};
+// rounds i0 .. i0 + BNS staged in LDS
+template <int NM>
+struct LSrc {
+  const int32_t (*w)[NM];
+  const uint64_t (*se)[NM];
+  const uint64_t (*sS)[NM];
+  const uint8_t (*co)[NM];
+  int i0;
+  __device__ int W(int j, int y) const { return w[j - i0][y]; }
+  __device__ uint64_t see(int j, int y) const { return se[j - i0][y]; }
+  __device__ uint64_t ss(int j, int y) const { return sS[j - i0][y]; }
+  __device__ bool coin(int j, int y) const { return co[j - i0][y] != 0; }
+};
+
+// DecideFame's pairs by round: workgroup (k, g) takes graph g's rounds i = k, k +
+// gridDim.x, ..., stages the witness rows of rounds i .. i + BNS in LDS and decides
+// round i at every call whose window holds it (R_c in [i + 3, i + 1 + BNS], a
+// range of calls: R_c never decreases), one wave per call.  Round R_c - 2 (s = 0)
+// sees one voting round only (diff = 1 sets votes, decides nothing): no pair.
+template <int NM>
+__global__ __launch_bounds__(256) void kb_pairs(BT t) {
+  constexpr int RB = BNS + 1;
+  const int g = blockIdx.y;
+  if (t.scal[(int64_t)g * 8 + 6]) return;
+  const GDesc d = t.gd[g];
+  const int N = t.N, tid = threadIdx.x, wv = tid >> 6;
+  const int Rf = t.gx[(int64_t)g * 16 + GX_RF];
+  __shared__ int32_t sW[RB][NM];
+  __shared__ uint64_t sSee[RB][NM], sSs[RB][NM];
+  __shared__ uint8_t sCo[RB][NM];
+  const LSrc<NM> src{sW, sSee, sSs, sCo, 0};
+  for (int i = blockIdx.x; i <= Rf - 2; i += gridDim.x) {
+    for (int e = tid; e < RB * N; e += 256) {
+      const int jj = e / N, y = e - (e / N) * N, j = i + jj;
+      if (j < Rf) {
+        const int64_t rj = (int64_t)(d.ro + j) * N + y;
+        sW[jj][y] = t.W[rj];
+        sSee[jj][y] = t.seeb[rj];
+        sSs[jj][y] = t.ssb[rj];
+        sCo[jj][y] = t.WCOIN[rj];
+      } else {
+        sW[jj][y] = -1;
+      }
+    }
+    // s = 0 (j = i + 1 only: votes, no decision) is never computed
+    const int lo = i + 3 <= Rf ? t.rfirst[d.ro + i + 3] : d.K;
+    const int hi = i + 2 + BNS <= Rf ? t.rfirst[d.ro + i + 2 + BNS] : d.K;
+    __syncthreads();
+    LSrc<NM> sr = src;
+    sr.i0 = i;
+    for (int c = lo + wv; c < hi; c += 4) {
+      const int R = t.Rc[d.co + c], s = R - 2 - i;
+      uint64_t dec, val;
+      fame_pair<NM>(t, sr, i, (int)t.calls[d.co + c], R, dec, val);
+      if ((tid & 63) == 0) {
+        const int64_t p = (int64_t)(d.co + c) * BNS + s;
+        t.Dp[2 * p] = dec;
+        t.Dp[2 * p + 1] = val;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// The calls in order, one wave per graph.  Lane l keeps rounds l, l + 64, ...
+// (FRS slots): present witnesses, decided and famous masks, the open interval.
+// Per call: its arrivals, then DecideFame's rounds LCR+1 .. R_c-2 from the pairs
+// (inline past the window), setLastConsensusRound (the highest decided round of
+// the loop), then every touched round's (decided, famous set) state: a change
+// closes the open interval [start, c) and opens one when decided with a famous
+// witness.  Rounds with no famous witness receive nothing (len(s) > 0 fails).
+template <int NM>
+__global__ __launch_bounds__(64) void kb_fold(BT t) {
+  const int g = blockIdx.x;
+  const GDesc d = t.gd[g];
+  const int lane = threadIdx.x, N = t.N, K = d.K;
+  int32_t* gx = t.gx + (int64_t)g * 16;
+  if (t.scal[(int64_t)g * 8 + 6]) return;
+  const int Rf = gx[GX_RF], narr = gx[GX_NARR];
+  if (Rf > 64 * FRS) {
+    if (lane == 0) t.scal[(int64_t)g * 8 + 7] = 1;
+    return;
+  }
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  uint64_t pres[FRS], dfn[FRS], vl[FRS], oF[FRS];
+  int ost[FRS], ni[FRS], fst[FRS];
+  bool tch[FRS];
+#pragma unroll
+  for (int q = 0; q < FRS; q++) {
+    pres[q] = dfn[q] = vl[q] = oF[q] = 0;
+    ost[q] = -1;
+    ni[q] = 0;
+    fst[q] = INF;
+    tch[q] = false;
+  }
+  int LCR = -1, lcr_call = -1, nth = 0, miss = 0;
+  bool fail = false;
+  // emission of the closing intervals of slot q at call ce (lanes with em)
+  auto emit = [&](int q, bool em, int ce) {
+    const uint64_t m = ballot(em);
+    if (!m) return;
+    if (em) {
+      const int r = q * 64 + lane, slot = nth + __popcll(m & below);
+      if (ni[q] < BVCAP && slot < BICAP) {
+        const int64_t iv = (int64_t)(d.ro + r) * BVCAP + ni[q];
+        t.ivh[iv] = make_int4(ost[q], ce, slot, 0);
+        t.ivF[iv] = oF[q];
+        t.thR[(int64_t)g * BICAP + slot] = r;
+        t.thF[(int64_t)g * BICAP + slot] = oF[q];
+      } else {
+        fail = true;
+      }
+      ni[q]++;
+    }
+    nth += __popcll(m);
+  };
+  int ap = 0, abase = 0;
+  uint64_t areg = lane < narr ? t.arr[d.eo + lane] : ~0ull;
+  for (int c0 = 0; c0 < K; c0 += 64) {
+    const int cl = c0 + lane;
+    const bool on = cl < K;
+    const int Rreg = on ? t.Rc[d.co + cl] : 0;
+    const int Nreg = on ? (int)t.calls[d.co + cl] : 0;
+    uint64_t Dd[BNS], Dv[BNS];
+#pragma unroll
+    for (int s = 0; s < BNS; s++) {
+      const int64_t p = ((int64_t)(d.co + cl)) * BNS + s;
+      const bool ok = on && s > 0 && Rreg - 2 - s >= 0;
+      Dd[s] = ok ? t.Dp[2 * p] : 0;
+      Dv[s] = ok ? t.Dp[2 * p + 1] : 0;
+    }
+    const int m = min(64, K - c0);
+    for (int cc = 0; cc < m; cc++) {
+      const int c = c0 + cc;
+      // DivideRounds: the call's new witnesses join their rounds
+      while (ap < narr) {
+        if (ap - abase == 64) {
+          abase = ap;
+          areg = ap + lane < narr ? t.arr[d.eo + ap + lane] : ~0ull;
+        }
+        const uint64_t a = rl64(areg, ap - abase);
+        if ((int)(a >> 32) != c) break;
+        const int r = (int)((a >> 8) & 0xFFFFFF), k = (int)(a & 0xFF);
+#pragma unroll
+        for (int q = 0; q < FRS; q++)
+          if (q == (r >> 6) && lane == (r & 63)) {
+            pres[q] |= 1ull << k;
+            tch[q] = tch[q] || ost[q] >= 0;  // a new witness can only undo a decided state
+          }
+        ap++;
+      }
+      // DecideFame's rounds
+      const int R = rl(Rreg, cc);
+      int newL = -1;
+      // (round R - 2 meets one voting round: nothing is decided there, it is not decided
+      // from an earlier call either -- R never decreases -- so it is skipped)
+      for (int i = LCR + 1; i <= R - 3; i++) {
+        const int s = R - 2 - i;
+        uint64_t dec = 0, v = 0;
+        if (s < BNS) {
+#pragma unroll
+          for (int q = 0; q < BNS; q++)
+            if (q == s) {
+              dec = rl64(Dd[q], cc);
+              v = rl64(Dv[q], cc);
+            }
+        } else {
+          fame_pair<NM>(t, GSrc{t, (int64_t)d.ro, N}, i, rl(Nreg, cc), R, dec, v);
+          miss++;
+        }
+        bool dcd = false;
+#pragma unroll
+        for (int q = 0; q < FRS; q++)
+          if (q == (i >> 6) && lane == (i & 63)) {
+            dfn[q] |= dec;
+            vl[q] = (vl[q] & ~dec) | v;
+            tch[q] = true;
+            dcd = (pres[q] & ~dfn[q]) == 0;
+          }
+        if (ballot(dcd)) newL = i;  // WitnessesDecided (roundInfo.go:78-85)
+      }
+      if (newL >= 0) {
+        LCR = newL;
+        lcr_call = c;
+      }
+      // the touched rounds' receive state
+#pragma unroll
+      for (int q = 0; q < FRS; q++) {
+        if (q * 64 >= Rf || !ballot(tch[q])) continue;
+        bool em = false;
+        uint64_t key = oF[q];
+        if (tch[q]) {
+          const bool dcd = (pres[q] & ~dfn[q]) == 0;
+          key = dcd ? pres[q] & vl[q] : 0;
+          em = key != oF[q] && ost[q] >= 0;
+        }
+        emit(q, em, c);
+        if (tch[q] && key != oF[q]) {
+          ost[q] = key ? c : -1;
+          oF[q] = key;
+          if (key && fst[q] == INF) fst[q] = c;
+        }
+        tch[q] = false;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < FRS; q++)
+    if (q * 64 < Rf) emit(q, ost[q] >= 0, K);
+  if (ballot(fail)) {
+    if (lane == 0) t.scal[(int64_t)g * 8 + 7] = 1;
+    return;
+  }
+  // per round: interval count, the suffix minimum of the first intervals' starts
+  // (kb_receive stops once no higher round can receive earlier), the fame row
+  int carry = INF;
+#pragma unroll
+  for (int q = FRS - 1; q >= 0; q--) {
+    int v = fst[q];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_down(v, o);
+      if (lane + o < 64) v = min(v, u);
+    }
+    v = min(v, carry);
+    carry = rl(v, 0);
+    const int r = q * 64 + lane;
+    if (r < Rf) {
+      t.nivl[d.ro + r] = ni[q];
+      t.fsuf[d.ro + r] = v;
+      if (dfn[q])
+        for (int x = 0; x < N; x++)
+          if ((dfn[q] >> x) & 1) t.fame[(int64_t)(d.ro + r) * N + x] = (int8_t)((vl[q] >> x) & 1 ? 1 : 2);
+    }
+  }
+  if (lane == 0) {
+    gx[GX_LCR] = LCR;
+    gx[GX_LCRC] = lcr_call;
+    gx[GX_NIV] = nth;
+    gx[GX_MISS] = miss;
+  }
+}
+
+// the receive thresholds of every interval: one wave per interval, lane = creator
+template <int NM>
+__global__ __launch_bounds__(256) void kb_theta(BT t) {
+  const int g = blockIdx.x;
+  const GDesc d = t.gd[g];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, N = t.N;
+  if (t.scal[(int64_t)g * 8 + 6] || t.scal[(int64_t)g * 8 + 7]) return;
+  const int nth = t.gx[(int64_t)g * 16 + GX_NIV];
+  const int32_t* LA = t.LA + d.eo * N;
+  for (int s = wv; s < nth; s += 4) {
+    const int r = t.thR[(int64_t)g * BICAP + s];
+    const uint64_t F = t.thF[(int64_t)g * BICAP + s];
+    const int m = __popcll(F), need = m / 2 + 1;  // len(s) > len(fws)/2
+    const int w = lane < N ? t.W[(int64_t)(d.ro + r) * N + lane] : -1;
+    int32_t vals[NM];
+#pragma unroll
+    for (int dd = 0; dd < NM; dd++)
+      vals[dd] = (F >> dd) & 1 && lane < N ? LA[(int64_t)rl(w, dd) * N + lane] : INT32_MIN;
+    sort_regs32<NM>(vals);
+    int th = INT32_MIN;
+#pragma unroll
+    for (int a = 0; a < NM; a++)
+      if (a == NM - need) th = vals[a];
+    if (lane < N) t.thp[((int64_t)g * BICAP + s) * N + lane] = th;
+  }
+}
+
+// One thread per chain position (events below the last call): the event's receiving
+// call and round, then the median timestamp over OldestSelfAncestorToSee(w, x) of the
+// famous witnesses w that see x (w = (d, i_w) sees x iff FD[x][d] <= i_w, and the
+// chain-d event at FD[x][d] is then OldestSelfAncestorToSee), the upper median len/2.
+// Lanes take consecutive positions of one chain, whose first descendants on chain d
+// never decrease: the timestamp gathers of a wave stay on a few lines.
+template <int NM>
+__global__ __launch_bounds__(256) void kb_receive(BT t) {
+  const int g = blockIdx.y;
+  if (t.scal[(int64_t)g * 8 + 6] || t.scal[(int64_t)g * 8 + 7]) return;
+  const GDesc d = t.gd[g];
+  const int N = t.N, cc = t.ccap, lane = threadIdx.x & 63;
+  const int nb = (cc + 255) >> 8;  // position blocks per chain
+  const int c = blockIdx.x / nb, p0 = (blockIdx.x - c * nb) * 256;
+  const int len = t.clen[g * N + c];
+  if (p0 >= len) return;  // uniform per workgroup
+  const int p = p0 + threadIdx.x;
+  const int64_t cb = (int64_t)g * N * cc, cpos = (int64_t)c * cc + p;
+  const int n_last = t.gx[(int64_t)g * 16 + GX_NLAST];
+  const int x = p < len ? t.chain[cb + cpos] : -1;
+  const bool on = x >= 0 && x < n_last;
+  const int64_t eo = d.eo;
+  int best_c = INF, bi = -1;
+  uint64_t bF = 0;
+  if (on) {
+    const int r = t.round[eo + x], cl = t.xcall[eo + x];
+    const int Rf = t.gx[(int64_t)g * 16 + GX_RF];
+    for (int i = r + 1; i < Rf; i++) {
+      if (t.fsuf[d.ro + i] >= best_c) break;
+      const int n = t.nivl[d.ro + i];
+      for (int k = 0; k < n; k++) {
+        const int64_t iv = (int64_t)(d.ro + i) * BVCAP + k;
+        const int4 hv = t.ivh[iv];
+        if (hv.y <= cl) continue;
+        const int cand = max(hv.x, cl);
+        if (cand >= best_c) break;
+        if (p <= t.thp[((int64_t)g * BICAP + hv.z) * N + c]) {
+          best_c = cand;
+          bi = i;
+          bF = t.ivF[iv];
+          break;
+        }
+      }
+    }
+  }
+  // the call bucket's slot: one atomic per distinct call in the wave (a wave's
+  // consecutive positions are mostly received at the same call)
+  {
+    uint64_t todo = ballot(bi >= 0);
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    int rank = -1;
+    while (todo) {
+      const int lead = __ffsll((unsigned long long)todo) - 1;
+      const int cv = rl(best_c, lead);
+      const uint64_t same = ballot(bi >= 0 && best_c == cv);
+      int base = 0;
+      if (lane == lead) base = atomicAdd(&t.bcnt[d.co + cv], __popcll(same));
+      base = rl(base, lead);
+      if (bi >= 0 && best_c == cv) rank = base + __popcll(same & below);
+      todo &= ~same;
+    }
+    if (on) {
+      t.rcall[eo + x] = bi >= 0 ? best_c : -1;
+      t.rrank[eo + x] = rank;
+    }
+  }
+  int64_t tx = 0;
+  if (bi >= 0) {
+    const int32_t* FDr = t.FD + (cb + cpos) * N;
+    const int64_t* tschg = t.tsch + cb;
+    const int32_t* wixr = t.WIX + (int64_t)(d.ro + bi) * N;
+    const int64_t tsx = tschg[cpos];
+    // the row and the witnesses' positions, loaded unconditionally (all in flight)
+    int32_t fd[NM], wx[NM];
+    if ((N & 3) == 0) {  // 16-byte aligned rows: vector loads
+#pragma unroll
+      for (int k = 0; k < NM / 4; k++) {
+        const int4 v = 4 * k < N ? ((const int4*)FDr)[k] : make_int4(INF, INF, INF, INF);
+        const int4 w = 4 * k < N ? ((const int4*)wixr)[k] : make_int4(-1, -1, -1, -1);
+        fd[4 * k] = v.x;
+        fd[4 * k + 1] = v.y;
+        fd[4 * k + 2] = v.z;
+        fd[4 * k + 3] = v.w;
+        wx[4 * k] = w.x;
+        wx[4 * k + 1] = w.y;
+        wx[4 * k + 2] = w.z;
+        wx[4 * k + 3] = w.w;
+      }
+    } else {
+#pragma unroll
+      for (int dd = 0; dd < NM; dd++) {
+        fd[dd] = dd < N ? FDr[dd] : INF;
+        wx[dd] = dd < N ? wixr[dd] : -1;
+      }
+    }
+    int32_t vals[NM];
+    int m = 0;
+    bool ovf = false;
+    int64_t tq[NM];
+#pragma unroll
+    for (int dd = 0; dd < NM; dd++) {  // every gather issued before any is used
+      const bool in = dd < N && ((bF >> dd) & 1) && fd[dd] != INF && fd[dd] <= wx[dd];
+      tq[dd] = tschg[(int64_t)dd * cc + (in ? fd[dd] : 0)];
+    }
+#pragma unroll
+    for (int dd = 0; dd < NM; dd++) {
+      const bool in = dd < N && ((bF >> dd) & 1) && fd[dd] != INF && fd[dd] <= wx[dd];
+      const int64_t o = tq[dd] - tsx;
+      ovf = ovf || (in && (o < -(int64_t)INT32_MAX || o > (int64_t)INT32_MAX));
+      vals[dd] = in ? (int32_t)o : INT32_MAX;  // fillers sort last (a real INT32_MAX ties with them)
+      m += in;
+    }
+    const int32_t* wix = wixr;
+    const int want = m / 2;
+    int64_t med = 0;
+    if (!ovf) {
+      sort_regs32<NM>(vals);
+#pragma unroll
+      for (int a = 0; a < NM; a++)
+        if (a == want) med = tsx + vals[a];
+    } else {  // the value whose rank among the m timestamps covers `want`, exact in 64 bits
+      auto tv = [&](int dd, int64_t& v) -> bool {
+        if (!((bF >> dd) & 1)) return false;
+        const int q = FDr[dd];
+        if (q == INF || q > wix[dd]) return false;
+        v = tschg[(int64_t)dd * cc + q];
+        return true;
+      };
+      for (int a = 0; a < N; a++) {
+        int64_t va;
+        if (!tv(a, va)) continue;
+        int lt = 0, eq = 0;
+        for (int b = 0; b < N; b++) {
+          int64_t vb;
+          if (!tv(b, vb)) continue;
+          lt += vb < va;
+          eq += vb == va;
+        }
+        if (lt <= want && want < lt + eq) {
+          med = va;
+          break;
+        }
+      }
+    }
+    t.rr[eo + x] = bi;
+    t.cts[eo + x] = med;
+    tx = t.ntx[eo + x];
+  }
+  tx = wave_sum64(tx);
+  if (lane == 0 && tx) atomicAdd((unsigned long long*)&t.gctx[g], (unsigned long long)tx);
+}
+
+// Per graph: the call buckets' offsets (the per-call batch sizes), the received
+// events' keys scattered into their buckets, the undetermined list in insertion
+// order, LastCommitedRoundEvents and the scalars.  One 1024-thread workgroup.
+template <int NM>
+__global__ __launch_bounds__(1024) void kb_order_prep(BT t) {
+  const int g = blockIdx.x;
+  if (t.scal[(int64_t)g * 8 + 6] || t.scal[(int64_t)g * 8 + 7]) return;
+  const GDesc d = t.gd[g];
+  const int tid = threadIdx.x, NT = 1024;
+  const int64_t eo = d.eo;
+  __shared__ int s_w[16];
+  const int32_t* gx = t.gx + (int64_t)g * 16;
+  const int K = d.K, n_last = gx[GX_NLAST];
+  int carry = 0;
+  for (int c0 = 0; c0 < K; c0 += NT) {
+    const int c = c0 + tid;
+    const int v = c < K ? t.bcnt[d.co + c] : 0;
+    int tot;
+    const int inc = block_scan_add(v, s_w, tot);
+    if (c < K) {
+      t.boff[d.co + c] = carry + inc - v;
+      t.counts[d.co + c] = v;
+      if (v > 0) {
+        const int k = atomicAdd(t.wlc, 1);
+        t.wl[k] = make_int4(g, v, carry + inc - v, 0);
+      }
+    }
+    carry += tot;
+  }
+  const int nord = carry;
+  __threadfence_block();
+  __syncthreads();
+  for (int x = tid; x < n_last; x += NT) {
+    const int c = t.rcall[eo + x];
+    if (c < 0) continue;
+    const int pos = ld(&t.boff[d.co + c]) + t.rrank[eo + x];
+    const int64_t so = 2 * eo + pos;
+    t.krr[so] = t.rr[eo + x];
+    t.kct[so] = t.cts[eo + x];
+    t.ks0[so] = t.S[(eo + x) * 4];
+    t.kid[so] = x;
+  }
+  // the undetermined list (UndeterminedEvents keeps insertion order)
+  int base = 0;
+  for (int x0 = 0; x0 < n_last; x0 += NT) {
+    const int x = x0 + tid;
+    const bool u = x < n_last && t.rcall[eo + x] < 0;
+    int tot;
+    const int inc = block_scan_add(u ? 1 : 0, s_w, tot);
+    if (u) t.U[eo + base + inc - 1] = x;
+    base += tot;
+  }
+  // LastCommitedRoundEvents: RoundEvents(LCR - 1) at the call that set LCR (hashgraph.go:666-673)
+  const int L = gx[GX_LCR], lc = gx[GX_LCRC];
+  int cnt = 0;
+  if (L >= 1) {
+    const int lim = (int)t.calls[d.co + lc];
+    for (int x = tid; x < lim; x += NT) cnt += t.round[eo + x] == L - 1;
+  }
+  int lcre;
+  block_scan_add(cnt, s_w, lcre);
+  if (tid == 0) {
+    int64_t* s = t.scal + (int64_t)g * 8;
+    s[0] = gx[GX_RF];
+    s[1] = L;
+    s[2] = lcre;
+    s[3] = t.gctx[g];
+    s[4] = nord;
+    s[5] = base;
+  }
+}
+
+// One call bucket per workgroup iteration (a work list over the whole batch):
+// ascending bitonic network whose merge stages compare mirrored pairs, so slots
+// past the bucket act as +infinity and need no storage.  Up to BLK keys in LDS;
+// larger buckets on their global scratch.
+__global__ __launch_bounds__(256) void kb_sort(BT t) {
+  __shared__ int32_t lr[BLK], li[BLK];
+  __shared__ int64_t lc[BLK];
+  __shared__ uint64_t ls[BLK];
+  const int tid = threadIdx.x, NT = 256;
+  const int nw = ld(t.wlc);
+  for (int w = blockIdx.x; w < nw; w += gridDim.x) {
+    const int4 gc = t.wl[w];
+    const int g = gc.x, n = gc.y, base = gc.z;
+    const int64_t eo = t.gd[g].eo;
+    const int64_t so = 2 * eo + base;
+    int P = 1;
+    while (P < n) P <<= 1;
+    if (n <= BLK) {
+      for (int k = tid; k < n; k += NT) {
+        lr[k] = t.krr[so + k];
+        li[k] = t.kid[so + k];
+        lc[k] = t.kct[so + k];
+        ls[k] = t.ks0[so + k];
+      }
+      __syncthreads();
+      for (int size = 2; size <= P; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+          for (int q = tid; q < P / 2; q += NT) {
+            int a, b;
+            if (stride == size >> 1) {
+              const int blk = q / stride, i = q - blk * stride;
+              a = blk * size + i;
+              b = blk * size + size - 1 - i;
+            } else {
+              a = 2 * q - (q & (stride - 1));
+              b = a + stride;
+            }
+            if (b >= n) continue;
+            if (key_less(t, eo, lr[b], lc[b], ls[b], li[b], lr[a], lc[a], ls[a], li[a])) {
+              const int r_ = lr[a], i_ = li[a];
+              const int64_t c_ = lc[a];
+              const uint64_t s_ = ls[a];
+              lr[a] = lr[b];
+              li[a] = li[b];
+              lc[a] = lc[b];
+              ls[a] = ls[b];
+              lr[b] = r_;
+              li[b] = i_;
+              lc[b] = c_;
+              ls[b] = s_;
+            }
+          }
+          stage_sync(size, stride);
+        }
+      }
+      __syncthreads();
+      for (int k = tid; k < n; k += NT) t.order[eo + base + k] = li[k];
+    } else {
+      for (int size = 2; size <= P; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+          for (int q = tid; q < P / 2; q += NT) {
+            int a, b;
+            if (stride == size >> 1) {
+              const int blk = q / stride, i = q - blk * stride;
+              a = blk * size + i;
+              b = blk * size + size - 1 - i;
+            } else {
+              a = 2 * q - (q & (stride - 1));
+              b = a + stride;
+            }
+            if (b >= n) continue;
+            const int ra = ld(t.krr + so + a), rb = ld(t.krr + so + b);
+            const int ia = ld(t.kid + so + a), ib = ld(t.kid + so + b);
+            const int64_t ca = ld(t.kct + so + a), cb = ld(t.kct + so + b);
+            const uint64_t sa = ld(t.ks0 + so + a), sb = ld(t.ks0 + so + b);
+            if (key_less(t, eo, rb, cb, sb, ib, ra, ca, sa, ia)) {
+              st(t.krr + so + a, rb);
+              st(t.krr + so + b, ra);
+              st(t.kid + so + a, ib);
+              st(t.kid + so + b, ia);
+              st(t.kct + so + a, cb);
+              st(t.kct + so + b, ca);
+              st(t.ks0 + so + a, sb);
+              st(t.ks0 + so + b, sa);
+            }
+          }
+          __threadfence_block();
+          __syncthreads();
+        }
+      }
+      for (int k = tid; k < n; k += NT) t.order[eo + base + k] = ld(t.kid + so + k);
+    }
+    __syncthreads();  // the LDS keys are the next bucket's
+  }
+}

@@ -126,27 +126,37 @@ struct hge_engine {
   // N > 32 past chain_limit: int32 positions for good (hge_wide32.hip); pending until
   // the next coordinate step converts the packed table
   bool wide32 = false, wide32_pending = false;
+  int w32_done = 0;  // to_wide32's progress: 1 the runs widened, 2 the FD rows, 4 the int32 LA table allocated
+  // test hook (HGE_TEST_W32_FAIL=k): to_wide32 fails once after its stage k (1 the int32
+  // LA table allocated, 2 the runs widened, 3 the FD rows widened)
+  int test_w32_fail = getenv("HGE_TEST_W32_FAIL") ? atoi(getenv("HGE_TEST_W32_FAIL")) : 0;
   int lcr = -1;             // LastConsensusRound (-1 nil)
   int lcre = 0;             // LastCommitedRoundEvents
   int64_t ctx = 0;          // ConsensusTransactions
   std::vector<int32_t> consensus;  // the consensus log (unbounded)
-  // a replay leaves its batch's order in HBM (the results block, s_out): the log's
-  // last cons_dev_n ids are downloaded on first use (consensus_sync), not inside the
-  // replay (40 MB at 256/10M)
-  const int32_t* cons_dev = nullptr;
-  int64_t cons_dev_n = 0;
+  // A replay delivers its order to host memory inside hge_replay_run: one DMA copy from
+  // the results block into a pinned buffer sized at hge_replay_prepare (pin_ord), the
+  // log's last cons_pin_n ids.  Readers take it from there (hge_replay_order: a view,
+  // hge_replay_fetch: one copy); the log's vector gets them on first use
+  // (consensus_sync), outside the replay.
+  int32_t* pin_ord = nullptr;
+  size_t pin_ord_cap = 0;
+  int64_t cons_pin_n = 0;
   bool lazy_order = false;
-  int64_t consensus_size() const { return (int64_t)consensus.size() + cons_dev_n; }
+  int64_t consensus_size() const { return (int64_t)consensus.size() + cons_pin_n; }
   void consensus_sync() {
-    if (!cons_dev_n) return;
-    const size_t old = consensus.size();
-    consensus.resize(old + (size_t)cons_dev_n);
-    // through the pinned arena (a pageable destination made the runtime stage it: 13 ms
-    // for the 40 MB of 256/10M)
-    d2h(consensus.data() + old, cons_dev, 4 * (size_t)cons_dev_n);
-    sync();
-    cons_dev = nullptr;
-    cons_dev_n = 0;
+    if (!cons_pin_n) return;
+    consensus.insert(consensus.end(), pin_ord, pin_ord + cons_pin_n);
+    cons_pin_n = 0;
+  }
+  void ensure_pin_ord(size_t n) {
+    if (n <= pin_ord_cap && pin_ord) return;
+    consensus_sync();
+    if (pin_ord) HIPCHK(hipHostFree(pin_ord));
+    pin_ord = nullptr;
+    pin_ord_cap = 0;
+    HIPCHK(hipHostMalloc((void**)&pin_ord, std::max<size_t>(n, 1) * 4, hipHostMallocDefault));
+    pin_ord_cap = std::max<size_t>(n, 1);
   }
   int64_t n_und = 0;
 
@@ -439,6 +449,10 @@ struct hge_engine {
     if (pin) (void)hipHostFree(pin);
     pin = nullptr;
     pin_cap = pin_used = 0;
+    if (pin_ord) (void)hipHostFree(pin_ord);
+    pin_ord = nullptr;
+    pin_ord_cap = 0;
+    cons_pin_n = 0;
     if (st) (void)hipStreamDestroy(st);
     st = nullptr;
   }
@@ -592,8 +606,7 @@ struct hge_engine {
   void reset_state() {
     sync();
     minw_full = true;
-    cons_dev = nullptr;
-    cons_dev_n = 0;
+    cons_pin_n = 0;
     h_creator.clear();
     h_index.clear();
     h_sp.clear();
@@ -618,6 +631,7 @@ struct hge_engine {
     consensus.clear();
     n_und = 0;
     wide32 = wide32_pending = false;  // a new stream starts on the packed path
+    w32_done = 0;
     chain_limit = chain_limit0;
     reset_rounds();
     HIPCHK(hipMemsetAsync(d_chain.p, 0xFF, (size_t)N * ccap * 4, st));
@@ -672,9 +686,11 @@ struct hge_engine {
         // the int32 LA table must fit beside what is allocated: else refuse
         // the event here (the stream stops, as at any rejection) rather than lift
         // the cap and fail at the next coordinate step
+        // to_wide32's peak: the int32 LA table, plus (uint16 runs and FD rows) one
+        // int32 table being widened while the other's old copy is still held
         size_t free_b = 0, total_b = 0;
-        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
-            free_b < sizeof(int32_t) * (size_t)N * N * (size_t)std::max(ccap, known + 2) + (64u << 20)) {
+        const size_t tab = sizeof(int32_t) * (size_t)N * N * (size_t)std::max(ccap, known + 2);
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b < (fdt16() ? 2 : 1) * tab + (64u << 20)) {
           err = "Chain capacity exceeded: the int32 position tables past 65,534 events per creator do not fit";
           return HGE_ERR_CAPACITY;
         }
@@ -1555,10 +1571,25 @@ struct hge_engine {
   // flag is cleared only once the int32 tables exist: a failed allocation leaves the
   // engine refusing every later step (the packed tables can no longer hold the
   // positions) instead of packing positions past 65,534 into uint16.
+  // A retry after a failed allocation resumes where the last attempt stopped: the int32
+  // LA table comes first (nothing is converted before it exists), and each uint16 table
+  // widened is marked in w32_done, so a retry never reads a widened table as uint16.
   void to_wide32() {
+    auto test_stop = [&](int stage) {  // HGE_TEST_W32_FAIL=stage: one failure after that stage
+      if (test_w32_fail == stage) {
+        test_w32_fail = 0;
+        throw EngineError(HGE_ERR_DEVICE, "test: to_wide32 stopped after stage " + std::to_string(stage));
+      }
+    };
+    if (!(w32_done & 4)) {
+      grow_chain_table(d_LA, ccap, false);
+      w32_done |= 4;
+      test_stop(1);
+    }
     if (fdt16()) {  // the runs and FD rows continue in int32 from here: widen the kept ones
       const size_t n = (size_t)N * N * ccap;
       for (int which = 0; which < 2; which++) {
+        if (w32_done & (1 << which)) continue;
         DBuf<int32_t>& b = which ? d_FD : d_FDT;
         int32_t* q = nullptr;
         HIPCHK(hipMalloc(&q, sizeof(int32_t) * n));
@@ -1568,13 +1599,15 @@ struct hge_engine {
         b.free_();
         b.p = q;
         b.n = n;
+        w32_done |= 1 << which;
+        test_stop(2 + which);
       }
     }
-    grow_chain_table(d_LA, ccap, false);
     s_w32.need(N);
     h2d(s_w32.p, coords_len.data(), 4 * (size_t)N);
     wide32 = true;
     wide32_pending = false;
+    w32_done = 0;
     Tables t = tables();
     int64_t most = 1;
     for (int c = 0; c < N; c++) most = std::max<int64_t>(most, (int64_t)coords_len[c] * N);
@@ -2502,9 +2535,13 @@ struct hge_engine {
         memcpy(&v, htx + 2 * (size_t)b2, 8);
         ntx += v;
       }
-      if (lazy) {
-        cons_dev = o_ids;
-        cons_dev_n = nrecv;
+      if (lazy) {  // delivered into the pinned order buffer (sized at hge_replay_prepare)
+        if ((size_t)nrecv > pin_ord_cap) throw EngineError(HGE_ERR_INTERNAL, "order buffer below the ordered count");
+        const int64_t td = now_ns();
+        if (nrecv) HIPCHK(hipMemcpyAsync(pin_ord, o_ids, 4 * (size_t)nrecv, hipMemcpyDeviceToHost, st));
+        sync();
+        stage_ms[5] = (float)((now_ns() - td) / 1e6);  // the delivery's wall time (hge_stage_times [5])
+        cons_pin_n = nrecv;
       } else {
         consensus.insert(consensus.end(), ids, ids + nrecv);
       }
@@ -3157,6 +3194,8 @@ int hge_replay_prepare(hge_engine* h, const hge_event* ev, int64_t n_sub,
     }
   }
   h->upload();
+  h->cons_pin_n = 0;
+  h->ensure_pin_ord((size_t)h->n_events);  // the replay's order is delivered here
   HIPCHK(hipStreamSynchronize(h->st));
   return HGE_OK;
   GUARD_END(h)
@@ -3175,8 +3214,7 @@ static void replay_begin(hge_engine* h) {
   h->lcre = 0;
   h->ctx = 0;
   h->consensus.clear();
-  h->cons_dev = nullptr;
-  h->cons_dev_n = 0;
+  h->cons_pin_n = 0;
   h->n_und = 0;
   h->ext_on = false;
   h->w_start = std::chrono::steady_clock::now();
@@ -3196,8 +3234,9 @@ static void replay_end(hge_engine* h, int64_t* n_ordered) {
   h->n_und = keep;
   h->und_fresh = keep > 0;
   h->replay_counts.clear();
-  // the consensus log (cleared above) is the replay's order, left in HBM until read
-  h->lazy_order = true;
+  // the consensus log (cleared above) is the replay's order, delivered to the pinned
+  // order buffer in one copy (not staged through the arena into the log's vector)
+  h->lazy_order = h->pin_ord_cap >= (size_t)keep;
   try {
     h->consensus_batch(h->replay_calls, true, true, true, nullptr, &h->replay_counts);
   } catch (...) {
@@ -3215,7 +3254,8 @@ static void replay_end(hge_engine* h, int64_t* n_ordered) {
     return (float)std::chrono::duration<double, std::milli>(y - x).count();
   };
   // [0] coordinates+rounds on the GPU, [1] their wall time, [2] consensus wall time,
-  // [3] consensus on the GPU, [4] replay wall time, [6] GPU total
+  // [3] consensus on the GPU, [4] replay wall time, [5] the order's delivery to host
+  // memory (wall, inside [2]), [6] GPU total
   h->stage_ms[0] = a;
   h->stage_ms[1] = ms(h->w_start, w1);
   h->stage_ms[2] = ms(w1, w2);
@@ -3448,11 +3488,30 @@ int hge_split_finish(hge_engine* h, const int32_t* rows, const uint64_t* ssc, in
 
 int hge_replay_fetch(hge_engine* h, int32_t* order_out, int64_t cap, int64_t* call_counts_out) {
   GUARD_BEGIN
-  h->consensus_sync();
-  for (int64_t i = 0; i < (int64_t)h->consensus.size() && i < cap && order_out; i++)
-    order_out[i] = h->consensus[i];
+  if (order_out) {
+    // the log's vector, then the delivered tail in the pinned buffer: one copy each
+    const int64_t a = std::min<int64_t>((int64_t)h->consensus.size(), std::max<int64_t>(cap, 0));
+    if (a > 0) memcpy(order_out, h->consensus.data(), 4 * (size_t)a);
+    const int64_t b = std::min<int64_t>(h->cons_pin_n, std::max<int64_t>(cap - a, 0));
+    if (b > 0) memcpy(order_out + a, h->pin_ord, 4 * (size_t)b);
+  }
   if (call_counts_out)
     for (size_t c = 0; c < h->replay_counts.size(); c++) call_counts_out[c] = h->replay_counts[c];
+  return HGE_OK;
+  GUARD_END(h)
+}
+
+int hge_replay_order(hge_engine* h, const int32_t** ids, int64_t* n) {
+  if (!h || !ids || !n) return HGE_ERR_ARG;
+  GUARD_BEGIN
+  if (!h->consensus.empty() || !h->cons_pin_n) h->consensus_sync();  // the whole log in one place
+  if (h->cons_pin_n) {
+    *ids = h->pin_ord;
+    *n = h->cons_pin_n;
+  } else {
+    *ids = h->consensus.data();
+    *n = (int64_t)h->consensus.size();
+  }
   return HGE_OK;
   GUARD_END(h)
 }

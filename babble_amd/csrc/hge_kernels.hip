@@ -2425,9 +2425,11 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
     wde[e] = __builtin_amdgcn_readfirstlane(wide);
     if (VPL == 4 && t.WLA16) {
       // lane l takes witnesses d = 4l .. 4l + 3: its thresholds in one 8-byte load
-      // (LA + 1 as uint16), its offsets in one 16-byte load, one fame word
-      const uint2 tw = *(const uint2*)(t.WLA16 + ((size_t)rr * N + cx) * N + 4 * lane);
-      const int4 ow = *(const int4*)(tdr + 4 * lane);
+      // (LA + 1 as uint16), its offsets in one 16-byte load, one fame word.  Lanes past
+      // N / 4 (N < 256) load the last group again and are masked out below (d >= N).
+      const int l4 = min(lane, (N >> 2) - 1);
+      const uint2 tw = *(const uint2*)(t.WLA16 + ((size_t)rr * N + cx) * N + 4 * l4);
+      const int4 ow = *(const int4*)(tdr + 4 * l4);
       const uint64_t f = seg_fws[(size_t)sg * NW + (lane >> 4)];
       const uint32_t u[4] = {tw.x & 0xFFFFu, tw.x >> 16, tw.y & 0xFFFFu, tw.y >> 16};
       const int32_t o4[4] = {ow.x, ow.y, ow.z, ow.w};
@@ -2450,7 +2452,7 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
     if (wde[e]) {
 #pragma unroll
       for (int k = 0; k < VPL; k++) {
-        const int dd = VPL == 4 && t.WLA16 ? 4 * lane + k : min(lane + 64 * k, N - 1);
+        const int dd = VPL == 4 && t.WLA16 ? min(4 * lane + k, N - 1) : min(lane + 64 * k, N - 1);
         const int f = fd_at(t, rw, dd);
         ts[e][k] = f != INF32 ? t.tsch[(size_t)dd * t.ccap + f] : 0;
       }

@@ -66,7 +66,7 @@ EXPORTS = [
     "hge_create", "hge_destroy", "hge_last_error", "hge_reset", "hge_insert_events",
     "hge_divide_rounds", "hge_decide_fame", "hge_decide_round_received", "hge_find_order",
     "hge_run_consensus", "hge_replay", "hge_replay_prepare", "hge_replay_run",
-    "hge_replay_fetch", "hge_event_count", "hge_participants", "hge_rounds",
+    "hge_replay_fetch", "hge_replay_order", "hge_event_count", "hge_participants", "hge_rounds",
     "hge_last_consensus_round", "hge_last_committed_round_events",
     "hge_consensus_transactions", "hge_consensus_count", "hge_consensus_events",
     "hge_undetermined", "hge_known", "hge_round_of", "hge_is_witness", "hge_round_witness",
@@ -91,6 +91,7 @@ EXPORTS = [
     # a batch of independent hashgraphs (config 5, hge_batch.hip)
     "hge_batch_create", "hge_batch_destroy", "hge_batch_last_error", "hge_batch_add", "hge_batch_stage",
     "hge_batch_run", "hge_batch_graphs", "hge_batch_info", "hge_batch_results", "hge_batch_kernel_ms",
+    "hge_batch_fallbacks",
     # the wire / hashing format (host only, hge_gob.cpp)
     "hge_gob_encode_wire_events", "hge_gob_decode_wire_events", "hge_gob_encode_event_body",
 ]
@@ -140,6 +141,7 @@ def lib():
     L.hge_replay_prepare.argtypes = [vp, ctypes.c_void_p, i64, P(i64), i64, P(i32)]
     L.hge_replay_run.argtypes = [vp, P(i64)]
     L.hge_replay_fetch.argtypes = [vp, P(i32), i64, P(i64)]
+    L.hge_replay_order.argtypes = [vp, P(P(i32)), P(i64)]
     for f in ("hge_event_count", "hge_consensus_transactions", "hge_consensus_count"):
         getattr(L, f).argtypes = [vp]
         getattr(L, f).restype = i64
@@ -236,6 +238,8 @@ def lib():
     L.hge_batch_results.argtypes = [vp, i32, P(i32), P(i64), P(i32), P(ctypes.c_uint8), P(i32), P(i64),
                                     P(ctypes.c_int8), P(i32)]
     L.hge_batch_kernel_ms.argtypes = [vp, P(ctypes.c_float), i32]
+    L.hge_batch_fallbacks.argtypes = [vp]
+    L.hge_batch_fallbacks.restype = ctypes.c_int64
     _lib = L
     return L
 
@@ -545,6 +549,16 @@ class Engine:
         self._check(self.L.hge_replay_run(self.h, ctypes.byref(n)))
         self._nordered = n.value
         return n.value
+
+    def order_view(self):
+        """The replay's order where hge_replay_run delivered it (pinned host memory), as a
+        numpy view without a copy: valid until the next replay or consensus call."""
+        p = ctypes.POINTER(ctypes.c_int32)()
+        n = ctypes.c_int64()
+        self._check(self.L.hge_replay_order(self.h, ctypes.byref(p), ctypes.byref(n)))
+        if n.value == 0:
+            return np.zeros(0, np.int32)
+        return np.ctypeslib.as_array(p, shape=(n.value,))
 
     def fetch(self):
         order = np.zeros(max(1, self._nordered), np.int32)
@@ -939,7 +953,11 @@ class Batch:
         keys = ("events", "calls", "rounds", "lcr", "lcre", "transactions", "ordered", "undetermined")
         return dict(zip(keys, a.tolist()))
 
-    KERNELS = ("kb_coords", "kb_fd", "kb_fdrows", "kb_front", "kb_consensus")
+    KERNELS = ("kb_coords", "kb_fd", "kb_fdrows", "kb_front", "kb_fame", "kb_fold", "kb_receive", "kb_order")
+
+    def fallbacks(self):
+        """Graphs the last run replayed call by call (kb_consensus) instead of in bulk."""
+        return int(self.L.hge_batch_fallbacks(self.h))
 
     def kernel_ms(self):
         """Device ms of the last run's stages (HIP events between the launches)."""

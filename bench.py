@@ -280,9 +280,10 @@ def small_replay(n, E, K, seed, device, steps=20):
                        else "MISMATCH vs CPU oracle")}
 
 
-def mc_kernel_bytes(kernel, n, events, ordered, rounds):
+def mc_kernel_bytes(kernel, n, events, ordered, rounds, calls=0):
     """Algorithmic bytes of one batch-engine stage over the whole batch:
-    `events` accepted events, `ordered` ordered ones, `rounds` summed over the graphs."""
+    `events` accepted events, `ordered` ordered ones, `rounds` and `calls` summed over
+    the graphs."""
     per_event = {
         "kb_coords": 4 * n + 16,  # the LA row written, the parents' creator / index / ids read
         "kb_fd": 8 * n,           # the LA row read, its firstDescendant runs written
@@ -294,7 +295,13 @@ def mc_kernel_bytes(kernel, n, events, ordered, rounds):
         # per round: N member rows and, per member, the N rows FD[(i, FD[w][i])]
         # (4N bytes each); per event its chain slot read and round / witness written
         return rounds * (4 * n * n + 4 * n * n * n) + 9 * events
-    return (4 * n + 48) * ordered  # kb_consensus: the median's rows and the sort key
+    if kernel == "kb_fame":  # per (call, s) pair: two rounds' witness ids, vote bits and coins read, 16 B out
+        return calls * 3 * (2 * 13 * n + 16)
+    if kernel == "kb_fold":  # the pairs' decisions read, the arrivals; per round its thresholds
+        return calls * 3 * 16 + rounds * 8 * n
+    if kernel == "kb_receive":  # per event its round / creator / index / call read; per ordered one the FD row
+        return 16 * events + (4 * n + 16) * ordered
+    return (4 * n + 48) * ordered  # kb_order (kb_consensus): the median's rows and the sort key
 
 
 def mc_main(args, n, E, K, rank, world, local_rank, dist):
@@ -352,6 +359,7 @@ def mc_line(args, n, E, K, rank, world, local_rank, dist, cpu_s=10.0):
         max_step, tot_ordered = reduce_step(dist, step_s, ordered, f"cuda:{local_rank}")
 
     rounds_tot = sum(batch.info(g)["rounds"] for g in range(per))
+    calls_tot = sum(batch.info(g)["calls"] for g in range(per))
     # every graph of this rank against the oracle's full-state digest
     checks = []
     dg = mc_digests(n, E, K, args.seed)
@@ -397,7 +405,7 @@ def mc_line(args, n, E, K, rank, world, local_rank, dist, cpu_s=10.0):
         return None
     value = tot_ordered / max_step
     dom = max(kms, key=kms.get)
-    kb = {k_: mc_kernel_bytes(k_, n, events, ordered, rounds_tot) for k_ in kms}
+    kb = {k_: mc_kernel_bytes(k_, n, events, ordered, rounds_tot, calls_tot) for k_ in kms}
     alg = kb[dom]
     achieved = alg / (kms[dom] * 1e-3) / 1e9
     hbm = {k_: {"ms": round(v_, 4), "alg_bytes": kb[k_], "achieved_gbs": round(kb[k_] / (v_ * 1e-3) / 1e9, 2)}
@@ -433,7 +441,9 @@ def mc_line(args, n, E, K, rank, world, local_rank, dist, cpu_s=10.0):
         "ingest_host_ms": round(ingest_s * 1e3, 2),
         "admission_ms": round(admission_s * 1e3, 2),
         "kernels_ms_per_replay": {k_: round(v_, 4) for k_, v_ in sorted(kms.items(), key=lambda kv: -kv[1])},
-        "kernel_launches_per_replay": {k_: 1 for k_ in kms},
+        "kernel_launches_per_replay": {"kb_coords": 1, "kb_fd": 1, "kb_fdrows": 1, "kb_front": 1, "kb_fame": 2,
+                                       "kb_fold": 2, "kb_receive": 1, "kb_order": 2},
+        "graphs_replayed_call_by_call": batch.fallbacks(),
     }
     batch.close()
     return line
@@ -547,12 +557,15 @@ def main():
         eng0.run()
     st_ms = eng0.stage_times()
     replay_ms = {"coords_gpu": st_ms[0], "coords_wall": st_ms[1], "consensus_gpu": st_ms[3],
-                 "consensus_wall": st_ms[2], "gpu": st_ms[6], "wall": st_ms[4]}
+                 "consensus_wall": st_ms[2], "gpu": st_ms[6], "wall": st_ms[4],
+                 "order_delivery_wall": st_ms[5]}
     replay_ms = {k: round(v, 4) for k, v in replay_ms.items()}
-    # the replay leaves the order in HBM; its download (PCIe) is timed apart, outside the step
+    # the step ends with the order in host memory (one DMA copy into the pinned buffer
+    # sized at hge_replay_prepare, replay_ms.order_delivery_wall); copying it out into a
+    # caller's array is timed apart
     t_f = time.perf_counter()
     gstatus, gorder, gcounts = eng0.fetch()
-    order_download_ms = (time.perf_counter() - t_f) * 1e3
+    order_fetch_ms = (time.perf_counter() - t_f) * 1e3
 
     # ---- profiled pass: per-kernel device time (HIP events on the engine stream) ----
     nprof = max(1, args.profile_steps)
@@ -730,7 +743,7 @@ def main():
             "ingest_host_ms": round(ingest_s * 1e3, 2),
             "admission_ms": None if admission_s is None else round(admission_s * 1e3, 2),
             "replay_ms": replay_ms,
-            "order_download_ms": round(order_download_ms, 3),
+            "order_fetch_copy_ms": round(order_fetch_ms, 3),
             "coordinate_sweeps": sweeps,
             "rounds": eng0.rounds(),
             "kernels_ms_per_replay": {k: round(v[0] / nprof, 4) for k, v in

@@ -157,12 +157,20 @@ int hge_replay_prepare(hge_engine* h, const hge_event* ev, int64_t n_sub,
                        const int64_t* call_points, int64_t n_calls, int32_t* status_out);
 int hge_replay_run(hge_engine* h, int64_t* n_ordered);
 int hge_replay_fetch(hge_engine* h, int32_t* order_out, int64_t cap, int64_t* call_counts_out);
+/* The consensus log without a copy: hge_replay_run delivers a replay's order into a
+ * pinned host buffer sized at hge_replay_prepare (the batches FindOrder hands its
+ * caller, hashgraph.go:744-757, all of them); *ids points at it (or at the log when
+ * online calls followed) and stays valid until the next replay, consensus call or
+ * hge_destroy. */
+int hge_replay_order(hge_engine* h, const int32_t** ids, int64_t* n);
 
 /* ---- a batch of independent hashgraphs (BASELINE config 5, Monte Carlo) -------- */
 /* Many small hashgraphs (N <= 64 participants each) replayed together: every stage
- * is one launch over the whole batch (one wavefront per graph) and each graph's
- * whole call schedule runs on the device, so a batch costs a handful of launches
- * however many graphs it holds (hge_batch.hip).  Per graph the semantics are
+ * is one launch over the whole batch and each graph's whole call schedule runs on
+ * the device in bulk (the calls' DecideFame pairs, one fold over the calls, the
+ * events' round received and medians, the call buckets' sorts), so a batch costs a
+ * handful of launches however many graphs it holds (hge_batch.hip,
+ * hge_batch_bulk.hip).  Per graph the semantics are
  * hge_replay's: parents are submission indices, admission (FromParentsLatest,
  * hashgraph.go:366-396, and the index rule of HGE_ERR_INDEX) happens in
  * hge_batch_add on the host, RunConsensus runs after every call point, and the
@@ -188,8 +196,13 @@ int hge_batch_info(hge_batch* b, int32_t g, int64_t* info);
 int hge_batch_results(hge_batch* b, int32_t g, int32_t* order, int64_t* counts, int32_t* round, uint8_t* witness,
                       int32_t* rr, int64_t* cts, int8_t* fame, int32_t* undetermined);
 /* device ms of the last run's stages (HIP events between the launches): coordinates,
- * firstDescendant runs, firstDescendant rows, rounds, consensus; returns the count */
+ * firstDescendant runs, firstDescendant rows, rounds, DecideFame pairs, the call
+ * fold and receive thresholds, round received and medians, the call buckets' order;
+ * returns the count */
 int hge_batch_kernel_ms(hge_batch* b, float* ms, int32_t cap);
+/* graphs the last run replayed call by call (kb_consensus) because the bulk fold
+ * could not hold them (more than 256 rounds, or a receive-interval table overflow) */
+int64_t hge_batch_fallbacks(hge_batch* b);
 
 /* ---- one hashgraph split across GPUs (babble_amd/dist.py) ------ */
 /* Sharded replay.  Every rank stages the whole stream (hge_replay_prepare) and

@@ -8,7 +8,9 @@ The graphs cover N from 1 to 64, forkers and fork cascades (every admission
 error), call schedules from K = 1 to one call for the whole stream (a batch
 past the LDS sort, the global-scratch path), other-parents that are not their
 chain's head (op_lag), coin rounds (N = 4 one-shot), and a second run of the
-same batch."""
+same batch.  The call schedule runs in bulk (hge_batch_bulk.hip); a graph past
+the bulk fold's 256 rounds is replayed call by call by kb_consensus in the same
+run, and HGB_SERIAL=1 puts every graph through kb_consensus."""
 import os
 import sys
 
@@ -27,6 +29,7 @@ CASES = [
     (4, 1000, 1, 2, 0, 0.0, 0.0, 0),
     (4, 1500, 1500, 12, 0, 0.0, 0.0, 0),     # one call: coin rounds, a 1.4k-key batch (global sort)
     (1, 50, 5, 3, 0, 0.0, 0.0, 0),
+    (1, 700, 5, 5, 0, 0.0, 0.0, 0),          # ~700 rounds: past the bulk fold, replayed by kb_consensus
     (2, 300, 2, 3, 0, 0.0, 0.0, 0),
     (5, 2000, 3, 13, 0, 0.0, 0.0, 0),
     (7, 3000, 7, 14, 2, 0.1, 0.5, 0),
@@ -86,7 +89,9 @@ def test_batch_many_graphs_one_launch_per_stage():
             b.add(dag, calls)
         b.run()
         ms = b.kernel_ms()
-        assert set(ms) == {"kb_coords", "kb_fd", "kb_fdrows", "kb_front", "kb_consensus"}
+        assert set(ms) == {"kb_coords", "kb_fd", "kb_fdrows", "kb_front", "kb_fame", "kb_fold", "kb_receive",
+                           "kb_order"}
+        assert b.fallbacks() == 0  # every graph in bulk
         for g in range(0, 256, 5):
             w = oracle_state(*streams[g])
             assert first_difference(b.state(g), w) is None, f"graph {g}"
@@ -105,5 +110,48 @@ def test_batch_refuses_bad_arguments():
             b.add(dag, np.array([5, 3], np.int64))  # not ascending
         with pytest.raises(HgeError):
             b.info(0)  # no graph yet
+    finally:
+        b.close()
+
+
+@pytest.mark.parametrize("n", [4, 32, 64])
+def test_batch_serial_path_matches_oracle(n, monkeypatch):
+    """HGB_SERIAL=1: every graph through the call-by-call kb_consensus (the bulk
+    path's fallback), against the oracle."""
+    from babble_amd.engine import Batch
+    from digest import first_difference
+    from make_mc_digests import oracle_state
+    monkeypatch.setenv("HGB_SERIAL", "1")
+    cases = [c for c in CASES if c[0] == n]
+    streams = [_stream(*c) for c in cases]
+    b = Batch(n)
+    try:
+        for dag, calls in streams:
+            b.add(dag, calls)
+        b.run()
+        assert b.fallbacks() == len(cases)
+        for g, (case, (dag, calls)) in enumerate(zip(cases, streams)):
+            diff = first_difference(b.state(g), oracle_state(dag, calls))
+            assert diff is None, f"case {case}: first differing field {diff}"
+    finally:
+        b.close()
+
+
+def test_batch_fallback_mixed_with_bulk():
+    """One batch holding a graph past the bulk fold (N = 1, ~700 rounds) and bulk
+    graphs: only that graph is replayed by kb_consensus, all equal the oracle."""
+    from babble_amd.engine import Batch
+    from digest import first_difference
+    from make_mc_digests import oracle_state
+    cases = [c for c in CASES if c[0] == 1]
+    streams = [_stream(*c) for c in cases]
+    b = Batch(1)
+    try:
+        for dag, calls in streams:
+            b.add(dag, calls)
+        b.run()
+        assert b.fallbacks() == 1
+        for g, (case, (dag, calls)) in enumerate(zip(cases, streams)):
+            assert first_difference(b.state(g), oracle_state(dag, calls)) is None, f"case {case}"
     finally:
         b.close()

@@ -57,7 +57,11 @@ def test_random_gossip(engines, n, events, k):
     run_case(engines(n), dag, k)
 
 
-@pytest.mark.parametrize("n,events,k", [(32, 4000, 32), (64, 4000, 64)])
+@pytest.mark.parametrize("n,events,k", [(32, 4000, 32), (64, 4000, 64),
+                                         # N = 192: DecideFame's per-round widening (N % 64 == 0, N >= 192)
+                                         # and uint16 FD rows; N = 200 / 224: the median's 4-witness
+                                         # lanes past N / 4 (N < 256) and uint16 FD rows
+                                         (192, 24000, 192), (200, 16000, 200), (224, 16000, 224)])
 def test_random_gossip_wide(engines, n, events, k):
     dag = random_gossip(n, events, seed=5 + n)
     run_case(engines(n), dag, k, check_events=False)
@@ -90,7 +94,8 @@ def test_online_matches_replay(engines):
     eng.close()
 
 
-@pytest.mark.parametrize("n,E,k", [(16, 6000, 16), (16, 3000, 3), (32, 6000, 32), (12, 2000, 1), (48, 5000, 48), (64, 6000, 64), (128, 6000, 128)])
+@pytest.mark.parametrize("n,E,k", [(16, 6000, 16), (16, 3000, 3), (32, 6000, 32), (12, 2000, 1), (48, 5000, 48),
+                                   (64, 6000, 64), (128, 6000, 128), (192, 16000, 192), (224, 12000, 224)])
 def test_online_matches_oracle_single_block_paths(engines, n, E, k):
     """Online calls take the single-block stages (k_fame_call; k_order_call at
     N <= 16; the frontier start in k_la_seq, the rounds assignment in the walk): the

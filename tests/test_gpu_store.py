@@ -205,6 +205,50 @@ def test_chain_past_uint16_switches_mid_stream_online(monkeypatch, n, events, li
         ref.close()
 
 
+@pytest.mark.parametrize("stage", [1, 2, 3])
+def test_chain_switch_resumes_after_a_failed_widening(monkeypatch, stage):
+    """The switch to int32 positions at N = 256 widens the uint16 runs and FD rows one
+    table at a time.  A failure part-way (HGE_TEST_W32_FAIL: once, after the int32 LA
+    table is allocated, after the runs are widened, or after the FD rows are) fails
+    that RunConsensus; the retry resumes from the tables not yet widened (never reading
+    a widened one as uint16) and the stream ends equal to an engine that never
+    switched."""
+    from babble_amd.engine import Engine, HgeError, events_array
+    from babble_amd.gossip import schedule
+    n, events = 256, 16000
+    dag = random_gossip(n, events, seed=91)
+    ev = events_array(dag)
+    calls = schedule(events, n)
+    ref = Engine(n, events + 64)
+    monkeypatch.setenv("HGE_CHAIN_LIMIT", "50")
+    monkeypatch.setenv("HGE_TEST_W32_FAIL", str(stage))
+    eng = Engine(n, events + 64)
+    try:
+        _, order, counts = ref.replay(ev, calls)
+        nxt, per, failed = 0, [], 0
+        for c in calls:
+            eng.insert_events(ev[nxt:c].copy())
+            try:
+                got = eng.run_consensus()
+            except HgeError as e:
+                assert "to_wide32 stopped" in str(e)
+                failed += 1
+                got = eng.run_consensus()
+            per.append(len(got))
+            nxt = c
+        assert failed == 1
+        np.testing.assert_array_equal(eng.consensus_events(), order)
+        np.testing.assert_array_equal(np.asarray(per), counts)
+        for x, y in zip(eng.event_received(), ref.event_received()):
+            np.testing.assert_array_equal(x, y)
+        for i in (0, events // 2, events - 1):
+            for x, y in zip(eng.coordinates(i), ref.coordinates(i)):
+                np.testing.assert_array_equal(x, y)
+    finally:
+        eng.close()
+        ref.close()
+
+
 def test_replay_rejects_bad_call_points():
     from babble_amd.engine import Engine, HgeError, events_array
     dag = random_gossip(4, 200, seed=2)
