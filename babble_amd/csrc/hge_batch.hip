@@ -109,8 +109,12 @@ struct BT {
   int32_t *nivl, *fsuf;  // [ro + r] intervals per round; the suffix minimum of their first starts
   int32_t *thp, *thR;    // [g * BICAP + s][N] receive thresholds; [g * BICAP + s] their round
   uint64_t* thF;         // [g * BICAP + s] their famous witnesses
-  int32_t* rcall;        // [eo + x] the call that receives x (-1 none)
-  int32_t* rrank;        // [eo + x] x's slot in that call's bucket (before the sort)
+  // chain layout [g][c][p] (kb_receive's lanes are consecutive positions of a chain)
+  int32_t* roundch;      // rounds
+  int32_t *rcall, *rrank;  // the call that receives the event (-1 none), its slot in that call's bucket
+  int32_t* rrch;         // round received
+  int32_t* rslot;        // the receiving interval's threshold slot (-1 none)
+  int64_t* ctsch;        // consensus timestamps
   int32_t *bcnt, *boff;  // [co + c] call buckets: size, offset
   int4* wl;              // the non-empty buckets (graph, size, offset in the graph's order)
   int32_t* wlc;          // their count
@@ -264,30 +268,47 @@ __global__ __launch_bounds__(256) void kb_coords(BT t) {
 // firstDescendants in run layout (UpdateAncestorFirstDescendant, hashgraph.go:466-494):
 // chain-j event k is the first chain-j descendant of the chain-c positions
 // (LA[(j,k-1)][c], LA[(j,k)][c]]; positions no chain-j event sees keep INF
-// (MaxInt64).  Lane r holds row k0 + r of chain j (all N columns, registers); for
-// each column c the 64 rows' runs tile one contiguous range of chain c's positions,
-// so the stores of a column are contiguous across the lanes.  The next 64 rows'
-// loads are in flight meanwhile.
+// (MaxInt64).  One wave per (graph, chain j, slice of FCW columns): lane r holds row
+// k0 + r of chain j (the slice's columns, registers); for each column c the 64 rows'
+// runs tile one contiguous range of chain c's positions, so the stores of a column
+// are contiguous across the lanes.  The next 64 rows' loads are in flight meanwhile.
+// (Slices of 16 columns: a wave holding all 32 columns took 176 VGPRs, two waves per SIMD.)
+constexpr int FCW = 16;
 template <int NM>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void kb_fd(BT t) {
-  const int g = blockIdx.x / t.N, j = blockIdx.x - (blockIdx.x / t.N) * t.N;  // one wave per (graph, chain j)
-  const GDesc d = t.gd[g];
+__global__ __launch_bounds__(64) void kb_fd(BT t) {
+  constexpr int NS_ = NM / FCW;
   const int N = t.N, cc = t.ccap, lane = threadIdx.x;
+  const int w = blockIdx.x, g = w / (N * NS_), j = (w / NS_) % N, c0 = (w % NS_) * FCW;
+  if (c0 >= N) return;
+  const GDesc d = t.gd[g];
   const int32_t* LA = t.LA + d.eo * N;
   const int lenc = lane < N ? t.clen[g * N + lane] : 0;  // lane c's chain length (the INF tails)
   {
     const int lenj = t.clen[g * N + j];
     const int32_t* ch = t.chain + ((int64_t)g * N + j) * cc;
     int32_t* outj = t.FDT + ((int64_t)g * N + j) * N * cc;  // + c * cc + p
-    int row[NM], nrow[NM];
-    int carry[NM];  // the last row's value of column c before the chunk (uniform)
+    const bool vec = (N & 3) == 0 && c0 + FCW <= N;  // 16-byte aligned slices
+    int row[FCW], nrow[FCW];
+    int carry[FCW];  // the last row's value of column c0 + c before the chunk (uniform)
 #pragma unroll
-    for (int c = 0; c < NM; c++) carry[c] = -1;
-    auto load = [&](int k0, int (&v)[NM]) {
+    for (int c = 0; c < FCW; c++) carry[c] = -1;
+    auto load = [&](int k0, int (&v)[FCW]) {
       const bool ok = k0 + lane < lenj;
       const int x = ok ? ch[k0 + lane] : 0;
+      const int32_t* r = LA + (int64_t)x * N + c0;
+      if (vec) {
 #pragma unroll
-      for (int c = 0; c < NM; c++) v[c] = ok && c < N ? LA[(int64_t)x * N + c] : -1;
+        for (int c = 0; c < FCW; c += 4) {
+          const int4 q = ok ? *(const int4*)(r + c) : make_int4(-1, -1, -1, -1);
+          v[c] = q.x;
+          v[c + 1] = q.y;
+          v[c + 2] = q.z;
+          v[c + 3] = q.w;
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < FCW; c++) v[c] = ok && c0 + c < N ? r[c] : -1;
+      }
     };
     if (lenj > 0) load(0, row);
     for (int k0 = 0; k0 < lenj; k0 += 64) {
@@ -296,27 +317,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
       const bool ok = k0 + lane < lenj;
       const int last = min(64, lenj - k0) - 1;  // the chunk's last valid lane
 #pragma unroll
-      for (int c = 0; c < NM; c++) {
-        if (c < N) {
+      for (int c = 0; c < FCW; c++) {
+        if (c0 + c < N) {
           const int up = __shfl_up(row[c], 1);
           const int a = lane == 0 ? carry[c] : up;  // positions (a, b] take k0 + lane
           const int b = ok ? row[c] : a;
-          int32_t* out = outj + (int64_t)c * cc;
+          int32_t* out = outj + (int64_t)(c0 + c) * cc;
           for (int p = a + 1; p <= b; p++) out[p] = k0 + lane;
           carry[c] = rl(row[c], last);
         }
       }
       if (more) {
 #pragma unroll
-        for (int c = 0; c < NM; c++) row[c] = nrow[c];
+        for (int c = 0; c < FCW; c++) row[c] = nrow[c];
       }
     }
     // chain c's positions no chain-j event sees: one coalesced sweep per column
 #pragma unroll
-    for (int c = 0; c < NM; c++) {
-      if (c < N) {
-        const int lc = rl(lenc, c);
-        int32_t* out = outj + (int64_t)c * cc;
+    for (int c = 0; c < FCW; c++) {
+      if (c0 + c < N) {
+        const int lc = rl(lenc, c0 + c);
+        int32_t* out = outj + (int64_t)(c0 + c) * cc;
         for (int p = carry[c] + 1 + lane; p < lc; p += 64) out[p] = INF;
       }
     }
@@ -390,9 +411,11 @@ __device__ __forceinline__ int kth_smallest(int (&v)[M], int k) {
   return r;
 }
 
-template <int NM>
-__global__ __launch_bounds__(1024) void kb_front(BT t) {
-  constexpr int NT = 1024, NW = NT / 64;
+// NT: 1024 threads while the graphs fit one workgroup per CU; 512 past that, so two
+// graphs share a CU (the kernel's ~88 VGPRs hold one 1024-thread workgroup per CU)
+template <int NM, int NT>
+__global__ __launch_bounds__(NT) void kb_front(BT t) {
+  constexpr int NW = NT / 64;
   const int g = blockIdx.x;
   const GDesc d = t.gd[g];
   const int N = t.N, SM = t.SM, cc = t.ccap, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -426,6 +449,7 @@ __global__ __launch_bounds__(1024) void kb_front(BT t) {
         for (int p = lo + k; p < hi; p += per) {
           const int x = chg[(int64_t)c * cc + p];
           t.round[d.eo + x] = r;
+          t.roundch[(int64_t)g * N * cc + (int64_t)c * cc + p] = r;
           t.wit[d.eo + x] = p == lo;
           if (p == lo) {
             t.W[row + c] = x;
@@ -1297,11 +1321,11 @@ struct hge_batch {
   bool dbg_on = getenv("HGB_STAMPS") != nullptr;
   // the bulk call schedule; HGB_SERIAL=1 (test hook): every graph through kb_consensus
   bool serial = getenv("HGB_SERIAL") != nullptr;
-  Buf<int32_t> d_glist, d_cg, d_Rc, d_rfirst, d_rrank, d_xcall, d_gx, d_nivl, d_fsuf, d_thp, d_thR, d_rcall, d_bcnt, d_boff, d_wlc;
+  Buf<int32_t> d_roundch, d_rrch, d_rslot, d_glist, d_cg, d_Rc, d_rfirst, d_rrank, d_xcall, d_gx, d_nivl, d_fsuf, d_thp, d_thR, d_rcall, d_bcnt, d_boff, d_wlc;
   Buf<uint64_t> d_arr, d_Dp, d_ivF, d_thF;
   Buf<int4> d_ivh;
   Buf<int4> d_wl;
-  Buf<int64_t> d_gctx;
+  Buf<int64_t> d_gctx, d_ctsch;
   int Emax = 0;
   int64_t n_fallback = 0;  // graphs the last run replayed through kb_consensus
 
@@ -1314,13 +1338,14 @@ struct hge_batch {
     for (auto* b : {&d_ts, &d_tsch, &d_calls, &d_cts, &d_counts, &d_scal, &d_kct}) b->free_();
     for (auto* b : {&d_S, &d_ssb, &d_seeb, &d_ks0, &d_Sch}) b->free_();
     d_ntxch.free_();
-    for (auto* b : {&d_glist, &d_cg, &d_Rc, &d_rfirst, &d_rrank, &d_xcall, &d_gx, &d_nivl, &d_fsuf, &d_thp, &d_thR, &d_rcall, &d_bcnt,
+    for (auto* b : {&d_roundch, &d_rrch, &d_rslot, &d_glist, &d_cg, &d_Rc, &d_rfirst, &d_rrank, &d_xcall, &d_gx, &d_nivl, &d_fsuf, &d_thp, &d_thR, &d_rcall, &d_bcnt,
                     &d_boff, &d_wlc})
       b->free_();
     for (auto* b : {&d_arr, &d_Dp, &d_ivF, &d_thF}) b->free_();
     d_ivh.free_();
     d_wl.free_();
     d_gctx.free_();
+    d_ctsch.free_();
     d_coin.free_();
     d_wit.free_();
     d_WCOIN.free_();
@@ -1516,8 +1541,13 @@ struct hge_batch {
     d_thp.need((size_t)G * BICAP * N);
     d_thR.need((size_t)G * BICAP);
     d_thF.need((size_t)G * BICAP);
-    d_rcall.need(E1);
-    d_rrank.need(E1);
+    const size_t CH = (size_t)G * N * ccap;
+    d_roundch.need(CH);
+    d_rcall.need(CH);
+    d_rrank.need(CH);
+    d_rrch.need(CH);
+    d_rslot.need(CH);
+    d_ctsch.need(CH);
     d_bcnt.need(K1);
     d_boff.need(K1);
     d_wl.need(K1);
@@ -1592,8 +1622,12 @@ struct hge_batch {
     t.thp = d_thp.p;
     t.thR = d_thR.p;
     t.thF = d_thF.p;
+    t.roundch = d_roundch.p;
     t.rcall = d_rcall.p;
     t.rrank = d_rrank.p;
+    t.rrch = d_rrch.p;
+    t.rslot = d_rslot.p;
+    t.ctsch = d_ctsch.p;
     t.bcnt = d_bcnt.p;
     t.boff = d_boff.p;
     t.wl = d_wl.p;
@@ -1613,11 +1647,12 @@ struct hge_batch {
   void run_stages(int G, const BT& t) {
     launch(kb_coords<NM>, G, t, 256);
     BCHK(hipEventRecord(ev[1], st));
-    launch(kb_fd<NM>, G * N, t);
+    launch(kb_fd<NM>, G * N * (NM / FCW), t);
     BCHK(hipEventRecord(ev[2], st));
     launch(kb_fdrows<NM>, G * N, t, 256);
     BCHK(hipEventRecord(ev[3], st));
-    launch(kb_front<NM>, G, t, 1024);
+    if (G > ncu) launch(kb_front<NM, 512>, G, t, 512);
+    else launch(kb_front<NM, 1024>, G, t, 1024);
     BCHK(hipEventRecord(ev[4], st));
     if (serial) {  // every graph through kb_consensus, after the run's readback
       for (int k = 5; k < 9; k++) BCHK(hipEventRecord(ev[k], st));
@@ -1631,7 +1666,9 @@ struct hge_batch {
     launch(kb_theta<NM>, G, t, 256);
     BCHK(hipEventRecord(ev[6], st));
     if (Emax > 0) {
-      hipLaunchKernelGGL(kb_receive<NM>, dim3((unsigned)(N * ((ccap + 255) / 256)), (unsigned)G), dim3(256), 0, st, t);
+      hipLaunchKernelGGL(kb_receive<NM>, dim3((unsigned)N, (unsigned)G), dim3(256), 0, st, t);
+      BCHK(hipGetLastError());
+      hipLaunchKernelGGL(kb_median<NM>, dim3((unsigned)(N * ((ccap + 255) / 256)), (unsigned)G), dim3(256), 0, st, t);
       BCHK(hipGetLastError());
     }
     BCHK(hipEventRecord(ev[7], st));

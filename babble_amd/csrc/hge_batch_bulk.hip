@@ -137,89 +137,73 @@ __global__ __launch_bounds__(1024) void kb_prep(BT t) {
 }
 
 // DecideFame for round i at a call that holds n_c events and R rounds
-// (hashgraph.go:598-664), one wave: lane y is a voter of round j (two half waves,
-// each its own witness x, at NM <= 32), the witnesses x of round i in chunks of
-// 16 per lane group.  For one x and one j every present y's yays / nays come from
-// popcounts at once; the y loop's `break` is the first y whose tally reaches SM
-// (a ballot's lowest bit): x's votes from round j are the v of the y before it and
-// its fame the v of that y; the last deciding j wins.  Coin rounds (diff % N == 0)
-// vote the middle bit where no supermajority; missing votes are nays.  dec: the
-// present witnesses decided at this call, val: their values (1 = famous).
-// src: the witness rows of rounds j >= i -- W(j, y) (id, -1 none), see(j, y) / ss(j, y)
-// (bits over round j-1's creators), coin(j, y).
+// (hashgraph.go:598-664), lane = witness x of round i; at NM <= 32 the two half
+// waves decide two calls at once (n_c, R: the lane's half's call; i is shared).
+// Per voting round j: x's votes of round j-1 are a bit mask `prev` over its
+// witnesses; the voters y of round j go in ascending creator order (the canonical
+// witness order), each with yays = |ss(y) & prev|, nays = |ss(y)| - yays (missing
+// votes are nays).  At diff = 1 a vote is See(y, x); in a normal round the first y
+// whose tally reaches SM decides x (SetFame, `break`: no later y votes); in a coin
+// round (diff % N == 0) y votes v on a supermajority, else its middle bit.  The last
+// deciding j wins.  dec: the present witnesses decided at this call, val: their
+// values (1 = famous), for the lane's half.
 template <int NM, typename Src>
 __device__ void fame_pair(const BT& t, const Src& src, int i, int n_c, int R, uint64_t& dec_out,
                           uint64_t& val_out) {
-  constexpr int HV = NM <= 32 ? 2 : 1, KX = 16, XPC = HV * KX;
+  constexpr int HV = NM <= 32 ? 2 : 1;
   const int lane = threadIdx.x & 63, N = t.N, SM = t.SM;
-  const int h = HV == 2 ? lane >> 5 : 0, y = HV == 2 ? (lane & 31) : lane;
-  auto half = [&](uint64_t m) -> uint64_t { return HV == 2 ? (m >> (32 * h)) & 0xFFFFFFFFull : m; };
-  const int wi = lane < N ? src.W(i, lane) : -1;
-  const uint64_t pm = ballot(lane < N && wi >= 0 && wi < n_c);
-  uint64_t dec = 0, val = 0;
-  for (int xc = 0; xc < N; xc += XPC) {
-    int fv[KX];
-    uint64_t prev[KX];
-#pragma unroll
-    for (int k = 0; k < KX; k++) {
-      fv[k] = 0;
-      prev[k] = 0;
-    }
-    for (int j = i + 1; j < R; j++) {
-      const int diff = j - i;
-      const int yid = y < N ? src.W(j, y) : -1;
-      const bool py = yid >= 0 && yid < n_c;
-      uint64_t yb = 0;
-      bool ycoin = false;
-      if (py) {
-        yb = diff == 1 ? src.see(j, y) : src.ss(j, y);
-        ycoin = src.coin(j, y);
+  const int x = HV == 2 ? (lane & 31) : lane, h = HV == 2 ? lane >> 5 : 0;
+  const int Rw = HV == 2 ? max(R, __shfl_xor(R, 32)) : R;  // the wave's last round
+  const int wxi = x < N ? src.W(i, x) : -1;
+  const bool xp = x < N && wxi >= 0 && wxi < n_c;
+  uint64_t prev = 0;
+  int fv = 0;
+  for (int j = i + 1; j < Rw; j++) {
+    const bool act = j < R;
+    const int diff = j - i;
+    // round j's witness rows, lane y holding voter y's (read back by readlane: the
+    // voter loop makes no memory access)
+    const int wl = x < N ? src.W(j, x) : -1;
+    const uint64_t bl = x < N ? (diff == 1 ? src.see(j, x) : src.ss(j, x)) : 0;
+    const bool cl = x < N && diff % N == 0 && src.coin(j, x);
+    const uint64_t cm = ballot(cl);
+    uint64_t cur = 0;
+    if (diff == 1) {
+      for (int y = 0; y < N; y++) {
+        const int wy = rl(wl, y);
+        const bool py = act && wy >= 0 && wy < n_c;
+        if (py && ((rl64(bl, y) >> x) & 1)) cur |= 1ull << y;  // setVote(y, x, See(y, x))
       }
-      const int tot = __popcll(yb);
-#pragma unroll
-      for (int k = 0; k < KX; k++) {
-        const int x = xc + h + HV * k;
-        uint64_t cur;
-        if (diff == 1) {
-          cur = half(ballot(py && x < 64 && ((yb >> (x & 63)) & 1)));  // setVote(y, x, See(y, x))
-        } else {
-          const int yays = __popcll(yb & prev[k]), nays = tot - yays;
-          const bool v = yays >= nays;
-          const int tt = v ? yays : nays;
-          if (diff % N != 0) {  // normal round: SetFame(x, v) and break at the first tt >= SM
-            const uint64_t dm = half(ballot(py && tt >= SM));
-            const uint64_t vm = half(ballot(py && v));
-            if (dm) {
-              const int ys = __ffsll((unsigned long long)dm) - 1;
-              fv[k] = (vm >> ys) & 1 ? 1 : 2;
-              cur = vm & ((1ull << ys) - 1);
-            } else {
-              cur = vm;
-            }
-          } else {  // coin round: the middle bit of y's hash when no supermajority
-            cur = half(ballot(py && (tt >= SM ? v : ycoin)));
-          }
+    } else if (diff % N != 0) {  // normal round
+      bool dh = false;
+      for (int y = 0; y < N; y++) {
+        const int wy = rl(wl, y);
+        const bool py = act && wy >= 0 && wy < n_c && !dh;
+        const uint64_t yb = rl64(bl, y);
+        const int yays = __popcll(yb & prev), nays = __popcll(yb) - yays;
+        const bool v = yays >= nays;
+        if (py && (v ? yays : nays) >= SM) {  // SetFame(x, v), break
+          fv = v ? 1 : 2;
+          dh = true;
+        } else if (py && v) {
+          cur |= 1ull << y;
         }
-        prev[k] = cur;
+      }
+    } else {  // coin round: the middle bit of y's hash when no supermajority
+      for (int y = 0; y < N; y++) {
+        const int wy = rl(wl, y);
+        const bool py = act && wy >= 0 && wy < n_c;
+        const uint64_t yb = rl64(bl, y);
+        const int yays = __popcll(yb & prev), nays = __popcll(yb) - yays;
+        const bool v = yays >= nays;
+        if (py && ((v ? yays : nays) >= SM ? v : ((cm >> y) & 1))) cur |= 1ull << y;
       }
     }
-#pragma unroll
-    for (int k = 0; k < KX; k++) {
-      const int x = xc + h + HV * k;
-      const bool on = y == 0 && x < N && ((pm >> x) & 1) && fv[k] != 0;
-      const uint64_t fb = ballot(on), vb = ballot(on && fv[k] == 1);
-      if (fb & 1) {
-        dec |= 1ull << (xc + HV * k);
-        if (vb & 1) val |= 1ull << (xc + HV * k);
-      }
-      if (HV == 2 && ((fb >> 32) & 1)) {
-        dec |= 1ull << (xc + 1 + HV * k);
-        if ((vb >> 32) & 1) val |= 1ull << (xc + 1 + HV * k);
-      }
-    }
+    if (act) prev = cur;
   }
-  dec_out = dec;
-  val_out = val;
+  const uint64_t db = ballot(xp && fv != 0), vb = ballot(xp && fv == 1);
+  dec_out = HV == 2 ? (db >> (32 * h)) & 0xFFFFFFFFull : db;
+  val_out = HV == 2 ? (vb >> (32 * h)) & 0xFFFFFFFFull : vb;
 }
 
 // the witness rows in HBM
@@ -282,12 +266,18 @@ __global__ __launch_bounds__(256) void kb_pairs(BT t) {
     __syncthreads();
     LSrc<NM> sr = src;
     sr.i0 = i;
-    for (int c = lo + wv; c < hi; c += 4) {
-      const int R = t.Rc[d.co + c], s = R - 2 - i;
+    // one call per half wave (NM <= 32), per wave at NM = 64
+    constexpr int HV = NM <= 32 ? 2 : 1;
+    const int h = HV == 2 ? (tid & 63) >> 5 : 0;
+    for (int c0 = lo + HV * wv; c0 < hi; c0 += 4 * HV) {
+      const int c = c0 + h;
+      const bool okc = c < hi;
+      const int R = okc ? t.Rc[d.co + c] : i + 1;  // (no voting round: nothing decided)
+      const int n_c = okc ? (int)t.calls[d.co + c] : 0;
       uint64_t dec, val;
-      fame_pair<NM>(t, sr, i, (int)t.calls[d.co + c], R, dec, val);
-      if ((tid & 63) == 0) {
-        const int64_t p = (int64_t)(d.co + c) * BNS + s;
+      fame_pair<NM>(t, sr, i, n_c, R, dec, val);
+      if (okc && (tid & (64 / HV - 1)) == 0) {
+        const int64_t p = (int64_t)(d.co + c) * BNS + (R - 2 - i);
         t.Dp[2 * p] = dec;
         t.Dp[2 * p + 1] = val;
       }
@@ -506,42 +496,65 @@ __global__ __launch_bounds__(256) void kb_theta(BT t) {
 // call and round, then the median timestamp over OldestSelfAncestorToSee(w, x) of the
 // famous witnesses w that see x (w = (d, i_w) sees x iff FD[x][d] <= i_w, and the
 // chain-d event at FD[x][d] is then OldestSelfAncestorToSee), the upper median len/2.
-// Lanes take consecutive positions of one chain, whose first descendants on chain d
-// never decrease: the timestamp gathers of a wave stay on a few lines.
+// One workgroup per (chain, graph): the graph's call points and receive intervals and
+// the chain's thresholds are staged in LDS, so the search is LDS reads.  Lanes take
+// consecutive positions of the chain, whose first descendants on chain d never
+// decrease: the timestamp gathers of a wave stay on a few lines.
+constexpr int RKL = 2048;  // call points staged in LDS
+constexpr int RRL = 128;   // rounds of receive intervals staged in LDS
 template <int NM>
 __global__ __launch_bounds__(256) void kb_receive(BT t) {
-  const int g = blockIdx.y;
+  const int g = blockIdx.y, c = blockIdx.x;
   if (t.scal[(int64_t)g * 8 + 6] || t.scal[(int64_t)g * 8 + 7]) return;
   const GDesc d = t.gd[g];
-  const int N = t.N, cc = t.ccap, lane = threadIdx.x & 63;
-  const int nb = (cc + 255) >> 8;  // position blocks per chain
-  const int c = blockIdx.x / nb, p0 = (blockIdx.x - c * nb) * 256;
+  const int N = t.N, cc = t.ccap, tid = threadIdx.x, lane = tid & 63;
   const int len = t.clen[g * N + c];
-  if (p0 >= len) return;  // uniform per workgroup
-  const int p = p0 + threadIdx.x;
-  const int64_t cb = (int64_t)g * N * cc, cpos = (int64_t)c * cc + p;
-  const int n_last = t.gx[(int64_t)g * 16 + GX_NLAST];
+  if (len == 0) return;
+  __shared__ int32_t s_calls[RKL];
+  __shared__ int32_t s_fsuf[RRL], s_niv[RRL];
+  __shared__ int4 s_ivh[RRL * BVCAP];
+  __shared__ int32_t s_th[BICAP];
+  const int32_t* gx = t.gx + (int64_t)g * 16;
+  const int n_last = gx[GX_NLAST], Rf = gx[GX_RF], nth = gx[GX_NIV];
+  const int K = d.K, KS = min(K, RKL), RS = min(Rf, RRL);
+  for (int k = tid; k < KS; k += 256) s_calls[k] = (int)t.calls[d.co + k];
+  for (int r = tid; r < RS; r += 256) {
+    s_fsuf[r] = t.fsuf[d.ro + r];
+    s_niv[r] = t.nivl[d.ro + r];
+  }
+  for (int e = tid; e < RS * BVCAP; e += 256) s_ivh[e] = t.ivh[(int64_t)d.ro * BVCAP + e];
+  for (int k = tid; k < nth; k += 256) s_th[k] = t.thp[((int64_t)g * BICAP + k) * N + c];
+  __syncthreads();
+  auto call_at = [&](int k) -> int { return k < RKL ? s_calls[k] : (int)t.calls[d.co + k]; };
+  const int64_t cb = (int64_t)g * N * cc, eo = d.eo;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (int p = tid; p - lane < len; p += 256) {  // (whole waves iterate together)
+  const int64_t cpos = (int64_t)c * cc + p;
   const int x = p < len ? t.chain[cb + cpos] : -1;
   const bool on = x >= 0 && x < n_last;
-  const int64_t eo = d.eo;
-  int best_c = INF, bi = -1;
-  uint64_t bF = 0;
+  int best_c = INF, bi = -1, bslot = -1;
   if (on) {
-    const int r = t.round[eo + x], cl = t.xcall[eo + x];
-    const int Rf = t.gx[(int64_t)g * 16 + GX_RF];
+    const int r = t.roundch[cb + cpos];
+    int cl = 0;  // x's insertion call: the first call with more than x events
+    for (int hi = K - 1; cl < hi;) {
+      const int mid = (cl + hi) >> 1;
+      if (call_at(mid) > x) hi = mid;
+      else cl = mid + 1;
+    }
     for (int i = r + 1; i < Rf; i++) {
-      if (t.fsuf[d.ro + i] >= best_c) break;
-      const int n = t.nivl[d.ro + i];
+      const bool li = i < RRL;
+      if ((li ? s_fsuf[i] : t.fsuf[d.ro + i]) >= best_c) break;
+      const int n = li ? s_niv[i] : t.nivl[d.ro + i];
       for (int k = 0; k < n; k++) {
         const int64_t iv = (int64_t)(d.ro + i) * BVCAP + k;
-        const int4 hv = t.ivh[iv];
+        const int4 hv = li ? s_ivh[i * BVCAP + k] : t.ivh[iv];
         if (hv.y <= cl) continue;
         const int cand = max(hv.x, cl);
         if (cand >= best_c) break;
-        if (p <= t.thp[((int64_t)g * BICAP + hv.z) * N + c]) {
+        if (p <= s_th[hv.z]) {
           best_c = cand;
           bi = i;
-          bF = t.ivF[iv];
+          bslot = hv.z;
           break;
         }
       }
@@ -550,69 +563,104 @@ __global__ __launch_bounds__(256) void kb_receive(BT t) {
   // the call bucket's slot: one atomic per distinct call in the wave (a wave's
   // consecutive positions are mostly received at the same call)
   {
-    uint64_t todo = ballot(bi >= 0);
-    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-    int rank = -1;
+    // group the lanes by call (ballots only), then every group's first lane adds the
+    // group's size at once: the atomics of one wave are in flight together
+    uint64_t todo = ballot(bi >= 0), mine = 0;
     while (todo) {
       const int lead = __ffsll((unsigned long long)todo) - 1;
       const int cv = rl(best_c, lead);
       const uint64_t same = ballot(bi >= 0 && best_c == cv);
-      int base = 0;
-      if (lane == lead) base = atomicAdd(&t.bcnt[d.co + cv], __popcll(same));
-      base = rl(base, lead);
-      if (bi >= 0 && best_c == cv) rank = base + __popcll(same & below);
+      if (bi >= 0 && best_c == cv) mine = same;
       todo &= ~same;
     }
-    if (on) {
-      t.rcall[eo + x] = bi >= 0 ? best_c : -1;
-      t.rrank[eo + x] = rank;
+    const int lead = mine ? __ffsll((unsigned long long)mine) - 1 : lane;
+    int base = 0;
+    if (mine && lane == lead) base = atomicAdd(&t.bcnt[d.co + best_c], __popcll(mine));
+    base = __shfl(base, lead);
+    const int rank = mine ? base + __popcll(mine & below) : -1;
+    if (p < len) {
+      t.rcall[cb + cpos] = bi >= 0 ? best_c : -1;
+      t.rrank[cb + cpos] = rank;
     }
   }
+  if (p < len) t.rslot[cb + cpos] = bi >= 0 ? bslot : -1;
+  }  // positions
+}
+
+// MedianTimestamp (hashgraph.go:762-770) of every received event, one thread per chain
+// position (kb_receive's layout: the timestamp gathers of a wave stay on few lines):
+// the upper median (len/2) over OldestSelfAncestorToSee(w, x) of the famous witnesses
+// w of the receiving interval that see x (w = (d, i_w) sees x iff FD[x][d] <= i_w,
+// and the chain-d event at FD[x][d] is then OldestSelfAncestorToSee).
+template <int NM>
+__global__ __launch_bounds__(256) void kb_median(BT t) {
+  const int g = blockIdx.y;
+  if (t.scal[(int64_t)g * 8 + 6] || t.scal[(int64_t)g * 8 + 7]) return;
+  const GDesc d = t.gd[g];
+  const int N = t.N, cc = t.ccap, lane = threadIdx.x & 63;
+  const int nb = (cc + 255) >> 8;  // position blocks per chain
+  const int c = blockIdx.x / nb, p = (blockIdx.x - c * nb) * 256 + threadIdx.x;
+  const int len = t.clen[g * N + c];
+  if (p - lane >= len) return;  // whole waves
+  const int64_t cb = (int64_t)g * N * cc, cpos = (int64_t)c * cc + p, eo = d.eo;
+  const int slot = p < len ? t.rslot[cb + cpos] : -1;
+  const int bi = slot >= 0 ? t.thR[(int64_t)g * BICAP + slot] : -1;
+  const uint64_t bF = slot >= 0 ? t.thF[(int64_t)g * BICAP + slot] : 0;
+  const int x = slot >= 0 ? t.chain[cb + cpos] : -1;
   int64_t tx = 0;
   if (bi >= 0) {
     const int32_t* FDr = t.FD + (cb + cpos) * N;
     const int64_t* tschg = t.tsch + cb;
     const int32_t* wixr = t.WIX + (int64_t)(d.ro + bi) * N;
     const int64_t tsx = tschg[cpos];
-    // the row and the witnesses' positions, loaded unconditionally (all in flight)
-    int32_t fd[NM], wx[NM];
-    if ((N & 3) == 0) {  // 16-byte aligned rows: vector loads
-#pragma unroll
-      for (int k = 0; k < NM / 4; k++) {
-        const int4 v = 4 * k < N ? ((const int4*)FDr)[k] : make_int4(INF, INF, INF, INF);
-        const int4 w = 4 * k < N ? ((const int4*)wixr)[k] : make_int4(-1, -1, -1, -1);
-        fd[4 * k] = v.x;
-        fd[4 * k + 1] = v.y;
-        fd[4 * k + 2] = v.z;
-        fd[4 * k + 3] = v.w;
-        wx[4 * k] = w.x;
-        wx[4 * k + 1] = w.y;
-        wx[4 * k + 2] = w.z;
-        wx[4 * k + 3] = w.w;
-      }
-    } else {
-#pragma unroll
-      for (int dd = 0; dd < NM; dd++) {
-        fd[dd] = dd < N ? FDr[dd] : INF;
-        wx[dd] = dd < N ? wixr[dd] : -1;
-      }
-    }
+    // the row, the witnesses' positions and the gathers, MB witnesses at a time (each
+    // batch's loads in flight together; a compiler barrier between batches keeps the
+    // register footprint to one batch)
     int32_t vals[NM];
     int m = 0;
     bool ovf = false;
-    int64_t tq[NM];
+    const bool vec = (N & 3) == 0;  // 16-byte aligned rows
+    constexpr int MB = 16;
 #pragma unroll
-    for (int dd = 0; dd < NM; dd++) {  // every gather issued before any is used
-      const bool in = dd < N && ((bF >> dd) & 1) && fd[dd] != INF && fd[dd] <= wx[dd];
-      tq[dd] = tschg[(int64_t)dd * cc + (in ? fd[dd] : 0)];
-    }
+    for (int b0 = 0; b0 < NM; b0 += MB) {
+      int32_t fd[MB], wx[MB];
+      if (vec) {
 #pragma unroll
-    for (int dd = 0; dd < NM; dd++) {
-      const bool in = dd < N && ((bF >> dd) & 1) && fd[dd] != INF && fd[dd] <= wx[dd];
-      const int64_t o = tq[dd] - tsx;
-      ovf = ovf || (in && (o < -(int64_t)INT32_MAX || o > (int64_t)INT32_MAX));
-      vals[dd] = in ? (int32_t)o : INT32_MAX;  // fillers sort last (a real INT32_MAX ties with them)
-      m += in;
+        for (int k = 0; k < MB; k += 4) {
+          const int4 v = b0 + k < N ? *(const int4*)(FDr + b0 + k) : make_int4(INF, INF, INF, INF);
+          const int4 w = b0 + k < N ? *(const int4*)(wixr + b0 + k) : make_int4(-1, -1, -1, -1);
+          fd[k] = v.x;
+          fd[k + 1] = v.y;
+          fd[k + 2] = v.z;
+          fd[k + 3] = v.w;
+          wx[k] = w.x;
+          wx[k + 1] = w.y;
+          wx[k + 2] = w.z;
+          wx[k + 3] = w.w;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < MB; k++) {
+          fd[k] = b0 + k < N ? FDr[b0 + k] : INF;
+          wx[k] = b0 + k < N ? wixr[b0 + k] : -1;
+        }
+      }
+      int64_t tq[MB];
+      bool in[MB];
+#pragma unroll
+      for (int k = 0; k < MB; k++) {
+        const int dd = b0 + k;
+        in[k] = dd < N && ((bF >> dd) & 1) && fd[k] != INF && fd[k] <= wx[k];
+        tq[k] = tschg[(int64_t)dd * cc + (in[k] ? fd[k] : 0)];
+      }
+#pragma unroll
+      for (int k = 0; k < MB; k++) {
+        const int64_t o = tq[k] - tsx;
+        ovf = ovf || (in[k] && (o < -(int64_t)INT32_MAX || o > (int64_t)INT32_MAX));
+        vals[b0 + k] = in[k] ? (int32_t)o : INT32_MAX;  // fillers sort last (a real INT32_MAX ties with them)
+        m += in[k];
+      }
+      asm volatile("" ::: "memory");
     }
     const int32_t* wix = wixr;
     const int want = m / 2;
@@ -648,7 +696,9 @@ __global__ __launch_bounds__(256) void kb_receive(BT t) {
     }
     t.rr[eo + x] = bi;
     t.cts[eo + x] = med;
-    tx = t.ntx[eo + x];
+    t.rrch[cb + cpos] = bi;
+    t.ctsch[cb + cpos] = med;
+    tx += t.ntxch[cb + cpos];
   }
   tx = wave_sum64(tx);
   if (lane == 0 && tx) atomicAdd((unsigned long long*)&t.gctx[g], (unsigned long long)tx);
@@ -686,21 +736,32 @@ __global__ __launch_bounds__(1024) void kb_order_prep(BT t) {
   const int nord = carry;
   __threadfence_block();
   __syncthreads();
-  for (int x = tid; x < n_last; x += NT) {
-    const int c = t.rcall[eo + x];
-    if (c < 0) continue;
-    const int pos = ld(&t.boff[d.co + c]) + t.rrank[eo + x];
-    const int64_t so = 2 * eo + pos;
-    t.krr[so] = t.rr[eo + x];
-    t.kct[so] = t.cts[eo + x];
-    t.ks0[so] = t.S[(eo + x) * 4];
-    t.kid[so] = x;
+  // the received events' keys into their buckets, from the chain layout (a chain's
+  // consecutive positions received at one call hold consecutive slots)
+  {
+    const int N = t.N, cc = t.ccap;
+    const int64_t cb = (int64_t)g * N * cc;
+    for (int e = tid; e < N * cc; e += NT) {
+      const int c = e / cc, p = e - (e / cc) * cc;
+      if (p >= t.clen[g * N + c]) continue;
+      {
+        const int64_t cp = cb + e;
+        const int rc = t.rcall[cp];
+        if (rc < 0) continue;
+        const int pos = ld(&t.boff[d.co + rc]) + t.rrank[cp];
+        const int64_t so = 2 * eo + pos;
+        t.krr[so] = t.rrch[cp];
+        t.kct[so] = t.ctsch[cp];
+        t.ks0[so] = t.Sch[cp];
+        t.kid[so] = t.chain[cp];
+      }
+    }
   }
   // the undetermined list (UndeterminedEvents keeps insertion order)
   int base = 0;
   for (int x0 = 0; x0 < n_last; x0 += NT) {
     const int x = x0 + tid;
-    const bool u = x < n_last && t.rcall[eo + x] < 0;
+    const bool u = x < n_last && t.rr[eo + x] < 0;
     int tot;
     const int inc = block_scan_add(u ? 1 : 0, s_w, tot);
     if (u) t.U[eo + base + inc - 1] = x;
