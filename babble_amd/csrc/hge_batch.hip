@@ -199,17 +199,27 @@ __global__ __launch_bounds__(256) void kb_coords(BT t) {
   if (tid < NM) headid[tid] = -1;
   __syncthreads();
   int32_t* LA = t.LA + d.eo * N;
+  // wave 0 holds the next chunk's event records (loaded while this chunk's steps run)
+  int nsp = -1, nop = -1, ncr = 0, noc = 0, nix = 0;
+  auto fetch = [&](int b) {
+    const int i = b + tid;
+    const bool on = i < d.E;
+    nsp = on ? t.sp[d.eo + i] : -1;
+    nop = on ? t.op[d.eo + i] : -1;
+    ncr = on ? t.cr[d.eo + i] : 0;
+    noc = on ? t.oc[d.eo + i] : 0;
+    nix = on ? t.ix[d.eo + i] : 0;
+  };
+  if (tid < 64) fetch(0);
   for (int base = 0; base < d.E; base += 64) {
     const int cnt = min(64, d.E - base);
     if (tid < 64) {
-      const int i = base + tid;
-      const bool on = i < d.E;
-      const int sp = on ? t.sp[d.eo + i] : -1, op = on ? t.op[d.eo + i] : -1;
-      const int cr = on ? t.cr[d.eo + i] : 0, oc = on ? t.oc[d.eo + i] : 0;
+      const int sp = nsp, op = nop, cr = ncr, oc = noc;
+      const bool on = base + tid < d.E;
       auto src = [&](int p, int c) -> int {
         return p < 0 ? -1 : p >= base ? p - base : headid[c] == p ? 64 + c : -2;
       };
-      einfo[tid] = make_int4(src(sp, cr), src(op, oc), cr, on ? t.ix[d.eo + i] : 0);
+      einfo[tid] = make_int4(src(sp, cr), src(op, oc), cr, nix);
       msp[tid] = sp;
       mop[tid] = op;
       if (tid < NM) clast[tid] = -1;
@@ -230,6 +240,7 @@ __global__ __launch_bounds__(256) void kb_coords(BT t) {
         gst[ng] = cnt;
         s_ng = ng;
       }
+      if (base + 64 < d.E) fetch(base + 64);
     }
     __syncthreads();
     const int ng = s_ng;
@@ -1673,7 +1684,14 @@ struct hge_batch {
     }
     BCHK(hipEventRecord(ev[7], st));
     launch(kb_order_prep<NM>, G, t, 1024);
-    launch(kb_sort, (int)std::min<int64_t>(std::max<int64_t>(Ktot, 1), (int64_t)ncu * 8), t, 256);
+    // call buckets: up to 1,024 keys one wave each (a workgroup of four while the
+    // batch has few buckets), larger ones a workgroup each
+    const int nbk = (int)std::min<int64_t>(std::max<int64_t>(Ktot, 1), (int64_t)ncu * 16);
+    if (Ktot > 16 * (int64_t)ncu) hipLaunchKernelGGL((kb_sort<64, 0, 1024>), dim3(nbk), dim3(64), 0, st, t, 0);
+    else hipLaunchKernelGGL((kb_sort<256, 0, 1024>), dim3(nbk), dim3(256), 0, st, t, 0);
+    BCHK(hipGetLastError());
+    hipLaunchKernelGGL((kb_sort<256, 1024, 4096>), dim3(ncu), dim3(256), 0, st, t, 1);
+    BCHK(hipGetLastError());
     BCHK(hipEventRecord(ev[8], st));
   }
 

@@ -32,7 +32,6 @@ constexpr int BNS = 3;      // DecideFame pairs per call: rounds R_c - 2 - s, s 
 constexpr int BVCAP = 4;    // receive intervals per round
 constexpr int BICAP = 512;  // receive intervals per graph
 constexpr int FRS = 4;      // rounds per lane in kb_fold (64 * FRS rounds)
-constexpr int BLK = 1024;   // call buckets sorted in LDS up to this many keys
 
 // per-graph internals, t.gx[g * 16 + k]
 enum { GX_NARR = 0, GX_LCR = 2, GX_LCRC = 3, GX_NIV = 4, GX_MISS = 5, GX_RF = 6, GX_NLAST = 7 };
@@ -286,152 +285,128 @@ __global__ __launch_bounds__(256) void kb_pairs(BT t) {
   }
 }
 
-// The calls in order, one wave per graph.  Lane l keeps rounds l, l + 64, ...
-// (FRS slots): present witnesses, decided and famous masks, the open interval.
-// Per call: its arrivals, then DecideFame's rounds LCR+1 .. R_c-2 from the pairs
-// (inline past the window), setLastConsensusRound (the highest decided round of
-// the loop), then every touched round's (decided, famous set) state: a change
-// closes the open interval [start, c) and opens one when decided with a famous
-// witness.  Rounds with no famous witness receive nothing (len(s) > 0 fails).
+// The calls in order, one wave per graph, visiting only the calls where DecideFame
+// has a round to decide: i in [LCR+1, R_c-3] (round R_c - 2 meets one voting round
+// and decides nothing, nor was it decided at an earlier call: R never decreases), so
+// from call c the next such call is the first with R >= LCR + 4 (rfirst).  Lane l
+// keeps rounds l, l + 64, ... (FRS slots): decided and famous masks.  A round's
+// present witnesses at call c come from its witnesses' arrival calls (LDS).
+// Each round has at most one receive interval: a round is decided only while
+// processed (i > LCR), and deciding it sets LCR >= i, so it is never processed again;
+// the next witness to arrive (fame undefined) ends the interval for good.  So the
+// interval [c, next arrival) with famous set F is written when the round is decided,
+// and setLastConsensusRound (hashgraph.go:666-673) follows the loop's highest
+// decided round.
 template <int NM>
 __global__ __launch_bounds__(64) void kb_fold(BT t) {
+  constexpr int RL = 64 * FRS;  // rounds held
   const int g = blockIdx.x;
   const GDesc d = t.gd[g];
   const int lane = threadIdx.x, N = t.N, K = d.K;
   int32_t* gx = t.gx + (int64_t)g * 16;
   if (t.scal[(int64_t)g * 8 + 6]) return;
   const int Rf = gx[GX_RF], narr = gx[GX_NARR];
-  if (Rf > 64 * FRS) {
+  if (Rf > RL || Rf * N > RL * 32) {
     if (lane == 0) t.scal[(int64_t)g * 8 + 7] = 1;
     return;
   }
-  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-  uint64_t pres[FRS], dfn[FRS], vl[FRS], oF[FRS];
-  int ost[FRS], ni[FRS], fst[FRS];
-  bool tch[FRS];
+  __shared__ int32_t wc[RL * 32];  // [r][creator]: the call its witness arrives at (K: none)
+  __shared__ int32_t rfl[RL + 1];  // rfirst
+  for (int e = lane; e < Rf * N; e += 64) wc[e] = K;
+  for (int r = lane; r <= Rf; r += 64) rfl[r] = r >= 3 ? t.rfirst[d.ro + r] : 0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  wsync();
+  for (int k = lane; k < narr; k += 64) {
+    const uint64_t a = t.arr[d.eo + k];
+    wc[(int)((a >> 8) & 0xFFFFFF) * N + (int)(a & 0xFF)] = (int)(a >> 32);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  wsync();
+  uint64_t dfn[FRS], vl[FRS];
+  int fst[FRS];
 #pragma unroll
   for (int q = 0; q < FRS; q++) {
-    pres[q] = dfn[q] = vl[q] = oF[q] = 0;
-    ost[q] = -1;
-    ni[q] = 0;
+    dfn[q] = vl[q] = 0;
     fst[q] = INF;
-    tch[q] = false;
   }
   int LCR = -1, lcr_call = -1, nth = 0, miss = 0;
-  bool fail = false;
-  // emission of the closing intervals of slot q at call ce (lanes with em)
-  auto emit = [&](int q, bool em, int ce) {
-    const uint64_t m = ballot(em);
-    if (!m) return;
-    if (em) {
-      const int r = q * 64 + lane, slot = nth + __popcll(m & below);
-      if (ni[q] < BVCAP && slot < BICAP) {
-        const int64_t iv = (int64_t)(d.ro + r) * BVCAP + ni[q];
-        t.ivh[iv] = make_int4(ost[q], ce, slot, 0);
-        t.ivF[iv] = oF[q];
-        t.thR[(int64_t)g * BICAP + slot] = r;
-        t.thF[(int64_t)g * BICAP + slot] = oF[q];
-      } else {
-        fail = true;
+  int c = -1, c0 = -INF, Rreg = 0, Nreg = 0;
+  uint64_t Dd[BNS], Dv[BNS];
+  while (true) {
+    const int need = LCR + 4;  // the next call with a round to decide has R >= LCR + 4
+    if (need > Rf) break;
+    c = max(c + 1, rfl[need]);
+    if (c >= K) break;
+    if (c >= c0 + 64) {  // the next 64 calls' R, sizes and pairs, lane l holding call c0 + l
+      c0 = c;
+      const int cl = c0 + lane;
+      const bool on = cl < K;
+      Rreg = on ? t.Rc[d.co + cl] : 0;
+      Nreg = on ? (int)t.calls[d.co + cl] : 0;
+#pragma unroll
+      for (int s = 0; s < BNS; s++) {
+        const int64_t p = ((int64_t)(d.co + cl)) * BNS + s;
+        const bool ok = on && s > 0 && Rreg - 2 - s >= 0;
+        Dd[s] = ok ? t.Dp[2 * p] : 0;
+        Dv[s] = ok ? t.Dp[2 * p + 1] : 0;
       }
-      ni[q]++;
     }
-    nth += __popcll(m);
-  };
-  int ap = 0, abase = 0;
-  uint64_t areg = lane < narr ? t.arr[d.eo + lane] : ~0ull;
-  for (int c0 = 0; c0 < K; c0 += 64) {
-    const int cl = c0 + lane;
-    const bool on = cl < K;
-    const int Rreg = on ? t.Rc[d.co + cl] : 0;
-    const int Nreg = on ? (int)t.calls[d.co + cl] : 0;
-    uint64_t Dd[BNS], Dv[BNS];
+    const int cc = c - c0, R = rl(Rreg, cc);
+    int newL = -1;
+    for (int i = LCR + 1; i <= R - 3; i++) {
+      const int s = R - 2 - i;
+      uint64_t dec = 0, v = 0;
+      if (s < BNS) {
 #pragma unroll
-    for (int s = 0; s < BNS; s++) {
-      const int64_t p = ((int64_t)(d.co + cl)) * BNS + s;
-      const bool ok = on && s > 0 && Rreg - 2 - s >= 0;
-      Dd[s] = ok ? t.Dp[2 * p] : 0;
-      Dv[s] = ok ? t.Dp[2 * p + 1] : 0;
-    }
-    const int m = min(64, K - c0);
-    for (int cc = 0; cc < m; cc++) {
-      const int c = c0 + cc;
-      // DivideRounds: the call's new witnesses join their rounds
-      while (ap < narr) {
-        if (ap - abase == 64) {
-          abase = ap;
-          areg = ap + lane < narr ? t.arr[d.eo + ap + lane] : ~0ull;
-        }
-        const uint64_t a = rl64(areg, ap - abase);
-        if ((int)(a >> 32) != c) break;
-        const int r = (int)((a >> 8) & 0xFFFFFF), k = (int)(a & 0xFF);
-#pragma unroll
-        for (int q = 0; q < FRS; q++)
-          if (q == (r >> 6) && lane == (r & 63)) {
-            pres[q] |= 1ull << k;
-            tch[q] = tch[q] || ost[q] >= 0;  // a new witness can only undo a decided state
+        for (int q = 0; q < BNS; q++)
+          if (q == s) {
+            dec = rl64(Dd[q], cc);
+            v = rl64(Dv[q], cc);
           }
-        ap++;
+      } else {
+        fame_pair<NM>(t, GSrc{t, (int64_t)d.ro, N}, i, rl(Nreg, cc), R, dec, v);
+        miss++;
       }
-      // DecideFame's rounds
-      const int R = rl(Rreg, cc);
-      int newL = -1;
-      // (round R - 2 meets one voting round: nothing is decided there, it is not decided
-      // from an earlier call either -- R never decreases -- so it is skipped)
-      for (int i = LCR + 1; i <= R - 3; i++) {
-        const int s = R - 2 - i;
-        uint64_t dec = 0, v = 0;
-        if (s < BNS) {
+      const int wci = lane < N ? wc[i * N + lane] : K;
+      const uint64_t pres = ballot(lane < N && wci <= c);
+      uint64_t df = 0, vv = 0;
 #pragma unroll
-          for (int q = 0; q < BNS; q++)
-            if (q == s) {
-              dec = rl64(Dd[q], cc);
-              v = rl64(Dv[q], cc);
-            }
-        } else {
-          fame_pair<NM>(t, GSrc{t, (int64_t)d.ro, N}, i, rl(Nreg, cc), R, dec, v);
-          miss++;
-        }
-        bool dcd = false;
-#pragma unroll
-        for (int q = 0; q < FRS; q++)
-          if (q == (i >> 6) && lane == (i & 63)) {
+      for (int q = 0; q < FRS; q++)
+        if (q == (i >> 6)) {
+          if (lane == (i & 63)) {
             dfn[q] |= dec;
             vl[q] = (vl[q] & ~dec) | v;
-            tch[q] = true;
-            dcd = (pres[q] & ~dfn[q]) == 0;
           }
-        if (ballot(dcd)) newL = i;  // WitnessesDecided (roundInfo.go:78-85)
-      }
-      if (newL >= 0) {
-        LCR = newL;
-        lcr_call = c;
-      }
-      // the touched rounds' receive state
+          df = rl64(dfn[q], i & 63);
+          vv = rl64(vl[q], i & 63);
+        }
+      if ((pres & ~df) == 0) {  // WitnessesDecided (roundInfo.go:78-85)
+        newL = i;
+        const uint64_t F = pres & vv;
+        if (F) {  // the receive interval [c, the next arrival)
+          const int ce = wave_min(lane < N && wci > c ? wci : K);
+          if (nth < BICAP) {
+            if (lane == 0) {
+              const int64_t iv = (int64_t)(d.ro + i) * BVCAP;
+              t.ivh[iv] = make_int4(c, ce, nth, 0);
+              t.ivF[iv] = F;
+              t.thR[(int64_t)g * BICAP + nth] = i;
+              t.thF[(int64_t)g * BICAP + nth] = F;
+            }
 #pragma unroll
-      for (int q = 0; q < FRS; q++) {
-        if (q * 64 >= Rf || !ballot(tch[q])) continue;
-        bool em = false;
-        uint64_t key = oF[q];
-        if (tch[q]) {
-          const bool dcd = (pres[q] & ~dfn[q]) == 0;
-          key = dcd ? pres[q] & vl[q] : 0;
-          em = key != oF[q] && ost[q] >= 0;
+            for (int q = 0; q < FRS; q++)
+              if (q == (i >> 6) && lane == (i & 63)) fst[q] = c;
+          }
+          nth++;
         }
-        emit(q, em, c);
-        if (tch[q] && key != oF[q]) {
-          ost[q] = key ? c : -1;
-          oF[q] = key;
-          if (key && fst[q] == INF) fst[q] = c;
-        }
-        tch[q] = false;
       }
     }
+    if (newL >= 0) {
+      LCR = newL;
+      lcr_call = c;
+    }
   }
-#pragma unroll
-  for (int q = 0; q < FRS; q++)
-    if (q * 64 < Rf) emit(q, ost[q] >= 0, K);
-  if (ballot(fail)) {
+  if (nth > BICAP) {
     if (lane == 0) t.scal[(int64_t)g * 8 + 7] = 1;
     return;
   }
@@ -450,7 +425,7 @@ __global__ __launch_bounds__(64) void kb_fold(BT t) {
     carry = rl(v, 0);
     const int r = q * 64 + lane;
     if (r < Rf) {
-      t.nivl[d.ro + r] = ni[q];
+      t.nivl[d.ro + r] = fst[q] != INF ? 1 : 0;
       t.fsuf[d.ro + r] = v;
       if (dfn[q])
         for (int x = 0; x < N; x++)
@@ -787,76 +762,126 @@ __global__ __launch_bounds__(1024) void kb_order_prep(BT t) {
   }
 }
 
-// One call bucket per workgroup iteration (a work list over the whole batch):
-// ascending bitonic network whose merge stages compare mirrored pairs, so slots
-// past the bucket act as +infinity and need no storage.  Up to BLK keys in LDS;
-// larger buckets on their global scratch.
-__global__ __launch_bounds__(256) void kb_sort(BT t) {
-  __shared__ int32_t lr[BLK], li[BLK];
-  __shared__ int64_t lc[BLK];
-  __shared__ uint64_t ls[BLK];
-  const int tid = threadIdx.x, NT = 256;
+// The call buckets' sorts (a work list over the whole batch): an ascending bitonic
+// network whose merge stages compare mirrored pairs, so slots past the bucket act as
+// +infinity and need no storage.  A bucket's keys (rr, cts, S, id) sort on an
+// order-preserving 64-bit prefix held in LDS with a 16-bit index:
+// (rr - rmin) << 60 | (cts - cmin) << 32 | S >> 32 when the bucket's rounds span
+// under 16 and its timestamps under 2^28 ns (else the prefix is 0); equal prefixes
+// compare the full key from HBM (consensus_sorter.go:36-59, PRN = 0).
+// kb_sort<TPB, LO, CAP> takes the buckets of LO < n <= CAP keys, TPB threads per
+// bucket (one wave while the batch has many buckets, four while it has few); the
+// largest class sorts buckets past CAP on their full keys in HBM.
+__device__ __forceinline__ void bitonic_pair(int q, int size, int stride, int& a, int& b) {
+  if (stride == size >> 1) {  // merge: mirrored pairs
+    const int blk = q / stride, i = q - blk * stride;
+    a = blk * size + i;
+    b = blk * size + size - 1 - i;
+  } else {
+    a = 2 * q - (q & (stride - 1));
+    b = a + stride;
+  }
+}
+__device__ __forceinline__ int64_t wave_min64(int64_t v) {
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (int64_t)__shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ int64_t wave_max64(int64_t v) {
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (int64_t)__shfl_xor(v, o));
+  return v;
+}
+template <int TPB, int LO, int CAP>
+__global__ __launch_bounds__(TPB) void kb_sort(BT t, int last) {
+  __shared__ uint64_t lk[CAP];
+  __shared__ uint16_t lx[CAP];
+  __shared__ int s_red[4][4];
+  __shared__ int64_t s_red64[4][2];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int nw = ld(t.wlc);
+  auto sync = [&](bool block) {
+    if (TPB == 64 || !block) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+      wsync();
+    } else {
+      __syncthreads();
+    }
+  };
   for (int w = blockIdx.x; w < nw; w += gridDim.x) {
     const int4 gc = t.wl[w];
     const int g = gc.x, n = gc.y, base = gc.z;
-    const int64_t eo = t.gd[g].eo;
-    const int64_t so = 2 * eo + base;
+    if (n <= LO || (n > CAP && !last)) continue;
+    const int64_t eo = t.gd[g].eo, so = 2 * eo + base;
     int P = 1;
     while (P < n) P <<= 1;
-    if (n <= BLK) {
-      for (int k = tid; k < n; k += NT) {
-        lr[k] = t.krr[so + k];
-        li[k] = t.kid[so + k];
-        lc[k] = t.kct[so + k];
-        ls[k] = t.ks0[so + k];
+    auto full_less = [&](int a, int b) -> bool {
+      return key_less(t, eo, t.krr[so + a], t.kct[so + a], t.ks0[so + a], t.kid[so + a], t.krr[so + b],
+                      t.kct[so + b], t.ks0[so + b], t.kid[so + b]);
+    };
+    if (n <= CAP) {
+      int rmn = INT32_MAX, rmx = INT32_MIN;
+      int64_t cmn = INT64_MAX, cmx = INT64_MIN;
+      for (int k = tid; k < n; k += TPB) {
+        const int r = t.krr[so + k];
+        const int64_t c = t.kct[so + k];
+        rmn = min(rmn, r);
+        rmx = max(rmx, r);
+        cmn = min(cmn, c);
+        cmx = max(cmx, c);
       }
-      __syncthreads();
-      for (int size = 2; size <= P; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-          for (int q = tid; q < P / 2; q += NT) {
-            int a, b;
-            if (stride == size >> 1) {
-              const int blk = q / stride, i = q - blk * stride;
-              a = blk * size + i;
-              b = blk * size + size - 1 - i;
-            } else {
-              a = 2 * q - (q & (stride - 1));
-              b = a + stride;
-            }
-            if (b >= n) continue;
-            if (key_less(t, eo, lr[b], lc[b], ls[b], li[b], lr[a], lc[a], ls[a], li[a])) {
-              const int r_ = lr[a], i_ = li[a];
-              const int64_t c_ = lc[a];
-              const uint64_t s_ = ls[a];
-              lr[a] = lr[b];
-              li[a] = li[b];
-              lc[a] = lc[b];
-              ls[a] = ls[b];
-              lr[b] = r_;
-              li[b] = i_;
-              lc[b] = c_;
-              ls[b] = s_;
-            }
-          }
-          stage_sync(size, stride);
+      rmn = wave_min(rmn);
+      rmx = wave_max(rmx);
+      cmn = wave_min64(cmn);
+      cmx = wave_max64(cmx);
+      if (TPB > 64) {
+        if (lane == 0) {
+          s_red[wv][0] = rmn;
+          s_red[wv][1] = rmx;
+          s_red64[wv][0] = cmn;
+          s_red64[wv][1] = cmx;
+        }
+        __syncthreads();
+        for (int k = 0; k < TPB / 64; k++) {
+          rmn = min(rmn, s_red[k][0]);
+          rmx = max(rmx, s_red[k][1]);
+          cmn = min(cmn, s_red64[k][0]);
+          cmx = max(cmx, s_red64[k][1]);
         }
       }
-      __syncthreads();
-      for (int k = tid; k < n; k += NT) t.order[eo + base + k] = li[k];
+      const bool fits = rmx - rmn < 16 && cmx - cmn < ((int64_t)1 << 28);
+      for (int k = tid; k < n; k += TPB) {
+        lk[k] = fits ? ((uint64_t)(t.krr[so + k] - rmn) << 60) | ((uint64_t)(t.kct[so + k] - cmn) << 32) |
+                           (t.ks0[so + k] >> 32)
+                     : 0;
+        lx[k] = (uint16_t)k;
+      }
+      sync(true);
+      for (int size = 2; size <= P; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+          for (int q = tid; q < P / 2; q += TPB) {
+            int a, b;
+            bitonic_pair(q, size, stride, a, b);
+            if (b >= n) continue;
+            const uint64_t ka = lk[a], kb = lk[b];
+            const int xa = lx[a], xb = lx[b];
+            if (kb < ka || (kb == ka && full_less(xb, xa))) {
+              lk[a] = kb;
+              lk[b] = ka;
+              lx[a] = (uint16_t)xb;
+              lx[b] = (uint16_t)xa;
+            }
+          }
+          const int next = stride > 1 ? stride >> 1 : size;  // the next stage's stride
+          sync(stride > 64 || next > 64);
+        }
+      sync(true);
+      for (int k = tid; k < n; k += TPB) t.order[eo + base + k] = t.kid[so + lx[k]];
+      sync(true);  // the LDS keys are the next bucket's
     } else {
       for (int size = 2; size <= P; size <<= 1) {
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
-          for (int q = tid; q < P / 2; q += NT) {
+          for (int q = tid; q < P / 2; q += TPB) {
             int a, b;
-            if (stride == size >> 1) {
-              const int blk = q / stride, i = q - blk * stride;
-              a = blk * size + i;
-              b = blk * size + size - 1 - i;
-            } else {
-              a = 2 * q - (q & (stride - 1));
-              b = a + stride;
-            }
+            bitonic_pair(q, size, stride, a, b);
             if (b >= n) continue;
             const int ra = ld(t.krr + so + a), rb = ld(t.krr + so + b);
             const int ia = ld(t.kid + so + a), ib = ld(t.kid + so + b);
@@ -877,8 +902,8 @@ __global__ __launch_bounds__(256) void kb_sort(BT t) {
           __syncthreads();
         }
       }
-      for (int k = tid; k < n; k += NT) t.order[eo + base + k] = ld(t.kid + so + k);
+      for (int k = tid; k < n; k += TPB) t.order[eo + base + k] = ld(t.kid + so + k);
+      __syncthreads();
     }
-    __syncthreads();  // the LDS keys are the next bucket's
   }
 }

@@ -126,7 +126,10 @@ struct hge_engine {
   // N > 32 past chain_limit: int32 positions for good (hge_wide32.hip); pending until
   // the next coordinate step converts the packed table
   bool wide32 = false, wide32_pending = false;
-  int w32_done = 0;  // to_wide32's progress: 1 the runs widened, 2 the FD rows, 4 the int32 LA table allocated
+  int w32_done = 0;
+  // an internal failure that left the host and device state apart: every later
+  // consensus call refuses (HGE_ERR_INTERNAL) until a new stream (hge_replay_prepare)
+  std::string failed;  // to_wide32's progress: 1 the runs widened, 2 the FD rows, 4 the int32 LA table allocated
   // test hook (HGE_TEST_W32_FAIL=k): to_wide32 fails once after its stage k (1 the int32
   // LA table allocated, 2 the runs widened, 3 the FD rows widened)
   int test_w32_fail = getenv("HGE_TEST_W32_FAIL") ? atoi(getenv("HGE_TEST_W32_FAIL")) : 0;
@@ -605,6 +608,7 @@ struct hge_engine {
 
   void reset_state() {
     sync();
+    failed.clear();  // a new stream (hge_reset, hge_replay_prepare)
     minw_full = true;
     cons_pin_n = 0;
     h_creator.clear();
@@ -1654,11 +1658,7 @@ struct hge_engine {
   // k_fd_transpose_ts<uint16_t>: half the run table's bytes written and read).  Neither the
   // direct walk nor theta reads FDT; the speculative walkers (N <= 128) and the
   // FDT-gather walk (N % 4 != 0) read int32 runs.
-#ifdef HGE_AB_NO_FDT16  // A/B builds: int32 runs throughout
-  bool fdt16() const { return false; }
-#else
   bool fdt16() const { return N > 128 && (N & 3) == 0 && !wide32; }
-#endif
 
   // 32 < N <= 256: lastAncestors by windowed exact propagation (hge_coords_win.hip)
   // instead of the sweeps
@@ -2996,7 +2996,10 @@ struct hge_engine {
     const size_t offw = d2h_pinned(d_minw.p, 4 * ((size_t)Rcap + 4));
     sync();
     const int32_t* hw = (const int32_t*)(pin + offw);
-    if (hw[Rcap + 1]) throw EngineError(HGE_ERR_INTERNAL, "online call: rounds table overflow past its bound");
+    if (hw[Rcap + 1]) {  // (unreachable: ensure_rcap covers R + m + 4) the host state has moved on: refuse later calls
+      failed = "online call: rounds table overflow past its bound";
+      throw EngineError(HGE_ERR_INTERNAL, failed);
+    }
     R = hw[Rcap];
     h_minw.assign(hw, hw + R);
     minw_full = false;
@@ -3041,6 +3044,8 @@ struct hge_engine {
 // C ABI
 // ---------------------------------------------------------------------------
 #define GUARD_BEGIN try {
+#define REFUSE_IF_FAILED(h) \
+  if (!(h)->failed.empty()) throw EngineError(HGE_ERR_INTERNAL, "engine state inconsistent since: " + (h)->failed);
 #define GUARD_END(h)                 \
   }                                  \
   catch (EngineError & e) {          \
@@ -3090,6 +3095,7 @@ int hge_reset(hge_engine* h) {
 int hge_insert_events(hge_engine* h, const hge_event* ev, int64_t n, int32_t* status_out,
                       int64_t* n_accepted) {
   GUARD_BEGIN
+  REFUSE_IF_FAILED(h)
   const int64_t c0 = hge_engine::now_ns();
   int64_t acc = 0;
   int rc = HGE_OK;
@@ -3113,6 +3119,7 @@ int hge_insert_events(hge_engine* h, const hge_event* ev, int64_t n, int32_t* st
 
 int hge_divide_rounds(hge_engine* h) {
   GUARD_BEGIN
+  REFUSE_IF_FAILED(h)
   h->divide();
   return HGE_OK;
   GUARD_END(h)
@@ -3120,6 +3127,7 @@ int hge_divide_rounds(hge_engine* h) {
 
 int hge_decide_fame(hge_engine* h) {
   GUARD_BEGIN
+  REFUSE_IF_FAILED(h)
     h->consensus_batch({h->n_divided}, true, false, false, nullptr, nullptr);
   return HGE_OK;
   GUARD_END(h)
@@ -3127,6 +3135,7 @@ int hge_decide_fame(hge_engine* h) {
 
 int hge_decide_round_received(hge_engine* h) {
   GUARD_BEGIN
+  REFUSE_IF_FAILED(h)
     h->consensus_batch({h->n_divided}, false, true, false, nullptr, nullptr);
   return HGE_OK;
   GUARD_END(h)
@@ -3134,6 +3143,7 @@ int hge_decide_round_received(hge_engine* h) {
 
 int hge_find_order(hge_engine* h, int32_t* ids_out, int64_t cap, int64_t* n_out) {
   GUARD_BEGIN
+  REFUSE_IF_FAILED(h)
     std::vector<int32_t> order;
   h->consensus_batch({h->n_divided}, false, true, true, &order, nullptr);
   for (int64_t i = 0; i < (int64_t)order.size() && i < cap && ids_out; i++) ids_out[i] = order[i];
@@ -3144,6 +3154,7 @@ int hge_find_order(hge_engine* h, int32_t* ids_out, int64_t cap, int64_t* n_out)
 
 int hge_run_consensus(hge_engine* h, int32_t* ids_out, int64_t cap, int64_t* n_out) {
   GUARD_BEGIN
+  REFUSE_IF_FAILED(h)
   const int64_t c0 = hge_engine::now_ns();
   std::vector<int32_t> order;
   if (!h->online_fast(order)) {
@@ -3268,6 +3279,7 @@ static void replay_end(hge_engine* h, int64_t* n_ordered) {
 
 int hge_replay_run(hge_engine* h, int64_t* n_ordered) {
   GUARD_BEGIN
+  REFUSE_IF_FAILED(h)
   h->sp_active = false;
   if (h->rec_on) h->rec_dec.clear();
   replay_begin(h);

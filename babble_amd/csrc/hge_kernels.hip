@@ -2104,7 +2104,12 @@ __global__ void k_round_received(Tables t, const int32_t* cand, int ncand, const
 // Wave-wide inclusive scans by DPP row shifts and row broadcasts (VALU, no LDS
 // crossbar): row_shr 1/2/4/8 scan each 16-lane row, row_bcast15 / row_bcast31 carry
 // rows 0 -> 1, 2 -> 3 and rows 0-1 -> 2-3.  A lane whose source is outside its row
-// (or a row the mask leaves out) takes the identity.
+// (or a row the mask leaves out) takes the identity.  Every lane of the wave must be
+// active (EXEC full): an inactive source lane would read as the identity, not its
+// value.  row_bcast15/31 exist on GFX9-family targets (CDNA) only.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__GFX9__)
+#error "HGE_DPP_SCAN needs the GFX9-family DPP row broadcasts (CDNA; built for gfx950)"
+#endif
 #define HGE_DPP_SCAN(x, op, id)                                                        \
   do {                                                                                 \
     x = op(x, __builtin_amdgcn_update_dpp((id), (x), 0x111, 0xf, 0xf, false));         \
@@ -2132,22 +2137,12 @@ __device__ __forceinline__ uint32_t wave_upper_median32_r8(const uint32_t (&v)[V
       mx = max(mx, v[k]);
     }
   }
-#ifdef HGE_MED_SHFL
-  for (int o = 32; o > 0; o >>= 1) {
-    mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
-    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-  }
-  mn = __builtin_amdgcn_readfirstlane(mn);
-  if (n == 0) return mn;  // no value (a candidate that is not stored)
-  const uint32_t span = __builtin_amdgcn_readfirstlane(mx - mn);
-#else
   int smn = (int)mn, smx = (int)mx;
   HGE_DPP_SCAN(smn, dpp_umin, -1);
   HGE_DPP_SCAN(smx, dpp_umax, 0);
   mn = (uint32_t)__builtin_amdgcn_readlane(smn, 63);  // lane 63: the whole wave
   if (n == 0) return mn;  // no value (a candidate that is not stored)
   const uint32_t span = (uint32_t)__builtin_amdgcn_readlane(smx, 63) - mn;
-#endif
   int kk = n / 2;  // 0-based rank of the upper median
   uint32_t vr[VPL];
   bool live[VPL];
@@ -2172,14 +2167,7 @@ __device__ __forceinline__ uint32_t wave_upper_median32_r8(const uint32_t (&v)[V
     const int4 b = *(const int4*)&hist[4 * lane];
     const int tot = b.x + b.y + b.z + b.w;
     int inc = tot;  // inclusive scan of the lanes' totals
-#ifdef HGE_MED_SHFL
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += y;
-    }
-#else
     HGE_DPP_SCAN(inc, dpp_add, 0);
-#endif
     const int ex = inc - tot;
     const uint64_t hit = __ballot(ex <= kk && kk < inc);
     const int L = (int)__builtin_ctzll(hit);
@@ -2471,11 +2459,7 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
       uint32_t v[VPL];
 #pragma unroll
       for (int k = 0; k < VPL; k++) v[k] = in[k] ? ((uint32_t)off[e][k] ^ 0x80000000u) : ~0u;
-#ifdef HGE_MED_NOSEL  // diagnostics: loads and flags only
-      med = bse[e] + (int64_t)(int32_t)(__builtin_amdgcn_readfirstlane(v[0]) ^ 0x80000000u);
-#else
       med = bse[e] + (int64_t)(int32_t)(wave_upper_median32_r8<VPL>(v, in, s_mhist[threadIdx.x >> 6]) ^ 0x80000000u);
-#endif
     } else {
       uint64_t v[VPL];
 #pragma unroll

@@ -43,4 +43,5 @@ def test_bulk_model_matches_oracle(case):
         np.testing.assert_array_equal(np.asarray(got[f]), np.asarray(want[f]), err_msg=f)
     o = np.asarray(want["order"])
     np.testing.assert_array_equal(got["cts"][o], np.asarray(want["cts"])[o], err_msg="cts")
-    assert got["stats"]["max_intervals"] <= 4
+    # one receive interval per round at most (kb_fold writes it when the round is decided)
+    assert got["stats"]["max_intervals"] <= 1
