@@ -143,6 +143,7 @@ struct hge_engine {
   // hge_replay_fetch: one copy); the log's vector gets them on first use
   // (consensus_sync), outside the replay.
   int32_t* pin_ord = nullptr;
+  int32_t* pin_ord_dev = nullptr;  // its device-side address (the sorts write there)
   size_t pin_ord_cap = 0;
   int64_t cons_pin_n = 0;
   bool lazy_order = false;
@@ -157,9 +158,12 @@ struct hge_engine {
     consensus_sync();
     if (pin_ord) HIPCHK(hipHostFree(pin_ord));
     pin_ord = nullptr;
+    pin_ord_dev = nullptr;
     pin_ord_cap = 0;
     HIPCHK(hipHostMalloc((void**)&pin_ord, std::max<size_t>(n, 1) * 4, hipHostMallocDefault));
     pin_ord_cap = std::max<size_t>(n, 1);
+    void* dp = nullptr;
+    pin_ord_dev = hipHostGetDevicePointer(&dp, pin_ord, 0) == hipSuccess ? (int32_t*)dp : nullptr;
   }
   int64_t n_und = 0;
 
@@ -454,6 +458,7 @@ struct hge_engine {
     pin_cap = pin_used = 0;
     if (pin_ord) (void)hipHostFree(pin_ord);
     pin_ord = nullptr;
+    pin_ord_dev = nullptr;
     pin_ord_cap = 0;
     cons_pin_n = 0;
     if (st) (void)hipStreamDestroy(st);
@@ -2199,6 +2204,12 @@ struct hge_engine {
     int32_t* o_cnt = s_out.p;  // [0] received [1] undetermined [2] LCR events [4..5] tx
     int32_t* o_cc = s_out.p + 8;
     int32_t* o_ids = s_out.p + 8 + ncalls;
+    // a replay's sorts write the order straight into the pinned order buffer (host
+    // memory mapped into the device: the writes cross PCIe while the later buckets
+    // sort; no copy after the replay)
+    const bool direct = lazy_order && !order_out && !spl && pin_ord_dev;
+    int32_t* ids_dst = o_ids;
+    bool wrote_direct = false;  // (only the bucket sorts below write there; other paths write o_ids)
     unsigned long long* o_ntx = (unsigned long long*)(s_out.p + 4);
     // the results header zeroed, with the new LastConsensusRound (o_cnt[3]) when the
     // device holds it (one launch in place of a memset and a copy)
@@ -2456,19 +2467,23 @@ struct hge_engine {
           KLAUNCH(k_bucket_keys, dim3(div_up(ncand, 256)), dim3(256), 0, st, t, cand, ncand, s_recv.p,
                   s_rr.p, s_cts.p, s_bpos.p, k1, d_rr.p, d_cts.p,
                   (unsigned long long*)(s_out.p + o_tx));
+          if (direct) {
+            ids_dst = pin_ord_dev;
+            wrote_direct = true;
+          }
           if (ncalls <= 8) {
             // a few buckets (an online call): one launch, each bucket to the path its size takes
             KLAUNCH(k_bucket_sort_all, dim3(ncalls), dim3(1024), 0, st, (const int32_t*)s_bpos.p,
-                    (const int32_t*)o_cc, (const int32_t*)blist, (const int32_t*)nblist, k1, k2, o_ids);
+                    (const int32_t*)o_cc, (const int32_t*)blist, (const int32_t*)nblist, k1, k2, ids_dst);
           } else {
             // buckets of 513 .. 2 * BIG_SORT keys in LDS (k_bucket_sort_big), the rest here
             KLAUNCH(k_bucket_sort, dim3(std::min(ncalls, 2048)), dim3(256), 0, st,
                     (const int32_t*)s_bpos.p, (const int32_t*)o_cc, (const int32_t*)blist,
-                    (const int32_t*)nblist, k1, k2, o_ids, 1);
+                    (const int32_t*)nblist, k1, k2, ids_dst, 1);
             if (ncand > 512)  // (no bucket past 512 keys otherwise)
               KLAUNCH(k_bucket_sort_big, dim3(std::min(ncalls, n_cu())), dim3(1024), 0, st,
                       (const int32_t*)s_bpos.p, (const int32_t*)o_cc, (const int32_t*)blist,
-                      (const int32_t*)nblist, (const OKey*)k1, k2, o_ids);
+                      (const int32_t*)nblist, (const OKey*)k1, k2, ids_dst);
           }
           // new undetermined list (in candidate order), scattered into the spare list
           // (same capacity) and swapped: no device copy
@@ -2538,9 +2553,12 @@ struct hge_engine {
       if (lazy) {  // delivered into the pinned order buffer (sized at hge_replay_prepare)
         if ((size_t)nrecv > pin_ord_cap) throw EngineError(HGE_ERR_INTERNAL, "order buffer below the ordered count");
         const int64_t td = now_ns();
-        if (nrecv) HIPCHK(hipMemcpyAsync(pin_ord, o_ids, 4 * (size_t)nrecv, hipMemcpyDeviceToHost, st));
-        sync();
-        stage_ms[5] = (float)((now_ns() - td) / 1e6);  // the delivery's wall time (hge_stage_times [5])
+        if (!wrote_direct && nrecv) {
+          HIPCHK(hipMemcpyAsync(pin_ord, o_ids, 4 * (size_t)nrecv, hipMemcpyDeviceToHost, st));
+          sync();
+        }
+        // the delivery's wall time after the sorts (hge_stage_times [5]; ~0 when written direct)
+        stage_ms[5] = (float)((now_ns() - td) / 1e6);
         cons_pin_n = nrecv;
       } else {
         consensus.insert(consensus.end(), ids, ids + nrecv);
