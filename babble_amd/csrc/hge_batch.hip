@@ -503,7 +503,9 @@ __global__ __launch_bounds__(NT) void kb_front(BT t) {
       zrow[dd][i] = P != INF ? FDg[((int64_t)dd * cc + P) * N + i] : INF;
     }
     __syncthreads();
-    // fss_c of every member (c fastest: a half wave reads one 128-byte row)
+    // fss_c of every member (c fastest: a half wave reads one 128-byte row; reading
+    // the run layout FDT here instead, with no FD rows built, took 1.82 -> 2.69 ms at
+    // 1,024 graphs)
     for (int e = tid; e < N * N; e += NT) {
       const int dd = e / N, c = e - (e / N) * N;
       int f = INF;
@@ -1660,7 +1662,7 @@ struct hge_batch {
     BCHK(hipEventRecord(ev[1], st));
     launch(kb_fd<NM>, G * N * (NM / FCW), t);
     BCHK(hipEventRecord(ev[2], st));
-    launch(kb_fdrows<NM>, G * N, t, 256);
+    launch(kb_fdrows<NM>, G * N, t, 256);  // rows for kb_front (kb_median reads the run layout)
     BCHK(hipEventRecord(ev[3], st));
     if (G > ncu) launch(kb_front<NM, 512>, G, t, 512);
     else launch(kb_front<NM, 1024>, G, t, 1024);

@@ -584,7 +584,10 @@ __global__ __launch_bounds__(256) void kb_median(BT t) {
   const int x = slot >= 0 ? t.chain[cb + cpos] : -1;
   int64_t tx = 0;
   if (bi >= 0) {
-    const int32_t* FDr = t.FD + (cb + cpos) * N;
+    // FD[x][dd] from the run layout FDT[g][dd][c][p]: a wave's lanes are consecutive
+    // positions p, so each dd is one coalesced load (no FD rows are built)
+    const int32_t* FDc = t.FDT + (int64_t)g * N * N * cc + (int64_t)c * cc + p;  // + dd * N * cc
+    const int64_t NC = (int64_t)N * cc;
     const int64_t* tschg = t.tsch + cb;
     const int32_t* wixr = t.WIX + (int64_t)(d.ro + bi) * N;
     const int64_t tsx = tschg[cpos];
@@ -599,15 +602,12 @@ __global__ __launch_bounds__(256) void kb_median(BT t) {
 #pragma unroll
     for (int b0 = 0; b0 < NM; b0 += MB) {
       int32_t fd[MB], wx[MB];
+#pragma unroll
+      for (int k = 0; k < MB; k++) fd[k] = b0 + k < N ? FDc[(b0 + k) * NC] : INF;
       if (vec) {
 #pragma unroll
         for (int k = 0; k < MB; k += 4) {
-          const int4 v = b0 + k < N ? *(const int4*)(FDr + b0 + k) : make_int4(INF, INF, INF, INF);
           const int4 w = b0 + k < N ? *(const int4*)(wixr + b0 + k) : make_int4(-1, -1, -1, -1);
-          fd[k] = v.x;
-          fd[k + 1] = v.y;
-          fd[k + 2] = v.z;
-          fd[k + 3] = v.w;
           wx[k] = w.x;
           wx[k + 1] = w.y;
           wx[k + 2] = w.z;
@@ -615,10 +615,7 @@ __global__ __launch_bounds__(256) void kb_median(BT t) {
         }
       } else {
 #pragma unroll
-        for (int k = 0; k < MB; k++) {
-          fd[k] = b0 + k < N ? FDr[b0 + k] : INF;
-          wx[k] = b0 + k < N ? wixr[b0 + k] : -1;
-        }
+        for (int k = 0; k < MB; k++) wx[k] = b0 + k < N ? wixr[b0 + k] : -1;
       }
       int64_t tq[MB];
       bool in[MB];
@@ -648,7 +645,7 @@ __global__ __launch_bounds__(256) void kb_median(BT t) {
     } else {  // the value whose rank among the m timestamps covers `want`, exact in 64 bits
       auto tv = [&](int dd, int64_t& v) -> bool {
         if (!((bF >> dd) & 1)) return false;
-        const int q = FDr[dd];
+        const int q = FDc[dd * NC];
         if (q == INF || q > wix[dd]) return false;
         v = tschg[(int64_t)dd * cc + q];
         return true;

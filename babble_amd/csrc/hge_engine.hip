@@ -19,6 +19,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/hge.h"
@@ -3523,7 +3524,16 @@ int hge_replay_fetch(hge_engine* h, int32_t* order_out, int64_t cap, int64_t* ca
     const int64_t a = std::min<int64_t>((int64_t)h->consensus.size(), std::max<int64_t>(cap, 0));
     if (a > 0) memcpy(order_out, h->consensus.data(), 4 * (size_t)a);
     const int64_t b = std::min<int64_t>(h->cons_pin_n, std::max<int64_t>(cap - a, 0));
-    if (b > 0) memcpy(order_out + a, h->pin_ord, 4 * (size_t)b);
+    // (one copy thread moves ~12 GB/s: a 40 MB order takes 8 in parallel)
+    const int nt = b >= (1 << 20) ? 8 : 1;
+    std::vector<std::thread> th;
+    for (int k = 1; k < nt; k++)
+      th.emplace_back([=] {
+        const int64_t lo = b * k / nt, hi = b * (k + 1) / nt;
+        memcpy(order_out + a + lo, h->pin_ord + lo, 4 * (size_t)(hi - lo));
+      });
+    if (b > 0) memcpy(order_out + a, h->pin_ord, 4 * (size_t)(b / nt));
+    for (auto& x : th) x.join();
   }
   if (call_counts_out)
     for (size_t c = 0; c < h->replay_counts.size(); c++) call_counts_out[c] = h->replay_counts[c];

@@ -121,23 +121,19 @@ def algorithmic_bytes(kernel, n, events, ordered, rounds=0):
 
 def pmc_traffic(config_key, kernel, launches_per_replay):
     """HBM bytes per launch of `kernel` in this configuration from the committed
-    rocprofv3 PMC passes (profiles/r05/pmc_traffic.json, else an earlier round's, made by
+    rocprofv3 PMC passes (profiles/r06/pmc_traffic.json, else an earlier round's, made by
     scripts/pmc_traffic.py on the GPU box): the kernel's bytes per replay over
     the launches that did work (k_la_sweep: the sweeps up to the quiet one), or None."""
-    pm = None
-    for rnd in ("r05", "r04", "r03", "r02"):  # the latest round's passes
+    name = kernel.strip("()").split("<")[0]
+    for rnd in ("r06", "r05", "r04", "r03", "r02"):  # the latest round's passes of this kernel
         try:
             pm = json.load(open(os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")))
-            break
         except (OSError, ValueError):
             continue
-    if pm is None:
-        return None
-    name = kernel.strip("()").split("<")[0]
-    v = pm.get("configs", {}).get(config_key, {}).get(name)
-    if not isinstance(v, dict) or "bytes_per_replay" not in v:
-        return None
-    return int(v["bytes_per_replay"] / max(launches_per_replay, 1))
+        v = pm.get("configs", {}).get(config_key, {}).get(name)
+        if isinstance(v, dict) and "bytes_per_replay" in v:
+            return int(v["bytes_per_replay"] / max(launches_per_replay, 1))
+    return None
 
 
 def golden_prefix(n, E, K, seed):
@@ -430,7 +426,8 @@ def mc_line(args, n, E, K, rank, world, local_rank, dist, cpu_s=10.0):
                    "ordered_per_step": tot_ordered,
                    "parallelism": f"replicas{world}: the batch split across {world} GPUs, no collective"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                     "traffic": pmc_traffic(f"mc_n{n}_e{E}_k{K}_g{args.graphs}" if world == 1 else None, dom, 1),
                      "algorithmic_bytes_per_launch": int(alg), "launch_ms": round(kms[dom], 4),
                      "hbm_kernels": hbm,
                      "path": {"bytes_per_event": 24 * n + 48,

@@ -19,7 +19,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-ROUND = "r05"  # the profiles/ directory this round's passes go to
+ROUND = "r06"  # the profiles/ directory this round's passes go to
 
 def run_pass(out_dir, counter, bench_args, parse_only=False):
     d = os.path.join(out_dir, counter.lower())
@@ -36,7 +36,7 @@ def run_pass(out_dir, counter, bench_args, parse_only=False):
         for row in csv.DictReader(open(f)):
             if row.get("Counter_Name") != counter:
                 continue
-            name = row["Kernel_Name"].split("(")[0].replace("void ", "").replace("hge::", "")
+            name = row["Kernel_Name"].split("(")[0].replace("void ", "").replace("hge::", "").replace("hgb::", "")
             name = name.split("<")[0].strip()
             v = float(row["Counter_Value"])
             s = per.setdefault(name, [0.0, 0])
@@ -54,7 +54,8 @@ def main():
     res = {}
     # every replay fills the chain table once (k_chain_fill): the replay count
     # (k_reset_rounds also runs at prepare time)
-    replays = max(1, fetch.get("k_chain_fill", [0.0, 0])[1])
+    # (the batch engine: kb_coords, once per batch replay)
+    replays = max(1, fetch.get("k_chain_fill", fetch.get("kb_coords", [0.0, 0]))[1])
     for name in sorted(set(fetch) | set(write)):
         fb, fl = fetch.get(name, [0.0, 0])
         wb, wl = write.get(name, [0.0, 0])
