@@ -168,21 +168,20 @@ __device__ __forceinline__ void lds_barrier() {
 // undetermined list kept in LDS.
 
 // lastAncestors (InitEventCoordinates, hashgraph.go:399-463): in insertion order,
-// LA[x] = max(LA[sp], LA[op]) with LA[x][creator] = index.  One 256-thread
-// workgroup per graph, SL = 256 / NM event slots of NM columns.  The events go in
-// chunks of 64; a step takes the longest run of consecutive events none of which
-// has a parent inside the run (an event's parents precede it, so the run's rows
-// depend only on rows already final) and computes their rows together.  At N = 32
-// runs average ~4.5 events (a parent lands among the last j events with
-// probability ~j/32 per parent).  A parent's row comes from the chunk's LDS ring
-// (written once per slot, so a step needs one barrier, LDS-scoped: the row stores
-// to HBM are never waited for inside a chunk), from the snapshot of the chain heads
-// taken at the chunk's start (the self-parent is its creator's head, admission
-// "Self-parent not last known", hashgraph.go:390-393; the other-parent nearly
-// always is), or from HBM behind the chunk boundary's full barrier.
-template <int NM>
-__global__ __launch_bounds__(256) void kb_coords(BT t) {
-  constexpr int SL = 256 / NM;
+// LA[x] = max(LA[sp], LA[op]) with LA[x][creator] = index.  One workgroup per graph
+// (NT threads: SL = NT / NM event slots of NM columns).  The events go in chunks of
+// 64; wave 0 gives each event of a chunk a level (one above its in-chunk parents),
+// and a step computes up to SL events of one level together (their rows depend only
+// on rows already final).  A parent's row comes from the chunk's LDS ring (written
+// once per slot, so a step needs one barrier, LDS-scoped: the row stores to HBM are
+// never waited for inside a chunk), from the snapshot of the chain heads taken at the
+// chunk's start (the self-parent is its creator's head, admission "Self-parent not
+// last known", hashgraph.go:390-393; the other-parent nearly always is), or from HBM
+// behind the chunk boundary's full barrier.  Wave 0 loads the next chunk's event
+// records while this chunk's steps run.
+template <int NM, int NT>
+__global__ __launch_bounds__(NT) void kb_coords(BT t) {
+  constexpr int SL = NT / NM;  // event slots per step
   const GDesc d = t.gd[blockIdx.x];
   const int N = t.N, tid = threadIdx.x, s = tid / NM, k = tid - (tid / NM) * NM;
   // rows 0..63: the chunk's ring; 64 + c: chain c's head row as of the chunk's start
@@ -192,10 +191,11 @@ __global__ __launch_bounds__(256) void kb_coords(BT t) {
   // -2 HBM), creator, index; the parents' ids for the HBM case
   __shared__ int4 einfo[64];
   __shared__ int32_t msp[64], mop[64];
-  __shared__ int32_t gst[65];   // the chunk's runs: [gst[i], gst[i + 1])
-  __shared__ int32_t clast[NM];  // the chunk's last event per chain (-1)
+  __shared__ int32_t ord[64];     // the chunk's events by level
+  __shared__ int32_t gst[130];    // the steps: ord[gst[i] .. gst[i + 1])
+  __shared__ int32_t clast[NM];   // the chunk's last event per chain (-1)
   __shared__ int s_ng;
-  for (int i = tid; i < NM * NM; i += 256) rows[64 + i / NM][i - (i / NM) * NM] = -1;
+  for (int i = tid; i < NM * NM; i += NT) rows[64 + i / NM][i - (i / NM) * NM] = -1;
   if (tid < NM) headid[tid] = -1;
   __syncthreads();
   int32_t* LA = t.LA + d.eo * N;
@@ -225,16 +225,30 @@ __global__ __launch_bounds__(256) void kb_coords(BT t) {
       if (tid < NM) clast[tid] = -1;
       wsync();
       if (on) atomicMax(&clast[cr], tid);
-      // the runs, greedily from the chunk's start: a run from u takes the events
-      // after u up to the first with a parent at or past base + u (at most SL)
-      const int pm = max(sp, op);
-      int u = 0, ng = 0;
-      while (u < cnt) {
-        const uint64_t bad = ballot(tid > u && (tid >= cnt || pm >= base + u));
-        const int lim = bad ? __ffsll((unsigned long long)bad) - 1 : 64;
-        if (tid == 0) gst[ng] = u;
-        ng++;
-        u += min(lim - u, SL);
+      // levels inside the chunk: one above the in-chunk parents (parents precede
+      // their children, so the passes settle after the chunk's depth); the events of
+      // a level are independent and take the steps of that level, SL at a time
+      const int ps = on && sp >= base ? sp - base : -1, po = on && op >= base ? op - base : -1;
+      int lvl = 0;
+      while (true) {
+        const int a = __shfl(lvl, ps < 0 ? 0 : ps), b = __shfl(lvl, po < 0 ? 0 : po);
+        const int nl = max(ps >= 0 ? a + 1 : 0, po >= 0 ? b + 1 : 0);
+        const bool ch = nl != lvl;
+        lvl = nl;
+        if (!ballot(ch)) break;
+      }
+      const int maxl = wave_max(on ? lvl : 0);
+      const uint64_t below = tid ? (~0ull >> (64 - tid)) : 0ull;
+      int pos = 0, ng = 0;
+      for (int l = 0; l <= maxl; l++) {
+        const uint64_t m = ballot(on && lvl == l);
+        const int c_l = __popcll(m);
+        if (on && lvl == l) ord[pos + __popcll(m & below)] = tid;
+        for (int q = 0; q < c_l; q += SL) {
+          if (tid == 0) gst[ng] = pos + q;
+          ng++;
+        }
+        pos += c_l;
       }
       if (tid == 0) {
         gst[ng] = cnt;
@@ -244,15 +258,12 @@ __global__ __launch_bounds__(256) void kb_coords(BT t) {
     }
     __syncthreads();
     const int ng = s_ng;
-    int u = gst[0], un = gst[1];
-    int4 ei = einfo[min(u + s, 63)];
     for (int gi = 0; gi < ng; gi++) {
-      const int e = u + s;
-      const bool on = e < un && k < N;
-      // the next step's run and record, read ahead (nothing this step writes)
-      const int u2 = un, un2 = gi + 2 <= ng ? gst[min(gi + 2, ng)] : un;
-      const int4 ei2 = einfo[min(u2 + s, 63)];
+      const int q0 = gst[gi], q1 = gst[gi + 1];
+      const bool on = q0 + s < q1 && k < N;
       if (on) {
+        const int e = ord[q0 + s];
+        const int4 ei = einfo[e];
         const int a = ei.x >= 0 ? rows[ei.x][k] : ei.x == -1 ? -1 : ld(&LA[(int64_t)msp[e] * N + k]);
         const int b = ei.y >= 0 ? rows[ei.y][k] : ei.y == -1 ? -1 : ld(&LA[(int64_t)mop[e] * N + k]);
         const int val = k == ei.z ? ei.w : max(a, b);
@@ -260,9 +271,6 @@ __global__ __launch_bounds__(256) void kb_coords(BT t) {
         LA[(int64_t)(base + e) * N + k] = val;
       }
       lds_barrier();
-      u = u2;
-      un = un2;
-      ei = ei2;
     }
     // the heads after the chunk
     if (k < N)
@@ -1658,7 +1666,9 @@ struct hge_batch {
 
   template <int NM>
   void run_stages(int G, const BT& t) {
-    launch(kb_coords<NM>, G, t, 256);
+    // a workgroup of 1,024 threads per graph while two fit a CU, else 512
+    if (G <= 2 * ncu) launch(kb_coords<NM, 1024>, G, t, 1024);
+    else launch(kb_coords<NM, 512>, G, t, 512);
     BCHK(hipEventRecord(ev[1], st));
     launch(kb_fd<NM>, G * N * (NM / FCW), t);
     BCHK(hipEventRecord(ev[2], st));
