@@ -407,27 +407,30 @@ __global__ __launch_bounds__(256) void kb_fdrows(BT t) {
 // see bits LA[x][d] >= index(w) (the vote adjacency of DecideFame).
 // k-th smallest (1-based) of M register values: bitonic network, then a select
 template <int M>
-__device__ __forceinline__ int kth_smallest(int (&v)[M], int k) {
+__device__ __forceinline__ int kth_smallest(const int (&v)[M], int k) {
+  // bisection over the value range: the smallest t with #{v <= t} >= k (INF when
+  // fewer than k values are finite); positions span a few hundred, so ~9 counting
+  // passes of M compares, register-light (a bitonic network held M values plus its
+  // temporaries, ~88 VGPRs in kb_front: one 1,024-thread workgroup per CU)
+  int lo = INF, hi = INT32_MIN, fin = 0;
 #pragma unroll
-  for (int size = 2; size <= M; size <<= 1)
+  for (int i = 0; i < M; i++) {
+    if (v[i] != INF) {
+      lo = min(lo, v[i]);
+      hi = max(hi, v[i]);
+      fin++;
+    }
+  }
+  if (fin < k) return INF;
+  while (lo < hi) {
+    const int mid = lo + ((hi - lo) >> 1);
+    int cnt = 0;
 #pragma unroll
-    for (int stride = size >> 1; stride > 0; stride >>= 1)
-#pragma unroll
-      for (int i = 0; i < M; i++) {
-        const int j = i ^ stride;
-        if (j > i) {
-          const bool up = (i & size) == 0;
-          const int a = v[i], b = v[j];
-          v[i] = up ? min(a, b) : max(a, b);
-          v[j] = up ? max(a, b) : min(a, b);
-        }
-      }
-  // v is ascending: v[k-1] is the maximum of v[0..k-1] (a select chain on i == k-1
-  // is turned into a dynamically indexed scratch array)
-  int r = INT32_MIN;
-#pragma unroll
-  for (int i = 0; i < M; i++) r = max(r, i < k ? v[i] : INT32_MIN);
-  return r;
+    for (int i = 0; i < M; i++) cnt += v[i] <= mid;
+    if (cnt >= k) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo;
 }
 
 // NT: 1024 threads while the graphs fit one workgroup per CU; 512 past that, so two
