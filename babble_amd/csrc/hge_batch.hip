@@ -405,7 +405,6 @@ __global__ __launch_bounds__(256) void kb_fdrows(BT t) {
 // the positions [C_r[c], C_{r+1}[c]), the first of them the witness; a witness's
 // strongly-see bits over round r-1's witnesses are fss_c(w) <= its position, its
 // see bits LA[x][d] >= index(w) (the vote adjacency of DecideFame).
-// k-th smallest (1-based) of M register values: bitonic network, then a select
 template <int M>
 __device__ __forceinline__ int kth_smallest(const int (&v)[M], int k) {
   // bisection over the value range: the smallest t with #{v <= t} >= k (INF when
@@ -1677,7 +1676,8 @@ struct hge_batch {
     BCHK(hipEventRecord(ev[2], st));
     launch(kb_fdrows<NM>, G * N, t, 256);  // rows for kb_front (kb_median reads the run layout)
     BCHK(hipEventRecord(ev[3], st));
-    if (G > ncu) launch(kb_front<NM, 512>, G, t, 512);
+    if (G > 2 * ncu) launch(kb_front<NM, 256>, G, t, 256);
+    else if (G > ncu) launch(kb_front<NM, 512>, G, t, 512);
     else launch(kb_front<NM, 1024>, G, t, 1024);
     BCHK(hipEventRecord(ev[4], st));
     if (serial) {  // every graph through kb_consensus, after the run's readback
