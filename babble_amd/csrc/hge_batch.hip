@@ -102,7 +102,7 @@ struct BT {
   int32_t *Rc, *xcall;   // [co + c] Rounds() after call c's DivideRounds; [eo + x] x's insertion call
   int32_t* rfirst;       // [ro + r] the first call with R_c >= r (r <= the last call's R)
   uint64_t* arr;         // [eo + k] the witnesses in insertion order: call << 32 | round << 8 | creator
-  uint64_t* Dp;          // [((co + c) * BNS + s) * 2 + {0, 1}] DecideFame's decided / famous masks
+  uint64_t* Dp;          // [((co + c) * NS + s) * 2 + {0, 1}], NS <= BNS DecideFame's decided / famous masks
   int32_t* gx;           // [g][16] per-graph internals (GX_*)
   int4* ivh;             // [(ro + r) * BVCAP + k] receive intervals: first call, end call, theta slot
   uint64_t* ivF;         // ... and their famous witnesses
@@ -1685,10 +1685,12 @@ struct hge_batch {
       return;
     }
     launch(kb_prep<NM>, G, t, 1024);
-    hipLaunchKernelGGL(kb_pairs<NM>, dim3(8, (unsigned)G), dim3(256), 0, st, t);
+    if (G > ncu) hipLaunchKernelGGL((kb_pairs<NM, 2>), dim3(8, (unsigned)G), dim3(256), 0, st, t);
+    else hipLaunchKernelGGL((kb_pairs<NM, 3>), dim3(8, (unsigned)G), dim3(256), 0, st, t);
     BCHK(hipGetLastError());
     BCHK(hipEventRecord(ev[5], st));
-    launch(kb_fold<NM>, G, t, 64);
+    if (G > ncu) launch((kb_fold<NM, 2>), G, t, 64);
+    else launch((kb_fold<NM, 3>), G, t, 64);
     launch(kb_theta<NM>, G, t, 256);
     BCHK(hipEventRecord(ev[6], st));
     if (Emax > 0) {

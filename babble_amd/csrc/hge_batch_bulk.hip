@@ -28,7 +28,7 @@
 // A graph the fold cannot hold (more than 64 * FRS rounds, an interval table past
 // its capacity) is flagged in scal[7] and replayed by kb_consensus.
 
-constexpr int BNS = 3;      // DecideFame pairs per call: rounds R_c - 2 - s, s < BNS
+constexpr int BNS = 3;      // at most BNS DecideFame pairs per call kept: rounds R_c - 2 - s, s < NS <= BNS
 constexpr int BVCAP = 4;    // receive intervals per round
 constexpr int BICAP = 512;  // receive intervals per graph
 constexpr int FRS = 4;      // rounds per lane in kb_fold (64 * FRS rounds)
@@ -215,7 +215,7 @@ struct GSrc {
   __device__ uint64_t ss(int j, int y) const { return t.ssb[(ro + j) * N + y]; }
   __device__ bool coin(int j, int y) const { return t.WCOIN[(ro + j) * N + y] != 0; }
 };
-// rounds i0 .. i0 + BNS staged in LDS
+// rounds i0 .. i0 + NS staged in LDS
 template <int NM>
 struct LSrc {
   const int32_t (*w)[NM];
@@ -230,13 +230,15 @@ struct LSrc {
 };
 
 // DecideFame's pairs by round: workgroup (k, g) takes graph g's rounds i = k, k +
-// gridDim.x, ..., stages the witness rows of rounds i .. i + BNS in LDS and decides
-// round i at every call whose window holds it (R_c in [i + 3, i + 1 + BNS], a
+// gridDim.x, ..., stages the witness rows of rounds i .. i + NS in LDS and decides
+// round i at every call whose window holds it (R_c in [i + 3, i + 1 + NS], a
 // range of calls: R_c never decreases), one wave per call.  Round R_c - 2 (s = 0)
 // sees one voting round only (diff = 1 sets votes, decides nothing): no pair.
-template <int NM>
+// NS = 3 while graphs fit one per CU; past that NS = 2 (s = 2 is ~3 pairs per graph,
+// computed inline by kb_fold, cheaper than a third of kb_pairs' work once the chip is full).
+template <int NM, int NS>
 __global__ __launch_bounds__(256) void kb_pairs(BT t) {
-  constexpr int RB = BNS + 1;
+  constexpr int RB = NS + 1;
   const int g = blockIdx.y;
   if (t.scal[(int64_t)g * 8 + 6]) return;
   const GDesc d = t.gd[g];
@@ -261,7 +263,7 @@ __global__ __launch_bounds__(256) void kb_pairs(BT t) {
     }
     // s = 0 (j = i + 1 only: votes, no decision) is never computed
     const int lo = i + 3 <= Rf ? t.rfirst[d.ro + i + 3] : d.K;
-    const int hi = i + 2 + BNS <= Rf ? t.rfirst[d.ro + i + 2 + BNS] : d.K;
+    const int hi = i + 2 + NS <= Rf ? t.rfirst[d.ro + i + 2 + NS] : d.K;
     __syncthreads();
     LSrc<NM> sr = src;
     sr.i0 = i;
@@ -276,7 +278,7 @@ __global__ __launch_bounds__(256) void kb_pairs(BT t) {
       uint64_t dec, val;
       fame_pair<NM>(t, sr, i, n_c, R, dec, val);
       if (okc && (tid & (64 / HV - 1)) == 0) {
-        const int64_t p = (int64_t)(d.co + c) * BNS + (R - 2 - i);
+        const int64_t p = (int64_t)(d.co + c) * NS + (R - 2 - i);
         t.Dp[2 * p] = dec;
         t.Dp[2 * p + 1] = val;
       }
@@ -297,7 +299,7 @@ __global__ __launch_bounds__(256) void kb_pairs(BT t) {
 // interval [c, next arrival) with famous set F is written when the round is decided,
 // and setLastConsensusRound (hashgraph.go:666-673) follows the loop's highest
 // decided round.
-template <int NM>
+template <int NM, int NS>
 __global__ __launch_bounds__(64) void kb_fold(BT t) {
   constexpr int RL = 64 * FRS;  // rounds held
   const int g = blockIdx.x;
@@ -331,7 +333,7 @@ __global__ __launch_bounds__(64) void kb_fold(BT t) {
   }
   int LCR = -1, lcr_call = -1, nth = 0, miss = 0;
   int c = -1, c0 = -INF, Rreg = 0, Nreg = 0;
-  uint64_t Dd[BNS], Dv[BNS];
+  uint64_t Dd[NS], Dv[NS];
   while (true) {
     const int need = LCR + 4;  // the next call with a round to decide has R >= LCR + 4
     if (need > Rf) break;
@@ -344,8 +346,8 @@ __global__ __launch_bounds__(64) void kb_fold(BT t) {
       Rreg = on ? t.Rc[d.co + cl] : 0;
       Nreg = on ? (int)t.calls[d.co + cl] : 0;
 #pragma unroll
-      for (int s = 0; s < BNS; s++) {
-        const int64_t p = ((int64_t)(d.co + cl)) * BNS + s;
+      for (int s = 0; s < NS; s++) {
+        const int64_t p = ((int64_t)(d.co + cl)) * NS + s;
         const bool ok = on && s > 0 && Rreg - 2 - s >= 0;
         Dd[s] = ok ? t.Dp[2 * p] : 0;
         Dv[s] = ok ? t.Dp[2 * p + 1] : 0;
@@ -356,9 +358,9 @@ __global__ __launch_bounds__(64) void kb_fold(BT t) {
     for (int i = LCR + 1; i <= R - 3; i++) {
       const int s = R - 2 - i;
       uint64_t dec = 0, v = 0;
-      if (s < BNS) {
+      if (s < NS) {
 #pragma unroll
-        for (int q = 0; q < BNS; q++)
+        for (int q = 0; q < NS; q++)
           if (q == s) {
             dec = rl64(Dd[q], cc);
             v = rl64(Dv[q], cc);
