@@ -119,6 +119,7 @@ struct BT {
   int4* wl;              // the non-empty buckets (graph, size, offset in the graph's order)
   int32_t* wlc;          // their count
   int64_t* gctx;         // [g] ConsensusTransactions
+  int2* cinf;            // [eo + x] kb_levels' records for kb_coords
 };
 
 __device__ __forceinline__ int rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -168,19 +169,119 @@ __device__ __forceinline__ void lds_barrier() {
 // undetermined list kept in LDS.
 
 // lastAncestors (InitEventCoordinates, hashgraph.go:399-463): in insertion order,
-// LA[x] = max(LA[sp], LA[op]) with LA[x][creator] = index.  One workgroup per graph
-// (NT threads: SL = NT / NM event slots of NM columns).  The events go in chunks of
-// 64; wave 0 gives each event of a chunk a level (one above its in-chunk parents),
-// and a step computes up to SL events of one level together (their rows depend only
-// on rows already final).  A parent's row comes from the chunk's LDS ring (written
-// once per slot, so a step needs one barrier, LDS-scoped: the row stores to HBM are
-// never waited for inside a chunk), from the snapshot of the chain heads taken at the
-// chunk's start (the self-parent is its creator's head, admission "Self-parent not
-// last known", hashgraph.go:390-393; the other-parent nearly always is), or from HBM
-// behind the chunk boundary's full barrier.  Wave 0 loads the next chunk's event
-// records while this chunk's steps run.
-template <int NM, int NT>
+// LA[x] = max(LA[sp], LA[op]) with LA[x][creator] = index.  The events go in chunks of
+// 64.  kb_levels gives every event of every chunk, all graphs at once, its level inside
+// its chunk (one above its in-chunk parents) and its parents' row sources; kb_coords
+// (one workgroup per graph) then walks the chunks, one step per level.
+//
+// kb_levels: one wave per (graph, chunk), lane = event.  A parent's row source is a
+// row of the chunk's LDS ring (the parent is in the chunk), the chain head as of the
+// chunk's start (the parent is its chain's last event before the chunk: the
+// self-parent always is, admission "Self-parent not last known", hashgraph.go:390-393,
+// and the other-parent nearly always), or HBM.  cinf[x] = {srcA | srcB << 8 |
+// level << 16 | last << 23 | levels << 24, creator | index << 8}; last: x is its
+// chain's last event in the chunk (its row becomes that chain's head).
+__global__ __launch_bounds__(256) void kb_levels(BT t) {
+  const int g = blockIdx.y, lane = threadIdx.x & 63;
+  const GDesc d = t.gd[g];
+  const int base = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+  if (base >= d.E) return;
+  const int N = t.N, cc = t.ccap, i = base + lane;
+  const bool on = i < d.E;
+  const int sp = on ? t.sp[d.eo + i] : -1, op = on ? t.op[d.eo + i] : -1;
+  const int cr = on ? t.cr[d.eo + i] : 0, oc = on ? t.oc[d.eo + i] : 0, ix = on ? t.ix[d.eo + i] : 0;
+  const int32_t* chg = t.chain + (int64_t)g * N * cc;
+  const int32_t* lng = t.clen + (int64_t)g * N;
+  // the event after position q of chain c (INF: none)
+  auto next = [&](int c, int q) { return q + 1 < lng[c] ? chg[(int64_t)c * cc + q + 1] : INF; };
+  auto src = [&](int p, int c) -> int {
+    if (p < 0) return -1;
+    if (p >= base) return p - base;
+    return next(c, t.ix[d.eo + p]) >= base ? 64 + c : -2;
+  };
+  const int sa = src(sp, cr), sb = src(op, oc);
+  const bool last = on && next(cr, ix) >= base + 64;
+  const int ps = on && sp >= base ? sp - base : -1, po = on && op >= base ? op - base : -1;
+  int lvl = 0;
+  while (true) {  // parents precede their children: settles after the chunk's depth
+    const int x = __shfl(lvl, ps < 0 ? 0 : ps), y = __shfl(lvl, po < 0 ? 0 : po);
+    const int nl = max(ps >= 0 ? x + 1 : 0, po >= 0 ? y + 1 : 0);
+    const bool ch = nl != lvl;
+    lvl = nl;
+    if (!ballot(ch)) break;
+  }
+  const int nlev = wave_max(on ? lvl : 0) + 1;
+  if (on)
+    t.cinf[d.eo + i] = make_int2((sa & 0xFF) | (sb & 0xFF) << 8 | lvl << 16 | (last ? 1 << 23 : 0) | nlev << 24,
+                                 cr | ix << 8);
+}
+
+// kb_coords: one workgroup per graph, NT threads; thread (s, k) owns column k of the
+// chunk's events s, s + SL, ... (SL = NT / NM), their kb_levels records in registers
+// (the next chunk's loaded while this one runs).  A step computes one level: every
+// event of it reads its parents' rows from LDS (ring or heads) or HBM and writes its
+// own; one LDS-scoped barrier per step (the row stores to HBM are never waited for
+// inside a chunk).  After the chunk the chains' last events' rows become the heads,
+// behind a full barrier (which also completes the chunk's HBM stores).
+// LV = false (past two graphs per CU: the chip is full, and kb_levels' extra pass
+// measured 1.04 -> 1.42 ms at 1,024 graphs), the earlier form: wave 0 levels each chunk
+// itself, and a step computes up to SL events of one level together (their rows depend
+// only on rows already final).  The parents' row sources are found the same way (the
+// heads' ids kept in LDS); wave 0 loads the next chunk's event records while this
+// chunk's steps run.
+template <int NM, int NT, bool LV>
 __global__ __launch_bounds__(NT) void kb_coords(BT t) {
+  if constexpr (LV) {
+  constexpr int SL = NT / NM, EPT = 64 / SL;
+  const GDesc d = t.gd[blockIdx.x];
+  const int N = t.N, tid = threadIdx.x, s = tid / NM, k = tid - (tid / NM) * NM;
+  // rows 0..63: the chunk's ring; 64 + c: chain c's head row as of the chunk's start
+  __shared__ int32_t rows[64 + NM][NM];
+  for (int i = tid; i < NM * NM; i += NT) rows[64 + i / NM][i - (i / NM) * NM] = -1;
+  __syncthreads();
+  int32_t* LA = t.LA + d.eo * N;
+  const int2* ci = t.cinf + d.eo;
+  int2 nx[EPT];
+  int nlv = 0;
+  auto fetch = [&](int b) {
+#pragma unroll
+    for (int u = 0; u < EPT; u++) {
+      const int e = b + s + SL * u;
+      nx[u] = e < d.E ? ci[e] : make_int2(0, 0);
+    }
+    nlv = b < d.E ? ci[b].x >> 24 : 0;  // the chunk's level count (its first event's record)
+  };
+  fetch(0);
+  for (int base = 0; base < d.E; base += 64) {
+    int2 in[EPT];
+#pragma unroll
+    for (int u = 0; u < EPT; u++) in[u] = nx[u];
+    const int nlev = nlv;
+    if (base + 64 < d.E) fetch(base + 64);
+    int val[EPT];
+    for (int l = 0; l < nlev; l++) {
+#pragma unroll
+      for (int u = 0; u < EPT; u++) {
+        const int e = s + SL * u;
+        if (base + e < d.E && k < N && ((in[u].x >> 16) & 63) == l) {
+          const int sa = (int)(int8_t)(in[u].x & 0xFF), sb = (int)(int8_t)((in[u].x >> 8) & 0xFF);
+          const int a = sa >= 0 ? rows[sa][k] : sa == -1 ? -1 : ld(&LA[(int64_t)t.sp[d.eo + base + e] * N + k]);
+          const int b = sb >= 0 ? rows[sb][k] : sb == -1 ? -1 : ld(&LA[(int64_t)t.op[d.eo + base + e] * N + k]);
+          const int v = k == (in[u].y & 0xFF) ? in[u].y >> 8 : max(a, b);
+          val[u] = v;
+          rows[e][k] = v;
+          LA[(int64_t)(base + e) * N + k] = v;
+        }
+      }
+      lds_barrier();
+    }
+    // the heads after the chunk (every read of the old heads is behind the last barrier)
+#pragma unroll
+    for (int u = 0; u < EPT; u++)
+      if (base + s + SL * u < d.E && k < N && (in[u].x >> 23 & 1)) rows[64 + (in[u].y & 0xFF)][k] = val[u];
+    __syncthreads();  // also: the chunk's row stores are complete before the next one reads HBM
+  }
+  } else {
   constexpr int SL = NT / NM;  // event slots per step
   const GDesc d = t.gd[blockIdx.x];
   const int N = t.N, tid = threadIdx.x, s = tid / NM, k = tid - (tid / NM) * NM;
@@ -281,7 +382,9 @@ __global__ __launch_bounds__(NT) void kb_coords(BT t) {
     if (tid < N && clast[tid] >= 0) headid[tid] = base + clast[tid];
     __syncthreads();  // also: the chunk's row stores are complete before the next one reads HBM
   }
+  }
 }
+
 
 // ---------------------------------------------------------------------------
 // firstDescendants in run layout (UpdateAncestorFirstDescendant, hashgraph.go:466-494):
@@ -1348,6 +1451,7 @@ struct hge_batch {
   Buf<uint64_t> d_arr, d_Dp, d_ivF, d_thF;
   Buf<int4> d_ivh;
   Buf<int4> d_wl;
+  Buf<int2> d_cinf;
   Buf<int64_t> d_gctx, d_ctsch;
   int Emax = 0;
   int64_t n_fallback = 0;  // graphs the last run replayed through kb_consensus
@@ -1367,6 +1471,7 @@ struct hge_batch {
     for (auto* b : {&d_arr, &d_Dp, &d_ivF, &d_thF}) b->free_();
     d_ivh.free_();
     d_wl.free_();
+    d_cinf.free_();
     d_gctx.free_();
     d_ctsch.free_();
     d_coin.free_();
@@ -1576,6 +1681,7 @@ struct hge_batch {
     d_wl.need(K1);
     d_wlc.need(1);
     d_gctx.need(G);
+    d_cinf.need(E1);
     BCHK(hipStreamSynchronize(st));
     staged = true;
   }
@@ -1656,6 +1762,7 @@ struct hge_batch {
     t.wl = d_wl.p;
     t.wlc = d_wlc.p;
     t.gctx = d_gctx.p;
+    t.cinf = d_cinf.p;
     return t;
   }
 
@@ -1669,8 +1776,17 @@ struct hge_batch {
   template <int NM>
   void run_stages(int G, const BT& t) {
     // a workgroup of 1,024 threads per graph while two fit a CU, else 512
-    if (G <= 2 * ncu) launch(kb_coords<NM, 1024>, G, t, 1024);
-    else launch(kb_coords<NM, 512>, G, t, 512);
+    // 1,024 threads per graph and the kb_levels pass while two graphs fit a CU, else
+    // 512 threads levelling their own chunks
+    if (G <= 2 * ncu) {
+      if (Emax > 0) {
+        hipLaunchKernelGGL(kb_levels, dim3((unsigned)((Emax + 255) / 256), (unsigned)G), dim3(256), 0, st, t);
+        BCHK(hipGetLastError());
+      }
+      launch(kb_coords<NM, 1024, true>, G, t, 1024);
+    } else {
+      launch(kb_coords<NM, 512, false>, G, t, 512);
+    }
     BCHK(hipEventRecord(ev[1], st));
     launch(kb_fd<NM>, G * N * (NM / FCW), t);
     BCHK(hipEventRecord(ev[2], st));
@@ -1685,11 +1801,11 @@ struct hge_batch {
       return;
     }
     launch(kb_prep<NM>, G, t, 1024);
-    if (G > ncu) hipLaunchKernelGGL((kb_pairs<NM, 2>), dim3(8, (unsigned)G), dim3(256), 0, st, t);
+    if (G > 2 * ncu) hipLaunchKernelGGL((kb_pairs<NM, 2>), dim3(8, (unsigned)G), dim3(256), 0, st, t);
     else hipLaunchKernelGGL((kb_pairs<NM, 3>), dim3(8, (unsigned)G), dim3(256), 0, st, t);
     BCHK(hipGetLastError());
     BCHK(hipEventRecord(ev[5], st));
-    if (G > ncu) launch((kb_fold<NM, 2>), G, t, 64);
+    if (G > 2 * ncu) launch((kb_fold<NM, 2>), G, t, 64);
     else launch((kb_fold<NM, 3>), G, t, 64);
     launch(kb_theta<NM>, G, t, 256);
     BCHK(hipEventRecord(ev[6], st));

@@ -234,7 +234,7 @@ struct LSrc {
 // round i at every call whose window holds it (R_c in [i + 3, i + 1 + NS], a
 // range of calls: R_c never decreases), one wave per call.  Round R_c - 2 (s = 0)
 // sees one voting round only (diff = 1 sets votes, decides nothing): no pair.
-// NS = 3 while graphs fit one per CU; past that NS = 2 (s = 2 is ~3 pairs per graph,
+// NS = 3 while two graphs fit a CU; past that NS = 2 (s = 2 is ~3 pairs per graph,
 // computed inline by kb_fold, cheaper than a third of kb_pairs' work once the chip is full).
 template <int NM, int NS>
 __global__ __launch_bounds__(256) void kb_pairs(BT t) {

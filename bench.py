@@ -438,7 +438,7 @@ def mc_line(args, n, E, K, rank, world, local_rank, dist, cpu_s=10.0):
         "ingest_host_ms": round(ingest_s * 1e3, 2),
         "admission_ms": round(admission_s * 1e3, 2),
         "kernels_ms_per_replay": {k_: round(v_, 4) for k_, v_ in sorted(kms.items(), key=lambda kv: -kv[1])},
-        "kernel_launches_per_replay": {"kb_coords": 1, "kb_fd": 1, "kb_fdrows": 1, "kb_front": 1, "kb_fame": 2,
+        "kernel_launches_per_replay": {"kb_coords": 1 if per > 512 else 2, "kb_fd": 1, "kb_fdrows": 1, "kb_front": 1, "kb_fame": 2,
                                        "kb_fold": 2, "kb_receive": 1, "kb_order": 2},
         "graphs_replayed_call_by_call": batch.fallbacks(),
     }
