@@ -604,10 +604,7 @@ __global__ void __launch_bounds__(256) k_fd_transpose_ts(Tables t, const FT* FDT
     // read phase: lane tx walks row q = p0 + tx (its own timestamp is one load), all
     // 16 FDT loads of a thread in flight, then all 16 timestamp gathers
     const int64_t own = t.tsch[(size_t)a * ccap + min(p0 + tx, pend - 1)];
-#ifndef HGE_FDTS_CH
-#define HGE_FDTS_CH 16
-#endif
-    constexpr int CH = HGE_FDTS_CH;  // rows in flight per thread
+    constexpr int CH = 16;  // rows in flight per thread
 #pragma unroll
     for (int h = 0; h < 16; h += CH) {
       int kv[CH];

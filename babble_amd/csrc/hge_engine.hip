@@ -2828,7 +2828,7 @@ struct hge_engine {
                        s_segcall.p, s_segdec.p, s_segfws.p, s_theta.p, s_recv.p, s_rr.p,         \
                        s_cts.p, bseg);                                                           \
     if (wmed)                                                                                    \
-      KLAUNCH(k_median_wave<B>, dim3(div_up(ncand, 4 * HGE_MW_E)), dim3(256), 0, st, tables(),              \
+      KLAUNCH(k_median_wave<B>, dim3(div_up(ncand, 4 * MED_EPW)), dim3(256), 0, st, tables(),              \
               ident ? (const int32_t*)nullptr : cand, ncand, s_recv.p, s_rr.p, bseg, s_segfws.p,  \
               s_cts.p);                                                                          \
     break;

@@ -2358,6 +2358,8 @@ __global__ void __launch_bounds__(256) k_witness_la(Tables t, int rr_lo) {
 // Every per-witness input is a coalesced row: the "sees x" thresholds
 // WLA[rr][cx][.] (k_witness_la) and the timestamp offsets FDTD[x][.] (k_fd_transpose_ts),
 // instead of 2N scattered gathers per event.
+// events per k_median_wave wave (the grid is sized from it)
+constexpr int MED_EPW = 1;
 template <int VPL>
 __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* cand, int ncand,
                                                      const int32_t* recv_call, const int32_t* rr_in,
@@ -2366,10 +2368,7 @@ __global__ void __launch_bounds__(256) k_median_wave(Tables t, const int32_t* ca
   // MW_E events per wave (candidates q0 + e * nw, nw = the grid's wave count; 1 measured
   // fastest once the select became cheap: 6.36 vs 6.62 ms at 2, 8.19 at 3): all
   // their loads are in flight together before the first select
-#ifndef HGE_MW_E
-#define HGE_MW_E 1
-#endif
-  constexpr int MW_E = HGE_MW_E;
+  constexpr int MW_E = MED_EPW;
   __shared__ __attribute__((aligned(16))) int s_mhist[4][256];  // each wave's select bins
   const int nw = gridDim.x * 4;
   // (the XCD-aware order of k_fame_decide measured 0.2 ms slower here, and a
