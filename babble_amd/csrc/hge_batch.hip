@@ -386,6 +386,30 @@ __global__ __launch_bounds__(NT) void kb_coords(BT t) {
 }
 
 
+// The per-replay resets of the pooled tables in one launch (14 stream fills cost ~5 µs
+// of launch each, ~70 µs of a 128-graph replay): segment k gets its 4-byte pattern,
+// 16-byte stores over its whole 16-byte units, then the tail bytes.
+struct ClrSeg {
+  void* p;
+  uint64_t bytes;
+  uint32_t pat;
+};
+struct ClrList {
+  ClrSeg s[16];
+  int n;
+};
+__global__ __launch_bounds__(256) void kb_clear(ClrList L) {
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (uint64_t)gridDim.x * blockDim.x;
+  for (int k = 0; k < L.n; k++) {
+    const ClrSeg sg = L.s[k];
+    const uint64_t n16 = sg.bytes >> 4;
+    const uint4 v = make_uint4(sg.pat, sg.pat, sg.pat, sg.pat);
+    uint4* q = (uint4*)sg.p;
+    for (uint64_t i = tid; i < n16; i += nth) q[i] = v;
+    for (uint64_t b = (n16 << 4) + tid; b < sg.bytes; b += nth) ((uint8_t*)sg.p)[b] = (uint8_t)sg.pat;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // firstDescendants in run layout (UpdateAncestorFirstDescendant, hashgraph.go:466-494):
 // chain-j event k is the first chain-j descendant of the chain-c positions
@@ -544,7 +568,7 @@ __global__ __launch_bounds__(NT) void kb_front(BT t) {
   const GDesc d = t.gd[g];
   const int N = t.N, SM = t.SM, cc = t.ccap, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   __shared__ int32_t zrow[NM][NM];     // [member d][i]: the FD row of (d, C_r[d])
-  __shared__ int32_t fssL[2][NM][NM];  // [r & 1][member d][chain c]: fss_c((d, C_r[d])), INF: no member
+  __shared__ int32_t fssL[3][NM][NM];  // [r % 3][member d][chain c]: fss_c((d, C_r[d])), INF: no member
   __shared__ int32_t Cl[3][NM];        // C_{r-1}, C_r, C_{r+1} by r mod 3 (INF: none)
   __shared__ int32_t lenL[NM];
   __shared__ int s_more;
@@ -590,7 +614,7 @@ __global__ __launch_bounds__(NT) void kb_front(BT t) {
         if (lane < N) {
           const int pw = Cp[lane];
           if (pw != INF && pw < min(Cc[lane], lenL[lane])) {  // (lane, pw) is a witness of round r-1
-            ss = fssL[(r - 1) & 1][lane][c] <= lo;
+            ss = fssL[(r + 2) % 3][lane][c] <= lo;
             const int x = chg[(int64_t)c * cc + lo];
             see = LA[(int64_t)x * N + lane] >= pw;
           }
@@ -619,20 +643,43 @@ __global__ __launch_bounds__(NT) void kb_front(BT t) {
     // fss_c of every member (c fastest: a half wave reads one 128-byte row; reading
     // the run layout FDT here instead, with no FD rows built, took 1.82 -> 2.69 ms at
     // 1,024 graphs)
-    for (int e = tid; e < N * N; e += NT) {
-      const int dd = e / N, c = e - (e / N) * N;
-      int f = INF;
-      if (Cc[dd] != INF) {
-        int v[NM];
+    // One (member, chain) pair per thread (N^2 <= NT): round r - 1's outputs go out
+    // while this round's gathers are in flight (its chain-id loads overlap them; the
+    // outputs' reads of C_{r-2} and fss(r - 2) precede the barrier after which the
+    // select overwrites C_{r-2}'s slot, and fssL holds three rounds).
+    const bool one = N * N <= NT;
+    if (one) {
+      const int e = tid, dd = e / N, c = e - (e / N) * N;
+      const bool act = e < N * N && Cc[dd] != INF;
+      int v[NM];
 #pragma unroll
-        for (int i = 0; i < NM; i++) {
-          const int z = i < N ? zrow[dd][i] : INF;
-          v[i] = z != INF ? FDg[((int64_t)i * cc + z) * N + c] : INF;
-        }
+      for (int i = 0; i < NM; i++) {
+        const int z = act && i < N ? zrow[dd][i] : INF;
+        v[i] = z != INF ? FDg[((int64_t)i * cc + z) * N + c] : INF;
+      }
+      if (r > 0) outputs(r - 1);
+      int f = INF;
+      if (act) {
         f = kth_smallest<NM>(v, SM);
         if (dd == c && f != INF) f = max(f, Cc[c] + 1);
       }
-      fssL[r & 1][dd][c] = f;
+      if (e < N * N) fssL[r % 3][dd][c] = f;
+    } else {
+      for (int e = tid; e < N * N; e += NT) {
+        const int dd = e / N, c = e - (e / N) * N;
+        int f = INF;
+        if (Cc[dd] != INF) {
+          int v[NM];
+#pragma unroll
+          for (int i = 0; i < NM; i++) {
+            const int z = i < N ? zrow[dd][i] : INF;
+            v[i] = z != INF ? FDg[((int64_t)i * cc + z) * N + c] : INF;
+          }
+          f = kth_smallest<NM>(v, SM);
+          if (dd == c && f != INF) f = max(f, Cc[c] + 1);
+        }
+        fssL[r % 3][dd][c] = f;
+      }
     }
     __syncthreads();
     // the next frontier
@@ -641,7 +688,7 @@ __global__ __launch_bounds__(NT) void kb_front(BT t) {
       if (lane < N && Cc[lane] != INF) {
         int v[NM];
 #pragma unroll
-        for (int dd = 0; dd < NM; dd++) v[dd] = dd < N ? fssL[r & 1][dd][lane] : INF;
+        for (int dd = 0; dd < NM; dd++) v[dd] = dd < N ? fssL[r % 3][dd][lane] : INF;
         const int sel = kth_smallest<NM>(v, SM);
         nxt = sel < lenL[lane] ? sel : INF;
       }
@@ -650,8 +697,11 @@ __global__ __launch_bounds__(NT) void kb_front(BT t) {
       if (lane == 0) s_more = any != 0;
     }
     __syncthreads();
-    outputs(r);
-    if (!s_more) break;  // uniform: written before the barrier above
+    if (!one) outputs(r);
+    if (!s_more) {  // uniform: written before the barrier above
+      if (one) outputs(r);
+      break;
+    }
   }
 }
 
@@ -1834,21 +1884,25 @@ struct hge_batch {
     if (G == 0) return 0;
     const size_t RN = (size_t)std::max<int64_t>(Rtot, 1) * N;
     const size_t E1 = (size_t)std::max<int64_t>(Etot, 1);
-    BCHK(hipMemsetAsync(d_W.p, 0xFF, RN * 4, st));
-    BCHK(hipMemsetAsync(d_WIX.p, 0xFF, RN * 4, st));
-    BCHK(hipMemsetAsync(d_ssb.p, 0, RN * 8, st));
-    BCHK(hipMemsetAsync(d_seeb.p, 0, RN * 8, st));
-    BCHK(hipMemsetAsync(d_fame.p, 0, RN, st));
-    BCHK(hipMemsetAsync(d_rcnt.p, 0, RN / N * 4, st));
-    BCHK(hipMemsetAsync(d_ver.p, 0, RN / N * 4, st));
-    BCHK(hipMemsetAsync(d_thv.p, 0xFF, RN / N * 4, st));
-    BCHK(hipMemsetAsync(d_rr.p, 0xFF, E1 * 4, st));
-    BCHK(hipMemsetAsync(d_cts.p, 0, E1 * 8, st));
-    BCHK(hipMemsetAsync(d_scal.p, 0, (size_t)G * 64, st));
     const size_t K1 = (size_t)std::max<int64_t>(Ktot, 1);
-    BCHK(hipMemsetAsync(d_bcnt.p, 0, K1 * 4, st));
-    BCHK(hipMemsetAsync(d_wlc.p, 0, 4, st));
-    BCHK(hipMemsetAsync(d_gctx.p, 0, (size_t)G * 8, st));
+    ClrList cl{};
+    auto seg = [&](void* p, size_t bytes, uint32_t pat) { cl.s[cl.n++] = ClrSeg{p, (uint64_t)bytes, pat}; };
+    seg(d_W.p, RN * 4, ~0u);
+    seg(d_WIX.p, RN * 4, ~0u);
+    seg(d_ssb.p, RN * 8, 0);
+    seg(d_seeb.p, RN * 8, 0);
+    seg(d_fame.p, RN, 0);
+    seg(d_rcnt.p, RN / N * 4, 0);
+    seg(d_ver.p, RN / N * 4, 0);
+    seg(d_thv.p, RN / N * 4, ~0u);
+    seg(d_rr.p, E1 * 4, ~0u);
+    seg(d_cts.p, E1 * 8, 0);
+    seg(d_scal.p, (size_t)G * 64, 0);
+    seg(d_bcnt.p, K1 * 4, 0);
+    seg(d_wlc.p, 4, 0);
+    seg(d_gctx.p, (size_t)G * 8, 0);
+    hipLaunchKernelGGL(kb_clear, dim3((unsigned)std::min<size_t>(2048, (E1 * 8 / 16 + 255) / 256 + 1)), dim3(256), 0, st, cl);
+    BCHK(hipGetLastError());
     BT t = tables();
     BCHK(hipEventRecord(ev[0], st));
     if (N <= 32) run_stages<32>(G, t);
