@@ -216,7 +216,8 @@ __global__ __launch_bounds__(256) void kb_levels(BT t) {
                                  cr | ix << 8);
 }
 
-// kb_coords: one workgroup per graph, NT threads; thread (s, k) owns column k of the
+// kb_coords: one workgroup per graph (SPLIT = 1) or per (graph, 1/SPLIT of the columns:
+// every column's recurrence is independent of the others), NT threads; thread (s, k) owns column k of the
 // chunk's events s, s + SL, ... (SL = NT / NM), their kb_levels records in registers
 // (the next chunk's loaded while this one runs).  A step computes one level: every
 // event of it reads its parents' rows from LDS (ring or heads) or HBM and writes its
@@ -229,15 +230,18 @@ __global__ __launch_bounds__(256) void kb_levels(BT t) {
 // only on rows already final).  The parents' row sources are found the same way (the
 // heads' ids kept in LDS); wave 0 loads the next chunk's event records while this
 // chunk's steps run.
-template <int NM, int NT, bool LV>
+template <int NM, int NT, bool LV, int SPLIT = 1>
 __global__ __launch_bounds__(NT) void kb_coords(BT t) {
   if constexpr (LV) {
-  constexpr int SL = NT / NM, EPT = 64 / SL;
-  const GDesc d = t.gd[blockIdx.x];
-  const int N = t.N, tid = threadIdx.x, s = tid / NM, k = tid - (tid / NM) * NM;
+  constexpr int CPW = NM / SPLIT, SL = NT / CPW, EPT = 64 / SL;
+  static_assert(EPT >= 1 && SL * EPT == 64, "slots tile the chunk");
+  const GDesc d = t.gd[blockIdx.x / SPLIT];
+  const int part = blockIdx.x % SPLIT;
+  const int N = t.N, tid = threadIdx.x, s = tid / CPW, kl = tid - (tid / CPW) * CPW, k = part * CPW + kl;
   // rows 0..63: the chunk's ring; 64 + c: chain c's head row as of the chunk's start
-  __shared__ int32_t rows[64 + NM][NM];
-  for (int i = tid; i < NM * NM; i += NT) rows[64 + i / NM][i - (i / NM) * NM] = -1;
+  // (this workgroup's CPW columns: the recurrence is column by column)
+  __shared__ int32_t rows[64 + NM][CPW];
+  for (int i = tid; i < NM * CPW; i += NT) rows[64 + i / CPW][i - (i / CPW) * CPW] = -1;
   __syncthreads();
   int32_t* LA = t.LA + d.eo * N;
   const int2* ci = t.cinf + d.eo;
@@ -265,11 +269,11 @@ __global__ __launch_bounds__(NT) void kb_coords(BT t) {
         const int e = s + SL * u;
         if (base + e < d.E && k < N && ((in[u].x >> 16) & 63) == l) {
           const int sa = (int)(int8_t)(in[u].x & 0xFF), sb = (int)(int8_t)((in[u].x >> 8) & 0xFF);
-          const int a = sa >= 0 ? rows[sa][k] : sa == -1 ? -1 : ld(&LA[(int64_t)t.sp[d.eo + base + e] * N + k]);
-          const int b = sb >= 0 ? rows[sb][k] : sb == -1 ? -1 : ld(&LA[(int64_t)t.op[d.eo + base + e] * N + k]);
+          const int a = sa >= 0 ? rows[sa][kl] : sa == -1 ? -1 : ld(&LA[(int64_t)t.sp[d.eo + base + e] * N + k]);
+          const int b = sb >= 0 ? rows[sb][kl] : sb == -1 ? -1 : ld(&LA[(int64_t)t.op[d.eo + base + e] * N + k]);
           const int v = k == (in[u].y & 0xFF) ? in[u].y >> 8 : max(a, b);
           val[u] = v;
-          rows[e][k] = v;
+          rows[e][kl] = v;
           LA[(int64_t)(base + e) * N + k] = v;
         }
       }
@@ -278,7 +282,7 @@ __global__ __launch_bounds__(NT) void kb_coords(BT t) {
     // the heads after the chunk (every read of the old heads is behind the last barrier)
 #pragma unroll
     for (int u = 0; u < EPT; u++)
-      if (base + s + SL * u < d.E && k < N && (in[u].x >> 23 & 1)) rows[64 + (in[u].y & 0xFF)][k] = val[u];
+      if (base + s + SL * u < d.E && k < N && (in[u].x >> 23 & 1)) rows[64 + (in[u].y & 0xFF)][kl] = val[u];
     __syncthreads();  // also: the chunk's row stores are complete before the next one reads HBM
   }
   } else {
@@ -1833,7 +1837,12 @@ struct hge_batch {
         hipLaunchKernelGGL(kb_levels, dim3((unsigned)((Emax + 255) / 256), (unsigned)G), dim3(256), 0, st, t);
         BCHK(hipGetLastError());
       }
-      launch(kb_coords<NM, 1024, true>, G, t, 1024);
+      // the columns split over two workgroups while both still get a CU of their own
+      // (128 graphs: 0.46 -> 0.43 ms; at 256 graphs, two per CU, 0.49 -> 0.51; four
+      // 8-column parts: 0.45 / 0.55)
+      if (2 * G <= ncu) hipLaunchKernelGGL((kb_coords<NM, 512, true, 2>), dim3(G * 2), dim3(512), 0, st, t);
+      else launch(kb_coords<NM, 1024, true>, G, t, 1024);
+      BCHK(hipGetLastError());
     } else {
       launch(kb_coords<NM, 512, false>, G, t, 512);
     }
