@@ -425,10 +425,12 @@ __global__ __launch_bounds__(256) void kb_clear(ClrList L) {
 // (Slices of 16 columns: a wave holding all 32 columns took 176 VGPRs, two waves per SIMD.)
 constexpr int FCW = 16;
 template <int NM>
-__global__ __launch_bounds__(64) void kb_fd(BT t) {
+__global__ __launch_bounds__(64 * (NM / FCW)) void kb_fd(BT t) {
   constexpr int NS_ = NM / FCW;
-  const int N = t.N, cc = t.ccap, lane = threadIdx.x;
-  const int w = blockIdx.x, g = w / (N * NS_), j = (w / NS_) % N, c0 = (w % NS_) * FCW;
+  // a (graph, chain) per workgroup, one wave per slice: the slices read the same LA rows
+  // (one 128-byte line at N = 32) together on one CU instead of on two XCDs
+  const int N = t.N, cc = t.ccap, lane = threadIdx.x & 63;
+  const int w = blockIdx.x * NS_ + (threadIdx.x >> 6), g = w / (N * NS_), j = (w / NS_) % N, c0 = (w % NS_) * FCW;
   if (c0 >= N) return;
   const GDesc d = t.gd[g];
   const int32_t* LA = t.LA + d.eo * N;
@@ -1847,7 +1849,7 @@ struct hge_batch {
       launch(kb_coords<NM, 512, false>, G, t, 512);
     }
     BCHK(hipEventRecord(ev[1], st));
-    launch(kb_fd<NM>, G * N * (NM / FCW), t);
+    launch(kb_fd<NM>, G * N, t, 64 * (NM / FCW));
     BCHK(hipEventRecord(ev[2], st));
     launch(kb_fdrows<NM>, G * N, t, 256);  // rows for kb_front (kb_median reads the run layout)
     BCHK(hipEventRecord(ev[3], st));
