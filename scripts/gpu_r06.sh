@@ -104,7 +104,7 @@ print('nofd=$v', round(d['value']/1e6,2), d['ms_per_step'], d['kernels_ms_per_re
 import json
 d=json.loads(open('gpurun_out/r06/ab_$v.json').read().strip().splitlines()[-1])
 k=d['kernels_ms_per_replay']
-print('$v', round(d['value']/1e6,2), d['ms_per_step'], {n: k[n] for n in k if 'median' in n or 'sort' in n or 'rounds_direct' in n}, d['parity'][:40])"
+print('$v', round(d['value']/1e6,2), d['ms_per_step'], {n: k[n] for n in k if 'transpose' in n or 'runs' in n or 'rounds_direct' in n}, d['parity'][:40])"
          done; unset HGE_LIB ;;
     mcgpu) timeout -k 10 600 $PYT -m gpu tests/test_gpu_mc.py tests/test_gpu_batch.py > gpurun_out/r06/mcgpu.log 2>&1 || { tail -40 gpurun_out/r06/mcgpu.log; exit 1; }
          tail -3 gpurun_out/r06/mcgpu.log ;;
